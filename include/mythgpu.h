@@ -1,0 +1,232 @@
+/*
+ * mythgpu.h — C-ABI of libmythgpu.so, the MI355X batched execution core for
+ * Mythril's LASER engine.
+ *
+ * The reference (dellalibera/mythril v0.23.18) is pure Python and has no FFI;
+ * its hot path is a set of Python seams.  Each entry point
+ * below names the seam it replaces; the Python host layer in mythril_amd/
+ * binds them with ctypes (ctypes releases the GIL around every call).
+ *
+ * Conventions
+ *   - every call returns 0 on success or a negative MG_E* code and never throws
+ *     across the ABI; the message of the last failure is kept per context and
+ *     returned by mg_last_error();
+ *   - a 256-bit EVM word is 8 little-endian uint32 limbs (limb 0 = bits 0..31);
+ *   - host buffers are plain lane-major arrays (mg_lane_soa); the device keeps
+ *     its own lane-interleaved layout and transposes on upload/download;
+ *   - one context per GPU, used from one host thread at a time.
+ */
+#ifndef MYTHGPU_H
+#define MYTHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_ABI_VERSION 1u
+
+/* ------------------------------------------------------------------ errors */
+#define MG_OK          0
+#define MG_EINVAL     -1   /* bad argument (shape, size, id)                   */
+#define MG_EDEVICE    -2   /* HIP runtime failure                               */
+#define MG_ENOMEM     -3   /* device or host allocation failed                  */
+#define MG_ESTATE     -4   /* call out of order (e.g. step before upload)       */
+#define MG_ENOCODE    -5   /* unknown code_id                                   */
+
+/* ------------------------------------------------------------ lane status */
+/* What ended (or paused) a lane.  Fields pc/sp/msize/gas of a lane that is no
+ * longer RUNNING describe the state at the START of the instruction that ended
+ * it — the same state the reference puts in `final_states` with track_gas=True
+ * (svm.py:331-334 appends the pre-step global_state).                       */
+#define MG_RUNNING        0u  /* max_steps reached, still runnable              */
+#define MG_HALT_STOP      1u  /* STOP: TransactionEndSignal, world state kept   */
+#define MG_HALT_RETURN    2u  /* RETURN: world state kept, ret_offset/ret_len   */
+#define MG_HALT_REVERT    3u  /* REVERT: world state discarded                  */
+#define MG_HALT_END       4u  /* pc past the instruction list (svm.py:384-389)  */
+#define MG_HALT_DROPPED   5u  /* JUMPI true branch to invalid target: no
+                                 successor and no exception (instructions.py:1614-1636) */
+#define MG_VMEXC          6u  /* VmException; aux = MG_EXC_*                    */
+#define MG_HOOK           7u  /* yielded before an opcode set in hook_mask      */
+#define MG_ESCAPE         8u  /* needs host semantics; aux = op | reason << 8   */
+#define MG_DEPTH          9u  /* strategy depth cutoff (strategy/__init__.py:29) */
+
+#define MG_EXC_STACK_UNDERFLOW     1u
+#define MG_EXC_STACK_OVERFLOW      2u
+#define MG_EXC_INVALID_JUMP        3u
+#define MG_EXC_INVALID_INSTRUCTION 4u
+#define MG_EXC_OUT_OF_GAS          5u
+#define MG_EXC_WRITE_PROTECTION    6u
+
+#define MG_ESC_OPCODE   1u   /* opcode with symbolic or world-state semantics   */
+#define MG_ESC_MEMORY   2u   /* memory would grow past the lane's page          */
+#define MG_ESC_STORAGE  3u   /* storage slot table full                         */
+#define MG_ESC_STACK    4u   /* stack would grow past the lane's stack_cap      */
+
+/* lane flags */
+#define MG_LANE_STATIC    1u  /* environment.static (WriteProtection)          */
+#define MG_LANE_CREATION  2u  /* ContractCreationTransaction: CODE and CALLDATA ops escape */
+
+/* environment words, per lane */
+#define MG_ENV_ADDRESS   0
+#define MG_ENV_CALLER    1
+#define MG_ENV_ORIGIN    2
+#define MG_ENV_CALLVALUE 3
+#define MG_ENV_GASPRICE  4
+#define MG_ENV_WORDS     5
+
+#define MG_STACK_LIMIT 1024u              /* MachineStack.STACK_LIMIT           */
+#define MG_MSTATE_GAS_LIMIT 1000000000ull /* GlobalState default gas_limit      */
+
+/* ------------------------------------------------------- host lane layout */
+/* Lane-major host image of a batch of concrete EVM paths.  Any pointer may be
+ * NULL on download to skip that field.                                     */
+typedef struct mg_lane_soa {
+    uint32_t n;             /* lanes described by the arrays below            */
+    uint32_t stack_cap;     /* stack entries per lane in `stack`              */
+    uint32_t mem_cap;       /* bytes per lane in `memory` (multiple of 32)    */
+    uint32_t calldata_cap;  /* bytes per lane in `calldata`                   */
+    uint32_t storage_cap;   /* slots per lane in `storage`                    */
+    uint32_t _pad;
+    uint32_t *code_id;      /* [n]                                             */
+    uint32_t *pc;           /* [n] instruction INDEX (Appendix A #1)          */
+    uint32_t *sp;           /* [n] stack depth                                */
+    uint32_t *msize;        /* [n] memory size in bytes                       */
+    uint32_t *depth;        /* [n] JUMPI depth (mstate.depth)                 */
+    uint32_t *status;       /* [n] MG_RUNNING / MG_HALT_* / ...               */
+    uint32_t *aux;          /* [n] exception kind / escape op|reason / hook op */
+    uint32_t *steps;        /* [n] lane-steps executed (cumulative)           */
+    uint32_t *flags;        /* [n] MG_LANE_*                                  */
+    uint64_t *gas_min;      /* [n] mstate.min_gas_used                        */
+    uint64_t *gas_max;      /* [n] mstate.max_gas_used                        */
+    uint64_t *gas_limit;    /* [n] transaction gas_limit                      */
+    uint32_t *calldata_len; /* [n]                                             */
+    uint8_t  *calldata;     /* [n][calldata_cap]                              */
+    uint32_t *env;          /* [n][MG_ENV_WORDS][8]                           */
+    uint32_t *stack;        /* [n][stack_cap][8]   slot 0 = bottom            */
+    uint8_t  *memory;       /* [n][mem_cap]                                    */
+    uint32_t *storage_count;/* [n]                                             */
+    uint32_t *storage;      /* [n][storage_cap][16] key limbs 0..7, value 8..15 */
+    uint32_t *ret_offset;   /* [n] RETURN/REVERT data offset (low 32 bits)    */
+    uint32_t *ret_len;      /* [n] RETURN/REVERT data length (low 32 bits)    */
+} mg_lane_soa;
+
+/* Per-call statistics of mg_step. */
+typedef struct mg_step_stats {
+    uint64_t lane_steps;    /* instructions executed by all lanes in the call */
+    uint32_t running;       /* lanes still MG_RUNNING after the call          */
+    uint32_t halted;        /* lanes in a terminal status                     */
+    uint32_t hooked;        /* lanes in MG_HOOK                               */
+    uint32_t escaped;       /* lanes in MG_ESCAPE                             */
+    float    kernel_ms;     /* device time of the stepping kernel(s)          */
+    uint32_t launches;      /* kernel launches issued                         */
+} mg_step_stats;
+
+/* Batch configuration, fixed at mg_lanes_alloc. */
+typedef struct mg_batch_cfg {
+    uint32_t n_lanes;
+    uint32_t stack_cap;     /* <= MG_STACK_LIMIT                              */
+    uint32_t mem_cap;       /* bytes, multiple of 32                           */
+    uint32_t calldata_cap;  /* bytes                                           */
+    uint32_t storage_cap;   /* slots                                           */
+    uint32_t coverage;      /* 1: record the per-code coverage bitmap         */
+} mg_batch_cfg;
+
+typedef struct mg_ctx mg_ctx;
+
+/* ------------------------------------------------------------- lifecycle */
+int         mg_abi_version(void);
+int         mg_open(int device, mg_ctx **out);
+void        mg_close(mg_ctx *ctx);
+const char *mg_last_error(mg_ctx *ctx);
+/* Opcode table the device uses (support/opcodes.py:16-144 + instruction_data.py:
+ * 51-56): gas (min,max) and required stack items for a byte, or -1 if the
+ * byte disassembles to INVALID (asm.py:126-131).                            */
+int         mg_opcode_info(uint32_t byte, uint32_t *gas_min, uint32_t *gas_max,
+                           uint32_t *stack_req);
+
+/* ------------------------------------------------------------------ code */
+/* Replaces Disassembly(code) (disassembly.py:9-56, asm.py:99-148) +
+ * util.get_instruction_index (util.py:45-59): builds the instruction table
+ * (pc = index), push immediates, the ">="-jump-resolve table and keeps the
+ * full bytecode for CODECOPY/CODESIZE.                                        */
+int         mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t *code_id);
+/* Number of instructions of a loaded code (len(instruction_list)).          */
+int         mg_code_info(mg_ctx *ctx, uint32_t code_id, uint32_t *n_instr);
+
+/* ----------------------------------------------------------------- lanes */
+int         mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg);
+/* Upload lanes [first, first+n) from host (host->n must equal n).  The
+ * upload also becomes the batch's resident initial image (see mg_lanes_reset). */
+int         mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *host, uint32_t first, uint32_t n);
+int         mg_lanes_download(mg_ctx *ctx, mg_lane_soa *host, uint32_t first, uint32_t n);
+/* Re-initialise every lane from the resident initial image on the device
+ * (no host traffic): pc, sp, msize, gas, status, storage, steps.            */
+int         mg_lanes_reset(mg_ctx *ctx);
+
+/* Replaces the LaserEVM.exec() drain for device-eligible lanes (svm.py:293-337
+ * + execute_state svm.py:369-491 + Instruction.evaluate instructions.py:235-267):
+ * steps every RUNNING lane until it halts, escapes, reaches an opcode whose bit
+ * is set in hook_mask (bit b of hook_mask[b>>6]), or has executed max_steps
+ * instructions in this call.  max_depth: states with depth >= max_depth are
+ * dropped (0 = unlimited).                                                   */
+int         mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
+                    uint32_t max_depth, mg_step_stats *stats);
+/* Same, asynchronous: enqueue only (no stats, no host sync).                */
+int         mg_step_async(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
+                          uint32_t max_depth);
+int         mg_sync(mg_ctx *ctx);
+
+/* Coverage plugin state (coverage_plugin.py:68-85): one byte per instruction
+ * index, 1 = executed by some lane since the last mg_coverage_clear.         */
+int         mg_coverage(mg_ctx *ctx, uint32_t code_id, uint8_t *bytes, uint32_t n);
+int         mg_coverage_clear(mg_ctx *ctx);
+
+/* Number of Keccak-256 evaluations (SHA3 with concrete input) and EXP
+ * evaluations per lane since upload/reset: the host re-registers them with
+ * keccak_function_manager / exponent_function_manager when it materialises a
+ * lane as a GlobalState (keccak_function_manager.py:95-114).                 */
+int         mg_event_counts(mg_ctx *ctx, uint32_t *sha3_count, uint32_t *exp_count,
+                            uint32_t first, uint32_t n);
+
+/* -------------------------------------------------- constraint prefilter */
+/* A batch of constraint sets, each compiled by the host into a register
+ * program over 256-bit values (mythril_amd/smt/flatten.py).  Replaces the
+ * model loop of ModelCache.check_quick_sat (support_utils.py:60-68).        */
+typedef struct mg_dag_batch {
+    uint32_t n_dags;
+    uint32_t n_slots;       /* register slots a program may use (<= 16)       */
+    const uint32_t *prog_off;   /* [n_dags+1] offsets into `insns`            */
+    const uint32_t *insns;      /* [total][4] encoded instructions            */
+    const uint32_t *consts;     /* [n_consts][8] 256-bit constants            */
+    uint32_t n_consts;
+} mg_dag_batch;
+
+/* Candidate models, most-recently-used first (LRU order of
+ * support_utils.py:62-63).  Variables absent from a model take 0
+ * (z3 model_completion).                                  */
+typedef struct mg_model_batch {
+    uint32_t n_models;
+    uint32_t n_vars;
+    const uint32_t *values;     /* [n_vars][n_models][8]                      */
+} mg_model_batch;
+
+/* first_sat_model[d] = smallest model index m (MRU order) whose evaluation of
+ * DAG d is true, UINT32_MAX if none; sat_count[d] = number of satisfying
+ * models (may be NULL).                                                      */
+int         mg_eval(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models,
+                    uint32_t *first_sat_model, uint32_t *sat_count, float *kernel_ms);
+
+/* Device-resident variant used by the benchmark: upload once, evaluate many
+ * times without host traffic. */
+int         mg_eval_upload(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models);
+int         mg_eval_run(mg_ctx *ctx, uint32_t dag_first, uint32_t dag_count, float *kernel_ms);
+int         mg_eval_download(mg_ctx *ctx, uint32_t *first_sat_model, uint32_t *sat_count,
+                             uint32_t dag_first, uint32_t dag_count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MYTHGPU_H */

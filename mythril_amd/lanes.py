@@ -1,0 +1,238 @@
+"""Host image of a batch of concrete EVM lanes (the mg_lane_soa of include/mythgpu.h).
+
+One lane is one LASER path in the concrete subset: the fields mirror what the
+reference keeps in a GlobalState (state/global_state.py:21-56):
+MachineState pc/stack/memory/gas/depth (state/machine_state.py:95-231), the active
+account's concrete storage (state/account.py:18-99), ConcreteCalldata
+(state/calldata.py:121-165) and the Environment words (state/environment.py:12-60).
+
+Layout is lane-major numpy arrays; ``LaneBatch.soa()`` wraps them in the ctypes
+struct the C-ABI takes.  256-bit words are 8 little-endian uint32 limbs.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Iterable, Optional, Sequence
+
+import numpy as np
+
+# ---- constants mirrored from include/mythgpu.h -------------------------------
+MG_RUNNING, MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT = 0, 1, 2, 3
+MG_HALT_END, MG_HALT_DROPPED, MG_VMEXC, MG_HOOK, MG_ESCAPE, MG_DEPTH = 4, 5, 6, 7, 8, 9
+STATUS_NAMES = {
+    MG_RUNNING: "running", MG_HALT_STOP: "stop", MG_HALT_RETURN: "return",
+    MG_HALT_REVERT: "revert", MG_HALT_END: "end", MG_HALT_DROPPED: "dropped",
+    MG_VMEXC: "vmexception", MG_HOOK: "hook", MG_ESCAPE: "escape", MG_DEPTH: "depth",
+}
+# statuses after which the reference keeps the world state (svm.py:384-389, 452-460)
+WORLD_STATE_KEPT = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_END)
+
+MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
+MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
+MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK = 1, 2, 3, 4
+
+MG_LANE_STATIC, MG_LANE_CREATION = 1, 2
+ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
+MG_ENV_WORDS = 5
+MG_STACK_LIMIT = 1024
+MSTATE_GAS_LIMIT = 1_000_000_000
+
+M256 = (1 << 256) - 1
+
+
+def word_to_limbs(x: int) -> np.ndarray:
+    x &= M256
+    return np.array([(x >> (32 * k)) & 0xFFFFFFFF for k in range(8)], dtype=np.uint32)
+
+
+def limbs_to_word(l: Sequence[int]) -> int:
+    return sum(int(v) << (32 * k) for k, v in enumerate(l))
+
+
+def words_to_limbs(xs: Iterable[int]) -> np.ndarray:
+    """Vectorised int -> (n, 8) uint32."""
+    xs = list(xs)
+    out = np.zeros((len(xs), 8), dtype=np.uint32)
+    for i, x in enumerate(xs):
+        x &= M256
+        b = x.to_bytes(32, "little")
+        out[i] = np.frombuffer(b, dtype="<u4")
+    return out
+
+
+class MgLaneSoa(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32), ("mem_cap", ctypes.c_uint32),
+        ("calldata_cap", ctypes.c_uint32), ("storage_cap", ctypes.c_uint32),
+        ("_pad", ctypes.c_uint32),
+        ("code_id", ctypes.c_void_p), ("pc", ctypes.c_void_p), ("sp", ctypes.c_void_p),
+        ("msize", ctypes.c_void_p), ("depth", ctypes.c_void_p), ("status", ctypes.c_void_p),
+        ("aux", ctypes.c_void_p), ("steps", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+        ("gas_min", ctypes.c_void_p), ("gas_max", ctypes.c_void_p), ("gas_limit", ctypes.c_void_p),
+        ("calldata_len", ctypes.c_void_p), ("calldata", ctypes.c_void_p), ("env", ctypes.c_void_p),
+        ("stack", ctypes.c_void_p), ("memory", ctypes.c_void_p),
+        ("storage_count", ctypes.c_void_p), ("storage", ctypes.c_void_p),
+        ("ret_offset", ctypes.c_void_p), ("ret_len", ctypes.c_void_p),
+    ]
+
+
+_U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
+               "calldata_len", "storage_count", "ret_offset", "ret_len")
+_U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
+
+
+@dataclass
+class LaneShape:
+    n: int
+    stack_cap: int = MG_STACK_LIMIT
+    mem_cap: int = 1024
+    calldata_cap: int = 128
+    storage_cap: int = 16
+
+    def __post_init__(self):
+        if self.mem_cap % 32:
+            raise ValueError("mem_cap must be a multiple of 32")
+        if not 0 < self.stack_cap <= MG_STACK_LIMIT:
+            raise ValueError("stack_cap must be in 1..1024")
+
+
+class LaneBatch:
+    """Lane-major numpy image of ``n`` lanes."""
+
+    def __init__(self, shape: LaneShape):
+        self.shape = shape
+        n = shape.n
+        for f in _U32_FIELDS:
+            setattr(self, f, np.zeros(n, dtype=np.uint32))
+        for f in _U64_FIELDS:
+            setattr(self, f, np.zeros(n, dtype=np.uint64))
+        self.calldata = np.zeros((n, shape.calldata_cap), dtype=np.uint8)
+        self.env = np.zeros((n, MG_ENV_WORDS, 8), dtype=np.uint32)
+        self.stack = np.zeros((n, shape.stack_cap, 8), dtype=np.uint32)
+        self.memory = np.zeros((n, shape.mem_cap), dtype=np.uint8)
+        self.storage = np.zeros((n, shape.storage_cap, 16), dtype=np.uint32)
+
+    @property
+    def n(self) -> int:
+        return self.shape.n
+
+    # ---- ctypes view ---------------------------------------------------
+    def soa(self) -> MgLaneSoa:
+        s = MgLaneSoa()
+        s.n = self.shape.n
+        s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
+        s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+            arr = getattr(self, f)
+            assert arr.flags["C_CONTIGUOUS"]
+            setattr(s, f, arr.ctypes.data)
+        self._keep = s  # keep the struct alive with the arrays
+        return s
+
+    def copy(self) -> "LaneBatch":
+        out = LaneBatch(self.shape)
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+            getattr(out, f)[...] = getattr(self, f)
+        return out
+
+    # ---- per-lane construction ----------------------------------------
+    def set_lane(self, i: int, *, code_id: int = 0, calldata: bytes = b"",
+                 address: int = 0, caller: int = 0, origin: int = 0, callvalue: int = 0,
+                 gasprice: int = 0, gas_limit: int = 8_000_000,
+                 storage: Optional[Dict[int, int]] = None, flags: int = 0) -> None:
+        """Initial state of a concrete message call, as transaction/concolic.py:75-122
+        builds it: pc 0, empty stack and memory, gas 0, depth 0."""
+        if len(calldata) > self.shape.calldata_cap:
+            raise ValueError("calldata longer than calldata_cap")
+        storage = storage or {}
+        if len(storage) > self.shape.storage_cap:
+            raise ValueError("more initial storage slots than storage_cap")
+        self.code_id[i] = code_id
+        self.pc[i] = self.sp[i] = self.msize[i] = self.depth[i] = 0
+        self.status[i] = MG_RUNNING
+        self.aux[i] = self.steps[i] = 0
+        self.flags[i] = flags
+        self.gas_min[i] = self.gas_max[i] = 0
+        self.gas_limit[i] = gas_limit
+        self.calldata[i] = 0
+        self.calldata[i, : len(calldata)] = np.frombuffer(bytes(calldata), dtype=np.uint8)
+        self.calldata_len[i] = len(calldata)
+        for k, v in ((ENV_ADDRESS, address), (ENV_CALLER, caller), (ENV_ORIGIN, origin),
+                     (ENV_CALLVALUE, callvalue), (ENV_GASPRICE, gasprice)):
+            self.env[i, k] = word_to_limbs(v)
+        self.storage[i] = 0
+        for s, (k, v) in enumerate(storage.items()):
+            self.storage[i, s, :8] = word_to_limbs(k)
+            self.storage[i, s, 8:] = word_to_limbs(v)
+        self.storage_count[i] = len(storage)
+        self.stack[i] = 0
+        self.memory[i] = 0
+        self.ret_offset[i] = self.ret_len[i] = 0
+
+    # ---- per-lane inspection ------------------------------------------
+    def stack_words(self, i: int):
+        return [limbs_to_word(self.stack[i, k]) for k in range(int(self.sp[i]))]
+
+    def storage_dict(self, i: int, drop_zero: bool = True) -> Dict[int, int]:
+        out = {}
+        for s in range(int(self.storage_count[i])):
+            k = limbs_to_word(self.storage[i, s, :8])
+            v = limbs_to_word(self.storage[i, s, 8:])
+            out[k] = v
+        if drop_zero:
+            out = {k: v for k, v in out.items() if v}
+        return out
+
+    def memory_bytes(self, i: int) -> bytes:
+        return bytes(self.memory[i, : int(self.msize[i])])
+
+    def return_data(self, i: int) -> bytes:
+        """RETURN/REVERT data: memory[off:off+len], bytes past msize read as 0
+        (state/memory.py:152-157 reads missing keys as 0)."""
+        off, ln = int(self.ret_offset[i]), int(self.ret_len[i])
+        m = self.memory_bytes(i)
+        return bytes(m[k] if k < len(m) else 0 for k in range(off, off + ln))
+
+    def summary(self, i: int) -> dict:
+        return {
+            "status": STATUS_NAMES.get(int(self.status[i]), str(int(self.status[i]))),
+            "aux": int(self.aux[i]), "pc": int(self.pc[i]), "sp": int(self.sp[i]),
+            "msize": int(self.msize[i]), "depth": int(self.depth[i]),
+            "steps": int(self.steps[i]),
+            "gas": (int(self.gas_min[i]), int(self.gas_max[i])),
+        }
+
+
+# Fields compared lane-by-lane in parity tests (device vs oracle).
+PARITY_SCALARS = ("pc", "sp", "msize", "depth", "status", "aux", "steps", "gas_min",
+                  "gas_max", "storage_count")
+
+
+def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = None,
+                 limit: int = 10) -> list:
+    """Bit-exact comparison of two images; returns a list of human-readable diffs."""
+    out = []
+    idx = range(a.n) if lanes is None else lanes
+    idx = np.asarray(list(idx))
+    for f in PARITY_SCALARS:
+        x, y = getattr(a, f)[idx], getattr(b, f)[idx]
+        bad = np.nonzero(x != y)[0]
+        for j in bad[:limit]:
+            out.append(f"lane {idx[j]}: {f} {x[j]} != {y[j]}")
+    # stack contents up to sp, memory up to msize, storage up to count, return data
+    for i in idx:
+        if len(out) >= limit:
+            break
+        sp = int(a.sp[i])
+        if sp == int(b.sp[i]) and not np.array_equal(a.stack[i, :sp], b.stack[i, :sp]):
+            out.append(f"lane {i}: stack differs")
+        ms = int(a.msize[i])
+        if ms == int(b.msize[i]) and not np.array_equal(a.memory[i, :ms], b.memory[i, :ms]):
+            out.append(f"lane {i}: memory differs")
+        if a.storage_dict(i, drop_zero=False) != b.storage_dict(i, drop_zero=False):
+            out.append(f"lane {i}: storage differs")
+        if int(a.status[i]) in (MG_HALT_RETURN, MG_HALT_REVERT):
+            if (a.ret_offset[i], a.ret_len[i]) != (b.ret_offset[i], b.ret_len[i]):
+                out.append(f"lane {i}: return range differs")
+    return out
