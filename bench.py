@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Headline benchmark: EVM lane-steps/s of the batched LASER core (BASELINE.json).
+
+Workload (configs[1]): 65,536 concrete lanes per GPU stepping token.sol's
+runtime (precompiled overflow.sol.o, see mythril_amd/workloads.py) with random
+calldata.  One step = one batch: reset every lane from its
+resident initial image (calldata, env, storage already in HBM) and run the
+stepping kernel until every lane has halted.  Weak scaling: every rank runs its
+own 65,536 lanes (seed + rank); the only collective is the coverage all-gather
+after the timed region's batches (§8(e)), over RCCL.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--profile-only", action="store_true",
+                    help="run warmup+steps with no JSON extras (for rocprofv3)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mythril_amd import workloads
+    from mythril_amd.device import GpuDevice
+    from mythril_amd import roofline
+
+    dev = GpuDevice(local)
+    code = workloads.bytecode("overflow.sol.o")
+    cid = dev.load_code(code)
+    batch = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + rank,
+                               stack_cap=1024, mem_cap=1024)
+    dev.alloc(batch.shape, coverage=True)
+    dev.upload(workloads.slim_copy(batch))
+
+    def one_batch():
+        dev.reset()
+        return dev.step()
+
+    for _ in range(args.warmup):
+        one_batch()
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    lane_steps = 0
+    kernel_ms = []
+    for _ in range(args.steps):
+        st = one_batch()
+        lane_steps += st.lane_steps
+        kernel_ms.append(st.kernel_ms)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    # coverage all-gather over RCCL (coverage_plugin.py semantics: OR of bits)
+    cov = dev.coverage(cid)
+    if dist_on:
+        t = torch.from_numpy(cov.astype(np.uint8)).cuda()
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        cov_union = torch.stack(parts).amax(0).cpu().numpy()
+        tt = torch.tensor([elapsed, float(lane_steps)], dtype=torch.float64, device="cuda")
+        mx = tt.clone()
+        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        elapsed, total_steps = float(mx[0]), int(tt[1])
+    else:
+        cov_union = cov
+        total_steps = lane_steps
+
+    if rank == 0 and not args.profile_only:
+        value = total_steps / elapsed
+        steps_per_batch = lane_steps / max(args.steps, 1)
+        kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
+        roof = roofline.lane_step_roofline(dev, batch, cid, kernel_ms=kms)
+        out = {
+            "metric": "EVM lane-steps/s (kernel 1, C2: 65,536 concrete lanes/GPU, token.sol runtime)",
+            "value": value,
+            "unit": "lane-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1000.0 * elapsed / max(args.steps, 1),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32x8 (256-bit integer)",
+            "data": "synthetic calldata (PCG64 seed 0x4D595448 + rank), precompiled overflow.sol.o",
+            "config": {"workload": "C2: 65,536 concrete lanes/GPU stepping token.sol runtime "
+                                   "(overflow.sol.o) with random calldata",
+                       "lanes_per_gpu": args.lanes, "lane_steps_per_batch": steps_per_batch,
+                       "kernel_ms_per_batch": kms,
+                       "coverage_instructions": int(cov_union.sum()),
+                       "parallelism": f"lanes sharded x{world}, RCCL coverage all-gather"},
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline:
+            from oracle import cpu_baseline
+            out["cpu_baseline"] = cpu_baseline.c2_lane_steps(code, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -174,6 +174,12 @@ int         mg_lanes_reset(mg_ctx *ctx);
  * dropped (0 = unlimited).                                                   */
 int         mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                     uint32_t max_depth, mg_step_stats *stats);
+/* Profiling variant (the InstructionProfiler plugin's per-opcode counts,
+ * instruction_profiler.py:41-115, as native counters): op_counts[256] =
+ * instructions executed per opcode byte; extra[4] = {SHA3 input bytes,
+ * CALLDATACOPY/CODECOPY bytes, storage entries scanned, Keccak blocks}.     */
+int         mg_step_profile(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
+                            uint32_t max_depth, uint64_t *op_counts, uint64_t *extra);
 /* Same, asynchronous: enqueue only (no stats, no host sync).                */
 int         mg_step_async(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                           uint32_t max_depth);

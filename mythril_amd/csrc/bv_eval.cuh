@@ -1,0 +1,363 @@
+// bv_eval.cuh — kernel 2: constraint-set x candidate-model evaluation (prefilter).
+//
+// Replaces the model loop of ModelCache.check_quick_sat (support_utils.py:60-68):
+// `for model in reversed(lru): if is_true(model.eval(And(constraints),
+// model_completion=True)): return model`.  The host (mythril_amd/smt/flatten.py)
+// compiles each constraint set into a straight-line register program over
+// 256-bit values; this kernel evaluates every program against every model.
+//
+// Mapping: one thread = one candidate model; a workgroup stages a tile of
+// programs in LDS and all its waves run the SAME instruction stream, so the op,
+// operand kinds and widths are wave-uniform (readfirstlane -> scalar branches,
+// no divergence); only the 256-bit values are per lane.  Results are reduced per
+// wave with ballots: sat count (popc) and first satisfying model (ffs) per DAG.
+//
+// Instruction (4 x u32):
+//   w0: op[0:8) | width[8:17) | store[17] | dst_slot[18:22)
+//   w1, w2, w3: operand refs: kind[30:32) (0 acc, 1 slot, 2 var, 3 const) | index[0:30)
+//               or immediates (EXTRACT lo, SEXT source width, CONCAT low width,
+//               compare operand width), per op.
+// The result always lands in the accumulator; `store` also writes slot dst.
+#pragma once
+#include <string>
+
+#include "u256.cuh"
+#include "../../include/mythgpu.h"
+
+enum BvOp : uint32_t {
+    BV_COPY = 0,       // acc = A
+    BV_ADD, BV_SUB, BV_MUL, BV_UDIV, BV_UREM, BV_SDIV, BV_SREM, BV_SMOD,
+    BV_AND, BV_OR, BV_XOR, BV_NOT, BV_NEG, BV_SHL, BV_LSHR, BV_ASHR,
+    BV_EQ, BV_ULT, BV_ULE, BV_UGT, BV_UGE, BV_SLT, BV_SLE, BV_SGT, BV_SGE,   // w3 = operand width
+    BV_BAND, BV_BOR, BV_BXOR, BV_BNOT, BV_BIMPLIES,
+    BV_ITE,            // A cond, B then, C else
+    BV_EXTRACT,        // A, w2 = lo
+    BV_CONCAT,         // A high, B low, w3 = width of B
+    BV_ZEXT,           // A (value already masked)
+    BV_SEXT,           // A, w2 = source width
+    BV_ADD_NOOVF_U,    // bvadd_noovfl unsigned; w3 = operand width
+    BV_MUL_NOOVF_U,    // bvumul_noovfl;        w3 = operand width
+    BV_SUB_NOUDF_U,    // BVSubNoUnderflow unsigned: b <= a
+    BV_NE,             // w3 = operand width
+    BV_NUM_OPS
+};
+
+#define BV_REF_ACC 0u
+#define BV_REF_SLOT 1u
+#define BV_REF_VAR 2u
+#define BV_REF_CONST 3u
+#define BV_MAX_SLOTS 8u
+#define BV_BLOCK 256u
+#define BV_TILE_INSNS 2048u   // LDS program tile: 32 KiB
+
+struct BvState {
+    uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0;
+    uint4 *insns = nullptr;          // [total]
+    uint32_t *prog_off = nullptr;    // [n_dags + 1]
+    uint32_t *tile_dag = nullptr;    // [n_tiles + 1] first DAG of each tile
+    uint4 *consts = nullptr;         // [n_consts][2]
+    uint4 *values = nullptr;         // [n_vars][n_models][2]
+    uint32_t *first_sat = nullptr;   // [n_dags]
+    uint32_t *sat_count = nullptr;   // [n_dags]
+    size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
+    std::vector<uint32_t> h_tiles;
+};
+
+DEV U256 bv_mask(U256 v, uint32_t width) {
+    if (width >= 256u) return v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t lo = 32u * i;
+        if (width <= lo) v.w[i] = 0u;
+        else if (width < lo + 32u) v.w[i] &= (1u << (width - lo)) - 1u;
+    }
+    return v;
+}
+// sign-extend a width-bit value to 256 bits
+DEV U256 bv_sext(U256 v, uint32_t width) {
+    if (width >= 256u || width == 0u) return v;
+    const uint32_t sb = width - 1u;
+    const bool neg = (u_shr_n(v, sb, 0u).w[0] & 1u) != 0u;
+    if (!neg) return v;
+    return u_or(v, u_shl_n(u_ones(), width));
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+struct BvCtx {
+    const uint4 *__restrict__ values;
+    const uint4 *__restrict__ consts;
+    uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
+    uint32_t n_models, model, tid;
+};
+
+DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
+    const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
+    U256 r;
+    if (kind == BV_REF_ACC) return acc;
+    if (kind == BV_REF_SLOT) {
+        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid];
+        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid];
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        return r;
+    }
+    if (kind == BV_REF_VAR) {
+        const size_t row = (size_t)idx * c.n_models + c.model;
+        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        return r;
+    }
+    // constant: uniform address -> scalar loads
+    const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
+    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    return r;
+}
+
+__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
+                                                      const uint32_t *__restrict__ prog_off,
+                                                      const uint32_t *__restrict__ tile_dag,
+                                                      const uint4 *__restrict__ consts,
+                                                      const uint4 *__restrict__ values, uint32_t n_models,
+                                                      uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles,
+                                                      uint32_t tiles_pad, uint32_t dag_lo, uint32_t dag_hi,
+                                                      uint32_t *__restrict__ first_sat,
+                                                      uint32_t *__restrict__ sat_count) {
+    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+    uint4 *prog = smem;                          // [BV_TILE_INSNS]
+    uint4 *slots = smem + BV_TILE_INSNS;         // [n_slots][2][BV_BLOCK]
+    // chunk-major order with the tile count padded to a multiple of 8: the blocks
+    // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
+    const uint32_t b = blockIdx.x;
+    const uint32_t tile = tile_first + (b % tiles_pad);
+    const uint32_t chunk = b / tiles_pad;
+    if (tile >= tile_first + n_tiles) return;
+    const uint32_t d0 = max(tile_dag[tile], dag_lo), d1 = min(tile_dag[tile + 1], dag_hi);
+    if (d0 >= d1) return;
+    const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
+    for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
+    __syncthreads();
+
+    const uint32_t tid = threadIdx.x;
+    const uint32_t model = chunk * BV_BLOCK + tid;
+    const bool live = model < n_models;
+    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid};
+
+    for (uint32_t d = d0; d < d1; ++d) {
+        const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
+        U256 acc = u_zero();
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint4 ins = prog[p];
+            const uint32_t w0 = uni(ins.x), ra = uni(ins.y), rb = uni(ins.z), rc = uni(ins.w);
+            const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
+            U256 A = bv_fetch(c, acc, ra);
+            U256 r;
+            switch (op) {
+            case BV_COPY: r = A; break;
+            case BV_NOT: r = u_not(A); break;
+            case BV_NEG: r = u_neg(A); break;
+            case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
+            case BV_EXTRACT: r = u_shr_n(A, rb & 0xffu, 0u); break;
+            case BV_ZEXT: r = A; break;
+            case BV_SEXT: r = bv_sext(A, rb); break;
+            default: {
+                U256 B = bv_fetch(c, acc, rb);
+                switch (op) {
+                case BV_ADD: r = u_add(A, B); break;
+                case BV_SUB: r = u_sub(A, B); break;
+                case BV_MUL: r = u_mul(A, B); break;
+                case BV_UDIV: r = z_udiv(A, B); break;
+                case BV_UREM: r = z_urem(A, B); break;
+                case BV_SDIV: r = z_sdiv(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_SREM: r = z_srem(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_SMOD: r = z_smod(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_AND: r = u_and(A, B); break;
+                case BV_OR: r = u_or(A, B); break;
+                case BV_XOR: r = u_xor(A, B); break;
+                case BV_SHL: r = (u_fits32(B) && B.w[0] < width) ? u_shl_n(A, B.w[0]) : u_zero(); break;
+                case BV_LSHR: r = (u_fits32(B) && B.w[0] < width) ? u_shr_n(A, B.w[0], 0u) : u_zero(); break;
+                case BV_ASHR: {
+                    const U256 sa = bv_sext(A, width);
+                    const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
+                    const uint32_t sh = (u_fits32(B) && B.w[0] < width) ? B.w[0] : 255u;
+                    r = u_shr_n(sa, sh, fill);
+                    break;
+                }
+                case BV_EQ: r = u_small(u_eq(A, B)); break;
+                case BV_NE: r = u_small(!u_eq(A, B)); break;
+                case BV_ULT: r = u_small(u_lt(A, B)); break;
+                case BV_ULE: r = u_small(!u_lt(B, A)); break;
+                case BV_UGT: r = u_small(u_lt(B, A)); break;
+                case BV_UGE: r = u_small(!u_lt(A, B)); break;
+                case BV_SLT: r = u_small(u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
+                case BV_SLE: r = u_small(!u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
+                case BV_SGT: r = u_small(u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
+                case BV_SGE: r = u_small(!u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
+                case BV_BAND: r = u_small(A.w[0] & B.w[0] & 1u); break;
+                case BV_BOR: r = u_small((A.w[0] | B.w[0]) & 1u); break;
+                case BV_BXOR: r = u_small((A.w[0] ^ B.w[0]) & 1u); break;
+                case BV_BIMPLIES: r = u_small(((A.w[0] & 1u) ^ 1u) | (B.w[0] & 1u)); break;
+                case BV_ITE: {
+                    const U256 C = bv_fetch(c, acc, rc);
+                    r = u_select((A.w[0] & 1u) != 0u, B, C);
+                    break;
+                }
+                case BV_CONCAT: r = u_or(u_shl_n(A, rc), B); break;
+                case BV_ADD_NOOVF_U: {  // top bit of the (w+1)-bit sum is 0
+                    const U256 s = u_add(A, B);
+                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_n(s, rc, 0u));
+                    r = u_small(!ovf);
+                    break;
+                }
+                case BV_MUL_NOOVF_U: {  // high w bits of the 2w-bit product are 0
+                    bool ovf;
+                    if (u_iszero(A) || u_iszero(B)) ovf = false;
+                    else {
+                        const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
+                        ovf = u_lt(q, B);   // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
+                    }
+                    r = u_small(!ovf);
+                    break;
+                }
+                case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
+                default: r = u_zero(); break;
+                }
+            }
+            }
+            r = bv_mask(r, width);
+            acc = r;
+            if ((w0 >> 17) & 1u) {
+                const uint32_t ds = (w0 >> 18) & 0xfu;
+                slots[(ds * 2u) * BV_BLOCK + tid] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+                slots[(ds * 2u + 1u) * BV_BLOCK + tid] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
+            }
+        }
+        const bool sat = live && (acc.w[0] & 1u);
+        const uint64_t bal = __ballot(sat);
+        if ((tid & 63u) == 0u && bal) {
+            atomicAdd(&sat_count[d], (uint32_t)__popcll(bal));
+            atomicMin(&first_sat[d], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
+        }
+    }
+}
+
+template <class T>
+static int bv_ensure(T *&p, size_t &cap, size_t need) {
+    if (need <= cap && p) return 0;
+    hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, std::max<size_t>(need, 1) * sizeof(T)) != hipSuccess) return MG_ENOMEM;
+    cap = std::max<size_t>(need, 1);
+    return 0;
+}
+
+static void bv_free(BvState &s) {
+    hipFree(s.insns); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.consts);
+    hipFree(s.values); hipFree(s.first_sat); hipFree(s.sat_count);
+    s = BvState{};
+}
+
+static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch *models, hipStream_t st,
+                     std::string &msg) {
+    if (dags->n_dags == 0 || !dags->prog_off || !dags->insns) { msg = "empty DAG batch"; return MG_EINVAL; }
+    if (dags->n_slots > BV_MAX_SLOTS) { msg = "too many slots"; return MG_EINVAL; }
+    if (models->n_models == 0 || (models->n_vars && !models->values)) { msg = "empty model batch"; return MG_EINVAL; }
+    const uint32_t n = dags->n_dags;
+    const uint32_t total = dags->prog_off[n];
+    // validate programs on the host: refs in range, program fits a tile
+    for (uint32_t d = 0; d < n; ++d) {
+        const uint32_t a = dags->prog_off[d], b = dags->prog_off[d + 1];
+        if (b < a || b - a > BV_TILE_INSNS || b > total) { msg = "bad program offsets / program too long"; return MG_EINVAL; }
+    }
+    for (uint32_t i = 0; i < total; ++i) {
+        const uint32_t *w = dags->insns + 4 * (size_t)i;
+        const uint32_t op = w[0] & 0xffu, width = (w[0] >> 8) & 0x1ffu;
+        if (op >= BV_NUM_OPS || width == 0 || width > 256) { msg = "bad instruction " + std::to_string(i); return MG_EINVAL; }
+        if (((w[0] >> 17) & 1u) && ((w[0] >> 18) & 0xfu) >= dags->n_slots) { msg = "slot out of range"; return MG_EINVAL; }
+        const int nref = (op == BV_ITE) ? 3 : (op == BV_COPY || op == BV_NOT || op == BV_NEG || op == BV_BNOT ||
+                                               op == BV_EXTRACT || op == BV_ZEXT || op == BV_SEXT) ? 1 : 2;
+        for (int k = 0; k < nref; ++k) {
+            const uint32_t ref = w[1 + k], kind = ref >> 30, idx = ref & 0x3fffffffu;
+            if ((kind == BV_REF_SLOT && idx >= dags->n_slots) || (kind == BV_REF_VAR && idx >= models->n_vars) ||
+                (kind == BV_REF_CONST && idx >= dags->n_consts)) {
+                msg = "operand out of range at instruction " + std::to_string(i);
+                return MG_EINVAL;
+            }
+        }
+    }
+    // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
+    s.h_tiles.clear();
+    s.h_tiles.push_back(0);
+    uint32_t acc = 0;
+    for (uint32_t d = 0; d < n; ++d) {
+        const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
+        if (acc + len > BV_TILE_INSNS || (d - s.h_tiles.back()) >= 64u) { s.h_tiles.push_back(d); acc = 0; }
+        acc += len;
+    }
+    s.h_tiles.push_back(n);
+    s.n_tiles = (uint32_t)s.h_tiles.size() - 1;
+    int rc = 0;
+    if ((rc = bv_ensure(s.insns, s.cap_insns, total))) { msg = "alloc insns"; return rc; }
+    if ((rc = bv_ensure(s.prog_off, s.cap_dags, (size_t)n + 1))) { msg = "alloc offsets"; return rc; }
+    if ((rc = bv_ensure(s.tile_dag, s.cap_tiles, s.h_tiles.size()))) { msg = "alloc tiles"; return rc; }
+    if ((rc = bv_ensure(s.consts, s.cap_consts, (size_t)std::max<uint32_t>(dags->n_consts, 1) * 2))) { msg = "alloc consts"; return rc; }
+    if ((rc = bv_ensure(s.values, s.cap_values, (size_t)std::max<uint32_t>(models->n_vars, 1) * models->n_models * 2))) { msg = "alloc values"; return rc; }
+    hipFree(s.first_sat); hipFree(s.sat_count);
+    s.first_sat = s.sat_count = nullptr;
+    if (hipMalloc(&s.first_sat, (size_t)n * 4) != hipSuccess || hipMalloc(&s.sat_count, (size_t)n * 4) != hipSuccess) {
+        msg = "alloc outputs";
+        return MG_ENOMEM;
+    }
+    hipError_t e = hipSuccess;
+    e = e ? e : hipMemcpyAsync(s.insns, dags->insns, (size_t)total * 16, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.prog_off, dags->prog_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.tile_dag, s.h_tiles.data(), s.h_tiles.size() * 4, hipMemcpyHostToDevice, st);
+    if (dags->n_consts) e = e ? e : hipMemcpyAsync(s.consts, dags->consts, (size_t)dags->n_consts * 32, hipMemcpyHostToDevice, st);
+    if (models->n_vars)
+        e = e ? e : hipMemcpyAsync(s.values, models->values, (size_t)models->n_vars * models->n_models * 32, hipMemcpyHostToDevice, st);
+    e = e ? e : hipStreamSynchronize(st);
+    if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
+    s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
+    s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
+    return 0;
+}
+
+static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_t st, std::string &msg) {
+    if (!s.n_dags) { msg = "mg_eval_run before mg_eval_upload"; return MG_ESTATE; }
+    if (dag_first + (uint64_t)dag_count > s.n_dags || dag_count == 0) { msg = "DAG range out of bounds"; return MG_EINVAL; }
+    const uint32_t dag_hi = dag_first + dag_count;
+    hipError_t e = hipMemsetAsync(s.first_sat + dag_first, 0xff, (size_t)dag_count * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(s.sat_count + dag_first, 0, (size_t)dag_count * 4, st);
+    if (e != hipSuccess) { msg = hipGetErrorString(e); return MG_EDEVICE; }
+    // tiles covering [dag_first, dag_hi)
+    const auto &t = s.h_tiles;
+    uint32_t t0 = (uint32_t)(std::upper_bound(t.begin(), t.end(), dag_first) - t.begin()) - 1;
+    uint32_t t1 = (uint32_t)(std::lower_bound(t.begin(), t.end(), dag_hi) - t.begin());
+    const uint32_t nt = t1 - t0;
+    const uint32_t tiles_pad = (nt + 7u) & ~7u;
+    const uint32_t chunks = (s.n_models + BV_BLOCK - 1) / BV_BLOCK;
+    const size_t grid = (size_t)tiles_pad * chunks;
+    if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
+    const size_t lds = ((size_t)BV_TILE_INSNS + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
+    hipLaunchKernelGGL(k_bv_eval, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st, s.insns, s.prog_off, s.tile_dag,
+                       s.consts, s.values, s.n_models, s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
+                       s.first_sat, s.sat_count);
+    e = hipGetLastError();
+    if (e != hipSuccess) { msg = std::string("k_bv_eval launch: ") + hipGetErrorString(e); return MG_EDEVICE; }
+    return 0;
+}
+
+static int bv_download(BvState &s, uint32_t *first_sat, uint32_t *sat_count, uint32_t dag_first, uint32_t dag_count,
+                       hipStream_t st, std::string &msg) {
+    if (dag_first + (uint64_t)dag_count > s.n_dags) { msg = "DAG range out of bounds"; return MG_EINVAL; }
+    hipError_t e = hipSuccess;
+    if (first_sat) e = hipMemcpyAsync(first_sat, s.first_sat + dag_first, (size_t)dag_count * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && sat_count)
+        e = hipMemcpyAsync(sat_count, s.sat_count + dag_first, (size_t)dag_count * 4, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { msg = hipGetErrorString(e); return MG_EDEVICE; }
+    return 0;
+}

@@ -1,0 +1,51 @@
+// device_state.h — HBM layout of a lane batch and of loaded codes.
+//
+// Lane state is interleaved by lane so that the 64 lanes of a wave that sit at
+// the same pc / stack depth touch one contiguous span per access:
+//   stack    [slot][lane]      32-byte word per lane   (2 x dwordx4 per access)
+//   memory   [dword][lane]     big-endian dword: EVM byte 4d+0 in bits 31..24
+//   calldata [dword][lane]     same packing as memory
+//   env      [word][lane]      32 bytes
+//   storage  [slot][lane]      64 bytes: key limbs 0..7, value limbs 8..15
+// Scalars are one array per field.  A 256-bit word is 8 little-endian u32 limbs.
+#pragma once
+#include <stdint.h>
+
+struct DevLanes {
+    uint32_t n;          // lanes in the batch
+    uint32_t N;          // row pitch in lanes (n rounded up to 64)
+    uint32_t stack_cap, mem_cap, calldata_cap, storage_cap;
+    // scalars [N]
+    uint32_t *code_id, *pc, *sp, *msize, *depth, *status, *aux, *steps, *flags;
+    uint32_t *calldata_len, *storage_count, *ret_offset, *ret_len;
+    uint32_t *sha3_count, *exp_count;
+    uint64_t *gas_min, *gas_max, *gas_limit;
+    // interleaved state
+    uint4 *stack;        // [stack_cap][N][2]
+    uint32_t *mem;       // [mem_cap/4][N]
+    uint32_t *calldata;  // [calldata_cap/4][N]
+    uint4 *env;          // [5][N][2]
+    uint4 *storage;      // [storage_cap][N][4]
+};
+
+// One loaded code (Disassembly): arrays live in one device arena.
+struct DevCode {
+    uint32_t n_instr;    // len(instruction_list)
+    uint32_t n_bytes;    // len(bytecode) for CODESIZE / CODECOPY
+    uint32_t n_jres;     // entries of the jump-resolve table (last address + 1)
+    uint32_t op_off;     // u8  [n_instr]            opcode byte (0xfe = INVALID)
+    uint32_t addr_off;   // u32 [n_instr]            byte address of instruction
+    uint32_t push_off;   // u32 [n_instr][8]         push immediate (limbs)
+    uint32_t jres_off;   // u32 [n_jres]             first index with addr >= t
+    uint32_t bytes_off;  // u8  [n_bytes]            full bytecode
+    uint32_t cov_off;    // u8  [n_instr]            coverage bytes
+    uint32_t _pad[3];
+};
+
+// Per-launch statistics accumulated by the stepping kernel.
+struct DevCounters {
+    unsigned long long lane_steps;
+    unsigned int running, halted, hooked, escaped;
+};
+
+#define MG_JRES_NONE 0xffffffffu

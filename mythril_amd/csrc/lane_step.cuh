@@ -1,0 +1,597 @@
+// lane_step.cuh — kernel 1: batched concrete LASER stepping, one EVM path per lane.
+//
+// Replaces, for device-eligible paths, the reference hot loop
+//   LaserEVM.exec (svm.py:293-337) -> execute_state (svm.py:369-491)
+//   -> Instruction.evaluate (instructions.py:235-267) -> StateTransition
+//      (instructions.py:98-202) -> opcode mutators (instructions.py:269-1959)
+// with the reference's quirks.  Every lane steps until it
+// halts, escapes to the host, reaches a hooked opcode or has executed max_steps
+// instructions in this launch.  A lane that stops keeps the state it had at the
+// start of the stopping instruction (the pre-step state of final_states).
+//
+// Each opcode handler runs in three phases: (1) pops, checks, memory-extension
+// gas and escape decisions, no writes; (2) accumulate_gas + its OOG check
+// (instructions.py:162-176) — the only exception the reference raises after a
+// mutator has written; (3) writes.
+#pragma once
+#include "device_state.h"
+#include "keccak.cuh"
+#include "u256.cuh"
+
+// ---- constants shared with the host side (mythgpu.hip) ----------------------
+struct OpInfo {
+    uint32_t gmin, gmax;   // support/opcodes.py:16-144 GAS
+    uint32_t req;          // STACK[0]: items required by the svm precheck
+    uint32_t valid;        // 0 -> disassembles to INVALID
+};
+__constant__ OpInfo kOp[256];
+// opcodes whose semantics need the host (symbolic values, world state, calls)
+__constant__ uint64_t kEscape[4];
+
+#define ST_RUNNING 0u
+#define ST_STOP 1u
+#define ST_RETURN 2u
+#define ST_REVERT 3u
+#define ST_END 4u
+#define ST_DROPPED 5u
+#define ST_VMEXC 6u
+#define ST_HOOK 7u
+#define ST_ESCAPE 8u
+#define ST_DEPTH 9u
+
+#define EXC_UNDERFLOW 1u
+#define EXC_OVERFLOW 2u
+#define EXC_BADJUMP 3u
+#define EXC_INVALID 4u
+#define EXC_OOG 5u
+#define EXC_WRITEPROT 6u
+
+#define ESC_OPCODE 1u
+#define ESC_MEMORY 2u
+#define ESC_STORAGE 3u
+#define ESC_STACK 4u
+
+#define LANE_STATIC 1u
+#define LANE_CREATION 2u
+
+#define MSTATE_GAS_LIMIT 1000000000ull
+#define STACK_LIMIT 1024u
+#define BIG_END (1ull << 32)
+#define HUGE_GAS (1ull << 62)
+
+// ---- lane-interleaved accessors ---------------------------------------------
+DEV U256 ld_word(const uint4 *base, size_t idx) {
+    const uint4 x = base[2 * idx], y = base[2 * idx + 1];
+    U256 r;
+    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    return r;
+}
+DEV void st_word(uint4 *base, size_t idx, const U256 &v) {
+    base[2 * idx] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    base[2 * idx + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+}
+struct LaneView {
+    const DevLanes &L;
+    uint32_t lane;
+    DEV size_t row(uint32_t r) const { return (size_t)r * L.N + lane; }
+    DEV U256 stack(uint32_t slot) const { return ld_word(L.stack, row(slot)); }
+    DEV void set_stack(uint32_t slot, const U256 &v) const { st_word(L.stack, row(slot), v); }
+    DEV U256 env(int w) const { return ld_word(L.env, row((uint32_t)w)); }
+    DEV uint32_t mdw(uint32_t dw) const { return L.mem[row(dw)]; }
+    DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? L.mem[row(dw)] : 0u; }
+    DEV void set_mdw(uint32_t dw, uint32_t v) const { L.mem[row(dw)] = v; }
+    DEV uint32_t mbyte(uint32_t off) const { return (mdw(off >> 2) >> (24u - 8u * (off & 3u))) & 0xffu; }
+    DEV void set_mbyte(uint32_t off, uint32_t b) const {
+        const uint32_t sh = 24u - 8u * (off & 3u);
+        const uint32_t d = mdw(off >> 2);
+        set_mdw(off >> 2, (d & ~(0xffu << sh)) | ((b & 0xffu) << sh));
+    }
+    // 32 bytes at off (off + 32 <= mem_cap)
+    DEV U256 mword(uint32_t off) const {
+        U256 r;
+        const uint32_t d0 = off >> 2, s = 8u * (off & 3u);
+        if (s == 0u) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r.w[7 - k] = mdw(d0 + k);
+        } else {
+            uint32_t d[9];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) d[j] = mdw_safe(d0 + j);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r.w[7 - k] = (d[k] << s) | (d[k + 1] >> (32u - s));
+        }
+        return r;
+    }
+    DEV void set_mword(uint32_t off, const U256 &v) const {
+        const uint32_t d0 = off >> 2, s = 8u * (off & 3u);
+        if (s == 0u) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) set_mdw(d0 + k, v.w[7 - k]);
+        } else {
+            const uint32_t keep = 0xffffffffu >> s;   // low bits of the first dword are ours
+            const uint32_t first = mdw(d0), last = mdw(d0 + 8);
+            set_mdw(d0, (first & ~keep) | (v.w[7] >> s));
+#pragma unroll
+            for (int j = 1; j < 8; ++j) set_mdw(d0 + j, (v.w[8 - j] << (32u - s)) | (v.w[7 - j] >> s));
+            set_mdw(d0 + 8, (v.w[0] << (32u - s)) | (last & keep));
+        }
+    }
+    DEV void mzero(uint32_t from, uint32_t to) const {   // [from, to), multiples of 32
+        for (uint32_t dw = from >> 2; dw < (to >> 2); ++dw) set_mdw(dw, 0u);
+    }
+    DEV uint32_t cbyte(uint32_t idx) const {
+        return (L.calldata[row(idx >> 2)] >> (24u - 8u * (idx & 3u))) & 0xffu;
+    }
+};
+
+// ---- memory extension (machine_state.py:132-191) -----------------------------
+#define MX_OK 0
+#define MX_OOG 1
+#define MX_ESCAPE 2
+// later_min < 0: no OOG check follows in this instruction; otherwise the
+// instruction ends with an OOG check after adding later_min gas.
+DEV int mem_extend(const U256 &start, const U256 &size, uint32_t &msize, uint64_t &gmin,
+                   uint64_t &gmax, uint32_t mem_cap, int64_t later_min, uint64_t txlim) {
+    const U256 end = u_add(start, size);
+    // python ints do not wrap; anything past 2^32 bytes costs > 1e9 gas
+    const bool wrapped = u_lt(end, start);
+    if (wrapped || !(end.w[2] == 0u && end.w[3] == 0u && end.w[4] == 0u && end.w[5] == 0u &&
+                     end.w[6] == 0u && end.w[7] == 0u))
+        return MX_OOG;
+    const uint64_t e = (uint64_t)end.w[0] | ((uint64_t)end.w[1] << 32);
+    if (e > BIG_END) return MX_OOG;
+    if ((uint64_t)msize > e) return MX_OK;
+    const uint64_t nw = (e + 31u) >> 5, ow = msize >> 5;
+    if (nw == ow) return MX_OK;
+    const uint64_t fee = (3u * nw + (nw * nw) / 512u) - (3u * ow + (ow * ow) / 512u);
+    const uint64_t nmin = gmin + fee;
+    if (nmin > MSTATE_GAS_LIMIT) return MX_OOG;
+    if (nw * 32u > mem_cap) {
+        if (later_min >= 0 && (nmin + (uint64_t)later_min > MSTATE_GAS_LIMIT ||
+                               nmin + (uint64_t)later_min >= txlim))
+            return MX_OOG;
+        return MX_ESCAPE;
+    }
+    gmin = nmin;
+    gmax += fee;
+    msize = (uint32_t)(nw * 32u);
+    return MX_OK;
+}
+
+DEV bool gas_oog(uint64_t gmin, uint64_t txlim) { return gmin > MSTATE_GAS_LIMIT || gmin >= txlim; }
+
+// Keccak-256 of memory [off, off+len) (off + len <= msize <= mem_cap)
+DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
+    uint64_t st[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) st[i] = 0ull;
+    uint32_t pos = 0;
+    const uint32_t s = 8u * (off & 3u);
+    // little-endian u64 made of the 8 memory bytes at off + p
+    auto le64 = [&](uint32_t p) -> uint64_t {
+        const uint32_t dw = (off + p) >> 2;
+        const uint32_t a = V.mdw_safe(dw), b = V.mdw_safe(dw + 1u);
+        uint32_t be0, be1;
+        if (s == 0u) { be0 = a; be1 = b; }
+        else {
+            const uint32_t c = V.mdw_safe(dw + 2u);
+            be0 = (a << s) | (b >> (32u - s));
+            be1 = (b << s) | (c >> (32u - s));
+        }
+        return (uint64_t)__builtin_bswap32(be0) | ((uint64_t)__builtin_bswap32(be1) << 32);
+    };
+    for (;;) {
+        const uint32_t rem = len - pos;
+        const bool last = rem < 136u;
+#pragma unroll
+        for (int j = 0; j < 17; ++j) {
+            uint64_t v = 0ull;
+            const int32_t nvalid = (int32_t)rem - 8 * j;
+            if (nvalid > 0) {
+                v = le64(pos + 8u * (uint32_t)j);
+                if (nvalid < 8) v &= (1ull << (8 * nvalid)) - 1ull;
+            }
+            if (last) {
+                if (nvalid >= 0 && nvalid < 8) v ^= 0x01ull << (8 * nvalid);
+                if (j == 16) v ^= 0x80ull << 56;
+            }
+            st[j] ^= v;
+        }
+        keccak_f1600(st);
+        if (last) break;
+        pos += 136u;
+    }
+    U256 r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r.w[7 - 2 * q] = __builtin_bswap32((uint32_t)st[q]);
+        r.w[6 - 2 * q] = __builtin_bswap32((uint32_t)(st[q] >> 32));
+    }
+    return r;
+}
+
+// ---- the stepping kernel -------------------------------------------------------
+__global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
+                                                   const uint8_t *__restrict__ a8,
+                                                   const uint32_t *__restrict__ a32,
+                                                   uint8_t *__restrict__ cov, uint32_t cov_on,
+                                                   uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3,
+                                                   uint32_t max_steps, uint32_t max_depth,
+                                                   DevCounters *__restrict__ ctr,
+                                                   unsigned long long *__restrict__ prof) {
+    // optional instruction profile (the InstructionProfiler plugin's per-opcode
+    // counts, instruction_profiler.py:41-115, as native counters): 256 opcode
+    // counts + [sha3 bytes, copy bytes, storage entries scanned, sha3 blocks]
+    __shared__ uint32_t s_prof[260];
+    if (prof) {
+        for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x) s_prof[i] = 0u;
+        __syncthreads();
+    }
+    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in_range = lane < L.n;
+    uint32_t status = in_range ? L.status[lane] : ST_STOP;
+    uint32_t executed = 0;
+
+    if (status == ST_RUNNING) {
+        const LaneView V{L, lane};
+        const DevCode C = codes[L.code_id[lane]];
+        const uint8_t *__restrict__ ops = a8 + C.op_off;
+        const uint32_t flags = L.flags[lane];
+        const uint64_t txlim = L.gas_limit[lane];
+        uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
+        uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
+        uint32_t aux = 0, n_sha3 = 0, n_exp = 0;
+        const uint64_t mask[4] = {m0, m1, m2, m3};
+
+        for (;;) {
+            if (max_depth != 0u && depth >= max_depth) { status = ST_DEPTH; break; }
+            if (pc >= C.n_instr) { status = ST_END; break; }
+            const uint32_t op = ops[pc];
+            if ((mask[op >> 6] >> (op & 63u)) & 1ull) { status = ST_HOOK; aux = op; break; }
+            if (executed >= max_steps) break;
+            if (((kEscape[op >> 6] >> (op & 63u)) & 1ull) ||
+                ((flags & LANE_CREATION) && op >= 0x35u && op <= 0x39u)) {
+                status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
+            }
+            if (cov_on && cov[C.cov_off + pc] == 0) cov[C.cov_off + pc] = 1;
+            if (prof) atomicAdd(&s_prof[op], 1u);
+            ++executed;
+
+            const OpInfo info = kOp[op];
+            const uint32_t msize0 = msize;
+            uint32_t nsp = sp, nmsize = msize, ndepth = depth, npc = pc + 1u;
+            uint64_t ngmin = gmin, ngmax = gmax;
+            uint32_t stop = ST_RUNNING, sx = 0;
+            bool by_table = true;
+
+#define STOPX(s_, x_) { stop = (s_); sx = (x_); break; }
+#define EXCX(k_) STOPX(ST_VMEXC, (k_))
+#define ESCX(r_) STOPX(ST_ESCAPE, op | ((r_) << 8))
+#define NEEDPOP(k_) if (nsp < (uint32_t)(k_)) EXCX(EXC_UNDERFLOW)
+#define GASCOMMIT() if (by_table) { ngmin += info.gmin; ngmax += info.gmax; by_table = false; \
+                                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG) }
+#define PUSHV(v_) { if (nsp + 1u > STACK_LIMIT) EXCX(EXC_OVERFLOW) \
+                    if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK) \
+                    GASCOMMIT() V.set_stack(nsp, (v_)); ++nsp; }
+#define MEMX(st_, sz_, later_) { const int mx_ = mem_extend((st_), (sz_), nmsize, ngmin, ngmax, \
+                                                        L.mem_cap, (later_), txlim); \
+                                 if (mx_ == MX_OOG) EXCX(EXC_OOG) if (mx_ == MX_ESCAPE) ESCX(ESC_MEMORY) }
+#define ZEROFILL() if (nmsize > msize0) V.mzero(msize0, nmsize);
+
+            do {
+                // svm.py:391-402 precheck; instructions.py:188-193 write protection
+                if (sp < info.req) EXCX(EXC_UNDERFLOW)
+                if ((flags & LANE_STATIC) && (op == 0x55u || (op >= 0xa0u && op <= 0xa4u)))
+                    EXCX(EXC_WRITEPROT)
+                if (op >= 0x60u && op <= 0x7fu) {                       // PUSH1..32
+                    const U256 v = ld_word(reinterpret_cast<const uint4 *>(a32 + C.push_off), pc);
+                    PUSHV(v)
+                    break;
+                }
+                if (op >= 0x80u && op <= 0x8fu) {                       // DUP1..16
+                    const uint32_t k = op - 0x7fu;
+                    NEEDPOP(k)
+                    const U256 v = V.stack(nsp - k);
+                    PUSHV(v)
+                    break;
+                }
+                if (op >= 0x90u && op <= 0x9fu) {                       // SWAP1..16
+                    const uint32_t k = op - 0x8fu;
+                    NEEDPOP(k + 1u)
+                    const U256 a = V.stack(nsp - 1u), b = V.stack(nsp - 1u - k);
+                    GASCOMMIT()
+                    V.set_stack(nsp - 1u, b);
+                    V.set_stack(nsp - 1u - k, a);
+                    break;
+                }
+                if (op >= 0xa0u && op <= 0xa4u) {                       // LOG0..4: pops only
+                    NEEDPOP(2u + (op - 0xa0u))
+                    nsp -= 2u + (op - 0xa0u);
+                    break;
+                }
+                U256 a, b, c;
+                switch (op) {
+                case 0x00: STOPX(ST_STOP, 0u)
+                case 0x01: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_add(a, b)) break;
+                case 0x02: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_mul(a, b)) break;
+                case 0x03: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_sub(a, b)) break;
+                case 0x04: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    PUSHV(u_iszero(b) ? u_zero() : z_udiv(a, b)) break;
+                case 0x05: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    PUSHV(u_iszero(b) ? u_zero() : z_sdiv(a, b)) break;
+                case 0x06: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    PUSHV(u_iszero(b) ? u_zero() : z_urem(a, b)) break;
+                case 0x07: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    PUSHV(u_iszero(b) ? u_zero() : z_srem(a, b)) break;
+                case 0x08:  // ADDMOD: URem(URem(a,n) + URem(b,n), n), 256-bit wrap
+                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
+                    PUSHV(z_urem(u_add(z_urem(a, c), z_urem(b, c)), c)) break;
+                case 0x09:  // MULMOD: URem(URem(a,n) * URem(b,n), n)
+                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
+                    PUSHV(z_urem(u_mul(z_urem(a, c), z_urem(b, c)), c)) break;
+                case 0x0a:  // EXP, concrete pow(b, e, 2^256)
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    ++n_exp;
+                    PUSHV(u_exp(a, b)) break;
+                case 0x0b: {  // SIGNEXTEND with the signed test s0 <= 31
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    const U256 tb = u_add(u_shl_n(a, 3u), u_small(7));
+                    const U256 set = u_shl(u_small(1), tb);
+                    const bool sign = !u_iszero(u_and(b, set));
+                    const bool le31 = !u_slt(u_small(31), a);
+                    const U256 r = le31 ? (sign ? u_or(b, u_neg(set)) : u_and(b, u_sub(set, u_small(1)))) : b;
+                    PUSHV(r) break;
+                }
+                case 0x10: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_lt(a, b))) break;
+                case 0x11: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_lt(b, a))) break;
+                case 0x12: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_slt(a, b))) break;
+                case 0x13: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_slt(b, a))) break;
+                case 0x14: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_eq(a, b))) break;
+                case 0x15: NEEDPOP(1) a = V.stack(--nsp); PUSHV(u_small(u_iszero(a))) break;
+                case 0x16: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_and(a, b)) break;
+                case 0x17: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_or(a, b)) break;
+                case 0x18: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_xor(a, b)) break;
+                case 0x19: NEEDPOP(1) a = V.stack(--nsp); PUSHV(u_not(a)) break;
+                case 0x1a: {  // BYTE
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    U256 r = u_zero();
+                    if (u_fits32(a) && a.w[0] <= 31u) r.w[0] = u_shr_n(b, (31u - a.w[0]) * 8u, 0u).w[0] & 0xffu;
+                    PUSHV(r) break;
+                }
+                case 0x1b: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_shl(b, a)) break;
+                case 0x1c: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_lshr(b, a)) break;
+                case 0x1d: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_ashr(b, a)) break;
+                case 0x20: {  // SHA3: own gas first, then mem_extend (instructions.py:1013-1051)
+                    by_table = false;
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    const bool big = (b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u;
+                    const uint64_t blen = (uint64_t)b.w[0] | ((uint64_t)b.w[1] << 32);
+                    const uint64_t g = (big || blen > BIG_END) ? HUGE_GAS : 30ull + 6ull * ((blen + 31ull) >> 5);
+                    ngmin += g; ngmax += g;
+                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
+                    MEMX(a, b, -1)
+                    ZEROFILL()
+                    U256 h;
+                    if (b.w[0] == 0u) {  // get_empty_keccak_hash (keccak_function_manager.py:87-93)
+                        h.w[7] = 0xc5d24601u; h.w[6] = 0x86f7233cu; h.w[5] = 0x927e7db2u; h.w[4] = 0xdcc703c0u;
+                        h.w[3] = 0xe500b653u; h.w[2] = 0xca82273bu; h.w[1] = 0x7bfad804u; h.w[0] = 0x5d85a470u;
+                    } else {
+                        h = keccak_mem(V, a.w[0], b.w[0]);
+                    }
+                    if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
+                    ++n_sha3;
+                    V.set_stack(nsp, h); ++nsp;   // pops 2, pushes 1: cannot overflow
+                    break;
+                }
+                case 0x30: PUSHV(V.env(0)) break;   // ADDRESS
+                case 0x32: PUSHV(V.env(2)) break;   // ORIGIN
+                case 0x33: PUSHV(V.env(1)) break;   // CALLER
+                case 0x34: PUSHV(V.env(3)) break;   // CALLVALUE
+                case 0x3a: PUSHV(V.env(4)) break;   // GASPRICE
+                case 0x35: {  // CALLDATALOAD: byte (off+k) mod 2^256, 0 past the end
+                    NEEDPOP(1) a = V.stack(--nsp);
+                    const uint32_t cdl = L.calldata_len[lane];
+                    U256 r;
+                    const bool fits = u_fits32(a);
+                    if (fits && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl) {
+                        const uint32_t d0 = a.w[0] >> 2;
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) r.w[7 - k] = L.calldata[V.row(d0 + k)];
+                    } else {
+                        bool wrapc = true;
+#pragma unroll
+                        for (int k = 1; k < 8; ++k) wrapc = wrapc && a.w[k] == 0xffffffffu;
+                        r = u_zero();
+#pragma unroll
+                        for (int k = 0; k < 32; ++k) {
+                            const uint64_t t = (uint64_t)a.w[0] + (uint64_t)k;
+                            bool ok = false;
+                            uint32_t idx = 0;
+                            if (fits) { ok = t < cdl; idx = (uint32_t)t; }
+                            else if (wrapc && t >= (1ull << 32)) { idx = (uint32_t)(t - (1ull << 32)); ok = idx < cdl; }
+                            if (ok) r.w[7 - k / 4] |= V.cbyte(idx) << (24 - 8 * (k % 4));
+                        }
+                    }
+                    PUSHV(r) break;
+                }
+                case 0x36: PUSHV(u_small(L.calldata_len[lane])) break;
+                case 0x37: {  // CALLDATACOPY: nothing at all for size 0
+                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
+                    if (u_iszero(c)) break;
+                    MEMX(a, c, (int64_t)info.gmin)
+                    GASCOMMIT()
+                    ZEROFILL()
+                    const uint32_t cdl = L.calldata_len[lane];
+                    bool bfits = u_fits32(b), wrapc = true;
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) wrapc = wrapc && b.w[k] == 0xffffffffu;
+                    if (prof) atomicAdd(&s_prof[257], c.w[0]);
+                    for (uint32_t k = 0; k < c.w[0]; ++k) {
+                        const uint64_t t = (uint64_t)b.w[0] + k;
+                        uint32_t v = 0u;
+                        if (bfits) { if (t < cdl) v = V.cbyte((uint32_t)t); }
+                        else if (wrapc && t >= (1ull << 32) && t - (1ull << 32) < cdl) v = V.cbyte((uint32_t)(t - (1ull << 32)));
+                        V.set_mbyte(a.w[0] + k, v);
+                    }
+                    break;
+                }
+                case 0x38: PUSHV(u_small(C.n_bytes)) break;  // CODESIZE
+                case 0x39: {  // CODECOPY: extends even for size 0; copy stops at the end of code
+                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
+                    MEMX(a, c, (int64_t)info.gmin)
+                    GASCOMMIT()
+                    ZEROFILL()
+                    uint32_t ncopy = 0u;
+                    if (u_fits32(b) && b.w[0] < C.n_bytes) ncopy = min(C.n_bytes - b.w[0], c.w[0]);
+                    if (prof) atomicAdd(&s_prof[257], ncopy);
+                    for (uint32_t k = 0; k < ncopy; ++k) V.set_mbyte(a.w[0] + k, a8[C.bytes_off + b.w[0] + k]);
+                    break;
+                }
+                case 0x3d: PUSHV(u_zero()) break;                 // RETURNDATASIZE: none
+                case 0x3e: NEEDPOP(3) nsp -= 3u; break;           // RETURNDATACOPY: no-op
+                case 0x45: PUSHV(u_small(MSTATE_GAS_LIMIT)) break; // GASLIMIT
+                case 0x50: NEEDPOP(1) nsp -= 1u; break;           // POP
+                case 0x51: {  // MLOAD
+                    NEEDPOP(1) a = V.stack(--nsp);
+                    MEMX(a, u_small(32), (int64_t)info.gmin)
+                    GASCOMMIT()
+                    ZEROFILL()
+                    V.set_stack(nsp, V.mword(a.w[0])); ++nsp;
+                    break;
+                }
+                case 0x52: {  // MSTORE
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    MEMX(a, u_small(32), (int64_t)info.gmin)
+                    GASCOMMIT()
+                    ZEROFILL()
+                    V.set_mword(a.w[0], b);
+                    break;
+                }
+                case 0x53: {  // MSTORE8
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    MEMX(a, u_small(1), (int64_t)info.gmin)
+                    GASCOMMIT()
+                    ZEROFILL()
+                    V.set_mbyte(a.w[0], b.w[0] & 0xffu);
+                    break;
+                }
+                case 0x54: {  // SLOAD over K(0) + stores
+                    NEEDPOP(1) a = V.stack(--nsp);
+                    const uint32_t cnt = L.storage_count[lane];
+                    if (prof) atomicAdd(&s_prof[258], cnt);
+                    U256 r = u_zero();
+                    for (uint32_t s = 0; s < cnt; ++s) {
+                        const size_t base = V.row(s) * 2;
+                        if (u_eq(ld_word(L.storage, base), a)) { r = ld_word(L.storage, base + 1); break; }
+                    }
+                    PUSHV(r) break;
+                }
+                case 0x55: {  // SSTORE
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    const uint32_t cnt = L.storage_count[lane];
+                    if (prof) atomicAdd(&s_prof[258], cnt);
+                    uint32_t slot = cnt;
+                    for (uint32_t s = 0; s < cnt; ++s)
+                        if (u_eq(ld_word(L.storage, V.row(s) * 2), a)) { slot = s; break; }
+                    if (slot == cnt && cnt >= L.storage_cap) ESCX(ESC_STORAGE)
+                    GASCOMMIT()
+                    if (slot == cnt) {
+                        st_word(L.storage, V.row(slot) * 2, a);
+                        L.storage_count[lane] = cnt + 1u;
+                    }
+                    st_word(L.storage, V.row(slot) * 2 + 1, b);
+                    break;
+                }
+                case 0x56: {  // JUMP: gas 8 by hand, no OOG check
+                    by_table = false;
+                    NEEDPOP(1) a = V.stack(--nsp);
+                    uint32_t idx = MG_JRES_NONE;
+                    if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
+                    if (idx == MG_JRES_NONE || ops[idx] != 0x5bu) EXCX(EXC_BADJUMP)
+                    ngmin += 8u; ngmax += 8u; npc = idx;
+                    break;
+                }
+                case 0x57: {  // JUMPI: gas 10 by hand, depth + 1 on the side taken
+                    by_table = false;
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    if (u_iszero(b)) {
+                        ngmin += 10u; ngmax += 10u; ++ndepth;
+                    } else {
+                        uint32_t idx = MG_JRES_NONE;
+                        if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
+                        if (idx == MG_JRES_NONE || ops[idx] != 0x5bu) STOPX(ST_DROPPED, 0u)
+                        ngmin += 10u; ngmax += 10u; ++ndepth; npc = idx;
+                    }
+                    break;
+                }
+                case 0x58: PUSHV(u_small(a32[C.addr_off + pc])) break;  // PC
+                case 0x59: PUSHV(u_small(msize0)) break;                // MSIZE
+                case 0x5b: break;                                        // JUMPDEST
+                case 0x5c: EXCX(EXC_OOG)                                // BEGINSUB
+                case 0xf3: {  // RETURN
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    MEMX(a, b, 0)
+                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
+                    L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
+                    STOPX(ST_RETURN, 0u)
+                }
+                case 0xfd: {  // REVERT: no memory extension
+                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                    L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
+                    STOPX(ST_REVERT, 0u)
+                }
+                case 0xfe: EXCX(EXC_INVALID)
+                default: ESCX(ESC_OPCODE)
+                }
+                if (stop != ST_RUNNING) break;
+                GASCOMMIT()
+            } while (0);
+#undef STOPX
+#undef EXCX
+#undef ESCX
+#undef NEEDPOP
+#undef GASCOMMIT
+#undef PUSHV
+#undef MEMX
+#undef ZEROFILL
+            if (stop != ST_RUNNING) {
+                status = stop;
+                aux = sx;
+                if (stop == ST_ESCAPE) --executed;
+                break;
+            }
+            pc = npc; sp = nsp; msize = nmsize; depth = ndepth; gmin = ngmin; gmax = ngmax;
+        }
+        L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
+        L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
+        L.status[lane] = status; L.aux[lane] = aux;
+        L.steps[lane] += executed;
+        if (n_sha3) L.sha3_count[lane] += n_sha3;
+        if (n_exp) L.exp_count[lane] += n_exp;
+    }
+
+    if (prof) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x)
+            if (s_prof[i]) atomicAdd(&prof[i], (unsigned long long)s_prof[i]);
+    }
+    // wave-level statistics: one atomic per counter per wave
+    if (ctr) {
+        unsigned long long s = executed;
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const uint64_t b_run = __ballot(in_range && status == ST_RUNNING);
+        const uint64_t b_hook = __ballot(in_range && status == ST_HOOK);
+        const uint64_t b_esc = __ballot(in_range && status == ST_ESCAPE);
+        const uint64_t b_all = __ballot(in_range);
+        if ((threadIdx.x & 63u) == 0u) {
+            if (s) atomicAdd(&ctr->lane_steps, s);
+            const unsigned nr = __popcll(b_run), nh = __popcll(b_hook), ne = __popcll(b_esc);
+            const unsigned na = __popcll(b_all);
+            if (nr) atomicAdd(&ctr->running, nr);
+            if (nh) atomicAdd(&ctr->hooked, nh);
+            if (ne) atomicAdd(&ctr->escaped, ne);
+            if (na - nr - nh - ne) atomicAdd(&ctr->halted, na - nr - nh - ne);
+        }
+    }
+}

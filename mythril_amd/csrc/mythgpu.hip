@@ -1,0 +1,743 @@
+// mythgpu.hip — libmythgpu.so: C-ABI, context, code tables and lane batches for
+// the MI355X batched LASER core.  See include/mythgpu.h for the contract.
+//
+// One translation unit: the device kernels are included from lane_step.cuh
+// (kernel 1, concrete lane stepper) and bv_eval.cuh (kernel 2, constraint
+// prefilter).  Pure HIP runtime, no torch, no dual code paths.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mythgpu.h"
+#include "bv_eval.cuh"
+#include "lane_step.cuh"
+
+// ------------------------------------------------------------------ context
+struct mg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    // codes
+    std::vector<DevCode> codes;
+    std::vector<uint8_t> a8;
+    std::vector<uint32_t> a32;
+    uint32_t cov_total = 0;
+    DevCode *d_codes = nullptr;
+    uint8_t *d_a8 = nullptr;
+    uint32_t *d_a32 = nullptr;
+    uint8_t *d_cov = nullptr;
+    size_t cap_codes = 0, cap_a8 = 0, cap_a32 = 0, cap_cov = 0;
+    // lanes
+    mg_batch_cfg cfg{};
+    bool have_lanes = false, uploaded = false, init_fresh = false;
+    DevLanes L{};
+    std::vector<void *> lane_allocs;
+    // resident initial image for mg_lanes_reset
+    uint32_t *i_pc = nullptr, *i_depth = nullptr, *i_status = nullptr, *i_aux = nullptr,
+             *i_steps = nullptr, *i_storage_count = nullptr;
+    uint64_t *i_gas_min = nullptr, *i_gas_max = nullptr;
+    uint4 *i_storage = nullptr;
+    // staging for upload/download (lane-major)
+    void *d_stage = nullptr;
+    size_t stage_bytes = 0;
+    DevCounters *d_ctr = nullptr;
+    // kernel 2
+    BvState bv{};
+};
+
+static int set_err(mg_ctx *ctx, int code, const char *fmt, ...) {
+    if (ctx) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+#define HIPX(ctx, call)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return set_err((ctx), MG_EDEVICE, "%s failed: %s (%s:%d)", #call,               \
+                           hipGetErrorString(e_), __FILE__, __LINE__);                      \
+    } while (0)
+
+// ------------------------------------------------------------- opcode table
+// support/opcodes.py:16-144: gas (min, max) and STACK[0] (svm precheck count,
+// with the table's own values: ADDMOD 2, EXTCODESIZE 0, SSTORE 1, DUP/SWAP 0).
+static void build_optable(OpInfo t[256]) {
+    std::memset(t, 0, sizeof(OpInfo) * 256);
+    auto op = [&](int b, uint32_t req, uint32_t g0, uint32_t g1) { t[b] = OpInfo{g0, g1, req, 1u}; };
+    op(0x00, 0, 0, 0);
+    const uint32_t arith_gas[12] = {0, 3, 5, 3, 5, 5, 5, 5, 8, 8, 10, 5};
+    for (int b = 0x01; b <= 0x0b; ++b) op(b, b == 0x09 ? 3 : 2, arith_gas[b], b == 0x0a ? 340 : arith_gas[b]);
+    for (int b = 0x10; b <= 0x1d; ++b) op(b, (b == 0x15 || b == 0x19) ? 1 : 2, 3, 3);
+    op(0x20, 2, 30, 30 + 6 * 8);
+    const struct { int b; uint32_t req, g0, g1; } env[] = {
+        {0x30, 0, 2, 2}, {0x31, 1, 700, 700}, {0x32, 0, 2, 2}, {0x33, 0, 2, 2}, {0x34, 0, 2, 2},
+        {0x35, 1, 3, 3}, {0x36, 0, 2, 2}, {0x37, 3, 2, 2 + 3 * 768}, {0x38, 0, 2, 2},
+        {0x39, 3, 2, 2 + 3 * 768}, {0x3a, 0, 2, 2}, {0x3b, 0, 700, 700},
+        {0x3c, 4, 700, 700 + 3 * 768}, {0x3d, 0, 2, 2}, {0x3e, 3, 3, 3}, {0x3f, 1, 700, 700},
+        {0x40, 1, 20, 20}, {0x50, 1, 2, 2}, {0x51, 1, 3, 96}, {0x52, 2, 3, 98}, {0x53, 2, 3, 98},
+        {0x54, 1, 800, 800}, {0x55, 1, 5000, 25000}, {0x56, 1, 8, 8}, {0x57, 2, 10, 10},
+        {0x58, 0, 2, 2}, {0x59, 0, 2, 2}, {0x5a, 0, 2, 2}, {0x5b, 0, 1, 1}, {0x5c, 0, 2, 2},
+        {0x5d, 0, 5, 5}, {0x5e, 1, 10, 10}, {0xf0, 3, 32000, 32000}, {0xf5, 4, 32000, 32000},
+        {0xf1, 7, 700, 34700}, {0xf2, 7, 700, 34700}, {0xf3, 2, 0, 0}, {0xf4, 6, 700, 34700},
+        {0xfa, 6, 700, 34700}, {0xfd, 2, 0, 0}, {0xfe, 0, 0, 0}, {0xff, 1, 5000, 30000}};
+    for (const auto &e : env) op(e.b, e.req, e.g0, e.g1);
+    for (int b = 0x41; b <= 0x48; ++b) op(b, 0, 2, 2);
+    for (int b = 0x60; b <= 0x9f; ++b) op(b, 0, 3, 3);   // PUSH1..32, DUP1..16, SWAP1..16
+    for (int k = 0; k <= 4; ++k) op(0xa0 + k, k + 2, 375 * (k + 1), 375 * (k + 1) + 8 * 32);
+}
+
+// Opcodes that need host semantics on a concrete lane (SURVEY Appendix A #12,
+// instructions.py:906-931, 1150-1435, 1699-1708, 1998-2543): symbolic block
+// values, the balances array, other accounts' code, calls, creates, subroutines.
+static void build_escape(uint64_t m[4]) {
+    const int esc[] = {0x31, 0x3b, 0x3c, 0x3f, 0x40, 0x41, 0x42, 0x43, 0x44, 0x46, 0x47, 0x48,
+                       0x5a, 0x5d, 0x5e, 0xf0, 0xf1, 0xf2, 0xf4, 0xf5, 0xfa, 0xff};
+    m[0] = m[1] = m[2] = m[3] = 0;
+    for (int b : esc) m[b >> 6] |= 1ull << (b & 63);
+}
+
+extern "C" int mg_abi_version(void) { return (int)MG_ABI_VERSION; }
+
+extern "C" int mg_opcode_info(uint32_t byte, uint32_t *gmin, uint32_t *gmax, uint32_t *req) {
+    static OpInfo t[256];
+    static bool ready = false;
+    if (!ready) { build_optable(t); ready = true; }
+    if (byte > 255 || !t[byte].valid) return -1;
+    if (gmin) *gmin = t[byte].gmin;
+    if (gmax) *gmax = t[byte].gmax;
+    if (req) *req = t[byte].req;
+    return 0;
+}
+
+extern "C" int mg_open(int device, mg_ctx **out) {
+    if (!out) return MG_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MG_EDEVICE;
+    if (device < 0 || device >= ndev) return MG_EINVAL;
+    mg_ctx *ctx = new mg_ctx();
+    ctx->device = device;
+    int rc = MG_OK;
+    do {
+        if (hipSetDevice(device) != hipSuccess) { rc = MG_EDEVICE; break; }
+        if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { rc = MG_EDEVICE; break; }
+        if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) { rc = MG_EDEVICE; break; }
+        OpInfo t[256];
+        build_optable(t);
+        uint64_t esc[4];
+        build_escape(esc);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kOp), t, sizeof t) != hipSuccess) { rc = MG_EDEVICE; break; }
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kEscape), esc, sizeof esc) != hipSuccess) { rc = MG_EDEVICE; break; }
+        if (hipMalloc(&ctx->d_ctr, sizeof(DevCounters)) != hipSuccess) { rc = MG_ENOMEM; break; }
+    } while (0);
+    if (rc != MG_OK) { mg_close(ctx); return rc; }
+    *out = ctx;
+    return MG_OK;
+}
+
+static void free_lanes(mg_ctx *ctx) {
+    for (void *p : ctx->lane_allocs) hipFree(p);
+    ctx->lane_allocs.clear();
+    ctx->have_lanes = ctx->uploaded = false;
+    ctx->L = DevLanes{};
+}
+
+extern "C" void mg_close(mg_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    free_lanes(ctx);
+    bv_free(ctx->bv);
+    hipFree(ctx->d_codes); hipFree(ctx->d_a8); hipFree(ctx->d_a32); hipFree(ctx->d_cov);
+    hipFree(ctx->d_stage); hipFree(ctx->d_ctr);
+    if (ctx->ev0) hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) hipEventDestroy(ctx->ev1);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+extern "C" const char *mg_last_error(mg_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+// -------------------------------------------------------------------- code
+// Python's repr of a bytes object: asm.py:107-123 tests `"bzzr" in str(bytes[-43:])`.
+static std::string py_bytes_repr(const uint8_t *p, size_t n) {
+    bool sq = false, dq = false;
+    for (size_t i = 0; i < n; ++i) { sq |= p[i] == '\''; dq |= p[i] == '"'; }
+    const char q = (sq && !dq) ? '"' : '\'';
+    static const char hx[] = "0123456789abcdef";
+    std::string s = "b";
+    s += q;
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t c = p[i];
+        if (c == (uint8_t)q || c == '\\') { s += '\\'; s += (char)c; }
+        else if (c == '\t') s += "\\t";
+        else if (c == '\n') s += "\\n";
+        else if (c == '\r') s += "\\r";
+        else if (c < 32 || c >= 127) { s += "\\x"; s += hx[c >> 4]; s += hx[c & 15]; }
+        else s += (char)c;
+    }
+    s += q;
+    return s;
+}
+
+template <class T>
+static int ensure_dev(mg_ctx *ctx, T *&ptr, size_t &cap, size_t need) {
+    if (need <= cap && ptr) return MG_OK;
+    size_t ncap = std::max(need, cap * 2 + 64);
+    T *p = nullptr;
+    if (hipMalloc(&p, ncap * sizeof(T)) != hipSuccess) return set_err(ctx, MG_ENOMEM, "hipMalloc code arena");
+    hipFree(ptr);
+    ptr = p;
+    cap = ncap;
+    return MG_OK;
+}
+
+// Disassembly (asm.py:99-148) + get_instruction_index (util.py:45-59) tables.
+extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t *code_id) {
+    if (!ctx || (!code && n) || !code_id) return set_err(ctx, MG_EINVAL, "mg_load_code: bad args");
+    if (n > (1u << 30)) return set_err(ctx, MG_EINVAL, "mg_load_code: code too large");
+    OpInfo t[256];
+    build_optable(t);
+    size_t length = n;
+    const size_t tail = std::min<size_t>(n, 43);
+    if (py_bytes_repr(code + n - tail, tail).find("bzzr") != std::string::npos)
+        length = n >= 43 ? n - 43 : 0;
+    std::vector<uint8_t> ops;
+    std::vector<uint32_t> addrs, push;
+    size_t a = 0;
+    while (a < length) {
+        const uint8_t b = code[a];
+        uint32_t pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        addrs.push_back((uint32_t)a);
+        if (!t[b].valid) {
+            ops.push_back(0xfe);
+        } else {
+            ops.push_back(b);
+            if (b >= 0x60 && b <= 0x7f) {
+                const size_t np = b - 0x5f;
+                // argument from the FULL bytecode, right-padded with zeros (instructions.py:316)
+                for (size_t i = 0; i < np; ++i) {
+                    const uint8_t v = (a + 1 + i < n) ? code[a + 1 + i] : 0;
+                    const size_t bit = 8 * (np - 1 - i);
+                    pv[bit / 32] |= (uint32_t)v << (bit % 32);
+                }
+                a += np;
+            }
+        }
+        push.insert(push.end(), pv, pv + 8);
+        a += 1;
+    }
+    DevCode dc{};
+    dc.n_instr = (uint32_t)ops.size();
+    dc.n_bytes = (uint32_t)n;
+    dc.n_jres = dc.n_instr ? addrs.back() + 1u : 0u;
+    // arena8: ops, bytes
+    dc.op_off = (uint32_t)ctx->a8.size();
+    ctx->a8.insert(ctx->a8.end(), ops.begin(), ops.end());
+    dc.bytes_off = (uint32_t)ctx->a8.size();
+    ctx->a8.insert(ctx->a8.end(), code, code + n);
+    while (ctx->a8.size() % 16) ctx->a8.push_back(0);
+    // arena32: push (32-byte aligned), addr, jres
+    while (ctx->a32.size() % 8) ctx->a32.push_back(0);
+    dc.push_off = (uint32_t)ctx->a32.size();
+    ctx->a32.insert(ctx->a32.end(), push.begin(), push.end());
+    dc.addr_off = (uint32_t)ctx->a32.size();
+    ctx->a32.insert(ctx->a32.end(), addrs.begin(), addrs.end());
+    dc.jres_off = (uint32_t)ctx->a32.size();
+    {
+        size_t k = 0;
+        for (uint32_t tgt = 0; tgt < dc.n_jres; ++tgt) {
+            while (k < addrs.size() && addrs[k] < tgt) ++k;
+            ctx->a32.push_back(k < addrs.size() ? (uint32_t)k : MG_JRES_NONE);
+        }
+    }
+    dc.cov_off = ctx->cov_total;
+    ctx->cov_total += dc.n_instr + 1u;
+    ctx->codes.push_back(dc);
+    // re-upload arenas (small)
+    int rc;
+    if ((rc = ensure_dev(ctx, ctx->d_codes, ctx->cap_codes, ctx->codes.size()))) return rc;
+    if ((rc = ensure_dev(ctx, ctx->d_a8, ctx->cap_a8, ctx->a8.size() + 16))) return rc;
+    if ((rc = ensure_dev(ctx, ctx->d_a32, ctx->cap_a32, ctx->a32.size() + 16))) return rc;
+    const size_t old_cov = ctx->cap_cov;
+    uint8_t *old_cov_ptr = ctx->d_cov;
+    if (ctx->cov_total > ctx->cap_cov) {
+        uint8_t *p = nullptr;
+        const size_t ncap = std::max<size_t>(ctx->cov_total, 2 * ctx->cap_cov + 256);
+        if (hipMalloc(&p, ncap) != hipSuccess) return set_err(ctx, MG_ENOMEM, "hipMalloc coverage");
+        HIPX(ctx, hipMemsetAsync(p, 0, ncap, ctx->stream));
+        if (old_cov_ptr) HIPX(ctx, hipMemcpyAsync(p, old_cov_ptr, old_cov, hipMemcpyDeviceToDevice, ctx->stream));
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(old_cov_ptr);
+        ctx->d_cov = p;
+        ctx->cap_cov = ncap;
+    }
+    HIPX(ctx, hipMemcpyAsync(ctx->d_codes, ctx->codes.data(), ctx->codes.size() * sizeof(DevCode),
+                             hipMemcpyHostToDevice, ctx->stream));
+    HIPX(ctx, hipMemcpyAsync(ctx->d_a8, ctx->a8.data(), ctx->a8.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPX(ctx, hipMemcpyAsync(ctx->d_a32, ctx->a32.data(), ctx->a32.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    *code_id = (uint32_t)(ctx->codes.size() - 1);
+    return MG_OK;
+}
+
+extern "C" int mg_code_info(mg_ctx *ctx, uint32_t code_id, uint32_t *n_instr) {
+    if (!ctx || code_id >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "unknown code_id %u", code_id);
+    if (n_instr) *n_instr = ctx->codes[code_id].n_instr;
+    return MG_OK;
+}
+
+// ------------------------------------------------------------------- lanes
+template <class T>
+static int lane_alloc(mg_ctx *ctx, T *&p, size_t count) {
+    void *q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess)
+        return set_err(ctx, MG_ENOMEM, "hipMalloc %zu bytes for lanes", count * sizeof(T));
+    ctx->lane_allocs.push_back(q);
+    p = (T *)q;
+    return MG_OK;
+}
+
+extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
+    if (!ctx || !cfg) return MG_EINVAL;
+    if (cfg->n_lanes == 0 || cfg->stack_cap == 0 || cfg->stack_cap > MG_STACK_LIMIT ||
+        cfg->mem_cap % 32 || cfg->calldata_cap % 4 || cfg->storage_cap == 0)
+        return set_err(ctx, MG_EINVAL, "mg_lanes_alloc: bad batch configuration");
+    HIPX(ctx, hipSetDevice(ctx->device));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    free_lanes(ctx);
+    ctx->cfg = *cfg;
+    DevLanes &L = ctx->L;
+    L.n = cfg->n_lanes;
+    L.N = (cfg->n_lanes + 63u) & ~63u;
+    L.stack_cap = cfg->stack_cap; L.mem_cap = cfg->mem_cap;
+    L.calldata_cap = std::max<uint32_t>(cfg->calldata_cap, 4u); L.storage_cap = cfg->storage_cap;
+    const size_t N = L.N;
+    int rc = 0;
+    uint32_t **u32s[] = {&L.code_id, &L.pc, &L.sp, &L.msize, &L.depth, &L.status, &L.aux, &L.steps,
+                         &L.flags, &L.calldata_len, &L.storage_count, &L.ret_offset, &L.ret_len,
+                         &L.sha3_count, &L.exp_count, &ctx->i_pc, &ctx->i_depth, &ctx->i_status,
+                         &ctx->i_aux, &ctx->i_steps, &ctx->i_storage_count};
+    for (auto pp : u32s)
+        if ((rc = lane_alloc(ctx, *pp, N))) return rc;
+    uint64_t **u64s[] = {&L.gas_min, &L.gas_max, &L.gas_limit, &ctx->i_gas_min, &ctx->i_gas_max};
+    for (auto pp : u64s)
+        if ((rc = lane_alloc(ctx, *pp, N))) return rc;
+    if ((rc = lane_alloc(ctx, L.stack, (size_t)L.stack_cap * N * 2))) return rc;
+    if ((rc = lane_alloc(ctx, L.mem, (size_t)(L.mem_cap / 4) * N))) return rc;
+    if ((rc = lane_alloc(ctx, L.calldata, (size_t)(L.calldata_cap / 4) * N))) return rc;
+    if ((rc = lane_alloc(ctx, L.env, (size_t)MG_ENV_WORDS * N * 2))) return rc;
+    if ((rc = lane_alloc(ctx, L.storage, (size_t)L.storage_cap * N * 4))) return rc;
+    if ((rc = lane_alloc(ctx, ctx->i_storage, (size_t)L.storage_cap * N * 4))) return rc;
+    // no lane runs before upload
+    HIPX(ctx, hipMemsetAsync(L.status, 0xff, N * 4, ctx->stream));
+    HIPX(ctx, hipMemsetAsync(L.sha3_count, 0, N * 4, ctx->stream));
+    HIPX(ctx, hipMemsetAsync(L.exp_count, 0, N * 4, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->have_lanes = true;
+    ctx->cfg.calldata_cap = L.calldata_cap;
+    return MG_OK;
+}
+
+// lane-major host units -> interleaved device units:
+// dst[(u * N + lane) * W + k] = src[(lane * Uh + u) * W + k]  for u < Uh
+__global__ void k_scatter_units(const uint32_t *__restrict__ src, uint32_t n, uint32_t Uh,
+                                uint32_t W, uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)n * Uh * W;
+    if (i >= total) return;
+    const uint32_t k = i % W;
+    const size_t rest = i / W;
+    const uint32_t u = rest % Uh;
+    const uint32_t lane = (uint32_t)(rest / Uh);
+    dst[((size_t)u * N + first + lane) * W + k] = src[i];
+}
+__global__ void k_gather_units(const uint32_t *__restrict__ src, uint32_t n, uint32_t Uh,
+                               uint32_t W, uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)n * Uh * W;
+    if (i >= total) return;
+    const uint32_t k = i % W;
+    const size_t rest = i / W;
+    const uint32_t u = rest % Uh;
+    const uint32_t lane = (uint32_t)(rest / Uh);
+    dst[i] = src[((size_t)u * N + first + lane) * W + k];
+}
+// lane-major bytes -> interleaved big-endian dwords (memory / calldata); Dh dwords per lane
+__global__ void k_scatter_bytes(const uint8_t *__restrict__ src, uint32_t n, uint32_t Dh,
+                                uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)n * Dh) return;
+    const uint32_t d = i % Dh, lane = (uint32_t)(i / Dh);
+    const uint8_t *p = src + (size_t)lane * Dh * 4 + (size_t)d * 4;
+    dst[(size_t)d * N + first + lane] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+                                         ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+__global__ void k_gather_bytes(const uint32_t *__restrict__ src, uint32_t n, uint32_t Dh,
+                               uint8_t *__restrict__ dst, uint32_t N, uint32_t first) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)n * Dh) return;
+    const uint32_t d = i % Dh, lane = (uint32_t)(i / Dh);
+    const uint32_t v = src[(size_t)d * N + first + lane];
+    uint8_t *p = dst + (size_t)lane * Dh * 4 + (size_t)d * 4;
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+// restore the working state from the resident initial image
+__global__ void k_reset(DevLanes L, const uint32_t *__restrict__ i_pc, const uint32_t *__restrict__ i_depth,
+                        const uint32_t *__restrict__ i_status, const uint32_t *__restrict__ i_aux,
+                        const uint32_t *__restrict__ i_steps, const uint32_t *__restrict__ i_cnt,
+                        const uint64_t *__restrict__ i_gmin, const uint64_t *__restrict__ i_gmax,
+                        const uint4 *__restrict__ i_storage) {
+    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= L.n) return;
+    L.pc[lane] = i_pc[lane]; L.sp[lane] = 0; L.msize[lane] = 0; L.depth[lane] = i_depth[lane];
+    L.status[lane] = i_status[lane]; L.aux[lane] = i_aux[lane]; L.steps[lane] = i_steps[lane];
+    L.gas_min[lane] = i_gmin[lane]; L.gas_max[lane] = i_gmax[lane];
+    L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
+    const uint32_t cnt = i_cnt[lane];
+    L.storage_count[lane] = cnt;
+    for (uint32_t s = 0; s < cnt; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const size_t idx = ((size_t)s * L.N + lane) * 4 + k;
+            L.storage[idx] = i_storage[idx];
+        }
+}
+
+static int ensure_stage(mg_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->stage_bytes) return MG_OK;
+    hipFree(ctx->d_stage);
+    ctx->d_stage = nullptr;
+    ctx->stage_bytes = 0;
+    if (hipMalloc(&ctx->d_stage, bytes) != hipSuccess) return set_err(ctx, MG_ENOMEM, "hipMalloc staging %zu", bytes);
+    ctx->stage_bytes = bytes;
+    return MG_OK;
+}
+
+static unsigned blocks_for(size_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
+
+// upload one lane-major field of Uh units x W dwords per lane
+static int up_units(mg_ctx *ctx, const void *host, uint32_t n, uint32_t Uh, uint32_t W, void *dst, uint32_t first) {
+    if (!host || Uh == 0) return MG_OK;
+    const size_t bytes = (size_t)n * Uh * W * 4;
+    int rc;
+    if ((rc = ensure_stage(ctx, bytes))) return rc;
+    HIPX(ctx, hipMemcpyAsync(ctx->d_stage, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_scatter_units, dim3(blocks_for((size_t)n * Uh * W)), dim3(256), 0, ctx->stream,
+                       (const uint32_t *)ctx->d_stage, n, Uh, W, (uint32_t *)dst, ctx->L.N, first);
+    HIPX(ctx, hipGetLastError());
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+static int down_units(mg_ctx *ctx, void *host, uint32_t n, uint32_t Uh, uint32_t W, const void *src, uint32_t first) {
+    if (!host || Uh == 0) return MG_OK;
+    const size_t bytes = (size_t)n * Uh * W * 4;
+    int rc;
+    if ((rc = ensure_stage(ctx, bytes))) return rc;
+    hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)n * Uh * W)), dim3(256), 0, ctx->stream,
+                       (const uint32_t *)src, n, Uh, W, (uint32_t *)ctx->d_stage, ctx->L.N, first);
+    HIPX(ctx, hipGetLastError());
+    HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+static int up_bytes(mg_ctx *ctx, const uint8_t *host, uint32_t n, uint32_t bytes_h, uint32_t *dst, uint32_t first) {
+    if (!host || bytes_h == 0) return MG_OK;
+    const uint32_t Dh = bytes_h / 4;
+    const size_t bytes = (size_t)n * bytes_h;
+    int rc;
+    if ((rc = ensure_stage(ctx, bytes))) return rc;
+    HIPX(ctx, hipMemcpyAsync(ctx->d_stage, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_scatter_bytes, dim3(blocks_for((size_t)n * Dh)), dim3(256), 0, ctx->stream,
+                       (const uint8_t *)ctx->d_stage, n, Dh, dst, ctx->L.N, first);
+    HIPX(ctx, hipGetLastError());
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+static int down_bytes(mg_ctx *ctx, uint8_t *host, uint32_t n, uint32_t bytes_h, const uint32_t *src, uint32_t first) {
+    if (!host || bytes_h == 0) return MG_OK;
+    const uint32_t Dh = bytes_h / 4;
+    const size_t bytes = (size_t)n * bytes_h;
+    int rc;
+    if ((rc = ensure_stage(ctx, bytes))) return rc;
+    hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)n * Dh)), dim3(256), 0, ctx->stream,
+                       src, n, Dh, (uint8_t *)ctx->d_stage, ctx->L.N, first);
+    HIPX(ctx, hipGetLastError());
+    HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+static int up_scalar(mg_ctx *ctx, const void *host, size_t elem, uint32_t n, void *dst, uint32_t first) {
+    if (!host) return MG_OK;
+    HIPX(ctx, hipMemcpyAsync((char *)dst + (size_t)first * elem, host, (size_t)n * elem,
+                             hipMemcpyHostToDevice, ctx->stream));
+    return MG_OK;
+}
+static int down_scalar(mg_ctx *ctx, void *host, size_t elem, uint32_t n, const void *src, uint32_t first) {
+    if (!host) return MG_OK;
+    HIPX(ctx, hipMemcpyAsync(host, (const char *)src + (size_t)first * elem, (size_t)n * elem,
+                             hipMemcpyDeviceToHost, ctx->stream));
+    return MG_OK;
+}
+
+static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx->have_lanes) return set_err(ctx, MG_ESTATE, "mg_lanes_alloc first");
+    if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
+        return set_err(ctx, MG_EINVAL, "lane range [%u,%u) outside batch of %u (host n=%u)", first,
+                       first + n, ctx->L.n, h ? h->n : 0);
+    if (h->stack_cap > ctx->L.stack_cap || h->mem_cap > ctx->L.mem_cap || h->mem_cap % 4 ||
+        h->calldata_cap > ctx->L.calldata_cap || h->calldata_cap % 4 || h->storage_cap > ctx->L.storage_cap)
+        return set_err(ctx, MG_EINVAL, "host image capacities exceed the batch configuration");
+    return MG_OK;
+}
+
+extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_host_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    DevLanes &L = ctx->L;
+    // validate code ids and capacities on the host before any kernel sees them
+    for (uint32_t i = 0; i < n; ++i) {
+        if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
+        if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
+            h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap)
+            return set_err(ctx, MG_EINVAL, "lane %u: state exceeds its host capacities", first + i);
+    }
+    bool fresh = true;
+    for (uint32_t i = 0; i < n && fresh; ++i) fresh = h->sp[i] == 0 && h->msize[i] == 0;
+    const size_t S4 = 4, S8 = 8;
+    if ((rc = up_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
+    if ((rc = up_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
+    if ((rc = up_scalar(ctx, h->sp, S4, n, L.sp, first))) return rc;
+    if ((rc = up_scalar(ctx, h->msize, S4, n, L.msize, first))) return rc;
+    if ((rc = up_scalar(ctx, h->depth, S4, n, L.depth, first))) return rc;
+    if ((rc = up_scalar(ctx, h->status, S4, n, L.status, first))) return rc;
+    if ((rc = up_scalar(ctx, h->aux, S4, n, L.aux, first))) return rc;
+    if ((rc = up_scalar(ctx, h->steps, S4, n, L.steps, first))) return rc;
+    if ((rc = up_scalar(ctx, h->flags, S4, n, L.flags, first))) return rc;
+    if ((rc = up_scalar(ctx, h->calldata_len, S4, n, L.calldata_len, first))) return rc;
+    if ((rc = up_scalar(ctx, h->storage_count, S4, n, L.storage_count, first))) return rc;
+    if ((rc = up_scalar(ctx, h->ret_offset, S4, n, L.ret_offset, first))) return rc;
+    if ((rc = up_scalar(ctx, h->ret_len, S4, n, L.ret_len, first))) return rc;
+    if ((rc = up_scalar(ctx, h->gas_min, S8, n, L.gas_min, first))) return rc;
+    if ((rc = up_scalar(ctx, h->gas_max, S8, n, L.gas_max, first))) return rc;
+    if ((rc = up_scalar(ctx, h->gas_limit, S8, n, L.gas_limit, first))) return rc;
+    // resident initial image
+    if ((rc = up_scalar(ctx, h->pc, S4, n, ctx->i_pc, first))) return rc;
+    if ((rc = up_scalar(ctx, h->depth, S4, n, ctx->i_depth, first))) return rc;
+    if ((rc = up_scalar(ctx, h->status, S4, n, ctx->i_status, first))) return rc;
+    if ((rc = up_scalar(ctx, h->aux, S4, n, ctx->i_aux, first))) return rc;
+    if ((rc = up_scalar(ctx, h->steps, S4, n, ctx->i_steps, first))) return rc;
+    if ((rc = up_scalar(ctx, h->storage_count, S4, n, ctx->i_storage_count, first))) return rc;
+    if ((rc = up_scalar(ctx, h->gas_min, S8, n, ctx->i_gas_min, first))) return rc;
+    if ((rc = up_scalar(ctx, h->gas_max, S8, n, ctx->i_gas_max, first))) return rc;
+    HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
+    HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = up_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first))) return rc;
+    if ((rc = up_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
+    if ((rc = up_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first))) return rc;
+    if ((rc = up_units(ctx, h->storage, n, h->storage_cap, 16, ctx->i_storage, first))) return rc;
+    if ((rc = up_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
+    if ((rc = up_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
+    ctx->uploaded = true;
+    ctx->init_fresh = (first == 0 && n == L.n) ? fresh : (ctx->init_fresh && fresh);
+    return MG_OK;
+}
+
+extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_host_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    DevLanes &L = ctx->L;
+    const size_t S4 = 4, S8 = 8;
+    if ((rc = down_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
+    if ((rc = down_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
+    if ((rc = down_scalar(ctx, h->sp, S4, n, L.sp, first))) return rc;
+    if ((rc = down_scalar(ctx, h->msize, S4, n, L.msize, first))) return rc;
+    if ((rc = down_scalar(ctx, h->depth, S4, n, L.depth, first))) return rc;
+    if ((rc = down_scalar(ctx, h->status, S4, n, L.status, first))) return rc;
+    if ((rc = down_scalar(ctx, h->aux, S4, n, L.aux, first))) return rc;
+    if ((rc = down_scalar(ctx, h->steps, S4, n, L.steps, first))) return rc;
+    if ((rc = down_scalar(ctx, h->flags, S4, n, L.flags, first))) return rc;
+    if ((rc = down_scalar(ctx, h->calldata_len, S4, n, L.calldata_len, first))) return rc;
+    if ((rc = down_scalar(ctx, h->storage_count, S4, n, L.storage_count, first))) return rc;
+    if ((rc = down_scalar(ctx, h->ret_offset, S4, n, L.ret_offset, first))) return rc;
+    if ((rc = down_scalar(ctx, h->ret_len, S4, n, L.ret_len, first))) return rc;
+    if ((rc = down_scalar(ctx, h->gas_min, S8, n, L.gas_min, first))) return rc;
+    if ((rc = down_scalar(ctx, h->gas_max, S8, n, L.gas_max, first))) return rc;
+    if ((rc = down_scalar(ctx, h->gas_limit, S8, n, L.gas_limit, first))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = down_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first))) return rc;
+    if ((rc = down_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
+    if ((rc = down_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first))) return rc;
+    if ((rc = down_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
+    if ((rc = down_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
+    return MG_OK;
+}
+
+extern "C" int mg_lanes_reset(mg_ctx *ctx) {
+    if (!ctx) return MG_EINVAL;
+    if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_lanes_reset before mg_lanes_upload");
+    if (!ctx->init_fresh)
+        return set_err(ctx, MG_ESTATE, "mg_lanes_reset needs an uploaded image with empty stacks and memory");
+    hipLaunchKernelGGL(k_reset, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, ctx->i_pc,
+                       ctx->i_depth, ctx->i_status, ctx->i_aux, ctx->i_steps, ctx->i_storage_count,
+                       ctx->i_gas_min, ctx->i_gas_max, ctx->i_storage);
+    HIPX(ctx, hipGetLastError());
+    return MG_OK;
+}
+
+static unsigned g_block = 256;
+
+static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
+                       DevCounters *ctr, unsigned long long *prof = nullptr) {
+    const uint64_t zero[4] = {0, 0, 0, 0};
+    const uint64_t *m = hook_mask ? hook_mask : zero;
+    hipLaunchKernelGGL(k_lane_step, dim3(blocks_for(ctx->L.n, g_block)), dim3(g_block), 0, ctx->stream, ctx->L,
+                       ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
+                       m[2], m[3], max_steps, max_depth, ctr, prof);
+    HIPX(ctx, hipGetLastError());
+    return MG_OK;
+}
+
+extern "C" int mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
+                       mg_step_stats *stats) {
+    if (!ctx) return MG_EINVAL;
+    if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_step before mg_lanes_upload");
+    HIPX(ctx, hipSetDevice(ctx->device));
+    HIPX(ctx, hipMemsetAsync(ctx->d_ctr, 0, sizeof(DevCounters), ctx->stream));
+    HIPX(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr);
+    if (rc) return rc;
+    HIPX(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    DevCounters c{};
+    HIPX(ctx, hipMemcpyAsync(&c, ctx->d_ctr, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if (stats) {
+        float ms = 0.f;
+        HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        stats->lane_steps = c.lane_steps;
+        stats->running = c.running;
+        stats->halted = c.halted;
+        stats->hooked = c.hooked;
+        stats->escaped = c.escaped;
+        stats->kernel_ms = ms;
+        stats->launches = 1;
+    }
+    return MG_OK;
+}
+
+extern "C" int mg_step_profile(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
+                               uint64_t *op_counts, uint64_t *extra) {
+    if (!ctx || !op_counts || !extra) return MG_EINVAL;
+    if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_step_profile before mg_lanes_upload");
+    HIPX(ctx, hipSetDevice(ctx->device));
+    unsigned long long *d = nullptr;
+    HIPX(ctx, hipMalloc(&d, 260 * sizeof(unsigned long long)));
+    hipMemsetAsync(d, 0, 260 * sizeof(unsigned long long), ctx->stream);
+    int rc = launch_step(ctx, hook_mask, max_steps, max_depth, nullptr, d);
+    unsigned long long h[260];
+    if (!rc) {
+        hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, ctx->stream);
+        hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) rc = set_err(ctx, MG_EDEVICE, "profile step: %s", hipGetErrorString(e));
+    }
+    hipFree(d);
+    if (rc) return rc;
+    for (int i = 0; i < 256; ++i) op_counts[i] = h[i];
+    for (int i = 0; i < 4; ++i) extra[i] = h[256 + i];
+    return MG_OK;
+}
+
+extern "C" int mg_step_async(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth) {
+    if (!ctx) return MG_EINVAL;
+    if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_step_async before mg_lanes_upload");
+    return launch_step(ctx, hook_mask, max_steps, max_depth, nullptr);
+}
+
+extern "C" int mg_sync(mg_ctx *ctx) {
+    if (!ctx) return MG_EINVAL;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+extern "C" int mg_coverage(mg_ctx *ctx, uint32_t code_id, uint8_t *bytes, uint32_t n) {
+    if (!ctx || code_id >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "unknown code_id");
+    const DevCode &c = ctx->codes[code_id];
+    if (!bytes || n < c.n_instr) return set_err(ctx, MG_EINVAL, "coverage buffer too small");
+    HIPX(ctx, hipMemcpyAsync(bytes, ctx->d_cov + c.cov_off, c.n_instr, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+extern "C" int mg_coverage_clear(mg_ctx *ctx) {
+    if (!ctx) return MG_EINVAL;
+    if (ctx->d_cov) HIPX(ctx, hipMemsetAsync(ctx->d_cov, 0, ctx->cap_cov, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+extern "C" int mg_event_counts(mg_ctx *ctx, uint32_t *sha3_count, uint32_t *exp_count, uint32_t first, uint32_t n) {
+    if (!ctx || !ctx->have_lanes || first + (uint64_t)n > ctx->L.n) return set_err(ctx, MG_EINVAL, "bad lane range");
+    if (sha3_count) HIPX(ctx, hipMemcpyAsync(sha3_count, ctx->L.sha3_count + first, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (exp_count) HIPX(ctx, hipMemcpyAsync(exp_count, ctx->L.exp_count + first, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+// ----------------------------------------------------------- kernel 2 C-ABI
+extern "C" int mg_eval_upload(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models) {
+    if (!ctx || !dags || !models) return MG_EINVAL;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    std::string msg;
+    const int rc = bv_upload(ctx->bv, dags, models, ctx->stream, msg);
+    if (rc) return set_err(ctx, rc, "%s", msg.c_str());
+    return MG_OK;
+}
+
+extern "C" int mg_eval_run(mg_ctx *ctx, uint32_t dag_first, uint32_t dag_count, float *kernel_ms) {
+    if (!ctx) return MG_EINVAL;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    std::string msg;
+    if (kernel_ms) HIPX(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    const int rc = bv_run(ctx->bv, dag_first, dag_count, ctx->stream, msg);
+    if (rc) return set_err(ctx, rc, "%s", msg.c_str());
+    if (kernel_ms) {
+        HIPX(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        HIPX(ctx, hipEventSynchronize(ctx->ev1));
+        HIPX(ctx, hipEventElapsedTime(kernel_ms, ctx->ev0, ctx->ev1));
+    }
+    return MG_OK;
+}
+
+extern "C" int mg_eval_download(mg_ctx *ctx, uint32_t *first_sat, uint32_t *sat_count, uint32_t dag_first,
+                                uint32_t dag_count) {
+    if (!ctx) return MG_EINVAL;
+    std::string msg;
+    const int rc = bv_download(ctx->bv, first_sat, sat_count, dag_first, dag_count, ctx->stream, msg);
+    if (rc) return set_err(ctx, rc, "%s", msg.c_str());
+    return MG_OK;
+}
+
+extern "C" int mg_eval(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models, uint32_t *first_sat,
+                       uint32_t *sat_count, float *kernel_ms) {
+    int rc;
+    if ((rc = mg_eval_upload(ctx, dags, models))) return rc;
+    if ((rc = mg_eval_run(ctx, 0, dags->n_dags, kernel_ms))) return rc;
+    return mg_eval_download(ctx, first_sat, sat_count, 0, dags->n_dags);
+}

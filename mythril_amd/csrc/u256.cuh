@@ -1,0 +1,311 @@
+// u256.cuh — 256-bit two's-complement arithmetic on 8 x u32 limbs for CDNA4.
+//
+// Every loop is fully unrolled over compile-time limb indices so values stay in
+// VGPRs (a runtime-indexed register array would go to scratch); runtime shift
+// amounts are applied with a 3-stage limb barrel shifter (v_cndmask per limb)
+// followed by a 64-bit funnel shift per limb.  Semantics are z3's bit-vector
+// semantics used by mythril/laser/smt/bitvec.py (bvudiv x 0 = 2^256-1,
+// bvurem x 0 = x, bvsdiv x 0 = x<0 ? 1 : -1, bvsrem x 0 = x).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+
+struct U256 {
+    uint32_t w[8];  // w[0] = least significant limb
+};
+
+DEV U256 u_zero() {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = 0u;
+    return r;
+}
+DEV U256 u_ones() {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = 0xffffffffu;
+    return r;
+}
+DEV U256 u_small(uint64_t x) {
+    U256 r = u_zero();
+    r.w[0] = (uint32_t)x;
+    r.w[1] = (uint32_t)(x >> 32);
+    return r;
+}
+DEV bool u_iszero(const U256 &a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i];
+    return o == 0u;
+}
+// high 7 limbs zero: the value is a u32
+DEV bool u_fits32(const U256 &a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) o |= a.w[i];
+    return o == 0u;
+}
+DEV bool u_eq(const U256 &a, const U256 &b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i] ^ b.w[i];
+    return o == 0u;
+}
+// unsigned a < b: borrow out of a - b
+DEV bool u_lt(const U256 &a, const U256 &b) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t t = (uint64_t)a.w[i] - (uint64_t)b.w[i] - br;
+        br = (uint32_t)(t >> 63);
+    }
+    return br != 0u;
+}
+DEV bool u_isneg(const U256 &a) { return (a.w[7] >> 31) != 0u; }
+DEV bool u_slt(const U256 &a, const U256 &b) {
+    bool na = u_isneg(a), nb = u_isneg(b);
+    return na != nb ? na : u_lt(a, b);
+}
+DEV U256 u_add(const U256 &a, const U256 &b) {
+    U256 r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c += (uint64_t)a.w[i] + b.w[i];
+        r.w[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return r;
+}
+DEV U256 u_sub(const U256 &a, const U256 &b) {
+    U256 r;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t t = (uint64_t)a.w[i] - (uint64_t)b.w[i] - br;
+        r.w[i] = (uint32_t)t;
+        br = (uint32_t)(t >> 63);
+    }
+    return r;
+}
+DEV U256 u_neg(const U256 &a) { return u_sub(u_zero(), a); }
+// low 256 bits of a*b (schoolbook, 36 limb products)
+DEV U256 u_mul(const U256 &a, const U256 &b) {
+    uint32_t r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = 0; i + j < 8; ++j) {
+            uint64_t t = (uint64_t)a.w[i] * b.w[j] + r[i + j] + carry;
+            r[i + j] = (uint32_t)t;
+            carry = t >> 32;
+        }
+    }
+    U256 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o.w[i] = r[i];
+    return o;
+}
+DEV U256 u_and(const U256 &a, const U256 &b) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = a.w[i] & b.w[i];
+    return r;
+}
+DEV U256 u_or(const U256 &a, const U256 &b) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = a.w[i] | b.w[i];
+    return r;
+}
+DEV U256 u_xor(const U256 &a, const U256 &b) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = a.w[i] ^ b.w[i];
+    return r;
+}
+DEV U256 u_not(const U256 &a) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = ~a.w[i];
+    return r;
+}
+DEV U256 u_select(bool c, const U256 &a, const U256 &b) {
+    U256 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = c ? a.w[i] : b.w[i];
+    return r;
+}
+
+// ---- shifts ------------------------------------------------------------------
+// limb barrel shifts by q in [0, 8)
+DEV U256 u_shl_limbs(U256 a, uint32_t q) {
+#pragma unroll
+    for (int stage = 0; stage < 3; ++stage) {
+        const int s = 1 << stage;
+        const bool on = (q >> stage) & 1u;
+        U256 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.w[i] = i >= s ? a.w[i - s] : 0u;
+        a = u_select(on, t, a);
+    }
+    return a;
+}
+DEV U256 u_shr_limbs(U256 a, uint32_t q, uint32_t fill) {
+#pragma unroll
+    for (int stage = 0; stage < 3; ++stage) {
+        const int s = 1 << stage;
+        const bool on = (q >> stage) & 1u;
+        U256 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.w[i] = i + s < 8 ? a.w[i + s] : fill;
+        a = u_select(on, t, a);
+    }
+    return a;
+}
+// (hi:lo) << r, high half, r in [0,32)
+DEV uint32_t fsl(uint32_t hi, uint32_t lo, uint32_t r) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32u - r));
+}
+// (hi:lo) >> r, low half, r in [0,32)
+DEV uint32_t fsr(uint32_t hi, uint32_t lo, uint32_t r) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> r);
+}
+// a << n for n < 256
+DEV U256 u_shl_n(U256 a, uint32_t n) {
+    a = u_shl_limbs(a, n >> 5);
+    const uint32_t r = n & 31u;
+    U256 o;
+#pragma unroll
+    for (int i = 7; i >= 1; --i) o.w[i] = fsl(a.w[i], a.w[i - 1], r);
+    o.w[0] = a.w[0] << r;
+    return o;
+}
+// logical a >> n for n < 256; fill = 0 or 0xffffffff (arithmetic)
+DEV U256 u_shr_n(U256 a, uint32_t n, uint32_t fill) {
+    a = u_shr_limbs(a, n >> 5, fill);
+    const uint32_t r = n & 31u;
+    U256 o;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) o.w[i] = fsr(a.w[i + 1], a.w[i], r);
+    o.w[7] = fsr(fill, a.w[7], r);
+    return o;
+}
+// z3 bvshl / bvlshr / bvashr (shift >= 256 -> 0 / sign fill)
+DEV U256 u_shl(const U256 &a, const U256 &s) {
+    if (!u_fits32(s) || s.w[0] >= 256u) return u_zero();
+    return u_shl_n(a, s.w[0]);
+}
+DEV U256 u_lshr(const U256 &a, const U256 &s) {
+    if (!u_fits32(s) || s.w[0] >= 256u) return u_zero();
+    return u_shr_n(a, s.w[0], 0u);
+}
+DEV U256 u_ashr(const U256 &a, const U256 &s) {
+    const uint32_t fill = u_isneg(a) ? 0xffffffffu : 0u;
+    if (!u_fits32(s) || s.w[0] >= 256u) {
+        U256 r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.w[i] = fill;
+        return r;
+    }
+    return u_shr_n(a, s.w[0], fill);
+}
+// number of significant bits (0 for 0)
+DEV uint32_t u_bitlen(const U256 &a) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (a.w[i]) r = 32u * i + 32u - (uint32_t)__builtin_clz(a.w[i]);
+    return r;
+}
+DEV uint32_t u_popcount(const U256 &a) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p += (uint32_t)__builtin_popcount(a.w[i]);
+    return p;
+}
+
+// ---- division ------------------------------------------------------------------
+// Unsigned a / b and a % b for b != 0.  Power-of-two divisors are shifts; other
+// divisors run shift-subtract over only the (bitlen(a) - bitlen(b) + 1) quotient
+// bit positions that can be non-zero, so a selector extraction (x / 2^224) or a
+// small quotient costs a handful of iterations.
+DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) {
+    const uint32_t lb = u_bitlen(b), la = u_bitlen(a);
+    if (u_popcount(b) == 1u) {
+        const uint32_t k = lb - 1u;
+        q = u_shr_n(a, k, 0u);
+        r = u_and(a, u_sub(b, u_small(1)));
+        return;
+    }
+    q = u_zero();
+    r = a;
+    if (la < lb) return;
+    uint32_t d = la - lb;
+    U256 bs = u_shl_n(b, d);
+    for (uint32_t i = 0; i <= d; ++i) {
+        const bool ge = !u_lt(r, bs);
+        r = u_select(ge, u_sub(r, bs), r);
+        // q = (q << 1) | ge
+#pragma unroll
+        for (int k = 7; k >= 1; --k) q.w[k] = (q.w[k] << 1) | (q.w[k - 1] >> 31);
+        q.w[0] = (q.w[0] << 1) | (ge ? 1u : 0u);
+        // bs >>= 1
+#pragma unroll
+        for (int k = 0; k < 7; ++k) bs.w[k] = (bs.w[k] >> 1) | (bs.w[k + 1] << 31);
+        bs.w[7] >>= 1;
+    }
+}
+DEV U256 z_udiv(const U256 &a, const U256 &b) {
+    if (u_iszero(b)) return u_ones();
+    U256 q, r;
+    u_divmod_nz(a, b, q, r);
+    return q;
+}
+DEV U256 z_urem(const U256 &a, const U256 &b) {
+    if (u_iszero(b)) return a;
+    U256 q, r;
+    u_divmod_nz(a, b, q, r);
+    return r;
+}
+DEV U256 z_sdiv(const U256 &a, const U256 &b) {
+    const bool na = u_isneg(a), nb = u_isneg(b);
+    if (u_iszero(b)) return na ? u_small(1) : u_ones();
+    U256 q, r;
+    u_divmod_nz(na ? u_neg(a) : a, nb ? u_neg(b) : b, q, r);
+    return (na != nb) ? u_neg(q) : q;
+}
+DEV U256 z_srem(const U256 &a, const U256 &b) {
+    if (u_iszero(b)) return a;
+    const bool na = u_isneg(a), nb = u_isneg(b);
+    U256 q, r;
+    u_divmod_nz(na ? u_neg(a) : a, nb ? u_neg(b) : b, q, r);
+    return na ? u_neg(r) : r;
+}
+// z3 bvsmod: remainder with the sign of the divisor
+DEV U256 z_smod(const U256 &a, const U256 &b) {
+    if (u_iszero(b)) return a;
+    U256 r = z_srem(a, b);
+    if (u_iszero(r) || u_isneg(r) == u_isneg(b)) return r;
+    return u_add(r, b);
+}
+// pow(base, exp, 2^256), square-and-multiply over the exponent's bits
+DEV U256 u_exp(U256 base, const U256 &e) {
+    U256 acc = u_small(1);
+    const uint32_t nb = u_bitlen(e);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        uint32_t word = e.w[k];
+        for (uint32_t j = 0; j < 32u && 32u * k + j < nb; ++j) {
+            if (word & 1u) acc = u_mul(acc, base);
+            base = u_mul(base, base);
+            word >>= 1;
+        }
+    }
+    return acc;
+}

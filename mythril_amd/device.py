@@ -1,0 +1,167 @@
+"""One MI355X context: codes, a resident lane batch, stepping and evaluation.
+
+Thin object wrapper over the C-ABI (native.py).  One ``GpuDevice`` per GPU and
+per process (contexts are single-threaded; multi-GPU = one
+process per GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import native
+from .lanes import LaneBatch, LaneShape
+
+
+@dataclass
+class StepStats:
+    lane_steps: int
+    running: int
+    halted: int
+    hooked: int
+    escaped: int
+    kernel_ms: float
+
+
+def _mask_array(hook_mask: Optional[Sequence[int]]):
+    m = list(hook_mask) if hook_mask is not None else [0, 0, 0, 0]
+    return (ctypes.c_uint64 * 4)(*[int(x) & ((1 << 64) - 1) for x in m])
+
+
+def hook_mask_for(opcodes) -> list:
+    """256-bit mask (4 x u64) with the given opcode bytes set."""
+    m = [0, 0, 0, 0]
+    for b in opcodes:
+        m[b >> 6] |= 1 << (b & 63)
+    return m
+
+
+class GpuDevice:
+    def __init__(self, device: int = 0):
+        self.lib = native.load()
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.mg_open(device, ctypes.byref(self.ctx))
+        if rc != native.MG_OK:
+            raise native.MythGpuError(f"mg_open({device}) failed with {rc}")
+        self.device = device
+        self.shape: Optional[LaneShape] = None
+        self.codes = []
+
+    # -- errors --------------------------------------------------------------
+    def _check(self, rc: int, what: str):
+        if rc != native.MG_OK:
+            msg = self.lib.mg_last_error(self.ctx)
+            raise native.MythGpuError(f"{what}: rc={rc}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.mg_close(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- codes ---------------------------------------------------------------
+    def load_code(self, code: bytes) -> int:
+        cid = ctypes.c_uint32()
+        self._check(self.lib.mg_load_code(self.ctx, bytes(code), len(code), ctypes.byref(cid)),
+                    "mg_load_code")
+        self.codes.append(bytes(code))
+        return cid.value
+
+    def n_instr(self, code_id: int) -> int:
+        n = ctypes.c_uint32()
+        self._check(self.lib.mg_code_info(self.ctx, code_id, ctypes.byref(n)), "mg_code_info")
+        return n.value
+
+    # -- lanes ---------------------------------------------------------------
+    def alloc(self, shape: LaneShape, coverage: bool = False):
+        cfg = native.MgBatchCfg(shape.n, shape.stack_cap, shape.mem_cap, shape.calldata_cap,
+                                shape.storage_cap, 1 if coverage else 0)
+        self._check(self.lib.mg_lanes_alloc(self.ctx, ctypes.byref(cfg)), "mg_lanes_alloc")
+        self.shape = shape
+
+    def upload(self, batch: LaneBatch, first: int = 0):
+        soa = batch.soa()
+        self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, batch.n),
+                    "mg_lanes_upload")
+
+    def download(self, batch: LaneBatch, first: int = 0):
+        soa = batch.soa()
+        self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, batch.n),
+                    "mg_lanes_download")
+
+    def reset(self):
+        self._check(self.lib.mg_lanes_reset(self.ctx), "mg_lanes_reset")
+
+    def step(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0) -> StepStats:
+        st = native.MgStepStats()
+        self._check(self.lib.mg_step(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
+                                     ctypes.byref(st)), "mg_step")
+        return StepStats(st.lane_steps, st.running, st.halted, st.hooked, st.escaped, st.kernel_ms)
+
+    def step_profile(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0):
+        """Step with per-opcode counters; returns (op_counts[256], extra[4])."""
+        ops = np.zeros(256, dtype=np.uint64)
+        extra = np.zeros(4, dtype=np.uint64)
+        self._check(self.lib.mg_step_profile(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
+                                             ops.ctypes.data, extra.ctypes.data), "mg_step_profile")
+        return ops, extra
+
+    def step_async(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0):
+        self._check(self.lib.mg_step_async(self.ctx, _mask_array(hook_mask), max_steps, max_depth),
+                    "mg_step_async")
+
+    def sync(self):
+        self._check(self.lib.mg_sync(self.ctx), "mg_sync")
+
+    def coverage(self, code_id: int) -> np.ndarray:
+        n = self.n_instr(code_id)
+        out = np.zeros(max(n, 1), dtype=np.uint8)
+        self._check(self.lib.mg_coverage(self.ctx, code_id, out.ctypes.data, out.size), "mg_coverage")
+        return out[:n]
+
+    def coverage_clear(self):
+        self._check(self.lib.mg_coverage_clear(self.ctx), "mg_coverage_clear")
+
+    def event_counts(self, n: int, first: int = 0):
+        sha3 = np.zeros(n, dtype=np.uint32)
+        exp = np.zeros(n, dtype=np.uint32)
+        self._check(self.lib.mg_event_counts(self.ctx, sha3.ctypes.data, exp.ctypes.data, first, n),
+                    "mg_event_counts")
+        return sha3, exp
+
+    # -- kernel 2 ------------------------------------------------------------
+    def eval_upload(self, program, models):
+        """program: mythril_amd.smt.program.ProgramBatch; models: ModelPool."""
+        self._dags = program.c_struct()
+        self._models = models.c_struct()
+        self._check(self.lib.mg_eval_upload(self.ctx, ctypes.byref(self._dags),
+                                            ctypes.byref(self._models)), "mg_eval_upload")
+        self._n_dags = program.n_dags
+
+    def eval_run(self, first: int = 0, count: Optional[int] = None) -> float:
+        count = self._n_dags - first if count is None else count
+        ms = ctypes.c_float()
+        self._check(self.lib.mg_eval_run(self.ctx, first, count, ctypes.byref(ms)), "mg_eval_run")
+        return ms.value
+
+    def eval_download(self, first: int = 0, count: Optional[int] = None):
+        count = self._n_dags - first if count is None else count
+        fs = np.zeros(count, dtype=np.uint32)
+        sc = np.zeros(count, dtype=np.uint32)
+        self._check(self.lib.mg_eval_download(self.ctx, fs.ctypes.data, sc.ctypes.data, first, count),
+                    "mg_eval_download")
+        return fs, sc
+
+    def eval(self, program, models):
+        self.eval_upload(program, models)
+        ms = self.eval_run()
+        fs, sc = self.eval_download()
+        return fs, sc, ms

@@ -1,0 +1,121 @@
+"""Algorithmic work of a lane-step batch and its roofline fraction.
+
+The per-unit figures are SURVEY §8(d)'s cost table, applied to the opcode
+histogram the device itself counts in a profiling pass (mg_step_profile — the
+InstructionProfiler plugin's per-opcode counts as native counters):
+
+* int32 ops of a lane-step: PUSH/DUP/SWAP/POP 8; ADD/SUB 16; AND/OR/XOR/NOT 8;
+  compares 16; MUL 192 (w(w+1)/2 mul_lo + w(w-1)/2 mul_hi + 2w^2 adds, w=8);
+  DIV/MOD/SDIV/SMOD 2048 (32 w^2); ADDMOD/MULMOD 3 divisions + add/mul; shifts,
+  BYTE, SIGNEXTEND 24 (3w); SHA3 8,900 per 136-byte Keccak block; SLOAD/SSTORE
+  16 per storage entry compared; everything else 8; plus 4 per step for gas.
+* bytes of a lane-step: 32 x (words popped + pushed) + memory bytes touched
+  (MLOAD/MSTORE 32, MSTORE8 1, CALLDATALOAD 32, *COPY size, SHA3 length) + 64 per
+  SLOAD/SSTORE + 1 opcode byte + push-immediate bytes.
+
+Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; INT32 VALU 256 CU x 64 lanes x
+2.4 GHz = 39.3 T ops/s.  The dominant kernel's fraction is the larger one.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+HBM_PEAK_GBS = 8000.0
+VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12   # 39.32
+
+
+def _tables():
+    ops = np.full(256, 8.0)
+    words = np.zeros(256)            # words popped + pushed
+    extra_bytes = np.zeros(256)
+    for b in (0x01, 0x03):
+        ops[b] = 16
+    ops[0x02] = 192
+    for b in (0x04, 0x05, 0x06, 0x07):
+        ops[b] = 2048
+    ops[0x08] = 3 * 2048 + 16
+    ops[0x09] = 3 * 2048 + 192
+    ops[0x0A] = 16 * 192
+    for b in (0x0B, 0x1A, 0x1B, 0x1C, 0x1D):
+        ops[b] = 24
+    for b in range(0x10, 0x16):
+        ops[b] = 16
+    for b in (0x01, 0x02, 0x03, 0x04, 0x05, 0x06, 0x07, 0x0A, 0x0B, 0x10, 0x11, 0x12, 0x13, 0x14,
+              0x16, 0x17, 0x18, 0x1A, 0x1B, 0x1C, 0x1D):
+        words[b] = 3
+    for b in (0x15, 0x19, 0x35, 0x51, 0x54):
+        words[b] = 2
+    words[0x08] = words[0x09] = 4
+    words[0x20] = 3
+    for b in (0x30, 0x32, 0x33, 0x34, 0x36, 0x38, 0x3A, 0x3D, 0x45, 0x58, 0x59):
+        words[b] = 1
+    for b in (0x37, 0x39, 0x3E):
+        words[b] = 3
+    words[0x50] = 1
+    words[0x52] = words[0x53] = words[0x55] = 2
+    words[0x56] = 1
+    words[0x57] = 2
+    words[0xF3] = words[0xFD] = 2
+    for k in range(32):
+        words[0x60 + k] = 1
+        extra_bytes[0x60 + k] = k + 1
+    for k in range(16):
+        words[0x80 + k] = 2
+        words[0x90 + k] = 4
+    for k in range(5):
+        words[0xA0 + k] = 2 + k
+    extra_bytes[0x35] = 32
+    extra_bytes[0x51] = extra_bytes[0x52] = 32
+    extra_bytes[0x53] = 1
+    extra_bytes[0x54] = extra_bytes[0x55] = 64
+    return ops, words, extra_bytes
+
+
+OPS, WORDS, EXTRA_BYTES = _tables()
+
+
+def algorithmic_work(op_counts: np.ndarray, extra: np.ndarray):
+    """(int32 ops, bytes, lane-steps) of a batch from its opcode histogram.
+    extra = [sha3 bytes, copy bytes, storage entries scanned, keccak blocks]."""
+    c = op_counts.astype(np.float64)
+    steps = float(c.sum())
+    ops = float((c * OPS).sum()) + 4.0 * steps
+    # SHA3: per-block cost instead of the flat 8; SLOAD/SSTORE: per entry compared
+    ops += 8900.0 * float(extra[3]) - 8.0 * float(c[0x20])
+    ops += 16.0 * float(extra[2])
+    byts = float((c * (32.0 * WORDS + EXTRA_BYTES + 1.0)).sum())
+    byts += float(extra[0]) + float(extra[1])
+    return ops, byts, steps
+
+
+def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
+    """Profile one batch (untimed; the resident image is reset first) and price the
+    timed kernel's average launch against the HBM and INT32 VALU peaks."""
+    dev.reset()
+    op_counts, extra = dev.step_profile()
+    dev.reset()
+    ops, byts, steps = algorithmic_work(op_counts, extra)
+    sec = kernel_ms / 1e3 if kernel_ms > 0 else float("nan")
+    gbs = byts / sec / 1e9
+    tops = ops / sec / 1e12
+    hbm_frac = gbs / HBM_PEAK_GBS
+    valu_frac = tops / VALU_PEAK_TOPS
+    primary_hbm = hbm_frac >= valu_frac
+    return {
+        "bound": "hbm" if primary_hbm else "valu-int32",
+        "achieved": gbs if primary_hbm else tops,
+        "peak": HBM_PEAK_GBS if primary_hbm else VALU_PEAK_TOPS,
+        "unit": "GB/s" if primary_hbm else "T int32-ops/s",
+        "frac": hbm_frac if primary_hbm else valu_frac,
+        "traffic": None,
+        "kernel": "k_lane_step",
+        "kernel_ms": kernel_ms,
+        "algorithmic_bytes_per_launch": byts,
+        "algorithmic_int32_ops_per_launch": ops,
+        "bytes_per_lane_step": byts / max(steps, 1.0),
+        "int32_ops_per_lane_step": ops / max(steps, 1.0),
+        "alt": {"bound": "valu-int32" if primary_hbm else "hbm",
+                "achieved": tops if primary_hbm else gbs,
+                "peak": VALU_PEAK_TOPS if primary_hbm else HBM_PEAK_GBS,
+                "frac": valu_frac if primary_hbm else hbm_frac},
+    }

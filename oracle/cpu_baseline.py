@@ -1,0 +1,61 @@
+"""CPU baseline of bench.py (TEST INFRASTRUCTURE ONLY): the C oracle, timed on host cores.
+
+The reference (Python LASER + z3) cannot run on the GPU box (not importable, and
+the reference never travels there), so the comparator is the oracle's C port of
+the same semantics (``kind: "port"``), -O3, one pthread per core over disjoint
+lanes.  Bounded sample: the C2 lane batch is re-run from its initial image until
+about `seconds` of CPU time has elapsed.
+"""
+import ctypes
+import os
+import time
+
+from . import lib
+from .evm_ref import OracleEVM
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _usable_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, threads: int = 0) -> dict:
+    from mythril_amd import workloads
+    o = OracleEVM()
+    cid = o.load_code(code)
+    base = workloads.c2_batch(lanes, code_id=cid, stack_cap=64, mem_cap=1024)
+    threads = threads or min(16, _usable_cores())
+    mask = (ctypes.c_uint64 * 4)(0, 0, 0, 0)
+    lib().orc_run_mt.restype = ctypes.c_uint64
+    lib().orc_run_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+
+    def timed(nthreads, budget):
+        steps, el, reps = 0, 0.0, 0
+        while el < budget or reps == 0:
+            b = base.copy()
+            soa = b.soa()
+            t0 = time.perf_counter()
+            steps += int(lib().orc_run_mt(ctypes.addressof(soa), 0, b.n, mask, 1 << 30, 0, nthreads))
+            el += time.perf_counter() - t0
+            reps += 1
+        return steps / el, reps
+
+    single, reps1 = timed(1, min(seconds / 3, 5.0))
+    multi, repsn = timed(threads, seconds)
+    return {"value": multi, "unit": "lane-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C2 batch ({lanes} lanes, overflow.sol.o) x {repsn} runs on {threads} threads; "
+                      f"C oracle oracle/evm_ref.c -O3 ({_cpu_model()})",
+            "single_core_value": single}

@@ -628,3 +628,35 @@ uint64_t orc_run(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_
     }
     return total;
 }
+
+/* Multi-threaded driver for the CPU baseline: one pthread per core over
+ * disjoint lane ranges (lanes are independent paths). */
+#include <pthread.h>
+typedef struct { const mg_lane_soa *h; uint32_t first, n; const uint64_t *mask;
+                 uint32_t max_steps, max_depth; uint64_t steps; } orc_job;
+static void *orc_worker(void *arg) {
+    orc_job *j = (orc_job *)arg;
+    j->steps = orc_run(j->h, j->first, j->n, j->mask, j->max_steps, j->max_depth);
+    return NULL;
+}
+uint64_t orc_run_mt(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
+                    uint32_t max_steps, uint32_t max_depth, uint32_t threads) {
+    init_optable();
+    if (threads <= 1 || n < threads) return orc_run(h, first, n, hook_mask, max_steps, max_depth);
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    orc_job jobs[256];
+    uint32_t per = (n + threads - 1) / threads;
+    uint32_t started = 0;
+    for (uint32_t t = 0; t < threads; ++t) {
+        uint32_t a = first + t * per;
+        if (a >= first + n) break;
+        uint32_t cnt = (a + per > first + n) ? first + n - a : per;
+        jobs[t] = (orc_job){h, a, cnt, hook_mask, max_steps, max_depth, 0};
+        pthread_create(&tid[t], NULL, orc_worker, &jobs[t]);
+        started++;
+    }
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < started; ++t) { pthread_join(tid[t], NULL); total += jobs[t].steps; }
+    return total;
+}
