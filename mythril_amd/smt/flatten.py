@@ -1,0 +1,227 @@
+"""Compile constraint sets (expression DAGs) into kernel-2 register programs.
+
+``get_model`` hands quick-sat ``simplify(And(*constraints))`` (support/model.py:51-54);
+here every constraint set becomes one straight-line program whose last
+instruction leaves the conjunction's truth value in the accumulator:
+
+1. the DAG's internal nodes are scheduled post-order, each shared node once
+   (hash-consing = the reference's z3 AST sharing), larger operand subtrees
+   first so the last-computed operand is still in the accumulator;
+2. a node consumed only by the very next instruction travels in the
+   accumulator; every other node is stored to a slot, slots are reused by a
+   linear scan over live ranges (at most MAX_SLOTS);
+3. leaves are operand references: variables index the model pool, constants a
+   deduplicated pool.
+Sets that need more slots or wider than 256-bit values raise Unsupported and
+stay on z3 (the prefilter may only ever answer SAT).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from .expr import Bool, Node, TRUE
+from .program import (MAX_SLOTS, OPCODE, REF_ACC, REF_CONST, REF_SLOT, REF_VAR, TILE_INSNS,
+                      ProgramBatch, enc_w0, limbs, ref)
+
+_MAP = {"and": "and", "or": "or", "not": "not", "xor": "xor", "implies": "implies"}
+_CMP = {"eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
+        "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u"}
+
+
+class Unsupported(Exception):
+    pass
+
+
+class _Virt:
+    """One device instruction before slot assignment."""
+    __slots__ = ("op", "width", "args", "imm", "node")
+
+    def __init__(self, op, width, args, imm=None, node=None):
+        self.op, self.width, self.args, self.imm, self.node = op, width, args, imm, node
+
+
+class Compiler:
+    def __init__(self):
+        self.var_index: Dict[str, int] = {}
+        self.var_widths: List[int] = []
+        self.const_index: Dict[int, int] = {}
+        self.consts: List[int] = []
+        self.max_slots = 0
+
+    # -- leaves ---------------------------------------------------------------
+    def _leaf_ref(self, n: Node) -> int:
+        if n.op == "const":
+            i = self.const_index.get(n.param)
+            if i is None:
+                i = self.const_index[n.param] = len(self.consts)
+                self.consts.append(n.param)
+            return ref(REF_CONST, i)
+        i = self.var_index.get(n.param)
+        if i is None:
+            i = self.var_index[n.param] = len(self.var_widths)
+            self.var_widths.append(n.width)
+        elif self.var_widths[i] != n.width:
+            raise Unsupported(f"variable {n.param} used at two widths")
+        return ref(REF_VAR, i)
+
+    # -- scheduling -----------------------------------------------------------
+    @staticmethod
+    def _sizes(root: Node, size: Dict[Node, int]):
+        order, st = [], [root]
+        while st:
+            x = st.pop()
+            if x in size or x.op in ("const", "var"):
+                continue
+            size[x] = 0
+            order.append(x)
+            st.extend(x.args)
+        for x in reversed(order):
+            size[x] = 1 + sum(size.get(c, 0) for c in x.args)
+
+    def _emit(self, n: Node, virts: List[_Virt], vid: Dict[Node, int], size: Dict[Node, int]):
+        """Post-order emission of n's subtree; operands with bigger subtrees first so
+        the last-computed operand is still in the accumulator."""
+        stack = [(n, False)]
+        while stack:
+            x, ready = stack.pop()
+            if x in vid or x.op in ("const", "var"):
+                continue
+            if x.width > 256 or any(c.width > 256 for c in x.args):
+                raise Unsupported("bit-vector wider than 256 bits")
+            if not ready:
+                stack.append((x, True))
+                kids = sorted((c for c in set(x.args) if c not in vid and c.op not in ("const", "var")),
+                              key=lambda c: size.get(c, 0))
+                for c in kids:            # pushed smallest-first => computed largest-first
+                    stack.append((c, False))
+                continue
+            self._lower(x, virts, vid)
+
+    def _schedule(self, root: Node) -> List[_Virt]:
+        """The root conjunction And(c1..ck) is folded conjunct by conjunct (one
+        running result in a slot) instead of computing every conjunct first."""
+        size: Dict[Node, int] = {}
+        self._sizes(root, size)
+        virts: List[_Virt] = []
+        vid: Dict[Node, int] = {}
+        conj = list(root.args) if root.op == "and" else [root]
+        running = None
+        for c in conj:
+            self._emit(c, virts, vid, size)
+            cur = ("v", vid[c]) if c in vid else c
+            if running is None:
+                if not isinstance(cur, tuple):
+                    virts.append(_Virt("copy", c.width, [c]))
+                    cur = ("v", len(virts) - 1)
+                running = cur
+            else:
+                virts.append(_Virt("and", 1, [running, cur]))
+                running = ("v", len(virts) - 1)
+        if root.op == "and" and conj:
+            vid[root] = running[1]
+        return virts
+
+    def _lower(self, x: Node, virts: List[_Virt], vid: Dict[Node, int]):
+        def arg(c):
+            return ("v", vid[c]) if c in vid else c
+
+        op = x.op
+        if op in ("and", "or") and len(x.args) > 2:
+            acc = arg(x.args[0])
+            for c in x.args[1:]:
+                virts.append(_Virt(op, 1, [acc, arg(c)]))
+                acc = ("v", len(virts) - 1)
+            vid[x] = len(virts) - 1
+            return
+        if op in ("and", "or") and len(x.args) == 1:
+            virts.append(_Virt("copy", 1, [arg(x.args[0])]))
+        elif op == "extract":
+            virts.append(_Virt("extract", x.width, [arg(x.args[0])], imm=x.param[1]))
+        elif op == "sign_extend":
+            virts.append(_Virt("sign_extend", x.width, [arg(x.args[0])], imm=x.args[0].width))
+        elif op == "concat":
+            virts.append(_Virt("concat", x.width, [arg(x.args[0]), arg(x.args[1])], imm=x.args[1].width))
+        elif op in _CMP:
+            virts.append(_Virt(op, 1, [arg(x.args[0]), arg(x.args[1])], imm=x.args[0].width))
+        elif op in OPCODE:
+            virts.append(_Virt(op, x.width, [arg(c) for c in x.args]))
+        else:
+            raise Unsupported(f"operation {op} is not evaluated on the device")
+        vid[x] = len(virts) - 1
+
+    # -- slots + encoding -----------------------------------------------------
+    def compile(self, root: Node) -> np.ndarray:
+        virts = self._schedule(root)
+        n = len(virts)
+        uses: Dict[int, List[Tuple[int, int]]] = {}
+        for i, v in enumerate(virts):
+            for k, a in enumerate(v.args):
+                if isinstance(a, tuple):
+                    uses.setdefault(a[1], []).append((i, k))
+        needs_slot = {j for j, us in uses.items() if any(i != j + 1 for i, _ in us)}
+        last_use = {j: max(i for i, _ in uses[j]) for j in needs_slot}
+        slot_of: Dict[int, int] = {}
+        free = list(range(MAX_SLOTS - 1, -1, -1))
+        expiring: Dict[int, List[int]] = {}
+        for i in range(n):
+            for s in expiring.pop(i, []):
+                free.append(s)
+            if i in needs_slot:
+                if not free:
+                    raise Unsupported("constraint set needs more than 8 live values")
+                s = free.pop()
+                slot_of[i] = s
+                self.max_slots = max(self.max_slots, s + 1)
+                # the slot frees after its last reader has fetched its operands
+                expiring.setdefault(last_use[i] + 1, []).append(s)
+        out = np.zeros((n, 4), dtype=np.uint32)
+        for i, v in enumerate(virts):
+            refs = []
+            for a in v.args:
+                if isinstance(a, tuple):
+                    j = a[1]
+                    # the previous instruction's result is still in the accumulator
+                    refs.append(ref(REF_ACC, 0) if j == i - 1 else ref(REF_SLOT, slot_of[j]))
+                else:
+                    refs.append(self._leaf_ref(a))
+            w = [enc_w0(v.op, v.width, slot_of.get(i)), 0, 0, 0]
+            for k, r in enumerate(refs):
+                w[1 + k] = r
+            if v.op in ("extract", "sign_extend"):
+                w[2] = v.imm
+            elif v.op == "concat" or v.op in _CMP:
+                w[3] = v.imm
+            out[i] = w
+        if n > TILE_INSNS:
+            raise Unsupported("program longer than one LDS tile")
+        return out
+
+
+def compile_sets(sets: Sequence[Sequence], compiler: Compiler = None) -> Tuple[ProgramBatch, List[int]]:
+    """Compile constraint sets (each a list of Bool / Node) into one ProgramBatch.
+    Returns the batch and the indices of the sets it contains (unsupported sets
+    are left out and must go to z3)."""
+    c = compiler or Compiler()
+    progs, kept = [], []
+    for k, s in enumerate(sets):
+        raws = [x.raw if isinstance(x, Bool) else x for x in s]
+        raws = [r for r in raws if r is not TRUE]
+        root = raws[0] if len(raws) == 1 else (Node("and", 1, tuple(raws)) if raws else TRUE)
+        try:
+            progs.append(c.compile(root))
+            kept.append(k)
+        except Unsupported:
+            continue
+    off = np.zeros(len(progs) + 1, dtype=np.uint32)
+    if progs:
+        off[1:] = np.cumsum([p.shape[0] for p in progs])
+        insns = np.concatenate(progs)
+    else:
+        insns = np.zeros((0, 4), dtype=np.uint32)
+    consts = np.stack([limbs(x) for x in c.consts]) if c.consts else np.zeros((0, 8), np.uint32)
+    names = [None] * len(c.var_widths)
+    for name, i in c.var_index.items():
+        names[i] = name
+    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths)), kept
