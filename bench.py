@@ -34,6 +34,10 @@ def parse():
     ap.add_argument("--lanes", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--c4-dags", type=int, default=1_000_000)
+    ap.add_argument("--c4-models", type=int, default=4096)
+    ap.add_argument("--c4-steps", type=int, default=3)
+    ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--profile-only", action="store_true",
                     help="run warmup+steps with no JSON extras (for rocprofv3)")
     return ap.parse_args()
@@ -103,6 +107,10 @@ def main():
         cov_union = cov
         total_steps = lane_steps
 
+    c4 = None
+    if not args.no_c4:
+        c4 = run_c4(args, dev, rank, world, barrier, dist_on)
+
     if rank == 0 and not args.profile_only:
         value = total_steps / elapsed
         steps_per_batch = lane_steps / max(args.steps, 1)
@@ -132,9 +140,62 @@ def main():
         if not args.no_cpu_baseline:
             from oracle import cpu_baseline
             out["cpu_baseline"] = cpu_baseline.c2_lane_steps(code, args.cpu_seconds)
+        if c4 is not None:
+            if not args.no_cpu_baseline:
+                from oracle import cpu_baseline
+                c4["cpu_baseline"] = cpu_baseline.c4_evals(args.c4_models, args.cpu_seconds)
+            out["constraint_evals"] = c4
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
+
+
+def run_c4(args, dev, rank, world, barrier, dist_on):
+    """C4 (configs[3]): 1M constraint DAGs x 4096 candidate models, DAGs split
+    over ranks (strong scaling), models replicated; kernel 2 only in the timed
+    region (programs and models resident in HBM)."""
+    import torch
+    import torch.distributed as dist
+    from mythril_amd.smt import synth
+    chunks = synth.c4_chunks(args.c4_dags)
+    mine = [c[0] for i, c in enumerate(chunks) if i % world == rank]
+    prog, models = synth.c4_batch(args.c4_dags, args.c4_models, chunks=mine)
+    dev.eval_upload(prog, models)
+    dev.eval_run()                      # warm-up
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.c4_steps):
+        kms.append(dev.eval_run())
+    barrier()
+    el = time.perf_counter() - t0
+    fs, sc = dev.eval_download()
+    evals = prog.n_dags * models.n_models * args.c4_steps
+    n_sat = int((sc > 0).sum())
+    if dist_on:
+        t = torch.tensor([el, float(evals), float(n_sat)], dtype=torch.float64, device="cuda")
+        mx = t[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el, evals, n_sat = float(mx[0]), float(t[1]), int(t[2])
+    ops, gather_bytes = synth.program_cost(prog)
+    k_ms = float(np.mean(kms))
+    ops_launch = ops * models.n_models
+    tops = ops_launch / (k_ms / 1e3) / 1e12
+    from mythril_amd.roofline import VALU_PEAK_TOPS
+    return {
+        "metric": "constraint-evals/s (kernel 2, C4: 1M DAGs depth 32 x 4096 models)",
+        "value": evals / el, "unit": "constraint-evals/s", "n_gpus": world,
+        "ms_per_step": 1000.0 * el / args.c4_steps, "scaling": "strong",
+        "config": {"workload": "C4", "dags": args.c4_dags, "models": args.c4_models,
+                   "dags_with_a_satisfying_model": n_sat},
+        "roofline": {"bound": "valu-int32", "achieved": tops, "peak": VALU_PEAK_TOPS,
+                     "unit": "T int32-ops/s", "frac": tops / VALU_PEAK_TOPS, "traffic": None,
+                     "kernel": "k_bv_eval", "kernel_ms": k_ms,
+                     "algorithmic_int32_ops_per_launch": ops_launch,
+                     "int32_ops_per_eval": ops / max(prog.n_dags, 1),
+                     "model_bytes_per_eval": gather_bytes / max(prog.n_dags, 1)},
+    }
 
 
 if __name__ == "__main__":

@@ -1,0 +1,26 @@
+"""ctypes front end of the C program evaluator (oracle/bv_ref.c) — TEST INFRASTRUCTURE ONLY."""
+import ctypes
+import os
+
+import numpy as np
+
+from . import lib
+
+
+def eval_batch(prog, models, first: int = 0, count: int = None, threads: int = 0):
+    """(first_sat, sat_count) of programs [first, first+count) over every model."""
+    n = prog.n_dags
+    count = n - first if count is None else count
+    threads = threads or min(16, os.cpu_count() or 1)
+    fs = np.zeros(n, dtype=np.uint32)
+    sc = np.zeros(n, dtype=np.uint32)
+    insns = np.ascontiguousarray(prog.insns, dtype=np.uint32)
+    off = np.ascontiguousarray(prog.prog_off, dtype=np.uint32)
+    consts = np.ascontiguousarray(prog.consts if prog.consts.size else np.zeros((1, 8)), dtype=np.uint32)
+    vals = np.ascontiguousarray(models.values, dtype=np.uint32)
+    f = lib().orb_eval
+    f.restype = None
+    f.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] * 5 + [ctypes.c_void_p] * 2 + [ctypes.c_uint32]
+    f(insns.ctypes.data, off.ctypes.data, consts.ctypes.data, vals.ctypes.data, models.n_vars,
+      models.n_models, prog.n_slots, first, count, fs.ctypes.data, sc.ctypes.data, threads)
+    return fs[first:first + count], sc[first:first + count]

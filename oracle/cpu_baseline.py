@@ -59,3 +59,24 @@ def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, thread
             "sample": f"C2 batch ({lanes} lanes, overflow.sol.o) x {repsn} runs on {threads} threads; "
                       f"C oracle oracle/evm_ref.c -O3 ({_cpu_model()})",
             "single_core_value": single}
+
+
+def c4_evals(n_models: int = 4096, seconds: float = 10.0, threads: int = 0) -> dict:
+    """C4 constraint-evals/s of oracle/bv_ref.c on a bounded sample of DAGs (all
+    models), one pthread per core."""
+    from mythril_amd.smt import synth
+    from .bv_ref import eval_batch
+    threads = threads or min(16, _usable_cores())
+    models = synth.c4_models(n_models, synth.C4_SEED + 0x1000)
+    prog = synth.c4_programs(synth.Draws(4096, synth.C4_SEED))
+    done, el, d = 0, 0.0, 0
+    while el < seconds and d < prog.n_dags:
+        cnt = min(threads * 8, prog.n_dags - d)
+        t0 = time.perf_counter()
+        eval_batch(prog, models, first=d, count=cnt, threads=threads)
+        el += time.perf_counter() - t0
+        done += cnt * n_models
+        d += cnt
+    return {"value": done / el, "unit": "constraint-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{d} C4 DAGs x {n_models} models on {threads} threads; oracle/bv_ref.c -O3 "
+                      f"({_cpu_model()})"}

@@ -1,0 +1,104 @@
+"""Kernel-2 host layer on CPU: expression layer, flattener, C4 generator and the
+oracle evaluator agree with a pure-Python evaluation of the expressions."""
+import random
+
+import numpy as np
+import pytest
+
+from mythril_amd.smt import synth
+from mythril_amd.smt.expr import (And, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow,
+                                  Concat, Extract, If, Not, Or, SignExt, UDiv, UGE, UGT, ULE,
+                                  ULT, URem, SRem, LShR, ZeroExt, symbol_factory, Node)
+from mythril_amd.smt.flatten import Compiler, Unsupported, compile_sets
+from mythril_amd.smt.program import ModelPool
+from oracle.bv_ref import eval_batch
+from smt_eval import evaluate
+
+BVS, BVV = symbol_factory.BitVecSym, symbol_factory.BitVecVal
+
+
+def test_c4_programs_match_expressions():
+    dr = synth.Draws(300, seed=synth.C4_SEED)
+    prog = synth.c4_programs(dr)
+    models = synth.c4_models(96)
+    fs, sc = eval_batch(prog, models)
+    for i in range(0, 300, 3):
+        e = synth.dag_expr(dr, i)
+        vals = [evaluate(e, synth.model_dict(models, m)) for m in range(96)]
+        first = next((m for m, v in enumerate(vals) if v), 0xFFFFFFFF)
+        assert (first, sum(vals)) == (fs[i], sc[i]), i
+
+
+def test_c4_full_size_shape_and_determinism():
+    dr = synth.Draws(1000, seed=synth.C4_SEED)
+    a = synth.c4_programs(dr)
+    b = synth.c4_programs(synth.Draws(1000, seed=synth.C4_SEED))
+    assert np.array_equal(a.insns, b.insns) and np.array_equal(a.prog_off, b.prog_off)
+    lens = np.diff(a.prog_off.astype(np.int64))
+    assert 33 <= lens.min() and lens.max() <= 2 + 3 * synth.LEVELS + 1
+    assert 40 < lens.mean() < 70          # ~65 nodes per DAG, about 50 instructions
+
+
+def _random_constraints(rng, n_terms=6):
+    x, y, z = BVS("x", 256), BVS("y", 256), BVS("z", 256)
+    cd = BVS("cd4", 8)
+    terms = [x + y, x - z, x * y, UDiv(x, y), URem(z, x), x / y, SRem(y, z), x & z, x | y,
+             x ^ y, ~x, LShR(x, BVV(7, 256)), x << BVV(3, 256), x >> BVV(200, 256),
+             If(ULT(x, y), x, z), Concat(Extract(127, 0, x), Extract(127, 0, y)),
+             ZeroExt(248, cd), SignExt(248, cd), Extract(7, 0, x + z)]
+    preds = []
+    for _ in range(n_terms):
+        a, b = rng.choice(terms), rng.choice(terms)
+        if a.size() != b.size():
+            b = Extract(a.size() - 1, 0, ZeroExt(256 - b.size(), b)) if b.size() < 256 else \
+                Extract(a.size() - 1, 0, b)
+        k = rng.randrange(12)
+        preds.append([ULT(a, b), UGT(a, b), ULE(a, b), UGE(a, b), a < b, a > b, a <= b, a >= b,
+                      a == b, a != b,
+                      BVAddNoOverflow(a, b, False) if a.size() == b.size() else a == b,
+                      BVSubNoUnderflow(a, b, False)][k])
+    if rng.random() < 0.5:
+        preds.append(Or(preds[0], Not(preds[-1])))
+    if rng.random() < 0.3:
+        preds.append(BVMulNoOverflow(x, y, False))
+    return preds
+
+
+def test_flattener_matches_python_semantics():
+    rng = random.Random(1234)
+    sets = [_random_constraints(rng, rng.randrange(1, 8)) for _ in range(120)]
+    prog, kept = compile_sets(sets)
+    assert len(kept) == len(sets)
+    models_py = []
+    mrng = random.Random(99)
+    specials = [0, 1, 2, (1 << 255), (1 << 256) - 1, (1 << 160) - 1]
+    for _ in range(64):
+        models_py.append({name: (mrng.choice(specials) if mrng.random() < 0.3 else
+                                 mrng.getrandbits(w)) & ((1 << w) - 1)
+                          for name, w in zip(prog.var_names, prog.var_widths)})
+    pool = ModelPool.from_dicts(models_py, prog.var_names, prog.var_widths)
+    fs, sc = eval_batch(prog, pool)
+    for d, s in enumerate(sets):
+        root = And(*s)
+        vals = [evaluate(root.raw, m) for m in models_py]
+        first = next((m for m, v in enumerate(vals) if v), 0xFFFFFFFF)
+        assert (first, sum(vals)) == (fs[d], sc[d]), d
+
+
+def test_flattener_slot_pressure_and_unsupported():
+    x = BVS("x", 256)
+    # 40 conjuncts fold one by one: only the running result needs a slot
+    many = [ULT(x + BVV(k, 256), BVV(10 ** 6 + k, 256)) for k in range(40)]
+    prog, kept = compile_sets([many])
+    assert kept == [0] and prog.n_slots <= 2
+    wide = Concat(x, x)                   # 512-bit keccak-style input: stays on z3
+    prog2, kept2 = compile_sets([[wide == wide]])
+    assert kept2 == []
+
+
+def test_constant_folding_follows_z3():
+    assert (UDiv(BVV(5, 256), BVV(0, 256))).value == (1 << 256) - 1
+    assert (URem(BVV(5, 256), BVV(0, 256))).value == 5
+    assert (BVV(-7, 256) / BVV(2, 256)).value == (-3) % (1 << 256)
+    assert (BVV(1, 256) < BVV(-1, 256)).value is False     # signed <, bitvec.py:140-150
+    assert ULE(BVV(3, 256), BVV(3, 256)).value is True
