@@ -23,26 +23,39 @@ __device__ __forceinline__ uint64_t krotl(uint64_t v, int r) {
     return r == 0 ? v : ((v << r) | (v >> (64 - r)));
 }
 
+// In-place rounds: theta with 5 column parities, rho+pi as the single 24-cycle
+// of the lane permutation (one temporary), chi row by row (5 temporaries) — about
+// 70 live VGPRs instead of the 120 of a two-array formulation.
 __device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
-    constexpr int RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
-                             25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+    constexpr int PILN[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4,
+                              15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+    constexpr int ROTC[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14,
+                              27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
     for (int round = 0; round < 24; ++round) {
-        uint64_t C[5], D[5], B[25];
+        uint64_t bc[5];
 #pragma unroll
-        for (int x = 0; x < 5; ++x) C[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
+        for (int x = 0; x < 5; ++x) bc[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
 #pragma unroll
-        for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ krotl(C[(x + 1) % 5], 1);
+        for (int x = 0; x < 5; ++x) {
+            const uint64_t t = bc[(x + 4) % 5] ^ krotl(bc[(x + 1) % 5], 1);
 #pragma unroll
-        for (int i = 0; i < 25; ++i) st[i] ^= D[i % 5];
+            for (int y = 0; y < 25; y += 5) st[y + x] ^= t;
+        }
+        uint64_t t = st[1];
 #pragma unroll
-        for (int x = 0; x < 5; ++x)
+        for (int i = 0; i < 24; ++i) {
+            const int j = PILN[i];
+            const uint64_t tmp = st[j];
+            st[j] = krotl(t, ROTC[i]);
+            t = tmp;
+        }
 #pragma unroll
-            for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = krotl(st[x + 5 * y], RHO[x + 5 * y]);
+        for (int y = 0; y < 25; y += 5) {
 #pragma unroll
-        for (int y = 0; y < 5; ++y)
+            for (int x = 0; x < 5; ++x) bc[x] = st[y + x];
 #pragma unroll
-            for (int x = 0; x < 5; ++x)
-                st[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+            for (int x = 0; x < 5; ++x) st[y + x] = bc[x] ^ (~bc[(x + 1) % 5] & bc[(x + 2) % 5]);
+        }
         st[0] ^= kKeccakRC[round];
     }
 }

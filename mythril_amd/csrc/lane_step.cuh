@@ -24,9 +24,6 @@ struct OpInfo {
     uint32_t req;          // STACK[0]: items required by the svm precheck
     uint32_t valid;        // 0 -> disassembles to INVALID
 };
-__constant__ OpInfo kOp[256];
-// opcodes whose semantics need the host (symbolic values, world state, calls)
-__constant__ uint64_t kEscape[4];
 
 #define ST_RUNNING 0u
 #define ST_STOP 1u
@@ -211,7 +208,76 @@ DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
     return r;
 }
 
+// ---- decode table -----------------------------------------------------------------
+// One uint2 per opcode byte, built on the host (mythgpu.hip build_decode):
+//   x = gas_min | gas_max << 16                  (support/opcodes.py:16-144 GAS)
+//   y = req | npop << 4 | push << 8 | kind << 9  (req: svm precheck STACK[0];
+//       npop: words the mutator really pops; push: leaves one word; kind: handler)
+enum OpKind : uint32_t {
+    K_ALU = 0, K_PUSH, K_DUP, K_SWAP, K_LOG, K_POP, K_ENV, K_STOP, K_SHA3, K_CDLOAD, K_CDCOPY,
+    K_CODECOPY, K_RDCOPY, K_MLOAD, K_MSTORE, K_MSTORE8, K_SLOAD, K_SSTORE, K_JUMP, K_JUMPI,
+    K_JUMPDEST, K_BEGINSUB, K_RETURN, K_REVERT, K_INVALID, K_ESCAPE
+};
+__constant__ uint2 kDec[256];
+
+// Generic ALU opcodes: res = f(a, b, c) with a the first word popped.
+__device__ __noinline__ U256 alu_slow(uint32_t op, U256 a, U256 b, U256 c) {
+    switch (op) {
+    case 0x04: return u_iszero(b) ? u_zero() : z_udiv(a, b);            // DIV  (:505-520)
+    case 0x05: return u_iszero(b) ? u_zero() : z_sdiv(a, b);            // SDIV (:522-537)
+    case 0x06: return u_iszero(b) ? u_zero() : z_urem(a, b);            // MOD  (:539-551)
+    case 0x07: return u_iszero(b) ? u_zero() : z_srem(a, b);            // SMOD (:580-592)
+    case 0x08: return z_urem(u_add(z_urem(a, c), z_urem(b, c)), c);     // ADDMOD quirk (:594-607)
+    case 0x09: return z_urem(u_mul(z_urem(a, c), z_urem(b, c)), c);     // MULMOD quirk (:609-622)
+    case 0x0a: return u_exp(a, b);                                      // EXP concrete
+    default: return u_zero();
+    }
+}
+DEV U256 alu(uint32_t op, const U256 &a, const U256 &b, const U256 &c) {
+    switch (op) {
+    case 0x01: return u_add(a, b);
+    case 0x02: return u_mul(a, b);
+    case 0x03: return u_sub(a, b);
+    case 0x0b: {  // SIGNEXTEND with the signed test s0 <= 31 (:640-668)
+        const U256 tb = u_add(u_shl_n(a, 3u), u_small(7));
+        const U256 set = u_shl(u_small(1), tb);
+        const bool sign = !u_iszero(u_and(b, set));
+        if (u_slt(u_small(31), a)) return b;
+        return sign ? u_or(b, u_neg(set)) : u_and(b, u_sub(set, u_small(1)));
+    }
+    case 0x10: return u_small(u_lt(a, b));
+    case 0x11: return u_small(u_lt(b, a));
+    case 0x12: return u_small(u_slt(a, b));
+    case 0x13: return u_small(u_slt(b, a));
+    case 0x14: return u_small(u_eq(a, b));
+    case 0x15: return u_small(u_iszero(a));
+    case 0x16: return u_and(a, b);
+    case 0x17: return u_or(a, b);
+    case 0x18: return u_xor(a, b);
+    case 0x19: return u_not(a);
+    case 0x1a: {  // BYTE (:426-456)
+        U256 r = u_zero();
+        if (u_fits32(a) && a.w[0] <= 31u) r.w[0] = u_shr_n(b, (31u - a.w[0]) * 8u, 0u).w[0] & 0xffu;
+        return r;
+    }
+    case 0x1b: return u_shl(b, a);    // value << shift
+    case 0x1c: return u_lshr(b, a);
+    case 0x1d: return u_ashr(b, a);
+    default: return alu_slow(op, a, b, c);
+    }
+}
+
 // ---- the stepping kernel -------------------------------------------------------
+// Latency is the bound at this batch size (65,536 lanes = one wave per SIMD), so
+// the loop keeps every per-step dependency on chip:
+//   * the block's code is pre-decoded into LDS: one 8-byte LDS read per step
+//     yields opcode, gas, stack counts and handler kind;
+//   * the two top stack words live in registers (T0 = S[sp-1], T1 = S[sp-2]);
+//     HBM/L2 holds S[0 .. sp-2) and is read only for deeper operands;
+//   * coverage bits are collected in LDS and flushed once per launch.
+#define OPS_LDS 4096u     // instructions pre-decoded per block
+#define PUSH_LDS 1024u    // push immediates staged per block (32 B each)
+
 __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
                                                    const uint8_t *__restrict__ a8,
                                                    const uint32_t *__restrict__ a32,
@@ -220,60 +286,105 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                                                    uint32_t max_steps, uint32_t max_depth,
                                                    DevCounters *__restrict__ ctr,
                                                    unsigned long long *__restrict__ prof) {
-    // optional instruction profile (the InstructionProfiler plugin's per-opcode
-    // counts, instruction_profiler.py:41-115, as native counters): 256 opcode
-    // counts + [sha3 bytes, copy bytes, storage entries scanned, sha3 blocks]
+    __shared__ uint2 s_dec[256];
+    __shared__ uint2 s_pd[OPS_LDS];          // x = gas min | max << 16, y = op | dec.y << 8
+    __shared__ uint4 s_push[PUSH_LDS * 2];
+    __shared__ uint8_t s_cov[OPS_LDS];
+    __shared__ uint32_t s_code;
+    // optional instruction profile (InstructionProfiler's per-opcode counts,
+    // instruction_profiler.py:41-115, as native counters): 256 opcode counts +
+    // [sha3 bytes, copy bytes, storage entries scanned, keccak blocks]
     __shared__ uint32_t s_prof[260];
-    if (prof) {
-        for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x) s_prof[i] = 0u;
-        __syncthreads();
-    }
+
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in_range = lane < L.n;
     uint32_t status = in_range ? L.status[lane] : ST_STOP;
+    const uint32_t my_code = in_range ? L.code_id[lane] : 0u;
+    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_dec[i] = kDec[i];
+    if (prof)
+        for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x) s_prof[i] = 0u;
+    if (threadIdx.x == 0) s_code = 0xffffffffu;
+    __syncthreads();
+    if (status == ST_RUNNING) s_code = my_code;      // any running lane's code (benign race)
+    __syncthreads();
+    const uint32_t bcode = s_code;
+    const bool mixed = __syncthreads_or(status == ST_RUNNING && my_code != bcode);
+    bool staged = false, push_staged = false;
+    if (bcode != 0xffffffffu && !mixed) {
+        const DevCode BC = codes[bcode];
+        if (BC.n_instr <= OPS_LDS) {
+            for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x) {
+                const uint32_t op = a8[BC.op_off + i];
+                const uint2 d = kDec[op];
+                s_pd[i] = make_uint2(d.x, op | (d.y << 8));
+                s_cov[i] = 0;
+            }
+            if (BC.n_instr <= PUSH_LDS) {
+                const uint4 *gp = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
+                for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gp[i];
+                push_staged = true;
+            }
+            staged = true;
+        }
+        __syncthreads();
+    }
     uint32_t executed = 0;
 
     if (status == ST_RUNNING) {
         const LaneView V{L, lane};
-        const DevCode C = codes[L.code_id[lane]];
-        const uint8_t *__restrict__ ops = a8 + C.op_off;
+        const DevCode C = codes[my_code];
+        const uint8_t *__restrict__ gops = a8 + C.op_off;
+        const uint4 *__restrict__ gpush = reinterpret_cast<const uint4 *>(a32 + C.push_off);
         const uint32_t flags = L.flags[lane];
         const uint64_t txlim = L.gas_limit[lane];
         uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
         uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
         uint32_t aux = 0, n_sha3 = 0, n_exp = 0;
-        const uint64_t mask[4] = {m0, m1, m2, m3};
+        U256 T0 = sp >= 1u ? V.stack(sp - 1u) : u_zero();
+        U256 T1 = sp >= 2u ? V.stack(sp - 2u) : u_zero();
 
         for (;;) {
             if (max_depth != 0u && depth >= max_depth) { status = ST_DEPTH; break; }
             if (pc >= C.n_instr) { status = ST_END; break; }
-            const uint32_t op = ops[pc];
-            if ((mask[op >> 6] >> (op & 63u)) & 1ull) { status = ST_HOOK; aux = op; break; }
+            uint2 pd;
+            if (staged) pd = s_pd[pc];
+            else {
+                const uint32_t o = gops[pc];
+                const uint2 d = s_dec[o];
+                pd = make_uint2(d.x, o | (d.y << 8));
+            }
+            const uint32_t op = pd.y & 0xffu;
+            const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
+            if ((hm >> (op & 63u)) & 1ull) { status = ST_HOOK; aux = op; break; }
             if (executed >= max_steps) break;
-            if (((kEscape[op >> 6] >> (op & 63u)) & 1ull) ||
-                ((flags & LANE_CREATION) && op >= 0x35u && op <= 0x39u)) {
+            const uint32_t kind = pd.y >> 17;
+            if (kind == K_ESCAPE || ((flags & LANE_CREATION) && op >= 0x35u && op <= 0x39u)) {
                 status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
             }
-            if (cov_on && cov[C.cov_off + pc] == 0) cov[C.cov_off + pc] = 1;
+            if (cov_on) {
+                if (staged) s_cov[pc] = 1;
+                else cov[C.cov_off + pc] = 1;
+            }
             if (prof) atomicAdd(&s_prof[op], 1u);
             ++executed;
 
-            const OpInfo info = kOp[op];
+            const uint32_t req = (pd.y >> 8) & 15u, npop = (pd.y >> 12) & 15u;
+            const bool push = ((pd.y >> 16) & 1u) != 0u;
+            const uint32_t gtab_min = pd.x & 0xffffu, gtab_max = pd.x >> 16;
             const uint32_t msize0 = msize;
-            uint32_t nsp = sp, nmsize = msize, ndepth = depth, npc = pc + 1u;
+            uint32_t nmsize = msize, ndepth = depth, npc = pc + 1u;
             uint64_t ngmin = gmin, ngmax = gmax;
             uint32_t stop = ST_RUNNING, sx = 0;
-            bool by_table = true;
+            bool by_table = true, tos_done = false;
+            U256 a = T0, b = T1, c = u_zero(), res = u_zero();
+            U256 nT0 = T0, nT1 = T1;
+            uint32_t nsp = sp;
 
 #define STOPX(s_, x_) { stop = (s_); sx = (x_); break; }
 #define EXCX(k_) STOPX(ST_VMEXC, (k_))
 #define ESCX(r_) STOPX(ST_ESCAPE, op | ((r_) << 8))
-#define NEEDPOP(k_) if (nsp < (uint32_t)(k_)) EXCX(EXC_UNDERFLOW)
-#define GASCOMMIT() if (by_table) { ngmin += info.gmin; ngmax += info.gmax; by_table = false; \
+#define GASCOMMIT() if (by_table) { ngmin += gtab_min; ngmax += gtab_max; by_table = false; \
                                     if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG) }
-#define PUSHV(v_) { if (nsp + 1u > STACK_LIMIT) EXCX(EXC_OVERFLOW) \
-                    if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK) \
-                    GASCOMMIT() V.set_stack(nsp, (v_)); ++nsp; }
 #define MEMX(st_, sz_, later_) { const int mx_ = mem_extend((st_), (sz_), nmsize, ngmin, ngmax, \
                                                         L.mem_cap, (later_), txlim); \
                                  if (mx_ == MX_OOG) EXCX(EXC_OOG) if (mx_ == MX_ESCAPE) ESCX(ESC_MEMORY) }
@@ -281,90 +392,62 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
 
             do {
                 // svm.py:391-402 precheck; instructions.py:188-193 write protection
-                if (sp < info.req) EXCX(EXC_UNDERFLOW)
+                if (sp < req) EXCX(EXC_UNDERFLOW)
                 if ((flags & LANE_STATIC) && (op == 0x55u || (op >= 0xa0u && op <= 0xa4u)))
                     EXCX(EXC_WRITEPROT)
-                if (op >= 0x60u && op <= 0x7fu) {                       // PUSH1..32
-                    const U256 v = ld_word(reinterpret_cast<const uint4 *>(a32 + C.push_off), pc);
-                    PUSHV(v)
+                // operands: what the mutator pops (ADDMOD, SSTORE pop more than `req`)
+                if (sp < npop) EXCX(EXC_UNDERFLOW)
+                if (npop >= 3u) c = V.stack(sp - 3u);
+                nsp = sp - npop;
+                switch (kind) {
+                case K_ALU:
+                    if (op == 0x0a) ++n_exp;
+                    res = alu(op, a, b, c);
                     break;
-                }
-                if (op >= 0x80u && op <= 0x8fu) {                       // DUP1..16
+                case K_PUSH:                                        // (:278-320)
+                    res = push_staged ? ld_word(s_push, pc) : ld_word(gpush, pc);
+                    break;
+                case K_DUP: {                                       // (:322-331)
                     const uint32_t k = op - 0x7fu;
-                    NEEDPOP(k)
-                    const U256 v = V.stack(nsp - k);
-                    PUSHV(v)
+                    if (sp < k) EXCX(EXC_UNDERFLOW)
+                    res = k == 1u ? T0 : k == 2u ? T1 : V.stack(sp - k);
                     break;
                 }
-                if (op >= 0x90u && op <= 0x9fu) {                       // SWAP1..16
+                case K_SWAP: {                                      // (:333-343)
                     const uint32_t k = op - 0x8fu;
-                    NEEDPOP(k + 1u)
-                    const U256 a = V.stack(nsp - 1u), b = V.stack(nsp - 1u - k);
-                    GASCOMMIT()
-                    V.set_stack(nsp - 1u, b);
-                    V.set_stack(nsp - 1u - k, a);
+                    if (sp < k + 1u) EXCX(EXC_UNDERFLOW)
+                    if (k == 1u) {
+                        GASCOMMIT()
+                        nT0 = T1; nT1 = T0;
+                    } else {
+                        const U256 x = V.stack(sp - 1u - k);
+                        GASCOMMIT()
+                        V.set_stack(sp - 1u - k, T0);
+                        nT0 = x;
+                    }
+                    tos_done = true;
                     break;
                 }
-                if (op >= 0xa0u && op <= 0xa4u) {                       // LOG0..4: pops only
-                    NEEDPOP(2u + (op - 0xa0u))
-                    nsp -= 2u + (op - 0xa0u);
+                case K_LOG: case K_POP: case K_RDCOPY: case K_JUMPDEST:
+                    break;                                          // pops only / no-op
+                case K_ENV:
+                    switch (op) {
+                    case 0x30: res = V.env(0); break;               // ADDRESS
+                    case 0x32: res = V.env(2); break;               // ORIGIN
+                    case 0x33: res = V.env(1); break;               // CALLER
+                    case 0x34: res = V.env(3); break;               // CALLVALUE
+                    case 0x3a: res = V.env(4); break;               // GASPRICE
+                    case 0x36: res = u_small(L.calldata_len[lane]); break;
+                    case 0x38: res = u_small(C.n_bytes); break;     // CODESIZE
+                    case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
+                    case 0x58: res = u_small(a32[C.addr_off + pc]); break;
+                    case 0x59: res = u_small(msize0); break;
+                    default: res = u_zero(); break;                 // RETURNDATASIZE
+                    }
                     break;
-                }
-                U256 a, b, c;
-                switch (op) {
-                case 0x00: STOPX(ST_STOP, 0u)
-                case 0x01: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_add(a, b)) break;
-                case 0x02: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_mul(a, b)) break;
-                case 0x03: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_sub(a, b)) break;
-                case 0x04: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    PUSHV(u_iszero(b) ? u_zero() : z_udiv(a, b)) break;
-                case 0x05: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    PUSHV(u_iszero(b) ? u_zero() : z_sdiv(a, b)) break;
-                case 0x06: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    PUSHV(u_iszero(b) ? u_zero() : z_urem(a, b)) break;
-                case 0x07: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    PUSHV(u_iszero(b) ? u_zero() : z_srem(a, b)) break;
-                case 0x08:  // ADDMOD: URem(URem(a,n) + URem(b,n), n), 256-bit wrap
-                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
-                    PUSHV(z_urem(u_add(z_urem(a, c), z_urem(b, c)), c)) break;
-                case 0x09:  // MULMOD: URem(URem(a,n) * URem(b,n), n)
-                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
-                    PUSHV(z_urem(u_mul(z_urem(a, c), z_urem(b, c)), c)) break;
-                case 0x0a:  // EXP, concrete pow(b, e, 2^256)
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    ++n_exp;
-                    PUSHV(u_exp(a, b)) break;
-                case 0x0b: {  // SIGNEXTEND with the signed test s0 <= 31
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    const U256 tb = u_add(u_shl_n(a, 3u), u_small(7));
-                    const U256 set = u_shl(u_small(1), tb);
-                    const bool sign = !u_iszero(u_and(b, set));
-                    const bool le31 = !u_slt(u_small(31), a);
-                    const U256 r = le31 ? (sign ? u_or(b, u_neg(set)) : u_and(b, u_sub(set, u_small(1)))) : b;
-                    PUSHV(r) break;
-                }
-                case 0x10: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_lt(a, b))) break;
-                case 0x11: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_lt(b, a))) break;
-                case 0x12: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_slt(a, b))) break;
-                case 0x13: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_slt(b, a))) break;
-                case 0x14: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_small(u_eq(a, b))) break;
-                case 0x15: NEEDPOP(1) a = V.stack(--nsp); PUSHV(u_small(u_iszero(a))) break;
-                case 0x16: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_and(a, b)) break;
-                case 0x17: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_or(a, b)) break;
-                case 0x18: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_xor(a, b)) break;
-                case 0x19: NEEDPOP(1) a = V.stack(--nsp); PUSHV(u_not(a)) break;
-                case 0x1a: {  // BYTE
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    U256 r = u_zero();
-                    if (u_fits32(a) && a.w[0] <= 31u) r.w[0] = u_shr_n(b, (31u - a.w[0]) * 8u, 0u).w[0] & 0xffu;
-                    PUSHV(r) break;
-                }
-                case 0x1b: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_shl(b, a)) break;
-                case 0x1c: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_lshr(b, a)) break;
-                case 0x1d: NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp); PUSHV(u_ashr(b, a)) break;
-                case 0x20: {  // SHA3: own gas first, then mem_extend (instructions.py:1013-1051)
+                case K_STOP: STOPX(ST_STOP, 0u)
+                case K_SHA3: {  // own gas first, then mem_extend (instructions.py:1013-1051)
                     by_table = false;
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
                     const bool big = (b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u;
                     const uint64_t blen = (uint64_t)b.w[0] | ((uint64_t)b.w[1] << 32);
                     const uint64_t g = (big || blen > BIG_END) ? HUGE_GAS : 30ull + 6ull * ((blen + 31ull) >> 5);
@@ -372,58 +455,49 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                     if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
                     MEMX(a, b, -1)
                     ZEROFILL()
-                    U256 h;
                     if (b.w[0] == 0u) {  // get_empty_keccak_hash (keccak_function_manager.py:87-93)
-                        h.w[7] = 0xc5d24601u; h.w[6] = 0x86f7233cu; h.w[5] = 0x927e7db2u; h.w[4] = 0xdcc703c0u;
-                        h.w[3] = 0xe500b653u; h.w[2] = 0xca82273bu; h.w[1] = 0x7bfad804u; h.w[0] = 0x5d85a470u;
+                        res.w[7] = 0xc5d24601u; res.w[6] = 0x86f7233cu; res.w[5] = 0x927e7db2u; res.w[4] = 0xdcc703c0u;
+                        res.w[3] = 0xe500b653u; res.w[2] = 0xca82273bu; res.w[1] = 0x7bfad804u; res.w[0] = 0x5d85a470u;
                     } else {
-                        h = keccak_mem(V, a.w[0], b.w[0]);
+                        res = keccak_mem(V, a.w[0], b.w[0]);
+                        if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
                     }
-                    if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
                     ++n_sha3;
-                    V.set_stack(nsp, h); ++nsp;   // pops 2, pushes 1: cannot overflow
                     break;
                 }
-                case 0x30: PUSHV(V.env(0)) break;   // ADDRESS
-                case 0x32: PUSHV(V.env(2)) break;   // ORIGIN
-                case 0x33: PUSHV(V.env(1)) break;   // CALLER
-                case 0x34: PUSHV(V.env(3)) break;   // CALLVALUE
-                case 0x3a: PUSHV(V.env(4)) break;   // GASPRICE
-                case 0x35: {  // CALLDATALOAD: byte (off+k) mod 2^256, 0 past the end
-                    NEEDPOP(1) a = V.stack(--nsp);
+                case K_CDLOAD: {  // byte (off+k) mod 2^256, 0 past the end (calldata.py:46-90,137-146)
                     const uint32_t cdl = L.calldata_len[lane];
-                    U256 r;
                     const bool fits = u_fits32(a);
                     if (fits && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl) {
                         const uint32_t d0 = a.w[0] >> 2;
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) r.w[7 - k] = L.calldata[V.row(d0 + k)];
+                        for (int k = 0; k < 8; ++k) res.w[7 - k] = L.calldata[V.row(d0 + k)];
                     } else {
                         bool wrapc = true;
 #pragma unroll
                         for (int k = 1; k < 8; ++k) wrapc = wrapc && a.w[k] == 0xffffffffu;
-                        r = u_zero();
-#pragma unroll
-                        for (int k = 0; k < 32; ++k) {
-                            const uint64_t t = (uint64_t)a.w[0] + (uint64_t)k;
+                        for (uint32_t k = 0; k < 32u; ++k) {
+                            const uint64_t t = (uint64_t)a.w[0] + k;
                             bool ok = false;
                             uint32_t idx = 0;
                             if (fits) { ok = t < cdl; idx = (uint32_t)t; }
                             else if (wrapc && t >= (1ull << 32)) { idx = (uint32_t)(t - (1ull << 32)); ok = idx < cdl; }
-                            if (ok) r.w[7 - k / 4] |= V.cbyte(idx) << (24 - 8 * (k % 4));
+                            if (ok) {
+                                const uint32_t byte = V.cbyte(idx), sh = 8u * (31u - k);
+                                res = u_or(res, u_shl_n(u_small(byte), sh));
+                            }
                         }
                     }
-                    PUSHV(r) break;
+                    break;
                 }
-                case 0x36: PUSHV(u_small(L.calldata_len[lane])) break;
-                case 0x37: {  // CALLDATACOPY: nothing at all for size 0
-                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
+                case K_CDCOPY: {  // nothing at all for size 0 (:806-891)
                     if (u_iszero(c)) break;
-                    MEMX(a, c, (int64_t)info.gmin)
+                    MEMX(a, c, (int64_t)gtab_min)
                     GASCOMMIT()
                     ZEROFILL()
                     const uint32_t cdl = L.calldata_len[lane];
-                    bool bfits = u_fits32(b), wrapc = true;
+                    const bool bfits = u_fits32(b);
+                    bool wrapc = true;
 #pragma unroll
                     for (int k = 1; k < 8; ++k) wrapc = wrapc && b.w[k] == 0xffffffffu;
                     if (prof) atomicAdd(&s_prof[257], c.w[0]);
@@ -436,10 +510,8 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                     }
                     break;
                 }
-                case 0x38: PUSHV(u_small(C.n_bytes)) break;  // CODESIZE
-                case 0x39: {  // CODECOPY: extends even for size 0; copy stops at the end of code
-                    NEEDPOP(3) a = V.stack(--nsp); b = V.stack(--nsp); c = V.stack(--nsp);
-                    MEMX(a, c, (int64_t)info.gmin)
+                case K_CODECOPY: {  // extends even for size 0; copy stops at the end of code
+                    MEMX(a, c, (int64_t)gtab_min)
                     GASCOMMIT()
                     ZEROFILL()
                     uint32_t ncopy = 0u;
@@ -448,47 +520,34 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                     for (uint32_t k = 0; k < ncopy; ++k) V.set_mbyte(a.w[0] + k, a8[C.bytes_off + b.w[0] + k]);
                     break;
                 }
-                case 0x3d: PUSHV(u_zero()) break;                 // RETURNDATASIZE: none
-                case 0x3e: NEEDPOP(3) nsp -= 3u; break;           // RETURNDATACOPY: no-op
-                case 0x45: PUSHV(u_small(MSTATE_GAS_LIMIT)) break; // GASLIMIT
-                case 0x50: NEEDPOP(1) nsp -= 1u; break;           // POP
-                case 0x51: {  // MLOAD
-                    NEEDPOP(1) a = V.stack(--nsp);
-                    MEMX(a, u_small(32), (int64_t)info.gmin)
+                case K_MLOAD:
+                    MEMX(a, u_small(32), (int64_t)gtab_min)
                     GASCOMMIT()
                     ZEROFILL()
-                    V.set_stack(nsp, V.mword(a.w[0])); ++nsp;
+                    res = V.mword(a.w[0]);
                     break;
-                }
-                case 0x52: {  // MSTORE
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    MEMX(a, u_small(32), (int64_t)info.gmin)
+                case K_MSTORE:
+                    MEMX(a, u_small(32), (int64_t)gtab_min)
                     GASCOMMIT()
                     ZEROFILL()
                     V.set_mword(a.w[0], b);
                     break;
-                }
-                case 0x53: {  // MSTORE8
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
-                    MEMX(a, u_small(1), (int64_t)info.gmin)
+                case K_MSTORE8:
+                    MEMX(a, u_small(1), (int64_t)gtab_min)
                     GASCOMMIT()
                     ZEROFILL()
                     V.set_mbyte(a.w[0], b.w[0] & 0xffu);
                     break;
-                }
-                case 0x54: {  // SLOAD over K(0) + stores
-                    NEEDPOP(1) a = V.stack(--nsp);
+                case K_SLOAD: {  // over K(0) + stores (account.py:43-74)
                     const uint32_t cnt = L.storage_count[lane];
                     if (prof) atomicAdd(&s_prof[258], cnt);
-                    U256 r = u_zero();
                     for (uint32_t s = 0; s < cnt; ++s) {
                         const size_t base = V.row(s) * 2;
-                        if (u_eq(ld_word(L.storage, base), a)) { r = ld_word(L.storage, base + 1); break; }
+                        if (u_eq(ld_word(L.storage, base), a)) { res = ld_word(L.storage, base + 1); break; }
                     }
-                    PUSHV(r) break;
+                    break;
                 }
-                case 0x55: {  // SSTORE
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                case K_SSTORE: {
                     const uint32_t cnt = L.storage_count[lane];
                     if (prof) atomicAdd(&s_prof[258], cnt);
                     uint32_t slot = cnt;
@@ -503,56 +562,71 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                     st_word(L.storage, V.row(slot) * 2 + 1, b);
                     break;
                 }
-                case 0x56: {  // JUMP: gas 8 by hand, no OOG check
+                case K_JUMP: {  // gas 8 by hand, no OOG check (:1520-1556)
                     by_table = false;
-                    NEEDPOP(1) a = V.stack(--nsp);
                     uint32_t idx = MG_JRES_NONE;
                     if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
-                    if (idx == MG_JRES_NONE || ops[idx] != 0x5bu) EXCX(EXC_BADJUMP)
+                    if (idx == MG_JRES_NONE ||
+                        (staged ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) != 0x5bu) EXCX(EXC_BADJUMP)
                     ngmin += 8u; ngmax += 8u; npc = idx;
                     break;
                 }
-                case 0x57: {  // JUMPI: gas 10 by hand, depth + 1 on the side taken
+                case K_JUMPI: {  // gas 10 by hand, depth + 1 on the side taken (:1558-1636)
                     by_table = false;
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
                     if (u_iszero(b)) {
                         ngmin += 10u; ngmax += 10u; ++ndepth;
                     } else {
                         uint32_t idx = MG_JRES_NONE;
                         if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
-                        if (idx == MG_JRES_NONE || ops[idx] != 0x5bu) STOPX(ST_DROPPED, 0u)
+                        if (idx == MG_JRES_NONE ||
+                            (staged ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) != 0x5bu) STOPX(ST_DROPPED, 0u)
                         ngmin += 10u; ngmax += 10u; ++ndepth; npc = idx;
                     }
                     break;
                 }
-                case 0x58: PUSHV(u_small(a32[C.addr_off + pc])) break;  // PC
-                case 0x59: PUSHV(u_small(msize0)) break;                // MSIZE
-                case 0x5b: break;                                        // JUMPDEST
-                case 0x5c: EXCX(EXC_OOG)                                // BEGINSUB
-                case 0xf3: {  // RETURN
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                case K_BEGINSUB: EXCX(EXC_OOG)
+                case K_RETURN:  // (:1857-1874)
                     MEMX(a, b, 0)
                     if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
                     L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
                     STOPX(ST_RETURN, 0u)
-                }
-                case 0xfd: {  // REVERT: no memory extension
-                    NEEDPOP(2) a = V.stack(--nsp); b = V.stack(--nsp);
+                case K_REVERT:  // no memory extension (:1899-1934)
                     L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
                     STOPX(ST_REVERT, 0u)
-                }
-                case 0xfe: EXCX(EXC_INVALID)
+                case K_INVALID: EXCX(EXC_INVALID)
                 default: ESCX(ESC_OPCODE)
                 }
                 if (stop != ST_RUNNING) break;
+                if (!tos_done) {
+                    // new top-of-stack registers from the pops/push of this opcode
+                    if (push) {   // MachineStack.append: overflow check precedes the write
+                        if (nsp + 1u > STACK_LIMIT) EXCX(EXC_OVERFLOW)
+                        if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK)
+                        GASCOMMIT()
+                        if (npop == 0u) {            // T1 moves below the register window
+                            if (sp >= 2u) V.set_stack(sp - 2u, T1);
+                            nT1 = T0;
+                        } else if (npop == 1u) {
+                            nT1 = T1;
+                        } else {
+                            nT1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+                        }
+                        nT0 = res;
+                        ++nsp;
+                    } else if (npop == 1u) {
+                        nT0 = T1;
+                        nT1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                    } else if (npop >= 2u) {
+                        nT0 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+                        nT1 = sp >= npop + 2u ? V.stack(sp - npop - 2u) : u_zero();
+                    }
+                }
                 GASCOMMIT()
             } while (0);
 #undef STOPX
 #undef EXCX
 #undef ESCX
-#undef NEEDPOP
 #undef GASCOMMIT
-#undef PUSHV
 #undef MEMX
 #undef ZEROFILL
             if (stop != ST_RUNNING) {
@@ -562,7 +636,11 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
                 break;
             }
             pc = npc; sp = nsp; msize = nmsize; depth = ndepth; gmin = ngmin; gmax = ngmax;
+            T0 = nT0; T1 = nT1;
         }
+        // flush the register window: memory holds the canonical S[0 .. sp)
+        if (sp >= 1u) V.set_stack(sp - 1u, T0);
+        if (sp >= 2u) V.set_stack(sp - 2u, T1);
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;
@@ -571,6 +649,12 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
         if (n_exp) L.exp_count[lane] += n_exp;
     }
 
+    if (staged && cov_on) {
+        __syncthreads();
+        const DevCode BC = codes[bcode];
+        for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x)
+            if (s_cov[i]) cov[BC.cov_off + i] = 1;
+    }
     if (prof) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x)

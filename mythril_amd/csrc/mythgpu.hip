@@ -108,6 +108,52 @@ static void build_escape(uint64_t m[4]) {
     for (int b : esc) m[b >> 6] |= 1ull << (b & 63);
 }
 
+// Per-byte decode entry of kernel 1 (lane_step.cuh kDec): gas, precheck count,
+// words popped by the mutator, whether it pushes, and the handler kind.
+static void build_decode(uint2 d[256]) {
+    OpInfo t[256];
+    build_optable(t);
+    uint64_t esc[4];
+    build_escape(esc);
+    for (int b = 0; b < 256; ++b) {
+        uint32_t kind = K_INVALID, npop = 0, push = 0;
+        if (t[b].valid && ((esc[b >> 6] >> (b & 63)) & 1ull)) kind = K_ESCAPE;
+        else if (!t[b].valid || b == 0xfe) kind = K_INVALID;
+        else if (b == 0x00) kind = K_STOP;
+        else if ((b >= 0x01 && b <= 0x0b) || (b >= 0x10 && b <= 0x1d)) {
+            kind = K_ALU; push = 1;
+            npop = (b == 0x08 || b == 0x09) ? 3 : (b == 0x15 || b == 0x19) ? 1 : 2;
+        } else if (b >= 0x60 && b <= 0x7f) { kind = K_PUSH; push = 1; }
+        else if (b >= 0x80 && b <= 0x8f) { kind = K_DUP; push = 1; }
+        else if (b >= 0x90 && b <= 0x9f) kind = K_SWAP;
+        else if (b >= 0xa0 && b <= 0xa4) { kind = K_LOG; npop = 2 + (b - 0xa0); }
+        else switch (b) {
+            case 0x20: kind = K_SHA3; npop = 2; push = 1; break;
+            case 0x30: case 0x32: case 0x33: case 0x34: case 0x36: case 0x38: case 0x3a:
+            case 0x3d: case 0x45: case 0x58: case 0x59: kind = K_ENV; push = 1; break;
+            case 0x35: kind = K_CDLOAD; npop = 1; push = 1; break;
+            case 0x37: kind = K_CDCOPY; npop = 3; break;
+            case 0x39: kind = K_CODECOPY; npop = 3; break;
+            case 0x3e: kind = K_RDCOPY; npop = 3; break;
+            case 0x50: kind = K_POP; npop = 1; break;
+            case 0x51: kind = K_MLOAD; npop = 1; push = 1; break;
+            case 0x52: kind = K_MSTORE; npop = 2; break;
+            case 0x53: kind = K_MSTORE8; npop = 2; break;
+            case 0x54: kind = K_SLOAD; npop = 1; push = 1; break;
+            case 0x55: kind = K_SSTORE; npop = 2; break;
+            case 0x56: kind = K_JUMP; npop = 1; break;
+            case 0x57: kind = K_JUMPI; npop = 2; break;
+            case 0x5b: kind = K_JUMPDEST; break;
+            case 0x5c: kind = K_BEGINSUB; break;
+            case 0xf3: kind = K_RETURN; npop = 2; break;
+            case 0xfd: kind = K_REVERT; npop = 2; break;
+            default: kind = K_ESCAPE; break;
+        }
+        d[b].x = t[b].gmin | (t[b].gmax << 16);
+        d[b].y = t[b].req | (npop << 4) | (push << 8) | (kind << 9);
+    }
+}
+
 extern "C" int mg_abi_version(void) { return (int)MG_ABI_VERSION; }
 
 extern "C" int mg_opcode_info(uint32_t byte, uint32_t *gmin, uint32_t *gmax, uint32_t *req) {
@@ -134,12 +180,9 @@ extern "C" int mg_open(int device, mg_ctx **out) {
         if (hipSetDevice(device) != hipSuccess) { rc = MG_EDEVICE; break; }
         if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { rc = MG_EDEVICE; break; }
         if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) { rc = MG_EDEVICE; break; }
-        OpInfo t[256];
-        build_optable(t);
-        uint64_t esc[4];
-        build_escape(esc);
-        if (hipMemcpyToSymbol(HIP_SYMBOL(kOp), t, sizeof t) != hipSuccess) { rc = MG_EDEVICE; break; }
-        if (hipMemcpyToSymbol(HIP_SYMBOL(kEscape), esc, sizeof esc) != hipSuccess) { rc = MG_EDEVICE; break; }
+        uint2 dec[256];
+        build_decode(dec);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(kDec), dec, sizeof dec) != hipSuccess) { rc = MG_EDEVICE; break; }
         if (hipMalloc(&ctx->d_ctr, sizeof(DevCounters)) != hipSuccess) { rc = MG_ENOMEM; break; }
     } while (0);
     if (rc != MG_OK) { mg_close(ctx); return rc; }
