@@ -65,6 +65,11 @@ def main():
     cid = dev.load_code(code)
     batch = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + rank,
                                stack_cap=1024, mem_cap=1024)
+    # lanes bucketed by (code, selector, calldata length) so a wavefront walks
+    # one function's path (mythril_amd/lanes.py:bucket_order); parity of every
+    # lane is independent of its position in the batch
+    from mythril_amd.lanes import bucket_order, permuted
+    batch = permuted(batch, bucket_order(batch))
     dev.alloc(batch.shape, coverage=True)
     dev.upload(workloads.slim_copy(batch))
 

@@ -68,12 +68,36 @@ DEV void st_word(uint4 *base, size_t idx, const U256 &v) {
     base[2 * idx] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
     base[2 * idx + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
 }
+// LDS stack window: slots [0, win) of a lane live in LDS as [slot][half][thread]
+// 16-byte pieces (conflict-free ds_read_b128), deeper slots in HBM.
+#define LANE_BLOCK 256u
 struct LaneView {
     const DevLanes &L;
     uint32_t lane;
+    uint4 *win_base;     // LDS window of this block (nullptr: no window)
+    uint32_t win, tid;
     DEV size_t row(uint32_t r) const { return (size_t)r * L.N + lane; }
-    DEV U256 stack(uint32_t slot) const { return ld_word(L.stack, row(slot)); }
-    DEV void set_stack(uint32_t slot, const U256 &v) const { st_word(L.stack, row(slot), v); }
+    DEV U256 gstack(uint32_t slot) const { return ld_word(L.stack, row(slot)); }
+    DEV void set_gstack(uint32_t slot, const U256 &v) const { st_word(L.stack, row(slot), v); }
+    DEV U256 stack(uint32_t slot) const {
+        if (slot < win) {
+            const uint4 x = win_base[(slot * 2u) * LANE_BLOCK + tid];
+            const uint4 y = win_base[(slot * 2u + 1u) * LANE_BLOCK + tid];
+            U256 r;
+            r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+            r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+            return r;
+        }
+        return gstack(slot);
+    }
+    DEV void set_stack(uint32_t slot, const U256 &v) const {
+        if (slot < win) {
+            win_base[(slot * 2u) * LANE_BLOCK + tid] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+            win_base[(slot * 2u + 1u) * LANE_BLOCK + tid] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+        } else {
+            set_gstack(slot, v);
+        }
+    }
     DEV U256 env(int w) const { return ld_word(L.env, row((uint32_t)w)); }
     DEV uint32_t mdw(uint32_t dw) const { return L.mem[row(dw)]; }
     DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? L.mem[row(dw)] : 0u; }
@@ -275,21 +299,23 @@ DEV U256 alu(uint32_t op, const U256 &a, const U256 &b, const U256 &c) {
 //   * the two top stack words live in registers (T0 = S[sp-1], T1 = S[sp-2]);
 //     HBM/L2 holds S[0 .. sp-2) and is read only for deeper operands;
 //   * coverage bits are collected in LDS and flushed once per launch.
-#define OPS_LDS 4096u     // instructions pre-decoded per block
-#define PUSH_LDS 1024u    // push immediates staged per block (32 B each)
-
-__global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
-                                                   const uint8_t *__restrict__ a8,
-                                                   const uint32_t *__restrict__ a32,
-                                                   uint8_t *__restrict__ cov, uint32_t cov_on,
-                                                   uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3,
-                                                   uint32_t max_steps, uint32_t max_depth,
-                                                   DevCounters *__restrict__ ctr,
-                                                   unsigned long long *__restrict__ prof) {
+__global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
+                                                          const uint8_t *__restrict__ a8,
+                                                          const uint32_t *__restrict__ a32,
+                                                          uint8_t *__restrict__ cov, uint32_t cov_on,
+                                                          uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3,
+                                                          uint32_t max_steps, uint32_t max_depth,
+                                                          DevCounters *__restrict__ ctr,
+                                                          unsigned long long *__restrict__ prof,
+                                                          uint32_t win, uint32_t pd_cap) {
+    // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
+    //              [push immediates: pd_cap x 32 B][coverage bytes: pd_cap]
+    extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
+    uint4 *s_win = dyn;
+    uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * LANE_BLOCK);
+    uint4 *s_push = reinterpret_cast<uint4 *>(s_pd + pd_cap);
+    uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_push + 2u * pd_cap);
     __shared__ uint2 s_dec[256];
-    __shared__ uint2 s_pd[OPS_LDS];          // x = gas min | max << 16, y = op | dec.y << 8
-    __shared__ uint4 s_push[PUSH_LDS * 2];
-    __shared__ uint8_t s_cov[OPS_LDS];
     __shared__ uint32_t s_code;
     // optional instruction profile (InstructionProfiler's per-opcode counts,
     // instruction_profiler.py:41-115, as native counters): 256 opcode counts +
@@ -309,29 +335,30 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
     __syncthreads();
     const uint32_t bcode = s_code;
     const bool mixed = __syncthreads_or(status == ST_RUNNING && my_code != bcode);
-    bool staged = false, push_staged = false;
+    bool staged = false;
     if (bcode != 0xffffffffu && !mixed) {
         const DevCode BC = codes[bcode];
-        if (BC.n_instr <= OPS_LDS) {
+        if (BC.n_instr <= pd_cap) {
+            // pre-decode: opcode, gas, stack counts, kind, and the hook bit (bit 31)
             for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x) {
                 const uint32_t op = a8[BC.op_off + i];
                 const uint2 d = kDec[op];
-                s_pd[i] = make_uint2(d.x, op | (d.y << 8));
+                const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
+                const uint32_t hook = (uint32_t)((hm >> (op & 63u)) & 1ull);
+                s_pd[i] = make_uint2(d.x, op | (d.y << 8) | (hook << 31));
                 s_cov[i] = 0;
             }
-            if (BC.n_instr <= PUSH_LDS) {
-                const uint4 *gp = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
-                for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gp[i];
-                push_staged = true;
-            }
+            const uint4 *gp = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
+            for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gp[i];
             staged = true;
         }
         __syncthreads();
     }
+    const bool push_staged = staged;
     uint32_t executed = 0;
 
     if (status == ST_RUNNING) {
-        const LaneView V{L, lane};
+        const LaneView V{L, lane, win ? s_win : nullptr, win, threadIdx.x};
         const DevCode C = codes[my_code];
         const uint8_t *__restrict__ gops = a8 + C.op_off;
         const uint4 *__restrict__ gpush = reinterpret_cast<const uint4 *>(a32 + C.push_off);
@@ -340,6 +367,7 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
         uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
         uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
         uint32_t aux = 0, n_sha3 = 0, n_exp = 0;
+        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_stack(k, V.gstack(k));   // window fill
         U256 T0 = sp >= 1u ? V.stack(sp - 1u) : u_zero();
         U256 T1 = sp >= 2u ? V.stack(sp - 2u) : u_zero();
 
@@ -351,13 +379,13 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
             else {
                 const uint32_t o = gops[pc];
                 const uint2 d = s_dec[o];
-                pd = make_uint2(d.x, o | (d.y << 8));
+                const uint64_t hm = o < 64u ? m0 : o < 128u ? m1 : o < 192u ? m2 : m3;
+                pd = make_uint2(d.x, o | (d.y << 8) | ((uint32_t)((hm >> (o & 63u)) & 1ull) << 31));
             }
             const uint32_t op = pd.y & 0xffu;
-            const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
-            if ((hm >> (op & 63u)) & 1ull) { status = ST_HOOK; aux = op; break; }
+            if (pd.y >> 31) { status = ST_HOOK; aux = op; break; }
             if (executed >= max_steps) break;
-            const uint32_t kind = pd.y >> 17;
+            const uint32_t kind = (pd.y >> 17) & 31u;
             if (kind == K_ESCAPE || ((flags & LANE_CREATION) && op >= 0x35u && op <= 0x39u)) {
                 status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
             }
@@ -638,9 +666,10 @@ __global__ __launch_bounds__(256) void k_lane_step(DevLanes L, const DevCode *__
             pc = npc; sp = nsp; msize = nmsize; depth = ndepth; gmin = ngmin; gmax = ngmax;
             T0 = nT0; T1 = nT1;
         }
-        // flush the register window: memory holds the canonical S[0 .. sp)
+        // flush the registers, then the LDS window: HBM holds the canonical S[0 .. sp)
         if (sp >= 1u) V.set_stack(sp - 1u, T0);
         if (sp >= 2u) V.set_stack(sp - 2u, T1);
+        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_gstack(k, V.stack(k));
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;

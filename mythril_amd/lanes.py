@@ -236,3 +236,24 @@ def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = No
             if (a.ret_offset[i], a.ret_len[i]) != (b.ret_offset[i], b.ret_len[i]):
                 out.append(f"lane {i}: return range differs")
     return out
+
+
+_ALL_FIELDS = _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage")
+
+
+def bucket_order(batch: LaneBatch) -> np.ndarray:
+    """Lane order that groups paths likely to run in lockstep: same code, same
+    4-byte selector, same calldata length (SURVEY §7 'Divergence': bucket lanes
+    by code and entry block).  Lanes are independent, so any order is correct;
+    this one keeps a wave's 64 lanes on one instruction stream for longest."""
+    sel = np.zeros(batch.n, dtype=np.uint64)
+    for k in range(min(4, batch.shape.calldata_cap)):
+        sel = (sel << np.uint64(8)) | batch.calldata[:, k].astype(np.uint64)
+    return np.lexsort((batch.calldata_len, sel, batch.code_id))
+
+
+def permuted(batch: LaneBatch, order: np.ndarray) -> LaneBatch:
+    out = LaneBatch(batch.shape)
+    for f in _ALL_FIELDS:
+        getattr(out, f)[...] = getattr(batch, f)[order]
+    return out

@@ -165,3 +165,65 @@ def test_reset_replays_identically(dev, c2):
     n = dev.n_instr(cid)
     pcs = first.pc[first.pc < n]
     assert cov[pcs].all()
+
+
+def test_c2_bucketed_order_is_a_permutation(dev, c2):
+    """The bench uploads lanes in bucket_order; every lane's result is independent
+    of its position, so the permuted device run equals the permuted oracle run."""
+    from mythril_amd.lanes import bucket_order, permuted
+    b = workloads.c2_batch(16384, seed=5, stack_cap=64, mem_cap=1024)
+    order = bucket_order(b)
+    pb = permuted(b, order)
+    out, ref, _ = run_both(dev, [c2], pb)
+    assert not diff_batches(out, ref)
+    _, ref0, _ = run_both(dev, [c2], b)
+    assert not diff_batches(out, permuted(ref0, order))
+
+
+def _stack_program(rng, depth_target):
+    """Random straight-line program that grows the stack past the LDS window and
+    shuffles it with DUPn/SWAPn/arithmetic, then stores the top 8 words."""
+    code = bytearray()
+    depth = 0
+    for _ in range(rng.randrange(200, 600)):
+        r = rng.random()
+        if depth < 2 or (r < 0.35 and depth < depth_target):
+            n = rng.randrange(1, 33)
+            code += bytes([0x5F + n]) + rng.getrandbits(8 * n).to_bytes(n, "big")
+            depth += 1
+        elif r < 0.55 and 1 <= depth < depth_target:
+            k = rng.randrange(1, min(16, depth) + 1)
+            code.append(0x7F + k)          # DUPk
+            depth += 1
+        elif r < 0.75 and depth >= 2:
+            k = rng.randrange(1, min(16, depth - 1) + 1)
+            code.append(0x8F + k)          # SWAPk
+        elif r < 0.9:
+            code.append(rng.choice([0x01, 0x02, 0x03, 0x16, 0x17, 0x18, 0x1B, 0x1C]))
+            depth -= 1
+        else:
+            code.append(0x50)              # POP
+            depth -= 1
+        if depth > 1000:
+            break
+    for s in range(min(8, depth)):
+        code += bytes([0x60, s, 0x55])     # PUSH1 s; SSTORE (value = top)
+    return bytes(code)
+
+
+def test_deep_stack_window_edges(dev):
+    """Stacks that cross the LDS window (slots >= 16 live in HBM) in both directions,
+    several codes per block (unstaged decode path) and one code per block."""
+    rng = random.Random(0x57AC)
+    codes = [_stack_program(rng, t) for t in (8, 15, 16, 17, 18, 24, 40, 100, 400, 1000)
+             for _ in range(4)]
+    n = 4096
+    b = LaneBatch(LaneShape(n=n, stack_cap=1024, mem_cap=64, calldata_cap=32, storage_cap=16))
+    for i in range(n):
+        # blocks of 256 lanes: first half of the batch mixes codes, second half stages one
+        cid = (i % len(codes)) if i < n // 2 else ((i // 256) % len(codes))
+        b.set_lane(i, code_id=cid, gas_limit=10 ** 8)
+    out, ref, _ = run_both(dev, codes, b)
+    assert not diff_batches(out, ref)
+    assert (out.sp > 16).any()
+    assert (out.steps > 100).mean() > 0.5
