@@ -57,16 +57,33 @@ struct OpInfo {
 #define HUGE_GAS (1ull << 62)
 
 // ---- lane-interleaved accessors ---------------------------------------------
-DEV U256 ld_word(const uint4 *base, size_t idx) {
-    const uint4 x = base[2 * idx], y = base[2 * idx + 1];
+// Explicit address spaces: DevLanes is a by-value struct argument, so without
+// them every access through its pointers would be a flat (generic) access.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u g_u4;
+typedef __attribute__((address_space(3))) v4u l_u4;
+template <class T> DEV __attribute__((address_space(1))) T *gp(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
+DEV g_u4 *gv(const void *p) { return (g_u4 *)const_cast<void *>(p); }
+
+DEV U256 ld_word(const g_u4 *base, size_t idx) {
+    const v4u x = base[2 * idx], y = base[2 * idx + 1];
     U256 r;
     r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
     r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
     return r;
 }
-DEV void st_word(uint4 *base, size_t idx, const U256 &v) {
-    base[2 * idx] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-    base[2 * idx + 1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+DEV U256 ld_word(const l_u4 *base, size_t idx) {
+    const v4u x = base[2 * idx], y = base[2 * idx + 1];
+    U256 r;
+    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    return r;
+}
+DEV void st_word(g_u4 *base, size_t idx, const U256 &v) {
+    base[2 * idx] = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
+    base[2 * idx + 1] = v4u{v.w[4], v.w[5], v.w[6], v.w[7]};
 }
 // LDS stack window: slots [0, win) of a lane live in LDS as [slot][half][thread]
 // 16-byte pieces (conflict-free ds_read_b128), deeper slots in HBM.
@@ -74,34 +91,37 @@ DEV void st_word(uint4 *base, size_t idx, const U256 &v) {
 struct LaneView {
     const DevLanes &L;
     uint32_t lane;
-    uint4 *win_base;     // LDS window of this block (nullptr: no window)
+    l_u4 *win_base;      // LDS window of this block
     uint32_t win, tid;
     DEV size_t row(uint32_t r) const { return (size_t)r * L.N + lane; }
-    DEV U256 gstack(uint32_t slot) const { return ld_word(L.stack, row(slot)); }
-    DEV void set_gstack(uint32_t slot, const U256 &v) const { st_word(L.stack, row(slot), v); }
+    DEV U256 gstack(uint32_t slot) const { return ld_word(gv(L.stack), row(slot)); }
+    DEV void set_gstack(uint32_t slot, const U256 &v) const { st_word(gv(L.stack), row(slot), v); }
+    DEV U256 wstack(uint32_t slot) const {
+        const v4u x = win_base[(slot * 2u) * LANE_BLOCK + tid];
+        const v4u y = win_base[(slot * 2u + 1u) * LANE_BLOCK + tid];
+        U256 r;
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        return r;
+    }
+    DEV void set_wstack(uint32_t slot, const U256 &v) const {
+        win_base[(slot * 2u) * LANE_BLOCK + tid] = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
+        win_base[(slot * 2u + 1u) * LANE_BLOCK + tid] = v4u{v.w[4], v.w[5], v.w[6], v.w[7]};
+    }
     DEV U256 stack(uint32_t slot) const {
-        if (slot < win) {
-            const uint4 x = win_base[(slot * 2u) * LANE_BLOCK + tid];
-            const uint4 y = win_base[(slot * 2u + 1u) * LANE_BLOCK + tid];
-            U256 r;
-            r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-            r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-            return r;
-        }
-        return gstack(slot);
+        U256 r;
+        if (slot < win) r = wstack(slot);
+        else r = gstack(slot);
+        return r;
     }
     DEV void set_stack(uint32_t slot, const U256 &v) const {
-        if (slot < win) {
-            win_base[(slot * 2u) * LANE_BLOCK + tid] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-            win_base[(slot * 2u + 1u) * LANE_BLOCK + tid] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
-        } else {
-            set_gstack(slot, v);
-        }
+        if (slot < win) set_wstack(slot, v);
+        else set_gstack(slot, v);
     }
-    DEV U256 env(int w) const { return ld_word(L.env, row((uint32_t)w)); }
-    DEV uint32_t mdw(uint32_t dw) const { return L.mem[row(dw)]; }
-    DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? L.mem[row(dw)] : 0u; }
-    DEV void set_mdw(uint32_t dw, uint32_t v) const { L.mem[row(dw)] = v; }
+    DEV U256 env(int w) const { return ld_word(gv(L.env), row((uint32_t)w)); }
+    DEV uint32_t mdw(uint32_t dw) const { return gp(L.mem)[row(dw)]; }
+    DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? gp(L.mem)[row(dw)] : 0u; }
+    DEV void set_mdw(uint32_t dw, uint32_t v) const { gp(L.mem)[row(dw)] = v; }
     DEV uint32_t mbyte(uint32_t off) const { return (mdw(off >> 2) >> (24u - 8u * (off & 3u))) & 0xffu; }
     DEV void set_mbyte(uint32_t off, uint32_t b) const {
         const uint32_t sh = 24u - 8u * (off & 3u);
@@ -141,9 +161,8 @@ struct LaneView {
     DEV void mzero(uint32_t from, uint32_t to) const {   // [from, to), multiples of 32
         for (uint32_t dw = from >> 2; dw < (to >> 2); ++dw) set_mdw(dw, 0u);
     }
-    DEV uint32_t cbyte(uint32_t idx) const {
-        return (L.calldata[row(idx >> 2)] >> (24u - 8u * (idx & 3u))) & 0xffu;
-    }
+    DEV uint32_t cdw(uint32_t dw) const { return gp(L.calldata)[row(dw)]; }
+    DEV uint32_t cbyte(uint32_t idx) const { return (cdw(idx >> 2) >> (24u - 8u * (idx & 3u))) & 0xffu; }
 };
 
 // ---- memory extension (machine_state.py:132-191) -----------------------------
@@ -240,7 +259,8 @@ DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
 enum OpKind : uint32_t {
     K_ALU = 0, K_PUSH, K_DUP, K_SWAP, K_LOG, K_POP, K_ENV, K_STOP, K_SHA3, K_CDLOAD, K_CDCOPY,
     K_CODECOPY, K_RDCOPY, K_MLOAD, K_MSTORE, K_MSTORE8, K_SLOAD, K_SSTORE, K_JUMP, K_JUMPI,
-    K_JUMPDEST, K_BEGINSUB, K_RETURN, K_REVERT, K_INVALID, K_ESCAPE
+    K_JUMPDEST, K_BEGINSUB, K_RETURN, K_REVERT, K_INVALID, K_ESCAPE,
+    K_END   // sentinel after the last instruction (past-the-end pc, svm.py:384-389)
 };
 __constant__ uint2 kDec[256];
 
@@ -291,14 +311,330 @@ DEV U256 alu(uint32_t op, const U256 &a, const U256 &b, const U256 &c) {
     }
 }
 
+// ---- general handlers (one instruction, every opcode kind) ---------------------
+// Registers of one lane that an instruction may change.
+struct LaneRegs {
+    U256 T0, T1;                 // S[sp-1], S[sp-2]
+    uint64_t gmin, gmax;
+    uint32_t pc, sp, msize, depth;
+    uint32_t n_sha3, n_exp;
+    uint32_t stop, sx;           // out: ST_RUNNING or the stop status and its aux word
+};
+// What the handlers read besides the registers (per lane / per block).
+struct StepEnv {
+    const DevLanes *L;
+    DevCode C;
+    const uint8_t *a8;
+    const uint32_t *a32;
+    l_u4 *s_win;
+    const uint2 *s_pd;
+    const uint4 *s_push;
+    uint32_t *s_prof;
+    uint64_t txlim, glim;
+    uint32_t lane, tid, win, flags, sflag, psflag, prof;
+};
+
+// Executes the instruction decoded as (uk, ux) for one lane, exactly as the
+// reference would (three phases: checks, accumulate_gas, writes).  The fast
+// loop of k_lane_step handles the common opcodes itself and calls this for
+// everything else and for any lane whose fast-path preconditions fail, so
+// every exception, escape and corner case has a single implementation.
+__device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t uk, uint32_t ux) {
+    const DevLanes &L = *E.L;
+    const DevCode &C = E.C;
+    const uint32_t lane = E.lane;
+    const LaneView V{L, lane, E.s_win, E.win, E.tid};
+    const uint8_t *__restrict__ a8 = E.a8;
+    const uint32_t *__restrict__ a32 = E.a32;
+    const uint8_t *__restrict__ gops = a8 + C.op_off;
+    const uint64_t txlim = E.txlim, glim = E.glim;
+    const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
+    const uint32_t req = (uk >> 8) & 15u, npop = (uk >> 12) & 15u;
+    const bool push = ((uk >> 16) & 1u) != 0u;
+    const uint32_t gtab_min = ux & 0xffffu, gtab_max = ux >> 16;
+    const uint32_t sp = R.sp, pc = R.pc, msize0 = R.msize;
+    uint32_t nmsize = R.msize, ndepth = R.depth, npc = pc + 1u;
+    uint64_t ngmin = R.gmin, ngmax = R.gmax;
+    uint32_t stop = ST_RUNNING, sx = 0;
+    bool by_table = true;
+    const U256 a = R.T0, b = R.T1;
+    U256 c = u_zero(), res = u_zero();
+    const uint32_t nsp = sp - npop;
+    uint32_t *s_prof = E.s_prof;
+    const bool prof = E.prof != 0u;
+
+#define STOPX(s_, x_) { stop = (s_); sx = (x_); break; }
+#define EXCX(k_) STOPX(ST_VMEXC, (k_))
+#define ESCX(r_) STOPX(ST_ESCAPE, op | ((r_) << 8))
+#define GASCOMMIT() if (by_table) { ngmin += gtab_min; ngmax += gtab_max; by_table = false; \
+                                    if (ngmin >= glim) EXCX(EXC_OOG) }
+#define MEMX(st_, sz_, later_) { const int mx_ = mem_extend((st_), (sz_), nmsize, ngmin, ngmax, \
+                                                        L.mem_cap, (later_), txlim); \
+                                 if (mx_ == MX_OOG) EXCX(EXC_OOG) if (mx_ == MX_ESCAPE) ESCX(ESC_MEMORY) }
+#define ZEROFILL() if (nmsize > msize0) V.mzero(msize0, nmsize);
+#define JUMP_OK(idx_) ((idx_) != MG_JRES_NONE && \
+                       (E.sflag ? (E.s_pd[(idx_)].y & 0xffu) : (uint32_t)gops[(idx_)]) == 0x5bu)
+
+    do {
+        // svm.py:391-402 precheck; instructions.py:188-193 write protection;
+        // then what the mutator really pops (ADDMOD, SSTORE pop more than `req`)
+        if (sp < req) EXCX(EXC_UNDERFLOW)
+        if ((op == 0x55u || (op >= 0xa0u && op <= 0xa4u)) && (E.flags & LANE_STATIC)) EXCX(EXC_WRITEPROT)
+        if (sp < npop) EXCX(EXC_UNDERFLOW)
+        if (npop >= 3u) c = V.stack(sp - 3u);
+        bool tos_done = false;
+        switch (kind) {
+        case K_ALU:
+            if (op == 0x0a) ++R.n_exp;
+            res = alu(op, a, b, c);
+            break;
+        case K_PUSH:                                        // (:278-320)
+            res = E.psflag ? ld_word((const l_u4 *)E.s_push, pc)
+                           : ld_word(gv(a32 + C.push_off), pc);
+            break;
+        case K_DUP: {                                       // (:322-331)
+            const uint32_t k = op - 0x7fu;
+            if (sp < k) EXCX(EXC_UNDERFLOW)
+            res = k == 1u ? a : k == 2u ? b : V.stack(sp - k);
+            break;
+        }
+        case K_SWAP: {                                      // (:333-343)
+            const uint32_t k = op - 0x8fu;
+            if (sp < k + 1u) EXCX(EXC_UNDERFLOW)
+            if (k == 1u) {
+                GASCOMMIT()
+                R.T0 = b; R.T1 = a;
+            } else {
+                const U256 x = V.stack(sp - 1u - k);
+                GASCOMMIT()
+                V.set_stack(sp - 1u - k, a);
+                R.T0 = x;
+            }
+            tos_done = true;
+            break;
+        }
+        case K_LOG: case K_POP: case K_RDCOPY: case K_JUMPDEST:
+            break;                                          // pops only / no-op
+        case K_ENV:
+            switch (op) {
+            case 0x30: res = V.env(0); break;               // ADDRESS
+            case 0x32: res = V.env(2); break;               // ORIGIN
+            case 0x33: res = V.env(1); break;               // CALLER
+            case 0x34: res = V.env(3); break;               // CALLVALUE
+            case 0x3a: res = V.env(4); break;               // GASPRICE
+            case 0x36: res = u_small(L.calldata_len[lane]); break;
+            case 0x38: res = u_small(C.n_bytes); break;     // CODESIZE
+            case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
+            case 0x58: res = u_small(a32[C.addr_off + pc]); break;
+            case 0x59: res = u_small(msize0); break;
+            default: res = u_zero(); break;                 // RETURNDATASIZE
+            }
+            break;
+        case K_STOP: STOPX(ST_STOP, 0u)
+        case K_SHA3: {  // own gas first, then mem_extend (instructions.py:1013-1051)
+            by_table = false;
+            const bool big = (b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u;
+            const uint64_t blen = (uint64_t)b.w[0] | ((uint64_t)b.w[1] << 32);
+            const uint64_t g = (big || blen > BIG_END) ? HUGE_GAS : 30ull + 6ull * ((blen + 31ull) >> 5);
+            ngmin += g; ngmax += g;
+            if (ngmin >= glim) EXCX(EXC_OOG)
+            MEMX(a, b, -1)
+            ZEROFILL()
+            if (b.w[0] == 0u) {  // get_empty_keccak_hash (keccak_function_manager.py:87-93)
+                res.w[7] = 0xc5d24601u; res.w[6] = 0x86f7233cu; res.w[5] = 0x927e7db2u; res.w[4] = 0xdcc703c0u;
+                res.w[3] = 0xe500b653u; res.w[2] = 0xca82273bu; res.w[1] = 0x7bfad804u; res.w[0] = 0x5d85a470u;
+            } else {
+                res = keccak_mem(V, a.w[0], b.w[0]);
+                if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
+            }
+            ++R.n_sha3;
+            break;
+        }
+        case K_CDLOAD: {  // byte (off+k) mod 2^256, 0 past the end (calldata.py:46-90,137-146)
+            const uint32_t cdl = L.calldata_len[lane];
+            const bool fits = u_fits32(a);
+            if (fits && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl) {
+                const uint32_t d0 = a.w[0] >> 2;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) res.w[7 - k] = V.cdw(d0 + k);
+            } else {
+                bool wrapc = true;
+#pragma unroll
+                for (int k = 1; k < 8; ++k) wrapc = wrapc && a.w[k] == 0xffffffffu;
+                for (uint32_t k = 0; k < 32u; ++k) {
+                    const uint64_t t = (uint64_t)a.w[0] + k;
+                    bool ok = false;
+                    uint32_t idx = 0;
+                    if (fits) { ok = t < cdl; idx = (uint32_t)t; }
+                    else if (wrapc && t >= (1ull << 32)) { idx = (uint32_t)(t - (1ull << 32)); ok = idx < cdl; }
+                    if (ok) {
+                        const uint32_t byte = V.cbyte(idx), sh = 8u * (31u - k);
+                        res = u_or(res, u_shl_n(u_small(byte), sh));
+                    }
+                }
+            }
+            break;
+        }
+        case K_CDCOPY: {  // nothing at all for size 0 (:806-891)
+            if (u_iszero(c)) break;
+            MEMX(a, c, (int64_t)gtab_min)
+            GASCOMMIT()
+            ZEROFILL()
+            const uint32_t cdl = L.calldata_len[lane];
+            const bool bfits = u_fits32(b);
+            bool wrapc = true;
+#pragma unroll
+            for (int k = 1; k < 8; ++k) wrapc = wrapc && b.w[k] == 0xffffffffu;
+            if (prof) atomicAdd(&s_prof[257], c.w[0]);
+            for (uint32_t k = 0; k < c.w[0]; ++k) {
+                const uint64_t t = (uint64_t)b.w[0] + k;
+                uint32_t v = 0u;
+                if (bfits) { if (t < cdl) v = V.cbyte((uint32_t)t); }
+                else if (wrapc && t >= (1ull << 32) && t - (1ull << 32) < cdl) v = V.cbyte((uint32_t)(t - (1ull << 32)));
+                V.set_mbyte(a.w[0] + k, v);
+            }
+            break;
+        }
+        case K_CODECOPY: {  // extends even for size 0; copy stops at the end of code
+            MEMX(a, c, (int64_t)gtab_min)
+            GASCOMMIT()
+            ZEROFILL()
+            uint32_t ncopy = 0u;
+            if (u_fits32(b) && b.w[0] < C.n_bytes) ncopy = min(C.n_bytes - b.w[0], c.w[0]);
+            if (prof) atomicAdd(&s_prof[257], ncopy);
+            for (uint32_t k = 0; k < ncopy; ++k) V.set_mbyte(a.w[0] + k, a8[C.bytes_off + b.w[0] + k]);
+            break;
+        }
+        case K_MLOAD:
+            MEMX(a, u_small(32), (int64_t)gtab_min)
+            GASCOMMIT()
+            ZEROFILL()
+            res = V.mword(a.w[0]);
+            break;
+        case K_MSTORE:
+            MEMX(a, u_small(32), (int64_t)gtab_min)
+            GASCOMMIT()
+            ZEROFILL()
+            V.set_mword(a.w[0], b);
+            break;
+        case K_MSTORE8:
+            MEMX(a, u_small(1), (int64_t)gtab_min)
+            GASCOMMIT()
+            ZEROFILL()
+            V.set_mbyte(a.w[0], b.w[0] & 0xffu);
+            break;
+        case K_SLOAD: {  // over K(0) + stores (account.py:43-74)
+            const uint32_t cnt = L.storage_count[lane];
+            if (prof) atomicAdd(&s_prof[258], cnt);
+            for (uint32_t s = 0; s < cnt; ++s) {
+                const size_t base = V.row(s) * 2;
+                if (u_eq(ld_word(gv(L.storage), base), a)) { res = ld_word(gv(L.storage), base + 1); break; }
+            }
+            break;
+        }
+        case K_SSTORE: {
+            const uint32_t cnt = L.storage_count[lane];
+            if (prof) atomicAdd(&s_prof[258], cnt);
+            uint32_t slot = cnt;
+            for (uint32_t s = 0; s < cnt; ++s)
+                if (u_eq(ld_word(gv(L.storage), V.row(s) * 2), a)) { slot = s; break; }
+            if (slot == cnt && cnt >= L.storage_cap) ESCX(ESC_STORAGE)
+            GASCOMMIT()
+            if (slot == cnt) {
+                st_word(gv(L.storage), V.row(slot) * 2, a);
+                L.storage_count[lane] = cnt + 1u;
+            }
+            st_word(gv(L.storage), V.row(slot) * 2 + 1, b);
+            break;
+        }
+        case K_JUMP: {  // gas 8 by hand, no OOG check (:1520-1556)
+            by_table = false;
+            uint32_t idx = MG_JRES_NONE;
+            if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
+            if (!JUMP_OK(idx)) EXCX(EXC_BADJUMP)
+            ngmin += 8u; ngmax += 8u; npc = idx;
+            break;
+        }
+        case K_JUMPI: {  // gas 10 by hand, depth + 1 on the side taken (:1558-1636)
+            by_table = false;
+            if (u_iszero(b)) {
+                ngmin += 10u; ngmax += 10u; ++ndepth;
+            } else {
+                uint32_t idx = MG_JRES_NONE;
+                if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
+                if (!JUMP_OK(idx)) STOPX(ST_DROPPED, 0u)
+                ngmin += 10u; ngmax += 10u; ++ndepth; npc = idx;
+            }
+            break;
+        }
+        case K_BEGINSUB: EXCX(EXC_OOG)
+        case K_RETURN:  // (:1857-1874)
+            MEMX(a, b, 0)
+            if (ngmin >= glim) EXCX(EXC_OOG)
+            L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
+            STOPX(ST_RETURN, 0u)
+        case K_REVERT:  // no memory extension (:1899-1934)
+            L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
+            STOPX(ST_REVERT, 0u)
+        case K_INVALID: EXCX(EXC_INVALID)
+        default: ESCX(ESC_OPCODE)
+        }
+        if (stop != ST_RUNNING) break;
+        if (tos_done) { GASCOMMIT() break; }
+        // new top-of-stack registers from the pops / push of this opcode
+        if (push) {   // MachineStack.append: overflow check precedes the write
+            if (nsp + 1u > STACK_LIMIT) EXCX(EXC_OVERFLOW)
+            if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK)
+            GASCOMMIT()
+            if (npop == 0u) {            // T1 moves below the register window
+                if (sp >= 2u) V.set_stack(sp - 2u, b);
+                R.T1 = a;
+            } else if (npop >= 2u) {
+                R.T1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+            }
+            R.T0 = res;
+        } else {
+            GASCOMMIT()
+            if (npop == 1u) {
+                R.T0 = b;
+                R.T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+            } else if (npop >= 2u) {
+                R.T0 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+                R.T1 = sp >= npop + 2u ? V.stack(sp - npop - 2u) : u_zero();
+            }
+        }
+    } while (0);
+#undef STOPX
+#undef EXCX
+#undef ESCX
+#undef GASCOMMIT
+#undef MEMX
+#undef ZEROFILL
+#undef JUMP_OK
+    R.stop = stop;
+    R.sx = sx;
+    if (stop == ST_RUNNING) {
+        R.pc = npc; R.sp = nsp + (push ? 1u : 0u);
+        R.msize = nmsize; R.depth = ndepth; R.gmin = ngmin; R.gmax = ngmax;
+    }
+}
+
+// The opcodes the fast loop executes itself (when their preconditions hold).
+DEV bool alu_is_fast(uint32_t op) { return op <= 0x03u || op == 0x0bu || (op >= 0x10u && op <= 0x1du); }
+
 // ---- the stepping kernel -------------------------------------------------------
-// Latency is the bound at this batch size (65,536 lanes = one wave per SIMD), so
-// the loop keeps every per-step dependency on chip:
+// At 65,536 lanes there is one wave per SIMD, so a wave's instruction stream is
+// the bound: the loop keeps every per-step dependency on chip and dispatches
+// on wave-uniform values.
 //   * the block's code is pre-decoded into LDS: one 8-byte LDS read per step
 //     yields opcode, gas, stack counts and handler kind;
-//   * the two top stack words live in registers (T0 = S[sp-1], T1 = S[sp-2]);
-//     HBM/L2 holds S[0 .. sp-2) and is read only for deeper operands;
-//   * coverage bits are collected in LDS and flushed once per launch.
+//   * each iteration executes one opcode for the group of live lanes whose next
+//     instruction decodes like the lowest live lane's, so opcode, gas and stack
+//     effects are scalars and dispatch is a scalar branch;
+//   * the two top stack words live in registers, the next 14 in an LDS window,
+//     the rest in HBM;
+//   * common opcodes run inline; the rest (and any lane whose preconditions
+//     fail) go through slow_step, outside the loop's register allocation.
 __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
                                                           const uint8_t *__restrict__ a8,
                                                           const uint32_t *__restrict__ a32,
@@ -307,14 +643,15 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           uint32_t max_steps, uint32_t max_depth,
                                                           DevCounters *__restrict__ ctr,
                                                           unsigned long long *__restrict__ prof,
-                                                          uint32_t win, uint32_t pd_cap) {
+                                                          uint32_t win, uint32_t pd_cap, uint32_t jr_cap) {
     // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
-    //              [push immediates: pd_cap x 32 B][coverage bytes: pd_cap]
+    //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-    uint4 *s_win = dyn;
+    l_u4 *s_win = (l_u4 *)dyn;
     uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * LANE_BLOCK);
     uint4 *s_push = reinterpret_cast<uint4 *>(s_pd + pd_cap);
-    uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_push + 2u * pd_cap);
+    uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + 2u * pd_cap);
+    uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_jr + jr_cap);
     __shared__ uint2 s_dec[256];
     __shared__ uint32_t s_code;
     // optional instruction profile (InstructionProfiler's per-opcode counts,
@@ -335,10 +672,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     __syncthreads();
     const uint32_t bcode = s_code;
     const bool mixed = __syncthreads_or(status == ST_RUNNING && my_code != bcode);
-    bool staged = false;
+    bool staged = false, jstaged = false;
     if (bcode != 0xffffffffu && !mixed) {
         const DevCode BC = codes[bcode];
-        if (BC.n_instr <= pd_cap) {
+        if (BC.n_instr < pd_cap) {
             // pre-decode: opcode, gas, stack counts, kind, and the hook bit (bit 31)
             for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x) {
                 const uint32_t op = a8[BC.op_off + i];
@@ -348,328 +685,243 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 s_pd[i] = make_uint2(d.x, op | (d.y << 8) | (hook << 31));
                 s_cov[i] = 0;
             }
-            const uint4 *gp = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
-            for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gp[i];
+            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint2(0u, (uint32_t)K_END << 17);
+            const uint4 *gpu4 = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
+            for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gpu4[i];
             staged = true;
+            if (BC.n_jres <= jr_cap && BC.n_instr < 0xffffu) {
+                for (uint32_t i = threadIdx.x; i < BC.n_jres; i += blockDim.x) {
+                    const uint32_t t = a32[BC.jres_off + i];
+                    s_jr[i] = t == MG_JRES_NONE ? (uint16_t)0xffffu : (uint16_t)t;
+                }
+                jstaged = true;
+            }
         }
         __syncthreads();
     }
-    const bool push_staged = staged;
     uint32_t executed = 0;
+    const bool run0 = status == ST_RUNNING;
+    // block-uniform facts in scalar registers
+    const uint32_t sflag = __builtin_amdgcn_readfirstlane(staged ? 1u : 0u);
+    const uint32_t jflag = __builtin_amdgcn_readfirstlane(jstaged ? 1u : 0u);
+    const uint32_t stack_lim = L.stack_cap < STACK_LIMIT ? L.stack_cap : STACK_LIMIT;
 
-    if (status == ST_RUNNING) {
-        const LaneView V{L, lane, win ? s_win : nullptr, win, threadIdx.x};
-        const DevCode C = codes[my_code];
-        const uint8_t *__restrict__ gops = a8 + C.op_off;
-        const uint4 *__restrict__ gpush = reinterpret_cast<const uint4 *>(a32 + C.push_off);
-        const uint32_t flags = L.flags[lane];
-        const uint64_t txlim = L.gas_limit[lane];
-        uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
-        uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
-        uint32_t aux = 0, n_sha3 = 0, n_exp = 0;
-        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_stack(k, V.gstack(k));   // window fill
-        U256 T0 = sp >= 1u ? V.stack(sp - 1u) : u_zero();
-        U256 T1 = sp >= 2u ? V.stack(sp - 2u) : u_zero();
+    // ---- per-lane machine state (registers) ----
+    const LaneView V{L, lane, s_win, win, threadIdx.x};
+    DevCode C{};
+    uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
+    uint64_t txlim = 0, glim = 0, gmin = 0, gmax = 0;
+    U256 T0 = u_zero(), T1 = u_zero();
+    uint2 pd = make_uint2(0u, 0u);
+    bool live = false;
+    if (run0) {
+        C = codes[my_code];
+        flags = L.flags[lane];
+        txlim = L.gas_limit[lane];
+        // accumulate_gas OOG test (instructions.py:162-176): min > 1e9 or min >= tx gas limit
+        glim = txlim < MSTATE_GAS_LIMIT + 1ull ? txlim : MSTATE_GAS_LIMIT + 1ull;
+        pc = L.pc[lane]; sp = L.sp[lane]; msize = L.msize[lane]; depth = L.depth[lane];
+        gmin = L.gas_min[lane]; gmax = L.gas_max[lane];
+        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_wstack(k, V.gstack(k));   // window fill
+        if (sp >= 1u) T0 = V.stack(sp - 1u);
+        if (sp >= 2u) T1 = V.stack(sp - 2u);
+        live = true;
+    }
+    const bool creation = (flags & LANE_CREATION) != 0u;
+    const uint8_t *__restrict__ gops = a8 + C.op_off;
+    const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, txlim, glim,
+                    lane, threadIdx.x, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
 
-        for (;;) {
-            if (max_depth != 0u && depth >= max_depth) { status = ST_DEPTH; break; }
-            if (pc >= C.n_instr) { status = ST_END; break; }
-            uint2 pd;
-            if (staged) pd = s_pd[pc];
-            else {
-                const uint32_t o = gops[pc];
-                const uint2 d = s_dec[o];
-                const uint64_t hm = o < 64u ? m0 : o < 128u ? m1 : o < 192u ? m2 : m3;
-                pd = make_uint2(d.x, o | (d.y << 8) | ((uint32_t)((hm >> (o & 63u)) & 1ull) << 31));
-            }
-            const uint32_t op = pd.y & 0xffu;
-            if (pd.y >> 31) { status = ST_HOOK; aux = op; break; }
-            if (executed >= max_steps) break;
-            const uint32_t kind = (pd.y >> 17) & 31u;
-            if (kind == K_ESCAPE || ((flags & LANE_CREATION) && op >= 0x35u && op <= 0x39u)) {
-                status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
-            }
-            if (cov_on) {
-                if (staged) s_cov[pc] = 1;
-                else cov[C.cov_off + pc] = 1;
-            }
-            if (prof) atomicAdd(&s_prof[op], 1u);
-            ++executed;
+    // Decode the instruction at pc and run the checks svm.execute_state makes
+    // before evaluating it (svm.py:369-402): depth cut-off, past-the-end pc,
+    // hooked opcode, this launch's step budget, host-only opcode.
+#define FETCH() do {                                                                      \
+        if (sflag) {                                                                      \
+            pd = s_pd[pc];                    /* s_pd[n_instr] is the END sentinel */     \
+        } else if (pc >= C.n_instr) {                                                     \
+            pd = make_uint2(0u, (uint32_t)K_END << 17);                                   \
+        } else {                                                                          \
+            const uint32_t o_ = gops[pc];                                                 \
+            const uint2 d_ = s_dec[o_];                                                   \
+            const uint64_t hm_ = o_ < 64u ? m0 : o_ < 128u ? m1 : o_ < 192u ? m2 : m3;    \
+            pd = make_uint2(d_.x, o_ | (d_.y << 8) | ((uint32_t)((hm_ >> (o_ & 63u)) & 1ull) << 31)); \
+        }                                                                                 \
+        const uint32_t k_ = (pd.y >> 17) & 31u, o_ = pd.y & 0xffu;                       \
+        if ((pd.y >> 31) || k_ >= K_ESCAPE || executed >= max_steps ||                    \
+            (max_depth != 0u && depth >= max_depth) || (creation && o_ - 0x35u < 5u)) {   \
+            uint32_t st_ = ST_RUNNING;                                                    \
+            if (max_depth != 0u && depth >= max_depth) st_ = ST_DEPTH;                    \
+            else if (k_ == K_END) st_ = ST_END;                                           \
+            else if (pd.y >> 31) { st_ = ST_HOOK; aux = o_; }                             \
+            else if (executed >= max_steps) live = false;                                 \
+            else { st_ = ST_ESCAPE; aux = o_ | (ESC_OPCODE << 8); }                       \
+            if (st_ != ST_RUNNING) { status = st_; live = false; }                        \
+        }                                                                                 \
+    } while (0)
 
-            const uint32_t req = (pd.y >> 8) & 15u, npop = (pd.y >> 12) & 15u;
-            const bool push = ((pd.y >> 16) & 1u) != 0u;
-            const uint32_t gtab_min = pd.x & 0xffffu, gtab_max = pd.x >> 16;
-            const uint32_t msize0 = msize;
-            uint32_t nmsize = msize, ndepth = depth, npc = pc + 1u;
-            uint64_t ngmin = gmin, ngmax = gmax;
-            uint32_t stop = ST_RUNNING, sx = 0;
-            bool by_table = true, tos_done = false;
-            U256 a = T0, b = T1, c = u_zero(), res = u_zero();
-            U256 nT0 = T0, nT1 = T1;
-            uint32_t nsp = sp;
+    if (live) FETCH();
 
-#define STOPX(s_, x_) { stop = (s_); sx = (x_); break; }
-#define EXCX(k_) STOPX(ST_VMEXC, (k_))
-#define ESCX(r_) STOPX(ST_ESCAPE, op | ((r_) << 8))
-#define GASCOMMIT() if (by_table) { ngmin += gtab_min; ngmax += gtab_max; by_table = false; \
-                                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG) }
-#define MEMX(st_, sz_, later_) { const int mx_ = mem_extend((st_), (sz_), nmsize, ngmin, ngmax, \
-                                                        L.mem_cap, (later_), txlim); \
-                                 if (mx_ == MX_OOG) EXCX(EXC_OOG) if (mx_ == MX_ESCAPE) ESCX(ESC_MEMORY) }
-#define ZEROFILL() if (nmsize > msize0) V.mzero(msize0, nmsize);
+    for (;;) {
+        const uint64_t live_mask = __ballot(live);
+        if (live_mask == 0ull) break;
+        const int lead = __builtin_ctzll(live_mask);
+        const uint32_t uy = __builtin_amdgcn_readlane(pd.y, lead);
+        uint32_t ux = __builtin_amdgcn_readlane(pd.x, lead), uk = uy;
+        // opaque scalar copies: keep the decode below on SGPRs (otherwise the
+        // compiler substitutes the per-lane pd.y, equal inside the branch)
+        asm volatile("" : "+s"(uk), "+s"(ux));
+        if (!(live && pd.y == uy)) continue;
 
-            do {
-                // svm.py:391-402 precheck; instructions.py:188-193 write protection
-                if (sp < req) EXCX(EXC_UNDERFLOW)
-                if ((flags & LANE_STATIC) && (op == 0x55u || (op >= 0xa0u && op <= 0xa4u)))
-                    EXCX(EXC_WRITEPROT)
-                // operands: what the mutator pops (ADDMOD, SSTORE pop more than `req`)
-                if (sp < npop) EXCX(EXC_UNDERFLOW)
-                if (npop >= 3u) c = V.stack(sp - 3u);
-                nsp = sp - npop;
-                switch (kind) {
-                case K_ALU:
-                    if (op == 0x0a) ++n_exp;
-                    res = alu(op, a, b, c);
-                    break;
-                case K_PUSH:                                        // (:278-320)
-                    res = push_staged ? ld_word(s_push, pc) : ld_word(gpush, pc);
-                    break;
-                case K_DUP: {                                       // (:322-331)
-                    const uint32_t k = op - 0x7fu;
-                    if (sp < k) EXCX(EXC_UNDERFLOW)
-                    res = k == 1u ? T0 : k == 2u ? T1 : V.stack(sp - k);
-                    break;
+        const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
+        const uint32_t npop = (uk >> 12) & 15u, need = max((uk >> 8) & 15u, npop);
+        const bool push = ((uk >> 16) & 1u) != 0u;
+        if (cov_on) {
+            if (sflag) s_cov[pc] = 1;
+            else cov[C.cov_off + pc] = 1;
+        }
+        if (prof) atomicAdd(&s_prof[op], 1u);
+        ++executed;
+
+        // ---- fast path: result and preconditions, no writes ----
+        bool fast = true, ok = sp >= need;
+        U256 res;
+        uint32_t npc = pc + 1u, ndepth = depth;
+        uint64_t ngmin = gmin + (ux & 0xffffu), ngmax = gmax + (ux >> 16);
+        bool gas_check = true;
+        const U256 &a = T0, &b = T1;
+        switch (kind) {
+        case K_PUSH:
+            res = sflag ? ld_word((const l_u4 *)s_push, pc)
+                        : ld_word(gv(a32 + C.push_off), pc);
+            break;
+        case K_DUP: {
+            const uint32_t k = op - 0x7fu;
+            ok = ok && sp >= k;
+            if (k == 1u) res = a;
+            else if (k == 2u) res = b;
+            else res = V.stack(ok ? sp - k : 0u);
+            break;
+        }
+        case K_SWAP:
+            ok = ok && sp >= op - 0x8eu;
+            break;
+        case K_POP: case K_JUMPDEST:
+            break;
+        case K_JUMP: case K_JUMPI: {
+            gas_check = false;
+            const uint32_t add = kind == K_JUMP ? 8u : 10u;
+            ngmin = gmin + add; ngmax = gmax + add;
+            const bool take = kind == K_JUMP || !u_iszero(b);
+            if (kind == K_JUMPI) ++ndepth;
+            if (take) {
+                uint32_t idx = MG_JRES_NONE;
+                if (u_fits32(a) && a.w[0] < C.n_jres) {
+                    if (jflag) { idx = s_jr[a.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
+                    else idx = a32[C.jres_off + a.w[0]];
                 }
-                case K_SWAP: {                                      // (:333-343)
+                ok = ok && idx != MG_JRES_NONE &&
+                     (sflag ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu;
+                npc = idx;
+            }
+            break;
+        }
+        case K_ALU:
+            if (alu_is_fast(op)) res = alu(op, a, b, b);
+            else fast = false;
+            break;
+        case K_ENV:
+            switch (op) {
+            case 0x30: res = V.env(0); break;               // ADDRESS
+            case 0x32: res = V.env(2); break;               // ORIGIN
+            case 0x33: res = V.env(1); break;               // CALLER
+            case 0x34: res = V.env(3); break;               // CALLVALUE
+            case 0x3a: res = V.env(4); break;               // GASPRICE
+            case 0x36: res = u_small(L.calldata_len[lane]); break;
+            case 0x38: res = u_small(C.n_bytes); break;     // CODESIZE
+            case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
+            case 0x58: res = u_small(a32[C.addr_off + pc]); break;
+            case 0x59: res = u_small(msize); break;
+            default: res = u_zero(); break;                 // RETURNDATASIZE
+            }
+            break;
+        case K_MLOAD: case K_MSTORE:    // inside msize: no extension, table gas only
+            ok = ok && u_fits32(a) && msize >= 32u && a.w[0] <= msize - 32u;
+            if (kind == K_MLOAD && ok) res = V.mword(a.w[0]);
+            break;
+        case K_CDLOAD: {                // aligned and inside the calldata
+            const uint32_t cdl = L.calldata_len[lane];
+            ok = ok && u_fits32(a) && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl;
+            if (ok) {
+                const uint32_t d0 = a.w[0] >> 2;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) res.w[7 - k] = V.cdw(d0 + k);
+            }
+            break;
+        }
+        default:
+            fast = false;
+            break;
+        }
+
+        if (fast) {
+            if (gas_check) ok = ok && ngmin < glim;
+            if (push) ok = ok && sp - npop + 1u <= stack_lim;
+            if (ok) {
+                // ---- writes ----
+                if (kind == K_SWAP) {
                     const uint32_t k = op - 0x8fu;
-                    if (sp < k + 1u) EXCX(EXC_UNDERFLOW)
                     if (k == 1u) {
-                        GASCOMMIT()
-                        nT0 = T1; nT1 = T0;
+                        const U256 t = T0; T0 = T1; T1 = t;
                     } else {
                         const U256 x = V.stack(sp - 1u - k);
-                        GASCOMMIT()
                         V.set_stack(sp - 1u - k, T0);
-                        nT0 = x;
+                        T0 = x;
                     }
-                    tos_done = true;
-                    break;
-                }
-                case K_LOG: case K_POP: case K_RDCOPY: case K_JUMPDEST:
-                    break;                                          // pops only / no-op
-                case K_ENV:
-                    switch (op) {
-                    case 0x30: res = V.env(0); break;               // ADDRESS
-                    case 0x32: res = V.env(2); break;               // ORIGIN
-                    case 0x33: res = V.env(1); break;               // CALLER
-                    case 0x34: res = V.env(3); break;               // CALLVALUE
-                    case 0x3a: res = V.env(4); break;               // GASPRICE
-                    case 0x36: res = u_small(L.calldata_len[lane]); break;
-                    case 0x38: res = u_small(C.n_bytes); break;     // CODESIZE
-                    case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
-                    case 0x58: res = u_small(a32[C.addr_off + pc]); break;
-                    case 0x59: res = u_small(msize0); break;
-                    default: res = u_zero(); break;                 // RETURNDATASIZE
-                    }
-                    break;
-                case K_STOP: STOPX(ST_STOP, 0u)
-                case K_SHA3: {  // own gas first, then mem_extend (instructions.py:1013-1051)
-                    by_table = false;
-                    const bool big = (b.w[2] | b.w[3] | b.w[4] | b.w[5] | b.w[6] | b.w[7]) != 0u;
-                    const uint64_t blen = (uint64_t)b.w[0] | ((uint64_t)b.w[1] << 32);
-                    const uint64_t g = (big || blen > BIG_END) ? HUGE_GAS : 30ull + 6ull * ((blen + 31ull) >> 5);
-                    ngmin += g; ngmax += g;
-                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
-                    MEMX(a, b, -1)
-                    ZEROFILL()
-                    if (b.w[0] == 0u) {  // get_empty_keccak_hash (keccak_function_manager.py:87-93)
-                        res.w[7] = 0xc5d24601u; res.w[6] = 0x86f7233cu; res.w[5] = 0x927e7db2u; res.w[4] = 0xdcc703c0u;
-                        res.w[3] = 0xe500b653u; res.w[2] = 0xca82273bu; res.w[1] = 0x7bfad804u; res.w[0] = 0x5d85a470u;
-                    } else {
-                        res = keccak_mem(V, a.w[0], b.w[0]);
-                        if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
-                    }
-                    ++n_sha3;
-                    break;
-                }
-                case K_CDLOAD: {  // byte (off+k) mod 2^256, 0 past the end (calldata.py:46-90,137-146)
-                    const uint32_t cdl = L.calldata_len[lane];
-                    const bool fits = u_fits32(a);
-                    if (fits && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl) {
-                        const uint32_t d0 = a.w[0] >> 2;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) res.w[7 - k] = L.calldata[V.row(d0 + k)];
-                    } else {
-                        bool wrapc = true;
-#pragma unroll
-                        for (int k = 1; k < 8; ++k) wrapc = wrapc && a.w[k] == 0xffffffffu;
-                        for (uint32_t k = 0; k < 32u; ++k) {
-                            const uint64_t t = (uint64_t)a.w[0] + k;
-                            bool ok = false;
-                            uint32_t idx = 0;
-                            if (fits) { ok = t < cdl; idx = (uint32_t)t; }
-                            else if (wrapc && t >= (1ull << 32)) { idx = (uint32_t)(t - (1ull << 32)); ok = idx < cdl; }
-                            if (ok) {
-                                const uint32_t byte = V.cbyte(idx), sh = 8u * (31u - k);
-                                res = u_or(res, u_shl_n(u_small(byte), sh));
-                            }
-                        }
-                    }
-                    break;
-                }
-                case K_CDCOPY: {  // nothing at all for size 0 (:806-891)
-                    if (u_iszero(c)) break;
-                    MEMX(a, c, (int64_t)gtab_min)
-                    GASCOMMIT()
-                    ZEROFILL()
-                    const uint32_t cdl = L.calldata_len[lane];
-                    const bool bfits = u_fits32(b);
-                    bool wrapc = true;
-#pragma unroll
-                    for (int k = 1; k < 8; ++k) wrapc = wrapc && b.w[k] == 0xffffffffu;
-                    if (prof) atomicAdd(&s_prof[257], c.w[0]);
-                    for (uint32_t k = 0; k < c.w[0]; ++k) {
-                        const uint64_t t = (uint64_t)b.w[0] + k;
-                        uint32_t v = 0u;
-                        if (bfits) { if (t < cdl) v = V.cbyte((uint32_t)t); }
-                        else if (wrapc && t >= (1ull << 32) && t - (1ull << 32) < cdl) v = V.cbyte((uint32_t)(t - (1ull << 32)));
-                        V.set_mbyte(a.w[0] + k, v);
-                    }
-                    break;
-                }
-                case K_CODECOPY: {  // extends even for size 0; copy stops at the end of code
-                    MEMX(a, c, (int64_t)gtab_min)
-                    GASCOMMIT()
-                    ZEROFILL()
-                    uint32_t ncopy = 0u;
-                    if (u_fits32(b) && b.w[0] < C.n_bytes) ncopy = min(C.n_bytes - b.w[0], c.w[0]);
-                    if (prof) atomicAdd(&s_prof[257], ncopy);
-                    for (uint32_t k = 0; k < ncopy; ++k) V.set_mbyte(a.w[0] + k, a8[C.bytes_off + b.w[0] + k]);
-                    break;
-                }
-                case K_MLOAD:
-                    MEMX(a, u_small(32), (int64_t)gtab_min)
-                    GASCOMMIT()
-                    ZEROFILL()
-                    res = V.mword(a.w[0]);
-                    break;
-                case K_MSTORE:
-                    MEMX(a, u_small(32), (int64_t)gtab_min)
-                    GASCOMMIT()
-                    ZEROFILL()
-                    V.set_mword(a.w[0], b);
-                    break;
-                case K_MSTORE8:
-                    MEMX(a, u_small(1), (int64_t)gtab_min)
-                    GASCOMMIT()
-                    ZEROFILL()
-                    V.set_mbyte(a.w[0], b.w[0] & 0xffu);
-                    break;
-                case K_SLOAD: {  // over K(0) + stores (account.py:43-74)
-                    const uint32_t cnt = L.storage_count[lane];
-                    if (prof) atomicAdd(&s_prof[258], cnt);
-                    for (uint32_t s = 0; s < cnt; ++s) {
-                        const size_t base = V.row(s) * 2;
-                        if (u_eq(ld_word(L.storage, base), a)) { res = ld_word(L.storage, base + 1); break; }
-                    }
-                    break;
-                }
-                case K_SSTORE: {
-                    const uint32_t cnt = L.storage_count[lane];
-                    if (prof) atomicAdd(&s_prof[258], cnt);
-                    uint32_t slot = cnt;
-                    for (uint32_t s = 0; s < cnt; ++s)
-                        if (u_eq(ld_word(L.storage, V.row(s) * 2), a)) { slot = s; break; }
-                    if (slot == cnt && cnt >= L.storage_cap) ESCX(ESC_STORAGE)
-                    GASCOMMIT()
-                    if (slot == cnt) {
-                        st_word(L.storage, V.row(slot) * 2, a);
-                        L.storage_count[lane] = cnt + 1u;
-                    }
-                    st_word(L.storage, V.row(slot) * 2 + 1, b);
-                    break;
-                }
-                case K_JUMP: {  // gas 8 by hand, no OOG check (:1520-1556)
-                    by_table = false;
-                    uint32_t idx = MG_JRES_NONE;
-                    if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
-                    if (idx == MG_JRES_NONE ||
-                        (staged ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) != 0x5bu) EXCX(EXC_BADJUMP)
-                    ngmin += 8u; ngmax += 8u; npc = idx;
-                    break;
-                }
-                case K_JUMPI: {  // gas 10 by hand, depth + 1 on the side taken (:1558-1636)
-                    by_table = false;
-                    if (u_iszero(b)) {
-                        ngmin += 10u; ngmax += 10u; ++ndepth;
-                    } else {
-                        uint32_t idx = MG_JRES_NONE;
-                        if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
-                        if (idx == MG_JRES_NONE ||
-                            (staged ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) != 0x5bu) STOPX(ST_DROPPED, 0u)
-                        ngmin += 10u; ngmax += 10u; ++ndepth; npc = idx;
-                    }
-                    break;
-                }
-                case K_BEGINSUB: EXCX(EXC_OOG)
-                case K_RETURN:  // (:1857-1874)
-                    MEMX(a, b, 0)
-                    if (gas_oog(ngmin, txlim)) EXCX(EXC_OOG)
-                    L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
-                    STOPX(ST_RETURN, 0u)
-                case K_REVERT:  // no memory extension (:1899-1934)
-                    L.ret_offset[lane] = a.w[0]; L.ret_len[lane] = b.w[0];
-                    STOPX(ST_REVERT, 0u)
-                case K_INVALID: EXCX(EXC_INVALID)
-                default: ESCX(ESC_OPCODE)
-                }
-                if (stop != ST_RUNNING) break;
-                if (!tos_done) {
-                    // new top-of-stack registers from the pops/push of this opcode
-                    if (push) {   // MachineStack.append: overflow check precedes the write
-                        if (nsp + 1u > STACK_LIMIT) EXCX(EXC_OVERFLOW)
-                        if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK)
-                        GASCOMMIT()
-                        if (npop == 0u) {            // T1 moves below the register window
+                } else {
+                    if (kind == K_MSTORE) V.set_mword(a.w[0], b);
+                    if (push) {
+                        if (npop == 0u) {
                             if (sp >= 2u) V.set_stack(sp - 2u, T1);
-                            nT1 = T0;
-                        } else if (npop == 1u) {
-                            nT1 = T1;
-                        } else {
-                            nT1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+                            T1 = T0;
+                        } else if (npop >= 2u) {
+                            T1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
                         }
-                        nT0 = res;
-                        ++nsp;
+                        T0 = res;
                     } else if (npop == 1u) {
-                        nT0 = T1;
-                        nT1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                        T0 = T1;
+                        T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
                     } else if (npop >= 2u) {
-                        nT0 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
-                        nT1 = sp >= npop + 2u ? V.stack(sp - npop - 2u) : u_zero();
+                        T0 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
+                        T1 = sp >= npop + 2u ? V.stack(sp - npop - 2u) : u_zero();
                     }
+                    sp = sp - npop + (push ? 1u : 0u);
                 }
-                GASCOMMIT()
-            } while (0);
-#undef STOPX
-#undef EXCX
-#undef ESCX
-#undef GASCOMMIT
-#undef MEMX
-#undef ZEROFILL
-            if (stop != ST_RUNNING) {
-                status = stop;
-                aux = sx;
-                if (stop == ST_ESCAPE) --executed;
-                break;
+                pc = npc; depth = ndepth; gmin = ngmin; gmax = ngmax;
             }
-            pc = npc; sp = nsp; msize = nmsize; depth = ndepth; gmin = ngmin; gmax = ngmax;
-            T0 = nT0; T1 = nT1;
         }
+        if (!fast || !ok) {
+            LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u};
+            slow_step(R, E, uk, ux);
+            n_sha3 = R.n_sha3; n_exp = R.n_exp;
+            if (R.stop != ST_RUNNING) {
+                status = R.stop;
+                aux = R.sx;
+                if (R.stop == ST_ESCAPE) --executed;
+                live = false;
+            } else {
+                T0 = R.T0; T1 = R.T1; gmin = R.gmin; gmax = R.gmax;
+                pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth;
+            }
+        }
+        if (live) FETCH();
+    }
+#undef FETCH
+
+    if (run0) {
         // flush the registers, then the LDS window: HBM holds the canonical S[0 .. sp)
         if (sp >= 1u) V.set_stack(sp - 1u, T0);
         if (sp >= 2u) V.set_stack(sp - 2u, T1);
-        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_gstack(k, V.stack(k));
+        for (uint32_t k = 0; k < min(sp, win); ++k) V.set_gstack(k, V.wstack(k));
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;

@@ -646,28 +646,30 @@ extern "C" int mg_lanes_reset(mg_ctx *ctx) {
 }
 
 // LDS plan of one launch: the largest loaded code is pre-decoded into LDS (up to
-// 1024 instructions, 41 B each) and the rest of the 160 KiB CU budget, minus a
-// margin for the static arrays, holds the stack window (8 KiB per slot for a
-// 256-lane block), at most 16 slots.
-static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, size_t &bytes) {
-    uint32_t maxn = 0;
-    for (const DevCode &c : ctx->codes) maxn = std::max(maxn, c.n_instr);
-    pd_cap = (std::min<uint32_t>(maxn, 1024u) + 15u) & ~15u;
-    const size_t code_bytes = (size_t)pd_cap * (8 + 32 + 1);
+// 1023 instructions, 41 B each, plus the END sentinel) with its jump-resolve
+// table (2 B per byte address, up to 8192), and the rest of the 160 KiB CU
+// budget, minus a margin for the static arrays, holds the stack window (8 KiB
+// per slot for a 256-lane block), at most 16 slots.
+static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_t &jr_cap, size_t &bytes) {
+    uint32_t maxn = 0, maxj = 0;
+    for (const DevCode &c : ctx->codes) { maxn = std::max(maxn, c.n_instr); maxj = std::max(maxj, c.n_jres); }
+    pd_cap = (std::min<uint32_t>(maxn, 1023u) + 1u + 15u) & ~15u;   // + END sentinel
+    jr_cap = (std::min<uint32_t>(maxj, 8192u) + 15u) & ~15u;
+    const size_t code_bytes = (size_t)pd_cap * (8 + 32 + 1) + (size_t)jr_cap * 2;
     const size_t budget = 160u * 1024u - 4096u;
     const size_t slot_bytes = 2u * LANE_BLOCK * 16u;
     win = (uint32_t)std::min<size_t>(16, budget > code_bytes ? (budget - code_bytes) / slot_bytes : 0);
     win = std::min<uint32_t>(win, ctx->L.stack_cap);
-    bytes = (size_t)win * slot_bytes + (size_t)pd_cap * 40 + pd_cap + 16;
+    bytes = (size_t)win * slot_bytes + code_bytes + 16;
 }
 
 static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
                        DevCounters *ctr, unsigned long long *prof = nullptr) {
     const uint64_t zero[4] = {0, 0, 0, 0};
     const uint64_t *m = hook_mask ? hook_mask : zero;
-    uint32_t win = 0, pd_cap = 0;
+    uint32_t win = 0, pd_cap = 0, jr_cap = 0;
     size_t lds = 0;
-    lds_plan(ctx, win, pd_cap, lds);
+    lds_plan(ctx, win, pd_cap, jr_cap, lds);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)k_lane_step, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -677,7 +679,7 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     }
     hipLaunchKernelGGL(k_lane_step, dim3(blocks_for(ctx->L.n, LANE_BLOCK)), dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
-                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap);
+                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap);
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }

@@ -7,3 +7,5 @@ OUT=gpurun_out
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_lanes.py -x -v --timeout 300 --timeout-method thread > $OUT/pytest_quick.log 2>&1 && \
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-c4 > $OUT/bench_quick.log 2>&1
+[ -n "$OPBENCH" ] && timeout -k 10 300 python -u scripts/opbench.py > $OUT/opbench.log 2>&1
+true
