@@ -48,10 +48,12 @@ enum BvOp : uint32_t {
 #define BV_REF_CONST 3u
 #define BV_MAX_SLOTS 8u
 #define BV_BLOCK 256u
-#define BV_TILE_INSNS 2048u   // LDS program tile: 32 KiB
+#define BV_TILE_INSNS 2048u   // longest program (LDS tile upper bound: 32 KiB)
+#define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
+#define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
 
 struct BvState {
-    uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0;
+    uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0, tile_cap = 0;
     uint4 *insns = nullptr;          // [total]
     uint32_t *prog_off = nullptr;    // [n_dags + 1]
     uint32_t *tile_dag = nullptr;    // [n_tiles + 1] first DAG of each tile
@@ -73,13 +75,22 @@ DEV U256 bv_mask(U256 v, uint32_t width) {
     }
     return v;
 }
-// sign-extend a width-bit value to 256 bits
+// sign-extend a width-bit value to 256 bits.  Per-limb selects on the (wave-
+// uniform) width only: a runtime limb index would put the value in scratch.
 DEV U256 bv_sext(U256 v, uint32_t width) {
     if (width >= 256u || width == 0u) return v;
-    const uint32_t sb = width - 1u;
-    const bool neg = (u_shr_n(v, sb, 0u).w[0] & 1u) != 0u;
-    if (!neg) return v;
-    return u_or(v, u_shl_n(u_ones(), width));
+    const uint32_t sb = width - 1u, li = sb >> 5, bi = sb & 31u;
+    uint32_t top = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) top |= ((uint32_t)i == li) ? v.w[i] : 0u;
+    if (!((top >> bi) & 1u)) return v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t lo = 32u * i;
+        if (width <= lo) v.w[i] = 0xffffffffu;
+        else if (width < lo + 32u) v.w[i] |= 0xffffffffu << (width - lo);
+    }
+    return v;
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -123,24 +134,29 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       const uint4 *__restrict__ values, uint32_t n_models,
                                                       uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles,
                                                       uint32_t tiles_pad, uint32_t dag_lo, uint32_t dag_hi,
+                                                      uint32_t tile_cap, uint32_t chunks_per_block,
                                                       uint32_t *__restrict__ first_sat,
                                                       uint32_t *__restrict__ sat_count) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    uint4 *prog = smem;                          // [BV_TILE_INSNS]
-    uint4 *slots = smem + BV_TILE_INSNS;         // [n_slots][2][BV_BLOCK]
-    // chunk-major order with the tile count padded to a multiple of 8: the blocks
+    uint4 *prog = smem;                          // [tile_cap]
+    uint4 *slots = smem + tile_cap;              // [n_slots][2][BV_BLOCK]
+    // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
     const uint32_t tile = tile_first + (b % tiles_pad);
-    const uint32_t chunk = b / tiles_pad;
+    const uint32_t group = b / tiles_pad;
     if (tile >= tile_first + n_tiles) return;
     const uint32_t d0 = max(tile_dag[tile], dag_lo), d1 = min(tile_dag[tile + 1], dag_hi);
     if (d0 >= d1) return;
+    // the tile is read from HBM once per block and reused for every model chunk
     const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
     for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
     __syncthreads();
 
     const uint32_t tid = threadIdx.x;
+    const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
+    const uint32_t c_lo = group * chunks_per_block, c_hi = min(c_lo + chunks_per_block, n_chunks);
+    for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
     const uint32_t model = chunk * BV_BLOCK + tid;
     const bool live = model < n_models;
     BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid};
@@ -241,6 +257,7 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
             atomicMin(&first_sat[d], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
         }
     }
+    }
 }
 
 template <class T>
@@ -289,12 +306,17 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         }
     }
     // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
+    // LDS tile capacity: the longest program rounded up, at least BV_TILE_MIN, so
+    // short-program batches keep a small LDS footprint (higher occupancy)
+    uint32_t longest = 0;
+    for (uint32_t d = 0; d < n; ++d) longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d]);
+    s.tile_cap = std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u);
     s.h_tiles.clear();
     s.h_tiles.push_back(0);
     uint32_t acc = 0;
     for (uint32_t d = 0; d < n; ++d) {
         const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
-        if (acc + len > BV_TILE_INSNS || (d - s.h_tiles.back()) >= 64u) { s.h_tiles.push_back(d); acc = 0; }
+        if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= 64u) { s.h_tiles.push_back(d); acc = 0; }
         acc += len;
     }
     s.h_tiles.push_back(n);
@@ -338,13 +360,18 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     uint32_t t1 = (uint32_t)(std::lower_bound(t.begin(), t.end(), dag_hi) - t.begin());
     const uint32_t nt = t1 - t0;
     const uint32_t tiles_pad = (nt + 7u) & ~7u;
+    // model chunks per block: as many as keep >= BV_GROUP_TARGET blocks in flight,
+    // so each program tile is staged once per block instead of once per chunk
     const uint32_t chunks = (s.n_models + BV_BLOCK - 1) / BV_BLOCK;
-    const size_t grid = (size_t)tiles_pad * chunks;
+    const uint32_t groups_wanted = std::max<uint32_t>(1u, (BV_GROUP_TARGET + tiles_pad - 1u) / tiles_pad);
+    const uint32_t cpb = std::max<uint32_t>(1u, chunks / std::min(groups_wanted, chunks));
+    const uint32_t groups = (chunks + cpb - 1u) / cpb;
+    const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
-    const size_t lds = ((size_t)BV_TILE_INSNS + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
+    const size_t lds = ((size_t)s.tile_cap + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
     hipLaunchKernelGGL(k_bv_eval, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st, s.insns, s.prog_off, s.tile_dag,
                        s.consts, s.values, s.n_models, s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
-                       s.first_sat, s.sat_count);
+                       s.tile_cap, cpb, s.first_sat, s.sat_count);
     e = hipGetLastError();
     if (e != hipSuccess) { msg = std::string("k_bv_eval launch: ") + hipGetErrorString(e); return MG_EDEVICE; }
     return 0;

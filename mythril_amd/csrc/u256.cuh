@@ -3,7 +3,7 @@
 // Every loop is fully unrolled over compile-time limb indices so values stay in
 // VGPRs (a runtime-indexed register array would go to scratch); runtime shift
 // amounts are applied with a 3-stage limb barrel shifter (v_cndmask per limb)
-// followed by a 64-bit funnel shift per limb.  Semantics are z3's bit-vector
+// followed by a funnel shift per limb (v_alignbit_b32).  Semantics are z3's bit-vector
 // semantics used by mythril/laser/smt/bitvec.py (bvudiv x 0 = 2^256-1,
 // bvurem x 0 = x, bvsdiv x 0 = x<0 ? 1 : -1, bvsrem x 0 = x).
 #pragma once
@@ -168,13 +168,15 @@ DEV U256 u_shr_limbs(U256 a, uint32_t q, uint32_t fill) {
     }
     return a;
 }
-// (hi:lo) << r, high half, r in [0,32)
+// (hi:lo) << r, high half, r in [0,32).  v_alignbit_b32 keeps each funnel
+// shift in one VALU op; written as a 64-bit shift of (hi << 32 | lo) the
+// compiler may merge adjacent limbs into 64-bit scratch loads instead.
 DEV uint32_t fsl(uint32_t hi, uint32_t lo, uint32_t r) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (32u - r));
+    return r == 0u ? hi : __builtin_amdgcn_alignbit(hi, lo, 32u - r);
 }
 // (hi:lo) >> r, low half, r in [0,32)
 DEV uint32_t fsr(uint32_t hi, uint32_t lo, uint32_t r) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> r);
+    return __builtin_amdgcn_alignbit(hi, lo, r);
 }
 // a << n for n < 256
 DEV U256 u_shl_n(U256 a, uint32_t n) {
@@ -231,16 +233,120 @@ DEV uint32_t u_popcount(const U256 &a) {
 }
 
 // ---- division ------------------------------------------------------------------
-// Unsigned a / b and a % b for b != 0.  Power-of-two divisors are shifts; other
-// divisors run shift-subtract over only the (bitlen(a) - bitlen(b) + 1) quotient
-// bit positions that can be non-zero, so a selector extraction (x / 2^224) or a
-// small quotient costs a handful of iterations.
+// Unsigned a / b and a % b for b != 0.
+//
+// * power-of-two divisors are shifts;
+// * when every lane of the wave needs at most 32 quotient bits (bitlen(a) -
+//   bitlen(b) < 32: selector extraction, comparisons of similar magnitudes) the
+//   wave runs shift-subtract over only those bit positions;
+// * otherwise Knuth's algorithm D on 32-bit digits: b is normalised so its top
+//   bit is bit 255, a is shifted into 16 limbs by the same amount, and the 8
+//   quotient digits come out top-down.  Each digit is estimated from the top two
+//   remainder limbs with a Moller-Granlund 2-by-1 division by the precomputed
+//   reciprocal of b's top limb (no per-digit hardware divide), refined against
+//   the second limb, then the digit times b is subtracted with one add-back
+//   when the estimate was still one too large.  All limb indices are static
+//   (unrolled), so the 17-limb remainder stays in VGPRs.
+DEV uint32_t mulhi32(uint32_t a, uint32_t b) { return __umulhi(a, b); }
+
+// floor((2^64 - 1) / d) - 2^32 for d with its top bit set (MG 2011, eq. 1)
+DEV uint32_t mg_reciprocal(uint32_t d) {
+    return (uint32_t)((((uint64_t)(~d) << 32) | 0xffffffffull) / d);
+}
+// (u1:u0) / d for u1 < d, d normalised, v = mg_reciprocal(d)  (MG 2011, Alg. 4)
+DEV uint32_t mg_div21(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v, uint32_t &rem) {
+    const uint64_t p = (uint64_t)v * u1 + ((((uint64_t)u1 + 1u) << 32) | u0);
+    uint32_t q1 = (uint32_t)(p >> 32);
+    const uint32_t q0 = (uint32_t)p;
+    uint32_t r = u0 - q1 * d;
+    if (r > q0) { q1 -= 1u; r += d; }
+    if (r >= d) { q1 += 1u; r -= d; }
+    rem = r;
+    return q1;
+}
+
+DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256 &r) {
+    const uint32_t s = 256u - lb;                       // normalisation shift, < 256
+    const U256 vn = u_shl_n(b, s);
+    const U256 lo = u_shl_n(a, s);
+    const U256 hi = s == 0u ? u_zero() : u_shr_n(a, 256u - s, 0u);
+    uint32_t u[17];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { u[i] = lo.w[i]; u[8 + i] = hi.w[i]; }
+    u[16] = 0u;
+    const uint32_t v7 = vn.w[7], v6 = vn.w[6];
+    const uint32_t rcp = mg_reciprocal(v7);
+    q = u_zero();
+    // a < 2^256 so the digit at 2^256 is 0: u[15..8] < vn and the loop starts at 7
+#pragma unroll
+    for (int j = 7; j >= 0; --j) {
+        const uint32_t u2 = u[j + 8], u1 = u[j + 7], u0 = u[j + 6];
+        uint32_t qh, rh;
+        bool rh_ovf;
+        if (u2 >= v7) {                                 // u2 == v7: qhat = 2^32 - 1
+            qh = 0xffffffffu;
+            const uint64_t t = (uint64_t)u1 + v7;       // rhat = u1 + v7
+            rh = (uint32_t)t;
+            rh_ovf = (t >> 32) != 0u;
+        } else {
+            qh = mg_div21(u2, u1, v7, rcp, rh);
+            rh_ovf = false;
+        }
+        // refine: while qhat * v6 > (rhat : u0) decrement (at most twice)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!rh_ovf) {
+                const uint64_t lhs = (uint64_t)qh * v6;
+                const uint64_t rhs = ((uint64_t)rh << 32) | u0;
+                if (lhs > rhs) {
+                    qh -= 1u;
+                    const uint64_t t = (uint64_t)rh + v7;
+                    rh = (uint32_t)t;
+                    rh_ovf = (t >> 32) != 0u;
+                }
+            }
+        }
+        // u[j .. j+8] -= qh * vn
+        uint32_t carry = 0u, borrow = 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t p = (uint64_t)qh * vn.w[i] + carry;
+            carry = (uint32_t)(p >> 32);
+            const uint64_t t = (uint64_t)u[j + i] - (uint32_t)p - borrow;
+            u[j + i] = (uint32_t)t;
+            borrow = (uint32_t)(t >> 63);
+        }
+        const uint64_t t = (uint64_t)u[j + 8] - carry - borrow;
+        u[j + 8] = (uint32_t)t;
+        if ((t >> 63) != 0u) {                          // estimate one too large: add back
+            qh -= 1u;
+            uint32_t c = 0u;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint64_t w = (uint64_t)u[j + i] + vn.w[i] + c;
+                u[j + i] = (uint32_t)w;
+                c = (uint32_t)(w >> 32);
+            }
+            u[j + 8] += c;
+        }
+        q.w[j] = qh;
+    }
+    U256 rn;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn.w[i] = u[i];
+    r = u_shr_n(rn, s, 0u);
+}
+
 DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) {
     const uint32_t lb = u_bitlen(b), la = u_bitlen(a);
     if (u_popcount(b) == 1u) {
         const uint32_t k = lb - 1u;
         q = u_shr_n(a, k, 0u);
         r = u_and(a, u_sub(b, u_small(1)));
+        return;
+    }
+    if (__ballot(la >= lb + 32u) != 0ull) {            // some lane needs > 32 quotient bits
+        u_divmod_knuth(a, b, lb, q, r);
         return;
     }
     q = u_zero();

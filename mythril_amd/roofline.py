@@ -18,6 +18,9 @@ Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; INT32 VALU 256 CU x 64 lanes x
 """
 from __future__ import annotations
 
+import json
+from pathlib import Path
+
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0
@@ -88,6 +91,26 @@ def algorithmic_work(op_counts: np.ndarray, extra: np.ndarray):
     return ops, byts, steps
 
 
+PROFILES = Path(__file__).resolve().parent.parent / "profiles"
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN/traffic.json, written by scripts/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of the same bench command).
+    Returns (bytes, source) or (None, None) when no summary covers the kernel."""
+    for d in sorted(PROFILES.glob("r*"), reverse=True):
+        f = d / "traffic.json"
+        if f.is_file():
+            try:
+                rec = json.loads(f.read_text()).get(kernel)
+            except (OSError, ValueError):
+                rec = None
+            if rec:
+                return float(rec["traffic_bytes"]), str(f.relative_to(PROFILES.parent))
+    return None, None
+
+
 def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
     """Profile one batch (untimed; the resident image is reset first) and price the
     timed kernel's average launch against the HBM and INT32 VALU peaks."""
@@ -107,7 +130,9 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
         "peak": HBM_PEAK_GBS if primary_hbm else VALU_PEAK_TOPS,
         "unit": "GB/s" if primary_hbm else "T int32-ops/s",
         "frac": hbm_frac if primary_hbm else valu_frac,
-        "traffic": None,
+        "traffic": pmc_traffic("k_lane_step")[0],
+        "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+        "traffic_source": pmc_traffic("k_lane_step")[1],
         "kernel": "k_lane_step",
         "kernel_ms": kernel_ms,
         "algorithmic_bytes_per_launch": byts,

@@ -78,6 +78,8 @@ def test_arithmetic_device_equals_oracle_and_python(dev, op):
     rows = [tuple(rng.choice(sp) for _ in range(nargs)) for _ in range(512)]
     rows += [tuple(rng.getrandbits(rng.choice([8, 64, 128, 200, 255, 256])) for _ in range(nargs))
              for _ in range(1536)]
+    if op in (0x04, 0x05, 0x06, 0x07, 0x08, 0x09):
+        rows += [tuple(division_operand(rng) for _ in range(nargs)) for _ in range(2048)]
     b = LaneBatch(LaneShape(n=len(rows), stack_cap=16, mem_cap=64, calldata_cap=96, storage_cap=4))
     for i, row in enumerate(rows):
         b.set_lane(i, code_id=0, calldata=b"".join(x.to_bytes(32, "big") for x in row),
@@ -87,6 +89,31 @@ def test_arithmetic_device_equals_oracle_and_python(dev, op):
     assert (out.status == MG_HALT_STOP).all()
     for i, row in enumerate(rows):
         assert out.storage_dict(i, drop_zero=False)[0] == fn(*row), (hex(op), row)
+
+
+def division_operand(rng):
+    """Operands that reach every branch of the device's Knuth-D division
+    (u256.cuh): every divisor length, top-limb ties (qhat = 2^32 - 1), estimates
+    that need refinement or an add-back, and wave-mixed quotient lengths."""
+    kind = rng.randrange(8)
+    bits = rng.randint(1, 256)
+    if kind == 0:
+        return rng.getrandbits(bits) | (1 << (bits - 1))
+    if kind == 1:   # all-ones limbs
+        return (1 << bits) - 1
+    if kind == 2:   # top limb 0x80000000.., low limbs zero or ones
+        k = rng.randint(1, 8)
+        return ((1 << 31) << (32 * (k - 1))) | (rng.choice([0, (1 << (32 * (k - 1))) - 1]))
+    if kind == 3:   # repeated limb pattern (equal top limbs in u and v)
+        limb = rng.getrandbits(32) | (1 << 31)
+        return sum(limb << (32 * i) for i in range(rng.randint(1, 8)))
+    if kind == 4:   # 2^k +- small
+        return max(1, ((1 << rng.randint(1, 255)) + rng.randint(-3, 3)) & pysem.M)
+    if kind == 5:   # limbs of 0xffffffff and 0x00000000 mixed
+        return sum(rng.choice([0, 0xFFFFFFFF, 1, 0x80000000]) << (32 * i) for i in range(8))
+    if kind == 6:
+        return rng.getrandbits(256)
+    return rng.getrandbits(rng.choice([32, 33, 63, 64, 65, 96, 224, 225]))
 
 
 @pytest.fixture(scope="module")
