@@ -62,6 +62,7 @@ struct BvState {
     uint32_t *first_sat = nullptr;   // [n_dags]
     uint32_t *sat_count = nullptr;   // [n_dags]
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
+    bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
     std::vector<uint32_t> h_tiles;
 };
 
@@ -127,6 +128,7 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     return r;
 }
 
+template <bool kLdsProg>
 __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
@@ -138,8 +140,12 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       uint32_t *__restrict__ first_sat,
                                                       uint32_t *__restrict__ sat_count) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    uint4 *prog = smem;                          // [tile_cap]
-    uint4 *slots = smem + tile_cap;              // [n_slots][2][BV_BLOCK]
+    // kLdsProg: the program tile is staged in LDS and read with a broadcast
+    // ds_read + readfirstlane; otherwise instructions are read with scalar loads
+    // (uniform address -> s_load_dwordx4 through the scalar cache) and LDS only
+    // holds the register slots (higher occupancy)
+    uint4 *prog = smem;                          // [tile_cap] (kLdsProg)
+    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][BV_BLOCK]
     // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
@@ -150,8 +156,10 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     if (d0 >= d1) return;
     // the tile is read from HBM once per block and reused for every model chunk
     const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
-    for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
-    __syncthreads();
+    if (kLdsProg) {
+        for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
+        __syncthreads();
+    }
 
     const uint32_t tid = threadIdx.x;
     const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
@@ -165,8 +173,14 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
         const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
         U256 acc = u_zero();
         for (uint32_t p = p0; p < p1; ++p) {
-            const uint4 ins = prog[p];
-            const uint32_t w0 = uni(ins.x), ra = uni(ins.y), rb = uni(ins.z), rc = uni(ins.w);
+            uint32_t w0, ra, rb, rc;
+            if (kLdsProg) {
+                const uint4 ins = prog[p];
+                w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
+            } else {
+                const uint4 ins = insns[i0 + uni(p)];
+                w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
+            }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
             U256 A = bv_fetch(c, acc, ra);
             U256 r;
@@ -342,6 +356,8 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         e = e ? e : hipMemcpyAsync(s.values, models->values, (size_t)models->n_vars * models->n_models * 32, hipMemcpyHostToDevice, st);
     e = e ? e : hipStreamSynchronize(st);
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
+    const char *pv = getenv("MG_BV_PROG");
+    s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;
@@ -368,8 +384,10 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t groups = (chunks + cpb - 1u) / cpb;
     const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
-    const size_t lds = ((size_t)s.tile_cap + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
-    hipLaunchKernelGGL(k_bv_eval, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st, s.insns, s.prog_off, s.tile_dag,
+    const bool lds_prog = s.lds_prog;
+    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
+    hipLaunchKernelGGL(lds_prog ? k_bv_eval<true> : k_bv_eval<false>, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
+                       s.insns, s.prog_off, s.tile_dag,
                        s.consts, s.values, s.n_models, s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
                        s.tile_cap, cpb, s.first_sat, s.sat_count);
     e = hipGetLastError();

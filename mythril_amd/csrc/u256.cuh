@@ -53,14 +53,14 @@ DEV bool u_eq(const U256 &a, const U256 &b) {
     for (int i = 0; i < 8; ++i) o |= a.w[i] ^ b.w[i];
     return o == 0u;
 }
+// Carry chains use __builtin_addc / __builtin_subc, which lower to one
+// v_add_co / v_addc_co (v_sub_co / v_subb_co) per limb; the equivalent 64-bit
+// formulation costs 4-5x the VALU instructions (v_lshl_add_u64 + moves).
 // unsigned a < b: borrow out of a - b
 DEV bool u_lt(const U256 &a, const U256 &b) {
-    uint32_t br = 0;
+    unsigned br = 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t t = (uint64_t)a.w[i] - (uint64_t)b.w[i] - br;
-        br = (uint32_t)(t >> 63);
-    }
+    for (int i = 0; i < 8; ++i) (void)__builtin_subc(a.w[i], b.w[i], br, &br);
     return br != 0u;
 }
 DEV bool u_isneg(const U256 &a) { return (a.w[7] >> 31) != 0u; }
@@ -70,40 +70,38 @@ DEV bool u_slt(const U256 &a, const U256 &b) {
 }
 DEV U256 u_add(const U256 &a, const U256 &b) {
     U256 r;
-    uint64_t c = 0;
+    unsigned c = 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c += (uint64_t)a.w[i] + b.w[i];
-        r.w[i] = (uint32_t)c;
-        c >>= 32;
-    }
+    for (int i = 0; i < 8; ++i) r.w[i] = __builtin_addc(a.w[i], b.w[i], c, &c);
     return r;
 }
 DEV U256 u_sub(const U256 &a, const U256 &b) {
     U256 r;
-    uint32_t br = 0;
+    unsigned br = 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t t = (uint64_t)a.w[i] - (uint64_t)b.w[i] - br;
-        r.w[i] = (uint32_t)t;
-        br = (uint32_t)(t >> 63);
-    }
+    for (int i = 0; i < 8; ++i) r.w[i] = __builtin_subc(a.w[i], b.w[i], br, &br);
     return r;
 }
 DEV U256 u_neg(const U256 &a) { return u_sub(u_zero(), a); }
-// low 256 bits of a*b (schoolbook, 36 limb products)
+// low 256 bits of a*b (schoolbook, 36 limb products: 28 v_mad_u64_u32 and
+// 8 v_mul_lo_u32 for the products that only feed limb 7)
 DEV U256 u_mul(const U256 &a, const U256 &b) {
     uint32_t r[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) r[i] = 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        uint64_t carry = 0;
+        uint32_t carry = 0u;
 #pragma unroll
         for (int j = 0; i + j < 8; ++j) {
-            uint64_t t = (uint64_t)a.w[i] * b.w[j] + r[i + j] + carry;
-            r[i + j] = (uint32_t)t;
-            carry = t >> 32;
+            if (i + j == 7) {
+                r[7] += a.w[i] * b.w[j] + carry;
+            } else {
+                uint64_t t = (uint64_t)a.w[i] * b.w[j] + r[i + j];
+                t += carry;
+                r[i + j] = (uint32_t)t;
+                carry = (uint32_t)(t >> 32);
+            }
         }
     }
     U256 o;
@@ -307,26 +305,21 @@ DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256
             }
         }
         // u[j .. j+8] -= qh * vn
-        uint32_t carry = 0u, borrow = 0u;
+        uint32_t carry = 0u;
+        unsigned borrow = 0u;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint64_t p = (uint64_t)qh * vn.w[i] + carry;
             carry = (uint32_t)(p >> 32);
-            const uint64_t t = (uint64_t)u[j + i] - (uint32_t)p - borrow;
-            u[j + i] = (uint32_t)t;
-            borrow = (uint32_t)(t >> 63);
+            u[j + i] = __builtin_subc(u[j + i], (uint32_t)p, borrow, &borrow);
         }
-        const uint64_t t = (uint64_t)u[j + 8] - carry - borrow;
-        u[j + 8] = (uint32_t)t;
-        if ((t >> 63) != 0u) {                          // estimate one too large: add back
+        unsigned neg = 0u;
+        u[j + 8] = __builtin_subc(u[j + 8], carry, borrow, &neg);
+        if (neg) {                                      // estimate one too large: add back
             qh -= 1u;
-            uint32_t c = 0u;
+            unsigned c = 0u;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint64_t w = (uint64_t)u[j + i] + vn.w[i] + c;
-                u[j + i] = (uint32_t)w;
-                c = (uint32_t)(w >> 32);
-            }
+            for (int i = 0; i < 8; ++i) u[j + i] = __builtin_addc(u[j + i], vn.w[i], c, &c);
             u[j + 8] += c;
         }
         q.w[j] = qh;
