@@ -68,6 +68,11 @@ extern "C" {
 /* lane flags */
 #define MG_LANE_STATIC    1u  /* environment.static (WriteProtection)          */
 #define MG_LANE_CREATION  2u  /* ContractCreationTransaction: CODE and CALLDATA ops escape */
+#define MG_LANE_HOOK_ACK  4u  /* the host has fired the hooks of the instruction at pc:
+                                 the first instruction of the next mg_step call runs
+                                 even if its opcode is set in hook_mask            */
+#define MG_LANE_STEP1     8u  /* execute at most one instruction per mg_step call
+                                 (the host fires post-hooks on the successor)     */
 
 /* environment words, per lane */
 #define MG_ENV_ADDRESS   0
@@ -174,6 +179,12 @@ int         mg_lanes_reset(mg_ctx *ctx);
  * dropped (0 = unlimited).                                                   */
 int         mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                     uint32_t max_depth, mg_step_stats *stats);
+/* Same, with a step horizon: a lane also pauses (stays MG_RUNNING) once its
+ * cumulative `steps` reaches `horizon` (0 = none).  The host layer uses it to
+ * deliver hook and halt events in the reference's BFS round order
+ * (mythril_amd/laser/svm.py).                                                */
+int         mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
+                          uint32_t max_depth, uint32_t horizon, mg_step_stats *stats);
 /* Profiling variant (the InstructionProfiler plugin's per-opcode counts,
  * instruction_profiler.py:41-115, as native counters): op_counts[256] =
  * instructions executed per opcode byte; extra[4] = {SHA3 input bytes,

@@ -50,6 +50,8 @@ struct OpInfo {
 
 #define LANE_STATIC 1u
 #define LANE_CREATION 2u
+#define LANE_HOOK_ACK 4u
+#define LANE_STEP1 8u
 
 #define MSTATE_GAS_LIMIT 1000000000ull
 #define STACK_LIMIT 1024u
@@ -643,7 +645,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           uint32_t max_steps, uint32_t max_depth,
                                                           DevCounters *__restrict__ ctr,
                                                           unsigned long long *__restrict__ prof,
-                                                          uint32_t win, uint32_t pd_cap, uint32_t jr_cap) {
+                                                          uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
+                                                          uint32_t horizon) {
     // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
     //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
@@ -728,6 +731,15 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         live = true;
     }
     const bool creation = (flags & LANE_CREATION) != 0u;
+    // host hook protocol: HOOK_ACK lets the first instruction of this call run past
+    // its hook bit; STEP1 caps the lane at one instruction (post-hooks)
+    const bool hook_ack = (flags & LANE_HOOK_ACK) != 0u;
+    uint32_t lane_max = (flags & LANE_STEP1) ? min(max_steps, 1u) : max_steps;
+    // step horizon (mg_step_until): the lane pauses once its cumulative steps reach it
+    if (horizon && run0) {
+        const uint32_t s0 = L.steps[lane];
+        lane_max = min(lane_max, horizon > s0 ? horizon - s0 : 0u);
+    }
     const uint8_t *__restrict__ gops = a8 + C.op_off;
     const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, txlim, glim,
                     lane, threadIdx.x, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
@@ -747,13 +759,14 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             pd = make_uint2(d_.x, o_ | (d_.y << 8) | ((uint32_t)((hm_ >> (o_ & 63u)) & 1ull) << 31)); \
         }                                                                                 \
         const uint32_t k_ = (pd.y >> 17) & 31u, o_ = pd.y & 0xffu;                       \
-        if ((pd.y >> 31) || k_ >= K_ESCAPE || executed >= max_steps ||                    \
+        const bool hk_ = (pd.y >> 31) && !(hook_ack && executed == 0u);                  \
+        if (hk_ || k_ >= K_ESCAPE || executed >= lane_max ||                              \
             (max_depth != 0u && depth >= max_depth) || (creation && o_ - 0x35u < 5u)) {   \
             uint32_t st_ = ST_RUNNING;                                                    \
             if (max_depth != 0u && depth >= max_depth) st_ = ST_DEPTH;                    \
             else if (k_ == K_END) st_ = ST_END;                                           \
-            else if (pd.y >> 31) { st_ = ST_HOOK; aux = o_; }                             \
-            else if (executed >= max_steps) live = false;                                 \
+            else if (hk_) { st_ = ST_HOOK; aux = o_; }                                    \
+            else if (executed >= lane_max) live = false;                                  \
             else { st_ = ST_ESCAPE; aux = o_ | (ESC_OPCODE << 8); }                       \
             if (st_ != ST_RUNNING) { status = st_; live = false; }                        \
         }                                                                                 \

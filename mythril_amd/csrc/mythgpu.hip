@@ -664,7 +664,7 @@ static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_
 }
 
 static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
-                       DevCounters *ctr, unsigned long long *prof = nullptr) {
+                       DevCounters *ctr, unsigned long long *prof = nullptr, uint32_t horizon = 0) {
     const uint64_t zero[4] = {0, 0, 0, 0};
     const uint64_t *m = hook_mask ? hook_mask : zero;
     uint32_t win = 0, pd_cap = 0, jr_cap = 0;
@@ -679,19 +679,24 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     }
     hipLaunchKernelGGL(k_lane_step, dim3(blocks_for(ctx->L.n, LANE_BLOCK)), dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
-                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap);
+                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon);
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
 
 extern "C" int mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
                        mg_step_stats *stats) {
+    return mg_step_until(ctx, hook_mask, max_steps, max_depth, 0u, stats);
+}
+
+extern "C" int mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
+                             uint32_t horizon, mg_step_stats *stats) {
     if (!ctx) return MG_EINVAL;
     if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_step before mg_lanes_upload");
     HIPX(ctx, hipSetDevice(ctx->device));
     HIPX(ctx, hipMemsetAsync(ctx->d_ctr, 0, sizeof(DevCounters), ctx->stream));
     HIPX(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr);
+    int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr, nullptr, horizon);
     if (rc) return rc;
     HIPX(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     DevCounters c{};

@@ -97,13 +97,32 @@ class GpuDevice:
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, batch.n),
                     "mg_lanes_download")
 
+    def upload_range(self, batch: LaneBatch, first: int, n: int):
+        """Upload lanes [first, first + n) of `batch` to the same device lanes."""
+        soa = batch.soa_range(first, n)
+        self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, n),
+                    "mg_lanes_upload")
+
+    def download_range(self, batch: LaneBatch, first: int, n: int):
+        soa = batch.soa_range(first, n)
+        self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, n),
+                    "mg_lanes_download")
+
     def reset(self):
         self._check(self.lib.mg_lanes_reset(self.ctx), "mg_lanes_reset")
 
-    def step(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0) -> StepStats:
+    def step(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0,
+             horizon: int = 0) -> StepStats:
+        """mg_step (horizon 0) or mg_step_until: lanes also pause once their
+        cumulative steps reach `horizon`."""
         st = native.MgStepStats()
-        self._check(self.lib.mg_step(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
-                                     ctypes.byref(st)), "mg_step")
+        if horizon:
+            rc = self.lib.mg_step_until(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
+                                        horizon, ctypes.byref(st))
+        else:
+            rc = self.lib.mg_step(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
+                                  ctypes.byref(st))
+        self._check(rc, "mg_step")
         return StepStats(st.lane_steps, st.running, st.halted, st.hooked, st.escaped, st.kernel_ms)
 
     def step_profile(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0):

@@ -32,7 +32,7 @@ MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
 MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
 MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK = 1, 2, 3, 4
 
-MG_LANE_STATIC, MG_LANE_CREATION = 1, 2
+MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
 MG_ENV_WORDS = 5
 MG_STACK_LIMIT = 1024
@@ -128,6 +128,21 @@ class LaneBatch:
             assert arr.flags["C_CONTIGUOUS"]
             setattr(s, f, arr.ctypes.data)
         self._keep = s  # keep the struct alive with the arrays
+        return s
+
+    def soa_range(self, first: int, n: int) -> MgLaneSoa:
+        """Struct over lanes [first, first + n) of this image (for partial
+        mg_lanes_upload / mg_lanes_download of the lanes the host touched)."""
+        if first < 0 or n < 0 or first + n > self.shape.n:
+            raise ValueError("lane range out of bounds")
+        s = MgLaneSoa()
+        s.n = n
+        s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
+        s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+            arr = getattr(self, f)
+            setattr(s, f, arr.ctypes.data + first * arr.strides[0])
+        self._keep_range = s
         return s
 
     def copy(self) -> "LaneBatch":

@@ -1,0 +1,346 @@
+"""Host view of a concrete LASER path: GlobalState and its parts.
+
+Mirrors the attribute surface hooks and DetectionModules read from
+mythril/laser/ethereum/state/*.py — ``state.mstate.stack[-1].value``,
+``state.mstate.pc``, ``state.get_current_instruction()``,
+``state.environment.active_account.storage[k]``, ``state.world_state``,
+annotations — for paths whose values are all concrete.  Stack words are the
+expression layer's ``BitVec`` values (mythril_amd/smt/expr.py), as LASER's are.
+
+A GlobalState is materialised from a device lane only when the host must see
+it (a hook fires, the path ends); the lane record in HBM is the state while
+kernel 1 steps it.  ``to_lane``/``from_lane`` convert between the two.
+"""
+from __future__ import annotations
+
+from copy import copy
+from typing import Dict, List, Optional, Union
+
+import numpy as np
+
+from ..smt.expr import BitVec, Bool, Expression, symbol_factory
+from .disassembly import Disassembly
+
+M256 = (1 << 256) - 1
+STACK_LIMIT = 1024
+MSTATE_GAS_LIMIT = 1_000_000_000
+
+
+# --------------------------------------------------------------- exceptions
+class VmException(Exception):
+    """evm_exceptions.py:4-43 (names kept so `except StackUnderflowException`
+    in callers reads as in the reference)."""
+
+
+class StackUnderflowException(IndexError, VmException):
+    pass
+
+
+class StackOverflowException(VmException):
+    pass
+
+
+class InvalidJumpDestination(VmException):
+    pass
+
+
+class InvalidInstruction(VmException):
+    pass
+
+
+class OutOfGasException(VmException):
+    pass
+
+
+class WriteProtection(VmException):
+    pass
+
+
+def concrete(x) -> int:
+    """int of a concrete word (int, BitVec, Bool); raises for a symbolic one."""
+    if isinstance(x, Expression):
+        v = x.value
+        if v is None:
+            raise ValueError("symbolic value cannot be placed in a concrete lane")
+        return int(v) & M256
+    return int(x) & M256
+
+
+# --------------------------------------------------------------- machine
+class MachineStack(list):
+    """machine_state.py:18-92: list of 256-bit words, STACK_LIMIT 1024, pop of an
+    empty stack raises StackUnderflowException."""
+    STACK_LIMIT = STACK_LIMIT
+
+    def __init__(self, default_list=None):
+        super().__init__(default_list or [])
+
+    def append(self, element) -> None:
+        if isinstance(element, Bool):
+            element = symbol_factory.BitVecVal(1 if element.value else 0, 256)
+        elif not isinstance(element, BitVec):
+            element = symbol_factory.BitVecVal(int(element), 256)
+        if len(self) >= self.STACK_LIMIT:
+            raise StackOverflowException("Reached the EVM stack limit of 1024")
+        super().append(element)
+
+    def pop(self, index=-1):
+        try:
+            return super().pop(index)
+        except IndexError:
+            raise StackUnderflowException("Trying to pop from an empty stack")
+
+    def __getitem__(self, item):
+        try:
+            return super().__getitem__(item)
+        except IndexError:
+            raise StackUnderflowException("Trying to access a stack element which doesn't exist")
+
+
+class Memory:
+    """memory.py:28-208 for concrete bytes: reads of unset bytes give 0, writes at
+    index >= msize are dropped (memory.py:202-203)."""
+
+    def __init__(self, data: bytes = b""):
+        self._m = bytearray(data)
+
+    def __len__(self):
+        return len(self._m)
+
+    def extend(self, size: int):
+        self._m.extend(b"\x00" * size)
+
+    def __getitem__(self, item):
+        if isinstance(item, slice):
+            start, stop = item.start or 0, item.stop if item.stop is not None else len(self._m)
+            return [self._m[k] if k < len(self._m) else 0 for k in range(start, stop)]
+        return self._m[item] if item < len(self._m) else 0
+
+    def __setitem__(self, key: int, value: int):
+        if key < len(self._m):
+            self._m[key] = concrete(value) & 0xFF
+
+    def get_word_at(self, index: int) -> BitVec:
+        b = bytes(self[index: index + 32])
+        return symbol_factory.BitVecVal(int.from_bytes(b, "big"), 256)
+
+    def write_word_at(self, index: int, value) -> None:
+        v = concrete(value).to_bytes(32, "big")
+        for k in range(32):
+            self[index + k] = v[k]
+
+    def raw(self) -> bytes:
+        return bytes(self._m)
+
+
+class MachineState:
+    """machine_state.py:95-231 (concrete): pc is an instruction INDEX."""
+
+    def __init__(self, gas_limit: int = MSTATE_GAS_LIMIT, pc: int = 0, stack=None, memory=None,
+                 depth: int = 0, max_gas_used: int = 0, min_gas_used: int = 0):
+        self.pc = pc
+        self.stack = MachineStack(stack)
+        self.memory = memory if memory is not None else Memory()
+        self.gas_limit = gas_limit
+        self.min_gas_used = min_gas_used
+        self.max_gas_used = max_gas_used
+        self.depth = depth
+
+    @property
+    def memory_size(self) -> int:
+        return len(self.memory)
+
+    def pop(self, amount: int = 1):
+        if amount > len(self.stack):
+            raise StackUnderflowException
+        values = self.stack[-amount:][::-1]
+        del self.stack[-amount:]
+        return values[0] if amount == 1 else values
+
+    def __copy__(self):
+        return MachineState(self.gas_limit, self.pc, list(self.stack), Memory(self.memory.raw()),
+                            self.depth, self.max_gas_used, self.min_gas_used)
+
+    __deepcopy__ = lambda self, memo=None: self.__copy__()  # noqa: E731
+
+
+# --------------------------------------------------------------- accounts
+class Storage:
+    """account.py:18-99 for concrete storage (K(256,256,0) + stores): absent keys read 0."""
+
+    def __init__(self, concrete: bool = True, address=None, slots: Optional[Dict[int, int]] = None):
+        self.concrete = concrete
+        self.address = address
+        self.printable_storage: Dict[int, int] = dict(slots or {})
+
+    def __getitem__(self, item) -> BitVec:
+        return symbol_factory.BitVecVal(self.printable_storage.get(concrete(item), 0), 256)
+
+    def __setitem__(self, key, value) -> None:
+        self.printable_storage[concrete(key)] = concrete(value)
+
+    def items(self):
+        return self.printable_storage.items()
+
+    def __copy__(self):
+        return Storage(self.concrete, self.address, self.printable_storage)
+
+
+class Account:
+    """account.py:102-228 (concrete)."""
+
+    def __init__(self, address, code: Optional[Disassembly] = None, contract_name: str = None,
+                 balances=None, concrete_storage: bool = True, dynamic_loader=None, nonce: int = 0):
+        self.address = symbol_factory.BitVecVal(concrete(address), 256) if not isinstance(
+            address, BitVec) else address
+        self.nonce = nonce
+        self.code = code or Disassembly("")
+        self.contract_name = contract_name
+        self.storage = Storage(concrete_storage, address=self.address)
+        self._balance = 0
+
+    def set_balance(self, balance) -> None:
+        self._balance = concrete(balance)
+
+    def add_balance(self, balance) -> None:
+        self._balance = (self._balance + concrete(balance)) & M256
+
+    def balance(self) -> BitVec:
+        return symbol_factory.BitVecVal(self._balance, 256)
+
+    def __copy__(self):
+        a = Account(self.address, self.code, self.contract_name, nonce=self.nonce)
+        a.storage = copy(self.storage)
+        a._balance = self._balance
+        return a
+
+
+class WorldState:
+    """world_state.py:18-242 (concrete accounts; constraints stay empty for
+    concrete paths)."""
+
+    def __init__(self, transaction_sequence=None, annotations=None, constraints=None):
+        self._accounts: Dict[int, Account] = {}
+        self.constraints = list(constraints or [])
+        self.transaction_sequence = list(transaction_sequence or [])
+        self._annotations = list(annotations or [])
+        self.node = None
+
+    @property
+    def accounts(self) -> Dict[int, Account]:
+        return self._accounts
+
+    def put_account(self, account: Account) -> None:
+        self._accounts[concrete(account.address)] = account
+
+    def __getitem__(self, item) -> Account:
+        return self._accounts[concrete(item)]
+
+    def __copy__(self):
+        w = WorldState(self.transaction_sequence, self._annotations, self.constraints)
+        for k, a in self._accounts.items():
+            w._accounts[k] = copy(a)
+        w.node = self.node
+        return w
+
+    @property
+    def annotations(self):
+        return self._annotations
+
+    def annotate(self, annotation) -> None:
+        self._annotations.append(annotation)
+
+    def get_annotations(self, annotation_type: type):
+        return filter(lambda x: isinstance(x, annotation_type), self._annotations)
+
+
+class Environment:
+    """environment.py:12-60 (concrete words)."""
+
+    def __init__(self, active_account: Account, sender, calldata: bytes, gasprice, callvalue, origin,
+                 basefee=0, code: Optional[Disassembly] = None, static: bool = False):
+        self.active_account = active_account
+        self.active_function_name = ""
+        self.address = active_account.address
+        self.code = active_account.code if code is None else code
+        self.sender = sender if isinstance(sender, BitVec) else symbol_factory.BitVecVal(concrete(sender), 256)
+        self.calldata = bytes(calldata)
+        self.gasprice = gasprice if isinstance(gasprice, BitVec) else symbol_factory.BitVecVal(
+            concrete(gasprice), 256)
+        self.callvalue = callvalue if isinstance(callvalue, BitVec) else symbol_factory.BitVecVal(
+            concrete(callvalue), 256)
+        self.origin = origin if isinstance(origin, BitVec) else symbol_factory.BitVecVal(concrete(origin), 256)
+        self.basefee = basefee
+        self.static = static
+
+    def __copy__(self):
+        e = Environment(self.active_account, self.sender, self.calldata, self.gasprice, self.callvalue,
+                        self.origin, self.basefee, self.code, self.static)
+        e.active_function_name = self.active_function_name
+        return e
+
+
+# --------------------------------------------------------------- global state
+class GlobalState:
+    """global_state.py:18-163: one path.  ``lane`` is the host-side handle of the
+    device lane this state is mirrored into during LaserEVM.exec."""
+
+    def __init__(self, world_state: WorldState, environment: Environment, node=None,
+                 machine_state: Optional[MachineState] = None, transaction_stack=None,
+                 last_return_data=None, annotations=None):
+        self.node = node
+        self.world_state = world_state
+        self.environment = environment
+        self.mstate = machine_state if machine_state else MachineState(gas_limit=MSTATE_GAS_LIMIT)
+        self.transaction_stack = transaction_stack if transaction_stack else []
+        self.op_code = ""
+        self.last_return_data = last_return_data
+        self._annotations = annotations or []
+        self.lane_steps = 0          # instructions executed on the device in this exec()
+
+    def add_annotations(self, annotations: List) -> None:
+        self._annotations += annotations
+
+    def __copy__(self) -> "GlobalState":
+        world_state = copy(self.world_state)
+        environment = copy(self.environment)
+        environment.active_account = world_state[concrete(environment.active_account.address)]
+        g = GlobalState(world_state, environment, self.node, copy(self.mstate),
+                        transaction_stack=copy(self.transaction_stack),
+                        last_return_data=self.last_return_data,
+                        annotations=[copy(a) for a in self._annotations])
+        g.lane_steps = self.lane_steps
+        return g
+
+    @property
+    def accounts(self) -> Dict:
+        return self.world_state._accounts
+
+    def get_current_instruction(self) -> Dict:
+        return self.environment.code.instruction_list[self.mstate.pc]
+
+    @property
+    def instruction(self) -> Dict:
+        return self.get_current_instruction()
+
+    @property
+    def current_transaction(self):
+        try:
+            return self.transaction_stack[-1][0]
+        except IndexError:
+            return None
+
+    @property
+    def annotations(self) -> List:
+        return self._annotations
+
+    def annotate(self, annotation) -> None:
+        self._annotations.append(annotation)
+        if getattr(annotation, "persist_to_world_state", False):
+            self.world_state.annotate(annotation)
+
+    def get_annotations(self, annotation_type: type):
+        return filter(lambda x: isinstance(x, annotation_type), self.annotations)
+
+
+Word = Union[int, BitVec]

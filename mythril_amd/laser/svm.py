@@ -1,0 +1,605 @@
+"""LaserEVM for the MI355X batched core — the drop-in for the reference's
+``LaserEVM.exec`` / ``execute_state`` loop (laser/ethereum/svm.py:293-491).
+
+Same constructor arguments, same hook API (``register_hooks``,
+``register_laser_hooks``, ``register_instr_hooks``, ``laser_hook``, ``pre_hook``,
+``post_hook``, ``instr_hook``; the 11 laser hook types of svm.py:128-140), same
+``exec(create, track_gas)`` contract, same ``open_states`` / ``work_list`` /
+``total_states`` bookkeeping.  What differs is who steps the paths: every state
+of the work list becomes one lane of kernel 1 (libmythgpu.so); the host only
+sees a path when the reference would run host code for it:
+
+* before an opcode that has an svm pre/post hook or an instruction hook
+  (the lane stops with MG_HOOK; hooks fire on the materialised GlobalState;
+  the lane resumes with MG_LANE_HOOK_ACK and, when post hooks exist,
+  MG_LANE_STEP1 so they fire on the successor);
+* when the path ends (STOP/RETURN/REVERT/past-the-end/VmException/dropped
+  JUMPI): ``transaction_end`` hooks, ``_add_world_state``, ``final_states``;
+* when the opcode needs semantics outside the concrete subset (MG_ESCAPE):
+  the state is handed to ``escape_handler`` (in an integration, the
+  reference's own ``execute_state``); without one it is dropped exactly as
+  svm.py:314-316 drops a NotImplementedError.
+
+Event order.  The reference pops one state per iteration; for concrete paths
+(one successor each) BFS advances every path one instruction per round and DFS
+runs the newest path to its end first.  Kernel 1 runs the paths independently,
+so the host re-serialises the events: under BFS it delivers them by
+(instruction round, work-list position), pausing lanes at a step horizon
+(``mg_step_until``) so no path runs past an undelivered earlier event; under
+DFS by (reverse position, round).  Hooks therefore fire in the reference's
+order, and ``open_states`` / ``final_states`` come out in the reference's
+order.  Hook-free paths run in one launch.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from collections import defaultdict
+from copy import copy
+from datetime import datetime, timedelta
+from typing import Callable, DefaultDict, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
+                     MG_ESC_STACK, MG_ESC_STORAGE, MG_EXC_STACK_UNDERFLOW, MG_HALT_DROPPED,
+                     MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
+                     MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
+                     limbs_to_word, word_to_limbs)
+from ..smt.expr import symbol_factory
+from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
+from .signals import PluginSkipState, PluginSkipWorldState
+from .state import GlobalState, Memory, MachineStack, concrete
+from .strategy import DepthFirstSearchStrategy
+
+log = logging.getLogger(__name__)
+
+_EXECUTED_HALTS = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT, MG_VMEXC, MG_HALT_DROPPED)
+_INF = float("inf")
+_NO_GAS_LIMIT = (1 << 64) - 1
+
+
+class _Lane:
+    __slots__ = ("state", "pos", "phase", "dirty")
+
+    def __init__(self, state: GlobalState, pos: int):
+        self.state = state
+        self.pos = pos
+        self.phase = "run"        # run (on device) | event | paused | done
+        self.dirty = False        # host image changed, upload before the next launch
+
+
+class LaserEVM:
+    """The LASER engine with kernel 1 stepping every path of the work list."""
+
+    def __init__(self, dynamic_loader=None, max_depth=float("inf"), execution_timeout=60,
+                 create_timeout=10, strategy=DepthFirstSearchStrategy, transaction_count=2,
+                 requires_statespace=True, iprof=None, use_reachability_check=True,
+                 beam_width=None, device=None, escape_handler: Optional[Callable] = None):
+        self.execution_info: List = []
+        self.open_states: List = []
+        self.total_states = 0
+        self.dynamic_loader = dynamic_loader
+        self.use_reachability_check = use_reachability_check
+
+        self.work_list: List[GlobalState] = []
+        self.strategy = strategy(self.work_list, max_depth, beam_width=beam_width)
+        self.max_depth = max_depth
+        self.transaction_count = transaction_count
+
+        self.execution_timeout = execution_timeout or 0
+        self.create_timeout = create_timeout or 0
+
+        # the statespace graph (cfg.py nodes/edges) is not built by the batched
+        # core; a caller that needs it keeps the reference's host loop
+        self.requires_statespace = requires_statespace
+        self.nodes: Dict = {}
+        self.edges: List = []
+
+        self.time: Optional[datetime] = None
+        self.executed_transactions = False
+
+        self.pre_hooks: DefaultDict[str, List[Callable]] = defaultdict(list)
+        self.post_hooks: DefaultDict[str, List[Callable]] = defaultdict(list)
+
+        self._add_world_state_hooks: List[Callable] = []
+        self._execute_state_hooks: List[Callable] = []
+        self._start_exec_trans_hooks: List[Callable] = []
+        self._stop_exec_trans_hooks: List[Callable] = []
+        self._start_sym_trans_hooks: List[Callable] = []
+        self._stop_sym_trans_hooks: List[Callable] = []
+        self._start_sym_exec_hooks: List[Callable] = []
+        self._stop_sym_exec_hooks: List[Callable] = []
+        self._start_exec_hooks: List[Callable] = []
+        self._stop_exec_hooks: List[Callable] = []
+        self._transaction_end_hooks: List[Callable] = []
+
+        self.iprof = iprof
+        self.instr_pre_hook: Dict[str, List[Callable]] = {op: [] for op in OPCODES}
+        self.instr_post_hook: Dict[str, List[Callable]] = {op: [] for op in OPCODES}
+        self.hook_type_map = {
+            "start_execute_transactions": self._start_exec_trans_hooks,
+            "stop_execute_transactions": self._stop_exec_trans_hooks,
+            "add_world_state": self._add_world_state_hooks,
+            "execute_state": self._execute_state_hooks,
+            "start_sym_exec": self._start_sym_exec_hooks,
+            "stop_sym_exec": self._stop_sym_exec_hooks,
+            "start_sym_trans": self._start_sym_trans_hooks,
+            "stop_sym_trans": self._stop_sym_trans_hooks,
+            "start_exec": self._start_exec_hooks,
+            "stop_exec": self._stop_exec_hooks,
+            "transaction_end": self._transaction_end_hooks,
+        }
+        # batched-core specifics
+        self._device = device
+        self.escape_handler = escape_handler
+        self.record_coverage = False        # set by the coverage plugin
+        self.lane_steps = 0                 # device instructions executed by exec()
+        self.launches = 0
+        self._code_ids: Dict[bytes, int] = {}
+        self._code_objs: Dict[bytes, object] = {}
+        # coverage the reference's execute_state hook records for states the
+        # device never executes (escaped, skipped by a pre hook)
+        self._host_cov: Dict[bytes, set] = defaultdict(set)
+        self._cap_grow = 1
+        log.info("LASER EVM (MI355X batched core) initialized")
+
+    # ------------------------------------------------------------- device
+    @property
+    def device(self):
+        if self._device is None:
+            from ..device import GpuDevice
+            self._device = GpuDevice(int(os.environ.get("LOCAL_RANK", "0")))
+        return self._device
+
+    def code_id(self, code) -> int:
+        raw = code.raw
+        cid = self._code_ids.get(raw)
+        if cid is None:
+            cid = self.device.load_code(raw)
+            self._code_ids[raw] = cid
+            self._code_objs[raw] = code
+        return cid
+
+    # ------------------------------------------------------------- strategy / timeouts
+    def extend_strategy(self, extension, **kwargs) -> None:
+        self.strategy = extension(self.strategy, **kwargs)
+
+    def _check_create_termination(self) -> bool:
+        if len(self.open_states) != 0:
+            return (self.create_timeout > 0 and self.time is not None
+                    and self.time + timedelta(seconds=self.create_timeout) <= datetime.now())
+        return self._check_execution_termination()
+
+    def _check_execution_termination(self) -> bool:
+        return (self.execution_timeout > 0 and self.time is not None
+                and self.time + timedelta(seconds=self.execution_timeout) <= datetime.now())
+
+    # ------------------------------------------------------------- exec
+    def exec(self, create=False, track_gas=False) -> Optional[List[GlobalState]]:
+        """svm.py:293-337: drain the work list; returns the final states when
+        track_gas, else None."""
+        final_states: List[GlobalState] = []
+        for hook in self._start_exec_hooks:
+            hook()
+        while True:
+            states = self.strategy.drain()
+            if not states:
+                break
+            leftover = self._run_batch(states, final_states, create, track_gas)
+            if leftover is not None:       # timeout: the reference returns at once
+                return final_states + leftover if track_gas else None
+        for hook in self._stop_exec_hooks:
+            hook()
+        return final_states if track_gas else None
+
+    def _add_world_state(self, global_state: GlobalState) -> None:
+        """svm.py:339-348."""
+        for hook in self._add_world_state_hooks:
+            try:
+                hook(global_state)
+            except PluginSkipWorldState:
+                return
+        self.open_states.append(global_state.world_state)
+
+    def execute_state(self, global_state: GlobalState) -> Tuple[List[GlobalState], Optional[str]]:
+        """svm.py:369-491 for one state: a one-lane batch stepped one
+        instruction on the device with the same hook protocol as exec()."""
+        saved = self.work_list[:]
+        del self.work_list[:]
+        final: List[GlobalState] = []
+        instrs = global_state.environment.code.instruction_list
+        op = instrs[global_state.mstate.pc]["opcode"] if global_state.mstate.pc < len(instrs) else None
+        self._run_batch([global_state], final, False, True, single_step=True)
+        successors = self.work_list[:]
+        self.work_list[:] = saved
+        return successors, op
+
+    # ------------------------------------------------------------- hooks API
+    def register_hooks(self, hook_type: str, hook_dict: Dict[str, List[Callable]]):
+        if hook_type == "pre":
+            entrypoint = self.pre_hooks
+        elif hook_type == "post":
+            entrypoint = self.post_hooks
+        else:
+            raise ValueError("Invalid hook type %s. Must be one of {pre, post}", hook_type)
+        for op_code, funcs in hook_dict.items():
+            entrypoint[op_code].extend(funcs)
+
+    def register_laser_hooks(self, hook_type: str, hook: Callable):
+        if hook_type in self.hook_type_map:
+            self.hook_type_map[hook_type].append(hook)
+        else:
+            raise ValueError(f"Invalid hook type {hook_type}")
+
+    def register_instr_hooks(self, hook_type: str, opcode: str, hook: Callable):
+        table = self.instr_pre_hook if hook_type == "pre" else self.instr_post_hook
+        if opcode is None:
+            for op in OPCODES:
+                table[op].append(hook(op))
+        else:
+            table[opcode].append(hook)
+
+    def instr_hook(self, hook_type, opcode) -> Callable:
+        def hook_decorator(func: Callable):
+            self.register_instr_hooks(hook_type, opcode, func)
+        return hook_decorator
+
+    def laser_hook(self, hook_type: str) -> Callable:
+        def hook_decorator(func: Callable):
+            self.register_laser_hooks(hook_type, func)
+            return func
+        return hook_decorator
+
+    def pre_hook(self, op_code: str) -> Callable:
+        def hook_decorator(func: Callable):
+            self.pre_hooks[op_code].append(func)
+            return func
+        return hook_decorator
+
+    def post_hook(self, op_code: str) -> Callable:
+        def hook_decorator(func: Callable):
+            self.post_hooks[op_code].append(func)
+            return func
+        return hook_decorator
+
+    def _execute_pre_hook(self, op_code: str, global_state: GlobalState) -> None:
+        for hook in self.pre_hooks.get(op_code, ()):
+            hook(global_state)
+
+    def _execute_post_hook(self, op_code: str, global_states: List[GlobalState]) -> None:
+        for hook in self.post_hooks.get(op_code, ()):
+            for global_state in list(global_states):
+                try:
+                    hook(global_state)
+                except PluginSkipState:
+                    global_states.remove(global_state)
+
+    def _hooked_ops(self):
+        """Opcode bytes the device must stop before: any svm pre/post hook or
+        instruction pre/post hook; all of them when execute_state hooks exist."""
+        if self._execute_state_hooks:
+            return set(range(256))
+        ops = set()
+        for table in (self.pre_hooks, self.post_hooks, self.instr_pre_hook, self.instr_post_hook):
+            for name, hooks in table.items():
+                if hooks and name in OPCODES:
+                    ops.add(OPCODES[name])
+        return ops
+
+    def _has_post(self, name: str) -> bool:
+        return bool(self.post_hooks.get(name) or self.instr_post_hook.get(name)
+                    or self._execute_state_hooks)
+
+    # ------------------------------------------------------------- lanes
+    def _shape(self, states: List[GlobalState]) -> LaneShape:
+        n = len(states)
+        g = self._cap_grow
+        msz = max((len(s.mstate.memory) for s in states), default=0)
+        slots = max((len(s.environment.active_account.storage.printable_storage) for s in states),
+                    default=0)
+        cdl = max((len(s.environment.calldata) for s in states), default=0)
+        stack_cap = 1024 if n <= 4096 else min(1024, 128 * g)
+        mem_cap = max(4096 * g, 2 * msz)
+        mem_cap = min(mem_cap, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
+        mem_cap = max(mem_cap, (msz + 31) // 32 * 32)
+        mem_cap = (mem_cap + 31) // 32 * 32
+        return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
+                         calldata_cap=max((cdl + 31) // 32 * 32, 32),
+                         storage_cap=max(64 * g, 2 * slots + 16))
+
+    def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
+        env, ms = s.environment, s.mstate
+        tx = s.current_transaction
+        gas_limit = getattr(tx, "gas_limit", None)
+        b.code_id[i] = self.code_id(env.code)
+        b.pc[i] = ms.pc
+        stack = [concrete(x) for x in ms.stack]
+        b.sp[i] = len(stack)
+        b.stack[i] = 0
+        if stack:
+            b.stack[i, : len(stack)] = np.array(
+                [np.frombuffer(w.to_bytes(32, "little"), dtype="<u4") for w in stack])
+        mem = ms.memory.raw()
+        b.msize[i] = len(mem)
+        b.memory[i] = 0
+        b.memory[i, : len(mem)] = np.frombuffer(mem, dtype=np.uint8)
+        b.depth[i] = ms.depth
+        b.status[i] = MG_RUNNING
+        b.aux[i] = 0
+        b.flags[i] = MG_LANE_STATIC if env.static else 0
+        b.gas_min[i] = ms.min_gas_used
+        b.gas_max[i] = ms.max_gas_used
+        b.gas_limit[i] = _NO_GAS_LIMIT if gas_limit is None else min(concrete(gas_limit), _NO_GAS_LIMIT)
+        cd = env.calldata
+        b.calldata[i] = 0
+        b.calldata[i, : len(cd)] = np.frombuffer(cd, dtype=np.uint8)
+        b.calldata_len[i] = len(cd)
+        words = (env.address, env.sender, env.origin, env.callvalue, env.gasprice)
+        for k in range(MG_ENV_WORDS):
+            b.env[i, k] = word_to_limbs(concrete(words[k]))
+        slots = list(env.active_account.storage.printable_storage.items())
+        b.storage[i] = 0
+        for k, (key, val) in enumerate(slots):
+            b.storage[i, k, :8] = word_to_limbs(key)
+            b.storage[i, k, 8:] = word_to_limbs(val)
+        b.storage_count[i] = len(slots)
+        b.ret_offset[i] = b.ret_len[i] = 0
+
+    def _materialise(self, b: LaneBatch, i: int, s: GlobalState) -> GlobalState:
+        """Write lane i of the host image back into its GlobalState (in place)."""
+        ms = s.mstate
+        ms.pc = int(b.pc[i])
+        sp = int(b.sp[i])
+        ms.stack = MachineStack([symbol_factory.BitVecVal(limbs_to_word(b.stack[i, k]), 256)
+                                 for k in range(sp)])
+        ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
+        ms.depth = int(b.depth[i])
+        ms.min_gas_used = int(b.gas_min[i])
+        ms.max_gas_used = int(b.gas_max[i])
+        store = s.environment.active_account.storage.printable_storage
+        store.clear()
+        for k in range(int(b.storage_count[i])):
+            store[limbs_to_word(b.storage[i, k, :8])] = limbs_to_word(b.storage[i, k, 8:])
+        s.lane_steps = int(b.steps[i])
+        return s
+
+    # ------------------------------------------------------------- the batch loop
+    def _run_batch(self, states: List[GlobalState], final_states: List[GlobalState], create: bool,
+                   track_gas: bool, single_step: bool = False):
+        dev = self.device
+        n = len(states)
+        shape = self._shape(states)
+        b = LaneBatch(shape)
+        lanes = [_Lane(s, i) for i, s in enumerate(states)]
+        for i, s in enumerate(states):
+            self._pack(b, i, s)
+            b.steps[i] = 0
+        dev.alloc(shape, coverage=self.record_coverage)
+        dev.upload(b)
+        mask = _mask(self._hooked_ops())
+        depth = 0 if self.max_depth == _INF else int(self.max_depth)
+        bfs = getattr(self.strategy, "order", "bfs") == "bfs"
+        regrow: List[GlobalState] = []
+
+        def launch(run: List[int], horizon: int):
+            for ln in lanes:
+                if ln.dirty:
+                    dev.upload_range(b, ln.pos, 1)
+                    ln.dirty = False
+            st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
+                          horizon=horizon)
+            self.launches += 1
+            self.lane_steps += st.lane_steps
+            self.total_states += st.lane_steps      # one successor per executed step
+            for lo, cnt in _ranges(run):
+                dev.download_range(b, lo, cnt)
+            for i in run:
+                lanes[i].phase = "paused" if b.status[i] == MG_RUNNING else "event"
+
+        launch(list(range(n)), 0)
+        while True:
+            if (create and self._check_create_termination()) or (
+                    not create and self._check_execution_termination()):
+                left = [self._materialise(b, ln.pos, ln.state) for ln in lanes
+                        if ln.phase != "done"]
+                return left
+            ev = _next_event(lanes, b, bfs)
+            paused = [ln.pos for ln in lanes if ln.phase == "paused"]
+            if single_step:
+                for i in paused:
+                    ln = lanes[i]
+                    self._materialise(b, i, ln.state)
+                    self.work_list.append(ln.state)
+                    ln.phase = "done"
+                paused = []
+            if ev is None and not paused:
+                break
+            if paused:
+                if bfs:
+                    # paused paths might have events at or before ev's round
+                    p_min = min(int(b.steps[i]) for i in paused)
+                    if ev is None or p_min <= _event_round(b, ev):
+                        launch(paused, 0 if ev is None else _event_round(b, ev) + 1)
+                        continue
+                elif ev is None or max(paused) > ev:
+                    launch(paused, 0)           # DFS: the newest path runs on first
+                    continue
+            self._deliver(lanes[ev], b, final_states, track_gas, launch, regrow, single_step)
+        if regrow:
+            self._cap_grow *= 4
+            self.work_list.extend(regrow)
+        return None
+
+    def _deliver(self, ln: _Lane, b: LaneBatch, final_states, track_gas, launch, regrow,
+                 single_step: bool = False):
+        """Run the host side of one device event, as execute_state would."""
+        i, s = ln.pos, ln.state
+        status = int(b.status[i])
+        self._materialise(b, i, s)
+        instrs = s.environment.code.instruction_list
+        name = instrs[s.mstate.pc]["opcode"] if s.mstate.pc < len(instrs) else None
+        ln.phase = "done"
+        if self.record_coverage and status in (MG_HOOK, MG_ESCAPE) and name is not None:
+            self._host_cov[s.environment.code.raw].add(s.mstate.pc)
+
+        if status in _EXECUTED_HALTS:
+            self.total_states -= 1                  # the halting step had no successor
+        if status == MG_HOOK:
+            # execute_state returning [] puts the popped state in final_states
+            # when track_gas (svm.py:328-334), whatever the reason
+            try:
+                for hook in self._execute_state_hooks:
+                    hook(s)
+            except PluginSkipState:
+                if track_gas:
+                    final_states.append(s)
+                return
+            if len(s.mstate.stack) < get_required_stack_elements(name):
+                # svm.py:391-402: precheck underflow -- no pre hooks, no tx-end hooks
+                if track_gas:
+                    final_states.append(s)
+                return
+            try:
+                self._execute_pre_hook(name, s)
+            except PluginSkipState:
+                if track_gas:
+                    final_states.append(s)
+                return
+            pre_state = s
+            for hook in self.instr_pre_hook.get(name, ()):
+                hook(s)
+            post = self._has_post(name) or single_step
+            # hooks may have rewritten the state: repack, then run the hooked
+            # instruction alone (STEP1) when post hooks must see its successor
+            steps = int(b.steps[i])
+            self._pack(b, i, s)
+            b.steps[i] = steps
+            b.flags[i] |= MG_LANE_HOOK_ACK | (MG_LANE_STEP1 if post else 0)
+            if not post:
+                ln.phase, ln.dirty = "paused", True
+                return
+            ln.dirty = True
+            snapshot = copy(pre_state)
+            launch([i], steps + 1)
+            st2 = int(b.status[i])
+            b.flags[i] = int(b.flags[i]) & ~(MG_LANE_HOOK_ACK | MG_LANE_STEP1) & 0xFFFFFFFF
+            ln.dirty = True
+            executed = int(b.steps[i]) == steps + 1
+            if st2 in _EXECUTED_HALTS:
+                if st2 == MG_HALT_DROPPED:
+                    for hook in self.instr_post_hook.get(name, ()):
+                        hook(snapshot)
+                ln.phase = "event"
+                self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
+                return
+            if not executed:      # escaped or cut by depth before running: its own event
+                ln.phase = "event"
+                self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
+                return
+            for hook in self.instr_post_hook.get(name, ()):
+                hook(snapshot)
+            new = self._materialise(b, i, s)
+            successors = [new]
+            self._execute_post_hook(name, successors)
+            if not successors:
+                ln.phase = "done"
+                if track_gas:
+                    final_states.append(snapshot)
+                return
+            ln.phase = "paused" if st2 == MG_RUNNING else "event"
+            return
+
+        tx = s.current_transaction
+        if status in (MG_HALT_STOP, MG_HALT_RETURN):
+            if status == MG_HALT_RETURN and tx is not None:
+                tx.return_data = _return_data(b, i)
+            for hook in self._transaction_end_hooks:
+                hook(s, tx, None, False)
+            self._add_world_state(s)
+        elif status == MG_HALT_REVERT:
+            if tx is not None:
+                tx.return_data = _return_data(b, i)
+            for hook in self._transaction_end_hooks:
+                hook(s, tx, None, True)
+        elif status == MG_HALT_END:
+            self._add_world_state(s)
+        elif status == MG_VMEXC:
+            precheck = (int(b.aux[i]) == MG_EXC_STACK_UNDERFLOW and name is not None
+                        and len(s.mstate.stack) < get_required_stack_elements(name))
+            if not precheck:
+                for hook in self._transaction_end_hooks:
+                    hook(s, tx, None, False)
+        elif status == MG_HALT_DROPPED:
+            pass
+        elif status == MG_DEPTH:
+            return                  # the strategy skips it: not a final state
+        elif status == MG_ESCAPE:
+            reason = int(b.aux[i]) >> 8
+            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK):
+                regrow.append(s)    # rerun with larger lane capacities
+                return
+            if self.escape_handler is None:
+                log.debug("Encountered unimplemented instruction %s", name)
+                return              # svm.py:314-316: NotImplementedError -> continue
+            new_states = self.escape_handler(s)
+            self.work_list.extend(new_states)
+            self.total_states += len(new_states)
+            if new_states or not track_gas:
+                return
+        if track_gas:
+            final_states.append(s)
+
+
+    # ------------------------------------------------------------- coverage
+    def coverage(self) -> Dict[object, Tuple[int, List[bool]]]:
+        """coverage_plugin.py's table {bytecode: (n_instructions, [covered])} from
+        the device's per-code coverage bytes (plus host-recorded marks)."""
+        out = {}
+        for raw, cid in self._code_ids.items():
+            bits = self.device.coverage(cid).astype(bool)
+            for pc in self._host_cov.get(raw, ()):
+                if pc < bits.size:
+                    bits[pc] = True
+            out[self._code_objs[raw].bytecode] = (int(bits.size), bits.tolist())
+        return out
+
+
+def _mask(ops) -> List[int]:
+    m = [0, 0, 0, 0]
+    for o in ops:
+        m[o >> 6] |= 1 << (o & 63)
+    return m
+
+
+def _ranges(idx: List[int]):
+    idx = sorted(idx)
+    out = []
+    for i in idx:
+        if out and out[-1][0] + out[-1][1] == i:
+            out[-1][1] += 1
+        else:
+            out.append([i, 1])
+    return out
+
+
+def _event_round(b: LaneBatch, i: int) -> int:
+    st = int(b.status[i])
+    s = int(b.steps[i])
+    return s - 1 if st in _EXECUTED_HALTS else s
+
+
+def _next_event(lanes: List[_Lane], b: LaneBatch, bfs: bool) -> Optional[int]:
+    best, key = None, None
+    for ln in lanes:
+        if ln.phase != "event":
+            continue
+        r = _event_round(b, ln.pos)
+        k = (r, ln.pos) if bfs else (-ln.pos, r)
+        if key is None or k < key:
+            best, key = ln.pos, k
+    return best
+
+
+def _return_data(b: LaneBatch, i: int) -> bytes:
+    return b.return_data(i)

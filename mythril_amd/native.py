@@ -87,6 +87,7 @@ SIGNATURES = {
     "mg_lanes_reset": (_I, [_P]),
     "mg_step": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_async": (_I, [_P, _P, _U32, _U32]),
+    "mg_step_until": (_I, [_P, _P, _U32, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_profile": (_I, [_P, _P, _U32, _U32, _P, _P]),
     "mg_sync": (_I, [_P]),
     "mg_coverage": (_I, [_P, _U32, _P, _U32]),

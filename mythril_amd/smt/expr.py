@@ -16,9 +16,12 @@ bitvec.py:63-136 does; they never reach the device.
 """
 from __future__ import annotations
 
-from typing import Dict, Iterable, Optional, Tuple
+import weakref
+from typing import Iterable, Optional, Tuple
 
-_INTERN: Dict[tuple, "Node"] = {}
+# weak: a node lives while an expression (or a parent node) holds it, so the
+# table does not grow with every concrete value the host layer materialises
+_INTERN: "weakref.WeakValueDictionary[tuple, Node]" = weakref.WeakValueDictionary()
 
 
 class Node:

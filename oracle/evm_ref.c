@@ -204,6 +204,7 @@ typedef struct {
     uint64_t hook_mask[4];
     uint32_t max_steps;
     uint32_t max_depth;     /* 0 = unlimited */
+    uint32_t horizon;       /* stop when the lane's cumulative steps reach it; 0 = none */
 } orc_params;
 
 typedef struct {       /* working view of one lane */
@@ -318,11 +319,12 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         const uint32_t pc = h->pc[i];
         if (pc >= c->n_instr) { h->status[i] = MG_HALT_END; break; }
         const uint8_t op = c->op[pc];
-        if ((p->hook_mask[op >> 6] >> (op & 63)) & 1) {
+        const uint32_t flags = h->flags[i];
+        if (((p->hook_mask[op >> 6] >> (op & 63)) & 1) && !((flags & MG_LANE_HOOK_ACK) && done == 0)) {
             h->status[i] = MG_HOOK; h->aux[i] = op; break;
         }
-        if (done >= p->max_steps) break;
-        const uint32_t flags = h->flags[i];
+        if (done >= p->max_steps || ((flags & MG_LANE_STEP1) && done >= 1) ||
+            (p->horizon && h->steps[i] >= p->horizon)) break;
         if (is_env_escape(op) ||
             ((flags & MG_LANE_CREATION) && op >= 0x35 && op <= 0x39)) {
             /* creation lanes: CALLDATALOAD/SIZE/COPY and CODESIZE/COPY follow the
@@ -615,18 +617,23 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
 }
 
 /* Step lanes [first, first+n) of a host image.  Returns the lane-steps. */
-uint64_t orc_run(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
-                 uint32_t max_steps, uint32_t max_depth) {
+uint64_t orc_run_until(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
+                       uint32_t max_steps, uint32_t max_depth, uint32_t horizon) {
     init_optable();
     orc_params p;
     memcpy(p.hook_mask, hook_mask, sizeof p.hook_mask);
-    p.max_steps = max_steps; p.max_depth = max_depth;
+    p.max_steps = max_steps; p.max_depth = max_depth; p.horizon = horizon;
     uint64_t total = 0;
     for (uint32_t i = first; i < first + n; ++i) {
         if (h->code_id[i] >= (uint32_t)n_codes) { h->status[i] = MG_ESCAPE; continue; }
         total += run_lane(h, i, &p);
     }
     return total;
+}
+
+uint64_t orc_run(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
+                 uint32_t max_steps, uint32_t max_depth) {
+    return orc_run_until(h, first, n, hook_mask, max_steps, max_depth, 0);
 }
 
 /* Multi-threaded driver for the CPU baseline: one pthread per core over

@@ -43,8 +43,9 @@ class OracleEVM:
 
     def run(self, batch, first: int = 0, n: Optional[int] = None,
             hook_mask: Sequence[int] = (0, 0, 0, 0), max_steps: int = 1 << 30,
-            max_depth: int = 0) -> int:
+            max_depth: int = 0, horizon: int = 0) -> int:
         n = batch.n - first if n is None else n
         mask = (ctypes.c_uint64 * 4)(*[int(x) for x in hook_mask])
         soa = batch.soa()
-        return int(lib().orc_run(ctypes.addressof(soa), first, n, mask, max_steps, max_depth))
+        return int(lib().orc_run_until(ctypes.addressof(soa), first, n, mask, max_steps, max_depth,
+                                       horizon))
