@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 1u
+#define MG_ABI_VERSION 2u   /* 2: model tables (arrays, uninterpreted functions) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -223,11 +223,25 @@ typedef struct mg_dag_batch {
 
 /* Candidate models, most-recently-used first (LRU order of
  * support_utils.py:62-63).  Variables absent from a model take 0
- * (z3 model_completion).                                  */
+ * (z3 model_completion).
+ *
+ * Tables are the models' interpretations of symbolic arrays (storage,
+ * calldata, balances: array.py) and uninterpreted functions (keccak256_N and
+ * its inverse, Power: function.py), looked up by the program op BV_TAB.  For
+ * table t and model m, entries [tab_start[t][m], + tab_count[t][m]) of
+ * tab_entries hold (key k0: 8 limbs, key k1: 8 limbs, value: 16 limbs, i.e. up
+ * to 512 bits); a key not listed takes tab_default[t][m] (array default /
+ * function else value).                                                     */
 typedef struct mg_model_batch {
     uint32_t n_models;
     uint32_t n_vars;
     const uint32_t *values;     /* [n_vars][n_models][8]                      */
+    uint32_t n_tables;          /* 0: no tables (pointers below ignored)      */
+    const uint32_t *tab_start;  /* [n_tables][n_models]                       */
+    const uint32_t *tab_count;  /* [n_tables][n_models]                       */
+    const uint32_t *tab_entries;/* [n_entries][32]                            */
+    uint32_t n_entries;
+    const uint32_t *tab_default;/* [n_tables][n_models][16]                   */
 } mg_model_batch;
 
 /* first_sat_model[d] = smallest model index m (MRU order) whose evaluation of

@@ -39,6 +39,9 @@ enum BvOp : uint32_t {
     BV_MUL_NOOVF_U,    // bvumul_noovfl;        w3 = operand width
     BV_SUB_NOUDF_U,    // BVSubNoUnderflow unsigned: b <= a
     BV_NE,             // w3 = operand width
+    BV_TAB,            // A = key k0, B = key k1, w3 = table | part << 20 | lo << 21:
+                       // bits [256 part + lo, +width) of the model's array / function
+                       // interpretation at (k0, k1), else its default (lower.py)
     BV_NUM_OPS
 };
 
@@ -59,9 +62,15 @@ struct BvState {
     uint32_t *tile_dag = nullptr;    // [n_tiles + 1] first DAG of each tile
     uint4 *consts = nullptr;         // [n_consts][2]
     uint4 *values = nullptr;         // [n_vars][n_models][2]
+    uint32_t n_tables = 0, n_entries = 0;
+    uint32_t *tab_start = nullptr;   // [n_tables][n_models]
+    uint32_t *tab_count = nullptr;   // [n_tables][n_models]
+    uint4 *tab_entries = nullptr;    // [n_entries][8]: k0, k1, value (512 bits)
+    uint4 *tab_default = nullptr;    // [n_tables][n_models][4]
     uint32_t *first_sat = nullptr;   // [n_dags]
     uint32_t *sat_count = nullptr;   // [n_dags]
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
+    size_t cap_entries = 0;
     bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
     std::vector<uint32_t> h_tiles;
 };
@@ -96,12 +105,44 @@ DEV U256 bv_sext(U256 v, uint32_t width) {
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
+struct BvTables {
+    const uint32_t *__restrict__ start;
+    const uint32_t *__restrict__ count;
+    const uint4 *__restrict__ entries;
+    const uint4 *__restrict__ dflt;
+};
+
 struct BvCtx {
     const uint4 *__restrict__ values;
     const uint4 *__restrict__ consts;
     uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
     uint32_t n_models, model, tid;
+    BvTables tab;
 };
+
+DEV U256 ld2(const uint4 *p) {
+    const uint4 x = p[0], y = p[1];
+    U256 r;
+    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    return r;
+}
+
+// model interpretation lookup (entries are unique keys: first match wins)
+DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) {
+    const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
+    const size_t tm = (size_t)t * c.n_models + c.model;
+    const uint32_t s0 = c.tab.start[tm], cnt = c.tab.count[tm];
+    U256 v = ld2(c.tab.dflt + tm * 4u + part * 2u);
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const uint4 *e = c.tab.entries + (size_t)(s0 + k) * 8u;
+        if (u_eq(ld2(e), k0) && u_eq(ld2(e + 2), k1)) {
+            v = ld2(e + 4 + part * 2u);
+            break;
+        }
+    }
+    return lo ? u_shr_n(v, lo, 0u) : v;
+}
 
 DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
@@ -134,6 +175,7 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       const uint32_t *__restrict__ tile_dag,
                                                       const uint4 *__restrict__ consts,
                                                       const uint4 *__restrict__ values, uint32_t n_models,
+                                                      BvTables tab,
                                                       uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles,
                                                       uint32_t tiles_pad, uint32_t dag_lo, uint32_t dag_hi,
                                                       uint32_t tile_cap, uint32_t chunks_per_block,
@@ -167,7 +209,7 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
     const uint32_t model = chunk * BV_BLOCK + tid;
     const bool live = model < n_models;
-    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid};
+    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid, tab};
 
     for (uint32_t d = d0; d < d1; ++d) {
         const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
@@ -252,6 +294,7 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                     break;
                 }
                 case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
+                case BV_TAB: r = bv_table(c, A, B, rc); break;
                 default: r = u_zero(); break;
                 }
             }
@@ -288,6 +331,7 @@ static int bv_ensure(T *&p, size_t &cap, size_t need) {
 static void bv_free(BvState &s) {
     hipFree(s.insns); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.consts);
     hipFree(s.values); hipFree(s.first_sat); hipFree(s.sat_count);
+    hipFree(s.tab_start); hipFree(s.tab_count); hipFree(s.tab_entries); hipFree(s.tab_default);
     s = BvState{};
 }
 
@@ -308,6 +352,13 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         const uint32_t op = w[0] & 0xffu, width = (w[0] >> 8) & 0x1ffu;
         if (op >= BV_NUM_OPS || width == 0 || width > 256) { msg = "bad instruction " + std::to_string(i); return MG_EINVAL; }
         if (((w[0] >> 17) & 1u) && ((w[0] >> 18) & 0xfu) >= dags->n_slots) { msg = "slot out of range"; return MG_EINVAL; }
+        if (op == BV_TAB) {
+            const uint32_t imm = w[3], t = imm & 0xfffffu, lo = (imm >> 21) & 0xffu;
+            if (t >= models->n_tables || (imm >> 29) != 0u || lo + width > 256u) {
+                msg = "bad table reference at instruction " + std::to_string(i);
+                return MG_EINVAL;
+            }
+        }
         const int nref = (op == BV_ITE) ? 3 : (op == BV_COPY || op == BV_NOT || op == BV_NEG || op == BV_BNOT ||
                                                op == BV_EXTRACT || op == BV_ZEXT || op == BV_SEXT) ? 1 : 2;
         for (int k = 0; k < nref; ++k) {
@@ -341,6 +392,25 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     if ((rc = bv_ensure(s.tile_dag, s.cap_tiles, s.h_tiles.size()))) { msg = "alloc tiles"; return rc; }
     if ((rc = bv_ensure(s.consts, s.cap_consts, (size_t)std::max<uint32_t>(dags->n_consts, 1) * 2))) { msg = "alloc consts"; return rc; }
     if ((rc = bv_ensure(s.values, s.cap_values, (size_t)std::max<uint32_t>(models->n_vars, 1) * models->n_models * 2))) { msg = "alloc values"; return rc; }
+    if (models->n_tables) {
+        if (!models->tab_start || !models->tab_count || !models->tab_default ||
+            (models->n_entries && !models->tab_entries)) { msg = "table arrays missing"; return MG_EINVAL; }
+        const size_t tm = (size_t)models->n_tables * models->n_models;
+        for (size_t k = 0; k < tm; ++k)
+            if ((uint64_t)models->tab_start[k] + models->tab_count[k] > models->n_entries) {
+                msg = "table entries out of range"; return MG_EINVAL;
+            }
+        hipFree(s.tab_start); hipFree(s.tab_count); hipFree(s.tab_default);
+        s.tab_start = s.tab_count = nullptr;
+        s.tab_default = nullptr;
+        if (hipMalloc(&s.tab_start, tm * 4) != hipSuccess || hipMalloc(&s.tab_count, tm * 4) != hipSuccess ||
+            hipMalloc(&s.tab_default, tm * 64) != hipSuccess) {
+            msg = "alloc tables"; return MG_ENOMEM;
+        }
+        if ((rc = bv_ensure(s.tab_entries, s.cap_entries, (size_t)std::max<uint32_t>(models->n_entries, 1) * 8))) {
+            msg = "alloc table entries"; return rc;
+        }
+    }
     hipFree(s.first_sat); hipFree(s.sat_count);
     s.first_sat = s.sat_count = nullptr;
     if (hipMalloc(&s.first_sat, (size_t)n * 4) != hipSuccess || hipMalloc(&s.sat_count, (size_t)n * 4) != hipSuccess) {
@@ -354,8 +424,18 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     if (dags->n_consts) e = e ? e : hipMemcpyAsync(s.consts, dags->consts, (size_t)dags->n_consts * 32, hipMemcpyHostToDevice, st);
     if (models->n_vars)
         e = e ? e : hipMemcpyAsync(s.values, models->values, (size_t)models->n_vars * models->n_models * 32, hipMemcpyHostToDevice, st);
+    if (models->n_tables) {
+        const size_t tm = (size_t)models->n_tables * models->n_models;
+        e = e ? e : hipMemcpyAsync(s.tab_start, models->tab_start, tm * 4, hipMemcpyHostToDevice, st);
+        e = e ? e : hipMemcpyAsync(s.tab_count, models->tab_count, tm * 4, hipMemcpyHostToDevice, st);
+        e = e ? e : hipMemcpyAsync(s.tab_default, models->tab_default, tm * 64, hipMemcpyHostToDevice, st);
+        if (models->n_entries)
+            e = e ? e : hipMemcpyAsync(s.tab_entries, models->tab_entries, (size_t)models->n_entries * 128,
+                                       hipMemcpyHostToDevice, st);
+    }
     e = e ? e : hipStreamSynchronize(st);
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
+    s.n_tables = models->n_tables; s.n_entries = models->n_entries;
     const char *pv = getenv("MG_BV_PROG");
     s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
@@ -388,7 +468,8 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
     hipLaunchKernelGGL(lds_prog ? k_bv_eval<true> : k_bv_eval<false>, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
                        s.insns, s.prog_off, s.tile_dag,
-                       s.consts, s.values, s.n_models, s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
+                       s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
+                       s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
                        s.tile_cap, cpb, s.first_sat, s.sat_count);
     e = hipGetLastError();
     if (e != hipSuccess) { msg = std::string("k_bv_eval launch: ") + hipGetErrorString(e); return MG_EDEVICE; }

@@ -67,7 +67,10 @@ class MgDagBatch(ctypes.Structure):
 
 class MgModelBatch(ctypes.Structure):
     _fields_ = [("n_models", ctypes.c_uint32), ("n_vars", ctypes.c_uint32),
-                ("values", ctypes.c_void_p)]
+                ("values", ctypes.c_void_p), ("n_tables", ctypes.c_uint32),
+                ("tab_start", ctypes.c_void_p), ("tab_count", ctypes.c_void_p),
+                ("tab_entries", ctypes.c_void_p), ("n_entries", ctypes.c_uint32),
+                ("tab_default", ctypes.c_void_p)]
 
 
 # every symbol include/mythgpu.h declares: name -> (restype, argtypes)

@@ -359,3 +359,78 @@ class _SymbolFactory:
 
 
 symbol_factory = _SymbolFactory()
+
+
+# ----------------------------------------------------- arrays and functions
+# Array-sorted nodes have width 0 and carry (domain, range) widths in `param`:
+#   ("array", name, dom, rng)      symbolic array   (array.py:56-70 Array)
+#   K:     args (default,)         constant array   (array.py:73-86 K)
+#   store: args (array, index, value)
+# select(array, index) and uf(args...) are bit-vector nodes of the range width.
+def _select(arr: Node, idx: Node) -> Node:
+    """Select with the folding z3's simplify applies to concrete indices:
+    a store at an equal constant index answers, an unequal one is skipped, and
+    a K array answers its default."""
+    a = arr
+    while True:
+        if a.op == "store" and idx.op == "const" and a.args[1].op == "const":
+            if a.args[1].param == idx.param:
+                return a.args[2]
+            a = a.args[0]
+            continue
+        if a.op == "K":
+            if idx.op == "const":
+                return a.args[0]
+        break
+    return Node("select", a.param[-1], (a, idx))
+
+
+class BaseArray:
+    """array.py:14-53: ``arr[k]`` is Select, ``arr[k] = v`` replaces raw by Store."""
+
+    def __init__(self, raw: Node):
+        self.raw = raw
+
+    @property
+    def domain(self) -> int:
+        return self.raw.param[-2]
+
+    @property
+    def range(self) -> int:
+        return self.raw.param[-1]
+
+    def __getitem__(self, item) -> BitVec:
+        if isinstance(item, slice):
+            raise ValueError("Instance of BaseArray, does not support getitem with slices")
+        k = _bv(item, self.domain)
+        return BitVec(_select(self.raw, k.raw), k.annotations)
+
+    def __setitem__(self, key, value) -> None:
+        k = _bv(key, self.domain)
+        v = _bv(value, self.range)
+        self.raw = Node("store", 0, (self.raw, k.raw, v.raw), (self.domain, self.range))
+
+
+class Array(BaseArray):
+    def __init__(self, name: str, domain: int, value_range: int):
+        super().__init__(Node("array", 0, (), (name, domain, value_range)))
+
+
+class K(BaseArray):
+    def __init__(self, domain: int, value_range: int, value: int):
+        super().__init__(Node("K", 0, (const(value, value_range),), (domain, value_range)))
+
+
+class Function:
+    """function.py:7-29: an uninterpreted function over bit-vectors."""
+
+    def __init__(self, name: str, domain, value_range: int):
+        self.name = name
+        self.domain = list(domain)
+        self.range = value_range
+
+    def __call__(self, *items) -> BitVec:
+        args = tuple(_bv(x, w) for x, w in zip(items, self.domain))
+        return BitVec(Node("uf", self.range, tuple(a.raw for a in args),
+                           (self.name, tuple(self.domain), self.range)), _ann(*args))
+

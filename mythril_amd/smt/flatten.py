@@ -22,16 +22,13 @@ from typing import Dict, List, Sequence, Tuple
 import numpy as np
 
 from .expr import Bool, Node, TRUE
-from .program import (MAX_SLOTS, OPCODE, REF_ACC, REF_CONST, REF_SLOT, REF_VAR, TILE_INSNS,
-                      ProgramBatch, enc_w0, limbs, ref)
+from .lower import Lowering, Unsupported
+from .program import (MAX_SLOTS, OPCODE, REF_ACC, REF_CONST, REF_SLOT, REF_VAR, TAB_LO_SHIFT,
+                      TAB_PART_SHIFT, TILE_INSNS, ProgramBatch, enc_w0, limbs, ref)
 
 _MAP = {"and": "and", "or": "or", "not": "not", "xor": "xor", "implies": "implies"}
 _CMP = {"eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
         "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u"}
-
-
-class Unsupported(Exception):
-    pass
 
 
 class _Virt:
@@ -49,6 +46,9 @@ class Compiler:
         self.const_index: Dict[int, int] = {}
         self.consts: List[int] = []
         self.max_slots = 0
+        # arrays / functions / wide values -> 256-bit ops + table lookups (lower.py)
+        self.lowering = Lowering()
+        self.table_index: Dict[str, int] = {}
 
     # -- leaves ---------------------------------------------------------------
     def _leaf_ref(self, n: Node) -> int:
@@ -145,6 +145,13 @@ class Compiler:
             virts.append(_Virt("concat", x.width, [arg(x.args[0]), arg(x.args[1])], imm=x.args[1].width))
         elif op in _CMP:
             virts.append(_Virt(op, 1, [arg(x.args[0]), arg(x.args[1])], imm=x.args[0].width))
+        elif op == "tab":
+            name, part, lo = x.param
+            t = self.table_index.get(name)
+            if t is None:
+                t = self.table_index[name] = len(self.table_index)
+            virts.append(_Virt("tab", x.width, [arg(x.args[0]), arg(x.args[1])],
+                               imm=t | (part << TAB_PART_SHIFT) | (lo << TAB_LO_SHIFT)))
         elif op in OPCODE:
             virts.append(_Virt(op, x.width, [arg(c) for c in x.args]))
         else:
@@ -153,6 +160,7 @@ class Compiler:
 
     # -- slots + encoding -----------------------------------------------------
     def compile(self, root: Node) -> np.ndarray:
+        root = self.lowering.lower(root)
         virts = self._schedule(root)
         n = len(virts)
         uses: Dict[int, List[Tuple[int, int]]] = {}
@@ -191,7 +199,7 @@ class Compiler:
                 w[1 + k] = r
             if v.op in ("extract", "sign_extend"):
                 w[2] = v.imm
-            elif v.op == "concat" or v.op in _CMP:
+            elif v.op == "concat" or v.op in _CMP or v.op == "tab":
                 w[3] = v.imm
             out[i] = w
         if n > TILE_INSNS:
@@ -224,4 +232,8 @@ def compile_sets(sets: Sequence[Sequence], compiler: Compiler = None) -> Tuple[P
     names = [None] * len(c.var_widths)
     for name, i in c.var_index.items():
         names[i] = name
-    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths)), kept
+    tables = [None] * len(c.table_index)
+    for name, t in c.table_index.items():
+        tables[t] = c.lowering.tables[name]
+    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths),
+                        tables), kept

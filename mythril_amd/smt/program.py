@@ -17,10 +17,11 @@ OPS = ["copy", "bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem"
        "bvand", "bvor", "bvxor", "bvnot", "bvneg", "bvshl", "bvlshr", "bvashr",
        "eq", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
        "and", "or", "xor", "not", "implies", "ite", "extract", "concat", "zero_extend",
-       "sign_extend", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "distinct"]
+       "sign_extend", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "distinct", "tab"]
 OPCODE = {name: i for i, name in enumerate(OPS)}
 UNARY = {"copy", "bvnot", "bvneg", "not", "extract", "zero_extend", "sign_extend"}
 REF_ACC, REF_SLOT, REF_VAR, REF_CONST = 0, 1, 2, 3
+TAB_PART_SHIFT, TAB_LO_SHIFT, TAB_INDEX_MASK = 20, 21, (1 << 20) - 1
 MAX_SLOTS = 8
 TILE_INSNS = 2048
 
@@ -44,6 +45,7 @@ class ProgramBatch:
     n_slots: int
     var_names: List[str] = field(default_factory=list)
     var_widths: List[int] = field(default_factory=list)
+    tables: List = field(default_factory=list)      # lower.TableSig per table index
 
     @property
     def n_dags(self) -> int:
@@ -65,11 +67,43 @@ class ProgramBatch:
         return s
 
 
+class ArrayInterp:
+    """A model's interpretation of a symbolic array: default + entries
+    (z3's K(default) + stores / as-array)."""
+    __slots__ = ("default", "entries")
+
+    def __init__(self, default: int = 0, entries: Optional[Dict[int, int]] = None):
+        self.default = default
+        self.entries = dict(entries or {})
+
+
+class FuncInterp:
+    """A model's interpretation of an uninterpreted function: entries (argument
+    tuple -> value) + else value."""
+    __slots__ = ("else_value", "entries")
+
+    def __init__(self, else_value: int = 0, entries: Optional[Dict[tuple, int]] = None):
+        self.else_value = else_value
+        self.entries = dict(entries or {})
+
+
+def _wide_limbs(x: int) -> np.ndarray:
+    """512-bit value -> 16 little-endian u32 limbs."""
+    return np.frombuffer((x & ((1 << 512) - 1)).to_bytes(64, "little"), dtype="<u4")
+
+
 @dataclass
 class ModelPool:
     """values[v, m] = value of variable v in model m (256-bit limbs), models in
-    most-recently-used-first order (support_utils.py:62-63)."""
+    most-recently-used-first order (support_utils.py:62-63).  Tables hold the
+    models' array / function interpretations: for table t and model m the
+    entries tab_entries[tab_start[t, m] : + tab_count[t, m]] (each key k0, k1 and
+    a 512-bit value, 32 u32) and the default / else value tab_default[t, m]."""
     values: np.ndarray         # (n_vars, n_models, 8) uint32
+    tab_start: Optional[np.ndarray] = None     # (n_tables, n_models) uint32
+    tab_count: Optional[np.ndarray] = None     # (n_tables, n_models) uint32
+    tab_entries: Optional[np.ndarray] = None   # (n_entries, 32) uint32
+    tab_default: Optional[np.ndarray] = None   # (n_tables, n_models, 16) uint32
 
     @property
     def n_models(self) -> int:
@@ -79,19 +113,64 @@ class ModelPool:
     def n_vars(self) -> int:
         return int(self.values.shape[0])
 
+    @property
+    def n_tables(self) -> int:
+        return 0 if self.tab_start is None else int(self.tab_start.shape[0])
+
     def c_struct(self):
         from ..native import MgModelBatch
         self.values = np.ascontiguousarray(self.values, dtype=np.uint32)
-        return MgModelBatch(self.n_models, self.n_vars, self.values.ctypes.data)
+        if self.n_tables == 0:
+            return MgModelBatch(self.n_models, self.n_vars, self.values.ctypes.data, 0, None, None,
+                                None, 0, None)
+        for f in ("tab_start", "tab_count", "tab_entries", "tab_default"):
+            setattr(self, f, np.ascontiguousarray(getattr(self, f), dtype=np.uint32))
+        if self.tab_entries.shape[0] == 0:
+            self.tab_entries = np.zeros((1, 32), dtype=np.uint32)
+        return MgModelBatch(self.n_models, self.n_vars, self.values.ctypes.data, self.n_tables,
+                            self.tab_start.ctypes.data, self.tab_count.ctypes.data,
+                            self.tab_entries.ctypes.data, int(self.tab_entries.shape[0]),
+                            self.tab_default.ctypes.data)
 
     @staticmethod
-    def from_dicts(models: List[Dict[str, int]], var_names: List[str], var_widths: List[int]):
+    def from_dicts(models: List[Dict[str, object]], var_names: List[str], var_widths: List[int],
+                   tables: Optional[List] = None):
+        """models: name -> int for variables, ArrayInterp / FuncInterp for tables;
+        anything absent is completed with 0 (z3 model_completion)."""
         vals = np.zeros((max(len(var_names), 1), max(len(models), 1), 8), dtype=np.uint32)
         for m, model in enumerate(models):
             for v, (name, w) in enumerate(zip(var_names, var_widths)):
-                x = model.get(name, 0) & ((1 << w) - 1)   # absent -> 0 (model completion)
+                x = model.get(name, 0)
+                x = (x if isinstance(x, int) else 0) & ((1 << w) - 1)
                 vals[v, m] = np.frombuffer(x.to_bytes(32, "little"), dtype="<u4")
-        return ModelPool(vals)
+        pool = ModelPool(vals)
+        tables = tables or []
+        if tables:
+            nm = max(len(models), 1)
+            start = np.zeros((len(tables), nm), dtype=np.uint32)
+            count = np.zeros((len(tables), nm), dtype=np.uint32)
+            default = np.zeros((len(tables), nm, 16), dtype=np.uint32)
+            rows = []
+            for t, sig in enumerate(tables):
+                for m, model in enumerate(models):
+                    interp = model.get(sig.name)
+                    start[t, m] = len(rows)
+                    if isinstance(interp, ArrayInterp):
+                        default[t, m] = _wide_limbs(interp.default)
+                        items = [((k,), v) for k, v in interp.entries.items()]
+                    elif isinstance(interp, FuncInterp):
+                        default[t, m] = _wide_limbs(interp.else_value)
+                        items = list(interp.entries.items())
+                    else:
+                        items = []
+                    for args, v in items:
+                        k0, k1 = sig.key_chunks(tuple(args))
+                        rows.append(np.concatenate([limbs(k0), limbs(k1), _wide_limbs(v)]))
+                    count[t, m] = len(rows) - start[t, m]
+            entries = np.stack(rows) if rows else np.zeros((0, 32), dtype=np.uint32)
+            pool.tab_start, pool.tab_count, pool.tab_entries, pool.tab_default = \
+                start, count, entries, default
+        return pool
 
 
 def limbs(x: int) -> np.ndarray:

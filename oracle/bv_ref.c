@@ -22,7 +22,7 @@ enum {
     OP_AND, OP_OR, OP_XOR, OP_NOT, OP_NEG, OP_SHL, OP_LSHR, OP_ASHR,
     OP_EQ, OP_ULT, OP_ULE, OP_UGT, OP_UGE, OP_SLT, OP_SLE, OP_SGT, OP_SGE,
     OP_BAND, OP_BOR, OP_BXOR, OP_BNOT, OP_BIMPLIES, OP_ITE, OP_EXTRACT, OP_CONCAT,
-    OP_ZEXT, OP_SEXT, OP_ADD_NOOVF_U, OP_MUL_NOOVF_U, OP_SUB_NOUDF_U, OP_NE
+    OP_ZEXT, OP_SEXT, OP_ADD_NOOVF_U, OP_MUL_NOOVF_U, OP_SUB_NOUDF_U, OP_NE, OP_TAB
 };
 
 static u256 w_mask(u256 v, unsigned w) {
@@ -42,12 +42,34 @@ static u256 w_sext(u256 v, unsigned w) {
 }
 static u256 w_bool(int b) { return u_from64(b ? 1 : 0); }
 
+typedef struct {          /* model interpretations of arrays / functions */
+    uint32_t n_tables;
+    const uint32_t *start, *count, *entries, *dflt;
+} tables_t;
+
 typedef struct {
     const uint32_t *insns, *prog_off, *consts, *values;
     uint32_t n_vars, n_models, n_slots;
     uint32_t *first_sat, *sat_count;
     uint32_t d0, d1;
+    const tables_t *tab;
 } job_t;
+
+/* Value of table `imm` (index | part << 20 | lo << 21) at key (k0, k1) in model m:
+ * the listed entry with that key, else the default; bits [256 part + lo, ...). */
+static u256 table_lookup(const job_t *j, u256 k0, u256 k1, uint32_t imm, uint32_t m) {
+    const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
+    const size_t tm = (size_t)t * j->n_models + m;
+    u256 v = u_from_limbs32(j->tab->dflt + tm * 16 + part * 8);
+    for (uint32_t k = 0; k < j->tab->count[tm]; ++k) {
+        const uint32_t *e = j->tab->entries + ((size_t)j->tab->start[tm] + k) * 32;
+        if (u_eq(u_from_limbs32(e), k0) && u_eq(u_from_limbs32(e + 8), k1)) {
+            v = u_from_limbs32(e + 16 + part * 8);
+            break;
+        }
+    }
+    return u_lshr(v, u_from64(lo));
+}
 
 static u256 fetch(const job_t *j, u256 acc, const u256 *slots, uint32_t ref, uint32_t m) {
     uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
@@ -140,6 +162,7 @@ static int eval_one(const job_t *j, uint32_t d, uint32_t m) {
             break;
         }
         case OP_SUB_NOUDF_U: r = w_bool(!u_lt(a, b)); break;
+        case OP_TAB: r = table_lookup(j, a, b, w[3], m); break;
         default: r = u_zero(); break;
         }
         r = w_mask(r, width);
@@ -162,10 +185,12 @@ static void *worker(void *arg) {
 }
 
 /* Evaluate programs [d_first, d_first+d_count) on every model. */
-void orb_eval(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
-              const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
-              uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
-              uint32_t threads) {
+void orb_eval_tab(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
+                  const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
+                  uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
+                  uint32_t threads, uint32_t n_tables, const uint32_t *tab_start,
+                  const uint32_t *tab_count, const uint32_t *tab_entries, const uint32_t *tab_default) {
+    const tables_t tab = {n_tables, tab_start, tab_count, tab_entries, tab_default};
     if (threads < 1) threads = 1;
     if (threads > 128) threads = 128;
     if (threads > d_count) threads = d_count ? d_count : 1;
@@ -178,11 +203,19 @@ void orb_eval(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *c
         if (a >= d_first + d_count) break;
         uint32_t b = a + per > d_first + d_count ? d_first + d_count : a + per;
         jobs[t] = (job_t){insns, prog_off, consts, values, n_vars, n_models, n_slots,
-                          first_sat, sat_count, a, b};
+                          first_sat, sat_count, a, b, &tab};
         if (threads == 1) worker(&jobs[t]);
         else pthread_create(&tid[t], NULL, worker, &jobs[t]);
         started++;
     }
     if (threads > 1)
         for (uint32_t t = 0; t < started; ++t) pthread_join(tid[t], NULL);
+}
+
+void orb_eval(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
+              const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
+              uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
+              uint32_t threads) {
+    orb_eval_tab(insns, prog_off, consts, values, n_vars, n_models, n_slots, d_first, d_count,
+                 first_sat, sat_count, threads, 0, NULL, NULL, NULL, NULL);
 }

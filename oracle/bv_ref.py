@@ -18,9 +18,18 @@ def eval_batch(prog, models, first: int = 0, count: int = None, threads: int = 0
     off = np.ascontiguousarray(prog.prog_off, dtype=np.uint32)
     consts = np.ascontiguousarray(prog.consts if prog.consts.size else np.zeros((1, 8)), dtype=np.uint32)
     vals = np.ascontiguousarray(models.values, dtype=np.uint32)
-    f = lib().orb_eval
+    f = lib().orb_eval_tab
     f.restype = None
-    f.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] * 5 + [ctypes.c_void_p] * 2 + [ctypes.c_uint32]
+    f.argtypes = ([ctypes.c_void_p] * 4 + [ctypes.c_uint32] * 5 + [ctypes.c_void_p] * 2 +
+                  [ctypes.c_uint32, ctypes.c_uint32] + [ctypes.c_void_p] * 4)
+    if models.n_tables:
+        ts, tc, te, td = (np.ascontiguousarray(x, dtype=np.uint32) for x in
+                          (models.tab_start, models.tab_count,
+                           models.tab_entries if models.tab_entries.size else np.zeros((1, 32)),
+                           models.tab_default))
+        tabs = (models.n_tables, ts.ctypes.data, tc.ctypes.data, te.ctypes.data, td.ctypes.data)
+    else:
+        tabs = (0, None, None, None, None)
     f(insns.ctypes.data, off.ctypes.data, consts.ctypes.data, vals.ctypes.data, models.n_vars,
-      models.n_models, prog.n_slots, first, count, fs.ctypes.data, sc.ctypes.data, threads)
+      models.n_models, prog.n_slots, first, count, fs.ctypes.data, sc.ctypes.data, threads, *tabs)
     return fs[first:first + count], sc[first:first + count]

@@ -66,3 +66,29 @@ def test_c4_full_size_sampled_parity(dev):
     dev.eval_run(0, 1000)
     a, b = dev.eval_download(0, 1000)
     assert np.array_equal(a, fs[:1000]) and np.array_equal(b, sc[:1000])
+
+
+def test_arrays_functions_device_equals_oracle(dev):
+    """Storage / calldata arrays, keccak256_N functions and their inverses, Power,
+    512-bit keys (kernel-2 table lookups, BV_TAB) — device vs oracle."""
+    from test_smt_programs import _random_table_constraints, _random_table_models
+    rng = random.Random(2024)
+    sets = [_random_table_constraints(rng) for _ in range(600)]
+    prog, kept = compile_sets(sets)
+    assert len(kept) == len(sets) and prog.tables
+    models = _random_table_models(random.Random(11), 700, prog)
+    pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables)
+    fs, sc, _ = dev.eval(prog, pool)
+    rfs, rsc = eval_batch(prog, pool)
+    assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
+    assert (sc > 0).sum() > 50
+    # a pool without tables after one with them (table state reset on upload)
+    prog2, _ = compile_sets([[s for s in sets[0] if False] or [ULT_x()]])
+    pool2 = ModelPool.from_dicts([{"x": 1}, {"x": 5}], prog2.var_names, prog2.var_widths)
+    fs2, sc2, _ = dev.eval(prog2, pool2)
+    assert list(fs2) == [0] and list(sc2) == [1]
+
+
+def ULT_x():
+    from mythril_amd.smt.expr import ULT, symbol_factory
+    return ULT(symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecVal(3, 256))

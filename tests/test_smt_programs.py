@@ -91,9 +91,14 @@ def test_flattener_slot_pressure_and_unsupported():
     many = [ULT(x + BVV(k, 256), BVV(10 ** 6 + k, 256)) for k in range(40)]
     prog, kept = compile_sets([many])
     assert kept == [0] and prog.n_slots <= 2
-    wide = Concat(x, x)                   # 512-bit keccak-style input: stays on z3
-    prog2, kept2 = compile_sets([[wide == wide]])
-    assert kept2 == []
+    wide = Concat(x, x)                   # 512-bit keccak-style input: split in two chunks
+    prog2, kept2 = compile_sets([[wide == Concat(x, BVV(3, 256))]])
+    assert kept2 == [0]
+    wider = Concat(x, x, x)               # 768-bit equality: three chunk compares
+    prog3, kept3 = compile_sets([[wider == Concat(x, x, BVV(1, 256))]])
+    assert kept3 == [0]
+    prog4, kept4 = compile_sets([[wide + wide == wide]])    # 512-bit arithmetic: z3
+    assert kept4 == []
 
 
 def test_constant_folding_follows_z3():
@@ -102,3 +107,105 @@ def test_constant_folding_follows_z3():
     assert (BVV(-7, 256) / BVV(2, 256)).value == (-3) % (1 << 256)
     assert (BVV(1, 256) < BVV(-1, 256)).value is False     # signed <, bitvec.py:140-150
     assert ULE(BVV(3, 256), BVV(3, 256)).value is True
+
+
+# ------------------------------------------------ arrays, functions, keccak conjuncts
+from mythril_amd.smt.expr import Array, Function, K  # noqa: E402
+from mythril_amd.smt.program import ArrayInterp, FuncInterp  # noqa: E402
+
+M256 = (1 << 256) - 1
+
+
+def _random_table_constraints(rng):
+    """Constraint sets of the shapes LASER builds: storage
+    arrays with symbolic and concrete stores, calldata byte arrays, keccak
+    functions of 256- and 512-bit inputs with the inverse and interval conjuncts
+    of keccak_function_manager.py:150-179, Power."""
+    x, y, s = BVS("x", 256), BVS("y", 256), BVS("slot", 256)
+    storage = Array("Storage", 256, 256)
+    if rng.random() < 0.7:
+        storage[x] = y
+    if rng.random() < 0.5:
+        storage[BVV(1, 256)] = x + y
+    if rng.random() < 0.3:
+        storage[y] = BVV(rng.getrandbits(8), 256)
+    cd = K(256, 8, 0) if rng.random() < 0.5 else Array("calldata", 256, 8)
+    for k in range(rng.randrange(0, 4)):
+        cd[BVV(k, 256)] = Extract(7, 0, x >> BVV(8 * k, 256))
+    f512 = Function("keccak256_512", [512], 256)
+    inv512 = Function("keccak256_512-1", [256], 512)
+    f256 = Function("keccak256_256", [256], 256)
+    power = Function("Power", [256, 256], 256)
+    key = Concat(x, s)
+    h = f512(key)
+    lo = BVV(rng.getrandbits(255), 256)
+    pool = [
+        storage[x] == y, ULT(storage[s], BVV(1 << 200, 256)), storage[BVV(1, 256)] != BVV(0, 256),
+        Concat(cd[BVV(0, 256)], cd[BVV(1, 256)]) == Extract(15, 0, x),
+        ZeroExt(248, cd[y]) == BVV(0, 256),
+        inv512(h) == key, ULE(lo, h), ULT(h, lo + BVV(1 << 120, 256)),
+        URem(h, BVV(64, 256)) == BVV(0, 256),
+        f512(Concat(BVV(0xDEAD, 256), BVV(0, 256))) == BVV(rng.getrandbits(256), 256),
+        f256(y) == x, Extract(255, 0, inv512(f256(x))) == x,
+        power(BVV(2, 256), y) == x, storage[h] == BVV(0, 256),
+        Or(f512(key) == BVV(5, 256), And(key == Concat(y, BVV(0, 256)), f256(x) != y)),
+    ]
+    return [rng.choice(pool) for _ in range(rng.randrange(1, 6))]
+
+
+def _random_table_models(rng, n, prog):
+    """Models whose interpretations often contain the keys the constraints touch."""
+    out = []
+    for _ in range(n):
+        x, y, s = rng.getrandbits(256), rng.getrandbits(256), rng.choice([0, 1, 2, rng.getrandbits(256)])
+        if rng.random() < 0.3:
+            y = x
+        m = {"x": x, "y": y, "slot": s}
+        h = rng.getrandbits(256) & ~63 if rng.random() < 0.7 else rng.getrandbits(256)
+        if rng.random() < 0.8:
+            m["Storage"] = ArrayInterp(rng.choice([0, 7]), {x: rng.choice([y, 0]), 1: rng.getrandbits(8),
+                                                            s: rng.getrandbits(201)})
+        if rng.random() < 0.5:
+            m["calldata"] = ArrayInterp(0, {y: 0, 0: x & 0xFF})
+        if rng.random() < 0.8:
+            m["keccak256_512"] = FuncInterp(rng.choice([0, 5]), {((x << 256) | s,): h,
+                                                                   ((y << 256),): 5})
+        if rng.random() < 0.7:
+            m["keccak256_512-1"] = FuncInterp(0, {(h,): (x << 256) | s})
+        if rng.random() < 0.7:
+            m["keccak256_256"] = FuncInterp(rng.getrandbits(256), {(y,): x, (x,): rng.getrandbits(256)})
+        if rng.random() < 0.5:
+            m["Power"] = FuncInterp(1, {(2, y): x})
+        out.append(m)
+    return out
+
+
+def test_arrays_functions_wide_values_match_python_semantics():
+    rng = random.Random(4321)
+    sets = [_random_table_constraints(rng) for _ in range(150)]
+    prog, kept = compile_sets(sets)
+    assert len(kept) == len(sets)
+    assert {t.name for t in prog.tables} >= {"Storage", "keccak256_512", "keccak256_512-1"}
+    models = _random_table_models(random.Random(8), 80, prog)
+    pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables)
+    fs, sc = eval_batch(prog, pool)
+    hits = 0
+    for d, s in enumerate(sets):
+        root = And(*s)
+        vals = [evaluate(root.raw, m) for m in models]
+        first = next((m for m, v in enumerate(vals) if v), 0xFFFFFFFF)
+        assert (first, sum(vals)) == (fs[d], sc[d]), (d, s)
+        hits += sum(vals)
+    assert hits > 100            # the generator reaches satisfying interpretations
+
+
+def test_select_store_folding_follows_z3_simplify():
+    x = BVS("x", 256)
+    st = K(256, 256, 0)
+    st[BVV(1, 256)] = BVV(5, 256)
+    assert st[BVV(1, 256)].value == 5 and st[BVV(2, 256)].value == 0
+    a = Array("S", 256, 256)
+    a[BVV(1, 256)] = x
+    assert a[BVV(1, 256)].raw is x.raw
+    # a store at a different constant index is skipped: select(S, 2)
+    assert a[BVV(2, 256)].raw.args[0].op == "array"
