@@ -250,6 +250,14 @@ typedef struct mg_model_batch {
 int         mg_eval(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models,
                     uint32_t *first_sat_model, uint32_t *sat_count, float *kernel_ms);
 
+/* Same, plus the full satisfaction bitmap: bit m of sat_bits[d][m / 64] is set
+ * when model m satisfies DAG d (sat_bits: [n_dags][ceil(n_models / 64)]).  With
+ * it the host replays a sequence of check_quick_sat calls exactly, including
+ * the LRU moves of returned models between calls (support_utils.py:60-68).    */
+int         mg_eval_bits(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models,
+                         uint32_t *first_sat, uint32_t *sat_count, uint64_t *sat_bits,
+                         float *kernel_ms);
+
 /* Device-resident variant used by the benchmark: upload once, evaluate many
  * times without host traffic. */
 int         mg_eval_upload(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models);

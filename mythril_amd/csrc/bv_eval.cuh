@@ -69,6 +69,9 @@ struct BvState {
     uint4 *tab_default = nullptr;    // [n_tables][n_models][4]
     uint32_t *first_sat = nullptr;   // [n_dags]
     uint32_t *sat_count = nullptr;   // [n_dags]
+    unsigned long long *sat_bits = nullptr;   // [n_dags][bit_words] (mg_eval_bits)
+    size_t cap_bits = 0;
+    bool want_bits = false;
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
     size_t cap_entries = 0;
     bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
@@ -180,7 +183,9 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       uint32_t tiles_pad, uint32_t dag_lo, uint32_t dag_hi,
                                                       uint32_t tile_cap, uint32_t chunks_per_block,
                                                       uint32_t *__restrict__ first_sat,
-                                                      uint32_t *__restrict__ sat_count) {
+                                                      uint32_t *__restrict__ sat_count,
+                                                      unsigned long long *__restrict__ sat_bits,
+                                                      uint32_t bit_words) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
     // kLdsProg: the program tile is staged in LDS and read with a broadcast
     // ds_read + readfirstlane; otherwise instructions are read with scalar loads
@@ -310,6 +315,9 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
         const bool sat = live && (acc.w[0] & 1u);
         const uint64_t bal = __ballot(sat);
         if ((tid & 63u) == 0u && bal) {
+            // optional per-model bitmap (one u64 per wave): lets the host replay
+            // sequential check_quick_sat calls whose LRU bumps reorder the pool
+            if (sat_bits) sat_bits[(size_t)d * bit_words + ((chunk * BV_BLOCK + tid) >> 6)] = bal;
             atomicAdd(&sat_count[d], (uint32_t)__popcll(bal));
             atomicMin(&first_sat[d], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
         }
@@ -332,6 +340,7 @@ static void bv_free(BvState &s) {
     hipFree(s.insns); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.consts);
     hipFree(s.values); hipFree(s.first_sat); hipFree(s.sat_count);
     hipFree(s.tab_start); hipFree(s.tab_count); hipFree(s.tab_entries); hipFree(s.tab_default);
+    hipFree(s.sat_bits);
     s = BvState{};
 }
 
@@ -449,6 +458,13 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t dag_hi = dag_first + dag_count;
     hipError_t e = hipMemsetAsync(s.first_sat + dag_first, 0xff, (size_t)dag_count * 4, st);
     if (e == hipSuccess) e = hipMemsetAsync(s.sat_count + dag_first, 0, (size_t)dag_count * 4, st);
+    const uint32_t bit_words = (s.n_models + 63u) / 64u;
+    if (s.want_bits) {
+        const size_t need = (size_t)s.n_dags * bit_words;
+        if (bv_ensure(s.sat_bits, s.cap_bits, need)) { msg = "alloc sat bitmap"; return MG_ENOMEM; }
+        if (e == hipSuccess)
+            e = hipMemsetAsync(s.sat_bits + (size_t)dag_first * bit_words, 0, (size_t)dag_count * bit_words * 8, st);
+    }
     if (e != hipSuccess) { msg = hipGetErrorString(e); return MG_EDEVICE; }
     // tiles covering [dag_first, dag_hi)
     const auto &t = s.h_tiles;
@@ -470,16 +486,22 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
                        s.insns, s.prog_off, s.tile_dag,
                        s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
                        s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
-                       s.tile_cap, cpb, s.first_sat, s.sat_count);
+                       s.tile_cap, cpb, s.first_sat, s.sat_count, s.want_bits ? s.sat_bits : nullptr, bit_words);
     e = hipGetLastError();
     if (e != hipSuccess) { msg = std::string("k_bv_eval launch: ") + hipGetErrorString(e); return MG_EDEVICE; }
     return 0;
 }
 
 static int bv_download(BvState &s, uint32_t *first_sat, uint32_t *sat_count, uint32_t dag_first, uint32_t dag_count,
-                       hipStream_t st, std::string &msg) {
+                       hipStream_t st, std::string &msg, unsigned long long *sat_bits = nullptr) {
     if (dag_first + (uint64_t)dag_count > s.n_dags) { msg = "DAG range out of bounds"; return MG_EINVAL; }
     hipError_t e = hipSuccess;
+    if (sat_bits) {
+        if (!s.want_bits || !s.sat_bits) { msg = "no bitmap was computed"; return MG_ESTATE; }
+        const size_t bw = (s.n_models + 63u) / 64u;
+        e = hipMemcpyAsync(sat_bits, s.sat_bits + (size_t)dag_first * bw, (size_t)dag_count * bw * 8,
+                           hipMemcpyDeviceToHost, st);
+    }
     if (first_sat) e = hipMemcpyAsync(first_sat, s.first_sat + dag_first, (size_t)dag_count * 4, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess && sat_count)
         e = hipMemcpyAsync(sat_count, s.sat_count + dag_first, (size_t)dag_count * 4, hipMemcpyDeviceToHost, st);

@@ -808,6 +808,23 @@ extern "C" int mg_eval_download(mg_ctx *ctx, uint32_t *first_sat, uint32_t *sat_
     return MG_OK;
 }
 
+extern "C" int mg_eval_bits(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models,
+                            uint32_t *first_sat, uint32_t *sat_count, uint64_t *sat_bits, float *kernel_ms) {
+    if (!ctx || !dags || !models || !sat_bits) return MG_EINVAL;
+    int rc;
+    if ((rc = mg_eval_upload(ctx, dags, models))) return rc;
+    ctx->bv.want_bits = true;
+    rc = mg_eval_run(ctx, 0, dags->n_dags, kernel_ms);
+    if (!rc) {
+        std::string msg;
+        rc = bv_download(ctx->bv, first_sat, sat_count, 0, dags->n_dags, ctx->stream, msg,
+                         (unsigned long long *)sat_bits);
+        if (rc) set_err(ctx, rc, "%s", msg.c_str());
+    }
+    ctx->bv.want_bits = false;
+    return rc;
+}
+
 extern "C" int mg_eval(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_batch *models, uint32_t *first_sat,
                        uint32_t *sat_count, float *kernel_ms) {
     int rc;

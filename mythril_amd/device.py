@@ -179,6 +179,19 @@ class GpuDevice:
                     "mg_eval_download")
         return fs, sc
 
+    def eval_bits(self, program, models):
+        """(first_sat, sat_count, sat_bits[n_dags, ceil(n_models/64)] uint64, ms)."""
+        dags, mods = program.c_struct(), models.c_struct()
+        n, words = program.n_dags, (models.n_models + 63) // 64
+        fs = np.zeros(n, dtype=np.uint32)
+        sc = np.zeros(n, dtype=np.uint32)
+        bits = np.zeros((n, words), dtype=np.uint64)
+        ms = ctypes.c_float()
+        self._check(self.lib.mg_eval_bits(self.ctx, ctypes.byref(dags), ctypes.byref(mods),
+                                          fs.ctypes.data, sc.ctypes.data, bits.ctypes.data,
+                                          ctypes.byref(ms)), "mg_eval_bits")
+        return fs, sc, bits, ms.value
+
     def eval(self, program, models):
         self.eval_upload(program, models)
         ms = self.eval_run()

@@ -91,6 +91,8 @@ SIGNATURES = {
     "mg_step": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_async": (_I, [_P, _P, _U32, _U32]),
     "mg_step_until": (_I, [_P, _P, _U32, _U32, _U32, ctypes.POINTER(MgStepStats)]),
+    "mg_eval_bits": (_I, [_P, ctypes.POINTER(MgDagBatch), ctypes.POINTER(MgModelBatch), _P, _P, _P,
+                          ctypes.POINTER(ctypes.c_float)]),
     "mg_step_profile": (_I, [_P, _P, _U32, _U32, _P, _P]),
     "mg_sync": (_I, [_P]),
     "mg_coverage": (_I, [_P, _U32, _P, _U32]),

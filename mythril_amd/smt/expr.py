@@ -73,7 +73,9 @@ FALSE = const(0, 1)
 
 def _fold(op: str, width: int, args, param=None) -> Node:
     """Constant folding for all-constant arguments (what z3's simplify does to
-    BitVecNumRef operands; keeps concrete values concrete)."""
+    BitVecNumRef operands; keeps concrete values concrete), and x == x -> True."""
+    if op in ("eq", "distinct") and len(args) == 2 and args[0] is args[1]:
+        return TRUE if op == "eq" else FALSE
     if args and all(a.op == "const" for a in args):
         from .semantics import apply_op
         return const(apply_op(op, width, [a.param for a in args], [a.width for a in args], param),

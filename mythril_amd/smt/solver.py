@@ -1,0 +1,331 @@
+"""Feasibility checks with kernel 2 as the quick-sat prefilter.
+
+Mirrors, with the same names, arguments and error behaviour:
+
+* ``LRUCache`` / ``ModelCache`` (support/support_utils.py:34-68): the 100 most
+  recently used models; ``check_quick_sat(expr)`` returns the first model in
+  most-recently-used order under which the expression is true, moves it to
+  most-recent, and memoises per expression (``lru_cache(2**10)``).  The models
+  are evaluated on kernel 2 (``mg_eval``), all of them in one launch;
+  ``check_quick_sat_many`` evaluates a whole sequence of queries in one launch
+  (``mg_eval_bits``) and replays the sequential calls exactly, LRU moves
+  included.
+* ``get_model`` (support/model.py:21-82): ``lru_cache(2**23)``; a literal False
+  raises UnsatError; quick-sat only when nothing is minimised or maximised;
+  otherwise the SMT backend, whose model is cached with count 1.
+* ``Constraints`` (state/constraints.py:12-131): ``is_possible`` maps a timeout to
+  False (default timeout) or True (custom timeout) and UnsatError to False;
+  ``get_all_constraints`` appends the keccak conjunct.
+
+The prefilter only ever answers SAT with a model.  A constraint set the device
+cannot evaluate (flatten.Unsupported) and a set no cached model satisfies both
+fall through to the backend unchanged.  The backend is z3 in the reference; z3
+is not installed in this image nor on the GPU box, so ``solver_backend`` is a
+pluggable callable (constraints, minimize, maximize, timeout_ms) -> model that
+raises UnsatError / SolverTimeOutException; the default raises
+SolverTimeOutException.
+"""
+from __future__ import annotations
+
+import os
+import time
+from collections import OrderedDict
+from functools import lru_cache
+from typing import Callable, Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from .expr import And, Bool, Node, TRUE, symbol_factory
+from .flatten import compile_sets
+from .program import ArrayInterp, FuncInterp, ModelPool
+
+NO_MODEL = 0xFFFFFFFF
+
+
+class UnsatError(Exception):
+    """mythril/exceptions.py: the constraints are unsatisfiable."""
+
+
+class SolverTimeOutException(Exception):
+    """mythril/exceptions.py: the solver gave up."""
+
+
+def simplify(expr):
+    """Expressions are folded as they are built (expr._fold, lower._select), so
+    simplify returns its argument."""
+    return expr
+
+
+# ------------------------------------------------------------------ models
+class Model:
+    """A candidate model: variable values and array / function interpretations.
+    Hashed by identity, as z3 ModelRef objects are (they key the LRU cache)."""
+
+    def __init__(self, assignment: Optional[Dict[str, object]] = None):
+        self.assignment: Dict[str, object] = dict(assignment or {})
+
+    def __getitem__(self, name: str):
+        return self.assignment[name]
+
+    def get(self, name: str, default=None):
+        return self.assignment.get(name, default)
+
+    def decls(self) -> List[str]:
+        return list(self.assignment)
+
+    def __repr__(self):
+        return f"Model({self.assignment})"
+
+
+class LRUCache:
+    def __init__(self, size):
+        self.size = size
+        self.lru_cache: "OrderedDict" = OrderedDict()
+
+    def get(self, key):
+        try:
+            value = self.lru_cache.pop(key)
+            self.lru_cache[key] = value
+            return value
+        except KeyError:
+            return -1
+
+    def put(self, key, value):
+        try:
+            self.lru_cache.pop(key)
+        except KeyError:
+            if len(self.lru_cache) >= self.size:
+                self.lru_cache.popitem(last=False)
+        self.lru_cache[key] = value
+
+
+def _raw(expr) -> Node:
+    return expr.raw if isinstance(expr, Bool) else expr
+
+
+class ModelCache:
+    QUICK_SAT_MEMO = 2 ** 10
+
+    def __init__(self, device=None):
+        self.model_cache = LRUCache(size=100)
+        self._device = device
+        self._memo: "OrderedDict[Node, object]" = OrderedDict()
+        self.device_evals = 0          # constraint-evals run on kernel 2
+        self.launches = 0
+
+    @property
+    def device(self):
+        if self._device is None:
+            from ..device import GpuDevice
+            self._device = GpuDevice(int(os.environ.get("LOCAL_RANK", "0")))
+        return self._device
+
+    def put(self, key, value):
+        self.model_cache.put(key, value)
+
+    # -- memo = functools.lru_cache(maxsize=2**10) on check_quick_sat ---------
+    def _memo_get(self, key):
+        if key in self._memo:
+            self._memo.move_to_end(key)
+            return True, self._memo[key]
+        return False, None
+
+    def _memo_put(self, key, value):
+        self._memo[key] = value
+        self._memo.move_to_end(key)
+        if len(self._memo) > self.QUICK_SAT_MEMO:
+            self._memo.popitem(last=False)
+
+    def _pool(self, models: List[Model], prog) -> ModelPool:
+        return ModelPool.from_dicts([m.assignment for m in models], prog.var_names,
+                                    prog.var_widths, prog.tables)
+
+    def _select(self, model: Model) -> Model:
+        self.model_cache.put(model, self.model_cache.get(model) + 1)
+        return model
+
+    def check_quick_sat(self, constraints):
+        key = _raw(constraints)
+        hit, val = self._memo_get(key)
+        if hit:
+            return val
+        result = False
+        models = list(reversed(self.model_cache.lru_cache.keys()))      # MRU first
+        if models:
+            prog, kept = compile_sets([[key]])
+            if kept:
+                fs, _, _ = self.device.eval(prog, self._pool(models, prog))
+                self.device_evals += len(models)
+                self.launches += 1
+                if int(fs[0]) != NO_MODEL:
+                    result = self._select(models[int(fs[0])])
+        self._memo_put(key, result)
+        return result
+
+    def check_quick_sat_many(self, queries: Sequence) -> List[object]:
+        """[check_quick_sat(q) for q in queries], with every query not already
+        memoised evaluated against the current pool in ONE kernel-2 launch."""
+        keys = [_raw(q) for q in queries]
+        models0 = list(reversed(self.model_cache.lru_cache.keys()))
+        pos0 = {id(m): i for i, m in enumerate(models0)}
+        fresh = list(OrderedDict.fromkeys(k for k in keys if k not in self._memo))
+        bits: Dict[Node, np.ndarray] = {}
+        if models0 and fresh:
+            prog, kept = compile_sets([[k] for k in fresh])
+            if kept:
+                _, _, b, _ = self.device.eval_bits(prog, self._pool(models0, prog))
+                self.device_evals += len(kept) * len(models0)
+                self.launches += 1
+                for row, k in enumerate(kept):
+                    bits[fresh[k]] = b[row]
+        out = []
+        for k in keys:
+            hit, val = self._memo_get(k)
+            if hit:
+                out.append(val)
+                continue
+            result = False
+            b = bits.get(k)
+            if b is not None:
+                for m in reversed(self.model_cache.lru_cache.keys()):   # current MRU order
+                    p = pos0.get(id(m))
+                    if p is not None and (int(b[p >> 6]) >> (p & 63)) & 1:
+                        result = self._select(m)
+                        break
+            self._memo_put(k, result)
+            out.append(result)
+        return out
+
+
+model_cache = ModelCache()
+
+
+# ------------------------------------------------------------------ get_model
+class _Args:
+    """support/support_args.py: the solver timeout (ms) get_model uses."""
+    solver_timeout = 25000
+    solver_log = None
+
+
+args = _Args()
+
+
+class TimeHandler:
+    """laser/ethereum/time_handler.py: remaining analysis time in ms."""
+
+    def __init__(self):
+        self._start = None
+        self._timeout = None
+
+    def start_execution(self, timeout: int):
+        self._start = int(time.time() * 1000)
+        self._timeout = timeout * 1000
+
+    def time_remaining(self) -> int:
+        if self._start is None:
+            return 1 << 62
+        return self._timeout - (int(time.time() * 1000) - self._start)
+
+
+time_handler = TimeHandler()
+
+
+def _no_backend(constraints, minimize, maximize, timeout):
+    raise SolverTimeOutException("no SMT backend installed (z3 is absent in this image)")
+
+
+solver_backend: Callable = _no_backend
+
+
+def set_solver_backend(fn: Callable) -> None:
+    global solver_backend
+    solver_backend = fn
+    get_model.cache_clear()
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True,
+              solver_timeout=None):
+    timeout = solver_timeout or args.solver_timeout
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    for constraint in constraints:
+        if type(constraint) == bool and not constraint:
+            raise UnsatError
+    if type(constraints) != tuple:
+        constraints = constraints.get_all_constraints()
+    constraints = [c for c in constraints if type(c) != bool]
+    if len(maximize) + len(minimize) == 0:
+        ret_model = model_cache.check_quick_sat(simplify(And(*constraints)).raw)
+        if ret_model:
+            return ret_model
+    model = solver_backend(constraints, minimize, maximize, timeout)
+    model_cache.model_cache.put(model, 1)
+    return model
+
+
+# ------------------------------------------------------------------ Constraints
+def _keccak_conditions():
+    from .keccak_manager import keccak_function_manager
+    return keccak_function_manager.create_conditions()
+
+
+class Constraints(list):
+    def __init__(self, constraint_list: Optional[List] = None):
+        super().__init__(self._get_smt_bool_list(constraint_list or []))
+
+    def is_possible(self, solver_timeout=None) -> bool:
+        try:
+            get_model(self, solver_timeout=solver_timeout)
+        except SolverTimeOutException:
+            return solver_timeout is not None
+        except UnsatError:
+            return False
+        return True
+
+    def get_model(self, solver_timeout=None):
+        try:
+            return get_model(self, solver_timeout=solver_timeout)
+        except (SolverTimeOutException, UnsatError):
+            return None
+
+    def append(self, constraint) -> None:
+        constraint = simplify(constraint) if isinstance(constraint, Bool) else \
+            symbol_factory.Bool(constraint)
+        super().append(constraint)
+
+    @property
+    def as_list(self) -> List[Bool]:
+        return self[:] + [_keccak_conditions()]
+
+    def get_all_constraints(self):
+        return self[:] + [_keccak_conditions()]
+
+    def __copy__(self) -> "Constraints":
+        return Constraints(super().copy())
+
+    def copy(self) -> "Constraints":
+        return self.__copy__()
+
+    def __deepcopy__(self, memodict=None) -> "Constraints":
+        return Constraints(list(self))
+
+    def __add__(self, constraints) -> "Constraints":
+        return Constraints(list(self) + self._get_smt_bool_list(constraints))
+
+    def __iadd__(self, constraints: Iterable) -> "Constraints":
+        super().__iadd__(self._get_smt_bool_list(constraints))
+        return self
+
+    @staticmethod
+    def _get_smt_bool_list(constraints: Iterable) -> List[Bool]:
+        return [c if isinstance(c, Bool) else symbol_factory.Bool(c) for c in constraints]
+
+    def __hash__(self):
+        return tuple(self[:]).__hash__()
+
+    def __eq__(self, other):
+        return isinstance(other, list) and len(self) == len(other) and all(
+            _raw(a) is _raw(b) for a, b in zip(self, other))
