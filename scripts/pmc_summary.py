@@ -27,6 +27,7 @@ def per_kernel(path: Path, counter: str):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"].split("(")[0]
+            name = name.removeprefix("void ").split("<")[0].strip()
             acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
