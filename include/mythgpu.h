@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 2u   /* 2: model tables (arrays, uninterpreted functions) */
+#define MG_ABI_VERSION 3u   /* 2: model tables (arrays, uninterpreted functions)
+                               3: per-lane instruction traces + loop bound        */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -52,6 +53,8 @@ extern "C" {
 #define MG_HOOK           7u  /* yielded before an opcode set in hook_mask      */
 #define MG_ESCAPE         8u  /* needs host semantics; aux = op | reason << 8   */
 #define MG_DEPTH          9u  /* strategy depth cutoff (strategy/__init__.py:29) */
+#define MG_LOOP_BOUND    10u  /* BoundedLoopsStrategy dropped the state at a JUMPDEST
+                                 (bounded_loops.py:119-145); aux = loop count      */
 
 #define MG_EXC_STACK_UNDERFLOW     1u
 #define MG_EXC_STACK_OVERFLOW      2u
@@ -64,6 +67,7 @@ extern "C" {
 #define MG_ESC_MEMORY   2u   /* memory would grow past the lane's page          */
 #define MG_ESC_STORAGE  3u   /* storage slot table full                         */
 #define MG_ESC_STACK    4u   /* stack would grow past the lane's stack_cap      */
+#define MG_ESC_TRACE    5u   /* instruction trace would grow past trace_cap      */
 
 /* lane flags */
 #define MG_LANE_STATIC    1u  /* environment.static (WriteProtection)          */
@@ -116,6 +120,12 @@ typedef struct mg_lane_soa {
     uint32_t *storage;      /* [n][storage_cap][16] key limbs 0..7, value 8..15 */
     uint32_t *ret_offset;   /* [n] RETURN/REVERT data offset (low 32 bits)    */
     uint32_t *ret_len;      /* [n] RETURN/REVERT data length (low 32 bits)    */
+    /* JumpdestCountAnnotation.trace (bounded_loops.py:14-26): the byte address of
+     * every instruction the path has been popped at, when traces are on       */
+    uint32_t trace_cap;     /* entries per lane in `trace` (0: no traces)      */
+    uint32_t _pad2;
+    uint32_t *trace_len;    /* [n]                                             */
+    uint32_t *trace;        /* [n][trace_cap]                                  */
 } mg_lane_soa;
 
 /* Per-call statistics of mg_step. */
@@ -137,6 +147,7 @@ typedef struct mg_batch_cfg {
     uint32_t calldata_cap;  /* bytes                                           */
     uint32_t storage_cap;   /* slots                                           */
     uint32_t coverage;      /* 1: record the per-code coverage bitmap         */
+    uint32_t trace_cap;     /* instruction-trace entries per lane (0: none)   */
 } mg_batch_cfg;
 
 typedef struct mg_ctx mg_ctx;
@@ -179,6 +190,12 @@ int         mg_lanes_reset(mg_ctx *ctx);
  * dropped (0 = unlimited).                                                   */
 int         mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                     uint32_t max_depth, mg_step_stats *stats);
+/* BoundedLoopsStrategy (bounded_loops.py:84-145) on the device: with bound > 0
+ * (and a batch allocated with trace_cap > 0) every instruction a lane is popped
+ * at is appended to its trace, and at a JUMPDEST a lane whose loop count
+ * (get_loop_count) exceeds the bound stops with MG_LOOP_BOUND; creation lanes
+ * only when the count also reaches 128.  0 turns it off.                      */
+int         mg_set_loop_bound(mg_ctx *ctx, uint32_t bound);
 /* Same, with a step horizon: a lane also pauses (stays MG_RUNNING) once its
  * cumulative `steps` reaches `horizon` (0 = none).  The host layer uses it to
  * deliver hook and halt events in the reference's BFS round order

@@ -26,6 +26,10 @@ struct DevLanes {
     uint32_t *calldata;  // [calldata_cap/4][N]
     uint4 *env;          // [5][N][2]
     uint4 *storage;      // [storage_cap][N][4]
+    // instruction traces (BoundedLoopsStrategy): address per popped instruction
+    uint32_t trace_cap;
+    uint32_t *trace_len; // [N]
+    uint32_t *trace;     // [trace_cap][N]
 };
 
 // One loaded code (Disassembly): arrays live in one device arena.

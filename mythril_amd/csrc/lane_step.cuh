@@ -35,6 +35,7 @@ struct OpInfo {
 #define ST_HOOK 7u
 #define ST_ESCAPE 8u
 #define ST_DEPTH 9u
+#define ST_LOOP 10u
 
 #define EXC_UNDERFLOW 1u
 #define EXC_OVERFLOW 2u
@@ -47,6 +48,7 @@ struct OpInfo {
 #define ESC_MEMORY 2u
 #define ESC_STORAGE 3u
 #define ESC_STACK 4u
+#define ESC_TRACE 5u
 
 #define LANE_STATIC 1u
 #define LANE_CREATION 2u
@@ -624,6 +626,55 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
 // The opcodes the fast loop executes itself (when their preconditions hold).
 DEV bool alu_is_fast(uint32_t op) { return op <= 0x03u || op == 0x0bu || (op >= 0x10u && op <= 0x1du); }
 
+// ---- BoundedLoopsStrategy (bounded_loops.py:49-145) ---------------------------
+// The trace holds the byte address of every instruction the path was popped at.
+// get_loop_count: find the latest earlier occurrence (index >= 1) of the last two
+// addresses, take the segment between it and the current JUMPDEST as the key,
+// and count how many consecutive copies of it end the trace, where "equal" is
+// equality of calculate_hash = OR of address << 8k over the segment.  For
+// 16-bit addresses byte k of that hash is lo8(S[k]) | hi8(S[k-1]), so two
+// segments compare in one streaming pass.  Only called at JUMPDESTs.
+__device__ __noinline__ uint32_t loop_count_dev(const uint32_t *__restrict__ T, size_t N, uint32_t n) {
+    if (n < 4u) return 0u;
+    const uint32_t a = T[(size_t)(n - 2u) * N], b = T[(size_t)(n - 1u) * N];
+    int32_t i = (int32_t)n - 3;
+    for (; i >= 1; --i)
+        if (T[(size_t)i * N] == a && T[(size_t)(i + 1) * N] == b) break;
+    if (i < 1) return 0u;
+    const uint32_t size = n - (uint32_t)i - 2u, base = (uint32_t)i + 1u;
+    uint32_t count = 2u;                    // the key segment matches itself
+    for (int32_t j = (int32_t)base - (int32_t)size; j >= 0; j -= (int32_t)size) {
+        uint32_t pj = 0u, pb = 0u;
+        bool eq = true;
+        for (uint32_t k = 0; k <= size; ++k) {
+            const uint32_t xj = k < size ? T[(size_t)((uint32_t)j + k) * N] : 0u;
+            const uint32_t xb = k < size ? T[(size_t)(base + k) * N] : 0u;
+            if (((xj & 0xffu) | (pj >> 8)) != ((xb & 0xffu) | (pb >> 8))) { eq = false; break; }
+            pj = xj;
+            pb = xb;
+        }
+        if (!eq) break;
+        ++count;
+    }
+    return count;
+}
+
+// Append `addr` to the lane's trace; at a JUMPDEST apply the bound.  Returns the
+// new length (bits 0..31), the loop count (32..59) and the outcome (60..61):
+// 0 continue, 1 dropped by the bound, 2 trace full (escape to the host).
+__device__ __noinline__ uint64_t trace_step(uint32_t *__restrict__ trace, size_t N, uint32_t cap, uint32_t lane,
+                                            uint32_t tlen, uint32_t addr, uint32_t jumpdest, uint32_t bound,
+                                            uint32_t creation) {
+    if (tlen >= cap) return (uint64_t)tlen | (2ull << 60);
+    trace[(size_t)tlen * N + lane] = addr;
+    ++tlen;
+    if (!jumpdest) return tlen;
+    const uint32_t count = loop_count_dev(trace + lane, N, tlen);
+    // creation transactions only drop from max(128, bound) on (bounded_loops.py:137-145)
+    const bool drop = creation ? (count > bound && count >= 128u) : count > bound;
+    return (uint64_t)tlen | ((uint64_t)count << 32) | (drop ? (1ull << 60) : 0ull);
+}
+
 // ---- the stepping kernel -------------------------------------------------------
 // At 65,536 lanes there is one wave per SIMD, so a wave's instruction stream is
 // the bound: the loop keeps every per-step dependency on chip and dispatches
@@ -646,7 +697,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           DevCounters *__restrict__ ctr,
                                                           unsigned long long *__restrict__ prof,
                                                           uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
-                                                          uint32_t horizon) {
+                                                          uint32_t horizon, uint32_t loop_bound) {
     // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
     //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
@@ -713,6 +764,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const LaneView V{L, lane, s_win, win, threadIdx.x};
     DevCode C{};
     uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
+    uint32_t tlen = 0;                                    // trace length (BoundedLoops)
+    const uint32_t loop_on = loop_bound;                  // kernel argument: uniform
     uint64_t txlim = 0, glim = 0, gmin = 0, gmax = 0;
     U256 T0 = u_zero(), T1 = u_zero();
     uint2 pd = make_uint2(0u, 0u);
@@ -724,6 +777,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         // accumulate_gas OOG test (instructions.py:162-176): min > 1e9 or min >= tx gas limit
         glim = txlim < MSTATE_GAS_LIMIT + 1ull ? txlim : MSTATE_GAS_LIMIT + 1ull;
         pc = L.pc[lane]; sp = L.sp[lane]; msize = L.msize[lane]; depth = L.depth[lane];
+        if (loop_on) tlen = L.trace_len[lane];
         gmin = L.gas_min[lane]; gmax = L.gas_max[lane];
         for (uint32_t k = 0; k < min(sp, win); ++k) V.set_wstack(k, V.gstack(k));   // window fill
         if (sp >= 1u) T0 = V.stack(sp - 1u);
@@ -760,8 +814,23 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         }                                                                                 \
         const uint32_t k_ = (pd.y >> 17) & 31u, o_ = pd.y & 0xffu;                       \
         const bool hk_ = (pd.y >> 31) && !(hook_ack && executed == 0u);                  \
-        if (hk_ || k_ >= K_ESCAPE || executed >= lane_max ||                              \
-            (max_depth != 0u && depth >= max_depth) || (creation && o_ - 0x35u < 5u)) {   \
+        bool lstop_ = false;                                                              \
+        /* BoundedLoopsStrategy: every instruction the path is popped at (run,   */      \
+        /* hooked or escaped; not a budget pause, not the ACK re-fetch) is traced */     \
+        if (loop_on && k_ != K_END && !(max_depth != 0u && depth >= max_depth) &&        \
+            !(hook_ack && executed == 0u) && (hk_ || executed < lane_max)) {              \
+            const uint64_t tr_ = trace_step(L.trace, L.N, L.trace_cap, lane, tlen,        \
+                                            a32[C.addr_off + pc], o_ == 0x5bu, loop_bound,\
+                                            creation ? 1u : 0u);                          \
+            tlen = (uint32_t)tr_;                                                         \
+            const uint32_t res_ = (uint32_t)(tr_ >> 60);                                  \
+            if (res_ == 1u) { status = ST_LOOP; aux = (uint32_t)(tr_ >> 32) & 0x0fffffffu; \
+                              live = false; lstop_ = true; }                              \
+            else if (res_ == 2u) { status = ST_ESCAPE; aux = o_ | (ESC_TRACE << 8);        \
+                                   live = false; lstop_ = true; }                         \
+        }                                                                                 \
+        if (!lstop_ && (hk_ || k_ >= K_ESCAPE || executed >= lane_max ||                  \
+            (max_depth != 0u && depth >= max_depth) || (creation && o_ - 0x35u < 5u))) {  \
             uint32_t st_ = ST_RUNNING;                                                    \
             if (max_depth != 0u && depth >= max_depth) st_ = ST_DEPTH;                    \
             else if (k_ == K_END) st_ = ST_END;                                           \
@@ -938,6 +1007,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;
+        if (loop_on) L.trace_len[lane] = tlen;
         L.steps[lane] += executed;
         if (n_sha3) L.sha3_count[lane] += n_sha3;
         if (n_exp) L.exp_count[lane] += n_exp;

@@ -36,6 +36,7 @@ struct mg_ctx {
     // lanes
     mg_batch_cfg cfg{};
     bool have_lanes = false, uploaded = false, init_fresh = false;
+    uint32_t loop_bound = 0;             // mg_set_loop_bound (0: BoundedLoops off)
     DevLanes L{};
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
@@ -384,6 +385,10 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     if ((rc = lane_alloc(ctx, L.env, (size_t)MG_ENV_WORDS * N * 2))) return rc;
     if ((rc = lane_alloc(ctx, L.storage, (size_t)L.storage_cap * N * 4))) return rc;
     if ((rc = lane_alloc(ctx, ctx->i_storage, (size_t)L.storage_cap * N * 4))) return rc;
+    L.trace_cap = cfg->trace_cap;
+    if ((rc = lane_alloc(ctx, L.trace_len, N))) return rc;
+    if (L.trace_cap && (rc = lane_alloc(ctx, L.trace, (size_t)L.trace_cap * N))) return rc;
+    HIPX(ctx, hipMemsetAsync(L.trace_len, 0, N * 4, ctx->stream));
     // no lane runs before upload
     HIPX(ctx, hipMemsetAsync(L.status, 0xff, N * 4, ctx->stream));
     HIPX(ctx, hipMemsetAsync(L.sha3_count, 0, N * 4, ctx->stream));
@@ -449,6 +454,7 @@ __global__ void k_reset(DevLanes L, const uint32_t *__restrict__ i_pc, const uin
     L.status[lane] = i_status[lane]; L.aux[lane] = i_aux[lane]; L.steps[lane] = i_steps[lane];
     L.gas_min[lane] = i_gmin[lane]; L.gas_max[lane] = i_gmax[lane];
     L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
+    L.trace_len[lane] = 0;                 // reset images start with empty traces
     const uint32_t cnt = i_cnt[lane];
     L.storage_count[lane] = cnt;
     for (uint32_t s = 0; s < cnt; ++s)
@@ -541,7 +547,8 @@ static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, u
         return set_err(ctx, MG_EINVAL, "lane range [%u,%u) outside batch of %u (host n=%u)", first,
                        first + n, ctx->L.n, h ? h->n : 0);
     if (h->stack_cap > ctx->L.stack_cap || h->mem_cap > ctx->L.mem_cap || h->mem_cap % 4 ||
-        h->calldata_cap > ctx->L.calldata_cap || h->calldata_cap % 4 || h->storage_cap > ctx->L.storage_cap)
+        h->calldata_cap > ctx->L.calldata_cap || h->calldata_cap % 4 || h->storage_cap > ctx->L.storage_cap ||
+        h->trace_cap > ctx->L.trace_cap)
         return set_err(ctx, MG_EINVAL, "host image capacities exceed the batch configuration");
     return MG_OK;
 }
@@ -556,11 +563,13 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
     for (uint32_t i = 0; i < n; ++i) {
         if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
         if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
-            h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap)
+            h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap ||
+            (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u))
             return set_err(ctx, MG_EINVAL, "lane %u: state exceeds its host capacities", first + i);
     }
     bool fresh = true;
-    for (uint32_t i = 0; i < n && fresh; ++i) fresh = h->sp[i] == 0 && h->msize[i] == 0;
+    for (uint32_t i = 0; i < n && fresh; ++i)
+        fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0);
     const size_t S4 = 4, S8 = 8;
     if ((rc = up_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
     if ((rc = up_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
@@ -596,6 +605,12 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
     if ((rc = up_units(ctx, h->storage, n, h->storage_cap, 16, ctx->i_storage, first))) return rc;
     if ((rc = up_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
     if ((rc = up_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
+    if (h->trace_cap) {
+        if ((rc = up_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
+        if ((rc = up_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first))) return rc;
+    } else {
+        HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
+    }
     ctx->uploaded = true;
     ctx->init_fresh = (first == 0 && n == L.n) ? fresh : (ctx->init_fresh && fresh);
     return MG_OK;
@@ -630,6 +645,17 @@ extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, ui
     if ((rc = down_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first))) return rc;
     if ((rc = down_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
     if ((rc = down_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
+    if (h->trace_cap) {
+        if ((rc = down_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        if ((rc = down_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first))) return rc;
+    }
+    return MG_OK;
+}
+
+extern "C" int mg_set_loop_bound(mg_ctx *ctx, uint32_t bound) {
+    if (!ctx) return MG_EINVAL;
+    ctx->loop_bound = bound;
     return MG_OK;
 }
 
@@ -670,6 +696,11 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     uint32_t win = 0, pd_cap = 0, jr_cap = 0;
     size_t lds = 0;
     lds_plan(ctx, win, pd_cap, jr_cap, lds);
+    if (ctx->loop_bound && ctx->L.trace_cap) {
+        // the loop-count hash compares 16-bit byte addresses (EVM code < 64 KiB)
+        for (const DevCode &c : ctx->codes)
+            if (c.n_bytes > 65536u) return set_err(ctx, MG_EINVAL, "loop bound needs codes below 64 KiB");
+    }
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)k_lane_step, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -679,7 +710,8 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     }
     hipLaunchKernelGGL(k_lane_step, dim3(blocks_for(ctx->L.n, LANE_BLOCK)), dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
-                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon);
+                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
+                       ctx->L.trace_cap ? ctx->loop_bound : 0u);
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }

@@ -83,7 +83,7 @@ class GpuDevice:
     # -- lanes ---------------------------------------------------------------
     def alloc(self, shape: LaneShape, coverage: bool = False):
         cfg = native.MgBatchCfg(shape.n, shape.stack_cap, shape.mem_cap, shape.calldata_cap,
-                                shape.storage_cap, 1 if coverage else 0)
+                                shape.storage_cap, 1 if coverage else 0, shape.trace_cap)
         self._check(self.lib.mg_lanes_alloc(self.ctx, ctypes.byref(cfg)), "mg_lanes_alloc")
         self.shape = shape
 
@@ -107,6 +107,10 @@ class GpuDevice:
         soa = batch.soa_range(first, n)
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, n),
                     "mg_lanes_download")
+
+    def set_loop_bound(self, bound: int):
+        """BoundedLoopsStrategy on the device (0 = off); needs trace_cap > 0."""
+        self._check(self.lib.mg_set_loop_bound(self.ctx, int(bound)), "mg_set_loop_bound")
 
     def reset(self):
         self._check(self.lib.mg_lanes_reset(self.ctx), "mg_lanes_reset")

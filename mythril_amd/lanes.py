@@ -20,17 +20,19 @@ import numpy as np
 # ---- constants mirrored from include/mythgpu.h -------------------------------
 MG_RUNNING, MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT = 0, 1, 2, 3
 MG_HALT_END, MG_HALT_DROPPED, MG_VMEXC, MG_HOOK, MG_ESCAPE, MG_DEPTH = 4, 5, 6, 7, 8, 9
+MG_LOOP_BOUND = 10
 STATUS_NAMES = {
     MG_RUNNING: "running", MG_HALT_STOP: "stop", MG_HALT_RETURN: "return",
     MG_HALT_REVERT: "revert", MG_HALT_END: "end", MG_HALT_DROPPED: "dropped",
     MG_VMEXC: "vmexception", MG_HOOK: "hook", MG_ESCAPE: "escape", MG_DEPTH: "depth",
+    MG_LOOP_BOUND: "loop_bound",
 }
 # statuses after which the reference keeps the world state (svm.py:384-389, 452-460)
 WORLD_STATE_KEPT = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_END)
 
 MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
 MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
-MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK = 1, 2, 3, 4
+MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2, 3, 4, 5
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
@@ -74,11 +76,13 @@ class MgLaneSoa(ctypes.Structure):
         ("stack", ctypes.c_void_p), ("memory", ctypes.c_void_p),
         ("storage_count", ctypes.c_void_p), ("storage", ctypes.c_void_p),
         ("ret_offset", ctypes.c_void_p), ("ret_len", ctypes.c_void_p),
+        ("trace_cap", ctypes.c_uint32), ("_pad2", ctypes.c_uint32),
+        ("trace_len", ctypes.c_void_p), ("trace", ctypes.c_void_p),
     ]
 
 
 _U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
-               "calldata_len", "storage_count", "ret_offset", "ret_len")
+               "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len")
 _U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
 
 
@@ -89,6 +93,7 @@ class LaneShape:
     mem_cap: int = 1024
     calldata_cap: int = 128
     storage_cap: int = 16
+    trace_cap: int = 0
 
     def __post_init__(self):
         if self.mem_cap % 32:
@@ -112,6 +117,7 @@ class LaneBatch:
         self.stack = np.zeros((n, shape.stack_cap, 8), dtype=np.uint32)
         self.memory = np.zeros((n, shape.mem_cap), dtype=np.uint8)
         self.storage = np.zeros((n, shape.storage_cap, 16), dtype=np.uint32)
+        self.trace = np.zeros((n, max(shape.trace_cap, 1)), dtype=np.uint32)
 
     @property
     def n(self) -> int:
@@ -123,7 +129,9 @@ class LaneBatch:
         s.n = self.shape.n
         s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
         s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
-        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+        s.trace_cap = self.shape.trace_cap
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
+                                              "trace"):
             arr = getattr(self, f)
             assert arr.flags["C_CONTIGUOUS"]
             setattr(s, f, arr.ctypes.data)
@@ -139,7 +147,9 @@ class LaneBatch:
         s.n = n
         s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
         s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
-        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+        s.trace_cap = self.shape.trace_cap
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
+                                              "trace"):
             arr = getattr(self, f)
             setattr(s, f, arr.ctypes.data + first * arr.strides[0])
         self._keep_range = s
@@ -147,7 +157,8 @@ class LaneBatch:
 
     def copy(self) -> "LaneBatch":
         out = LaneBatch(self.shape)
-        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage"):
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
+                                              "trace"):
             getattr(out, f)[...] = getattr(self, f)
         return out
 
@@ -221,7 +232,7 @@ class LaneBatch:
 
 # Fields compared lane-by-lane in parity tests (device vs oracle).
 PARITY_SCALARS = ("pc", "sp", "msize", "depth", "status", "aux", "steps", "gas_min",
-                  "gas_max", "storage_count")
+                  "gas_max", "storage_count", "trace_len")
 
 
 def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = None,
@@ -247,13 +258,18 @@ def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = No
             out.append(f"lane {i}: memory differs")
         if a.storage_dict(i, drop_zero=False) != b.storage_dict(i, drop_zero=False):
             out.append(f"lane {i}: storage differs")
+        tl = int(a.trace_len[i])
+        if a.shape.trace_cap and tl == int(b.trace_len[i]) and \
+                not np.array_equal(a.trace[i, :tl], b.trace[i, :tl]):
+            out.append(f"lane {i}: trace differs")
         if int(a.status[i]) in (MG_HALT_RETURN, MG_HALT_REVERT):
             if (a.ret_offset[i], a.ret_len[i]) != (b.ret_offset[i], b.ret_len[i]):
                 out.append(f"lane {i}: return range differs")
     return out
 
 
-_ALL_FIELDS = _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage")
+_ALL_FIELDS = _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
+                                           "trace")
 
 
 def bucket_order(batch: LaneBatch) -> np.ndarray:

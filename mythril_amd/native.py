@@ -56,7 +56,8 @@ class MgStepStats(ctypes.Structure):
 class MgBatchCfg(ctypes.Structure):
     _fields_ = [("n_lanes", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32),
                 ("mem_cap", ctypes.c_uint32), ("calldata_cap", ctypes.c_uint32),
-                ("storage_cap", ctypes.c_uint32), ("coverage", ctypes.c_uint32)]
+                ("storage_cap", ctypes.c_uint32), ("coverage", ctypes.c_uint32),
+                ("trace_cap", ctypes.c_uint32)]
 
 
 class MgDagBatch(ctypes.Structure):
@@ -91,6 +92,7 @@ SIGNATURES = {
     "mg_step": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_async": (_I, [_P, _P, _U32, _U32]),
     "mg_step_until": (_I, [_P, _P, _U32, _U32, _U32, ctypes.POINTER(MgStepStats)]),
+    "mg_set_loop_bound": (_I, [_P, _U32]),
     "mg_eval_bits": (_I, [_P, ctypes.POINTER(MgDagBatch), ctypes.POINTER(MgModelBatch), _P, _P, _P,
                           ctypes.POINTER(ctypes.c_float)]),
     "mg_step_profile": (_I, [_P, _P, _U32, _U32, _P, _P]),

@@ -205,7 +205,38 @@ typedef struct {
     uint32_t max_steps;
     uint32_t max_depth;     /* 0 = unlimited */
     uint32_t horizon;       /* stop when the lane's cumulative steps reach it; 0 = none */
+    uint32_t loop_bound;    /* BoundedLoopsStrategy bound; 0 = off */
 } orc_params;
+
+/* bounded_loops.py:49-113 restated literally: calculate_hash(i, j) is the OR of
+ * trace[itr] << 8 (itr - i), kept here as a little-endian byte string so any
+ * address width compares exactly (the device streams 16-bit addresses). */
+static void seg_hash(const uint32_t *t, uint32_t a, uint32_t b, uint8_t *out, size_t cap) {
+    memset(out, 0, cap);
+    for (uint32_t itr = a; itr < b; ++itr)
+        for (int k = 0; k < 4; ++k) out[(itr - a) + k] |= (uint8_t)(t[itr] >> (8 * k));
+}
+
+uint32_t orc_loop_count(const uint32_t *t, uint32_t n) {
+    int64_t i;
+    int found = 0;
+    for (i = (int64_t)n - 3; i > 0; --i)
+        if (t[i] == t[n - 2] && t[i + 1] == t[n - 1]) { found = 1; break; }
+    if (!found) return 0;
+    const uint32_t size = n - (uint32_t)i - 2;
+    const size_t cap = (size_t)size + 4;
+    uint8_t *key = (uint8_t *)malloc(cap), *cur = (uint8_t *)malloc(cap);
+    seg_hash(t, (uint32_t)i + 1, n - 1, key, cap);
+    uint32_t count = 1;
+    for (int64_t j = i + 1; j >= 0; j -= size) {
+        seg_hash(t, (uint32_t)j, (uint32_t)j + size, cur, cap);
+        if (memcmp(cur, key, cap) != 0) break;
+        count++;
+    }
+    free(key);
+    free(cur);
+    return count;
+}
 
 typedef struct {       /* working view of one lane */
     const mg_lane_soa *h;
@@ -320,11 +351,30 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         if (pc >= c->n_instr) { h->status[i] = MG_HALT_END; break; }
         const uint8_t op = c->op[pc];
         const uint32_t flags = h->flags[i];
-        if (((p->hook_mask[op >> 6] >> (op & 63)) & 1) && !((flags & MG_LANE_HOOK_ACK) && done == 0)) {
-            h->status[i] = MG_HOOK; h->aux[i] = op; break;
+        const int acked = (flags & MG_LANE_HOOK_ACK) && done == 0;
+        const int hooked = ((p->hook_mask[op >> 6] >> (op & 63)) & 1) && !acked;
+        const int budget = done >= p->max_steps || ((flags & MG_LANE_STEP1) && done >= 1) ||
+                           (p->horizon && h->steps[i] >= p->horizon);
+        /* BoundedLoopsStrategy.get_strategic_global_state (bounded_loops.py:115-145):
+         * the state is popped -> its address joins the trace -> at a JUMPDEST the
+         * loop count may drop it, before any hook runs.  A budget pause is not a
+         * pop, and the re-fetch after a hook ACK is the same pop. */
+        if (p->loop_bound && h->trace_cap && !acked && (hooked || !budget)) {
+            uint32_t *tr = h->trace + (size_t)i * h->trace_cap;
+            if (h->trace_len[i] >= h->trace_cap) {
+                h->status[i] = MG_ESCAPE; h->aux[i] = op | (MG_ESC_TRACE << 8); break;
+            }
+            tr[h->trace_len[i]++] = c->addr[pc];
+            if (op == 0x5b) {
+                const uint32_t cnt = orc_loop_count(tr, h->trace_len[i]);
+                const int creation = (flags & MG_LANE_CREATION) != 0;
+                if (creation ? (cnt > p->loop_bound && cnt >= 128) : cnt > p->loop_bound) {
+                    h->status[i] = MG_LOOP_BOUND; h->aux[i] = cnt; break;
+                }
+            }
         }
-        if (done >= p->max_steps || ((flags & MG_LANE_STEP1) && done >= 1) ||
-            (p->horizon && h->steps[i] >= p->horizon)) break;
+        if (hooked) { h->status[i] = MG_HOOK; h->aux[i] = op; break; }
+        if (budget) break;
         if (is_env_escape(op) ||
             ((flags & MG_LANE_CREATION) && op >= 0x35 && op <= 0x39)) {
             /* creation lanes: CALLDATALOAD/SIZE/COPY and CODESIZE/COPY follow the
@@ -617,18 +667,23 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
 }
 
 /* Step lanes [first, first+n) of a host image.  Returns the lane-steps. */
-uint64_t orc_run_until(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
-                       uint32_t max_steps, uint32_t max_depth, uint32_t horizon) {
+uint64_t orc_run_loop(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
+                      uint32_t max_steps, uint32_t max_depth, uint32_t horizon, uint32_t loop_bound) {
     init_optable();
     orc_params p;
     memcpy(p.hook_mask, hook_mask, sizeof p.hook_mask);
-    p.max_steps = max_steps; p.max_depth = max_depth; p.horizon = horizon;
+    p.max_steps = max_steps; p.max_depth = max_depth; p.horizon = horizon; p.loop_bound = loop_bound;
     uint64_t total = 0;
     for (uint32_t i = first; i < first + n; ++i) {
         if (h->code_id[i] >= (uint32_t)n_codes) { h->status[i] = MG_ESCAPE; continue; }
         total += run_lane(h, i, &p);
     }
     return total;
+}
+
+uint64_t orc_run_until(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],
+                       uint32_t max_steps, uint32_t max_depth, uint32_t horizon) {
+    return orc_run_loop(h, first, n, hook_mask, max_steps, max_depth, horizon, 0);
 }
 
 uint64_t orc_run(const mg_lane_soa *h, uint32_t first, uint32_t n, const uint64_t hook_mask[4],

@@ -43,9 +43,15 @@ class OracleEVM:
 
     def run(self, batch, first: int = 0, n: Optional[int] = None,
             hook_mask: Sequence[int] = (0, 0, 0, 0), max_steps: int = 1 << 30,
-            max_depth: int = 0, horizon: int = 0) -> int:
+            max_depth: int = 0, horizon: int = 0, loop_bound: int = 0) -> int:
         n = batch.n - first if n is None else n
         mask = (ctypes.c_uint64 * 4)(*[int(x) for x in hook_mask])
         soa = batch.soa()
-        return int(lib().orc_run_until(ctypes.addressof(soa), first, n, mask, max_steps, max_depth,
-                                       horizon))
+        return int(lib().orc_run_loop(ctypes.addressof(soa), first, n, mask, max_steps, max_depth,
+                                      horizon, loop_bound))
+
+
+def loop_count(trace) -> int:
+    """oracle/evm_ref.c orc_loop_count (literal get_loop_count)."""
+    arr = np.ascontiguousarray(np.asarray(trace, dtype=np.uint32))
+    return int(lib().orc_loop_count(arr.ctypes.data, arr.size))

@@ -254,3 +254,98 @@ def test_deep_stack_window_edges(dev):
     assert not diff_batches(out, ref)
     assert (out.sp > 16).any()
     assert (out.steps > 100).mean() > 0.5
+
+
+# ------------------------------------------------------------ BoundedLoopsStrategy
+from test_loop_bound import LOOP, loop_batch  # noqa: E402
+
+
+def run_both_loop(dev, codes, batch, bound, hook_mask=None):
+    dev.set_loop_bound(bound)
+    try:
+        o = OracleEVM()
+        ids = [dev.load_code(c) for c in codes]
+        oids = [o.load_code(c) for c in codes]
+        g = batch.copy()
+        g.code_id[:] = np.array(ids, dtype=np.uint32)[batch.code_id]
+        r = batch.copy()
+        r.code_id[:] = np.array(oids, dtype=np.uint32)[batch.code_id]
+        dev.alloc(batch.shape)
+        dev.upload(g)
+        dev.step(hook_mask)
+        out = LaneBatch(batch.shape)
+        dev.download(out)
+        out.code_id[:] = batch.code_id
+        o.run(r, hook_mask=hook_mask or (0, 0, 0, 0), loop_bound=bound)
+        r.code_id[:] = batch.code_id
+        return out, r
+    finally:
+        dev.set_loop_bound(0)
+
+
+@pytest.mark.parametrize("bound", [1, 3, 10])
+def test_loop_bound_device_equals_oracle(dev, bound):
+    from mythril_amd.lanes import MG_ESCAPE, MG_LOOP_BOUND
+    rng = random.Random(bound)
+    ns = [rng.choice([rng.randrange(0, 40), rng.randrange(0, 200), 2 ** 255]) for _ in range(3000)]
+    b = loop_batch(ns, trace_cap=96 if bound < 10 else 48)
+    out, ref = run_both_loop(dev, [LOOP], b, bound)
+    assert not diff_batches(out, ref, limit=20)
+    st = out.status
+    assert (st == MG_HALT_STOP).sum() > 0
+    if bound < 10:
+        assert (st == MG_LOOP_BOUND).sum() > 0
+    else:
+        assert (st == MG_ESCAPE).sum() > 0    # a 48-entry trace fills before 11 iterations
+
+
+def test_loop_bound_with_hooks_traces_each_pop_once(dev):
+    """A lane stopped at a hooked JUMPDEST and resumed with HOOK_ACK is traced
+    once: the hook-by-hook run ends where the uninterrupted run ends."""
+    from mythril_amd.lanes import MG_LANE_HOOK_ACK
+    ns = list(range(0, 9)) * 20
+    b = loop_batch(ns, trace_cap=128)
+    whole, _ = run_both_loop(dev, [LOOP], b, 3)
+    mask = hook_mask_for([0x5B])
+    cur, ref = run_both_loop(dev, [LOOP], b, 3, hook_mask=mask)
+    assert not diff_batches(cur, ref)
+    for _ in range(200):
+        if not (cur.status == MG_HOOK).any():
+            break
+        for x in (cur, ref):
+            h = x.status == MG_HOOK
+            x.status[h] = MG_RUNNING
+            x.flags[h] |= np.uint32(MG_LANE_HOOK_ACK)
+        cur, ref2 = run_both_loop(dev, [LOOP], cur, 3, hook_mask=mask)
+        o = OracleEVM()
+        o.load_code(LOOP)
+        ref.code_id[:] = 0
+        o.run(ref, hook_mask=mask, loop_bound=3)
+        assert not diff_batches(cur, ref)
+        for x in (cur, ref):
+            x.flags[:] &= ~np.uint32(MG_LANE_HOOK_ACK)
+    for f in ("status", "pc", "steps", "trace_len", "aux"):
+        assert np.array_equal(getattr(cur, f), getattr(whole, f)), f
+
+
+def test_loop_bound_vmtests_and_c2(dev, c2):
+    vectors = [v for v in load_vmtests() if not v["ignored"]]
+    shape = vm_shape(vectors)
+    shape.trace_cap = 4096
+    b = LaneBatch(shape)
+    codes, index = [], {}
+    for i, v in enumerate(vectors):
+        if v["code"] not in index:
+            index[v["code"]] = len(codes)
+            codes.append(bytes.fromhex(v["code"]))
+        fill_lane(b, i, v, index[v["code"]])
+    out, ref = run_both_loop(dev, codes, b, 3)
+    assert not diff_batches(out, ref, limit=20)
+    cb = workloads.c2_batch(8192, seed=99, stack_cap=64, mem_cap=1024)
+    cb2 = LaneBatch(LaneShape(n=cb.n, stack_cap=64, mem_cap=1024, calldata_cap=96, storage_cap=16,
+                              trace_cap=512))
+    for f in ("code_id", "pc", "status", "calldata_len", "storage_count", "gas_limit",
+              "calldata", "env", "storage"):
+        getattr(cb2, f)[...] = getattr(cb, f)
+    out, ref = run_both_loop(dev, [c2], cb2, 2)
+    assert not diff_batches(out, ref, limit=20)
