@@ -74,7 +74,8 @@ extern "C" {
 #define MG_LANE_CREATION  2u  /* ContractCreationTransaction: CODE and CALLDATA ops escape */
 #define MG_LANE_HOOK_ACK  4u  /* the host has fired the hooks of the instruction at pc:
                                  the first instruction of the next mg_step call runs
-                                 even if its opcode is set in hook_mask            */
+                                 even if its opcode is set in hook_mask; cleared by
+                                 the device once that instruction has executed     */
 #define MG_LANE_STEP1     8u  /* execute at most one instruction per mg_step call
                                  (the host fires post-hooks on the successor)     */
 

@@ -1008,6 +1008,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;
         if (loop_on) L.trace_len[lane] = tlen;
+        // HOOK_ACK covers one instruction: consumed once the lane has executed
+        if (hook_ack && executed > 0u) L.flags[lane] = flags & ~LANE_HOOK_ACK;
         L.steps[lane] += executed;
         if (n_sha3) L.sha3_count[lane] += n_sha3;
         if (n_exp) L.exp_count[lane] += n_exp;

@@ -5,11 +5,13 @@ from .plugins import InstructionCoveragePlugin, LaserPlugin
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import (Account, Environment, GlobalState, MachineStack, MachineState, Memory,
                     Storage, WorldState)
-from .strategy import BreadthFirstSearchStrategy, DepthFirstSearchStrategy
+from .strategy import (BoundedLoopsStrategy, BreadthFirstSearchStrategy, DepthFirstSearchStrategy,
+                       JumpdestCountAnnotation)
 from .svm import LaserEVM
 from .transaction import MessageCallTransaction, execute_message_call, tx_id_manager
 
-__all__ = ["Account", "BreadthFirstSearchStrategy", "DepthFirstSearchStrategy", "Disassembly",
+__all__ = ["Account", "BoundedLoopsStrategy", "BreadthFirstSearchStrategy",
+           "JumpdestCountAnnotation", "DepthFirstSearchStrategy", "Disassembly",
            "Environment", "GlobalState", "InstructionCoveragePlugin", "LaserEVM", "LaserPlugin",
            "MachineStack", "MachineState", "Memory", "MessageCallTransaction",
            "PluginSkipState", "PluginSkipWorldState", "Storage", "WorldState", "disassemble",

@@ -43,3 +43,61 @@ class DepthFirstSearchStrategy(BasicSearchStrategy):
 
 class BreadthFirstSearchStrategy(BasicSearchStrategy):
     order = "bfs"
+
+
+class JumpdestCountAnnotation:
+    """bounded_loops.py:14-26: the addresses of the instructions the path was
+    popped at.  While the path runs on kernel 1 the trace lives in the lane's
+    device buffer; it is written back here whenever the state is materialised."""
+
+    def __init__(self):
+        self._reached_count = {}
+        self.trace: List[int] = []
+
+    def __copy__(self):
+        out = JumpdestCountAnnotation()
+        out._reached_count = dict(self._reached_count)
+        out.trace = list(self.trace)
+        return out
+
+
+class BoundedLoopsStrategy(BasicSearchStrategy):
+    """bounded_loops.py:29-145 as a strategy extension
+    (``laser.extend_strategy(BoundedLoopsStrategy, loop_bound=3)``).  The trace
+    append and the loop count at every JUMPDEST run on the device
+    (mg_set_loop_bound); a dropped path stops with MG_LOOP_BOUND and is never
+    returned to the execution loop, as the reference's ``continue`` skips it."""
+
+    def __init__(self, super_strategy: BasicSearchStrategy, **kwargs):
+        self.super_strategy = super_strategy
+        self.bound = kwargs["loop_bound"]
+        self.order = getattr(super_strategy, "order", "bfs")
+        BasicSearchStrategy.__init__(self, super_strategy.work_list, super_strategy.max_depth,
+                                     **kwargs)
+
+    def drain(self) -> List:
+        return self.super_strategy.drain()
+
+    @staticmethod
+    def get_loop_count(trace: List[int]) -> int:
+        """get_loop_count of a host-held trace (the device computes the same
+        count at every JUMPDEST).  Segments are compared by their OR-of-shifted
+        hash one byte at a time: byte k is lo8(S[k]) | hi8(S[k-1]) for 16-bit
+        addresses (EVM code is < 64 KiB)."""
+        n = len(trace)
+        last2 = (trace[-2], trace[-1]) if n >= 2 else None
+        start = next((i for i in range(n - 3, 0, -1) if (trace[i], trace[i + 1]) == last2), None)
+        if start is None:
+            return 0
+        base, size = start + 1, n - start - 2
+
+        def hash_bytes(at):
+            seg = trace[at: at + size] + [0]
+            return [(seg[k] & 0xFF) | ((seg[k - 1] >> 8) if k else 0) for k in range(size + 1)]
+
+        key = hash_bytes(base)
+        count, j = 2, base - size
+        while j >= 0 and hash_bytes(j) == key:
+            count += 1
+            j -= size
+        return count

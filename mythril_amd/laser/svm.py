@@ -42,7 +42,8 @@ from typing import Callable, DefaultDict, Dict, List, Optional, Tuple
 import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
-                     MG_ESC_STACK, MG_ESC_STORAGE, MG_EXC_STACK_UNDERFLOW, MG_HALT_DROPPED,
+                     MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_EXC_STACK_UNDERFLOW,
+                     MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
                      limbs_to_word, word_to_limbs)
@@ -50,7 +51,7 @@ from ..smt.expr import symbol_factory
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
-from .strategy import DepthFirstSearchStrategy
+from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
 
 log = logging.getLogger(__name__)
 
@@ -299,6 +300,10 @@ class LaserEVM:
         slots = max((len(s.environment.active_account.storage.printable_storage) for s in states),
                     default=0)
         cdl = max((len(s.environment.calldata) for s in states), default=0)
+        trace_cap = 0
+        if self._loop_bound():
+            tl = max((len(_trace_of(s)) for s in states), default=0)
+            trace_cap = max(4096 * g, 2 * tl)
         stack_cap = 1024 if n <= 4096 else min(1024, 128 * g)
         mem_cap = max(4096 * g, 2 * msz)
         mem_cap = min(mem_cap, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
@@ -306,7 +311,7 @@ class LaserEVM:
         mem_cap = (mem_cap + 31) // 32 * 32
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
-                         storage_cap=max(64 * g, 2 * slots + 16))
+                         storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap)
 
     def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
         env, ms = s.environment, s.mstate
@@ -345,6 +350,11 @@ class LaserEVM:
             b.storage[i, k, 8:] = word_to_limbs(val)
         b.storage_count[i] = len(slots)
         b.ret_offset[i] = b.ret_len[i] = 0
+        if b.shape.trace_cap:
+            tr = _trace_of(s)
+            b.trace[i] = 0
+            b.trace[i, : len(tr)] = tr
+            b.trace_len[i] = len(tr)
 
     def _materialise(self, b: LaneBatch, i: int, s: GlobalState) -> GlobalState:
         """Write lane i of the host image back into its GlobalState (in place)."""
@@ -362,7 +372,13 @@ class LaserEVM:
         for k in range(int(b.storage_count[i])):
             store[limbs_to_word(b.storage[i, k, :8])] = limbs_to_word(b.storage[i, k, 8:])
         s.lane_steps = int(b.steps[i])
+        if b.shape.trace_cap:
+            ann = _annotation_of(s)
+            ann.trace = [int(x) for x in b.trace[i, : int(b.trace_len[i])]]
         return s
+
+    def _loop_bound(self) -> int:
+        return int(getattr(self.strategy, "bound", 0) or 0)
 
     # ------------------------------------------------------------- the batch loop
     def _run_batch(self, states: List[GlobalState], final_states: List[GlobalState], create: bool,
@@ -377,6 +393,7 @@ class LaserEVM:
             b.steps[i] = 0
         dev.alloc(shape, coverage=self.record_coverage)
         dev.upload(b)
+        dev.set_loop_bound(self._loop_bound())
         mask = _mask(self._hooked_ops())
         depth = 0 if self.max_depth == _INF else int(self.max_depth)
         bfs = getattr(self.strategy, "order", "bfs") == "bfs"
@@ -532,12 +549,18 @@ class LaserEVM:
                     hook(s, tx, None, False)
         elif status == MG_HALT_DROPPED:
             pass
-        elif status == MG_DEPTH:
+        elif status in (MG_DEPTH, MG_LOOP_BOUND):
             return                  # the strategy skips it: not a final state
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
-            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK):
-                regrow.append(s)    # rerun with larger lane capacities
+            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE):
+                # rerun with larger lane capacities; the instruction was traced
+                # at its pop but not executed, and will be traced again
+                if reason != MG_ESC_TRACE and b.shape.trace_cap:
+                    ann = _annotation_of(s)
+                    if ann.trace:
+                        ann.trace.pop()
+                regrow.append(s)
                 return
             if self.escape_handler is None:
                 log.debug("Encountered unimplemented instruction %s", name)
@@ -563,6 +586,22 @@ class LaserEVM:
                     bits[pc] = True
             out[self._code_objs[raw].bytecode] = (int(bits.size), bits.tolist())
         return out
+
+
+def _annotation_of(state: GlobalState) -> JumpdestCountAnnotation:
+    for a in state.annotations:
+        if isinstance(a, JumpdestCountAnnotation):
+            return a
+    a = JumpdestCountAnnotation()
+    state.annotate(a)
+    return a
+
+
+def _trace_of(state: GlobalState) -> List[int]:
+    for a in state.annotations:
+        if isinstance(a, JumpdestCountAnnotation):
+            return a.trace
+    return []
 
 
 def _mask(ops) -> List[int]:

@@ -676,7 +676,10 @@ uint64_t orc_run_loop(const mg_lane_soa *h, uint32_t first, uint32_t n, const ui
     uint64_t total = 0;
     for (uint32_t i = first; i < first + n; ++i) {
         if (h->code_id[i] >= (uint32_t)n_codes) { h->status[i] = MG_ESCAPE; continue; }
-        total += run_lane(h, i, &p);
+        const uint32_t done = run_lane(h, i, &p);
+        /* HOOK_ACK covers one instruction: consumed once the lane has executed */
+        if (done && (h->flags[i] & MG_LANE_HOOK_ACK)) h->flags[i] &= ~MG_LANE_HOOK_ACK;
+        total += done;
     }
     return total;
 }

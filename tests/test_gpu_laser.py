@@ -280,3 +280,46 @@ def test_coverage_plugin_matches_oracle(dev):
     (nins, bits), = [v for k, v in plugin.coverage.items()]
     assert nins == ops.size
     assert bits == covered.tolist()
+
+
+# ------------------------------------------------------------ BoundedLoopsStrategy
+def _loop_states(vm, ns):
+    from test_loop_bound import LOOP
+    for n in ns:
+        ws = WorldState()
+        acct = Account(0xC0DE, code=Disassembly(LOOP))
+        ws.put_account(acct)
+        tx = MessageCallTransaction(world_state=ws, callee_account=acct, caller=0xCA11,
+                                    call_data=int(n).to_bytes(32, "big"), gas_price=1,
+                                    gas_limit=10 ** 7, origin=0xCA11, call_value=0)
+        _setup_global_state_for_execution(vm, tx)
+    return list(vm.work_list)
+
+
+@pytest.mark.parametrize("hooked", [False, True])
+def test_bounded_loops_strategy_drops_like_the_oracle(dev, hooked):
+    from mythril_amd.laser import BoundedLoopsStrategy, JumpdestCountAnnotation
+    from test_loop_bound import LOOP, loop_batch
+    ns = list(range(0, 12)) + [50, 2 ** 100]
+    b = loop_batch(ns)
+    o = OracleEVM()
+    b.code_id[:] = o.load_code(LOOP)
+    o.run(b, loop_bound=3)
+    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
+    seen = []
+    if hooked:
+        vm.register_hooks("pre", {"JUMPDEST": [lambda s: seen.append(s.mstate.pc)]})
+    states = _loop_states(vm, ns)
+    final = vm.exec(track_gas=True)
+    halted = [i for i in range(len(ns)) if int(b.status[i]) == 1]
+    assert len(vm.open_states) == len(halted)
+    assert {id(s) for s in final} == {id(states[i]) for i in halted}
+    for i in halted:
+        ann = [a for a in states[i].annotations if isinstance(a, JumpdestCountAnnotation)]
+        assert ann and ann[0].trace == [int(x) for x in b.trace[i, : int(b.trace_len[i])]]
+    if hooked:
+        # every JUMPDEST pop that survived the bound fired the hook once
+        assert len(seen) == sum(1 for i in range(len(ns))
+                                for x in b.trace[i, : int(b.trace_len[i])] if x == 3) \
+            - sum(1 for i in range(len(ns)) if int(b.status[i]) == 10)

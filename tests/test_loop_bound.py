@@ -15,11 +15,13 @@ from vmtests_util import load_json
 
 
 def test_loop_count_reference_vectors():
+    from mythril_amd.laser import BoundedLoopsStrategy
     vecs = load_json("loop_count.json")
     assert len(vecs) >= 5
     for v in vecs:
         assert loopref.loop_count(v["trace"]) == v["count"]
         assert loop_count(v["trace"]) == v["count"]
+        assert BoundedLoopsStrategy.get_loop_count(v["trace"]) == v["count"]
 
 
 def _random_trace(rng):
@@ -36,9 +38,11 @@ def _random_trace(rng):
 
 def test_c_loop_count_equals_python_restatement():
     rng = random.Random(2718)
+    from mythril_amd.laser import BoundedLoopsStrategy
     for _ in range(3000):
         t = _random_trace(rng)
         assert loop_count(t) == loopref.loop_count(t), t
+        assert BoundedLoopsStrategy.get_loop_count(t) == loopref.loop_count(t), t
 
 
 # PUSH1 0 CALLDATALOAD; loop: JUMPDEST PUSH1 1 SWAP1 SUB DUP1 PUSH1 3 JUMPI; STOP
