@@ -688,6 +688,9 @@ __device__ __noinline__ uint64_t trace_step(uint32_t *__restrict__ trace, size_t
 //     the rest in HBM;
 //   * common opcodes run inline; the rest (and any lane whose preconditions
 //     fail) go through slow_step, outside the loop's register allocation.
+// kLoop: BoundedLoopsStrategy traces on (a separate instantiation, so the common
+// case carries no trace call site in its loop)
+template <bool kLoop>
 __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
                                                           const uint8_t *__restrict__ a8,
                                                           const uint32_t *__restrict__ a32,
@@ -765,7 +768,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     DevCode C{};
     uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
     uint32_t tlen = 0;                                    // trace length (BoundedLoops)
-    const uint32_t loop_on = loop_bound;                  // kernel argument: uniform
+    const uint32_t loop_on = kLoop ? loop_bound : 0u;     // kernel argument: uniform
     uint64_t txlim = 0, glim = 0, gmin = 0, gmax = 0;
     U256 T0 = u_zero(), T1 = u_zero();
     uint2 pd = make_uint2(0u, 0u);
@@ -855,8 +858,6 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (!(live && pd.y == uy)) continue;
 
         const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
-        const uint32_t npop = (uk >> 12) & 15u, need = max((uk >> 8) & 15u, npop);
-        const bool push = ((uk >> 16) & 1u) != 0u;
         if (cov_on) {
             if (sflag) s_cov[pc] = 1;
             else cov[C.cov_off + pc] = 1;
@@ -864,124 +865,154 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (prof) atomicAdd(&s_prof[op], 1u);
         ++executed;
 
-        // ---- fast path: result and preconditions, no writes ----
-        bool fast = true, ok = sp >= need;
-        U256 res;
-        uint32_t npc = pc + 1u, ndepth = depth;
-        uint64_t ngmin = gmin + (ux & 0xffffu), ngmax = gmax + (ux >> 16);
-        bool gas_check = true;
-        const U256 &a = T0, &b = T1;
+        // ---- fast path: every case checks its preconditions per lane and, when
+        // they hold, applies the whole instruction itself; a lane whose checks
+        // fail (and every other opcode) runs the general handler below ----
+        const uint64_t ngmin = gmin + (ux & 0xffffu), ngmax = gmax + (ux >> 16);
+        const bool gas_ok = ngmin < glim;
+        bool ok = false;
+        // push `v` (table gas): T1 moves below the register window
+#define PUSHV(v_) do { const U256 pv_ = (v_);                                   \
+            if (sp >= 2u) V.set_stack(sp - 2u, T1);                          \
+            T1 = T0; T0 = pv_; ++sp; ++pc; gmin = ngmin; gmax = ngmax; } while (0)
         switch (kind) {
         case K_PUSH:
-            res = sflag ? ld_word((const l_u4 *)s_push, pc)
-                        : ld_word(gv(a32 + C.push_off), pc);
+            ok = gas_ok && sp + 1u <= stack_lim;
+            if (ok) PUSHV(sflag ? ld_word((const l_u4 *)s_push, pc) : ld_word(gv(a32 + C.push_off), pc));
             break;
         case K_DUP: {
             const uint32_t k = op - 0x7fu;
-            ok = ok && sp >= k;
-            if (k == 1u) res = a;
-            else if (k == 2u) res = b;
-            else res = V.stack(ok ? sp - k : 0u);
+            ok = gas_ok && sp >= k && sp + 1u <= stack_lim;
+            if (ok) PUSHV(k == 1u ? T0 : k == 2u ? T1 : V.stack(sp - k));
             break;
         }
-        case K_SWAP:
-            ok = ok && sp >= op - 0x8eu;
+        case K_SWAP: {
+            const uint32_t k = op - 0x8fu;
+            ok = gas_ok && sp >= k + 1u;
+            if (ok) {
+                if (k == 1u) {
+                    const U256 t = T0; T0 = T1; T1 = t;
+                } else {
+                    const U256 x = V.stack(sp - 1u - k);
+                    V.set_stack(sp - 1u - k, T0);
+                    T0 = x;
+                }
+                ++pc; gmin = ngmin; gmax = ngmax;
+            }
             break;
-        case K_POP: case K_JUMPDEST:
+        }
+        case K_POP:
+            ok = gas_ok && sp >= 1u;
+            if (ok) {
+                T0 = T1;
+                T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                --sp; ++pc; gmin = ngmin; gmax = ngmax;
+            }
             break;
-        case K_JUMP: case K_JUMPI: {
-            gas_check = false;
-            const uint32_t add = kind == K_JUMP ? 8u : 10u;
-            ngmin = gmin + add; ngmax = gmax + add;
-            const bool take = kind == K_JUMP || !u_iszero(b);
-            if (kind == K_JUMPI) ++ndepth;
+        case K_JUMPDEST:
+            ok = gas_ok;
+            if (ok) { ++pc; gmin = ngmin; gmax = ngmax; }
+            break;
+        case K_JUMP: case K_JUMPI: {   // gas 8 / 10 by hand, no OOG check
+            const bool jumpi = kind == K_JUMPI;
+            const bool take = !jumpi || !u_iszero(T1);
+            uint32_t npc = pc + 1u;
+            ok = sp >= (jumpi ? 2u : 1u);
             if (take) {
                 uint32_t idx = MG_JRES_NONE;
-                if (u_fits32(a) && a.w[0] < C.n_jres) {
-                    if (jflag) { idx = s_jr[a.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
-                    else idx = a32[C.jres_off + a.w[0]];
+                if (u_fits32(T0) && T0.w[0] < C.n_jres) {
+                    if (jflag) { idx = s_jr[T0.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
+                    else idx = a32[C.jres_off + T0.w[0]];
                 }
                 ok = ok && idx != MG_JRES_NONE &&
                      (sflag ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu;
                 npc = idx;
             }
+            if (ok) {
+                const uint32_t add = jumpi ? 10u : 8u;
+                gmin += add; gmax += add;
+                if (jumpi) {
+                    ++depth;
+                    T0 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                    T1 = sp >= 4u ? V.stack(sp - 4u) : u_zero();
+                    sp -= 2u;
+                } else {
+                    T0 = T1;
+                    T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                    --sp;
+                }
+                pc = npc;
+            }
             break;
         }
         case K_ALU:
-            if (alu_is_fast(op)) res = alu(op, a, b, b);
-            else fast = false;
-            break;
-        case K_ENV:
-            switch (op) {
-            case 0x30: res = V.env(0); break;               // ADDRESS
-            case 0x32: res = V.env(2); break;               // ORIGIN
-            case 0x33: res = V.env(1); break;               // CALLER
-            case 0x34: res = V.env(3); break;               // CALLVALUE
-            case 0x3a: res = V.env(4); break;               // GASPRICE
-            case 0x36: res = u_small(L.calldata_len[lane]); break;
-            case 0x38: res = u_small(C.n_bytes); break;     // CODESIZE
-            case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
-            case 0x58: res = u_small(a32[C.addr_off + pc]); break;
-            case 0x59: res = u_small(msize); break;
-            default: res = u_zero(); break;                 // RETURNDATASIZE
+            if (alu_is_fast(op)) {
+                const bool unary = op == 0x15u || op == 0x19u;      // ISZERO, NOT
+                ok = gas_ok && sp >= (unary ? 1u : 2u);
+                if (ok) {
+                    const U256 r = alu(op, T0, T1, T1);
+                    if (unary) {
+                        T0 = r;
+                    } else {
+                        T0 = r;
+                        T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                        --sp;
+                    }
+                    ++pc; gmin = ngmin; gmax = ngmax;
+                }
             }
             break;
-        case K_MLOAD: case K_MSTORE:    // inside msize: no extension, table gas only
-            ok = ok && u_fits32(a) && msize >= 32u && a.w[0] <= msize - 32u;
-            if (kind == K_MLOAD && ok) res = V.mword(a.w[0]);
+        case K_ENV:
+            ok = gas_ok && sp + 1u <= stack_lim;
+            if (ok) {
+                U256 r;
+                switch (op) {
+                case 0x30: r = V.env(0); break;                 // ADDRESS
+                case 0x32: r = V.env(2); break;                 // ORIGIN
+                case 0x33: r = V.env(1); break;                 // CALLER
+                case 0x34: r = V.env(3); break;                 // CALLVALUE
+                case 0x3a: r = V.env(4); break;                 // GASPRICE
+                case 0x36: r = u_small(L.calldata_len[lane]); break;
+                case 0x38: r = u_small(C.n_bytes); break;       // CODESIZE
+                case 0x45: r = u_small(MSTATE_GAS_LIMIT); break;
+                case 0x58: r = u_small(a32[C.addr_off + pc]); break;
+                case 0x59: r = u_small(msize); break;
+                default: r = u_zero(); break;                   // RETURNDATASIZE
+                }
+                PUSHV(r);
+            }
+            break;
+        case K_MLOAD:                   // inside msize: no extension, table gas only
+            ok = gas_ok && sp >= 1u && u_fits32(T0) && msize >= 32u && T0.w[0] <= msize - 32u;
+            if (ok) { T0 = V.mword(T0.w[0]); ++pc; gmin = ngmin; gmax = ngmax; }
+            break;
+        case K_MSTORE:
+            ok = gas_ok && sp >= 2u && u_fits32(T0) && msize >= 32u && T0.w[0] <= msize - 32u;
+            if (ok) {
+                V.set_mword(T0.w[0], T1);
+                T0 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                T1 = sp >= 4u ? V.stack(sp - 4u) : u_zero();
+                sp -= 2u; ++pc; gmin = ngmin; gmax = ngmax;
+            }
             break;
         case K_CDLOAD: {                // aligned and inside the calldata
             const uint32_t cdl = L.calldata_len[lane];
-            ok = ok && u_fits32(a) && (a.w[0] & 3u) == 0u && (uint64_t)a.w[0] + 32u <= cdl;
+            ok = gas_ok && sp >= 1u && u_fits32(T0) && (T0.w[0] & 3u) == 0u &&
+                 (uint64_t)T0.w[0] + 32u <= cdl;
             if (ok) {
-                const uint32_t d0 = a.w[0] >> 2;
+                const uint32_t d0 = T0.w[0] >> 2;
+                U256 r;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) res.w[7 - k] = V.cdw(d0 + k);
+                for (int k = 0; k < 8; ++k) r.w[7 - k] = V.cdw(d0 + k);
+                T0 = r; ++pc; gmin = ngmin; gmax = ngmax;
             }
             break;
         }
         default:
-            fast = false;
             break;
         }
-
-        if (fast) {
-            if (gas_check) ok = ok && ngmin < glim;
-            if (push) ok = ok && sp - npop + 1u <= stack_lim;
-            if (ok) {
-                // ---- writes ----
-                if (kind == K_SWAP) {
-                    const uint32_t k = op - 0x8fu;
-                    if (k == 1u) {
-                        const U256 t = T0; T0 = T1; T1 = t;
-                    } else {
-                        const U256 x = V.stack(sp - 1u - k);
-                        V.set_stack(sp - 1u - k, T0);
-                        T0 = x;
-                    }
-                } else {
-                    if (kind == K_MSTORE) V.set_mword(a.w[0], b);
-                    if (push) {
-                        if (npop == 0u) {
-                            if (sp >= 2u) V.set_stack(sp - 2u, T1);
-                            T1 = T0;
-                        } else if (npop >= 2u) {
-                            T1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
-                        }
-                        T0 = res;
-                    } else if (npop == 1u) {
-                        T0 = T1;
-                        T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
-                    } else if (npop >= 2u) {
-                        T0 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
-                        T1 = sp >= npop + 2u ? V.stack(sp - npop - 2u) : u_zero();
-                    }
-                    sp = sp - npop + (push ? 1u : 0u);
-                }
-                pc = npc; depth = ndepth; gmin = ngmin; gmax = ngmax;
-            }
-        }
-        if (!fast || !ok) {
+#undef PUSHV
+        if (!ok) {
             LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u};
             slow_step(R, E, uk, ux);
             n_sha3 = R.n_sha3; n_exp = R.n_exp;

@@ -703,15 +703,19 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     }
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)k_lane_step, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void *)k_lane_step<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024 - 4096);
+        (void)hipFuncSetAttribute((const void *)k_lane_step<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024 - 4096);
         (void)hipGetLastError();   // the attribute is advisory on gfx950; never leave a sticky error
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_lane_step, dim3(blocks_for(ctx->L.n, LANE_BLOCK)), dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
+    const uint32_t loop_bound = ctx->L.trace_cap ? ctx->loop_bound : 0u;
+    hipLaunchKernelGGL(loop_bound ? k_lane_step<true> : k_lane_step<false>, dim3(blocks_for(ctx->L.n, LANE_BLOCK)),
+                       dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
                        m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
-                       ctx->L.trace_cap ? ctx->loop_bound : 0u);
+                       loop_bound);
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
