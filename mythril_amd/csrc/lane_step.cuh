@@ -626,6 +626,15 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
 // The opcodes the fast loop executes itself (when their preconditions hold).
 DEV bool alu_is_fast(uint32_t op) { return op <= 0x03u || op == 0x0bu || (op >= 0x10u && op <= 0x1du); }
 
+// Pre-decoded word (s_pd[i].y): op | req << 8 | npop << 12 | push << 16 |
+// kind << 17 | PD_CREATION | PD_SPECIAL | hook << 31.
+#define PD_CREATION (1u << 29)   // escapes when the lane is a creation transaction
+#define PD_SPECIAL (1u << 30)    // kind >= K_ESCAPE (host opcode or past-the-end)
+DEV uint32_t pd_flags(uint32_t op, uint32_t dy, uint32_t hook) {
+    const uint32_t kind = (dy >> 9) & 31u;
+    return (hook << 31) | (kind >= K_ESCAPE ? PD_SPECIAL : 0u) | (op - 0x35u < 5u ? PD_CREATION : 0u);
+}
+
 // ---- BoundedLoopsStrategy (bounded_loops.py:49-145) ---------------------------
 // The trace holds the byte address of every instruction the path was popped at.
 // get_loop_count: find the latest earlier occurrence (index >= 1) of the last two
@@ -739,10 +748,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 const uint2 d = kDec[op];
                 const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
                 const uint32_t hook = (uint32_t)((hm >> (op & 63u)) & 1ull);
-                s_pd[i] = make_uint2(d.x, op | (d.y << 8) | (hook << 31));
+                s_pd[i] = make_uint2(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook));
                 s_cov[i] = 0;
             }
-            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint2(0u, (uint32_t)K_END << 17);
+            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);
             const uint4 *gpu4 = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
             for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gpu4[i];
             staged = true;
@@ -808,12 +817,13 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (sflag) {                                                                      \
             pd = s_pd[pc];                    /* s_pd[n_instr] is the END sentinel */     \
         } else if (pc >= C.n_instr) {                                                     \
-            pd = make_uint2(0u, (uint32_t)K_END << 17);                                   \
+            pd = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);                    \
         } else {                                                                          \
             const uint32_t o_ = gops[pc];                                                 \
             const uint2 d_ = s_dec[o_];                                                   \
             const uint64_t hm_ = o_ < 64u ? m0 : o_ < 128u ? m1 : o_ < 192u ? m2 : m3;    \
-            pd = make_uint2(d_.x, o_ | (d_.y << 8) | ((uint32_t)((hm_ >> (o_ & 63u)) & 1ull) << 31)); \
+            pd = make_uint2(d_.x, o_ | (d_.y << 8) |                                      \
+                            pd_flags(o_, d_.y, (uint32_t)((hm_ >> (o_ & 63u)) & 1ull)));  \
         }                                                                                 \
         const uint32_t k_ = (pd.y >> 17) & 31u, o_ = pd.y & 0xffu;                       \
         const bool hk_ = (pd.y >> 31) && !(hook_ack && executed == 0u);                  \
@@ -832,8 +842,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             else if (res_ == 2u) { status = ST_ESCAPE; aux = o_ | (ESC_TRACE << 8);        \
                                    live = false; lstop_ = true; }                         \
         }                                                                                 \
-        if (!lstop_ && (hk_ || k_ >= K_ESCAPE || executed >= lane_max ||                  \
-            (max_depth != 0u && depth >= max_depth) || (creation && o_ - 0x35u < 5u))) {  \
+        /* one test for the common case: bits 29/30 pre-decode "escape or END"  */      \
+        /* and "escapes in a creation transaction" (CALLDATA*, CODESIZE/COPY)    */      \
+        if (!lstop_ && (hk_ || (pd.y & PD_SPECIAL) || executed >= lane_max ||             \
+            (max_depth != 0u && depth >= max_depth) || (creation && (pd.y & PD_CREATION)))) { \
             uint32_t st_ = ST_RUNNING;                                                    \
             if (max_depth != 0u && depth >= max_depth) st_ = ST_DEPTH;                    \
             else if (k_ == K_END) st_ = ST_END;                                           \
