@@ -97,20 +97,10 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # coverage all-gather over RCCL (coverage_plugin.py semantics: OR of bits)
-    cov = dev.coverage(cid)
-    if dist_on:
-        t = torch.from_numpy(cov.astype(np.uint8)).cuda()
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        cov_union = torch.stack(parts).amax(0).cpu().numpy()
-        tt = torch.tensor([elapsed, float(lane_steps)], dtype=torch.float64, device="cuda")
-        mx = tt.clone()
-        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_steps = float(mx[0]), int(tt[1])
-    else:
-        cov_union = cov
-        total_steps = lane_steps
+    from mythril_amd import dist as mdist
+    cov_union = mdist.allgather_coverage(dev.coverage(cid))
+    elapsed, total_steps = mdist.reduce_timing(elapsed, float(lane_steps))
+    total_steps = int(total_steps)
 
     c4 = None
     if not args.no_c4:
@@ -162,8 +152,9 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
     import torch
     import torch.distributed as dist
     from mythril_amd.smt import synth
+    from mythril_amd import dist as mdist
     chunks = synth.c4_chunks(args.c4_dags)
-    mine = [c[0] for i, c in enumerate(chunks) if i % world == rank]
+    mine = [c[0] for c in mdist.shard(chunks, rank, world)]
     prog, models = synth.c4_batch(args.c4_dags, args.c4_models, chunks=mine)
     dev.eval_upload(prog, models)
     dev.eval_run()                      # warm-up
@@ -177,12 +168,9 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
     fs, sc = dev.eval_download()
     evals = prog.n_dags * models.n_models * args.c4_steps
     n_sat = int((sc > 0).sum())
-    if dist_on:
-        t = torch.tensor([el, float(evals), float(n_sat)], dtype=torch.float64, device="cuda")
-        mx = t[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        el, evals, n_sat = float(mx[0]), float(t[1]), int(t[2])
+    el, evals = mdist.reduce_timing(el, float(evals))
+    _, n_sat = mdist.reduce_timing(0.0, float(n_sat))
+    n_sat = int(n_sat)
     ops, gather_bytes = synth.program_cost(prog)
     k_ms = float(np.mean(kms))
     ops_launch = ops * models.n_models

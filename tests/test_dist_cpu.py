@@ -1,0 +1,50 @@
+"""The multi-GPU exchange (mythril_amd/dist.py) with world_size 2 on the gloo
+backend (CPU): sharding, coverage OR all-gather, model all-gather with unequal
+counts, max/sum timing reduction — the code bench.py runs over RCCL."""
+import os
+import socket
+
+import numpy as np
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mythril_amd import dist as mdist
+        res = {}
+        res["shard"] = mdist.shard(list(range(10)), rank, world)
+        cov = np.zeros(12, dtype=np.uint8)
+        cov[rank::3] = 1
+        res["cov"] = mdist.allgather_coverage(cov).tolist()
+        models = np.full((rank + 1, 2, 8), rank + 7, dtype=np.uint32)
+        res["models"] = mdist.allgather_models(models).tolist()
+        res["timing"] = mdist.reduce_timing(1.0 + rank, 100.0 * (rank + 1))
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_exchange_on_gloo():
+    world, port = 2, _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+        r0, r1 = out[0], out[1]
+    assert r0["shard"] == [0, 2, 4, 6, 8] and r1["shard"] == [1, 3, 5, 7, 9]
+    want = [1 if (k % 3) in (0, 1) else 0 for k in range(12)]
+    assert r0["cov"] == r1["cov"] == want
+    models = np.array(r0["models"])
+    assert models.shape == (3, 2, 8) and (models[0] == 7).all() and (models[1:] == 8).all()
+    assert r0["models"] == r1["models"]
+    assert r0["timing"] == r1["timing"] == (2.0, 300.0)
