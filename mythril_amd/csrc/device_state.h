@@ -43,7 +43,8 @@ struct DevCode {
     uint32_t jres_off;   // u32 [n_jres]             first index with addr >= t
     uint32_t bytes_off;  // u8  [n_bytes]            full bytecode
     uint32_t cov_off;    // u8  [n_instr]            coverage bytes
-    uint32_t _pad[3];
+    uint32_t run_off;    // u32 [n_instr][2]         straight-line run from each instruction
+    uint32_t _pad[2];
 };
 
 // Per-launch statistics accumulated by the stepping kernel.

@@ -56,6 +56,7 @@ struct OpInfo {
 #define LANE_STEP1 8u
 
 #define MSTATE_GAS_LIMIT 1000000000ull
+#define RUN_MAX 64u   // longest straight-line run executed as one block
 #define STACK_LIMIT 1024u
 #define BIG_END (1ull << 32)
 #define HUGE_GAS (1ull << 62)
@@ -711,11 +712,13 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
                                                           uint32_t horizon, uint32_t loop_bound) {
     // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
-    //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
+    //              [runs: pd_cap x 8 B][push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B]
+    //              [coverage: pd_cap]
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
     l_u4 *s_win = (l_u4 *)dyn;
     uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * LANE_BLOCK);
-    uint4 *s_push = reinterpret_cast<uint4 *>(s_pd + pd_cap);
+    uint2 *s_run = s_pd + pd_cap;
+    uint4 *s_push = reinterpret_cast<uint4 *>(s_run + pd_cap);
     uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + 2u * pd_cap);
     uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_jr + jr_cap);
     __shared__ uint2 s_dec[256];
@@ -749,6 +752,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
                 const uint32_t hook = (uint32_t)((hm >> (op & 63u)) & 1ull);
                 s_pd[i] = make_uint2(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook));
+                s_run[i] = make_uint2(a32[BC.run_off + 2u * i], a32[BC.run_off + 2u * i + 1u]);
                 s_cov[i] = 0;
             }
             if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);
@@ -858,10 +862,87 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
 
     if (live) FETCH();
 
+    // Straight-line runs: with no hook, no loop bound and no profiling in this
+    // launch, the lanes sitting at the lead lane's pc whose whole run passes its
+    // checks at once (stack depth, stack growth, table gas, step budget) execute
+    // the run as a block: one dispatch per run instead of per instruction.
+    const bool runs_on = sflag && !prof && !loop_on && ((m0 | m1 | m2 | m3) == 0ull);
+
     for (;;) {
         const uint64_t live_mask = __ballot(live);
         if (live_mask == 0ull) break;
         const int lead = __builtin_ctzll(live_mask);
+        if (runs_on) {
+            uint32_t upc = __builtin_amdgcn_readlane(pc, lead);
+            asm volatile("" : "+s"(upc));
+            const uint2 ri = s_run[upc];
+            const uint32_t rx = __builtin_amdgcn_readfirstlane(ri.x);
+            const uint32_t ry = __builtin_amdgcn_readfirstlane(ri.y);
+            const uint32_t rlen = rx & 0xffu;
+            if (rlen >= 2u) {
+                const uint32_t rneed = (rx >> 8) & 0xffu, rpeak = (rx >> 16) & 0xffu;
+                const uint32_t rg0 = ry & 0xffffu, rg1 = ry >> 16;
+                const bool in_run = live && pc == upc && sp >= rneed && sp + rpeak <= stack_lim &&
+                                    gmin + rg0 < glim && executed + rlen <= lane_max;
+                if ((__ballot(in_run) >> lead) & 1ull) {
+                    if (in_run) {
+                        for (uint32_t k = 0; k < rlen; ++k) {
+                            const uint32_t y = __builtin_amdgcn_readfirstlane(s_pd[upc + k].y);
+                            const uint32_t rop = y & 0xffu;
+                            switch ((y >> 17) & 31u) {
+                            case K_PUSH: {
+                                const U256 v = ld_word((const l_u4 *)s_push, upc + k);
+                                if (sp >= 2u) V.set_stack(sp - 2u, T1);
+                                T1 = T0; T0 = v; ++sp;
+                                break;
+                            }
+                            case K_DUP: {
+                                const uint32_t d = rop - 0x7fu;
+                                const U256 v = d == 1u ? T0 : d == 2u ? T1 : V.stack(sp - d);
+                                if (sp >= 2u) V.set_stack(sp - 2u, T1);
+                                T1 = T0; T0 = v; ++sp;
+                                break;
+                            }
+                            case K_SWAP: {
+                                const uint32_t d = rop - 0x8fu;
+                                if (d == 1u) {
+                                    const U256 t = T0; T0 = T1; T1 = t;
+                                } else {
+                                    const U256 x = V.stack(sp - 1u - d);
+                                    V.set_stack(sp - 1u - d, T0);
+                                    T0 = x;
+                                }
+                                break;
+                            }
+                            case K_POP:
+                                T0 = T1;
+                                T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                                --sp;
+                                break;
+                            case K_ALU: {
+                                const U256 r = alu(rop, T0, T1, T1);
+                                T0 = r;
+                                if (rop != 0x15u && rop != 0x19u) {     // binary: pop 2, push 1
+                                    T1 = sp >= 3u ? V.stack(sp - 3u) : u_zero();
+                                    --sp;
+                                }
+                                break;
+                            }
+                            default:                                    // JUMPDEST
+                                break;
+                            }
+                        }
+                        pc = upc + rlen; gmin += rg0; gmax += rg1; executed += rlen;
+                        FETCH();
+                    }
+                    if (cov_on) {
+                        const uint32_t wl = threadIdx.x & 63u;
+                        if (wl < rlen) s_cov[upc + wl] = 1;
+                    }
+                    continue;
+                }
+            }
+        }
         const uint32_t uy = __builtin_amdgcn_readlane(pd.y, lead);
         uint32_t ux = __builtin_amdgcn_readlane(pd.x, lead), uk = uy;
         // opaque scalar copies: keep the decode below on SGPRs (otherwise the

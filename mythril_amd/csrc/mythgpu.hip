@@ -307,6 +307,40 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
             ctx->a32.push_back(k < addrs.size() ? (uint32_t)k : MG_JRES_NONE);
         }
     }
+    // straight-line runs (kernel 1's block path): from every instruction, the
+    // run of simple opcodes (PUSH/DUP/SWAP/POP/JUMPDEST/fast ALU) that follows,
+    // at most RUN_MAX long, with the stack depth it needs, the growth it peaks
+    // at and its table gas, so a lane can check once and execute the run
+    // without per-instruction checks (lane_step.cuh).
+    {
+        const size_t ni = ops.size();
+        std::vector<uint32_t> rx(ni + 1, 0u), ry(ni + 1, 0u);
+        std::vector<int> need(ni + 1, 0), peak(ni + 1, 0), len(ni + 1, 0);
+        std::vector<uint32_t> g0(ni + 1, 0u), g1(ni + 1, 0u);
+        for (size_t i = ni; i-- > 0;) {
+            const uint32_t b = ops[i];
+            int req = -1, d = 0;
+            if (b >= 0x60 && b <= 0x7f) { req = 0; d = 1; }
+            else if (b >= 0x80 && b <= 0x8f) { req = (int)(b - 0x7f); d = 1; }
+            else if (b >= 0x90 && b <= 0x9f) { req = (int)(b - 0x8e); d = 0; }
+            else if (b == 0x50) { req = 1; d = -1; }
+            else if (b == 0x5b) { req = 0; d = 0; }
+            else if (b == 0x15 || b == 0x19) { req = 1; d = 0; }
+            else if (b <= 0x03 && b >= 0x01) { req = 2; d = -1; }
+            else if (b == 0x0b || (b >= 0x10 && b <= 0x1d)) { req = 2; d = -1; }
+            if (req < 0) continue;                      // not simple: runs end here
+            const bool cont = len[i + 1] > 0 && len[i + 1] < RUN_MAX;
+            len[i] = 1 + (cont ? len[i + 1] : 0);
+            need[i] = std::max(req, (cont ? need[i + 1] : 0) - d);
+            peak[i] = std::max(0, d + (cont ? peak[i + 1] : 0));
+            g0[i] = t[b].gmin + (cont ? g0[i + 1] : 0u);
+            g1[i] = t[b].gmax + (cont ? g1[i + 1] : 0u);
+            rx[i] = (uint32_t)len[i] | ((uint32_t)need[i] << 8) | ((uint32_t)peak[i] << 16);
+            ry[i] = g0[i] | (g1[i] << 16);
+        }
+        dc.run_off = (uint32_t)ctx->a32.size();
+        for (size_t i = 0; i < ni; ++i) { ctx->a32.push_back(rx[i]); ctx->a32.push_back(ry[i]); }
+    }
     dc.cov_off = ctx->cov_total;
     ctx->cov_total += dc.n_instr + 1u;
     ctx->codes.push_back(dc);
@@ -681,7 +715,7 @@ static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_
     for (const DevCode &c : ctx->codes) { maxn = std::max(maxn, c.n_instr); maxj = std::max(maxj, c.n_jres); }
     pd_cap = (std::min<uint32_t>(maxn, 1023u) + 1u + 15u) & ~15u;   // + END sentinel
     jr_cap = (std::min<uint32_t>(maxj, 8192u) + 15u) & ~15u;
-    const size_t code_bytes = (size_t)pd_cap * (8 + 32 + 1) + (size_t)jr_cap * 2;
+    const size_t code_bytes = (size_t)pd_cap * (8 + 8 + 32 + 1) + (size_t)jr_cap * 2;
     const size_t budget = 160u * 1024u - 4096u;
     const size_t slot_bytes = 2u * LANE_BLOCK * 16u;
     win = (uint32_t)std::min<size_t>(16, budget > code_bytes ? (budget - code_bytes) / slot_bytes : 0);
