@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--c4-models", type=int, default=4096)
     ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--rec-cap", type=int, default=128,
+                    help="function-manager record words per lane (0: registrations off)")
     ap.add_argument("--profile-only", action="store_true",
                     help="run warmup+steps with no JSON extras (for rocprofv3)")
     return ap.parse_args()
@@ -64,7 +66,7 @@ def main():
     code = workloads.bytecode("overflow.sol.o")
     cid = dev.load_code(code)
     batch = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + rank,
-                               stack_cap=1024, mem_cap=1024)
+                               stack_cap=1024, mem_cap=1024, rec_cap=args.rec_cap)
     # lanes bucketed by (code, selector, calldata length) so a wavefront walks
     # one function's path (mythril_amd/lanes.py:bucket_order); parity of every
     # lane is independent of its position in the batch
@@ -129,6 +131,7 @@ def main():
                        "lanes_per_gpu": args.lanes, "lane_steps_per_batch": steps_per_batch,
                        "kernel_ms_per_batch": kms,
                        "coverage_instructions": int(cov_union.sum()),
+                       "function_manager_records": args.rec_cap > 0,
                        "parallelism": f"lanes sharded x{world}, RCCL coverage all-gather"},
             "roofline": roof,
         }

@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 3u   /* 2: model tables (arrays, uninterpreted functions)
-                               3: per-lane instruction traces + loop bound        */
+#define MG_ABI_VERSION 4u   /* 2: model tables (arrays, uninterpreted functions)
+                               3: per-lane instruction traces + loop bound
+                               4: per-lane function-manager records (Keccak, EXP) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -68,6 +69,26 @@ extern "C" {
 #define MG_ESC_STORAGE  3u   /* storage slot table full                         */
 #define MG_ESC_STACK    4u   /* stack would grow past the lane's stack_cap      */
 #define MG_ESC_TRACE    5u   /* instruction trace would grow past trace_cap      */
+#define MG_ESC_RECORD   6u   /* function-manager record log would grow past rec_cap */
+
+/* Function-manager records: what the reference registers with its global
+ * function managers while a path runs, logged per lane in execution order so
+ * the host can replay the registrations when it materialises the lane.
+ * A record is [kind][len][step][result: 8 limbs][payload], in uint32 words;
+ * step = the lane's `steps` count before the instruction (its BFS round), so
+ * the host can replay registrations of all lanes in the reference's global order.
+ *   MG_REC_KECCAK  SHA3 of a concrete, non-empty memory slice
+ *                  (keccak_function_manager.create_keccak, keccak_function_manager.py:95-114:
+ *                  concrete_hashes[data] = hash).  len = input bytes; result =
+ *                  the hash; payload = ceil(len/4) words, input bytes packed
+ *                  big-endian (byte 4j+0 in bits 31..24 of word j).
+ *   MG_REC_EXP     EXP of concrete operands (exponent_function_manager.py:32-47:
+ *                  the path gains the constraint result == Power(base, exponent),
+ *                  instructions.py:624-638).  len = 0; result = base**exp mod 2^256;
+ *                  payload = base limbs then exponent limbs (16 words).             */
+#define MG_REC_KECCAK   1u
+#define MG_REC_EXP      2u
+#define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */
 #define MG_LANE_STATIC    1u  /* environment.static (WriteProtection)          */
@@ -127,6 +148,11 @@ typedef struct mg_lane_soa {
     uint32_t _pad2;
     uint32_t *trace_len;    /* [n]                                             */
     uint32_t *trace;        /* [n][trace_cap]                                  */
+    /* function-manager records (MG_REC_*), in execution order                  */
+    uint32_t rec_cap;       /* uint32 words per lane in `rec` (0: not recorded) */
+    uint32_t _pad3;
+    uint32_t *rec_len;      /* [n] words used                                  */
+    uint32_t *rec;          /* [n][rec_cap]                                    */
 } mg_lane_soa;
 
 /* Per-call statistics of mg_step. */
@@ -149,6 +175,7 @@ typedef struct mg_batch_cfg {
     uint32_t storage_cap;   /* slots                                           */
     uint32_t coverage;      /* 1: record the per-code coverage bitmap         */
     uint32_t trace_cap;     /* instruction-trace entries per lane (0: none)   */
+    uint32_t rec_cap;       /* function-manager record words per lane (0: none) */
 } mg_batch_cfg;
 
 typedef struct mg_ctx mg_ctx;

@@ -30,6 +30,10 @@ struct DevLanes {
     uint32_t trace_cap;
     uint32_t *trace_len; // [N]
     uint32_t *trace;     // [trace_cap][N]
+    // function-manager records (MG_REC_*): uint32 words per lane, in execution order
+    uint32_t rec_cap;
+    uint32_t *rec_len;   // [N]
+    uint32_t *rec;       // [rec_cap][N]
 };
 
 // One loaded code (Disassembly): arrays live in one device arena.

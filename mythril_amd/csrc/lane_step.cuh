@@ -49,6 +49,7 @@ struct OpInfo {
 #define ESC_STORAGE 3u
 #define ESC_STACK 4u
 #define ESC_TRACE 5u
+#define ESC_RECORD 6u
 
 #define LANE_STATIC 1u
 #define LANE_CREATION 2u
@@ -206,8 +207,11 @@ DEV int mem_extend(const U256 &start, const U256 &size, uint32_t &msize, uint64_
 
 DEV bool gas_oog(uint64_t gmin, uint64_t txlim) { return gmin > MSTATE_GAS_LIMIT || gmin >= txlim; }
 
-// Keccak-256 of memory [off, off+len) (off + len <= msize <= mem_cap)
-DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
+// Keccak-256 of memory [off, off+len) (off + len <= msize <= mem_cap).  With
+// rec != nullptr the input is also copied to the record payload at rec (one
+// big-endian word per N-strided row, bytes past len zero).
+DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len, uint32_t *__restrict__ rec = nullptr,
+                    size_t N = 0) {
     uint64_t st[25];
 #pragma unroll
     for (int i = 0; i < 25; ++i) st[i] = 0ull;
@@ -223,6 +227,12 @@ DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
             const uint32_t c = V.mdw_safe(dw + 2u);
             be0 = (a << s) | (b >> (32u - s));
             be1 = (b << s) | (c >> (32u - s));
+        }
+        if (rec) {
+            const uint32_t w = p >> 2;                       // payload word of be0
+            const int32_t v0 = (int32_t)len - (int32_t)p;   // valid bytes from p on
+            if (v0 > 0) rec[(size_t)w * N] = v0 >= 4 ? be0 : be0 & ~(0xffffffffu >> (8 * v0));
+            if (v0 > 4) rec[(size_t)(w + 1u) * N] = v0 >= 8 ? be1 : be1 & ~(0xffffffffu >> (8 * (v0 - 4)));
         }
         return (uint64_t)__builtin_bswap32(be0) | ((uint64_t)__builtin_bswap32(be1) << 32);
     };
@@ -254,6 +264,34 @@ DEV U256 keccak_mem(const LaneView &V, uint32_t off, uint32_t len) {
         r.w[6 - 2 * q] = __builtin_bswap32((uint32_t)(st[q] >> 32));
     }
     return r;
+}
+
+// ---- function-manager records (include/mythgpu.h MG_REC_*) ----------------------
+// Word k of lane `lane`'s record log lives at rec[k * N + lane].  The writers
+// fill words from `at` on and return the new length; the caller publishes it
+// (rec_len) only when the instruction completes.
+DEV uint32_t rec_head(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t kind, uint32_t len, uint32_t step,
+                      const U256 &r) {
+    uint32_t *__restrict__ q = L.rec + lane;
+    const size_t N = L.N;
+    q[(size_t)at * N] = kind;
+    q[(size_t)(at + 1u) * N] = len;
+    q[(size_t)(at + 2u) * N] = step;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[(size_t)(at + 3u + k) * N] = r.w[k];
+    return at + MG_REC_HEADER;
+}
+DEV uint32_t rec_exp(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t step, const U256 &r,
+                     const U256 &base, const U256 &exponent) {
+    at = rec_head(L, lane, at, MG_REC_EXP, 0u, step, r);
+    uint32_t *__restrict__ q = L.rec + lane;
+    const size_t N = L.N;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        q[(size_t)(at + k) * N] = base.w[k];
+        q[(size_t)(at + 8u + k) * N] = exponent.w[k];
+    }
+    return at + 16u;
 }
 
 // ---- decode table -----------------------------------------------------------------
@@ -324,6 +362,7 @@ struct LaneRegs {
     uint32_t pc, sp, msize, depth;
     uint32_t n_sha3, n_exp;
     uint32_t stop, sx;           // out: ST_RUNNING or the stop status and its aux word
+    uint32_t step;               // instructions this launch executed before this one
 };
 // What the handlers read besides the registers (per lane / per block).
 struct StepEnv {
@@ -367,6 +406,7 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
     const uint32_t nsp = sp - npop;
     uint32_t *s_prof = E.s_prof;
     const bool prof = E.prof != 0u;
+    uint32_t rec_at = 0u, rec_new = 0u;     // function-manager record log (rec_cap > 0)
 
 #define STOPX(s_, x_) { stop = (s_); sx = (x_); break; }
 #define EXCX(k_) STOPX(ST_VMEXC, (k_))
@@ -390,8 +430,15 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
         bool tos_done = false;
         switch (kind) {
         case K_ALU:
-            if (op == 0x0a) ++R.n_exp;
+            if (op == 0x0a && L.rec_cap) {
+                rec_at = L.rec_len[lane];
+                if (rec_at + MG_REC_HEADER + 16u > L.rec_cap) ESCX(ESC_RECORD)
+            }
             res = alu(op, a, b, c);
+            if (op == 0x0a) {
+                ++R.n_exp;
+                if (L.rec_cap) rec_new = rec_exp(L, lane, rec_at, L.steps[lane] + R.step, res, a, b);
+            }
             break;
         case K_PUSH:                                        // (:278-320)
             res = E.psflag ? ld_word((const l_u4 *)E.s_push, pc)
@@ -444,12 +491,21 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
             ngmin += g; ngmax += g;
             if (ngmin >= glim) EXCX(EXC_OOG)
             MEMX(a, b, -1)
+            if (b.w[0] != 0u && L.rec_cap) {
+                rec_at = L.rec_len[lane];
+                if ((uint64_t)rec_at + MG_REC_HEADER + ((b.w[0] + 3u) >> 2) > L.rec_cap) ESCX(ESC_RECORD)
+            }
             ZEROFILL()
             if (b.w[0] == 0u) {  // get_empty_keccak_hash (keccak_function_manager.py:87-93)
                 res.w[7] = 0xc5d24601u; res.w[6] = 0x86f7233cu; res.w[5] = 0x927e7db2u; res.w[4] = 0xdcc703c0u;
                 res.w[3] = 0xe500b653u; res.w[2] = 0xca82273bu; res.w[1] = 0x7bfad804u; res.w[0] = 0x5d85a470u;
             } else {
-                res = keccak_mem(V, a.w[0], b.w[0]);
+                res = keccak_mem(V, a.w[0], b.w[0],
+                                 L.rec_cap ? L.rec + lane + (size_t)(rec_at + MG_REC_HEADER) * L.N : nullptr, L.N);
+                if (L.rec_cap) {
+                    rec_head(L, lane, rec_at, MG_REC_KECCAK, b.w[0], L.steps[lane] + R.step, res);
+                    rec_new = rec_at + MG_REC_HEADER + ((b.w[0] + 3u) >> 2);
+                }
                 if (prof) { atomicAdd(&s_prof[256], b.w[0]); atomicAdd(&s_prof[259], b.w[0] / 136u + 1u); }
             }
             ++R.n_sha3;
@@ -619,6 +675,7 @@ __device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t u
     R.stop = stop;
     R.sx = sx;
     if (stop == ST_RUNNING) {
+        if (rec_new) L.rec_len[lane] = rec_new;
         R.pc = npc; R.sp = nsp + (push ? 1u : 0u);
         R.msize = nmsize; R.depth = ndepth; R.gmin = ngmin; R.gmax = ngmax;
     }
@@ -1106,7 +1163,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         }
 #undef PUSHV
         if (!ok) {
-            LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u};
+            LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed - 1u};
             slow_step(R, E, uk, ux);
             n_sha3 = R.n_sha3; n_exp = R.n_exp;
             if (R.stop != ST_RUNNING) {

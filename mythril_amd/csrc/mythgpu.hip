@@ -423,6 +423,10 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     if ((rc = lane_alloc(ctx, L.trace_len, N))) return rc;
     if (L.trace_cap && (rc = lane_alloc(ctx, L.trace, (size_t)L.trace_cap * N))) return rc;
     HIPX(ctx, hipMemsetAsync(L.trace_len, 0, N * 4, ctx->stream));
+    L.rec_cap = cfg->rec_cap;
+    if ((rc = lane_alloc(ctx, L.rec_len, N))) return rc;
+    if (L.rec_cap && (rc = lane_alloc(ctx, L.rec, (size_t)L.rec_cap * N))) return rc;
+    HIPX(ctx, hipMemsetAsync(L.rec_len, 0, N * 4, ctx->stream));
     // no lane runs before upload
     HIPX(ctx, hipMemsetAsync(L.status, 0xff, N * 4, ctx->stream));
     HIPX(ctx, hipMemsetAsync(L.sha3_count, 0, N * 4, ctx->stream));
@@ -489,6 +493,7 @@ __global__ void k_reset(DevLanes L, const uint32_t *__restrict__ i_pc, const uin
     L.gas_min[lane] = i_gmin[lane]; L.gas_max[lane] = i_gmax[lane];
     L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
     L.trace_len[lane] = 0;                 // reset images start with empty traces
+    L.rec_len[lane] = 0;                   // ... and empty record logs
     const uint32_t cnt = i_cnt[lane];
     L.storage_count[lane] = cnt;
     for (uint32_t s = 0; s < cnt; ++s)
@@ -582,7 +587,7 @@ static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, u
                        first + n, ctx->L.n, h ? h->n : 0);
     if (h->stack_cap > ctx->L.stack_cap || h->mem_cap > ctx->L.mem_cap || h->mem_cap % 4 ||
         h->calldata_cap > ctx->L.calldata_cap || h->calldata_cap % 4 || h->storage_cap > ctx->L.storage_cap ||
-        h->trace_cap > ctx->L.trace_cap)
+        h->trace_cap > ctx->L.trace_cap || h->rec_cap > ctx->L.rec_cap)
         return set_err(ctx, MG_EINVAL, "host image capacities exceed the batch configuration");
     return MG_OK;
 }
@@ -598,12 +603,14 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
         if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
         if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
             h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap ||
-            (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u))
+            (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u) ||
+            (h->rec_cap ? h->rec_len[i] > h->rec_cap : 0u))
             return set_err(ctx, MG_EINVAL, "lane %u: state exceeds its host capacities", first + i);
     }
     bool fresh = true;
     for (uint32_t i = 0; i < n && fresh; ++i)
-        fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0);
+        fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0) &&
+                (!h->rec_cap || h->rec_len[i] == 0);
     const size_t S4 = 4, S8 = 8;
     if ((rc = up_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
     if ((rc = up_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
@@ -645,6 +652,12 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
     } else {
         HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
     }
+    if (h->rec_cap) {
+        if ((rc = up_scalar(ctx, h->rec_len, S4, n, L.rec_len, first))) return rc;
+        if ((rc = up_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first))) return rc;
+    } else {
+        HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
+    }
     ctx->uploaded = true;
     ctx->init_fresh = (first == 0 && n == L.n) ? fresh : (ctx->init_fresh && fresh);
     return MG_OK;
@@ -683,6 +696,11 @@ extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, ui
         if ((rc = down_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
         HIPX(ctx, hipStreamSynchronize(ctx->stream));
         if ((rc = down_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first))) return rc;
+    }
+    if (h->rec_cap) {
+        if ((rc = down_scalar(ctx, h->rec_len, S4, n, L.rec_len, first))) return rc;
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        if ((rc = down_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first))) return rc;
     }
     return MG_OK;
 }

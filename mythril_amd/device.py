@@ -83,7 +83,8 @@ class GpuDevice:
     # -- lanes ---------------------------------------------------------------
     def alloc(self, shape: LaneShape, coverage: bool = False):
         cfg = native.MgBatchCfg(shape.n, shape.stack_cap, shape.mem_cap, shape.calldata_cap,
-                                shape.storage_cap, 1 if coverage else 0, shape.trace_cap)
+                                shape.storage_cap, 1 if coverage else 0, shape.trace_cap,
+                                shape.rec_cap)
         self._check(self.lib.mg_lanes_alloc(self.ctx, ctypes.byref(cfg)), "mg_lanes_alloc")
         self.shape = shape
 

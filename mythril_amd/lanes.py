@@ -33,6 +33,9 @@ WORLD_STATE_KEPT = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_END)
 MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
 MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
 MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2, 3, 4, 5
+MG_ESC_RECORD = 6
+# function-manager records (include/mythgpu.h MG_REC_*)
+MG_REC_KECCAK, MG_REC_EXP, MG_REC_HEADER = 1, 2, 11
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
@@ -78,11 +81,13 @@ class MgLaneSoa(ctypes.Structure):
         ("ret_offset", ctypes.c_void_p), ("ret_len", ctypes.c_void_p),
         ("trace_cap", ctypes.c_uint32), ("_pad2", ctypes.c_uint32),
         ("trace_len", ctypes.c_void_p), ("trace", ctypes.c_void_p),
+        ("rec_cap", ctypes.c_uint32), ("_pad3", ctypes.c_uint32),
+        ("rec_len", ctypes.c_void_p), ("rec", ctypes.c_void_p),
     ]
 
 
 _U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
-               "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len")
+               "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len", "rec_len")
 _U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
 
 
@@ -94,6 +99,7 @@ class LaneShape:
     calldata_cap: int = 128
     storage_cap: int = 16
     trace_cap: int = 0
+    rec_cap: int = 0
 
     def __post_init__(self):
         if self.mem_cap % 32:
@@ -118,6 +124,7 @@ class LaneBatch:
         self.memory = np.zeros((n, shape.mem_cap), dtype=np.uint8)
         self.storage = np.zeros((n, shape.storage_cap, 16), dtype=np.uint32)
         self.trace = np.zeros((n, max(shape.trace_cap, 1)), dtype=np.uint32)
+        self.rec = np.zeros((n, max(shape.rec_cap, 1)), dtype=np.uint32)
 
     @property
     def n(self) -> int:
@@ -130,8 +137,9 @@ class LaneBatch:
         s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
         s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
         s.trace_cap = self.shape.trace_cap
+        s.rec_cap = self.shape.rec_cap
         for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                              "trace"):
+                                              "trace", "rec"):
             arr = getattr(self, f)
             assert arr.flags["C_CONTIGUOUS"]
             setattr(s, f, arr.ctypes.data)
@@ -148,8 +156,9 @@ class LaneBatch:
         s.stack_cap, s.mem_cap = self.shape.stack_cap, self.shape.mem_cap
         s.calldata_cap, s.storage_cap = self.shape.calldata_cap, self.shape.storage_cap
         s.trace_cap = self.shape.trace_cap
+        s.rec_cap = self.shape.rec_cap
         for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                              "trace"):
+                                              "trace", "rec"):
             arr = getattr(self, f)
             setattr(s, f, arr.ctypes.data + first * arr.strides[0])
         self._keep_range = s
@@ -158,7 +167,7 @@ class LaneBatch:
     def copy(self) -> "LaneBatch":
         out = LaneBatch(self.shape)
         for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                              "trace"):
+                                              "trace", "rec"):
             getattr(out, f)[...] = getattr(self, f)
         return out
 
@@ -210,6 +219,29 @@ class LaneBatch:
             out = {k: v for k, v in out.items() if v}
         return out
 
+    def records(self, i: int, start: int = 0):
+        """Lane i's function-manager records in execution order, as (step, kind, ...):
+        (step, "keccak", input bytes, hash) and (step, "exp", base, exponent, result),
+        step = the lane's steps count before the instruction."""
+        out = []
+        q = self.rec[i, : int(self.rec_len[i])]
+        k = start
+        while k < q.size:
+            kind, ln, step = int(q[k]), int(q[k + 1]), int(q[k + 2])
+            r = limbs_to_word(q[k + 3: k + 11])
+            k += MG_REC_HEADER
+            if kind == MG_REC_KECCAK:
+                nw = (ln + 3) // 4
+                data = q[k: k + nw].astype(">u4").tobytes()[:ln]
+                out.append((step, "keccak", data, r))
+                k += nw
+            elif kind == MG_REC_EXP:
+                out.append((step, "exp", limbs_to_word(q[k: k + 8]), limbs_to_word(q[k + 8: k + 16]), r))
+                k += 16
+            else:
+                raise ValueError(f"lane {i}: bad record kind {kind} at word {k - MG_REC_HEADER}")
+        return out
+
     def memory_bytes(self, i: int) -> bytes:
         return bytes(self.memory[i, : int(self.msize[i])])
 
@@ -232,7 +264,7 @@ class LaneBatch:
 
 # Fields compared lane-by-lane in parity tests (device vs oracle).
 PARITY_SCALARS = ("pc", "sp", "msize", "depth", "status", "aux", "steps", "gas_min",
-                  "gas_max", "storage_count", "trace_len")
+                  "gas_max", "storage_count", "trace_len", "rec_len")
 
 
 def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = None,
@@ -262,6 +294,10 @@ def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = No
         if a.shape.trace_cap and tl == int(b.trace_len[i]) and \
                 not np.array_equal(a.trace[i, :tl], b.trace[i, :tl]):
             out.append(f"lane {i}: trace differs")
+        rl = int(a.rec_len[i])
+        if a.shape.rec_cap and rl == int(b.rec_len[i]) and \
+                not np.array_equal(a.rec[i, :rl], b.rec[i, :rl]):
+            out.append(f"lane {i}: function-manager records differ")
         if int(a.status[i]) in (MG_HALT_RETURN, MG_HALT_REVERT):
             if (a.ret_offset[i], a.ret_len[i]) != (b.ret_offset[i], b.ret_len[i]):
                 out.append(f"lane {i}: return range differs")
@@ -269,7 +305,7 @@ def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = No
 
 
 _ALL_FIELDS = _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                           "trace")
+                                           "trace", "rec")
 
 
 def bucket_order(batch: LaneBatch) -> np.ndarray:

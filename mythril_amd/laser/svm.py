@@ -32,6 +32,8 @@ order.  Hook-free paths run in one launch.
 """
 from __future__ import annotations
 
+import heapq
+import itertools
 import logging
 import os
 from collections import defaultdict
@@ -42,12 +44,15 @@ from typing import Callable, DefaultDict, Dict, List, Optional, Tuple
 import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
-                     MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_EXC_STACK_UNDERFLOW,
+                     MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE,
+                     MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
                      limbs_to_word, word_to_limbs)
+from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import symbol_factory
+from ..smt.keccak_manager import keccak_function_manager
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
@@ -311,7 +316,8 @@ class LaserEVM:
         mem_cap = (mem_cap + 31) // 32 * 32
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
-                         storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap)
+                         storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap,
+                         rec_cap=512 * g)
 
     def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
         env, ms = s.environment, s.mstate
@@ -355,6 +361,9 @@ class LaserEVM:
             b.trace[i] = 0
             b.trace[i, : len(tr)] = tr
             b.trace_len[i] = len(tr)
+        b.rec_len[i] = 0                # records already parsed into the replay queue
+        if hasattr(b, "rec_seen"):
+            b.rec_seen[i] = 0
 
     def _materialise(self, b: LaneBatch, i: int, s: GlobalState) -> GlobalState:
         """Write lane i of the host image back into its GlobalState (in place)."""
@@ -377,6 +386,42 @@ class LaserEVM:
             ann.trace = [int(x) for x in b.trace[i, : int(b.trace_len[i])]]
         return s
 
+    # ------------------------------------------------------------- function managers
+    def _collect_records(self, b: LaneBatch, run: List[int]) -> None:
+        """Queue the new function-manager records of lanes `run` (just downloaded)
+        under their global execution key: (round, position) for BFS, (-position,
+        round) for DFS -- the order in which the reference executes them."""
+        if not b.shape.rec_cap:
+            return
+        for i in run:
+            end, seen = int(b.rec_len[i]), int(b.rec_seen[i])
+            if end <= seen:
+                continue
+            for r in b.records(i, seen):
+                key = (r[0], i) if self._rec_bfs else (-i, r[0])
+                heapq.heappush(self._recq, (key, next(self._rec_seq), i, r))
+            b.rec_seen[i] = end
+
+    def _replay_records(self, lanes, bound=None, inclusive: bool = False) -> None:
+        """Register the queued records with key < bound (<= when inclusive; all
+        when bound is None): keccak_function_manager.create_keccak's
+        concrete_hashes entry for each SHA3 (keccak_function_manager.py:95-114)
+        and, for each EXP, exponent_function_manager's constraint appended to the
+        path's constraints (instructions.py:624-638)."""
+        q = self._recq
+        while q and (bound is None or q[0][0] < bound or (inclusive and q[0][0] == bound)):
+            _, _, i, r = heapq.heappop(q)
+            if r[1] == "keccak":
+                keccak_function_manager.register_concrete(r[2], r[3])
+            else:
+                _, cond = exponent_function_manager.create_condition(
+                    symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))
+                lanes[i].state.world_state.constraints.append(cond)
+
+    def _event_key(self, b: LaneBatch, i: int):
+        r = _event_round(b, i)
+        return (r, i) if self._rec_bfs else (-i, r)
+
     def _loop_bound(self) -> int:
         return int(getattr(self.strategy, "bound", 0) or 0)
 
@@ -387,6 +432,7 @@ class LaserEVM:
         n = len(states)
         shape = self._shape(states)
         b = LaneBatch(shape)
+        b.rec_seen = np.zeros(n, dtype=np.int64)
         lanes = [_Lane(s, i) for i, s in enumerate(states)]
         for i, s in enumerate(states):
             self._pack(b, i, s)
@@ -398,6 +444,7 @@ class LaserEVM:
         depth = 0 if self.max_depth == _INF else int(self.max_depth)
         bfs = getattr(self.strategy, "order", "bfs") == "bfs"
         regrow: List[GlobalState] = []
+        self._recq, self._rec_seq, self._rec_bfs, self._rec_lanes = [], itertools.count(), bfs, lanes
 
         def launch(run: List[int], horizon: int):
             for ln in lanes:
@@ -411,6 +458,7 @@ class LaserEVM:
             self.total_states += st.lane_steps      # one successor per executed step
             for lo, cnt in _ranges(run):
                 dev.download_range(b, lo, cnt)
+            self._collect_records(b, run)
             for i in run:
                 lanes[i].phase = "paused" if b.status[i] == MG_RUNNING else "event"
 
@@ -418,6 +466,7 @@ class LaserEVM:
         while True:
             if (create and self._check_create_termination()) or (
                     not create and self._check_execution_termination()):
+                self._replay_records(lanes)
                 left = [self._materialise(b, ln.pos, ln.state) for ln in lanes
                         if ln.phase != "done"]
                 return left
@@ -442,7 +491,9 @@ class LaserEVM:
                 elif ev is None or max(paused) > ev:
                     launch(paused, 0)           # DFS: the newest path runs on first
                     continue
+            self._replay_records(lanes, self._event_key(b, ev))
             self._deliver(lanes[ev], b, final_states, track_gas, launch, regrow, single_step)
+        self._replay_records(lanes)
         if regrow:
             self._cap_grow *= 4
             self.work_list.extend(regrow)
@@ -514,6 +565,9 @@ class LaserEVM:
                 ln.phase = "event"
                 self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
                 return
+            # the instruction's own registrations precede its post hooks
+            self._replay_records(self._rec_lanes, (steps, i) if self._rec_bfs else (-i, steps),
+                                 inclusive=True)
             for hook in self.instr_post_hook.get(name, ()):
                 hook(snapshot)
             new = self._materialise(b, i, s)
@@ -553,7 +607,7 @@ class LaserEVM:
             return                  # the strategy skips it: not a final state
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
-            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE):
+            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE, MG_ESC_RECORD):
                 # rerun with larger lane capacities; the instruction was traced
                 # at its pop but not executed, and will be traced again
                 if reason != MG_ESC_TRACE and b.shape.trace_cap:

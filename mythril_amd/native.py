@@ -57,7 +57,7 @@ class MgBatchCfg(ctypes.Structure):
     _fields_ = [("n_lanes", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32),
                 ("mem_cap", ctypes.c_uint32), ("calldata_cap", ctypes.c_uint32),
                 ("storage_cap", ctypes.c_uint32), ("coverage", ctypes.c_uint32),
-                ("trace_cap", ctypes.c_uint32)]
+                ("trace_cap", ctypes.c_uint32), ("rec_cap", ctypes.c_uint32)]
 
 
 class MgDagBatch(ctypes.Structure):

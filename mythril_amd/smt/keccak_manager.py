@@ -69,6 +69,16 @@ class KeccakFunctionManager:
         self.hash_result_store[length].append(func(data))
         return func(data)
 
+    def register_concrete(self, data: bytes, hash_value: int) -> BitVec:
+        """create_keccak for a concrete input whose hash the device already
+        computed (an MG_REC_KECCAK record of kernel 1): the same get_function
+        side effect and concrete_hashes entry, keyed by the 8*len-bit input."""
+        bv = symbol_factory.BitVecVal(int.from_bytes(data, "big"), 8 * len(data))
+        self.get_function(bv.size())
+        h = symbol_factory.BitVecVal(hash_value, 256)
+        self.concrete_hashes[bv] = h
+        return h
+
     def create_conditions(self) -> Bool:
         condition = symbol_factory.Bool(True)
         for inputs_list in self.symbolic_inputs.values():

@@ -43,10 +43,11 @@ def _int_limbs(x: int) -> np.ndarray:
 
 
 def c2_batch(n: int = 65536, code_id: int = 0, seed: int = C2_SEED, stack_cap: int = 1024,
-             mem_cap: int = 1024, storage_cap: int = 16, gas_limit: int = 8_000_000) -> LaneBatch:
+             mem_cap: int = 1024, storage_cap: int = 16, gas_limit: int = 8_000_000,
+             rec_cap: int = 0) -> LaneBatch:
     rng = np.random.Generator(np.random.PCG64(seed))
     shape = LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap, calldata_cap=96,
-                      storage_cap=storage_cap)
+                      storage_cap=storage_cap, rec_cap=rec_cap)
     b = LaneBatch(shape)
     # --- calldata: selector | arg0 | arg1, length 68 w.p. 15/16 else U{0..67}
     sel_known = rng.random(n) < 7 / 8

@@ -35,7 +35,7 @@ def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, thread
     from mythril_amd import workloads
     o = OracleEVM()
     cid = o.load_code(code)
-    base = workloads.c2_batch(lanes, code_id=cid, stack_cap=64, mem_cap=1024)
+    base = workloads.c2_batch(lanes, code_id=cid, stack_cap=64, mem_cap=1024, rec_cap=128)
     threads = threads or min(16, _usable_cores())
     mask = (ctypes.c_uint64 * 4)(0, 0, 0, 0)
     lib().orc_run_mt.restype = ctypes.c_uint64

@@ -312,6 +312,19 @@ static int storage_find(const mg_lane_soa *h, uint32_t i, u256 key) {
     return -1;
 }
 
+/* function-manager records: lane-major [n][rec_cap] words (include/mythgpu.h MG_REC_*) */
+static uint32_t rec_put_word(const mg_lane_soa *h, uint32_t i, uint32_t at, u256 v) {
+    uint32_t *q = h->rec + (size_t)i * h->rec_cap;
+    for (int k = 0; k < 4; ++k) { q[at + 2 * k] = (uint32_t)v.w[k]; q[at + 2 * k + 1] = (uint32_t)(v.w[k] >> 32); }
+    return at + 8;
+}
+/* step: the lane's steps count before this instruction (its BFS round) */
+static uint32_t rec_put_head(const mg_lane_soa *h, uint32_t i, uint32_t at, uint32_t kind, uint32_t len, u256 r) {
+    uint32_t *q = h->rec + (size_t)i * h->rec_cap;
+    q[at] = kind; q[at + 1] = len; q[at + 2] = h->steps[i] - 1;
+    return rec_put_word(h, i, at + 3, r);
+}
+
 static inline uint8_t mem_read_byte(const uint8_t *m, uint32_t msize, uint64_t k) {
     return k < msize ? m[k] : 0;
 }
@@ -390,6 +403,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         const orc_op *info = &OPT[op];
         int gas_by_table = 1, gas_done = 0;
         uint32_t status = MG_RUNNING, aux = 0;
+        uint32_t rec_new = 0;   /* function-manager record log length after this step */
 
         done++; h->steps[i]++;
 
@@ -449,11 +463,17 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
             PUSH1(z_urem(u_mul(z_urem(a, cc), z_urem(b, cc)), cc)); break;
         case 0x0a: { /* EXP concrete: pow(base, exp, 2**256) (exponent_function_manager.py:43-51) */
             NEED_POP(2); a = POP(); b = POP();
+            if (h->rec_cap && h->rec_len[i] + MG_REC_HEADER + 16 > h->rec_cap) ESC(MG_ESC_RECORD);
             u256 acc = u_from64(1), base = a;
             unsigned nb = u_bitlen(b);
             for (unsigned bit = 0; bit < nb; ++bit) {
                 if ((b.w[bit / 64] >> (bit % 64)) & 1) acc = u_mul(acc, base);
                 base = u_mul(base, base);
+            }
+            if (h->rec_cap) {   /* the path gains acc == Power(a, b) */
+                uint32_t at = rec_put_head(h, i, h->rec_len[i], MG_REC_EXP, 0, acc);
+                at = rec_put_word(h, i, at, a);
+                rec_new = rec_put_word(h, i, at, b);
             }
             PUSH1(acc); break;
         }
@@ -495,6 +515,8 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
             if (gas_oog(gmin, txlim)) EXC(MG_EXC_OUT_OF_GAS);
             MEMX(a, b, -1);
             uint64_t len = b.w[0];
+            if (len && h->rec_cap && (uint64_t)h->rec_len[i] + MG_REC_HEADER + (len + 3) / 4 > h->rec_cap)
+                ESC(MG_ESC_RECORD);
             uint8_t digest[32];
             if (len == 0) {
                 /* keccak_function_manager.get_empty_keccak_hash (:87-93) */
@@ -508,6 +530,18 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
                 uint8_t *tmp = malloc(len);
                 for (uint64_t k = 0; k < len; ++k) tmp[k] = mem_read_byte(mem, msize0, s0 + k);
                 orc_keccak256(tmp, len, digest);
+                if (h->rec_cap) {   /* keccak_function_manager.concrete_hashes[data] = hash */
+                    uint32_t at = rec_put_head(h, i, h->rec_len[i], MG_REC_KECCAK, (uint32_t)len,
+                                               u_from_be(digest, 32));
+                    uint32_t *q = h->rec + (size_t)i * h->rec_cap;
+                    for (uint64_t k = 0; k < len; k += 4) {
+                        uint32_t w = 0;
+                        for (uint64_t j = 0; j < 4; ++j)
+                            w |= (uint32_t)(k + j < len ? tmp[k + j] : 0) << (24 - 8 * j);
+                        q[at++] = w;
+                    }
+                    rec_new = at;
+                }
                 free(tmp);
             }
             NEED_PUSH(1);
@@ -658,6 +692,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         /* commit */
         h->pc[i] = new_pc; h->sp[i] = sp; h->msize[i] = msize; h->depth[i] = depth;
         h->gas_min[i] = gmin; h->gas_max[i] = gmax;
+        if (rec_new) h->rec_len[i] = rec_new;
         continue;
     stop:
         h->status[i] = status; h->aux[i] = aux;

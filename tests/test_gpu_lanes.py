@@ -349,3 +349,46 @@ def test_loop_bound_vmtests_and_c2(dev, c2):
         getattr(cb2, f)[...] = getattr(cb, f)
     out, ref = run_both_loop(dev, [c2], cb2, 2)
     assert not diff_batches(out, ref, limit=20)
+
+
+# ---- function-manager records (MG_REC_*): Keccak registrations and EXP constraints
+def test_records_device_equals_oracle(dev):
+    from test_records import PROGRAM, expected
+    caps = [0, 26, 27, 60, 100, 1024]
+    b = LaneBatch(LaneShape(n=len(caps) * 64, stack_cap=64, mem_cap=1024, calldata_cap=32,
+                            storage_cap=4, rec_cap=1024))
+    for i in range(b.n):
+        b.set_lane(i, gas_limit=10 ** 7)
+    out, ref, _ = run_both(dev, [PROGRAM], b)
+    assert not diff_batches(out, ref)
+    assert [r[1:] for r in out.records(0)] == expected()
+    # every capacity: the same escape point and the same partial log
+    for cap in caps:
+        s = LaneBatch(LaneShape(n=64, stack_cap=64, mem_cap=1024, calldata_cap=32, storage_cap=4,
+                                rec_cap=cap))
+        for i in range(64):
+            s.set_lane(i, gas_limit=10 ** 7)
+        out, ref, _ = run_both(dev, [PROGRAM], s)
+        diffs = diff_batches(out, ref)
+        assert not diffs, (cap, diffs)
+
+
+def test_records_vmtests_and_c2(dev, c2):
+    vectors = [v for v in load_vmtests() if not v["ignored"]]
+    shape = vm_shape(vectors)
+    shape.rec_cap = 1 << 12
+    b = LaneBatch(shape)
+    codes, index = [], {}
+    for i, v in enumerate(vectors):
+        if v["code"] not in index:
+            index[v["code"]] = len(codes)
+            codes.append(bytes.fromhex(v["code"]))
+        fill_lane(b, i, v, index[v["code"]])
+    out, ref, _ = run_both(dev, codes, b)
+    diffs = diff_batches(out, ref)
+    assert not diffs, diffs
+    b = workloads.c2_batch(65536, stack_cap=64, mem_cap=1024, rec_cap=128)
+    out, ref, _ = run_both(dev, [c2], b)
+    diffs = diff_batches(out, ref, limit=20)
+    assert not diffs, diffs
+    assert int(out.rec_len.astype(np.int64).sum()) > 65536 * 10

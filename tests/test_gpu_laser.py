@@ -21,6 +21,9 @@ from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, DepthFirstSe
                                MessageCallTransaction, PluginSkipState, PluginSkipWorldState,
                                WorldState, execute_message_call)
 from mythril_amd.laser.transaction import _setup_global_state_for_execution
+from mythril_amd.smt.exponent_manager import exponent_function_manager
+from mythril_amd.smt.expr import symbol_factory
+from mythril_amd.smt.keccak_manager import keccak_function_manager
 from oracle.evm_ref import OracleEVM
 from vmtests_util import account, fill_lane, load_vmtests, vm_shape
 
@@ -47,6 +50,34 @@ def _oracle_escapes(vectors):
     return {v["name"] for i, v in enumerate(vectors) if int(b.status[i]) == MG_ESCAPE}
 
 
+def _run_vmtest(dev, v):
+    """evm_test.py:124-152: the vector's pre-state, one concrete message call."""
+    world_state = WorldState()
+    for address, details in v["pre"].items():
+        acct = Account(int(address, 16), concrete_storage=True)
+        acct.code = Disassembly(details["code"])      # fixture codes carry no 0x
+        acct.nonce = int(details["nonce"])
+        for key, value in details["storage"].items():
+            acct.storage[int(key, 16)] = int(value, 16)
+        world_state.put_account(acct)
+        acct.set_balance(int(details["balance"], 16))
+    laser_evm = LaserEVM(device=dev)
+    laser_evm.open_states = [world_state]
+    final_states = execute_message_call(
+        laser_evm,
+        callee_address=int(v["address"], 16),
+        caller_address=int(v["caller"], 16),
+        origin_address=int(v["origin"], 16),
+        code=v["code"],
+        gas_limit=int(v["gas"]),
+        data=bytes.fromhex(v["data"]),
+        gas_price=int(v["gas_price"], 16),
+        value=int(v["value"], 16),
+        track_gas=True,
+    )
+    return laser_evm, final_states
+
+
 def test_vmtests_through_laser_evm(dev):
     vectors = [v for v in load_vmtests() if not v["ignored"]]
     escaping = _oracle_escapes(vectors)
@@ -54,29 +85,7 @@ def test_vmtests_through_laser_evm(dev):
     for v in vectors:
         if v["name"] in escaping:
             continue
-        world_state = WorldState()
-        for address, details in v["pre"].items():
-            acct = Account(int(address, 16), concrete_storage=True)
-            acct.code = Disassembly(details["code"])      # fixture codes carry no 0x
-            acct.nonce = int(details["nonce"])
-            for key, value in details["storage"].items():
-                acct.storage[int(key, 16)] = int(value, 16)
-            world_state.put_account(acct)
-            acct.set_balance(int(details["balance"], 16))
-        laser_evm = LaserEVM(device=dev)
-        laser_evm.open_states = [world_state]
-        final_states = execute_message_call(
-            laser_evm,
-            callee_address=int(v["address"], 16),
-            caller_address=int(v["caller"], 16),
-            origin_address=int(v["origin"], 16),
-            code=v["code"],
-            gas_limit=int(v["gas"]),
-            data=bytes.fromhex(v["data"]),
-            gas_price=int(v["gas_price"], 16),
-            value=int(v["value"], 16),
-            track_gas=True,
-        )
+        laser_evm, final_states = _run_vmtest(dev, v)
         gas_used = v["gas_used"]
         if gas_used is not None and gas_used < int(v["block_gas_limit"]):
             gas_min_max = [(s.mstate.min_gas_used, s.mstate.max_gas_used) for s in final_states]
@@ -95,6 +104,55 @@ def test_vmtests_through_laser_evm(dev):
                     assert acct.storage[int(index, 16)].value == int(value, 16), v["name"]
         passed += 1
     assert passed == len(vectors) - len(escaping) == 499
+
+
+# ------------------------------------------------------------------ function managers
+def _oracle_records(vectors):
+    shape = vm_shape(vectors)
+    shape.rec_cap = 1 << 16
+    b = LaneBatch(shape)
+    o = OracleEVM()
+    ids = {}
+    for i, v in enumerate(vectors):
+        if v["code"] not in ids:
+            ids[v["code"]] = o.load_code(bytes.fromhex(v["code"]))
+        fill_lane(b, i, v, ids[v["code"]])
+    o.run(b)
+    return [b.records(i) for i in range(b.n)]
+
+
+def _hash_table():
+    return [(k.value.to_bytes(k.size() // 8, "big"), h.value)
+            for k, h in keccak_function_manager.concrete_hashes.items()]
+
+
+def test_vmtests_function_manager_registrations(dev):
+    """Every SHA3 of a concrete slice lands in keccak_function_manager.concrete_hashes
+    and every concrete EXP adds result == Power(base, exp) to the path's
+    constraints, as the oracle's records of the same vectors say."""
+    vectors = [v for v in load_vmtests() if not v["ignored"]]
+    escaping = _oracle_escapes(vectors)
+    records = _oracle_records(vectors)
+    checked = 0
+    for v, recs in zip(vectors, records):
+        if v["name"] in escaping or not recs:
+            continue
+        keccak_function_manager.reset()
+        _, final_states = _run_vmtest(dev, v)
+        want = []
+        for r in recs:
+            if r[1] == "keccak" and (r[2], r[3]) not in want:
+                want.append((r[2], r[3]))
+        assert _hash_table() == want, v["name"]
+        want_c = [exponent_function_manager.create_condition(
+            symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))[1].raw
+            for r in recs if r[1] == "exp"]
+        assert final_states, v["name"]
+        for s in final_states:
+            assert [c.raw for c in s.world_state.constraints] == want_c, v["name"]
+        checked += 1
+    keccak_function_manager.reset()
+    assert checked >= 15
 
 
 # ------------------------------------------------------------------ hooks
@@ -323,3 +381,48 @@ def test_bounded_loops_strategy_drops_like_the_oracle(dev, hooked):
         assert len(seen) == sum(1 for i in range(len(ns))
                                 for x in b.trace[i, : int(b.trace_len[i])] if x == 3) \
             - sum(1 for i in range(len(ns)) if int(b.status[i]) == 10)
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_keccak_registrations_in_reference_order(dev, strategy):
+    """C2 paths hash mapping slots.  The reference registers each concrete hash
+    when its SHA3 executes, so a hook sees exactly the hashes of instructions
+    that ran before it in the strategy's global order; the final table holds
+    them in first-execution order."""
+    n = 96
+    _, txs = _c2_states(n)
+    b = workloads.c2_batch(n, seed=5, stack_cap=64, mem_cap=1024, rec_cap=512)
+    events = _oracle_events(b.copy(), {0x55}, set())
+    o = OracleEVM()
+    b.code_id[:] = o.load_code(CODE)
+    o.run(b)
+    bfs = strategy is BreadthFirstSearchStrategy
+    key = (lambda step, i: (step, i)) if bfs else (lambda step, i: (-i, step))
+    recs = sorted((key(r[0], i), r[2], r[3]) for i in range(n) for r in b.records(i)
+                  if r[1] == "keccak")
+    assert len(recs) > n
+
+    def seen_before(k):
+        out = []
+        for rk, data, h in recs:
+            if rk < k and (data, h) not in out:
+                out.append((data, h))
+        return len(out)
+
+    flat = sorted((key(rnd, i), i) for i, evs in events.items() for (_, rnd, _, _) in evs)
+    want = [seen_before(k) for k, _ in flat]
+    keccak_function_manager.reset()
+    vm = LaserEVM(device=dev, strategy=strategy)
+    log = []
+    vm.register_hooks("pre", {"SSTORE": [lambda s: log.append(len(keccak_function_manager.concrete_hashes))]})
+    for tx in txs:
+        _setup_global_state_for_execution(vm, tx)
+    vm.exec()
+    assert len(log) == len(want) > 0
+    assert log == want
+    final = []
+    for _, data, h in recs:
+        if (data, h) not in final:
+            final.append((data, h))
+    assert _hash_table() == final
+    keccak_function_manager.reset()
