@@ -115,17 +115,16 @@ class KeccakFunctionManager:
         return And(inv(func(func_input)) == func_input, Or(cond, concrete_cond))
 
     def get_concrete_hash_data(self, model) -> Dict[int, List[Optional[int]]]:
-        """Concrete hash values per input size under `model` (a solver.Model
-        whose function interpretations are FuncInterp tables)."""
-        from .program import FuncInterp
+        """Concrete hash values per input size under `model` (solver.Model /
+        ModelRef): model.eval of every symbolic hash application, without model
+        completion; the ones that stay symbolic are skipped."""
         out: Dict[int, List[Optional[int]]] = {}
         for size, vals in self.hash_result_store.items():
             out[size] = []
-            interp = model.get("keccak256_{}".format(size)) if model is not None else None
             for val in vals:
-                arg = val.raw.args[0]
-                if isinstance(interp, FuncInterp) and arg.op == "const":
-                    out[size].append(interp.entries.get((arg.param,), interp.else_value))
+                ev = model.eval(val.raw)
+                if ev is not None and ev.op == "const":
+                    out[size].append(ev.param)
         return out
 
 

@@ -35,7 +35,7 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence
 
 import numpy as np
 
-from .expr import And, Bool, Node, TRUE, symbol_factory
+from .expr import And, BitVec, Bool, Node, TRUE, _fold, _select, const, symbol_factory
 from .flatten import compile_sets
 from .program import ArrayInterp, FuncInterp, ModelPool
 
@@ -57,24 +57,143 @@ def simplify(expr):
 
 
 # ------------------------------------------------------------------ models
-class Model:
-    """A candidate model: variable values and array / function interpretations.
-    Hashed by identity, as z3 ModelRef objects are (they key the LRU cache)."""
+def _decl(node: Node):
+    """Name of the declaration an expression applies (z3 ``expr.decl()``) when a
+    model can declare it: a variable, an uninterpreted function or an array."""
+    if node.op in ("var", "array"):
+        return node.param if node.op == "var" else node.param[0]
+    if node.op == "uf":
+        return node.param[0]
+    return None
+
+
+class ModelRef:
+    """One interpretation (z3.ModelRef): variable values by name (Bools 0/1),
+    ArrayInterp per symbolic array, FuncInterp per uninterpreted function.
+    Hashed by identity, as z3 models are."""
 
     def __init__(self, assignment: Optional[Dict[str, object]] = None):
         self.assignment: Dict[str, object] = dict(assignment or {})
 
-    def __getitem__(self, name: str):
-        return self.assignment[name]
+    def decls(self) -> List[str]:
+        return list(self.assignment)
+
+    def __getitem__(self, name):
+        return self.assignment.get(name)
 
     def get(self, name: str, default=None):
         return self.assignment.get(name, default)
 
-    def decls(self) -> List[str]:
-        return list(self.assignment)
+    def eval(self, expression, model_completion: bool = False):
+        """z3 ModelRef.eval: substitute the interpretation and simplify (the
+        builders fold constant operands, expr._fold).  Without completion,
+        declarations the model lacks stay symbolic; with it they take 0 (BV),
+        False (Bool), a 0 array default, a 0 function else-value."""
+        raw = expression.raw if hasattr(expression, "raw") else expression
+        out = _substitute(raw, self.assignment, model_completion, {})
+        if isinstance(expression, Bool):
+            return Bool(out)
+        if isinstance(expression, BitVec):
+            return BitVec(out)
+        return out
 
     def __repr__(self):
-        return f"Model({self.assignment})"
+        return f"ModelRef({self.assignment})"
+
+
+def _substitute(node: Node, asg, completion: bool, memo) -> Node:
+    got = memo.get(id(node))
+    if got is not None:
+        return got
+    op = node.op
+    if op in ("const", "array"):
+        out = node
+    elif op == "var":
+        v = asg.get(node.param)
+        if v is None and completion:
+            v = 0
+        out = node if v is None else const(int(v), node.width)
+    else:
+        args = tuple(_substitute(a, asg, completion, memo) for a in node.args)
+        if op == "select":
+            out = _select(args[0], args[1])
+            if out.op == "select" and out.args[0].op == "array" and out.args[1].op == "const":
+                interp = asg.get(out.args[0].param[0])
+                if isinstance(interp, ArrayInterp):
+                    out = const(interp.entries.get(out.args[1].param, interp.default), out.width)
+                elif completion:
+                    out = const(0, out.width)
+        elif op == "uf":
+            out = Node(op, node.width, args, node.param)
+            if all(a.op == "const" for a in args):
+                interp = asg.get(node.param[0])
+                if isinstance(interp, FuncInterp):
+                    key = tuple(a.param for a in args)
+                    out = const(interp.entries.get(key, interp.else_value), node.width)
+                elif completion:
+                    out = const(0, node.width)
+        elif op in ("store", "K"):
+            out = Node(op, node.width, args, node.param)
+        else:
+            out = _fold(op, node.width, args, node.param)
+    memo[id(node)] = out
+    return out
+
+
+class Model:
+    """laser/smt/model.py:6-59: a model made of several internal models (the
+    independence solver's per-bucket models).  ``eval`` uses the first internal
+    model that declares the expression's declaration, else the last one;
+    ``__getitem__`` the first that interprets the item.  ``Model(dict)`` is
+    shorthand for one internal model with that assignment."""
+
+    def __init__(self, models=None):
+        if isinstance(models, dict):
+            models = [ModelRef(models)]
+        elif isinstance(models, ModelRef):
+            models = [models]
+        self.raw: List[ModelRef] = list(models or [])
+
+    def decls(self) -> List[str]:
+        out: List[str] = []
+        for m in self.raw:
+            out.extend(m.decls())
+        return out
+
+    def __getitem__(self, item):
+        if isinstance(item, int):
+            return self.decls()[item]
+        for m in self.raw:
+            r = m[item]
+            if r is not None:
+                return r
+        return None
+
+    def get(self, name: str, default=None):
+        r = self[name]
+        return default if r is None else r
+
+    def view(self, expression) -> Optional[ModelRef]:
+        """The internal model ``eval(expression)`` uses."""
+        raw = expression.raw if hasattr(expression, "raw") else expression
+        d = _decl(raw)
+        for k, m in enumerate(self.raw):
+            if (d is not None and d in m.assignment) or k == len(self.raw) - 1:
+                return m
+        return None
+
+    def eval(self, expression, model_completion: bool = False):
+        m = self.view(expression)
+        return None if m is None else m.eval(expression, model_completion)
+
+    @property
+    def assignment(self) -> Dict[str, object]:
+        """The interpretation quick-sat evaluates a conjunction under: And has no
+        declaration a model can declare, so the last internal model."""
+        return self.raw[-1].assignment if self.raw else {}
+
+    def __repr__(self):
+        return f"Model({[m.assignment for m in self.raw]})"
 
 
 class LRUCache:
@@ -136,8 +255,8 @@ class ModelCache:
         if len(self._memo) > self.QUICK_SAT_MEMO:
             self._memo.popitem(last=False)
 
-    def _pool(self, models: List[Model], prog) -> ModelPool:
-        return ModelPool.from_dicts([m.assignment for m in models], prog.var_names,
+    def _pool(self, models: List[Model], prog, key: Optional[Node] = None) -> ModelPool:
+        return ModelPool.from_dicts([_view(m, key) for m in models], prog.var_names,
                                     prog.var_widths, prog.tables)
 
     def _select(self, model: Model) -> Model:
@@ -154,7 +273,7 @@ class ModelCache:
         if models:
             prog, kept = compile_sets([[key]])
             if kept:
-                fs, _, _ = self.device.eval(prog, self._pool(models, prog))
+                fs, _, _ = self.device.eval(prog, self._pool(models, prog, key))
                 self.device_evals += len(models)
                 self.launches += 1
                 if int(fs[0]) != NO_MODEL:
@@ -169,6 +288,10 @@ class ModelCache:
         models0 = list(reversed(self.model_cache.lru_cache.keys()))
         pos0 = {id(m): i for i, m in enumerate(models0)}
         fresh = list(OrderedDict.fromkeys(k for k in keys if k not in self._memo))
+        if any(_decl(k) is not None for k in fresh) and \
+                any(isinstance(m, Model) and len(m.raw) > 1 for m in models0):
+            # a bare declaration picks a per-query internal model: sequential path
+            return [self.check_quick_sat(k) for k in keys]
         bits: Dict[Node, np.ndarray] = {}
         if models0 and fresh:
             prog, kept = compile_sets([[k] for k in fresh])
@@ -195,6 +318,17 @@ class ModelCache:
             self._memo_put(k, result)
             out.append(result)
         return out
+
+
+def _view(model, key: Optional[Node]) -> Dict[str, object]:
+    """The assignment ``model.eval(key, model_completion=True)`` evaluates
+    under (support_utils.py:65: quick-sat evals the conjunction on the cached
+    model): per Model.eval, the first internal model declaring the key's
+    declaration, else the last."""
+    if isinstance(model, Model):
+        m = model.view(key) if key is not None else (model.raw[-1] if model.raw else None)
+        return m.assignment if m is not None else {}
+    return model.assignment
 
 
 model_cache = ModelCache()

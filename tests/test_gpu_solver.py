@@ -112,3 +112,25 @@ def test_get_model_answers_from_the_device_cache(dev, monkeypatch):
         assert calls and len(calls) < len(qs)
     finally:
         solver.set_solver_backend(solver._no_backend)
+
+
+def test_multi_model_entries_use_their_last_internal_model(dev):
+    """Cached models made of several internal models (the independence
+    solver's, laser/smt/model.py) are evaluated by quick-sat under the last
+    internal model: And has no declaration a model declares (model.py:45-59)."""
+    from mythril_amd.smt.solver import ModelRef
+    qs, singles = _queries_and_models(23, 60, 80)
+    rng = random.Random(5)
+    wrapped = [Model([ModelRef(rng.choice(singles).assignment), ModelRef(m.assignment)])
+               for m in singles]
+    ref = PyModelCache(wrapped)
+    want = [ref.check_quick_sat(q) for q in qs]
+    mc = ModelCache(device=dev)
+    _fill(mc, wrapped)
+    got = [mc.check_quick_sat(q) for q in qs]
+    assert [id(m) if m else None for m in got] == [id(m) if m else None for m in want]
+    assert sum(1 for m in want if m) > 5
+    bat = ModelCache(device=dev)
+    _fill(bat, wrapped)
+    got_b = bat.check_quick_sat_many(qs)
+    assert [id(m) if m else None for m in got_b] == [id(m) if m else None for m in want]
