@@ -308,7 +308,7 @@ enum OpKind : uint32_t {
 __constant__ uint2 kDec[256];
 
 // Generic ALU opcodes: res = f(a, b, c) with a the first word popped.
-__device__ __noinline__ U256 alu_slow(uint32_t op, U256 a, U256 b, U256 c) {
+__device__ __forceinline__ U256 alu_slow(uint32_t op, U256 a, U256 b, U256 c) {
     switch (op) {
     case 0x04: return u_iszero(b) ? u_zero() : z_udiv(a, b);            // DIV  (:505-520)
     case 0x05: return u_iszero(b) ? u_zero() : z_sdiv(a, b);            // SDIV (:522-537)
@@ -383,7 +383,10 @@ struct StepEnv {
 // loop of k_lane_step handles the common opcodes itself and calls this for
 // everything else and for any lane whose fast-path preconditions fail, so
 // every exception, escape and corner case has a single implementation.
-__device__ __noinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t uk, uint32_t ux) {
+// Inlined (as is alu_slow): a call would need the lane registers and this
+// environment in addressable memory, i.e. a scratch frame, and a dispatch with
+// scratch pays ~35 us of setup per launch on gfx950 besides the spill traffic.
+__device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_t uk, uint32_t ux) {
     const DevLanes &L = *E.L;
     const DevCode &C = E.C;
     const uint32_t lane = E.lane;
@@ -754,7 +757,7 @@ __device__ __noinline__ uint64_t trace_step(uint32_t *__restrict__ trace, size_t
 //   * the two top stack words live in registers, the next 14 in an LDS window,
 //     the rest in HBM;
 //   * common opcodes run inline; the rest (and any lane whose preconditions
-//     fail) go through slow_step, outside the loop's register allocation.
+//     fail) go through slow_step, inlined too: the kernel uses no scratch.
 // kLoop: BoundedLoopsStrategy traces on (a separate instantiation, so the common
 // case carries no trace call site in its loop)
 template <bool kLoop>

@@ -31,6 +31,12 @@ PATTERNS = {
     "calldataload": bytes([0x60, 0x04, 0x35, 0x50]) * REP,
     "sload": bytes([0x60, 0x01, 0x54, 0x50]) * REP,
     "sha3_64": bytes([0x60, 0x40, 0x60, 0x00, 0x20, 0x50]) * REP,
+    "caller_pop": bytes([0x33, 0x50]) * REP,
+    "callvalue_pop": bytes([0x34, 0x50]) * REP,
+    "cdsize_pop": bytes([0x36, 0x50]) * REP,
+    "sstore": bytes([0x60, 0x07, 0x60, 0x01, 0x55]) * REP,
+    "jumpi_fall": bytes([0x5B, 0x60, 0x00, 0x60, 0x00, 0x57]) * REP,
+    "exp": bytes([0x60, 0x07]) + bytes([0x60, 0x03, 0x0A]) * REP,
 }
 
 

@@ -9,8 +9,8 @@ src = Path(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out")
 acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(src.glob("pmc_sq*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
-        if k.startswith("k_"):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+        if k.startswith("k_lane_step") or k.startswith("k_bv_eval"):
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
     print(k)
