@@ -47,7 +47,8 @@ struct mg_ctx {
     // staging for upload/download (lane-major)
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
-    DevCounters *d_ctr = nullptr;
+    DevCounters *d_ctr = nullptr;        // [blocks] per-block statistics of the last launch
+    std::vector<DevCounters> h_ctr;
     // kernel 2
     BvState bv{};
 };
@@ -184,7 +185,6 @@ extern "C" int mg_open(int device, mg_ctx **out) {
         uint2 dec[256];
         build_decode(dec);
         if (hipMemcpyToSymbol(HIP_SYMBOL(kDec), dec, sizeof dec) != hipSuccess) { rc = MG_EDEVICE; break; }
-        if (hipMalloc(&ctx->d_ctr, sizeof(DevCounters)) != hipSuccess) { rc = MG_ENOMEM; break; }
     } while (0);
     if (rc != MG_OK) { mg_close(ctx); return rc; }
     *out = ctx;
@@ -196,6 +196,7 @@ static void free_lanes(mg_ctx *ctx) {
     ctx->lane_allocs.clear();
     ctx->have_lanes = ctx->uploaded = false;
     ctx->L = DevLanes{};
+    ctx->d_ctr = nullptr;
 }
 
 extern "C" void mg_close(mg_ctx *ctx) {
@@ -205,7 +206,7 @@ extern "C" void mg_close(mg_ctx *ctx) {
     free_lanes(ctx);
     bv_free(ctx->bv);
     hipFree(ctx->d_codes); hipFree(ctx->d_a8); hipFree(ctx->d_a32); hipFree(ctx->d_cov);
-    hipFree(ctx->d_stage); hipFree(ctx->d_ctr);
+    hipFree(ctx->d_stage);
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -423,6 +424,8 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     if ((rc = lane_alloc(ctx, L.trace_len, N))) return rc;
     if (L.trace_cap && (rc = lane_alloc(ctx, L.trace, (size_t)L.trace_cap * N))) return rc;
     HIPX(ctx, hipMemsetAsync(L.trace_len, 0, N * 4, ctx->stream));
+    // per-block launch statistics (summed on the host)
+    if ((rc = lane_alloc(ctx, ctx->d_ctr, (size_t)(N / LANE_BLOCK + 1)))) return rc;
     L.rec_cap = cfg->rec_cap;
     if ((rc = lane_alloc(ctx, L.rec_len, N))) return rc;
     if (L.rec_cap && (rc = lane_alloc(ctx, L.rec, (size_t)L.rec_cap * N))) return rc;
@@ -782,14 +785,20 @@ extern "C" int mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t 
     if (!ctx) return MG_EINVAL;
     if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_step before mg_lanes_upload");
     HIPX(ctx, hipSetDevice(ctx->device));
-    HIPX(ctx, hipMemsetAsync(ctx->d_ctr, 0, sizeof(DevCounters), ctx->stream));
     HIPX(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr, nullptr, horizon);
     if (rc) return rc;
     HIPX(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    DevCounters c{};
-    HIPX(ctx, hipMemcpyAsync(&c, ctx->d_ctr, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+    const uint32_t nb = blocks_for(ctx->L.n, LANE_BLOCK);
+    ctx->h_ctr.resize(nb);
+    HIPX(ctx, hipMemcpyAsync(ctx->h_ctr.data(), ctx->d_ctr, nb * sizeof(DevCounters), hipMemcpyDeviceToHost,
+                             ctx->stream));
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    DevCounters c{};
+    for (const DevCounters &b : ctx->h_ctr) {
+        c.lane_steps += b.lane_steps; c.running += b.running; c.halted += b.halted;
+        c.hooked += b.hooked; c.escaped += b.escaped;
+    }
     if (stats) {
         float ms = 0.f;
         HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
