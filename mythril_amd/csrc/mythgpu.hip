@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/mythgpu.h"
+#include <cstdlib>
 #include "bv_eval.cuh"
 #include "lane_step.cuh"
 
@@ -48,6 +49,7 @@ struct mg_ctx {
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
     DevCounters *d_ctr = nullptr;        // [blocks] per-block statistics of the last launch
+    uint32_t ctr_cap = 0;
     std::vector<DevCounters> h_ctr;
     // kernel 2
     BvState bv{};
@@ -425,7 +427,8 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     if (L.trace_cap && (rc = lane_alloc(ctx, L.trace, (size_t)L.trace_cap * N))) return rc;
     HIPX(ctx, hipMemsetAsync(L.trace_len, 0, N * 4, ctx->stream));
     // per-block launch statistics (summed on the host)
-    if ((rc = lane_alloc(ctx, ctx->d_ctr, (size_t)(N / LANE_BLOCK + 1)))) return rc;
+    ctx->ctr_cap = (uint32_t)(N / LANE_BLOCK + 1);
+    if ((rc = lane_alloc(ctx, ctx->d_ctr, (size_t)ctx->ctr_cap))) return rc;
     L.rec_cap = cfg->rec_cap;
     if ((rc = lane_alloc(ctx, L.rec_len, N))) return rc;
     if (L.rec_cap && (rc = lane_alloc(ctx, L.rec, (size_t)L.rec_cap * N))) return rc;
@@ -766,6 +769,9 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
         attr_set = true;
     }
     const uint32_t loop_bound = ctx->L.trace_cap ? ctx->loop_bound : 0u;
+    if (ctr && blocks_for(ctx->L.n, LANE_BLOCK) > ctx->ctr_cap)
+        return set_err(ctx, MG_EINVAL, "launch of %u blocks exceeds the %u statistics slots",
+                       blocks_for(ctx->L.n, LANE_BLOCK), ctx->ctr_cap);
     hipLaunchKernelGGL(loop_bound ? k_lane_step<true> : k_lane_step<false>, dim3(blocks_for(ctx->L.n, LANE_BLOCK)),
                        dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
