@@ -5,7 +5,8 @@ Workload (configs[1]): 65,536 concrete lanes per GPU stepping token.sol's
 runtime (precompiled overflow.sol.o, see mythril_amd/workloads.py) with random
 calldata.  One step = one batch: reset every lane from its
 resident initial image (calldata, env, storage already in HBM) and run the
-stepping kernel until every lane has halted.  Weak scaling: every rank runs its
+stepping kernel until every lane has halted; the timed batches are enqueued
+back to back on the library's stream (mg_run_batches) with one host wait.  Weak scaling: every rank runs its
 own 65,536 lanes (seed + rank); the only collective is the coverage all-gather
 after the timed region's batches (§8(e)), over RCCL.
 
@@ -75,26 +76,23 @@ def main():
     dev.alloc(batch.shape, coverage=True)
     dev.upload(workloads.slim_copy(batch))
 
-    def one_batch():
-        dev.reset()
-        return dev.step()
-
-    for _ in range(args.warmup):
-        one_batch()
+    if args.warmup:
+        dev.run_batches(args.warmup)
 
     def barrier():
         if dist_on:
             dist.barrier()
         torch.cuda.synchronize()
 
+    # the K batches are enqueued back to back (reset + stepping launch each,
+    # mg_run_batches) with one host wait: no host round trip between batches
     barrier()
     t0 = time.perf_counter()
-    lane_steps = 0
-    kernel_ms = []
-    for _ in range(args.steps):
-        st = one_batch()
-        lane_steps += st.lane_steps
-        kernel_ms.append(st.kernel_ms)
+    stats = dev.run_batches(args.steps) if args.steps else []
+    lane_steps = sum(st.lane_steps for st in stats)
+    kernel_ms = [st.kernel_ms for st in stats]
+    if any(st.running for st in stats):
+        raise RuntimeError("a C2 batch ended with lanes still running")
     barrier()
     elapsed = time.perf_counter() - t0
 

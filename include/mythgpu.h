@@ -230,6 +230,11 @@ int         mg_set_loop_bound(mg_ctx *ctx, uint32_t bound);
  * (mythril_amd/laser/svm.py).                                                */
 int         mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                           uint32_t max_depth, uint32_t horizon, mg_step_stats *stats);
+/* n_batches whole batches enqueued back to back with one host wait: for each,
+ * mg_lanes_reset then one stepping launch, statistics into stats[b] (kernel_ms
+ * = that batch's stepping kernel).  Same preconditions as mg_lanes_reset.   */
+int         mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
+                           uint32_t max_depth, uint32_t n_batches, mg_step_stats *stats);
 /* Profiling variant (the InstructionProfiler plugin's per-opcode counts,
  * instruction_profiler.py:41-115, as native counters): op_counts[256] =
  * instructions executed per opcode byte; extra[4] = {SHA3 input bytes,

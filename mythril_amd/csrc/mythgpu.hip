@@ -51,6 +51,10 @@ struct mg_ctx {
     DevCounters *d_ctr = nullptr;        // [blocks] per-block statistics of the last launch
     uint32_t ctr_cap = 0;
     std::vector<DevCounters> h_ctr;
+    // mg_run_batches: per-batch statistics slots and per-launch events
+    DevCounters *d_ctr_multi = nullptr;
+    size_t ctr_multi_cap = 0;            // slots
+    std::vector<hipEvent_t> ev_batch;
     // kernel 2
     BvState bv{};
 };
@@ -211,6 +215,8 @@ extern "C" void mg_close(mg_ctx *ctx) {
     hipFree(ctx->d_stage);
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
+    for (hipEvent_t e : ctx->ev_batch) hipEventDestroy(e);
+    hipFree(ctx->d_ctr_multi);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -815,6 +821,68 @@ extern "C" int mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t 
         stats->escaped = c.escaped;
         stats->kernel_ms = ms;
         stats->launches = 1;
+    }
+    return MG_OK;
+}
+
+// Whole batches back to back on the stream: each batch re-initialises every
+// lane from the resident image (k_reset) and steps it (one k_lane_step launch),
+// with its own statistics slots and a HIP event pair around its stepping
+// kernel; the host waits once, after the last batch.  This is the
+// throughput form of `for i in range(n): mg_lanes_reset(); mg_step(...)`
+// (no host round trip between batches).
+extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
+                              uint32_t n_batches, mg_step_stats *stats) {
+    if (!ctx) return MG_EINVAL;
+    if (!stats || n_batches == 0u) return set_err(ctx, MG_EINVAL, "mg_run_batches needs n_batches > 0 and stats");
+    if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_run_batches before mg_lanes_upload");
+    if (!ctx->init_fresh)
+        return set_err(ctx, MG_ESTATE, "mg_run_batches needs an uploaded image with empty stacks and memory");
+    HIPX(ctx, hipSetDevice(ctx->device));
+    const uint32_t nb = blocks_for(ctx->L.n, LANE_BLOCK);
+    const size_t slots = (size_t)nb * n_batches;
+    if (slots > ctx->ctr_multi_cap) {
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(ctx->d_ctr_multi);
+        ctx->d_ctr_multi = nullptr;
+        ctx->ctr_multi_cap = 0;
+        if (hipMalloc(&ctx->d_ctr_multi, slots * sizeof(DevCounters)) != hipSuccess)
+            return set_err(ctx, MG_ENOMEM, "hipMalloc %zu statistics slots", slots);
+        ctx->ctr_multi_cap = slots;
+    }
+    while (ctx->ev_batch.size() < 2u * n_batches) {
+        hipEvent_t e = nullptr;
+        HIPX(ctx, hipEventCreate(&e));
+        ctx->ev_batch.push_back(e);
+    }
+    for (uint32_t b = 0; b < n_batches; ++b) {
+        int rc = mg_lanes_reset(ctx);
+        if (rc) return rc;
+        HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b], ctx->stream));
+        rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr_multi + (size_t)b * nb);
+        if (rc) return rc;
+        HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b + 1u], ctx->stream));
+    }
+    ctx->h_ctr.resize(slots);
+    HIPX(ctx, hipMemcpyAsync(ctx->h_ctr.data(), ctx->d_ctr_multi, slots * sizeof(DevCounters),
+                             hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    for (uint32_t b = 0; b < n_batches; ++b) {
+        DevCounters c{};
+        for (uint32_t k = 0; k < nb; ++k) {
+            const DevCounters &x = ctx->h_ctr[(size_t)b * nb + k];
+            c.lane_steps += x.lane_steps; c.running += x.running; c.halted += x.halted;
+            c.hooked += x.hooked; c.escaped += x.escaped;
+        }
+        float ms = 0.f;
+        HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[2u * b], ctx->ev_batch[2u * b + 1u]));
+        stats[b].lane_steps = c.lane_steps;
+        stats[b].running = c.running;
+        stats[b].halted = c.halted;
+        stats[b].hooked = c.hooked;
+        stats[b].escaped = c.escaped;
+        stats[b].kernel_ms = ms;
+        stats[b].launches = 1;
     }
     return MG_OK;
 }

@@ -130,6 +130,16 @@ class GpuDevice:
         self._check(rc, "mg_step")
         return StepStats(st.lane_steps, st.running, st.halted, st.hooked, st.escaped, st.kernel_ms)
 
+    def run_batches(self, n_batches: int, hook_mask=None, max_steps: int = 1 << 30,
+                    max_depth: int = 0):
+        """mg_run_batches: n_batches x (reset from the resident image + one
+        stepping launch) enqueued back to back, one host wait; per-batch stats."""
+        st = (native.MgStepStats * n_batches)()
+        self._check(self.lib.mg_run_batches(self.ctx, _mask_array(hook_mask), max_steps, max_depth,
+                                            n_batches, st), "mg_run_batches")
+        return [StepStats(s.lane_steps, s.running, s.halted, s.hooked, s.escaped, s.kernel_ms)
+                for s in st]
+
     def step_profile(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0):
         """Step with per-opcode counters; returns (op_counts[256], extra[4])."""
         ops = np.zeros(256, dtype=np.uint64)

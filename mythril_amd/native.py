@@ -91,6 +91,7 @@ SIGNATURES = {
     "mg_lanes_reset": (_I, [_P]),
     "mg_step": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_async": (_I, [_P, _P, _U32, _U32]),
+    "mg_run_batches": (_I, [_P, _P, _U32, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_until": (_I, [_P, _P, _U32, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_set_loop_bound": (_I, [_P, _U32]),
     "mg_eval_bits": (_I, [_P, ctypes.POINTER(MgDagBatch), ctypes.POINTER(MgModelBatch), _P, _P, _P,

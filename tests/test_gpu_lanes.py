@@ -194,6 +194,29 @@ def test_reset_replays_identically(dev, c2):
     assert cov[pcs].all()
 
 
+def test_run_batches_equal_reset_and_step(dev, c2):
+    """mg_run_batches (the bench's timed form) = reset + step per batch: every
+    batch reports the oracle's step count, the final lanes equal the oracle's,
+    and every batch ran to completion."""
+    b = workloads.c2_batch(8192, seed=5, stack_cap=64, mem_cap=1024, rec_cap=128)
+    o = OracleEVM()
+    ref = b.copy()
+    ref.code_id[:] = o.load_code(c2)
+    o.run(ref)
+    b.code_id[:] = dev.load_code(c2)
+    dev.alloc(b.shape)
+    dev.upload(workloads.slim_copy(b))
+    stats = dev.run_batches(4)
+    assert len(stats) == 4
+    for st in stats:
+        assert st.lane_steps == int(ref.steps.sum())
+        assert st.running == 0 and st.kernel_ms > 0
+    out = LaneBatch(b.shape)
+    dev.download(out)
+    out.code_id[:] = ref.code_id
+    assert not diff_batches(out, ref, limit=20)
+
+
 def test_c2_bucketed_order_is_a_permutation(dev, c2):
     """The bench uploads lanes in bucket_order; every lane's result is independent
     of its position, so the permuted device run equals the permuted oracle run."""
