@@ -147,6 +147,8 @@ class LaserEVM:
         # coverage the reference's execute_state hook records for states the
         # device never executes (escaped, skipped by a pre hook)
         self._host_cov: Dict[bytes, set] = defaultdict(set)
+        # coverage other ranks reported (sharded runs, laser/sharded.py), OR-ed in
+        self._peer_cov: Dict[str, np.ndarray] = {}
         self._cap_grow = 1
         log.info("LASER EVM (MI355X batched core) initialized")
 
@@ -638,8 +640,23 @@ class LaserEVM:
             for pc in self._host_cov.get(raw, ()):
                 if pc < bits.size:
                     bits[pc] = True
+            peer = self._peer_cov.get(self._code_objs[raw].bytecode)
+            if peer is not None:
+                bits[:min(bits.size, peer.size)] |= peer[:bits.size].astype(bool)
             out[self._code_objs[raw].bytecode] = (int(bits.size), bits.tolist())
+        for code, peer in self._peer_cov.items():
+            if code not in out:
+                out[code] = (int(peer.size), peer.astype(bool).tolist())
         return out
+
+    def merge_peer_coverage(self, table: Dict[str, np.ndarray]) -> None:
+        """OR other ranks' coverage bytes ({bytecode: uint8[n]}) into coverage()."""
+        for code, bits in table.items():
+            bits = np.asarray(bits, dtype=np.uint8)
+            old = self._peer_cov.get(code)
+            if old is not None and old.size == bits.size:
+                bits = old | bits
+            self._peer_cov[code] = bits
 
 
 def _annotation_of(state: GlobalState) -> JumpdestCountAnnotation:

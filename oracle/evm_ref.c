@@ -99,6 +99,9 @@ typedef struct {
 #define ORC_MAX_CODES 4096
 static orc_code CODES[ORC_MAX_CODES];
 static int n_codes = 0;
+/* optional coverage bytes per code (coverage_plugin.py:68-85 semantics of the
+ * device's mg_coverage: an instruction is covered once a lane starts it) */
+static uint8_t *COV[ORC_MAX_CODES];
 
 /* Python's repr of a bytes object (the text `str(bytes)` returns), used by
  * asm.py:107-123 to look for "bzzr" in the last 43 bytes. */
@@ -176,6 +179,14 @@ void orc_reset_codes(void) {
         free(CODES[i].bytes); free(CODES[i].op); free(CODES[i].addr); free(CODES[i].push);
     }
     n_codes = 0;
+    memset(COV, 0, sizeof COV);
+}
+
+/* Coverage sink of a loaded code (n_instr bytes owned by the caller; NULL = off). */
+int orc_set_coverage(uint32_t id, uint8_t *bytes) {
+    if (id >= (uint32_t)n_codes) return -1;
+    COV[id] = bytes;
+    return 0;
 }
 
 int orc_code_info(uint32_t id, uint32_t *n_instr, uint8_t *ops, uint32_t *addrs) {
@@ -406,6 +417,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         uint32_t rec_new = 0;   /* function-manager record log length after this step */
 
         done++; h->steps[i]++;
+        if (COV[h->code_id[i]]) COV[h->code_id[i]][pc] = 1;
 
 #define STOP_WITH(s, x) do { status = (s); aux = (x); goto stop; } while (0)
 #define EXC(k) STOP_WITH(MG_VMEXC, (k))

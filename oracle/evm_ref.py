@@ -41,6 +41,13 @@ class OracleEVM:
         lib().orc_code_info(code_id, ctypes.byref(n), ops.ctypes.data, addrs.ctypes.data)
         return ops, addrs
 
+    def set_coverage(self, code_id: int, buf: Optional[np.ndarray]) -> None:
+        """Record into `buf` (uint8[n_instr], kept alive by the caller) the
+        instructions lanes of `code_id` start, as the device's mg_coverage."""
+        if buf is not None:
+            assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+        lib().orc_set_coverage(code_id, None if buf is None else buf.ctypes.data)
+
     def run(self, batch, first: int = 0, n: Optional[int] = None,
             hook_mask: Sequence[int] = (0, 0, 0, 0), max_steps: int = 1 << 30,
             max_depth: int = 0, horizon: int = 0, loop_bound: int = 0) -> int:

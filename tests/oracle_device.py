@@ -1,0 +1,89 @@
+"""Test-only stand-in for mythril_amd.device.GpuDevice backed by the C oracle
+(oracle/evm_ref.c), so the host LASER mirror (mythril_amd/laser) and the
+multi-rank drivers run end to end on CPU under `-m "not gpu"` (gloo ranks).
+
+It is test infrastructure: the product path (LaserEVM's default device) is
+GpuDevice, which fails loudly without libmythgpu.so.  Lane images live in a
+host LaneBatch; `step` is one oracle run over it with the launch's hook mask,
+step budget, depth cut, horizon and loop bound, so its results are the ones the
+GPU parity tests pin kernel 1 against.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+from mythril_amd.device import StepStats
+from mythril_amd.lanes import (_ALL_FIELDS, LaneBatch, MG_ESCAPE, MG_HOOK, MG_RUNNING)
+from oracle.evm_ref import OracleEVM
+
+
+class OracleDevice:
+    def __init__(self):
+        self.o = OracleEVM()
+        self.codes = []
+        self._cov: Dict[int, np.ndarray] = {}
+        self._cov_on = False
+        self._img: Optional[LaneBatch] = None
+        self._bound = 0
+        self.shape = None
+
+    # -- codes
+    def load_code(self, code: bytes) -> int:
+        cid = self.o.load_code(bytes(code))
+        self.codes.append(bytes(code))
+        ops, _ = self.o.code_table(cid)
+        self._cov[cid] = np.zeros(max(ops.size, 1), dtype=np.uint8)
+        return cid
+
+    def n_instr(self, code_id: int) -> int:
+        ops, _ = self.o.code_table(code_id)
+        return int(ops.size)
+
+    # -- lanes
+    def alloc(self, shape, coverage: bool = False):
+        self.shape = shape
+        self._img = LaneBatch(shape)
+        self._cov_on = bool(coverage)
+
+    def _copy(self, src: LaneBatch, dst: LaneBatch, first: int, n: int):
+        for f in _ALL_FIELDS:
+            getattr(dst, f)[first:first + n] = getattr(src, f)[first:first + n]
+
+    def upload(self, batch: LaneBatch, first: int = 0):
+        self._copy(batch, self._img, first, batch.n)
+
+    def download(self, batch: LaneBatch, first: int = 0):
+        self._copy(self._img, batch, first, batch.n)
+
+    def upload_range(self, batch: LaneBatch, first: int, n: int):
+        self._copy(batch, self._img, first, n)
+
+    def download_range(self, batch: LaneBatch, first: int, n: int):
+        self._copy(self._img, batch, first, n)
+
+    def set_loop_bound(self, bound: int):
+        self._bound = int(bound)
+
+    def step(self, hook_mask=None, max_steps: int = 1 << 30, max_depth: int = 0,
+             horizon: int = 0) -> StepStats:
+        for cid, buf in self._cov.items():
+            self.o.set_coverage(cid, buf if self._cov_on else None)
+        bound = self._bound if self._img.shape.trace_cap else 0
+        steps = self.o.run(self._img, hook_mask=hook_mask or (0, 0, 0, 0), max_steps=max_steps,
+                           max_depth=max_depth, horizon=horizon, loop_bound=bound)
+        for cid in self._cov:
+            self.o.set_coverage(cid, None)
+        s = self._img.status
+        return StepStats(steps, int((s == MG_RUNNING).sum()),
+                         int(((s != MG_RUNNING) & (s != MG_HOOK) & (s != MG_ESCAPE)).sum()),
+                         int((s == MG_HOOK).sum()), int((s == MG_ESCAPE).sum()), 0.0)
+
+    # -- coverage
+    def coverage(self, code_id: int) -> np.ndarray:
+        return self._cov[code_id][:self.n_instr(code_id)].copy()
+
+    def coverage_clear(self):
+        for buf in self._cov.values():
+            buf[:] = 0
