@@ -36,6 +36,15 @@ struct DevLanes {
     uint32_t *rec;       // [rec_cap][N]
 };
 
+// Resident initial image of a batch (mg_lanes_reset); passed to the stepping
+// kernel when it re-initialises every lane itself before stepping
+// (mg_run_batches), pc == nullptr otherwise.
+struct DevResetImage {
+    const uint32_t *pc, *depth, *status, *aux, *steps, *storage_count;
+    const uint64_t *gas_min, *gas_max;
+    const uint4 *storage;
+};
+
 // One loaded code (Disassembly): arrays live in one device arena.
 struct DevCode {
     uint32_t n_instr;    // len(instruction_list)

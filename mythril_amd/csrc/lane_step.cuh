@@ -760,6 +760,25 @@ __device__ __noinline__ uint64_t trace_step(uint32_t *__restrict__ trace, size_t
 //     fail) go through slow_step, inlined too: the kernel uses no scratch.
 // kLoop: BoundedLoopsStrategy traces on (a separate instantiation, so the common
 // case carries no trace call site in its loop)
+// Re-initialise one lane from the resident image (mg_lanes_reset): empty stack,
+// memory, traces and record logs; pc, depth, status, gas and storage from the image.
+__device__ __forceinline__ void reset_lane(const DevLanes &L, const DevResetImage &R, uint32_t lane) {
+    L.pc[lane] = R.pc[lane]; L.sp[lane] = 0; L.msize[lane] = 0; L.depth[lane] = R.depth[lane];
+    L.status[lane] = R.status[lane]; L.aux[lane] = R.aux[lane]; L.steps[lane] = R.steps[lane];
+    L.gas_min[lane] = R.gas_min[lane]; L.gas_max[lane] = R.gas_max[lane];
+    L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
+    L.trace_len[lane] = 0;                 // reset images start with empty traces
+    L.rec_len[lane] = 0;                   // ... and empty record logs
+    const uint32_t cnt = R.storage_count[lane];
+    L.storage_count[lane] = cnt;
+    for (uint32_t s = 0; s < cnt; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const size_t idx = ((size_t)s * L.N + lane) * 4 + k;
+            L.storage[idx] = R.storage[idx];
+        }
+}
+
 template <bool kLoop>
 __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
                                                           const uint8_t *__restrict__ a8,
@@ -770,7 +789,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           DevCounters *__restrict__ ctr,
                                                           unsigned long long *__restrict__ prof,
                                                           uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
-                                                          uint32_t horizon, uint32_t loop_bound) {
+                                                          uint32_t horizon, uint32_t loop_bound,
+                                                          DevResetImage R) {
     // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
     //              [runs: pd_cap x 8 B][push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B]
     //              [coverage: pd_cap]
@@ -790,6 +810,9 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
 
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     const bool in_range = lane < L.n;
+    // mg_run_batches: re-initialise the lane from the resident image first (the
+    // reads below see this thread's own stores)
+    if (R.pc != nullptr && in_range) reset_lane(L, R, lane);
     uint32_t status = in_range ? L.status[lane] : ST_STOP;
     const uint32_t my_code = in_range ? L.code_id[lane] : 0u;
     for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_dec[i] = kDec[i];

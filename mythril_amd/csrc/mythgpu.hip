@@ -493,27 +493,10 @@ __global__ void k_gather_bytes(const uint32_t *__restrict__ src, uint32_t n, uin
     p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
 // restore the working state from the resident initial image
-__global__ void k_reset(DevLanes L, const uint32_t *__restrict__ i_pc, const uint32_t *__restrict__ i_depth,
-                        const uint32_t *__restrict__ i_status, const uint32_t *__restrict__ i_aux,
-                        const uint32_t *__restrict__ i_steps, const uint32_t *__restrict__ i_cnt,
-                        const uint64_t *__restrict__ i_gmin, const uint64_t *__restrict__ i_gmax,
-                        const uint4 *__restrict__ i_storage) {
+__global__ void k_reset(DevLanes L, DevResetImage R) {
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= L.n) return;
-    L.pc[lane] = i_pc[lane]; L.sp[lane] = 0; L.msize[lane] = 0; L.depth[lane] = i_depth[lane];
-    L.status[lane] = i_status[lane]; L.aux[lane] = i_aux[lane]; L.steps[lane] = i_steps[lane];
-    L.gas_min[lane] = i_gmin[lane]; L.gas_max[lane] = i_gmax[lane];
-    L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
-    L.trace_len[lane] = 0;                 // reset images start with empty traces
-    L.rec_len[lane] = 0;                   // ... and empty record logs
-    const uint32_t cnt = i_cnt[lane];
-    L.storage_count[lane] = cnt;
-    for (uint32_t s = 0; s < cnt; ++s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const size_t idx = ((size_t)s * L.N + lane) * 4 + k;
-            L.storage[idx] = i_storage[idx];
-        }
+    reset_lane(L, R, lane);
 }
 
 static int ensure_stage(mg_ctx *ctx, size_t bytes) {
@@ -723,14 +706,17 @@ extern "C" int mg_set_loop_bound(mg_ctx *ctx, uint32_t bound) {
     return MG_OK;
 }
 
+static DevResetImage reset_image(const mg_ctx *ctx) {
+    return DevResetImage{ctx->i_pc, ctx->i_depth, ctx->i_status, ctx->i_aux, ctx->i_steps,
+                         ctx->i_storage_count, ctx->i_gas_min, ctx->i_gas_max, ctx->i_storage};
+}
+
 extern "C" int mg_lanes_reset(mg_ctx *ctx) {
     if (!ctx) return MG_EINVAL;
     if (!ctx->uploaded) return set_err(ctx, MG_ESTATE, "mg_lanes_reset before mg_lanes_upload");
     if (!ctx->init_fresh)
         return set_err(ctx, MG_ESTATE, "mg_lanes_reset needs an uploaded image with empty stacks and memory");
-    hipLaunchKernelGGL(k_reset, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, ctx->i_pc,
-                       ctx->i_depth, ctx->i_status, ctx->i_aux, ctx->i_steps, ctx->i_storage_count,
-                       ctx->i_gas_min, ctx->i_gas_max, ctx->i_storage);
+    hipLaunchKernelGGL(k_reset, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, reset_image(ctx));
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
@@ -754,7 +740,8 @@ static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_
 }
 
 static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
-                       DevCounters *ctr, unsigned long long *prof = nullptr, uint32_t horizon = 0) {
+                       DevCounters *ctr, unsigned long long *prof = nullptr, uint32_t horizon = 0,
+                       const DevResetImage *reset = nullptr) {
     const uint64_t zero[4] = {0, 0, 0, 0};
     const uint64_t *m = hook_mask ? hook_mask : zero;
     uint32_t win = 0, pd_cap = 0, jr_cap = 0;
@@ -782,7 +769,7 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
                        m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
-                       loop_bound);
+                       loop_bound, reset ? *reset : DevResetImage{});
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
@@ -826,7 +813,7 @@ extern "C" int mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t 
 }
 
 // Whole batches back to back on the stream: each batch re-initialises every
-// lane from the resident image (k_reset) and steps it (one k_lane_step launch),
+// lane from the resident image and steps it (one k_lane_step launch),
 // with its own statistics slots and a HIP event pair around its stepping
 // kernel; the host waits once, after the last batch.  This is the
 // throughput form of `for i in range(n): mg_lanes_reset(); mg_step(...)`
@@ -855,11 +842,13 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
         HIPX(ctx, hipEventCreate(&e));
         ctx->ev_batch.push_back(e);
     }
+    // the stepping kernel re-initialises its lanes itself (reset_lane in its
+    // prologue): one launch per batch
+    const DevResetImage R = reset_image(ctx);
     for (uint32_t b = 0; b < n_batches; ++b) {
-        int rc = mg_lanes_reset(ctx);
-        if (rc) return rc;
         HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b], ctx->stream));
-        rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr_multi + (size_t)b * nb);
+        int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr_multi + (size_t)b * nb,
+                             nullptr, 0u, &R);
         if (rc) return rc;
         HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b + 1u], ctx->stream));
     }

@@ -13,8 +13,13 @@ InstructionProfiler plugin's per-opcode counts as native counters):
   (MLOAD/MSTORE 32, MSTORE8 1, CALLDATALOAD 32, *COPY size, SHA3 length) + 64 per
   SLOAD/SSTORE + 1 opcode byte + push-immediate bytes.
 
-Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; INT32 VALU 256 CU x 64 lanes x
-2.4 GHz = 39.3 T ops/s.  The dominant kernel's fraction is the larger one.
+Peaks (MI355X_MICROARCH.md): HBM 8.0 TB/s; INT32 VALU 256 CU x 4 SIMDs x 32
+lanes/clk (a wave64 VALU instruction issues over 2 cycles) x 2.4 GHz = 78.6 T
+ops/s, the integer counterpart of the guide's 157.3 TF f32 vector peak.  The
+dominant kernel's fraction is the larger one.  Next to the nominal peaks every
+roofline also carries the sustained ones the box measured with
+scripts/probes/peaks.hip (profiles/<round>/peaks.json): 16-byte streaming
+reads, and 16 independent add/xor chains per lane at 8 waves per SIMD.
 """
 from __future__ import annotations
 
@@ -24,7 +29,31 @@ from pathlib import Path
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0
-VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12   # 39.32
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64
+PROFILES = Path(__file__).resolve().parent.parent / "profiles"
+
+
+def sustained_peaks():
+    """(HBM read GB/s, INT32 T ops/s) measured on the box by
+    scripts/probes/peaks.hip, newest round first; (None, None) if absent."""
+    for f in sorted(PROFILES.glob("r*/peaks.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+            return float(d["hbm_read_gbs"]), float(d["int32_tops"])
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
+def with_sustained(roof: dict) -> dict:
+    """Add peak_sustained / frac_sustained for the roofline's bound."""
+    hbm, valu = sustained_peaks()
+    peak = hbm if roof["bound"] == "hbm" else valu
+    if peak:
+        roof["peak_sustained"] = peak
+        roof["frac_sustained"] = roof["achieved"] / peak
+        roof["peak_sustained_source"] = "scripts/probes/peaks.hip (profiles/*/peaks.json)"
+    return roof
 
 
 def _tables():
@@ -91,7 +120,6 @@ def algorithmic_work(op_counts: np.ndarray, extra: np.ndarray):
     return ops, byts, steps
 
 
-PROFILES = Path(__file__).resolve().parent.parent / "profiles"
 
 
 def pmc_traffic(kernel: str):
@@ -124,7 +152,7 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
     hbm_frac = gbs / HBM_PEAK_GBS
     valu_frac = tops / VALU_PEAK_TOPS
     primary_hbm = hbm_frac >= valu_frac
-    return {
+    return with_sustained({
         "bound": "hbm" if primary_hbm else "valu-int32",
         "achieved": gbs if primary_hbm else tops,
         "peak": HBM_PEAK_GBS if primary_hbm else VALU_PEAK_TOPS,
@@ -143,4 +171,4 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
                 "achieved": tops if primary_hbm else gbs,
                 "peak": VALU_PEAK_TOPS if primary_hbm else HBM_PEAK_GBS,
                 "frac": valu_frac if primary_hbm else hbm_frac},
-    }
+    })
