@@ -1,0 +1,9 @@
+#!/bin/bash
+# SQ counters of kernel 2 per C4 op class (scripts/k2_opclass.py), two passes.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_WAVE_CYCLES -d $OUT/pmck2_a -o run --output-format csv -- python3 scripts/k2_opclass.py > $OUT/pmck2_a.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH -d $OUT/pmck2_b -o run --output-format csv -- python3 scripts/k2_opclass.py > $OUT/pmck2_b.log 2>&1
