@@ -53,6 +53,7 @@ enum BvOp : uint32_t {
 #define BV_BLOCK 256u
 #define BV_TILE_INSNS 2048u   // longest program (LDS tile upper bound: 32 KiB)
 #define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
+#define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
 
 struct BvState {
@@ -203,10 +204,13 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     if (d0 >= d1) return;
     // the tile is read from HBM once per block and reused for every model chunk
     const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
-    if (kLdsProg) {
+    // per-block results of the tile's DAGs: waves combine in LDS, the block adds
+    // its totals to HBM once per DAG (not one atomic pair per wave per DAG)
+    __shared__ uint32_t blk_cnt[BV_TILE_DAGS], blk_first[BV_TILE_DAGS];
+    if (threadIdx.x < BV_TILE_DAGS) { blk_cnt[threadIdx.x] = 0u; blk_first[threadIdx.x] = 0xffffffffu; }
+    if (kLdsProg)
         for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
-        __syncthreads();
-    }
+    __syncthreads();
 
     const uint32_t tid = threadIdx.x;
     const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
@@ -318,10 +322,18 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
             // optional per-model bitmap (one u64 per wave): lets the host replay
             // sequential check_quick_sat calls whose LRU bumps reorder the pool
             if (sat_bits) sat_bits[(size_t)d * bit_words + ((chunk * BV_BLOCK + tid) >> 6)] = bal;
-            atomicAdd(&sat_count[d], (uint32_t)__popcll(bal));
-            atomicMin(&first_sat[d], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
+            atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
+            atomicMin(&blk_first[d - d0], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
         }
     }
+    }
+    __syncthreads();
+    if (tid < d1 - d0) {
+        const uint32_t n = blk_cnt[tid], f = blk_first[tid];
+        if (n) {
+            atomicAdd(&sat_count[d0 + tid], n);
+            atomicMin(&first_sat[d0 + tid], f);
+        }
     }
 }
 
@@ -390,7 +402,7 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     uint32_t acc = 0;
     for (uint32_t d = 0; d < n; ++d) {
         const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
-        if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= 64u) { s.h_tiles.push_back(d); acc = 0; }
+        if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= BV_TILE_DAGS) { s.h_tiles.push_back(d); acc = 0; }
         acc += len;
     }
     s.h_tiles.push_back(n);
