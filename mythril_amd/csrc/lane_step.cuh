@@ -560,6 +560,9 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
             break;
         }
         case K_CODECOPY: {  // extends even for size 0; copy stops at the end of code
+            // creation transaction (symbolic calldata): an offset at or past the end
+            // of the code copies constructor arguments (instructions.py:1089-1098)
+            if ((E.flags & LANE_CREATION) && !(u_fits32(b) && b.w[0] < C.n_bytes)) ESCX(ESC_OPCODE)
             MEMX(a, c, (int64_t)gtab_min)
             GASCOMMIT()
             ZEROFILL()
@@ -693,7 +696,7 @@ DEV bool alu_is_fast(uint32_t op) { return op <= 0x03u || op == 0x0bu || (op >= 
 #define PD_SPECIAL (1u << 30)    // kind >= K_ESCAPE (host opcode or past-the-end)
 DEV uint32_t pd_flags(uint32_t op, uint32_t dy, uint32_t hook) {
     const uint32_t kind = (dy >> 9) & 31u;
-    return (hook << 31) | (kind >= K_ESCAPE ? PD_SPECIAL : 0u) | (op - 0x35u < 5u ? PD_CREATION : 0u);
+    return (hook << 31) | (kind >= K_ESCAPE ? PD_SPECIAL : 0u) | (op - 0x35u < 4u ? PD_CREATION : 0u);
 }
 
 // ---- BoundedLoopsStrategy (bounded_loops.py:49-145) ---------------------------

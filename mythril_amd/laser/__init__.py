@@ -8,9 +8,12 @@ from .state import (Account, Environment, GlobalState, MachineStack, MachineStat
 from .strategy import (BoundedLoopsStrategy, BreadthFirstSearchStrategy, DepthFirstSearchStrategy,
                        JumpdestCountAnnotation)
 from .svm import LaserEVM
-from .transaction import MessageCallTransaction, execute_message_call, tx_id_manager
+from .transaction import (ContractCreationTransaction, MessageCallTransaction,
+                          execute_contract_creation, execute_message_call, generate_contract_address,
+                          tx_id_manager)
 
 __all__ = ["Account", "BoundedLoopsStrategy", "BreadthFirstSearchStrategy",
+           "ContractCreationTransaction", "execute_contract_creation", "generate_contract_address",
            "JumpdestCountAnnotation", "DepthFirstSearchStrategy", "Disassembly",
            "Environment", "GlobalState", "InstructionCoveragePlugin", "LaserEVM", "LaserPlugin",
            "MachineStack", "MachineState", "Memory", "MessageCallTransaction",

@@ -48,7 +48,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
-                     MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
+                     MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
                      limbs_to_word, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import symbol_factory
@@ -57,6 +57,7 @@ from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_element
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
 from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
+from .transaction import ContractCreationTransaction, install_runtime_code
 
 log = logging.getLogger(__name__)
 
@@ -340,7 +341,8 @@ class LaserEVM:
         b.depth[i] = ms.depth
         b.status[i] = MG_RUNNING
         b.aux[i] = 0
-        b.flags[i] = MG_LANE_STATIC if env.static else 0
+        b.flags[i] = (MG_LANE_STATIC if env.static else 0) | (
+            MG_LANE_CREATION if isinstance(tx, ContractCreationTransaction) else 0)
         b.gas_min[i] = ms.min_gas_used
         b.gas_max[i] = ms.max_gas_used
         b.gas_limit[i] = _NO_GAS_LIMIT if gas_limit is None else min(concrete(gas_limit), _NO_GAS_LIMIT)
@@ -585,11 +587,22 @@ class LaserEVM:
 
         tx = s.current_transaction
         if status in (MG_HALT_STOP, MG_HALT_RETURN):
-            if status == MG_HALT_RETURN and tx is not None:
+            keep = True
+            if isinstance(tx, ContractCreationTransaction):
+                # transaction_models.py:265-284 + svm.py:459-466: only a creation
+                # that returns code installs it and keeps its world state
+                data = _return_data(b, i) if status == MG_HALT_RETURN else b""
+                if data:
+                    install_runtime_code(tx, s, data)
+                else:
+                    tx.return_data = None
+                    keep = False
+            elif status == MG_HALT_RETURN and tx is not None:
                 tx.return_data = _return_data(b, i)
             for hook in self._transaction_end_hooks:
                 hook(s, tx, None, False)
-            self._add_world_state(s)
+            if keep:
+                self._add_world_state(s)
         elif status == MG_HALT_REVERT:
             if tx is not None:
                 tx.return_data = _return_data(b, i)

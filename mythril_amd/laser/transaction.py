@@ -1,16 +1,25 @@
-"""Concrete message calls into the batched LASER core.
+"""Concrete message calls and contract creations into the batched LASER core.
 
-Mirrors transaction/concolic.py:75-151 (``execute_message_call`` and
-``_setup_global_state_for_execution``) and the parts of
-transaction/transaction_models.py:21-232 those use (tx ids, MessageCallTransaction,
-initial_global_state with the value transfer).  Balances are concrete here: the
-reference's ``UGE(balances[sender], value)`` conjunct is a constant for
-concrete balances and is not recorded.
+Mirrors transaction/concolic.py:23-151 (``execute_contract_creation``,
+``execute_message_call`` and ``_setup_global_state_for_execution``) and the parts
+of transaction/transaction_models.py:21-284 those use (tx ids,
+MessageCallTransaction, ContractCreationTransaction, initial_global_state with the
+value transfer, the creation ``end`` that installs the returned runtime code).
+Balances are concrete here: the reference's ``UGE(balances[sender], value)``
+conjunct is a constant for concrete balances and is not recorded.
+
+A creation transaction's calldata is the reference's ``SymbolicCalldata``
+(concolic.py:57-70 passes ``call_data=None``): its lanes carry
+MG_LANE_CREATION, so CALLDATALOAD/SIZE/COPY, CODESIZE and a CODECOPY from at or
+past the end of the code (constructor arguments) escape to the host; an
+argument-less constructor (CODECOPY of its own runtime code, RETURN) runs on the
+device end to end.
 """
 from __future__ import annotations
 
 from typing import List, Optional, Union
 
+from ..keccak import keccak256
 from .disassembly import Disassembly
 from .state import (Account, Environment, GlobalState, WorldState, concrete)
 
@@ -87,6 +96,87 @@ class MessageCallTransaction:
                                                  concrete(self.callee_account.address))
 
 
+def _rlp_item(b: bytes) -> bytes:
+    if len(b) == 1 and b[0] < 0x80:
+        return b
+    assert len(b) < 56
+    return bytes([0x80 + len(b)]) + b
+
+
+def generate_contract_address(creator: int, nonce: int) -> int:
+    """py-evm ``eth._utils.address.generate_contract_address`` (used at
+    world_state.py:237): keccak256(rlp([sender, nonce]))[12:]."""
+    sender = _rlp_item(creator.to_bytes(20, "big"))
+    n = _rlp_item(nonce.to_bytes((nonce.bit_length() + 7) // 8, "big") if nonce else b"")
+    payload = sender + n
+    return int.from_bytes(keccak256(bytes([0xC0 + len(payload)]) + payload)[12:], "big")
+
+
+def create_account(world_state: WorldState, balance=0, address=None, concrete_storage=False,
+                   creator=None, code=None, nonce=0) -> Account:
+    """world_state.py:142-186: the creator's nonce picks the new address (and is
+    bumped); a missing creator account is created first."""
+    accounts = world_state.accounts
+    if creator is not None:
+        creator = concrete(creator)
+    if creator in accounts:
+        nonce = accounts[creator].nonce
+    elif creator:
+        create_account(world_state, address=creator)
+    if address is None:
+        if not creator:
+            raise ValueError("a concrete creation needs a creator (the reference draws a random address)")
+        address = generate_contract_address(creator, accounts[creator].nonce)
+    if creator:
+        accounts[creator].nonce += 1
+    acct = Account(address, code=code, concrete_storage=concrete_storage, nonce=nonce)
+    acct.set_balance(balance)
+    world_state.put_account(acct)
+    return acct
+
+
+class ContractCreationTransaction(MessageCallTransaction):
+    """transaction_models.py:206-284: a fresh account (concrete storage) runs the
+    creation code; ``end`` with non-empty return data installs it as the
+    account's code and returns the address, otherwise the world state is not
+    kept (svm.py:459-466)."""
+
+    def __init__(self, world_state: WorldState, caller=None, call_data=None, identifier=None,
+                 gas_price=0, gas_limit=None, origin=None, code: Optional[Disassembly] = None,
+                 call_value=0, contract_name=None, contract_address=None, base_fee=0):
+        contract_address = contract_address if isinstance(contract_address, int) else None
+        callee_account = create_account(world_state, 0, concrete_storage=True, creator=caller,
+                                        address=contract_address)
+        callee_account.contract_name = contract_name or callee_account.contract_name
+        super().__init__(world_state, callee_account, caller, b"", identifier, gas_price, gas_limit,
+                         origin, code, call_value, False, base_fee)
+        self.symbolic_calldata = call_data is None
+
+    def initial_global_state(self) -> GlobalState:
+        gs = super().initial_global_state()
+        gs.environment.active_function_name = "constructor"
+        return gs
+
+    def end(self, global_state: GlobalState, return_data=None, revert=False) -> None:
+        if not return_data:
+            self.return_data = None
+            raise TransactionEndSignal(global_state, revert)
+        install_runtime_code(self, global_state, return_data)
+        raise TransactionEndSignal(global_state, revert)
+
+
+def install_runtime_code(tx: ContractCreationTransaction, global_state: GlobalState,
+                         return_data: bytes) -> None:
+    """transaction_models.py:277-283: assign_bytecode(return data) on the active
+    account; the transaction's return data becomes the account's address."""
+    account = global_state.environment.active_account
+    account.code = Disassembly(bytes(return_data))
+    if concrete(account.address) in global_state.world_state.accounts:
+        global_state.world_state.accounts[concrete(account.address)].code = account.code
+    tx.return_data = hex(concrete(account.address))
+    assert account.code.instruction_list != []
+
+
 def _setup_global_state_for_execution(laser_evm, transaction) -> None:
     global_state = transaction.initial_global_state()
     global_state.transaction_stack.append((transaction, None))
@@ -118,3 +208,29 @@ def execute_message_call(laser_evm, callee_address, caller_address, origin_addre
         )
         _setup_global_state_for_execution(laser_evm, transaction)
     return laser_evm.exec(track_gas=track_gas)
+
+
+def execute_contract_creation(laser_evm, callee_address, caller_address, origin_address, data,
+                              gas_limit, gas_price, value, code=None, track_gas=False,
+                              contract_name=None) -> Union[None, List[GlobalState]]:
+    """concolic.execute_contract_creation (concolic.py:23-72): one
+    ContractCreationTransaction per open world state running ``data`` as the
+    creation code (symbolic calldata), then ``laser_evm.exec(True, track_gas)``."""
+    open_states: List[WorldState] = laser_evm.open_states[:]
+    del laser_evm.open_states[:]
+    for open_world_state in open_states:
+        next_transaction_id = tx_id_manager.get_next_tx_id()
+        transaction = ContractCreationTransaction(
+            world_state=open_world_state,
+            identifier=next_transaction_id,
+            gas_price=gas_price,
+            gas_limit=gas_limit,
+            origin=origin_address,
+            code=Disassembly(data),
+            caller=caller_address,
+            contract_name=contract_name,
+            call_data=None,
+            call_value=value,
+        )
+        _setup_global_state_for_execution(laser_evm, transaction)
+    return laser_evm.exec(True, track_gas=track_gas)

@@ -400,9 +400,10 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         if (hooked) { h->status[i] = MG_HOOK; h->aux[i] = op; break; }
         if (budget) break;
         if (is_env_escape(op) ||
-            ((flags & MG_LANE_CREATION) && op >= 0x35 && op <= 0x39)) {
-            /* creation lanes: CALLDATALOAD/SIZE/COPY and CODESIZE/COPY follow the
-             * constructor-argument rules of instructions.py:887-1003,1089-1139 */
+            ((flags & MG_LANE_CREATION) && op >= 0x35 && op <= 0x38)) {
+            /* creation lanes: CALLDATALOAD/SIZE/COPY and CODESIZE follow the
+             * constructor-argument rules of instructions.py:887-1003 (CODECOPY
+             * below: only offsets past the code read the symbolic calldata) */
             h->status[i] = MG_ESCAPE; h->aux[i] = op | (MG_ESC_OPCODE << 8); break;
         }
 
@@ -597,6 +598,9 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         case 0x38: PUSH1(u_from64(c->n_bytes)); break;   /* CODESIZE (:978-1003) */
         case 0x39: { /* CODECOPY -> _code_copy_helper (:1073-1250) */
             NEED_POP(3); a = POP(); b = POP(); cc = POP();   /* memory_offset, code_offset, size */
+            /* creation tx with SymbolicCalldata: code_offset >= code_size copies
+             * constructor arguments (instructions.py:1089-1098) -> host */
+            if ((flags & MG_LANE_CREATION) && !(u_fits64(b) && b.w[0] < c->n_bytes)) ESC(MG_ESC_OPCODE);
             MEMX(a, cc, info->gmin);                        /* even for size 0 */
             COMMIT_GAS();
             ZERO_FILL();
