@@ -232,7 +232,9 @@ int         mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max
                           uint32_t max_depth, uint32_t horizon, mg_step_stats *stats);
 /* n_batches whole batches enqueued back to back with one host wait: for each,
  * mg_lanes_reset then one stepping launch, statistics into stats[b] (kernel_ms
- * = that batch's stepping kernel).  Same preconditions as mg_lanes_reset.   */
+ * = the sequence's device time / n_batches, launch gaps included; with
+ * MG_BATCH_EVENTS=1 each launch is bracketed instead).  Same preconditions as
+ * mg_lanes_reset.                                                           */
 int         mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps,
                            uint32_t max_depth, uint32_t n_batches, mg_step_stats *stats);
 /* Profiling variant (the InstructionProfiler plugin's per-opcode counts,

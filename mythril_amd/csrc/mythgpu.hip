@@ -845,12 +845,20 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
     // the stepping kernel re-initialises its lanes itself (reset_lane in its
     // prologue): one launch per batch
     const DevResetImage R = reset_image(ctx);
+    // one event pair around the whole sequence, each batch reporting the mean:
+    // timing events between the launches cost ~8 us per batch on MI355X (C2
+    // 0.1765 -> 0.1688 ms per batch, scripts/gpu_ab_events.sh).  The mean includes
+    // the launch gaps, so it is an upper bound of the kernel's own duration.
+    // MG_BATCH_EVENTS=1 brackets every launch instead.
+    const char *bev = getenv("MG_BATCH_EVENTS");
+    const bool per_batch_events = bev && bev[0] == '1';
     for (uint32_t b = 0; b < n_batches; ++b) {
-        HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b], ctx->stream));
+        if (per_batch_events || b == 0u) HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b], ctx->stream));
         int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr_multi + (size_t)b * nb,
                              nullptr, 0u, &R);
         if (rc) return rc;
-        HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b + 1u], ctx->stream));
+        if (per_batch_events || b + 1u == n_batches)
+            HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b + 1u], ctx->stream));
     }
     ctx->h_ctr.resize(slots);
     HIPX(ctx, hipMemcpyAsync(ctx->h_ctr.data(), ctx->d_ctr_multi, slots * sizeof(DevCounters),
@@ -864,7 +872,12 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
             c.hooked += x.hooked; c.escaped += x.escaped;
         }
         float ms = 0.f;
-        HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[2u * b], ctx->ev_batch[2u * b + 1u]));
+        if (per_batch_events) {
+            HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[2u * b], ctx->ev_batch[2u * b + 1u]));
+        } else {
+            HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[0], ctx->ev_batch[2u * n_batches - 1u]));
+            ms /= (float)n_batches;
+        }
         stats[b].lane_steps = c.lane_steps;
         stats[b].running = c.running;
         stats[b].halted = c.halted;
