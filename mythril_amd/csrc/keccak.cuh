@@ -23,6 +23,22 @@ __device__ __forceinline__ uint64_t krotl(uint64_t v, int r) {
     return r == 0 ? v : ((v << r) | (v >> (64 - r)));
 }
 
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one VALU instruction
+// (truth-table index = S0*4 + S1*2 + S2).  Keccak's theta parities and theta
+// update are 3-way XORs (0x96) and chi's a ^ (~b & c) is table 0xD2: on 32-bit
+// halves that is one instruction where the xor / bfi+xor forms take two — at one
+// wave per SIMD (kernel 1's C2 grid) the VALU instruction count is the latency.
+__device__ __forceinline__ uint64_t k_xor3(uint64_t a, uint64_t b, uint64_t c) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t k_chi(uint64_t a, uint64_t b, uint64_t c) {   // a ^ (~b & c)
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0xD2);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0xD2);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // In-place rounds: theta with 5 column parities, rho+pi as the single 24-cycle
 // of the lane permutation (one temporary), chi row by row (5 temporaries) — about
 // 70 live VGPRs instead of the 120 of a two-array formulation.
@@ -34,12 +50,12 @@ __device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
     for (int round = 0; round < 24; ++round) {
         uint64_t bc[5];
 #pragma unroll
-        for (int x = 0; x < 5; ++x) bc[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
+        for (int x = 0; x < 5; ++x) bc[x] = k_xor3(k_xor3(st[x], st[x + 5], st[x + 10]), st[x + 15], st[x + 20]);
 #pragma unroll
         for (int x = 0; x < 5; ++x) {
-            const uint64_t t = bc[(x + 4) % 5] ^ krotl(bc[(x + 1) % 5], 1);
+            const uint64_t r = krotl(bc[(x + 1) % 5], 1);
 #pragma unroll
-            for (int y = 0; y < 25; y += 5) st[y + x] ^= t;
+            for (int y = 0; y < 25; y += 5) st[y + x] = k_xor3(st[y + x], bc[(x + 4) % 5], r);
         }
         uint64_t t = st[1];
 #pragma unroll
@@ -54,7 +70,7 @@ __device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
 #pragma unroll
             for (int x = 0; x < 5; ++x) bc[x] = st[y + x];
 #pragma unroll
-            for (int x = 0; x < 5; ++x) st[y + x] = bc[x] ^ (~bc[(x + 1) % 5] & bc[(x + 2) % 5]);
+            for (int x = 0; x < 5; ++x) st[y + x] = k_chi(bc[x], bc[(x + 1) % 5], bc[(x + 2) % 5]);
         }
         st[0] ^= kKeccakRC[round];
     }
