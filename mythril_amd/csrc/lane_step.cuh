@@ -58,6 +58,7 @@ struct OpInfo {
 
 #define MSTATE_GAS_LIMIT 1000000000ull
 #define RUN_MAX 64u   // longest straight-line run executed as one block
+static_assert(RUN_MAX <= 64u, "a run is read as one pre-decoded word per wave lane");
 #define STACK_LIMIT 1024u
 #define BIG_END (1ull << 32)
 #define HUGE_GAS (1ull << 62)
@@ -970,10 +971,17 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 const uint32_t rg0 = ry & 0xffffu, rg1 = ry >> 16;
                 const bool in_run = live && pc == upc && sp >= rneed && sp + rpeak <= stack_lim &&
                                     gmin + rg0 < glim && executed + rlen <= lane_max;
+                // the run's pre-decoded words, one per wave lane (rlen <= RUN_MAX = 64),
+                // read by the whole wave in one LDS access; instruction k is then
+                // v_readlane(k) instead of a dependent LDS round trip per instruction
+                // (opaque barrier: the load must run here with the whole wave active,
+                // not be sunk into the `in_run` branch where only some lanes load)
+                uint32_t ybulk = s_pd[min(upc + (threadIdx.x & 63u), pd_cap - 1u)].y;
+                asm volatile("" : "+v"(ybulk));
                 if ((__ballot(in_run) >> lead) & 1ull) {
                     if (in_run) {
                         for (uint32_t k = 0; k < rlen; ++k) {
-                            const uint32_t y = __builtin_amdgcn_readfirstlane(s_pd[upc + k].y);
+                            const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
                             const uint32_t rop = y & 0xffu;
                             switch ((y >> 17) & 31u) {
                             case K_PUSH: {

@@ -23,6 +23,15 @@ PATTERNS = {
     "and": bytes([0x60, 0x07]) + bytes([0x80, 0x16]) * REP,
     "eq_iszero": bytes([0x60, 0x07]) + bytes([0x80, 0x14, 0x15]) * REP,
     "mul": bytes([0x60, 0x07]) + bytes([0x80, 0x02]) * REP,
+    "eq": bytes([0x60, 0x07]) + bytes([0x80, 0x14]) * REP,
+    "lt": bytes([0x60, 0x07]) + bytes([0x80, 0x10]) * REP,
+    "iszero": bytes([0x60, 0x07]) + bytes([0x15]) * REP,
+    "not": bytes([0x60, 0x07]) + bytes([0x19]) * REP,
+    "xor": bytes([0x60, 0x07]) + bytes([0x80, 0x18]) * REP,
+    "and_iszero": bytes([0x60, 0x07]) + bytes([0x80, 0x16, 0x15]) * REP,
+    "eq_not": bytes([0x60, 0x07]) + bytes([0x80, 0x14, 0x19]) * REP,
+    "dup_iszero_pop": bytes([0x60, 0x07]) + bytes([0x80, 0x15, 0x50]) * REP,
+    "and_and": bytes([0x60, 0x07, 0x80]) + bytes([0x80, 0x16, 0x80]) * REP,
     "div": bytes([0x60, 0x07, 0x7F]) + b"\x13" * 32 + bytes([0x81, 0x81, 0x04, 0x50]) * REP,
     "shr": bytes([0x60, 0x07]) + bytes([0x60, 0x03, 0x1C]) * REP,
     "jumpdest": bytes([0x5B]) * REP,
