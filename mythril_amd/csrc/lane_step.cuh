@@ -92,28 +92,29 @@ DEV void st_word(g_u4 *base, size_t idx, const U256 &v) {
     base[2 * idx] = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
     base[2 * idx + 1] = v4u{v.w[4], v.w[5], v.w[6], v.w[7]};
 }
-// LDS stack window: slots [0, win) of a lane live in LDS as [slot][half][thread]
-// 16-byte pieces (conflict-free ds_read_b128), deeper slots in HBM.
+// LDS stack window: slots [0, win) of a lane live in LDS as [slot][half][lane of
+// the block] 16-byte pieces (conflict-free ds_read_b128), deeper slots in HBM.
+// `ws` = lanes per block (the row stride), `tid` = the lane's index in its block.
 #define LANE_BLOCK 256u
 struct LaneView {
     const DevLanes &L;
     uint32_t lane;
     l_u4 *win_base;      // LDS window of this block
-    uint32_t win, tid;
+    uint32_t win, tid, ws;
     DEV size_t row(uint32_t r) const { return (size_t)r * L.N + lane; }
     DEV U256 gstack(uint32_t slot) const { return ld_word(gv(L.stack), row(slot)); }
     DEV void set_gstack(uint32_t slot, const U256 &v) const { st_word(gv(L.stack), row(slot), v); }
     DEV U256 wstack(uint32_t slot) const {
-        const v4u x = win_base[(slot * 2u) * LANE_BLOCK + tid];
-        const v4u y = win_base[(slot * 2u + 1u) * LANE_BLOCK + tid];
+        const v4u x = win_base[(slot * 2u) * ws + tid];
+        const v4u y = win_base[(slot * 2u + 1u) * ws + tid];
         U256 r;
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
         return r;
     }
     DEV void set_wstack(uint32_t slot, const U256 &v) const {
-        win_base[(slot * 2u) * LANE_BLOCK + tid] = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
-        win_base[(slot * 2u + 1u) * LANE_BLOCK + tid] = v4u{v.w[4], v.w[5], v.w[6], v.w[7]};
+        win_base[(slot * 2u) * ws + tid] = v4u{v.w[0], v.w[1], v.w[2], v.w[3]};
+        win_base[(slot * 2u + 1u) * ws + tid] = v4u{v.w[4], v.w[5], v.w[6], v.w[7]};
     }
     DEV U256 stack(uint32_t slot) const {
         U256 r;
@@ -376,7 +377,7 @@ struct StepEnv {
     const uint4 *s_push;
     uint32_t *s_prof;
     uint64_t txlim, glim;
-    uint32_t lane, tid, win, flags, sflag, psflag, prof;
+    uint32_t lane, tid, ws, win, flags, sflag, psflag, prof;
 };
 
 // Executes the instruction decoded as (uk, ux) for one lane, exactly as the
@@ -391,7 +392,7 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
     const DevLanes &L = *E.L;
     const DevCode &C = E.C;
     const uint32_t lane = E.lane;
-    const LaneView V{L, lane, E.s_win, E.win, E.tid};
+    const LaneView V{L, lane, E.s_win, E.win, E.tid, E.ws};
     const uint8_t *__restrict__ a8 = E.a8;
     const uint32_t *__restrict__ a32 = E.a32;
     const uint8_t *__restrict__ gops = a8 + C.op_off;
@@ -794,13 +795,21 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           unsigned long long *__restrict__ prof,
                                                           uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
                                                           uint32_t horizon, uint32_t loop_bound,
-                                                          DevResetImage R) {
-    // Dynamic LDS: [stack window: win x 2 x 256 x 16 B][pre-decoded code: pd_cap x 8 B]
+                                                          DevResetImage R, uint32_t lpw) {
+    // Dynamic LDS: [stack window: win x 2 x lanes-per-block x 16 B][pre-decoded code: pd_cap x 8 B]
     //              [runs: pd_cap x 8 B][push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B]
     //              [coverage: pd_cap]
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
     l_u4 *s_win = (l_u4 *)dyn;
-    uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * LANE_BLOCK);
+    // Lanes per wave (`lpw` = 64, 32 or 16, launch-uniform): each wave holds lpw
+    // lanes in its first lpw threads and the rest idle, so a launch of n lanes has
+    // n / lpw waves.  At C2's 65,536 lanes, lpw = 64 is one wave per SIMD and the
+    // launch is bound by one wave's serial dispatch chain; fewer lanes per wave
+    // put 2 or 4 waves on each SIMD, whose chains then overlap (and each wave's
+    // lanes diverge less).  The idle threads still take part in the wave-wide
+    // LDS load of a run's pre-decoded words below.
+    const uint32_t lanes_pb = (LANE_BLOCK / 64u) * lpw;
+    uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * lanes_pb);
     uint2 *s_run = s_pd + pd_cap;
     uint4 *s_push = reinterpret_cast<uint4 *>(s_run + pd_cap);
     uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + 2u * pd_cap);
@@ -812,8 +821,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // [sha3 bytes, copy bytes, storage entries scanned, keccak blocks]
     __shared__ uint32_t s_prof[260];
 
-    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool in_range = lane < L.n;
+    const uint32_t wlane = threadIdx.x & 63u;
+    const uint32_t tid = (threadIdx.x >> 6) * lpw + wlane;     // lane index in the block
+    const uint32_t lane = blockIdx.x * lanes_pb + tid;
+    const bool in_range = wlane < lpw && lane < L.n;
     // mg_run_batches: re-initialise the lane from the resident image first (the
     // reads below see this thread's own stores)
     if (R.pc != nullptr && in_range) reset_lane(L, R, lane);
@@ -864,7 +875,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const uint32_t stack_lim = L.stack_cap < STACK_LIMIT ? L.stack_cap : STACK_LIMIT;
 
     // ---- per-lane machine state (registers) ----
-    const LaneView V{L, lane, s_win, win, threadIdx.x};
+    const LaneView V{L, lane, s_win, win, tid, lanes_pb};
     DevCode C{};
     uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
     uint32_t tlen = 0;                                    // trace length (BoundedLoops)
@@ -899,7 +910,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     }
     const uint8_t *__restrict__ gops = a8 + C.op_off;
     const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, txlim, glim,
-                    lane, threadIdx.x, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
+                    lane, tid, lanes_pb, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
 
     // Decode the instruction at pc and run the checks svm.execute_state makes
     // before evaluating it (svm.py:369-402): depth cut-off, past-the-end pc,

@@ -38,6 +38,7 @@ struct mg_ctx {
     mg_batch_cfg cfg{};
     bool have_lanes = false, uploaded = false, init_fresh = false;
     uint32_t loop_bound = 0;             // mg_set_loop_bound (0: BoundedLoops off)
+    uint32_t lpw = 64;                   // kernel-1 lanes per wave (MG_LANES_PER_WAVE: 64, 32, 16)
     DevLanes L{};
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
@@ -191,6 +192,12 @@ extern "C" int mg_open(int device, mg_ctx **out) {
         uint2 dec[256];
         build_decode(dec);
         if (hipMemcpyToSymbol(HIP_SYMBOL(kDec), dec, sizeof dec) != hipSuccess) { rc = MG_EDEVICE; break; }
+        const char *lpw = getenv("MG_LANES_PER_WAVE");
+        if (lpw && lpw[0]) {
+            const long v = strtol(lpw, nullptr, 10);
+            if (v != 64 && v != 32 && v != 16) { rc = MG_EINVAL; break; }
+            ctx->lpw = (uint32_t)v;
+        }
     } while (0);
     if (rc != MG_OK) { mg_close(ctx); return rc; }
     *out = ctx;
@@ -433,7 +440,7 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     if (L.trace_cap && (rc = lane_alloc(ctx, L.trace, (size_t)L.trace_cap * N))) return rc;
     HIPX(ctx, hipMemsetAsync(L.trace_len, 0, N * 4, ctx->stream));
     // per-block launch statistics (summed on the host)
-    ctx->ctr_cap = (uint32_t)(N / LANE_BLOCK + 1);
+    ctx->ctr_cap = (uint32_t)(N / (LANE_BLOCK / 4u) + 1);   // lpw >= 16
     if ((rc = lane_alloc(ctx, ctx->d_ctr, (size_t)ctx->ctr_cap))) return rc;
     L.rec_cap = cfg->rec_cap;
     if ((rc = lane_alloc(ctx, L.rec_len, N))) return rc;
@@ -724,16 +731,21 @@ extern "C" int mg_lanes_reset(mg_ctx *ctx) {
 // LDS plan of one launch: the largest loaded code is pre-decoded into LDS (up to
 // 1023 instructions, 41 B each, plus the END sentinel) with its jump-resolve
 // table (2 B per byte address, up to 8192), and the rest of the 160 KiB CU
-// budget, minus a margin for the static arrays, holds the stack window (8 KiB
-// per slot for a 256-lane block), at most 16 slots.
+// budget share of one block (64 / lpw blocks per CU), minus a margin for the
+// static arrays, holds the stack window (2 x 16 B per lane of the block per
+// slot: 8 KiB at 256 lanes), at most 16 slots.
+// lanes per kernel-1 workgroup: 4 waves of ctx->lpw lanes
+static inline uint32_t lane_block(const mg_ctx *ctx) { return (LANE_BLOCK / 64u) * ctx->lpw; }
+
 static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_t &jr_cap, size_t &bytes) {
     uint32_t maxn = 0, maxj = 0;
     for (const DevCode &c : ctx->codes) { maxn = std::max(maxn, c.n_instr); maxj = std::max(maxj, c.n_jres); }
     pd_cap = (std::min<uint32_t>(maxn, 1023u) + 1u + 15u) & ~15u;   // + END sentinel
     jr_cap = (std::min<uint32_t>(maxj, 8192u) + 15u) & ~15u;
     const size_t code_bytes = (size_t)pd_cap * (8 + 8 + 32 + 1) + (size_t)jr_cap * 2;
-    const size_t budget = 160u * 1024u - 4096u;
-    const size_t slot_bytes = 2u * LANE_BLOCK * 16u;
+    // 64 / lpw blocks share a CU (one wave per SIMD each), so each gets that share
+    const size_t budget = 160u * 1024u / (64u / ctx->lpw) - 4096u;
+    const size_t slot_bytes = 2u * lane_block(ctx) * 16u;
     win = (uint32_t)std::min<size_t>(16, budget > code_bytes ? (budget - code_bytes) / slot_bytes : 0);
     win = std::min<uint32_t>(win, ctx->L.stack_cap);
     bytes = (size_t)win * slot_bytes + code_bytes + 16;
@@ -762,14 +774,14 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
         attr_set = true;
     }
     const uint32_t loop_bound = ctx->L.trace_cap ? ctx->loop_bound : 0u;
-    if (ctr && blocks_for(ctx->L.n, LANE_BLOCK) > ctx->ctr_cap)
+    if (ctr && blocks_for(ctx->L.n, lane_block(ctx)) > ctx->ctr_cap)
         return set_err(ctx, MG_EINVAL, "launch of %u blocks exceeds the %u statistics slots",
-                       blocks_for(ctx->L.n, LANE_BLOCK), ctx->ctr_cap);
-    hipLaunchKernelGGL(loop_bound ? k_lane_step<true> : k_lane_step<false>, dim3(blocks_for(ctx->L.n, LANE_BLOCK)),
+                       blocks_for(ctx->L.n, lane_block(ctx)), ctx->ctr_cap);
+    hipLaunchKernelGGL(loop_bound ? k_lane_step<true> : k_lane_step<false>, dim3(blocks_for(ctx->L.n, lane_block(ctx))),
                        dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
                        m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
-                       loop_bound, reset ? *reset : DevResetImage{});
+                       loop_bound, reset ? *reset : DevResetImage{}, ctx->lpw);
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
@@ -788,7 +800,7 @@ extern "C" int mg_step_until(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t 
     int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr, nullptr, horizon);
     if (rc) return rc;
     HIPX(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    const uint32_t nb = blocks_for(ctx->L.n, LANE_BLOCK);
+    const uint32_t nb = blocks_for(ctx->L.n, lane_block(ctx));
     ctx->h_ctr.resize(nb);
     HIPX(ctx, hipMemcpyAsync(ctx->h_ctr.data(), ctx->d_ctr, nb * sizeof(DevCounters), hipMemcpyDeviceToHost,
                              ctx->stream));
@@ -826,7 +838,7 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
     if (!ctx->init_fresh)
         return set_err(ctx, MG_ESTATE, "mg_run_batches needs an uploaded image with empty stacks and memory");
     HIPX(ctx, hipSetDevice(ctx->device));
-    const uint32_t nb = blocks_for(ctx->L.n, LANE_BLOCK);
+    const uint32_t nb = blocks_for(ctx->L.n, lane_block(ctx));
     const size_t slots = (size_t)nb * n_batches;
     if (slots > ctx->ctr_multi_cap) {
         HIPX(ctx, hipStreamSynchronize(ctx->stream));
