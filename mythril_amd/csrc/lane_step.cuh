@@ -784,6 +784,16 @@ __device__ __forceinline__ void reset_lane(const DevLanes &L, const DevResetImag
         }
 }
 
+#ifdef MG_K1_CLOCKS
+// Diagnostic build only (scripts/k1_clocks.py): shader-clock cycles per wave,
+// binned by the opcode each dispatch-loop iteration executed (bin 256: a
+// straight-line run, 257: prologue, 258: epilogue, 259: iterations that
+// advanced no lane of this wave).  Lane 0 of each wave keeps its bins in LDS
+// and writes them out with plain vector stores at the end.
+#define CLK_BINS 260u
+__device__ uint32_t g_k1_clk[4096u * CLK_BINS];
+#endif
+
 template <bool kLoop>
 __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevCode *__restrict__ codes,
                                                           const uint8_t *__restrict__ a8,
@@ -837,6 +847,19 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     __syncthreads();
     if (status == ST_RUNNING) s_code = my_code;      // any running lane's code (benign race)
     __syncthreads();
+#ifdef MG_K1_CLOCKS
+    __shared__ uint32_t s_clk[LANE_BLOCK / 64u][CLK_BINS];
+    for (uint32_t i = threadIdx.x; i < (LANE_BLOCK / 64u) * CLK_BINS; i += blockDim.x) (&s_clk[0][0])[i] = 0u;
+    __syncthreads();
+    const uint64_t clk_start = __builtin_amdgcn_s_memtime();
+    uint64_t clk_t = clk_start;
+    uint32_t clk_bin = 257u;
+#define CLK_MARK(next_) do { const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
+        if ((threadIdx.x & 63u) == 0u) s_clk[threadIdx.x >> 6][clk_bin] += (uint32_t)(t_ - clk_t); \
+        clk_t = t_; clk_bin = (next_); } while (0)
+#else
+#define CLK_MARK(next_) do { } while (0)
+#endif
     const uint32_t bcode = s_code;
     const bool mixed = __syncthreads_or(status == ST_RUNNING && my_code != bcode);
     bool staged = false, jstaged = false;
@@ -967,6 +990,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const bool runs_on = sflag && !prof && !loop_on && ((m0 | m1 | m2 | m3) == 0ull);
 
     for (;;) {
+        CLK_MARK(259u);
         const uint64_t live_mask = __ballot(live);
         if (live_mask == 0ull) break;
         const int lead = __builtin_ctzll(live_mask);
@@ -990,6 +1014,9 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 uint32_t ybulk = s_pd[min(upc + (threadIdx.x & 63u), pd_cap - 1u)].y;
                 asm volatile("" : "+v"(ybulk));
                 if ((__ballot(in_run) >> lead) & 1ull) {
+#ifdef MG_K1_CLOCKS
+                    clk_bin = 256u;
+#endif
                     if (in_run) {
                         for (uint32_t k = 0; k < rlen; ++k) {
                             const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
@@ -1056,6 +1083,9 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (!(live && pd.y == uy)) continue;
 
         const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
+#ifdef MG_K1_CLOCKS
+        clk_bin = op;
+#endif
         if (cov_on) {
             if (sflag) s_cov[pc] = 1;
             else cov[C.cov_off + pc] = 1;
@@ -1227,6 +1257,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (live) FETCH();
     }
 #undef FETCH
+    CLK_MARK(258u);
 
     if (run0) {
         // flush the registers, then the LDS window: HBM holds the canonical S[0 .. sp)
@@ -1244,6 +1275,15 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (n_exp) L.exp_count[lane] += n_exp;
     }
 
+#ifdef MG_K1_CLOCKS
+    CLK_MARK(258u);
+    if ((threadIdx.x & 63u) == 0u) {
+        const uint32_t gw = blockIdx.x * (LANE_BLOCK / 64u) + (threadIdx.x >> 6);
+        if (gw < 4096u)
+            for (uint32_t i = 0; i < CLK_BINS; ++i) g_k1_clk[gw * CLK_BINS + i] = s_clk[threadIdx.x >> 6][i];
+    }
+#endif
+#undef CLK_MARK
     if (staged && cov_on) {
         __syncthreads();
         const DevCode BC = codes[bcode];

@@ -786,6 +786,16 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     return MG_OK;
 }
 
+#ifdef MG_K1_CLOCKS
+// diagnostic build only: the per-wave cycle bins of the last kernel-1 launch
+extern "C" int mg_k1_clocks(mg_ctx *ctx, uint32_t *out, size_t n) {
+    if (!ctx || !out) return MG_EINVAL;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    HIPX(ctx, hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k1_clk), std::min<size_t>(n, 4096u * CLK_BINS) * 4u));
+    return MG_OK;
+}
+#endif
+
 extern "C" int mg_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
                        mg_step_stats *stats) {
     return mg_step_until(ctx, hook_mask, max_steps, max_depth, 0u, stats);
