@@ -789,7 +789,8 @@ __device__ __forceinline__ void reset_lane(const DevLanes &L, const DevResetImag
 // binned by the opcode each dispatch-loop iteration executed (bin 256: a
 // straight-line run, 257: prologue, 258: epilogue, 259: iterations that
 // advanced no lane of this wave).  Lane 0 of each wave keeps its bins in LDS
-// and writes them out with plain vector stores at the end.
+// and writes them out with plain vector stores at the end.  Each bin packs
+// cycles in bits 0-23 and the number of iterations in bits 24-31.
 #define CLK_BINS 260u
 __device__ uint32_t g_k1_clk[4096u * CLK_BINS];
 #endif
@@ -855,7 +856,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     uint64_t clk_t = clk_start;
     uint32_t clk_bin = 257u;
 #define CLK_MARK(next_) do { const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
-        if ((threadIdx.x & 63u) == 0u) s_clk[threadIdx.x >> 6][clk_bin] += (uint32_t)(t_ - clk_t); \
+        if ((threadIdx.x & 63u) == 0u) s_clk[threadIdx.x >> 6][clk_bin] += (uint32_t)(t_ - clk_t) + (1u << 24); \
         clk_t = t_; clk_bin = (next_); } while (0)
 #else
 #define CLK_MARK(next_) do { } while (0)

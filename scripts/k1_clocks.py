@@ -4,7 +4,8 @@
 built with -DMG_K1_CLOCKS (ab/clk.so, MYTHGPU_LIB) and prints the shader-clock
 cycles per opcode bin for the slowest waves and for the mean wave.
 Bins: opcode byte = dispatch iterations that executed it (fast path or general
-handler), 256 = straight-line runs, 257 = prologue, 258 = epilogue,
+handler), 256 = straight-line runs (bins pack cycles in bits 0-23 and
+iterations in bits 24-31), 257 = prologue, 258 = epilogue,
 259 = loop overhead of iterations in which this wave advanced nothing."""
 import ctypes
 import os
@@ -61,7 +62,9 @@ def main(n=65536):
     buf = (ctypes.c_uint32 * (4096 * BINS))()
     assert lib.mg_k1_clocks(dev.ctx, buf, 4096 * BINS) == 0
     waves = (n + 63) // 64
-    clk = np.frombuffer(buf, dtype=np.uint32).reshape(4096, BINS)[:waves].astype(np.float64)
+    raw = np.frombuffer(buf, dtype=np.uint32).reshape(4096, BINS)[:waves]
+    clk = (raw & 0xFFFFFF).astype(np.float64)          # cycles (bits 0-23)
+    cnt = (raw >> 24).astype(np.float64)               # iterations (bits 24-31)
     tot = clk.sum(axis=1)
     print(f"launch {st.kernel_ms if hasattr(st, 'kernel_ms') else st}: waves {waves}, cycles/wave "
           f"mean {tot.mean():.0f} p50 {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max():.0f}")
@@ -70,6 +73,11 @@ def main(n=65536):
     show("16 slowest waves (mean)", clk[slow].mean(axis=0))
     for w in slow[:4]:
         show(f"wave {w}", clk[w], top=12)
+    for title, rows in (("mean wave", slice(None)), ("16 slowest waves", slow)):
+        c, k = clk[rows].mean(axis=0), cnt[rows].mean(axis=0)
+        order = [b for b in np.argsort(-c)[:14] if k[b] > 0]
+        print(f"{title}: iterations per wave {k.sum():.1f}; per bin iterations x cycles/iteration")
+        print("   " + "  ".join(f"{name(int(b))}:{k[b]:.1f}x{c[b] / k[b]:.0f}" for b in order))
 
 
 if __name__ == "__main__":
