@@ -367,6 +367,11 @@ struct LaneRegs {
     uint32_t step;               // instructions this launch executed before this one
 };
 // What the handlers read besides the registers (per lane / per block).
+// Per-wave Keccak result cache in LDS (SHA3 of 64 aligned bytes: a mapping
+// slot keccak(key . slot), the common case).  Entry e = 16 input dwords + 8 hash
+// limbs; word KC_E * 24 holds the valid mask, the next one the replacement index.
+#define KC_E 4u
+#define KC_WAVE (KC_E * 24u + 2u)
 struct StepEnv {
     const DevLanes *L;
     DevCode C;
@@ -376,6 +381,7 @@ struct StepEnv {
     const uint2 *s_pd;
     const uint4 *s_push;
     uint32_t *s_prof;
+    uint32_t *s_kc;      // this wave's Keccak cache (KC_WAVE words)
     uint64_t txlim, glim;
     uint32_t lane, tid, ws, win, flags, sflag, psflag, prof;
 };
@@ -505,8 +511,55 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
                 res.w[7] = 0xc5d24601u; res.w[6] = 0x86f7233cu; res.w[5] = 0x927e7db2u; res.w[4] = 0xdcc703c0u;
                 res.w[3] = 0xe500b653u; res.w[2] = 0xca82273bu; res.w[1] = 0x7bfad804u; res.w[0] = 0x5d85a470u;
             } else {
-                res = keccak_mem(V, a.w[0], b.w[0],
-                                 L.rec_cap ? L.rec + lane + (size_t)(rec_at + MG_REC_HEADER) * L.N : nullptr, L.N);
+                // Keccak cache: when every lane running this SHA3 finds its 64-byte
+                // aligned input among its wave's cached entries (e.g. balances[caller]
+                // hashed again), the hashes come from LDS and Keccak-f is skipped; else
+                // all lanes hash and the lowest uncached lane's result is inserted.
+                // Exact 16-dword compare: results are unchanged either way.
+                uint32_t *kc = E.s_kc;
+                const bool cacheable = b.w[0] == 64u && (a.w[0] & 3u) == 0u;
+                uint32_t din[16];
+                bool hit = false;
+                if (cacheable) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) din[k] = V.mdw_safe((a.w[0] >> 2) + (uint32_t)k);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const uint32_t valid = kc[KC_E * 24u];
+                    for (uint32_t e = 0; e < KC_E; ++e) {
+                        if (!((valid >> e) & 1u)) continue;
+                        bool eq = true;
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) eq = eq && kc[e * 24u + k] == din[k];
+                        if (eq && !hit) {
+                            hit = true;
+#pragma unroll
+                            for (int k = 0; k < 8; ++k) res.w[k] = kc[e * 24u + 16u + k];
+                        }
+                    }
+                }
+                const uint64_t act = __ballot(true);
+                if (__ballot(hit) == act) {
+                    if (L.rec_cap) {
+                        uint32_t *rp = L.rec + lane + (size_t)(rec_at + MG_REC_HEADER) * L.N;
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) rp[(size_t)k * L.N] = din[k];
+                    }
+                } else {
+                    res = keccak_mem(V, a.w[0], b.w[0],
+                                     L.rec_cap ? L.rec + lane + (size_t)(rec_at + MG_REC_HEADER) * L.N : nullptr,
+                                     L.N);
+                    const uint64_t ins = __ballot(cacheable && !hit);
+                    if (ins != 0ull && (uint32_t)__builtin_ctzll(ins) == (threadIdx.x & 63u)) {
+                        const uint32_t e = kc[KC_E * 24u + 1u] % KC_E;
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) kc[e * 24u + k] = din[k];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) kc[e * 24u + 16u + k] = res.w[k];
+                        kc[KC_E * 24u] = kc[KC_E * 24u] | (1u << e);
+                        kc[KC_E * 24u + 1u] = e + 1u;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
                 if (L.rec_cap) {
                     rec_head(L, lane, rec_at, MG_REC_KECCAK, b.w[0], L.steps[lane] + R.step, res);
                     rec_new = rec_at + MG_REC_HEADER + ((b.w[0] + 3u) >> 2);
@@ -831,6 +884,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // instruction_profiler.py:41-115, as native counters): 256 opcode counts +
     // [sha3 bytes, copy bytes, storage entries scanned, keccak blocks]
     __shared__ uint32_t s_prof[260];
+    __shared__ uint32_t s_kc[(LANE_BLOCK / 64u) * KC_WAVE];
 
     const uint32_t wlane = threadIdx.x & 63u;
     const uint32_t tid = (threadIdx.x >> 6) * lpw + wlane;     // lane index in the block
@@ -845,6 +899,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     if (prof)
         for (uint32_t i = threadIdx.x; i < 260u; i += blockDim.x) s_prof[i] = 0u;
     if (threadIdx.x == 0) s_code = 0xffffffffu;
+    if ((threadIdx.x & 63u) < 2u) s_kc[(threadIdx.x >> 6) * KC_WAVE + KC_E * 24u + (threadIdx.x & 63u)] = 0u;
     __syncthreads();
     if (status == ST_RUNNING) s_code = my_code;      // any running lane's code (benign race)
     __syncthreads();
@@ -933,7 +988,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         lane_max = min(lane_max, horizon > s0 ? horizon - s0 : 0u);
     }
     const uint8_t *__restrict__ gops = a8 + C.op_off;
-    const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, txlim, glim,
+    const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, s_kc + (threadIdx.x >> 6) * KC_WAVE, txlim, glim,
                     lane, tid, lanes_pb, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
 
     // Decode the instruction at pc and run the checks svm.execute_state makes

@@ -744,7 +744,7 @@ static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_
     jr_cap = (std::min<uint32_t>(maxj, 8192u) + 15u) & ~15u;
     const size_t code_bytes = (size_t)pd_cap * (8 + 8 + 32 + 1) + (size_t)jr_cap * 2;
     // 64 / lpw blocks share a CU (one wave per SIMD each), so each gets that share
-    const size_t budget = 160u * 1024u / (64u / ctx->lpw) - 4096u;
+    const size_t budget = 160u * 1024u / (64u / ctx->lpw) - 6144u;
     const size_t slot_bytes = 2u * lane_block(ctx) * 16u;
     win = (uint32_t)std::min<size_t>(16, budget > code_bytes ? (budget - code_bytes) / slot_bytes : 0);
     win = std::min<uint32_t>(win, ctx->L.stack_cap);
@@ -767,9 +767,9 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)k_lane_step<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024 - 4096);
+                                  160 * 1024 - 6144);
         (void)hipFuncSetAttribute((const void *)k_lane_step<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024 - 4096);
+                                  160 * 1024 - 6144);
         (void)hipGetLastError();   // the attribute is advisory on gfx950; never leave a sticky error
         attr_set = true;
     }
