@@ -11,6 +11,11 @@ own 65,536 lanes (seed + rank); the only collective is the coverage all-gather
 after the timed region's batches (§8(e)), over RCCL.
 
 Prints ONE JSON line (rank 0).
+
+Multi-GPU: `python bench.py --gpus N` with no WORLD_SIZE in the environment
+starts N rank processes itself (one per GPU, RANK/LOCAL_RANK/WORLD_SIZE set,
+rendezvous on 127.0.0.1) before anything touches a GPU, and exits with their
+status; under torch.distributed.run (WORLD_SIZE set) it is one of the ranks.
 """
 from __future__ import annotations
 
@@ -27,7 +32,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -43,27 +48,71 @@ def parse():
                     help="function-manager record words per lane (0: registrations off)")
     ap.add_argument("--profile-only", action="store_true",
                     help="run warmup+steps with no JSON extras (for rocprofv3)")
-    return ap.parse_args()
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, script: str = None) -> int:
+    """Start one rank process per GPU (RANK = LOCAL_RANK = k, WORLD_SIZE = n,
+    MASTER_ADDR 127.0.0.1) and wait for all; returns the worst exit status.
+    The parent never initialises a GPU: it only spawns and waits."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for k in range(n):
+        env = dict(os.environ, RANK=str(k), LOCAL_RANK=str(k), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, script or str(Path(__file__).resolve())] + list(argv),
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def main(argv=None, device_factory=None, backend: str = "nccl"):
+    """One rank of the benchmark.  device_factory(local_rank) -> device (default
+    GpuDevice); backend: the torch.distributed backend for world > 1 (nccl =
+    RCCL over xGMI on the GPU box)."""
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}",
+              file=sys.stderr)
     import torch
     import torch.distributed as dist
 
     dist_on = world > 1
+    gpu = device_factory is None
     if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gpu:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from mythril_amd import workloads
-    from mythril_amd.device import GpuDevice
     from mythril_amd import roofline
 
-    dev = GpuDevice(local)
+    if gpu:
+        from mythril_amd.device import GpuDevice
+        dev = GpuDevice(local)
+    else:
+        dev = device_factory(local)
     code = workloads.bytecode("overflow.sol.o")
     cid = dev.load_code(code)
     batch = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + rank,
@@ -82,7 +131,8 @@ def main():
     def barrier():
         if dist_on:
             dist.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
 
     # the K batches are enqueued back to back (reset + stepping launch each,
     # mg_run_batches) with one host wait: no host round trip between batches
@@ -110,7 +160,7 @@ def main():
         value = total_steps / elapsed
         steps_per_batch = lane_steps / max(args.steps, 1)
         kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
-        roof = roofline.lane_step_roofline(dev, batch, cid, kernel_ms=kms)
+        roof = None if args.no_roofline else roofline.lane_step_roofline(dev, batch, cid, kernel_ms=kms)
         out = {
             "metric": "EVM lane-steps/s (kernel 1, C2: 65,536 concrete lanes/GPU, token.sol runtime)",
             "value": value,

@@ -77,6 +77,66 @@ def exchange_coverage(laser_evm) -> Dict[str, np.ndarray]:
     return union
 
 
+def _encode_model(model) -> list:
+    """A Model as plain data (every internal ModelRef's assignment)."""
+    from ..smt.program import ArrayInterp, FuncInterp
+    out = []
+    for ref in getattr(model, "raw", [model]):
+        asg = {}
+        for name, v in ref.assignment.items():
+            if isinstance(v, ArrayInterp):
+                asg[name] = ("A", v.default, dict(v.entries))
+            elif isinstance(v, FuncInterp):
+                asg[name] = ("F", v.else_value, dict(v.entries))
+            else:
+                asg[name] = int(v)
+        out.append(asg)
+    return out
+
+
+def _decode_model(refs: list):
+    from ..smt.program import ArrayInterp, FuncInterp
+    from ..smt.solver import Model, ModelRef
+    models = []
+    for asg in refs:
+        d = {}
+        for name, v in asg.items():
+            if isinstance(v, tuple) and v[0] == "A":
+                d[name] = ArrayInterp(v[1], v[2])
+            elif isinstance(v, tuple) and v[0] == "F":
+                d[name] = FuncInterp(v[1], v[2])
+            else:
+                d[name] = v
+        models.append(ModelRef(d))
+    return Model(models)
+
+
+def exchange_models(model_cache=None) -> int:
+    """the satisfying models every rank found since the last
+    exchange (z3 fallback answers cached by get_model, support/model.py:76-78)
+    join every other rank's candidate pool — kernel 2's ModelCache — in rank
+    order, each with count 1 as a fresh backend model gets.  One all-gather per
+    transaction round; returns the number of peer models received."""
+    from .. import dist as mdist
+    from ..smt import solver
+    cache = model_cache or solver.model_cache
+    rank, world = mdist.rank_world()
+    mine = [_encode_model(m) for m in cache.take_fresh()]
+    if world == 1:
+        return 0
+    import torch.distributed as dist
+    parts: List[Optional[list]] = [None] * world
+    dist.all_gather_object(parts, mine)
+    got = 0
+    for r, models in enumerate(parts):
+        if r == rank:
+            continue
+        for enc in models or []:
+            cache.put(_decode_model(enc), 1, peer=True)
+            got += 1
+    return got
+
+
 def execute_message_calls(laser_evm, callee_address, caller_address, origin_address,
                           datas: Sequence[bytes], gas_limit, gas_price, value, code=None,
                           track_gas: bool = False, exchange_cov: bool = True):
@@ -120,6 +180,8 @@ def execute_message_calls(laser_evm, callee_address, caller_address, origin_addr
     final = laser_evm.exec(track_gas=track_gas)
     if exchange_cov and world > 1 and laser_evm.record_coverage:
         exchange_coverage(laser_evm)
+    if world > 1:
+        exchange_models()
     return final
 
 

@@ -103,11 +103,18 @@ def _rlp_item(b: bytes) -> bytes:
     return bytes([0x80 + len(b)]) + b
 
 
+def _int_bytes(x: int) -> bytes:
+    """rlp's big_endian_int sedes: minimal big-endian bytes, 0 -> b''."""
+    return x.to_bytes((x.bit_length() + 7) // 8, "big") if x else b""
+
+
 def generate_contract_address(creator: int, nonce: int) -> int:
     """py-evm ``eth._utils.address.generate_contract_address`` (used at
-    world_state.py:237): keccak256(rlp([sender, nonce]))[12:]."""
-    sender = _rlp_item(creator.to_bytes(20, "big"))
-    n = _rlp_item(nonce.to_bytes((nonce.bit_length() + 7) // 8, "big") if nonce else b"")
+    world_state.py:237): keccak256(rlp([sender, nonce]))[12:].  The reference
+    passes the creator as an int (its account key), which rlp encodes like the
+    nonce: minimal big-endian bytes, so leading zero bytes of the address drop."""
+    sender = _rlp_item(_int_bytes(creator))
+    n = _rlp_item(_int_bytes(nonce))
     payload = sender + n
     return int.from_bytes(keccak256(bytes([0xC0 + len(payload)]) + payload)[12:], "big")
 

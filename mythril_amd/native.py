@@ -31,24 +31,44 @@ def sources():
         INCLUDE / "mythgpu.h"]
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile libmythgpu.so for gfx950 in-tree (hipcc; one translation unit)."""
-    newest = max(p.stat().st_mtime for p in sources())
-    if not force and LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest:
-        return LIB_PATH
+HASH_PATH = LIB_PATH.with_name(LIB_PATH.name + ".sha256")
+
+
+def _command(out: str):
     # -structurizecfg-skip-uniform-regions: the interpreters' opcode switches
     # branch on wave-uniform values (readfirstlane); left unstructured they are
     # plain scalar branches instead of an exec-masked flag chain through every
     # case.  A/B on MI355X (scripts/gpu_ab_skip.sh): kernel 2 C4 8.0 -> 11.9 G
     # constraint-evals/s (VGPRs 101 -> 69), kernel 1 C2 36.6 -> 38.4 G lane-steps/s.
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-mllvm", "-structurizecfg-skip-uniform-regions=true",
-           "-Wno-unused-value", "-Wno-unused-result", str(CSRC / "mythgpu.hip"),
-           "-o", str(LIB_PATH) + ".tmp"]
+    return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
+            "-mllvm", "-structurizecfg-skip-uniform-regions=true",
+            "-Wno-unused-value", "-Wno-unused-result", str(CSRC / "mythgpu.hip"), "-o", out]
+
+
+def source_hash() -> str:
+    """sha256 over the sources and the compile command: the identity of a build."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sources():
+        h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
+    h.update(" ".join(_command("OUT")[1:]).encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile libmythgpu.so for gfx950 in-tree (hipcc; one translation unit).
+    Rebuilds whenever the recorded source hash differs (a library copied from
+    elsewhere, or built from older sources, is never trusted by mtime)."""
+    want = source_hash()
+    if not force and LIB_PATH.exists() and HASH_PATH.exists() and \
+            HASH_PATH.read_text().strip() == want:
+        return LIB_PATH
+    cmd = _command(str(LIB_PATH) + ".tmp")
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(str(LIB_PATH) + ".tmp", LIB_PATH)
+    HASH_PATH.write_text(want + "\n")
     return LIB_PATH
 
 
@@ -127,6 +147,12 @@ def load() -> ctypes.CDLL:
         raise MythGpuError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback in mythril_amd)")
+    if "MYTHGPU_LIB" not in os.environ:
+        got = HASH_PATH.read_text().strip() if HASH_PATH.exists() else "missing"
+        if got != source_hash():
+            raise MythGpuError(
+                f"{path} was not built from the current sources (recorded hash {got[:12]}): "
+                "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

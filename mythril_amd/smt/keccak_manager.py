@@ -27,12 +27,14 @@ class KeccakFunctionManager:
     hash_matcher = "fffffff"
 
     def __init__(self):
+        # set once: reset() keeps the counter (keccak_function_manager.py:38-54), so
+        # sizes first seen after a reset get fresh, lower intervals
+        self._index_counter = TOTAL_PARTS - 34534
         self.reset()
 
     def reset(self):
         self.store_function: Dict[int, Tuple[Function, Function]] = {}
         self.interval_hook_for_size: Dict[int, int] = {}
-        self._index_counter = TOTAL_PARTS - 34534
         self.hash_result_store: Dict[int, List[BitVec]] = {}
         self.quick_inverse: Dict[BitVec, BitVec] = {}
         self.concrete_hashes: Dict[BitVec, BitVec] = {}

@@ -22,8 +22,9 @@ cannot evaluate (flatten.Unsupported) and a set no cached model satisfies both
 fall through to the backend unchanged.  The backend is z3 in the reference; z3
 is not installed in this image nor on the GPU box, so ``solver_backend`` is a
 pluggable callable (constraints, minimize, maximize, timeout_ms) -> model that
-raises UnsatError / SolverTimeOutException; the default raises
-SolverTimeOutException.
+raises UnsatError / SolverTimeOutException.  Without one installed, a
+quick-sat miss raises SolverBackendMissing: it is never mapped to "unsat" or
+"timeout", so no feasible path is ever pruned silently.
 """
 from __future__ import annotations
 
@@ -48,6 +49,12 @@ class UnsatError(Exception):
 
 class SolverTimeOutException(Exception):
     """mythril/exceptions.py: the solver gave up."""
+
+
+class SolverBackendMissing(RuntimeError):
+    """Kernel 2 found no cached model and no SMT backend is installed, so the
+    query cannot be decided.  Deliberately not a SolverTimeOutException /
+    UnsatError: is_possible() would turn either into a silent prune."""
 
 
 def simplify(expr):
@@ -229,6 +236,7 @@ class ModelCache:
         self.model_cache = LRUCache(size=100)
         self._device = device
         self._memo: "OrderedDict[Node, object]" = OrderedDict()
+        self._fresh: List = []          # models this rank found since the last exchange
         self.device_evals = 0          # constraint-evals run on kernel 2
         self.launches = 0
 
@@ -239,8 +247,19 @@ class ModelCache:
             self._device = GpuDevice(int(os.environ.get("LOCAL_RANK", "0")))
         return self._device
 
-    def put(self, key, value):
+    def put(self, key, value, peer: bool = False):
+        """Cache a model (support_utils.py:34-53 put).  peer=True: a model another
+        rank found (§8(e) all-gather), not re-shared at the next exchange."""
         self.model_cache.put(key, value)
+        if not peer:
+            self._fresh.append(key)
+            if len(self._fresh) > self.model_cache.size:     # older ones are evicted anyway
+                del self._fresh[0]
+
+    def take_fresh(self) -> List:
+        """Models this rank cached since the last call (for the all-gather)."""
+        out, self._fresh = self._fresh, []
+        return out
 
     # -- memo = functools.lru_cache(maxsize=2**10) on check_quick_sat ---------
     def _memo_get(self, key):
@@ -365,7 +384,9 @@ time_handler = TimeHandler()
 
 
 def _no_backend(constraints, minimize, maximize, timeout):
-    raise SolverTimeOutException("no SMT backend installed (z3 is absent in this image)")
+    raise SolverBackendMissing(
+        "quick-sat found no satisfying model and no SMT backend is installed (z3 is absent "
+        "in this image): install one with mythril_amd.smt.solver.set_solver_backend()")
 
 
 solver_backend: Callable = _no_backend
@@ -396,7 +417,7 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         if ret_model:
             return ret_model
     model = solver_backend(constraints, minimize, maximize, timeout)
-    model_cache.model_cache.put(model, 1)
+    model_cache.put(model, 1)
     return model
 
 

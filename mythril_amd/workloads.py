@@ -42,18 +42,34 @@ def _int_limbs(x: int) -> np.ndarray:
     return np.array([(x >> (32 * k)) & 0xFFFFFFFF for k in range(8)], dtype=np.uint32)
 
 
+def dispatch_selectors(code: bytes):
+    """The 4-byte function selectors of a solc dispatcher: every PUSH4 argument
+    compared by an EQ within the next two instructions."""
+    from .laser.disassembly import disassemble
+    ins = disassemble(code)
+    out = []
+    for k, i in enumerate(ins):
+        if i["opcode"] == "PUSH4" and any(j["opcode"] == "EQ" for j in ins[k + 1:k + 3]):
+            v = int(i["argument"], 16)
+            if v not in out and v != 0xFFFFFFFF:
+                out.append(v)
+    return tuple(out)
+
+
 def c2_batch(n: int = 65536, code_id: int = 0, seed: int = C2_SEED, stack_cap: int = 1024,
              mem_cap: int = 1024, storage_cap: int = 16, gas_limit: int = 8_000_000,
-             rec_cap: int = 0) -> LaneBatch:
+             rec_cap: int = 0, selectors=C2_SELECTORS) -> LaneBatch:
+    """SURVEY §8(d) C2 lanes.  `selectors` = the function selectors drawn with
+    probability 7/8 (C2: token.sol's three; other codes: dispatch_selectors)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     shape = LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap, calldata_cap=96,
                       storage_cap=storage_cap, rec_cap=rec_cap)
     b = LaneBatch(shape)
     # --- calldata: selector | arg0 | arg1, length 68 w.p. 15/16 else U{0..67}
     sel_known = rng.random(n) < 7 / 8
-    sel_pick = rng.integers(0, 3, n)
+    sel_pick = rng.integers(0, len(selectors), n)
     sel_rand = rng.integers(0, 1 << 32, n, dtype=np.uint64)
-    sel = np.where(sel_known, np.array(C2_SELECTORS, dtype=np.uint64)[sel_pick], sel_rand)
+    sel = np.where(sel_known, np.array(selectors, dtype=np.uint64)[sel_pick], sel_rand)
     cd = np.zeros((n, 96), dtype=np.uint8)
     for k in range(4):
         cd[:, k] = (sel >> np.uint64(8 * (3 - k))) & np.uint64(0xFF)

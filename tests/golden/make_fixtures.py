@@ -15,6 +15,10 @@ and expected outputs taken from the reference's test suite — never source text
 * keccak_kat.json   <- mythril/laser/ethereum/function_managers/keccak_function_manager.py:92
 * bytecodes.json    <- tests/testdata/inputs/*.sol.o (precompiled runtime code)
 * integration.json  <- tests/integration_tests/analysis_tests.py:9-54 expectations
+* shift_rows.json   <- tests/instructions/{shl,shr,sar}_test.py `test_data` rows
+* keccak_cases.json <- tests/laser/keccak_tests.py:7-145 (inputs and expected sat/unsat)
+* disassembly.json  <- tests/disassembler_test.py:8-10 (code, 3,523 instructions)
+* model_cases.json  <- tests/laser/smt/model_test.py:5-56
 
 Usage:  python tests/golden/make_fixtures.py [--reference /root/reference]
 """
@@ -156,6 +160,124 @@ def make_bytecodes(ref: Path):
     return out
 
 
+# ---------------------------------------------------------------- symbolic literals
+# The reference's SMT tests build their inputs with symbol_factory calls
+# (BitVecVal(v, w) / BitVecSym(name, w)); these are read as DATA: each call
+# becomes {"kind": "val", "value", "size"} or {"kind": "sym", "name", "size"}.
+_VAL_NAMES = {"BitVecVal", "BVV"}
+_SYM_NAMES = {"BitVecSym", "BV"}
+
+
+def _lit(node):
+    """Literal value of a restricted expression (ints, -, *, <<, //, BVV/BV calls)."""
+    if isinstance(node, ast.Constant):
+        return node.value
+    if isinstance(node, ast.UnaryOp) and isinstance(node.op, ast.USub):
+        return -_lit(node.operand)
+    if isinstance(node, ast.BinOp):
+        a, b = _lit(node.left), _lit(node.right)
+        ops = {ast.Mult: lambda: a * b, ast.LShift: lambda: a << b,
+               ast.FloorDiv: lambda: a // b, ast.Add: lambda: a + b, ast.Sub: lambda: a - b}
+        return ops[type(node.op)]()
+    if isinstance(node, ast.Call):
+        fname = node.func.attr if isinstance(node.func, ast.Attribute) else node.func.id
+        args = [_lit(a) for a in node.args]
+        if fname in _VAL_NAMES:
+            return {"kind": "val", "value": args[0], "size": args[1]}
+        if fname in _SYM_NAMES:
+            return {"kind": "sym", "name": args[0], "size": args[1]}
+        raise ValueError(fname)
+    if isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name) and node.value.id == "z3":
+        return node.attr                                  # z3.sat / z3.unsat
+    if isinstance(node, (ast.List, ast.Tuple)):
+        return [_lit(e) for e in node.elts]
+    raise ValueError(ast.dump(node))
+
+
+def make_keccak_cases(ref: Path):
+    """tests/laser/keccak_tests.py: the parametrized (input1, input2, expected)
+    rows of test_keccak_basic (:7-27) and the expected check() result of every
+    other test function (:41-145), in file order.  The constructions of those
+    functions are restated in tests/test_keccak_pinning.py; the test order
+    matters because KeccakFunctionManager.reset() keeps _index_counter
+    (keccak_function_manager.py:48-54), so interval indices keep decreasing
+    across tests of one process."""
+    tree = ast.parse((ref / "tests/laser/keccak_tests.py").read_text())
+    basic, named, order = [], {}, []
+    for node in tree.body:
+        if not isinstance(node, ast.FunctionDef):
+            continue
+        order.append(node.name)
+        for dec in node.decorator_list:
+            if isinstance(dec, ast.Call) and getattr(dec.func, "attr", "") == "parametrize":
+                for row in dec.args[1].elts:
+                    i1, i2, exp = [_lit(e) for e in row.elts]
+                    basic.append({"input1": i1, "input2": i2, "expected": exp})
+        for sub in ast.walk(node):
+            if isinstance(sub, ast.Assert) and isinstance(sub.test, ast.Compare) \
+                    and isinstance(sub.test.comparators[0], ast.Attribute):
+                named[node.name] = _lit(sub.test.comparators[0])
+    return {"basic": basic, "named": named, "order": order}
+
+
+def make_disassembly(ref: Path):
+    """tests/disassembler_test.py:8-10: a runtime code whose instruction list
+    has 3,523 entries (bzzr metadata trimmed, asm.py:112-123)."""
+    tree = ast.parse((ref / "tests/disassembler_test.py").read_text())
+    code, count = None, None
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Assign) and getattr(node.targets[0], "id", "") == "code" \
+                and isinstance(node.value, ast.Constant):
+            code = node.value.value
+        if isinstance(node, ast.Call) and getattr(node.func, "attr", "") == "assertEqual":
+            count = ast.literal_eval(node.args[1])
+    return {"code": code, "instructions": count}
+
+
+def make_model_cases(ref: Path):
+    """tests/laser/smt/model_test.py:5-56: solver.add(x == BitVecVal(2, 256));
+    the model declares x and evaluates it to 2 (decls / __getitem__ / eval)."""
+    tree = ast.parse((ref / "tests/laser/smt/model_test.py").read_text())
+    out = []
+    for node in tree.body:
+        if not isinstance(node, ast.FunctionDef):
+            continue
+        sym = val = want = None
+        for sub in ast.walk(node):
+            if isinstance(sub, ast.Call) and isinstance(sub.func, ast.Attribute):
+                if sub.func.attr == "BitVecSym":
+                    sym = _lit(sub)
+                elif sub.func.attr == "BitVecVal":
+                    val = _lit(sub)
+            if isinstance(sub, ast.Assert) and isinstance(sub.test, ast.Compare) \
+                    and isinstance(sub.test.left, ast.Constant):
+                want = sub.test.left.value
+        out.append({"test": node.name, "var": sym, "equals": val, "expected_value": want})
+    return out
+
+
+def make_shift_rows(ref: Path):
+    """tests/instructions/{shl,shr,sar}_test.py `test_data`: stack [value, shift]
+    -> expected top of stack, for the rows whose operands are concrete or whose
+    expected result is a literal (the symbolic `a << 270 == 0` row)."""
+    out = {}
+    for op in ("shl", "shr", "sar"):
+        tree = ast.parse((ref / f"tests/instructions/{op}_test.py").read_text())
+        rows = []
+        for node in tree.body:
+            if isinstance(node, ast.Assign) and getattr(node.targets[0], "id", "") == "test_data":
+                for row in node.value.elts:
+                    try:
+                        (value, shift), exp = _lit(row.elts[0]), _lit(row.elts[1])
+                    except (ValueError, KeyError, TypeError):
+                        continue                       # expected is an expression (a << b)
+                    if isinstance(exp, int):
+                        exp = {"kind": "val", "value": exp, "size": 256}
+                    rows.append({"value": value, "shift": shift, "expected": exp})
+        out[op] = rows
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -165,6 +287,10 @@ def main():
         "vmtests.json": make_vmtests(ref),
         "opcodes.json": make_opcodes(ref),
         "shift_vectors.json": make_shift_vectors(ref),
+        "shift_rows.json": make_shift_rows(ref),
+        "keccak_cases.json": make_keccak_cases(ref),
+        "disassembly.json": make_disassembly(ref),
+        "model_cases.json": make_model_cases(ref),
         "loop_count.json": make_loop_counts(ref),
         "bytecodes.json": make_bytecodes(ref),
         "keccak_kat.json": {

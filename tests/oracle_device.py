@@ -49,10 +49,30 @@ class OracleDevice:
 
     def _copy(self, src: LaneBatch, dst: LaneBatch, first: int, n: int):
         for f in _ALL_FIELDS:
-            getattr(dst, f)[first:first + n] = getattr(src, f)[first:first + n]
+            a, b = getattr(dst, f), getattr(src, f)
+            if a.shape[1:] == b.shape[1:]:
+                a[first:first + n] = b[first:first + n]
+            else:                      # slim image (workloads.slim_copy): the overlap, rest zero
+                a[first:first + n] = 0
+                sl = tuple(slice(0, min(x, y)) for x, y in zip(a.shape[1:], b.shape[1:]))
+                a[(slice(first, first + n),) + sl] = b[(slice(first, first + n),) + sl]
 
     def upload(self, batch: LaneBatch, first: int = 0):
         self._copy(batch, self._img, first, batch.n)
+        self._init = LaneBatch(self._img.shape)           # the resident initial image
+        self._copy(self._img, self._init, 0, self._img.n)
+
+    def reset(self):
+        self._copy(self._init, self._img, 0, self._img.n)
+
+    def run_batches(self, n_batches: int, hook_mask=None, max_steps: int = 1 << 30,
+                    max_depth: int = 0):
+        """mg_run_batches: n x (reset from the resident image + one step)."""
+        out = []
+        for _ in range(n_batches):
+            self.reset()
+            out.append(self.step(hook_mask, max_steps, max_depth))
+        return out
 
     def download(self, batch: LaneBatch, first: int = 0):
         self._copy(self._img, batch, first, batch.n)

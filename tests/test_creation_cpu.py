@@ -16,6 +16,19 @@ def test_contract_address_known_answers():
     assert generate_contract_address(s, 3) == 0xFFFD933A0BC612844EAF0C6FE3E5B8E9B6C1D19C
 
 
+
+def test_contract_address_leading_zero_creator():
+    """The reference passes the creator as an int (world_state.py:171,237), so rlp
+    writes it like any integer: minimal big-endian bytes.  A creator whose top
+    byte is 0 is therefore shorter than 20 bytes in the preimage (here 2 bytes:
+    0x82 0x12 0x34), then the nonce (0 -> 0x80), under a 0xc4 list header."""
+    from mythril_amd.keccak import keccak256
+    want = int.from_bytes(keccak256(bytes([0xC4, 0x82, 0x12, 0x34, 0x80]))[12:], "big")
+    assert generate_contract_address(0x1234, 0) == want
+    want1 = int.from_bytes(keccak256(bytes([0xC4, 0x82, 0x12, 0x34, 0x01]))[12:], "big")
+    assert generate_contract_address(0x1234, 1) == want1
+
+
 def _installed(name, value=0):
     laser_evm, finals, addr = deploy(OracleDevice(), name, value)
     return laser_evm, finals, addr

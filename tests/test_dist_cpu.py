@@ -48,3 +48,40 @@ def test_two_rank_exchange_on_gloo():
     assert models.shape == (3, 2, 8) and (models[0] == 7).all() and (models[1:] == 8).all()
     assert r0["models"] == r1["models"]
     assert r0["timing"] == r1["timing"] == (2.0, 300.0)
+
+
+def _model_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mythril_amd.laser.sharded import exchange_models
+        from mythril_amd.smt.program import ArrayInterp, FuncInterp
+        from mythril_amd.smt.solver import Model, ModelCache
+        mc = ModelCache(device=object())
+        own = Model({"x": 5 + rank, "Storage": ArrayInterp(rank, {1: 2}),
+                     "keccak256_512": FuncInterp(0, {(7 + rank,): 9})})
+        mc.put(own, 1)
+        got = exchange_models(mc)
+        again = exchange_models(mc)          # nothing new: peers' models are not re-shared
+        pool = list(mc.model_cache.lru_cache)
+        out[rank] = (got, again, [m.raw[0].assignment["x"] for m in pool],
+                     [m.raw[0].assignment["Storage"].default for m in pool],
+                     [dict(m.raw[0].assignment["keccak256_512"].entries) for m in pool])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_model_allgather_feeds_every_candidate_pool():
+    """newly found satisfying models join every rank's ModelCache."""
+    world, port = 3, _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_model_worker, args=(world, port, out), nprocs=world, join=True)
+        res = [out[r] for r in range(world)]
+    for rank, (got, again, xs, defaults, ents) in enumerate(res):
+        assert got == world - 1 and again == 0
+        assert xs[0] == 5 + rank                           # own model first (put first)
+        assert sorted(xs) == [5, 6, 7]
+        assert xs[1:] == [5 + r for r in range(world) if r != rank]   # peers in rank order
+        assert sorted(defaults) == [0, 1, 2]
+        assert all({(7 + r,): 9} in ents for r in range(world))

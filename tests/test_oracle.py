@@ -167,3 +167,22 @@ def test_jump_resolution_first_address_at_or_above():
     b.set_lane(0, code_id=cid2)
     o.run(b)
     assert b.status[0] == MG_HALT_STOP and b.storage_dict(0) == {0: 1}
+
+
+def test_disassembler_fixture_instruction_count():
+    """disassembler_test.py:8-10: the reference's 3,523-instruction code (bzzr
+    metadata trimmed).  Oracle and host instruction lists both have 3,523
+    entries and agree instruction by instruction."""
+    from mythril_amd.laser.disassembly import Disassembly
+    from mythril_amd.laser.opcodes import OPCODES
+    fx = load_json("disassembly.json")
+    code = bytes.fromhex(fx["code"][2:])
+    o = OracleEVM()
+    ops, addrs = o.code_table(o.load_code(code))
+    host = Disassembly(fx["code"]).instruction_list
+    assert len(host) == ops.size == fx["instructions"] == 3523
+    for k, ins in enumerate(host):
+        assert ins["address"] == addrs[k]
+        byte = OPCODES.get(ins["opcode"])
+        if byte is not None:
+            assert byte == ops[k], (k, ins)

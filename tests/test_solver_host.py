@@ -87,6 +87,19 @@ def test_constraints_is_possible_error_mapping(fresh):
     assert Constraints([False]).is_possible() is False
 
 
+def test_missing_backend_is_loud_not_a_prune(fresh):
+    """Without an SMT backend a quick-sat miss raises SolverBackendMissing; it is
+    never turned into is_possible() == False (a silent prune)."""
+    x = BVS("x", 256)
+    solver.set_solver_backend(solver._no_backend)
+    c = Constraints([ULT(x, BVV(11, 256))])
+    with pytest.raises(solver.SolverBackendMissing):
+        c.is_possible()
+    with pytest.raises(solver.SolverBackendMissing):
+        c.get_model()
+    assert not issubclass(solver.SolverBackendMissing, (SolverTimeOutException, UnsatError))
+
+
 def test_keccak_manager_reference_behaviour():
     km = KeccakFunctionManager()
     assert km.get_empty_keccak_hash().value == int.from_bytes(keccak256(b""), "big")
