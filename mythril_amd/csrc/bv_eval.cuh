@@ -55,6 +55,7 @@ enum BvOp : uint32_t {
 #define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
 #define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
+#define BV_MPT_DEFAULT 2u     // models per thread (k_bv_eval<.., M>)
 
 struct BvState {
     uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0, tile_cap = 0;
@@ -76,6 +77,7 @@ struct BvState {
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
     size_t cap_entries = 0;
     bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
+    uint32_t mpt = BV_MPT_DEFAULT;   // models per thread (1, 2 or 4); MG_BV_MPT overrides
     std::vector<uint32_t> h_tiles;
 };
 
@@ -119,8 +121,8 @@ struct BvTables {
 struct BvCtx {
     const uint4 *__restrict__ values;
     const uint4 *__restrict__ consts;
-    uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
-    uint32_t n_models, model, tid;
+    uint4 *slots;          // LDS [n_slots][2][M][BV_BLOCK]
+    uint32_t n_models, tid;
     BvTables tab;
 };
 
@@ -133,13 +135,14 @@ DEV U256 ld2(const uint4 *p) {
 }
 
 // model interpretation lookup (entries are unique keys: first match wins)
-DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) {
+DEV U256 bv_table(BvTables tab, uint32_t n_models, uint32_t model, U256 k0, U256 k1,
+                                      uint32_t imm) {
     const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
-    const size_t tm = (size_t)t * c.n_models + c.model;
-    const uint32_t s0 = c.tab.start[tm], cnt = c.tab.count[tm];
-    U256 v = ld2(c.tab.dflt + tm * 4u + part * 2u);
+    const size_t tm = (size_t)t * n_models + model;
+    const uint32_t s0 = tab.start[tm], cnt = tab.count[tm];
+    U256 v = ld2(tab.dflt + tm * 4u + part * 2u);
     for (uint32_t k = 0; k < cnt; ++k) {
-        const uint4 *e = c.tab.entries + (size_t)(s0 + k) * 8u;
+        const uint4 *e = tab.entries + (size_t)(s0 + k) * 8u;
         if (u_eq(ld2(e), k0) && u_eq(ld2(e + 2), k1)) {
             v = ld2(e + 4 + part * 2u);
             break;
@@ -148,32 +151,90 @@ DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) 
     return lo ? u_shr_n(v, lo, 0u) : v;
 }
 
-DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
-    const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
-    U256 r;
-    if (kind == BV_REF_ACC) return acc;
-    if (kind == BV_REF_SLOT) {
-        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid];
-        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid];
-        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-        return r;
+// division-class ops (z3 semantics, division by zero included)
+DEV U256 bv_divop(uint32_t op, U256 A, U256 B, uint32_t width, uint32_t rc) {
+    switch (op) {
+    case BV_UDIV: return z_udiv(A, B);
+    case BV_UREM: return z_urem(A, B);
+    case BV_SDIV: return z_sdiv(bv_sext(A, width), bv_sext(B, width));
+    case BV_SREM: return z_srem(bv_sext(A, width), bv_sext(B, width));
+    case BV_SMOD: return z_smod(bv_sext(A, width), bv_sext(B, width));
+    default: {                     // BV_MUL_NOOVF_U: high w bits of the 2w-bit product are 0
+        bool ovf;
+        if (u_iszero(A) || u_iszero(B)) ovf = false;
+        else {
+            const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
+            ovf = u_lt(q, B);      // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
+        }
+        return u_small(!ovf);
     }
-    if (kind == BV_REF_VAR) {
-        const size_t row = (size_t)idx * c.n_models + c.model;
-        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
-        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-        return r;
     }
-    // constant: uniform address -> scalar loads
-    const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
-    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-    return r;
 }
 
-template <bool kLdsProg>
+// M models per thread: thread t of a block evaluates models
+// chunk_base + m * BV_BLOCK + t (m < M) with ONE instruction stream, so the
+// instruction fetch, decode and dispatch (scalar, wave-uniform) are paid once
+// for M evaluations.
+template <int M>
+DEV void bv_fetch(const BvCtx &c, const U256 (&acc)[M], uint32_t ref, const uint32_t (&model)[M],
+                  U256 (&out)[M]) {
+    const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
+    if (kind == BV_REF_ACC) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) out[m] = acc[m];
+    } else if (kind == BV_REF_SLOT) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const uint4 x = c.slots[((idx * 2u) * M + m) * BV_BLOCK + c.tid];
+            const uint4 y = c.slots[((idx * 2u + 1u) * M + m) * BV_BLOCK + c.tid];
+            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
+            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
+        }
+    } else if (kind == BV_REF_VAR) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const size_t row = (size_t)idx * c.n_models + model[m];
+            const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
+            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
+            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
+        }
+    } else {
+        // constant: uniform address -> scalar loads, shared by the M models
+        const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
+            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
+        }
+    }
+}
+
+#define BV_FOR_M _Pragma("unroll") for (int m = 0; m < M; ++m)
+
+// Apply a large op (Knuth division, table scan) to the M models with ONE inlined
+// copy of its code: a rolled loop over m whose operands and result move through
+// static-index selects on the (uniform) loop counter, so nothing is dynamically
+// indexed (no scratch) and the code is not replicated M times.
+#define BV_ROLLED(EXPR)                                                        \
+    do {                                                                       \
+        if (M == 1) {                                                          \
+            const U256 a_ = A[0], b_ = B[0];                                   \
+            const uint32_t model_ = model[0];                                  \
+            r[0] = (EXPR);                                                     \
+            break;                                                             \
+        }                                                                      \
+        _Pragma("nounroll") for (int mm = 0; mm < M; ++mm) {                   \
+            U256 a_ = A[0], b_ = B[0];                                         \
+            uint32_t model_ = model[0];                                        \
+            _Pragma("unroll") for (int k = 1; k < M; ++k)                      \
+                if (k == mm) { a_ = A[k]; b_ = B[k]; model_ = model[k]; }      \
+            const U256 res_ = (EXPR);                                          \
+            _Pragma("unroll") for (int k = 0; k < M; ++k)                      \
+                if (k == mm) r[k] = res_;                                      \
+        }                                                                      \
+    } while (0)
+
+template <bool kLdsProg, int M>
 __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
@@ -193,7 +254,7 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     // (uniform address -> s_load_dwordx4 through the scalar cache) and LDS only
     // holds the register slots (higher occupancy)
     uint4 *prog = smem;                          // [tile_cap] (kLdsProg)
-    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][BV_BLOCK]
+    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][M][BV_BLOCK]
     // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
@@ -213,16 +274,23 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     __syncthreads();
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
+    constexpr uint32_t CHUNK = BV_BLOCK * (uint32_t)M;
+    const uint32_t n_chunks = (n_models + CHUNK - 1u) / CHUNK;
     const uint32_t c_lo = group * chunks_per_block, c_hi = min(c_lo + chunks_per_block, n_chunks);
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-    const uint32_t model = chunk * BV_BLOCK + tid;
-    const bool live = model < n_models;
-    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid, tab};
+    uint32_t model[M];
+    bool live[M];
+    BV_FOR_M {
+        const uint32_t mm = chunk * CHUNK + (uint32_t)m * BV_BLOCK + tid;
+        live[m] = mm < n_models;
+        model[m] = live[m] ? mm : 0u;
+    }
+    const BvCtx c{values, consts, slots, n_models, tid, tab};
 
     for (uint32_t d = d0; d < d1; ++d) {
         const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
-        U256 acc = u_zero();
+        U256 acc[M];
+        BV_FOR_M acc[m] = u_zero();
         for (uint32_t p = p0; p < p1; ++p) {
             uint32_t w0, ra, rb, rc;
             if (kLdsProg) {
@@ -233,97 +301,98 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
             }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
-            U256 A = bv_fetch(c, acc, ra);
-            U256 r;
+            U256 A[M], r[M];
+            bv_fetch<M>(c, acc, ra, model, A);
             switch (op) {
-            case BV_COPY: r = A; break;
-            case BV_NOT: r = u_not(A); break;
-            case BV_NEG: r = u_neg(A); break;
-            case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
-            case BV_EXTRACT: r = u_shr_n(A, rb & 0xffu, 0u); break;
-            case BV_ZEXT: r = A; break;
-            case BV_SEXT: r = bv_sext(A, rb); break;
+            case BV_COPY: BV_FOR_M r[m] = A[m]; break;
+            case BV_NOT: BV_FOR_M r[m] = u_not(A[m]); break;
+            case BV_NEG: BV_FOR_M r[m] = u_neg(A[m]); break;
+            case BV_BNOT: BV_FOR_M r[m] = u_small((A[m].w[0] & 1u) ^ 1u); break;
+            case BV_EXTRACT: BV_FOR_M r[m] = u_shr_n(A[m], rb & 0xffu, 0u); break;
+            case BV_ZEXT: BV_FOR_M r[m] = A[m]; break;
+            case BV_SEXT: BV_FOR_M r[m] = bv_sext(A[m], rb); break;
             default: {
-                U256 B = bv_fetch(c, acc, rb);
+                U256 B[M];
+                bv_fetch<M>(c, acc, rb, model, B);
                 switch (op) {
-                case BV_ADD: r = u_add(A, B); break;
-                case BV_SUB: r = u_sub(A, B); break;
-                case BV_MUL: r = u_mul(A, B); break;
-                case BV_UDIV: r = z_udiv(A, B); break;
-                case BV_UREM: r = z_urem(A, B); break;
-                case BV_SDIV: r = z_sdiv(bv_sext(A, width), bv_sext(B, width)); break;
-                case BV_SREM: r = z_srem(bv_sext(A, width), bv_sext(B, width)); break;
-                case BV_SMOD: r = z_smod(bv_sext(A, width), bv_sext(B, width)); break;
-                case BV_AND: r = u_and(A, B); break;
-                case BV_OR: r = u_or(A, B); break;
-                case BV_XOR: r = u_xor(A, B); break;
-                case BV_SHL: r = (u_fits32(B) && B.w[0] < width) ? u_shl_n(A, B.w[0]) : u_zero(); break;
-                case BV_LSHR: r = (u_fits32(B) && B.w[0] < width) ? u_shr_n(A, B.w[0], 0u) : u_zero(); break;
-                case BV_ASHR: {
-                    const U256 sa = bv_sext(A, width);
-                    const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
-                    const uint32_t sh = (u_fits32(B) && B.w[0] < width) ? B.w[0] : 255u;
-                    r = u_shr_n(sa, sh, fill);
+                case BV_ADD: BV_FOR_M r[m] = u_add(A[m], B[m]); break;
+                case BV_SUB: BV_FOR_M r[m] = u_sub(A[m], B[m]); break;
+                case BV_MUL: BV_FOR_M r[m] = u_mul(A[m], B[m]); break;
+                case BV_UDIV: case BV_UREM: case BV_SDIV: case BV_SREM: case BV_SMOD: case BV_MUL_NOOVF_U:
+                    BV_ROLLED(bv_divop(op, a_, b_, width, rc));
                     break;
-                }
-                case BV_EQ: r = u_small(u_eq(A, B)); break;
-                case BV_NE: r = u_small(!u_eq(A, B)); break;
-                case BV_ULT: r = u_small(u_lt(A, B)); break;
-                case BV_ULE: r = u_small(!u_lt(B, A)); break;
-                case BV_UGT: r = u_small(u_lt(B, A)); break;
-                case BV_UGE: r = u_small(!u_lt(A, B)); break;
-                case BV_SLT: r = u_small(u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
-                case BV_SLE: r = u_small(!u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
-                case BV_SGT: r = u_small(u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
-                case BV_SGE: r = u_small(!u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
-                case BV_BAND: r = u_small(A.w[0] & B.w[0] & 1u); break;
-                case BV_BOR: r = u_small((A.w[0] | B.w[0]) & 1u); break;
-                case BV_BXOR: r = u_small((A.w[0] ^ B.w[0]) & 1u); break;
-                case BV_BIMPLIES: r = u_small(((A.w[0] & 1u) ^ 1u) | (B.w[0] & 1u)); break;
-                case BV_ITE: {
-                    const U256 C = bv_fetch(c, acc, rc);
-                    r = u_select((A.w[0] & 1u) != 0u, B, C);
+                case BV_AND: BV_FOR_M r[m] = u_and(A[m], B[m]); break;
+                case BV_OR: BV_FOR_M r[m] = u_or(A[m], B[m]); break;
+                case BV_XOR: BV_FOR_M r[m] = u_xor(A[m], B[m]); break;
+                case BV_SHL:
+                    BV_FOR_M r[m] = (u_fits32(B[m]) && B[m].w[0] < width) ? u_shl_n(A[m], B[m].w[0]) : u_zero();
                     break;
-                }
-                case BV_CONCAT: r = u_or(u_shl_n(A, rc), B); break;
-                case BV_ADD_NOOVF_U: {  // top bit of the (w+1)-bit sum is 0
-                    const U256 s = u_add(A, B);
-                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_n(s, rc, 0u));
-                    r = u_small(!ovf);
+                case BV_LSHR:
+                    BV_FOR_M r[m] = (u_fits32(B[m]) && B[m].w[0] < width) ? u_shr_n(A[m], B[m].w[0], 0u) : u_zero();
                     break;
-                }
-                case BV_MUL_NOOVF_U: {  // high w bits of the 2w-bit product are 0
-                    bool ovf;
-                    if (u_iszero(A) || u_iszero(B)) ovf = false;
-                    else {
-                        const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
-                        ovf = u_lt(q, B);   // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
+                case BV_ASHR:
+                    BV_FOR_M {
+                        const U256 sa = bv_sext(A[m], width);
+                        const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
+                        const uint32_t sh = (u_fits32(B[m]) && B[m].w[0] < width) ? B[m].w[0] : 255u;
+                        r[m] = u_shr_n(sa, sh, fill);
                     }
-                    r = u_small(!ovf);
+                    break;
+                case BV_EQ: BV_FOR_M r[m] = u_small(u_eq(A[m], B[m])); break;
+                case BV_NE: BV_FOR_M r[m] = u_small(!u_eq(A[m], B[m])); break;
+                case BV_ULT: BV_FOR_M r[m] = u_small(u_lt(A[m], B[m])); break;
+                case BV_ULE: BV_FOR_M r[m] = u_small(!u_lt(B[m], A[m])); break;
+                case BV_UGT: BV_FOR_M r[m] = u_small(u_lt(B[m], A[m])); break;
+                case BV_UGE: BV_FOR_M r[m] = u_small(!u_lt(A[m], B[m])); break;
+                case BV_SLT: BV_FOR_M r[m] = u_small(u_slt(bv_sext(A[m], rc), bv_sext(B[m], rc))); break;
+                case BV_SLE: BV_FOR_M r[m] = u_small(!u_slt(bv_sext(B[m], rc), bv_sext(A[m], rc))); break;
+                case BV_SGT: BV_FOR_M r[m] = u_small(u_slt(bv_sext(B[m], rc), bv_sext(A[m], rc))); break;
+                case BV_SGE: BV_FOR_M r[m] = u_small(!u_slt(bv_sext(A[m], rc), bv_sext(B[m], rc))); break;
+                case BV_BAND: BV_FOR_M r[m] = u_small(A[m].w[0] & B[m].w[0] & 1u); break;
+                case BV_BOR: BV_FOR_M r[m] = u_small((A[m].w[0] | B[m].w[0]) & 1u); break;
+                case BV_BXOR: BV_FOR_M r[m] = u_small((A[m].w[0] ^ B[m].w[0]) & 1u); break;
+                case BV_BIMPLIES: BV_FOR_M r[m] = u_small(((A[m].w[0] & 1u) ^ 1u) | (B[m].w[0] & 1u)); break;
+                case BV_ITE: {
+                    U256 C[M];
+                    bv_fetch<M>(c, acc, rc, model, C);
+                    BV_FOR_M r[m] = u_select((A[m].w[0] & 1u) != 0u, B[m], C[m]);
                     break;
                 }
-                case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
-                case BV_TAB: r = bv_table(c, A, B, rc); break;
-                default: r = u_zero(); break;
+                case BV_CONCAT: BV_FOR_M r[m] = u_or(u_shl_n(A[m], rc), B[m]); break;
+                case BV_ADD_NOOVF_U:   // top bit of the (w+1)-bit sum is 0
+                    BV_FOR_M {
+                        const U256 s = u_add(A[m], B[m]);
+                        const bool ovf = rc >= 256u ? u_lt(s, A[m]) : !u_iszero(u_shr_n(s, rc, 0u));
+                        r[m] = u_small(!ovf);
+                    }
+                    break;
+                case BV_SUB_NOUDF_U: BV_FOR_M r[m] = u_small(!u_lt(A[m], B[m])); break;
+                case BV_TAB: BV_ROLLED(bv_table(c.tab, n_models, model_, a_, b_, rc)); break;
+                default: BV_FOR_M r[m] = u_zero(); break;
                 }
             }
             }
-            r = bv_mask(r, width);
-            acc = r;
+            if (width < 256u) { BV_FOR_M r[m] = bv_mask(r[m], width); }
+            BV_FOR_M acc[m] = r[m];
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;
-                slots[(ds * 2u) * BV_BLOCK + tid] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
-                slots[(ds * 2u + 1u) * BV_BLOCK + tid] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
+                BV_FOR_M {
+                    slots[((ds * 2u) * M + m) * BV_BLOCK + tid] = make_uint4(r[m].w[0], r[m].w[1], r[m].w[2], r[m].w[3]);
+                    slots[((ds * 2u + 1u) * M + m) * BV_BLOCK + tid] = make_uint4(r[m].w[4], r[m].w[5], r[m].w[6], r[m].w[7]);
+                }
             }
         }
-        const bool sat = live && (acc.w[0] & 1u);
-        const uint64_t bal = __ballot(sat);
-        if ((tid & 63u) == 0u && bal) {
-            // optional per-model bitmap (one u64 per wave): lets the host replay
-            // sequential check_quick_sat calls whose LRU bumps reorder the pool
-            if (sat_bits) sat_bits[(size_t)d * bit_words + ((chunk * BV_BLOCK + tid) >> 6)] = bal;
-            atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
-            atomicMin(&blk_first[d - d0], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
+        BV_FOR_M {
+            const bool sat = live[m] && (acc[m].w[0] & 1u);
+            const uint64_t bal = __ballot(sat);
+            if ((tid & 63u) == 0u && bal) {
+                const uint32_t base = chunk * CHUNK + (uint32_t)m * BV_BLOCK + tid;   // tid % 64 == 0
+                // optional per-model bitmap (one u64 per wave): lets the host replay
+                // sequential check_quick_sat calls whose LRU bumps reorder the pool
+                if (sat_bits) sat_bits[(size_t)d * bit_words + (base >> 6)] = bal;
+                atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
+                atomicMin(&blk_first[d - d0], base + (uint32_t)(__ffsll((long long)bal) - 1));
+            }
         }
     }
     }
@@ -459,6 +528,14 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     s.n_tables = models->n_tables; s.n_entries = models->n_entries;
     const char *pv = getenv("MG_BV_PROG");
     s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
+    const char *mv = getenv("MG_BV_MPT");
+    s.mpt = mv ? (uint32_t)atoi(mv) : BV_MPT_DEFAULT;
+    if (s.mpt != 1u && s.mpt != 2u && s.mpt != 4u) s.mpt = BV_MPT_DEFAULT;
+    // a pool smaller than one block of threads gains nothing from more models per thread
+    while (s.mpt > 1u && (size_t)models->n_models <= (size_t)BV_BLOCK * (s.mpt / 2u)) s.mpt /= 2u;
+    // LDS per block (program tile + M register slots per thread) within 64 KiB
+    const size_t slots_b = (size_t)std::max<uint32_t>(dags->n_slots, 1) * 2u * BV_BLOCK * sizeof(uint4);
+    while (s.mpt > 1u && (size_t)s.tile_cap * sizeof(uint4) + slots_b * s.mpt > 65536u) s.mpt /= 2u;
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;
@@ -486,15 +563,19 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t tiles_pad = (nt + 7u) & ~7u;
     // model chunks per block: as many as keep >= BV_GROUP_TARGET blocks in flight,
     // so each program tile is staged once per block instead of once per chunk
-    const uint32_t chunks = (s.n_models + BV_BLOCK - 1) / BV_BLOCK;
+    const uint32_t chunk_models = BV_BLOCK * s.mpt;
+    const uint32_t chunks = (s.n_models + chunk_models - 1) / chunk_models;
     const uint32_t groups_wanted = std::max<uint32_t>(1u, (BV_GROUP_TARGET + tiles_pad - 1u) / tiles_pad);
     const uint32_t cpb = std::max<uint32_t>(1u, chunks / std::min(groups_wanted, chunks));
     const uint32_t groups = (chunks + cpb - 1u) / cpb;
     const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
     const bool lds_prog = s.lds_prog;
-    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
-    hipLaunchKernelGGL(lds_prog ? k_bv_eval<true> : k_bv_eval<false>, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
+    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK * s.mpt) *
+                       sizeof(uint4);
+    auto kern = lds_prog ? (s.mpt == 4u ? k_bv_eval<true, 4> : s.mpt == 2u ? k_bv_eval<true, 2> : k_bv_eval<true, 1>)
+                         : (s.mpt == 4u ? k_bv_eval<false, 4> : s.mpt == 2u ? k_bv_eval<false, 2> : k_bv_eval<false, 1>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
                        s.insns, s.prog_off, s.tile_dag,
                        s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
                        s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,

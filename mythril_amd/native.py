@@ -51,7 +51,9 @@ def source_hash() -> str:
     h = hashlib.sha256()
     for p in sources():
         h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
-    h.update(" ".join(_command("OUT")[1:]).encode())
+    # the flags only: the compiler and source paths differ between this container
+    # and the GPU box's copy of the tree
+    h.update(" ".join(a for a in _command("OUT")[1:] if not a.startswith("/")).encode())
     return h.hexdigest()
 
 

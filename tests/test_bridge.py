@@ -1,0 +1,175 @@
+"""The seam to the reference's objects (mythril_amd/bridge.py), on CPU:
+
+* to_dag over a z3-shaped AST (tests/fakez3.py) lands on the very nodes this
+  repo's expression layer builds for the same terms (hash-consing makes that an
+  identity check) and evaluates identically; real z3 is absent here, so the
+  converter is parity unpinned against z3's own output;
+* pack_global_state / unpack_global_state round-trip a reference-shaped
+  GlobalState (tests/refshapes.py) through the batched LaserEVM on the oracle
+  device, and symbolic states are rejected;
+* every ```python block of INTEGRATION.md that is marked runnable executes
+  against these functions."""
+import random
+import re
+from pathlib import Path
+
+import pytest
+
+import fakez3 as z
+import refshapes as R
+from mythril_amd import bridge
+from mythril_amd import workloads
+from mythril_amd.smt.expr import (And, Array, Concat, Extract, Function, If, K, LShR, Not, Or,
+                                  SignExt, UDiv, UGE, ULT, URem, SRem, ZeroExt, symbol_factory)
+from smt_eval import evaluate
+
+BVS, BVV = symbol_factory.BitVecSym, symbol_factory.BitVecVal
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_to_dag_lands_on_the_same_nodes():
+    x, y = z.BitVec("x", 256), z.BitVec("y", 256)
+    X, Y = BVS("x", 256), BVS("y", 256)
+    cases = [
+        (z.bv("BADD", x, y), X + Y),
+        (z.bv("BADD", x, y, z.BitVecVal(3, 256)), X + Y + BVV(3, 256)),
+        (z.bv("BSUB", x, z.BitVecVal(1, 256)), X - BVV(1, 256)),
+        (z.bv("BUDIV_I", x, y), UDiv(X, Y)),
+        (z.bv("BUREM", x, y), URem(X, Y)),
+        (z.bv("BSREM_I", x, y), SRem(X, Y)),
+        (z.bv("BSDIV", x, y), X / Y),
+        (z.bv("BASHR", x, y), X >> Y),
+        (z.bv("BLSHR", x, y), LShR(X, Y)),
+        (z.bv("BNOT", x), ~X),
+        (z.pred("ULT", x, y), ULT(X, Y)),
+        (z.pred("SLT", x, y), X < Y),
+        (z.pred("EQ", x, y), X == Y),
+        (z.pred("NOT", z.pred("EQ", x, y)), Not(X == Y)),
+        (z.pred("OR", z.pred("ULT", x, y), z.pred("EQ", x, y)), Or(ULT(X, Y), X == Y)),
+        (z.pred("AND", z.pred("ULT", x, y), z.pred("SGT", x, y)), And(ULT(X, Y), X > Y)),
+        (z.If(z.pred("ULT", x, y), x, y), If(ULT(X, Y), X, Y)),
+        (z.Concat(z.Extract(127, 0, x), z.Extract(255, 128, y)),
+         Concat(Extract(127, 0, X), Extract(255, 128, Y))),
+        (z.ZeroExt(248, z.BitVec("c", 8)), ZeroExt(248, BVS("c", 8))),
+        (z.SignExt(248, z.BitVec("c", 8)), SignExt(248, BVS("c", 8))),
+    ]
+    for ze, ours in cases:
+        assert bridge.to_dag(ze, z) is ours.raw, ours
+
+
+def test_to_dag_arrays_functions_and_folding():
+    x = z.BitVec("x", 256)
+    S = z.Array("Storage", 256, 256)
+    st = z.Store(S, z.BitVecVal(1, 256), x)
+    sel = z.Select(st, z.BitVecVal(1, 256))
+    assert bridge.to_dag(sel, z) is BVS("x", 256).raw          # select-over-store folds as z3 simplify
+    ours = Array("Storage", 256, 256)
+    ours[BVV(1, 256)] = BVS("x", 256)
+    assert bridge.to_dag(z.Select(st, x), z) is ours[BVS("x", 256)].raw
+    k = z.K(256, z.BitVecVal(0, 8))
+    assert bridge.to_dag(z.Select(k, z.BitVecVal(5, 256)), z).param == 0
+    f = z.Function("keccak256_512", [512], 256)
+    arg = z.Concat(x, z.BitVecVal(0, 256))
+    F = Function("keccak256_512", [512], 256)
+    assert bridge.to_dag(f(arg), z) is F(Concat(BVS("x", 256), BVV(0, 256))).raw
+    assert bridge.to_dag(z.bv("BADD", z.BitVecVal(2, 256), z.BitVecVal(3, 256)), z).param == 5
+    with pytest.raises(bridge.Unconvertible):
+        bridge.to_dag(z.pred("BSMUL_NO_OVFL", x, x), z)
+
+
+def _rand_z3(rng, depth, x, y):
+    if depth == 0:
+        return rng.choice([x, y, z.BitVecVal(rng.getrandbits(256), 256), z.BitVecVal(rng.randrange(300), 256)])
+    op = rng.choice(["BADD", "BSUB", "BMUL", "BUDIV", "BUREM", "BAND", "BOR", "BXOR", "BSHL",
+                     "BLSHR", "BASHR", "ITE", "EXT"])
+    a, b = _rand_z3(rng, depth - 1, x, y), _rand_z3(rng, depth - 1, x, y)
+    if op == "ITE":
+        return z.If(z.pred(rng.choice(["ULT", "SLT", "EQ", "UGEQ"]), a, b), a, b)
+    if op == "EXT":
+        return z.ZeroExt(128, z.Extract(200, 73, a))
+    return z.bv(op, a, b)
+
+
+def test_to_dag_random_terms_evaluate_like_their_definition():
+    """Random z3-shaped terms: the converted DAG evaluated under random models
+    equals a direct evaluation of the fake AST with the SMT-LIB semantics."""
+    from mythril_amd.smt.semantics import apply_op
+    names = {"BADD": "bvadd", "BSUB": "bvsub", "BMUL": "bvmul", "BUDIV": "bvudiv",
+             "BUREM": "bvurem", "BAND": "bvand", "BOR": "bvor", "BXOR": "bvxor", "BSHL": "bvshl",
+             "BLSHR": "bvlshr", "BASHR": "bvashr", "ULT": "bvult", "SLT": "bvslt", "EQ": "eq",
+             "UGEQ": "bvuge"}
+    ops = {getattr(z, "Z3_OP_" + k): v for k, v in names.items()}
+
+    def ev(e, m):
+        k = e.decl().kind()
+        if k == z.Z3_OP_BNUM:
+            return e.as_long()
+        if k == z.Z3_OP_UNINTERPRETED:
+            return m[e.decl().name()]
+        a = [ev(c, m) for c in e.children()]
+        if k == z.Z3_OP_ITE:
+            return a[1] if a[0] else a[2]
+        if k == z.Z3_OP_EXTRACT:
+            hi, lo = e.decl().params()
+            return (a[0] >> lo) & ((1 << (hi - lo + 1)) - 1)
+        if k == z.Z3_OP_ZERO_EXT:
+            return a[0]
+        w = e.children()[0].size()
+        return apply_op(ops[k], 1 if k in (z.Z3_OP_ULT, z.Z3_OP_SLT, z.Z3_OP_EQ, z.Z3_OP_UGEQ) else w,
+                        a, [w, w], None)
+
+    rng = random.Random(5)
+    x, y = z.BitVec("x", 256), z.BitVec("y", 256)
+    for _ in range(150):
+        e = _rand_z3(rng, rng.randrange(1, 4), x, y)
+        node = bridge.to_dag(e, z)
+        for _ in range(4):
+            m = {"x": rng.choice([0, 1, rng.getrandbits(256)]), "y": rng.choice([2, rng.getrandbits(256)])}
+            assert evaluate(node, m) == ev(e, m)
+
+
+def _ref_state(calldata: bytes, symbolic=False):
+    code = workloads.bytecode("overflow.sol.o").hex()
+    acct = R.Account(workloads.CONTRACT, code, concrete_storage=not symbolic)
+    acct.storage[R.BitVec(1)] = R.BitVec(10 ** 6)
+    cd = R.SymbolicCalldata() if symbolic else R.ConcreteCalldata(calldata)
+    env = R.Environment(acct, workloads.ATTACKER, cd, 1, 0, workloads.ATTACKER)
+    return R.GlobalState(R.WorldState(), env, R.MachineState(), R.MessageCallTransaction(8_000_000))
+
+
+def test_pack_rejects_symbolic_state():
+    assert bridge.is_concrete(_ref_state(bytes.fromhex("18160ddd")))
+    assert not bridge.is_concrete(_ref_state(b"", symbolic=True))
+    s = _ref_state(bytes.fromhex("18160ddd"))
+    s.mstate.stack.append(R.BitVec(None, 256, "calldatasize"))
+    assert not bridge.is_concrete(s)
+    with pytest.raises(bridge.NotConcrete):
+        bridge.pack_global_state(s)
+
+
+def _integration_blocks():
+    text = (ROOT / "INTEGRATION.md").read_text()
+    return [b for b in re.findall(r"```python\n(.*?)```", text, re.S) if b.startswith("# runnable")]
+
+
+def test_integration_snippets_execute():
+    """The runnable INTEGRATION.md blocks, with the reference-shaped stand-ins
+    as `ref_states` / `symbol_factory` and the oracle as the device."""
+    from oracle_device import OracleDevice
+    blocks = _integration_blocks()
+    assert len(blocks) >= 2
+    ref_states = [_ref_state(bytes.fromhex("18160ddd")),
+                  _ref_state(bytes.fromhex("70a08231") + workloads.ATTACKER.to_bytes(32, "big")),
+                  _ref_state(b"", symbolic=True)]
+    ns = {"ref_states": ref_states, "device": OracleDevice(), "symbol_factory": R.symbol_factory,
+          "z3": z, "ref_constraints": [z.pred("ULT", z.BitVec("x", 256), z.BitVecVal(9, 256))]}
+    for b in blocks:
+        exec(compile(b, "INTEGRATION.md", "exec"), ns)
+    # totalSupply() returns slot 1: the device ran to RETURN and wrote back
+    s0 = ref_states[0]
+    assert ns["final"] and s0.mstate.pc > 0 and s0.mstate.min_gas_used > 0
+    assert len(s0.mstate.memory) >= 0x80
+    word = bytes(s0.mstate.memory[k] for k in range(0x80, 0xA0))
+    assert int.from_bytes(word, "big") == 10 ** 6
+    assert ref_states[2].mstate.pc == 0                      # symbolic: left to the reference
+    assert ns["query"].raw.op == "bvult"
