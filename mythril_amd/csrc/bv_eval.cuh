@@ -56,13 +56,14 @@ enum BvOp : uint32_t {
 #define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
 #define BV_MPT_DEFAULT 2u     // models per thread (k_bv_eval<.., M>)
+#define BV_LDS_MAX (96u * 1024u)   // dynamic LDS a kernel-2 block may take
 
 struct BvState {
     uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0, tile_cap = 0;
-    uint4 *insns = nullptr;          // [total]
-    uint32_t *prog_off = nullptr;    // [n_dags + 1]
+    uint4 *timg = nullptr;           // tile images: per tile [its instructions][its constants x 2]
+    uint32_t *prog_off = nullptr;    // [n_dags + 1] instruction offsets (global numbering)
     uint32_t *tile_dag = nullptr;    // [n_tiles + 1] first DAG of each tile
-    uint4 *consts = nullptr;         // [n_consts][2]
+    uint32_t *tile_img = nullptr;    // [n_tiles + 1] offset (uint4) of each tile image in timg
     uint4 *values = nullptr;         // [n_vars][n_models][2]
     uint32_t n_tables = 0, n_entries = 0;
     uint32_t *tab_start = nullptr;   // [n_tables][n_models]
@@ -74,11 +75,11 @@ struct BvState {
     unsigned long long *sat_bits = nullptr;   // [n_dags][bit_words] (mg_eval_bits)
     size_t cap_bits = 0;
     bool want_bits = false;
-    size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
+    size_t cap_timg = 0, cap_dags = 0, cap_values = 0, cap_tiles = 0, cap_timgoff = 0;
     size_t cap_entries = 0;
-    bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
     uint32_t mpt = BV_MPT_DEFAULT;   // models per thread (1, 2 or 4); MG_BV_MPT overrides
-    std::vector<uint32_t> h_tiles;
+    std::vector<uint32_t> h_tiles, h_timg_off;
+    std::vector<uint4> h_timg;
 };
 
 DEV U256 bv_mask(U256 v, uint32_t width) {
@@ -120,7 +121,7 @@ struct BvTables {
 
 struct BvCtx {
     const uint4 *__restrict__ values;
-    const uint4 *__restrict__ consts;
+    const uint4 *consts;   // LDS: this tile's constants (2 x uint4 each)
     uint4 *slots;          // LDS [n_slots][2][M][BV_BLOCK]
     uint32_t n_models, tid;
     BvTables tab;
@@ -199,8 +200,9 @@ DEV void bv_fetch(const BvCtx &c, const U256 (&acc)[M], uint32_t ref, const uint
             out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
         }
     } else {
-        // constant: uniform address -> scalar loads, shared by the M models
-        const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
+        // constant: the tile's own pool, staged in LDS with its instructions
+        // (uniform address: a broadcast read), shared by the M models
+        const uint4 x = c.consts[2u * idx], y = c.consts[2u * idx + 1u];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
@@ -234,11 +236,11 @@ DEV void bv_fetch(const BvCtx &c, const U256 (&acc)[M], uint32_t ref, const uint
         }                                                                      \
     } while (0)
 
-template <bool kLdsProg, int M>
-__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
+template <int M>
+__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ timg,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
-                                                      const uint4 *__restrict__ consts,
+                                                      const uint32_t *__restrict__ tile_img,
                                                       const uint4 *__restrict__ values, uint32_t n_models,
                                                       BvTables tab,
                                                       uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles,
@@ -249,12 +251,12 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       unsigned long long *__restrict__ sat_bits,
                                                       uint32_t bit_words) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    // kLdsProg: the program tile is staged in LDS and read with a broadcast
-    // ds_read + readfirstlane; otherwise instructions are read with scalar loads
-    // (uniform address -> s_load_dwordx4 through the scalar cache) and LDS only
-    // holds the register slots (higher occupancy)
-    uint4 *prog = smem;                          // [tile_cap] (kLdsProg)
-    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][M][BV_BLOCK]
+    // The tile image — the tile's programs followed by the constants they use,
+    // remapped to tile-local indices on the host (bv_upload) — is staged into LDS
+    // with one coalesced copy and read with broadcast ds_reads; constants never
+    // cost a dependent scalar load from a table that, at C4's 1M DAGs, is 1 GB.
+    uint4 *prog = smem;                          // [tile_cap]
+    uint4 *slots = smem + tile_cap;              // [n_slots][2][M][BV_BLOCK]
     // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
@@ -264,14 +266,17 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     const uint32_t d0 = max(tile_dag[tile], dag_lo), d1 = min(tile_dag[tile + 1], dag_hi);
     if (d0 >= d1) return;
     // the tile is read from HBM once per block and reused for every model chunk
-    const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
     // per-block results of the tile's DAGs: waves combine in LDS, the block adds
     // its totals to HBM once per DAG (not one atomic pair per wave per DAG)
     __shared__ uint32_t blk_cnt[BV_TILE_DAGS], blk_first[BV_TILE_DAGS];
     if (threadIdx.x < BV_TILE_DAGS) { blk_cnt[threadIdx.x] = 0u; blk_first[threadIdx.x] = 0xffffffffu; }
-    if (kLdsProg)
-        for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
+    const uint32_t img0 = tile_img[tile], img_n = tile_img[tile + 1] - img0;
+    // a range-limited run (dag_lo/dag_hi) stages the whole tile: consts follow
+    // the tile's full instruction list
+    const uint32_t t_i0 = prog_off[tile_dag[tile]], t_n = prog_off[tile_dag[tile + 1]] - t_i0;
+    for (uint32_t i = threadIdx.x; i < img_n; i += BV_BLOCK) prog[i] = timg[img0 + i];
     __syncthreads();
+    const uint4 *tconst = prog + t_n;
 
     const uint32_t tid = threadIdx.x;
     constexpr uint32_t CHUNK = BV_BLOCK * (uint32_t)M;
@@ -285,21 +290,15 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
         live[m] = mm < n_models;
         model[m] = live[m] ? mm : 0u;
     }
-    const BvCtx c{values, consts, slots, n_models, tid, tab};
+    const BvCtx c{values, tconst, slots, n_models, tid, tab};
 
     for (uint32_t d = d0; d < d1; ++d) {
-        const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
+        const uint32_t p0 = prog_off[d] - t_i0, p1 = prog_off[d + 1] - t_i0;
         U256 acc[M];
         BV_FOR_M acc[m] = u_zero();
         for (uint32_t p = p0; p < p1; ++p) {
-            uint32_t w0, ra, rb, rc;
-            if (kLdsProg) {
-                const uint4 ins = prog[p];
-                w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
-            } else {
-                const uint4 ins = insns[i0 + uni(p)];
-                w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
-            }
+            const uint4 ins = prog[p];
+            const uint32_t w0 = uni(ins.x), ra = uni(ins.y), rb = uni(ins.z), rc = uni(ins.w);
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
             U256 A[M], r[M];
             bv_fetch<M>(c, acc, ra, model, A);
@@ -418,7 +417,7 @@ static int bv_ensure(T *&p, size_t &cap, size_t need) {
 }
 
 static void bv_free(BvState &s) {
-    hipFree(s.insns); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.consts);
+    hipFree(s.timg); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.tile_img);
     hipFree(s.values); hipFree(s.first_sat); hipFree(s.sat_count);
     hipFree(s.tab_start); hipFree(s.tab_count); hipFree(s.tab_entries); hipFree(s.tab_default);
     hipFree(s.sat_bits);
@@ -460,27 +459,102 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
             }
         }
     }
-    // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
-    // LDS tile capacity: the longest program rounded up, at least BV_TILE_MIN, so
-    // short-program batches keep a small LDS footprint (higher occupancy)
+    // Tiles: consecutive DAGs (at most BV_TILE_DAGS) whose tile image fits the LDS
+    // tile: their instructions plus every constant they use, each constant once
+    // per tile, operand refs rewritten to tile-local constant indices.
+    const size_t slots_b1 = (size_t)std::max<uint32_t>(dags->n_slots, 1) * 2u * BV_BLOCK * sizeof(uint4);
+    const uint32_t img_max = (uint32_t)((BV_LDS_MAX - slots_b1) / sizeof(uint4));
+    auto nrefs = [](uint32_t op) -> int {
+        return (op == BV_ITE) ? 3 : (op == BV_COPY || op == BV_NOT || op == BV_NEG || op == BV_BNOT ||
+                                      op == BV_EXTRACT || op == BV_ZEXT || op == BV_SEXT) ? 1 : 2;
+    };
+    std::vector<uint32_t> stamp(std::max<uint32_t>(dags->n_consts, 1), 0xffffffffu);
+    std::vector<uint32_t> local(std::max<uint32_t>(dags->n_consts, 1), 0u);
+    // per DAG: its own distinct constants (image size alone) -> tile capacity
     uint32_t longest = 0;
-    for (uint32_t d = 0; d < n; ++d) longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d]);
-    s.tile_cap = std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u);
-    s.h_tiles.clear();
-    s.h_tiles.push_back(0);
-    uint32_t acc = 0;
     for (uint32_t d = 0; d < n; ++d) {
-        const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
-        if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= BV_TILE_DAGS) { s.h_tiles.push_back(d); acc = 0; }
-        acc += len;
+        uint32_t uc = 0;
+        for (uint32_t i = dags->prog_off[d]; i < dags->prog_off[d + 1]; ++i) {
+            const uint32_t *w = dags->insns + 4 * (size_t)i;
+            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
+                if ((w[1 + k] >> 30) == BV_REF_CONST) {
+                    const uint32_t g = w[1 + k] & 0x3fffffffu;
+                    if (stamp[g] != d) { stamp[g] = d; ++uc; }
+                }
+        }
+        longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d] + 2u * uc);
     }
+    if (longest > img_max) { msg = "program plus its constants exceed the LDS tile"; return MG_EINVAL; }
+    s.tile_cap = std::min(img_max, std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u));
+    std::fill(stamp.begin(), stamp.end(), 0xffffffffu);
+    s.h_tiles.assign(1, 0u);
+    s.h_timg_off.assign(1, 0u);
+    s.h_timg.clear();
+    s.h_timg.reserve((size_t)total * 2);
+    std::vector<uint32_t> tconsts;          // global indices of the current tile's constants
+    uint32_t tile_id = 0, t_insns = 0;
+    auto close_tile = [&](uint32_t d_end) {
+        for (uint32_t g : tconsts) {
+            const uint32_t *c = dags->consts + 8 * (size_t)g;
+            s.h_timg.push_back(make_uint4(c[0], c[1], c[2], c[3]));
+            s.h_timg.push_back(make_uint4(c[4], c[5], c[6], c[7]));
+        }
+        s.h_tiles.push_back(d_end);
+        s.h_timg_off.push_back((uint32_t)s.h_timg.size());
+        tconsts.clear();
+        t_insns = 0;
+        ++tile_id;
+    };
+    for (uint32_t d = 0; d < n; ++d) {
+        const uint32_t a = dags->prog_off[d], b = dags->prog_off[d + 1];
+        uint32_t fresh = 0;                 // constants this DAG adds to the tile
+        for (uint32_t i = a; i < b; ++i) {
+            const uint32_t *w = dags->insns + 4 * (size_t)i;
+            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
+                if ((w[1 + k] >> 30) == BV_REF_CONST) {
+                    const uint32_t g = w[1 + k] & 0x3fffffffu;
+                    if (stamp[g] != tile_id && local[g] != 0xfffffffeu) { local[g] = 0xfffffffeu; ++fresh; }
+                }
+        }
+        for (uint32_t i = a; i < b; ++i) {          // undo the counting marks
+            const uint32_t *w = dags->insns + 4 * (size_t)i;
+            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
+                if ((w[1 + k] >> 30) == BV_REF_CONST && local[w[1 + k] & 0x3fffffffu] == 0xfffffffeu)
+                    local[w[1 + k] & 0x3fffffffu] = 0u;
+        }
+        if (d > s.h_tiles.back() &&
+            (t_insns + (b - a) + 2u * ((uint32_t)tconsts.size() + fresh) > s.tile_cap ||
+             d - s.h_tiles.back() >= BV_TILE_DAGS)) {
+            close_tile(d);
+            // the new tile's image starts with this DAG: instructions come first,
+            // so move nothing -- images are built tile by tile below
+        }
+        for (uint32_t i = a; i < b; ++i) {
+            const uint32_t *w = dags->insns + 4 * (size_t)i;
+            uint32_t x[4] = {w[0], w[1], w[2], w[3]};
+            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
+                if ((x[1 + k] >> 30) == BV_REF_CONST) {
+                    const uint32_t g = x[1 + k] & 0x3fffffffu;
+                    if (stamp[g] != tile_id) {
+                        stamp[g] = tile_id;
+                        local[g] = (uint32_t)tconsts.size();
+                        tconsts.push_back(g);
+                    }
+                    x[1 + k] = (BV_REF_CONST << 30) | local[g];
+                }
+            s.h_timg.push_back(make_uint4(x[0], x[1], x[2], x[3]));
+        }
+        t_insns += b - a;
+    }
+    close_tile(n);
+    s.h_tiles.pop_back();                         // close_tile pushed n: keep one n at the end
     s.h_tiles.push_back(n);
     s.n_tiles = (uint32_t)s.h_tiles.size() - 1;
     int rc = 0;
-    if ((rc = bv_ensure(s.insns, s.cap_insns, total))) { msg = "alloc insns"; return rc; }
+    if ((rc = bv_ensure(s.timg, s.cap_timg, s.h_timg.size()))) { msg = "alloc tile images"; return rc; }
     if ((rc = bv_ensure(s.prog_off, s.cap_dags, (size_t)n + 1))) { msg = "alloc offsets"; return rc; }
     if ((rc = bv_ensure(s.tile_dag, s.cap_tiles, s.h_tiles.size()))) { msg = "alloc tiles"; return rc; }
-    if ((rc = bv_ensure(s.consts, s.cap_consts, (size_t)std::max<uint32_t>(dags->n_consts, 1) * 2))) { msg = "alloc consts"; return rc; }
+    if ((rc = bv_ensure(s.tile_img, s.cap_timgoff, s.h_timg_off.size()))) { msg = "alloc tile offsets"; return rc; }
     if ((rc = bv_ensure(s.values, s.cap_values, (size_t)std::max<uint32_t>(models->n_vars, 1) * models->n_models * 2))) { msg = "alloc values"; return rc; }
     if (models->n_tables) {
         if (!models->tab_start || !models->tab_count || !models->tab_default ||
@@ -508,10 +582,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         return MG_ENOMEM;
     }
     hipError_t e = hipSuccess;
-    e = e ? e : hipMemcpyAsync(s.insns, dags->insns, (size_t)total * 16, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.timg, s.h_timg.data(), s.h_timg.size() * 16, hipMemcpyHostToDevice, st);
     e = e ? e : hipMemcpyAsync(s.prog_off, dags->prog_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st);
     e = e ? e : hipMemcpyAsync(s.tile_dag, s.h_tiles.data(), s.h_tiles.size() * 4, hipMemcpyHostToDevice, st);
-    if (dags->n_consts) e = e ? e : hipMemcpyAsync(s.consts, dags->consts, (size_t)dags->n_consts * 32, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.tile_img, s.h_timg_off.data(), s.h_timg_off.size() * 4, hipMemcpyHostToDevice, st);
     if (models->n_vars)
         e = e ? e : hipMemcpyAsync(s.values, models->values, (size_t)models->n_vars * models->n_models * 32, hipMemcpyHostToDevice, st);
     if (models->n_tables) {
@@ -526,16 +600,14 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     e = e ? e : hipStreamSynchronize(st);
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
     s.n_tables = models->n_tables; s.n_entries = models->n_entries;
-    const char *pv = getenv("MG_BV_PROG");
-    s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
     const char *mv = getenv("MG_BV_MPT");
     s.mpt = mv ? (uint32_t)atoi(mv) : BV_MPT_DEFAULT;
     if (s.mpt != 1u && s.mpt != 2u && s.mpt != 4u) s.mpt = BV_MPT_DEFAULT;
     // a pool smaller than one block of threads gains nothing from more models per thread
     while (s.mpt > 1u && (size_t)models->n_models <= (size_t)BV_BLOCK * (s.mpt / 2u)) s.mpt /= 2u;
-    // LDS per block (program tile + M register slots per thread) within 64 KiB
+    // LDS per block (program tile + M register slots per thread) within BV_LDS_MAX
     const size_t slots_b = (size_t)std::max<uint32_t>(dags->n_slots, 1) * 2u * BV_BLOCK * sizeof(uint4);
-    while (s.mpt > 1u && (size_t)s.tile_cap * sizeof(uint4) + slots_b * s.mpt > 65536u) s.mpt /= 2u;
+    while (s.mpt > 1u && (size_t)s.tile_cap * sizeof(uint4) + slots_b * s.mpt > BV_LDS_MAX) s.mpt /= 2u;
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;
@@ -570,14 +642,15 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t groups = (chunks + cpb - 1u) / cpb;
     const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
-    const bool lds_prog = s.lds_prog;
-    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK * s.mpt) *
-                       sizeof(uint4);
-    auto kern = lds_prog ? (s.mpt == 4u ? k_bv_eval<true, 4> : s.mpt == 2u ? k_bv_eval<true, 2> : k_bv_eval<true, 1>)
-                         : (s.mpt == 4u ? k_bv_eval<false, 4> : s.mpt == 2u ? k_bv_eval<false, 2> : k_bv_eval<false, 1>);
+    const size_t lds = ((size_t)s.tile_cap + (size_t)s.n_slots * 2 * BV_BLOCK * s.mpt) * sizeof(uint4);
+    auto kern = s.mpt == 4u ? k_bv_eval<4> : s.mpt == 2u ? k_bv_eval<2> : k_bv_eval<1>;
+    if (lds > 65536u) {
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BV_LDS_MAX);
+        (void)hipGetLastError();
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
-                       s.insns, s.prog_off, s.tile_dag,
-                       s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
+                       s.timg, s.prog_off, s.tile_dag, s.tile_img,
+                       s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
                        s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
                        s.tile_cap, cpb, s.first_sat, s.sat_count, s.want_bits ? s.sat_bits : nullptr, bit_words);
     e = hipGetLastError();

@@ -844,7 +844,8 @@ __device__ __forceinline__ void reset_lane(const DevLanes &L, const DevResetImag
 // advanced no lane of this wave).  Lane 0 of each wave keeps its bins in LDS
 // and writes them out with plain vector stores at the end.  Each bin packs
 // cycles in bits 0-23 and the number of iterations in bits 24-31.
-#define CLK_BINS 260u
+#define CLK_BINS 262u   // opcode bins, 256 runs, 257 prologue, 258 epilogue, 259 idle,
+                        // 260 dispatch head (loop top -> decoded), 261 FETCH of the next pc
 __device__ uint32_t g_k1_clk[4096u * CLK_BINS];
 #endif
 
@@ -859,7 +860,11 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           unsigned long long *__restrict__ prof,
                                                           uint32_t win, uint32_t pd_cap, uint32_t jr_cap,
                                                           uint32_t horizon, uint32_t loop_bound,
-                                                          DevResetImage R, uint32_t lpw) {
+                                                          DevResetImage R, uint32_t lpw_flags) {
+    // lpw_flags: lanes per wave in bits 0..7; bit 8 = register-form runs only
+    // (MG_K1_RUNS=reg, for A/B runs against the LDS-resident form)
+    const uint32_t lpw = lpw_flags & 0xffu;
+    const bool lds_runs_on = (lpw_flags & 0x100u) == 0u;
     // Dynamic LDS: [stack window: win x 2 x lanes-per-block x 16 B][pre-decoded code: pd_cap x 8 B]
     //              [runs: pd_cap x 8 B][push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B]
     //              [coverage: pd_cap]
@@ -907,12 +912,18 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     __shared__ uint32_t s_clk[LANE_BLOCK / 64u][CLK_BINS];
     for (uint32_t i = threadIdx.x; i < (LANE_BLOCK / 64u) * CLK_BINS; i += blockDim.x) (&s_clk[0][0])[i] = 0u;
     __syncthreads();
-    const uint64_t clk_start = __builtin_amdgcn_s_memtime();
-    uint64_t clk_t = clk_start;
-    uint32_t clk_bin = 257u;
-#define CLK_MARK(next_) do { const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
-        if ((threadIdx.x & 63u) == 0u) s_clk[threadIdx.x >> 6][clk_bin] += (uint32_t)(t_ - clk_t) + (1u << 24); \
-        clk_t = t_; clk_bin = (next_); } while (0)
+    // wave-uniform clock state in LDS, updated by the first active lane, so a
+    // mark inside a divergent region charges the right bin
+    __shared__ uint64_t s_clk_t[LANE_BLOCK / 64u];
+    __shared__ uint32_t s_clk_bin[LANE_BLOCK / 64u];
+    if ((threadIdx.x & 63u) == 0u) { s_clk_t[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+                                     s_clk_bin[threadIdx.x >> 6] = 257u; }
+#define CLK_MARK(next_) do { const uint64_t t_ = __builtin_amdgcn_s_memtime();                   \
+        const uint64_t act_ = __ballot(1);                                                     \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(act_)) {                           \
+            const uint32_t w_ = threadIdx.x >> 6;                                              \
+            s_clk[w_][s_clk_bin[w_]] += (uint32_t)(t_ - s_clk_t[w_]) + (1u << 24);             \
+            s_clk_t[w_] = t_; s_clk_bin[w_] = (next_); } } while (0)
 #else
 #define CLK_MARK(next_) do { } while (0)
 #endif
@@ -1046,7 +1057,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const bool runs_on = sflag && !prof && !loop_on && ((m0 | m1 | m2 | m3) == 0ull);
 
     for (;;) {
-        CLK_MARK(259u);
+        CLK_MARK(260u);
         const uint64_t live_mask = __ballot(live);
         if (live_mask == 0ull) break;
         const int lead = __builtin_ctzll(live_mask);
@@ -1060,8 +1071,19 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             if (rlen >= 2u) {
                 const uint32_t rneed = (rx >> 8) & 0xffu, rpeak = (rx >> 16) & 0xffu;
                 const uint32_t rg0 = ry & 0xffffu, rg1 = ry >> 16;
+                // LDS-resident form: when the lead lane's whole run stays inside the
+                // LDS stack window, the lanes at the lead's pc AND stack depth run it
+                // with the depth as a scalar: every stack word lives in the window
+                // for the run's duration (T0/T1 spilled on entry, reloaded on exit),
+                // PUSH/DUP/SWAP are LDS copies at scalar offsets and POP/JUMPDEST
+                // cost nothing.  Otherwise the register form below.
+                uint32_t usp = __builtin_amdgcn_readlane(sp, lead);
+                asm volatile("" : "+s"(usp));
+                const bool lds_run = lds_runs_on && usp >= rneed && usp + rpeak <= win &&
+                                     usp + rpeak <= stack_lim;
                 const bool in_run = live && pc == upc && sp >= rneed && sp + rpeak <= stack_lim &&
-                                    gmin + rg0 < glim && executed + rlen <= lane_max;
+                                    gmin + rg0 < glim && executed + rlen <= lane_max &&
+                                    (!lds_run || sp == usp);
                 // the run's pre-decoded words, one per wave lane (rlen <= RUN_MAX = 64),
                 // read by the whole wave in one LDS access; instruction k is then
                 // v_readlane(k) instead of a dependent LDS round trip per instruction
@@ -1070,10 +1092,54 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 uint32_t ybulk = s_pd[min(upc + (threadIdx.x & 63u), pd_cap - 1u)].y;
                 asm volatile("" : "+v"(ybulk));
                 if ((__ballot(in_run) >> lead) & 1ull) {
-#ifdef MG_K1_CLOCKS
-                    clk_bin = 256u;
-#endif
-                    if (in_run) {
+                    CLK_MARK(256u);
+                    if (in_run && lds_run) {
+                        uint32_t s = usp;
+                        if (s >= 1u) V.set_wstack(s - 1u, T0);
+                        if (s >= 2u) V.set_wstack(s - 2u, T1);
+                        for (uint32_t k = 0; k < rlen; ++k) {
+                            const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
+                            const uint32_t rop = y & 0xffu;
+                            switch ((y >> 17) & 31u) {
+                            case K_PUSH:
+                                V.set_wstack(s, ld_word((const l_u4 *)s_push, upc + k));
+                                ++s;
+                                break;
+                            case K_DUP:
+                                V.set_wstack(s, V.wstack(s - (rop - 0x7fu)));
+                                ++s;
+                                break;
+                            case K_SWAP: {
+                                const uint32_t d = rop - 0x8fu;
+                                const U256 x = V.wstack(s - 1u), z = V.wstack(s - 1u - d);
+                                V.set_wstack(s - 1u, z);
+                                V.set_wstack(s - 1u - d, x);
+                                break;
+                            }
+                            case K_POP:
+                                --s;
+                                break;
+                            case K_ALU: {
+                                const U256 a = V.wstack(s - 1u);
+                                if (rop == 0x15u || rop == 0x19u) {        // ISZERO, NOT
+                                    V.set_wstack(s - 1u, alu(rop, a, a, a));
+                                } else {                                  // pop 2, push 1
+                                    const U256 b = V.wstack(s - 2u);
+                                    V.set_wstack(s - 2u, alu(rop, a, b, b));
+                                    --s;
+                                }
+                                break;
+                            }
+                            default:                                      // JUMPDEST
+                                break;
+                            }
+                        }
+                        T0 = s >= 1u ? V.wstack(s - 1u) : u_zero();
+                        T1 = s >= 2u ? V.wstack(s - 2u) : u_zero();
+                        sp = s;
+                        pc = upc + rlen; gmin += rg0; gmax += rg1; executed += rlen;
+                        FETCH();
+                    } else if (in_run) {
                         for (uint32_t k = 0; k < rlen; ++k) {
                             const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
                             const uint32_t rop = y & 0xffu;
@@ -1139,9 +1205,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (!(live && pd.y == uy)) continue;
 
         const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
-#ifdef MG_K1_CLOCKS
-        clk_bin = op;
-#endif
+        CLK_MARK(op);
         if (cov_on) {
             if (sflag) s_cov[pc] = 1;
             else cov[C.cov_off + pc] = 1;
@@ -1310,6 +1374,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth;
             }
         }
+        CLK_MARK(261u);
         if (live) FETCH();
     }
 #undef FETCH

@@ -751,6 +751,13 @@ static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_
     bytes = (size_t)win * slot_bytes + code_bytes + 16;
 }
 
+// MG_K1_RUNS=reg: straight-line runs in the register form only (A/B switch,
+// read per launch so one process can alternate the two forms)
+static uint32_t k1_flags() {
+    const char *r = getenv("MG_K1_RUNS");
+    return (r && std::string(r) == "reg") ? 0x100u : 0u;
+}
+
 static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
                        DevCounters *ctr, unsigned long long *prof = nullptr, uint32_t horizon = 0,
                        const DevResetImage *reset = nullptr) {
@@ -781,7 +788,7 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
                        m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
-                       loop_bound, reset ? *reset : DevResetImage{}, ctx->lpw);
+                       loop_bound, reset ? *reset : DevResetImage{}, ctx->lpw | k1_flags());
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }

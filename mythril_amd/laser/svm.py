@@ -450,11 +450,13 @@ class LaserEVM:
         regrow: List[GlobalState] = []
         self._recq, self._rec_seq, self._rec_bfs, self._rec_lanes = [], itertools.count(), bfs, lanes
 
+        sched = self._sched = _Schedule(lanes, b, bfs)
+
         def launch(run: List[int], horizon: int):
-            for ln in lanes:
-                if ln.dirty:
-                    dev.upload_range(b, ln.pos, 1)
-                    ln.dirty = False
+            for pos in sorted(sched.dirty):
+                dev.upload_range(b, pos, 1)
+                lanes[pos].dirty = False
+            sched.dirty.clear()
             st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
                           horizon=horizon)
             self.launches += 1
@@ -464,7 +466,7 @@ class LaserEVM:
                 dev.download_range(b, lo, cnt)
             self._collect_records(b, run)
             for i in run:
-                lanes[i].phase = "paused" if b.status[i] == MG_RUNNING else "event"
+                sched.set(i, "paused" if b.status[i] == MG_RUNNING else "event")
 
         launch(list(range(n)), 0)
         while True:
@@ -474,26 +476,24 @@ class LaserEVM:
                 left = [self._materialise(b, ln.pos, ln.state) for ln in lanes
                         if ln.phase != "done"]
                 return left
-            ev = _next_event(lanes, b, bfs)
-            paused = [ln.pos for ln in lanes if ln.phase == "paused"]
+            ev = sched.next_event()
             if single_step:
-                for i in paused:
+                for i in sorted(sched.paused):
                     ln = lanes[i]
                     self._materialise(b, i, ln.state)
                     self.work_list.append(ln.state)
-                    ln.phase = "done"
-                paused = []
-            if ev is None and not paused:
+                    sched.set(i, "done")
+            if ev is None and not sched.paused:
                 break
-            if paused:
+            if sched.paused:
                 if bfs:
                     # paused paths might have events at or before ev's round
-                    p_min = min(int(b.steps[i]) for i in paused)
+                    p_min = sched.paused_first()[0]
                     if ev is None or p_min <= _event_round(b, ev):
-                        launch(paused, 0 if ev is None else _event_round(b, ev) + 1)
+                        launch(sorted(sched.paused), 0 if ev is None else _event_round(b, ev) + 1)
                         continue
-                elif ev is None or max(paused) > ev:
-                    launch(paused, 0)           # DFS: the newest path runs on first
+                elif ev is None or -sched.paused_first()[0] > ev:
+                    launch(sorted(sched.paused), 0)     # DFS: the newest path runs on first
                     continue
             self._replay_records(lanes, self._event_key(b, ev))
             self._deliver(lanes[ev], b, final_states, track_gas, launch, regrow, single_step)
@@ -511,7 +511,7 @@ class LaserEVM:
         self._materialise(b, i, s)
         instrs = s.environment.code.instruction_list
         name = instrs[s.mstate.pc]["opcode"] if s.mstate.pc < len(instrs) else None
-        ln.phase = "done"
+        self._sched.set(i, "done")
         if self.record_coverage and status in (MG_HOOK, MG_ESCAPE) and name is not None:
             self._host_cov[s.environment.code.raw].add(s.mstate.pc)
 
@@ -549,24 +549,24 @@ class LaserEVM:
             b.steps[i] = steps
             b.flags[i] |= MG_LANE_HOOK_ACK | (MG_LANE_STEP1 if post else 0)
             if not post:
-                ln.phase, ln.dirty = "paused", True
+                self._sched.set(i, "paused"); self._sched.mark_dirty(i)
                 return
-            ln.dirty = True
+            self._sched.mark_dirty(i)
             snapshot = copy(pre_state)
             launch([i], steps + 1)
             st2 = int(b.status[i])
             b.flags[i] = int(b.flags[i]) & ~(MG_LANE_HOOK_ACK | MG_LANE_STEP1) & 0xFFFFFFFF
-            ln.dirty = True
+            self._sched.mark_dirty(i)
             executed = int(b.steps[i]) == steps + 1
             if st2 in _EXECUTED_HALTS:
                 if st2 == MG_HALT_DROPPED:
                     for hook in self.instr_post_hook.get(name, ()):
                         hook(snapshot)
-                ln.phase = "event"
+                self._sched.set(i, "event")
                 self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
                 return
             if not executed:      # escaped or cut by depth before running: its own event
-                ln.phase = "event"
+                self._sched.set(i, "event")
                 self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
                 return
             # the instruction's own registrations precede its post hooks
@@ -578,11 +578,11 @@ class LaserEVM:
             successors = [new]
             self._execute_post_hook(name, successors)
             if not successors:
-                ln.phase = "done"
+                self._sched.set(i, "done")
                 if track_gas:
                     final_states.append(snapshot)
                 return
-            ln.phase = "paused" if st2 == MG_RUNNING else "event"
+            self._sched.set(i, "paused" if st2 == MG_RUNNING else "event")
             return
 
         tx = s.current_transaction
@@ -710,6 +710,59 @@ def _event_round(b: LaneBatch, i: int) -> int:
     st = int(b.status[i])
     s = int(b.steps[i])
     return s - 1 if st in _EXECUTED_HALTS else s
+
+
+class _Schedule:
+    """Phases of one batch's lanes with O(log n) access to what the event loop
+    needs: the next event in the reference's order (BFS: smallest (round,
+    position); DFS: (-position, round)), the paused lanes (BFS: fewest
+    cumulative steps first; DFS: highest position first) and the lanes whose
+    host image changed.  Heaps with lazy deletion: an entry is valid while its
+    lane is still in that phase with the same key."""
+
+    def __init__(self, lanes: List[_Lane], b: LaneBatch, bfs: bool):
+        self.lanes, self.b, self.bfs = lanes, b, bfs
+        self._ev: List = []
+        self._pz: List = []
+        self.paused: set = set()
+        self.dirty: set = set()
+
+    def _key(self, pos: int):
+        r = _event_round(self.b, pos)
+        return (r, pos) if self.bfs else (-pos, r)
+
+    def _pkey(self, pos: int):
+        return (int(self.b.steps[pos]), pos) if self.bfs else (-pos,)
+
+    def set(self, pos: int, phase: str) -> None:
+        self.lanes[pos].phase = phase
+        self.paused.discard(pos)
+        if phase == "event":
+            heapq.heappush(self._ev, (self._key(pos), pos))
+        elif phase == "paused":
+            self.paused.add(pos)
+            heapq.heappush(self._pz, (self._pkey(pos), pos))
+
+    def mark_dirty(self, pos: int) -> None:
+        self.lanes[pos].dirty = True
+        self.dirty.add(pos)
+
+    def next_event(self) -> Optional[int]:
+        while self._ev:
+            key, pos = self._ev[0]
+            if self.lanes[pos].phase == "event" and key == self._key(pos):
+                return pos
+            heapq.heappop(self._ev)
+        return None
+
+    def paused_first(self):
+        """Key of the first paused lane: (steps, pos) under BFS, (-pos,) under DFS."""
+        while self._pz:
+            key, pos = self._pz[0]
+            if pos in self.paused and key == self._pkey(pos):
+                return key
+            heapq.heappop(self._pz)
+        return None
 
 
 def _next_event(lanes: List[_Lane], b: LaneBatch, bfs: bool) -> Optional[int]:

@@ -20,13 +20,13 @@ from mythril_amd import workloads  # noqa: E402
 from mythril_amd.device import GpuDevice  # noqa: E402
 from mythril_amd.lanes import bucket_order, permuted  # noqa: E402
 
-BINS = 260
+BINS = 262
 NAMES = {0x01: "ADD", 0x02: "MUL", 0x03: "SUB", 0x04: "DIV", 0x10: "LT", 0x11: "GT", 0x14: "EQ",
          0x15: "ISZERO", 0x16: "AND", 0x19: "NOT", 0x1C: "SHR", 0x20: "SHA3", 0x33: "CALLER",
          0x34: "CALLVALUE", 0x35: "CDLOAD", 0x36: "CDSIZE", 0x39: "CODECOPY", 0x50: "POP", 0x51: "MLOAD",
          0x52: "MSTORE", 0x54: "SLOAD", 0x55: "SSTORE", 0x56: "JUMP", 0x57: "JUMPI", 0x5B: "JUMPDEST",
          0xF3: "RETURN", 0xFD: "REVERT", 0x00: "STOP", 256: "runs", 257: "prologue", 258: "epilogue",
-         259: "idle-iter"}
+         259: "idle-iter", 260: "dispatch-head", 261: "fetch"}
 
 
 def name(b):
