@@ -48,6 +48,9 @@ def parse(argv=None):
                     help="function-manager record words per lane (0: registrations off)")
     ap.add_argument("--profile-only", action="store_true",
                     help="run warmup+steps with no JSON extras (for rocprofv3)")
+    ap.add_argument("--hooked-lanes", type=int, default=4096,
+                    help="lanes of the hooked-C2 field (0: off): C2 through LaserEVM with the "
+                         "default detection modules' opcode hooks registered")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
@@ -152,6 +155,10 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
     elapsed, total_steps = mdist.reduce_timing(elapsed, float(lane_steps))
     total_steps = int(total_steps)
 
+    hooked = None
+    if args.hooked_lanes and gpu:
+        hooked = run_hooked_c2(dev, args.hooked_lanes, rank)
+
     c4 = None
     if not args.no_c4:
         c4 = run_c4(args, dev, rank, world, barrier, dist_on)
@@ -191,9 +198,67 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
                 from oracle import cpu_baseline
                 c4["cpu_baseline"] = cpu_baseline.c4_evals(args.c4_models, args.cpu_seconds)
             out["constraint_evals"] = c4
+        if hooked is not None:
+            out["hooked_c2"] = hooked
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
+
+
+# the opcodes the default detection modules hook (union of
+# analysis/module/modules/*.py pre_hooks / post_hooks; pruner plugins add more)
+DEFAULT_MODULE_PRE = ["ADD", "MUL", "EXP", "SUB", "SSTORE", "SLOAD", "JUMP", "JUMPI", "STOP",
+                      "RETURN", "REVERT", "INVALID", "CALL", "CALLCODE", "DELEGATECALL", "STATICCALL",
+                      "CREATE", "CREATE2", "SELFDESTRUCT", "BLOCKHASH", "LOG1", "MSTORE"]
+DEFAULT_MODULE_POST = ["ORIGIN", "BLOCKHASH", "COINBASE", "GASLIMIT", "TIMESTAMP", "NUMBER", "CALL",
+                       "STATICCALL", "DELEGATECALL", "CALLCODE"]
+
+
+def run_hooked_c2(dev, n_lanes, rank):
+    """C2's lanes through the batched LaserEVM (host mirror, BFS) with a counting
+    hook on every opcode the default detection modules hook: how `myth analyze`
+    drives kernel 1.  Every hooked instruction yields the lane to the host,
+    which fires the hooks in the reference's order and resumes it.  Reports
+    lane-steps/s, hook events/s and the wall time split into device (kernel-1
+    launches) and host."""
+    from mythril_amd import workloads
+    from mythril_amd.laser import Account, Disassembly, LaserEVM, MessageCallTransaction, WorldState
+    from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
+    from mythril_amd.laser.transaction import _setup_global_state_for_execution
+    from mythril_amd.lanes import limbs_to_word
+
+    code = workloads.bytecode("overflow.sol.o")
+    b = workloads.c2_batch(n_lanes, seed=workloads.C2_SEED + 7 + rank)
+    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    events = [0]
+
+    def hook(_state):
+        events[0] += 1
+    laser.register_hooks("pre", {op: [hook] for op in DEFAULT_MODULE_PRE})
+    laser.register_hooks("post", {op: [hook] for op in DEFAULT_MODULE_POST})
+    dis = Disassembly(code)
+    for i in range(n_lanes):
+        ws = WorldState()
+        acct = Account(workloads.CONTRACT, code=dis, concrete_storage=True)
+        for k in range(int(b.storage_count[i])):
+            acct.storage.printable_storage[limbs_to_word(b.storage[i, k, :8])] = \
+                limbs_to_word(b.storage[i, k, 8:])
+        ws.put_account(acct)
+        tx = MessageCallTransaction(world_state=ws, callee_account=acct, caller=workloads.ATTACKER,
+                                    call_data=bytes(b.calldata[i, :int(b.calldata_len[i])]),
+                                    gas_price=1, gas_limit=8_000_000, origin=workloads.ATTACKER,
+                                    code=dis, call_value=0)
+        _setup_global_state_for_execution(laser, tx)
+    t0 = time.perf_counter()
+    laser.exec()
+    wall = time.perf_counter() - t0
+    dev_s = laser.device_ms / 1e3
+    return {"metric": "lane-steps/s with the default modules' hooks (kernel 1 + host LaserEVM)",
+            "lanes": n_lanes, "lane_steps": int(laser.lane_steps), "hook_events": events[0],
+            "launches": int(laser.launches), "wall_s": wall, "device_s": dev_s,
+            "host_s": wall - dev_s, "lane_steps_per_s": laser.lane_steps / wall,
+            "hook_events_per_s": events[0] / wall,
+            "hooked_opcodes": {"pre": DEFAULT_MODULE_PRE, "post": DEFAULT_MODULE_POST}}
 
 
 def run_c4(args, dev, rank, world, barrier, dist_on):

@@ -55,15 +55,13 @@ enum BvOp : uint32_t {
 #define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
 #define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
-#define BV_MPT_DEFAULT 2u     // models per thread (k_bv_eval<.., M>)
-#define BV_LDS_MAX (96u * 1024u)   // dynamic LDS a kernel-2 block may take
 
 struct BvState {
     uint32_t n_dags = 0, n_models = 0, n_vars = 0, n_slots = 0, n_consts = 0, n_tiles = 0, tile_cap = 0;
-    uint4 *timg = nullptr;           // tile images: per tile [its instructions][its constants x 2]
-    uint32_t *prog_off = nullptr;    // [n_dags + 1] instruction offsets (global numbering)
+    uint4 *insns = nullptr;          // [total]
+    uint32_t *prog_off = nullptr;    // [n_dags + 1]
     uint32_t *tile_dag = nullptr;    // [n_tiles + 1] first DAG of each tile
-    uint32_t *tile_img = nullptr;    // [n_tiles + 1] offset (uint4) of each tile image in timg
+    uint4 *consts = nullptr;         // [n_consts][2]
     uint4 *values = nullptr;         // [n_vars][n_models][2]
     uint32_t n_tables = 0, n_entries = 0;
     uint32_t *tab_start = nullptr;   // [n_tables][n_models]
@@ -75,11 +73,10 @@ struct BvState {
     unsigned long long *sat_bits = nullptr;   // [n_dags][bit_words] (mg_eval_bits)
     size_t cap_bits = 0;
     bool want_bits = false;
-    size_t cap_timg = 0, cap_dags = 0, cap_values = 0, cap_tiles = 0, cap_timgoff = 0;
+    size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
     size_t cap_entries = 0;
-    uint32_t mpt = BV_MPT_DEFAULT;   // models per thread (1, 2 or 4); MG_BV_MPT overrides
-    std::vector<uint32_t> h_tiles, h_timg_off;
-    std::vector<uint4> h_timg;
+    bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
+    std::vector<uint32_t> h_tiles;
 };
 
 DEV U256 bv_mask(U256 v, uint32_t width) {
@@ -121,9 +118,9 @@ struct BvTables {
 
 struct BvCtx {
     const uint4 *__restrict__ values;
-    const uint4 *consts;   // LDS: this tile's constants (2 x uint4 each)
-    uint4 *slots;          // LDS [n_slots][2][M][BV_BLOCK]
-    uint32_t n_models, tid;
+    const uint4 *__restrict__ consts;
+    uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
+    uint32_t n_models, model, tid;
     BvTables tab;
 };
 
@@ -136,14 +133,13 @@ DEV U256 ld2(const uint4 *p) {
 }
 
 // model interpretation lookup (entries are unique keys: first match wins)
-DEV U256 bv_table(BvTables tab, uint32_t n_models, uint32_t model, U256 k0, U256 k1,
-                                      uint32_t imm) {
+DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) {
     const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
-    const size_t tm = (size_t)t * n_models + model;
-    const uint32_t s0 = tab.start[tm], cnt = tab.count[tm];
-    U256 v = ld2(tab.dflt + tm * 4u + part * 2u);
+    const size_t tm = (size_t)t * c.n_models + c.model;
+    const uint32_t s0 = c.tab.start[tm], cnt = c.tab.count[tm];
+    U256 v = ld2(c.tab.dflt + tm * 4u + part * 2u);
     for (uint32_t k = 0; k < cnt; ++k) {
-        const uint4 *e = tab.entries + (size_t)(s0 + k) * 8u;
+        const uint4 *e = c.tab.entries + (size_t)(s0 + k) * 8u;
         if (u_eq(ld2(e), k0) && u_eq(ld2(e + 2), k1)) {
             v = ld2(e + 4 + part * 2u);
             break;
@@ -152,95 +148,36 @@ DEV U256 bv_table(BvTables tab, uint32_t n_models, uint32_t model, U256 k0, U256
     return lo ? u_shr_n(v, lo, 0u) : v;
 }
 
-// division-class ops (z3 semantics, division by zero included)
-DEV U256 bv_divop(uint32_t op, U256 A, U256 B, uint32_t width, uint32_t rc) {
-    switch (op) {
-    case BV_UDIV: return z_udiv(A, B);
-    case BV_UREM: return z_urem(A, B);
-    case BV_SDIV: return z_sdiv(bv_sext(A, width), bv_sext(B, width));
-    case BV_SREM: return z_srem(bv_sext(A, width), bv_sext(B, width));
-    case BV_SMOD: return z_smod(bv_sext(A, width), bv_sext(B, width));
-    default: {                     // BV_MUL_NOOVF_U: high w bits of the 2w-bit product are 0
-        bool ovf;
-        if (u_iszero(A) || u_iszero(B)) ovf = false;
-        else {
-            const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
-            ovf = u_lt(q, B);      // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
-        }
-        return u_small(!ovf);
-    }
-    }
-}
-
-// M models per thread: thread t of a block evaluates models
-// chunk_base + m * BV_BLOCK + t (m < M) with ONE instruction stream, so the
-// instruction fetch, decode and dispatch (scalar, wave-uniform) are paid once
-// for M evaluations.
-template <int M>
-DEV void bv_fetch(const BvCtx &c, const U256 (&acc)[M], uint32_t ref, const uint32_t (&model)[M],
-                  U256 (&out)[M]) {
+DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
-    if (kind == BV_REF_ACC) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) out[m] = acc[m];
-    } else if (kind == BV_REF_SLOT) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const uint4 x = c.slots[((idx * 2u) * M + m) * BV_BLOCK + c.tid];
-            const uint4 y = c.slots[((idx * 2u + 1u) * M + m) * BV_BLOCK + c.tid];
-            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
-            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
-        }
-    } else if (kind == BV_REF_VAR) {
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const size_t row = (size_t)idx * c.n_models + model[m];
-            const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
-            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
-            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
-        }
-    } else {
-        // constant: the tile's own pool, staged in LDS with its instructions
-        // (uniform address: a broadcast read), shared by the M models
-        const uint4 x = c.consts[2u * idx], y = c.consts[2u * idx + 1u];
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-            out[m].w[0] = x.x; out[m].w[1] = x.y; out[m].w[2] = x.z; out[m].w[3] = x.w;
-            out[m].w[4] = y.x; out[m].w[5] = y.y; out[m].w[6] = y.z; out[m].w[7] = y.w;
-        }
+    U256 r;
+    if (kind == BV_REF_ACC) return acc;
+    if (kind == BV_REF_SLOT) {
+        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid];
+        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid];
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        return r;
     }
+    if (kind == BV_REF_VAR) {
+        const size_t row = (size_t)idx * c.n_models + c.model;
+        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        return r;
+    }
+    // constant: uniform address -> scalar loads
+    const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
+    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    return r;
 }
 
-#define BV_FOR_M _Pragma("unroll") for (int m = 0; m < M; ++m)
-
-// Apply a large op (Knuth division, table scan) to the M models with ONE inlined
-// copy of its code: a rolled loop over m whose operands and result move through
-// static-index selects on the (uniform) loop counter, so nothing is dynamically
-// indexed (no scratch) and the code is not replicated M times.
-#define BV_ROLLED(EXPR)                                                        \
-    do {                                                                       \
-        if (M == 1) {                                                          \
-            const U256 a_ = A[0], b_ = B[0];                                   \
-            const uint32_t model_ = model[0];                                  \
-            r[0] = (EXPR);                                                     \
-            break;                                                             \
-        }                                                                      \
-        _Pragma("nounroll") for (int mm = 0; mm < M; ++mm) {                   \
-            U256 a_ = A[0], b_ = B[0];                                         \
-            uint32_t model_ = model[0];                                        \
-            _Pragma("unroll") for (int k = 1; k < M; ++k)                      \
-                if (k == mm) { a_ = A[k]; b_ = B[k]; model_ = model[k]; }      \
-            const U256 res_ = (EXPR);                                          \
-            _Pragma("unroll") for (int k = 0; k < M; ++k)                      \
-                if (k == mm) r[k] = res_;                                      \
-        }                                                                      \
-    } while (0)
-
-template <int M>
-__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ timg,
+template <bool kLdsProg>
+__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
-                                                      const uint32_t *__restrict__ tile_img,
+                                                      const uint4 *__restrict__ consts,
                                                       const uint4 *__restrict__ values, uint32_t n_models,
                                                       BvTables tab,
                                                       uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles,
@@ -251,12 +188,12 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                                                       unsigned long long *__restrict__ sat_bits,
                                                       uint32_t bit_words) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    // The tile image — the tile's programs followed by the constants they use,
-    // remapped to tile-local indices on the host (bv_upload) — is staged into LDS
-    // with one coalesced copy and read with broadcast ds_reads; constants never
-    // cost a dependent scalar load from a table that, at C4's 1M DAGs, is 1 GB.
-    uint4 *prog = smem;                          // [tile_cap]
-    uint4 *slots = smem + tile_cap;              // [n_slots][2][M][BV_BLOCK]
+    // kLdsProg: the program tile is staged in LDS and read with a broadcast
+    // ds_read + readfirstlane; otherwise instructions are read with scalar loads
+    // (uniform address -> s_load_dwordx4 through the scalar cache) and LDS only
+    // holds the register slots (higher occupancy)
+    uint4 *prog = smem;                          // [tile_cap] (kLdsProg)
+    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][BV_BLOCK]
     // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
@@ -266,132 +203,127 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
     const uint32_t d0 = max(tile_dag[tile], dag_lo), d1 = min(tile_dag[tile + 1], dag_hi);
     if (d0 >= d1) return;
     // the tile is read from HBM once per block and reused for every model chunk
+    const uint32_t i0 = prog_off[d0], i1 = prog_off[d1];
     // per-block results of the tile's DAGs: waves combine in LDS, the block adds
     // its totals to HBM once per DAG (not one atomic pair per wave per DAG)
     __shared__ uint32_t blk_cnt[BV_TILE_DAGS], blk_first[BV_TILE_DAGS];
     if (threadIdx.x < BV_TILE_DAGS) { blk_cnt[threadIdx.x] = 0u; blk_first[threadIdx.x] = 0xffffffffu; }
-    const uint32_t img0 = tile_img[tile], img_n = tile_img[tile + 1] - img0;
-    // a range-limited run (dag_lo/dag_hi) stages the whole tile: consts follow
-    // the tile's full instruction list
-    const uint32_t t_i0 = prog_off[tile_dag[tile]], t_n = prog_off[tile_dag[tile + 1]] - t_i0;
-    for (uint32_t i = threadIdx.x; i < img_n; i += BV_BLOCK) prog[i] = timg[img0 + i];
+    if (kLdsProg)
+        for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
     __syncthreads();
-    const uint4 *tconst = prog + t_n;
 
     const uint32_t tid = threadIdx.x;
-    constexpr uint32_t CHUNK = BV_BLOCK * (uint32_t)M;
-    const uint32_t n_chunks = (n_models + CHUNK - 1u) / CHUNK;
+    const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
     const uint32_t c_lo = group * chunks_per_block, c_hi = min(c_lo + chunks_per_block, n_chunks);
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-    uint32_t model[M];
-    bool live[M];
-    BV_FOR_M {
-        const uint32_t mm = chunk * CHUNK + (uint32_t)m * BV_BLOCK + tid;
-        live[m] = mm < n_models;
-        model[m] = live[m] ? mm : 0u;
-    }
-    const BvCtx c{values, tconst, slots, n_models, tid, tab};
+    const uint32_t model = chunk * BV_BLOCK + tid;
+    const bool live = model < n_models;
+    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid, tab};
 
     for (uint32_t d = d0; d < d1; ++d) {
-        const uint32_t p0 = prog_off[d] - t_i0, p1 = prog_off[d + 1] - t_i0;
-        U256 acc[M];
-        BV_FOR_M acc[m] = u_zero();
+        const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
+        U256 acc = u_zero();
         for (uint32_t p = p0; p < p1; ++p) {
-            const uint4 ins = prog[p];
-            const uint32_t w0 = uni(ins.x), ra = uni(ins.y), rb = uni(ins.z), rc = uni(ins.w);
+            uint32_t w0, ra, rb, rc;
+            if (kLdsProg) {
+                const uint4 ins = prog[p];
+                w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
+            } else {
+                const uint4 ins = insns[i0 + uni(p)];
+                w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
+            }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
-            U256 A[M], r[M];
-            bv_fetch<M>(c, acc, ra, model, A);
+            U256 A = bv_fetch(c, acc, ra);
+            U256 r;
             switch (op) {
-            case BV_COPY: BV_FOR_M r[m] = A[m]; break;
-            case BV_NOT: BV_FOR_M r[m] = u_not(A[m]); break;
-            case BV_NEG: BV_FOR_M r[m] = u_neg(A[m]); break;
-            case BV_BNOT: BV_FOR_M r[m] = u_small((A[m].w[0] & 1u) ^ 1u); break;
-            case BV_EXTRACT: BV_FOR_M r[m] = u_shr_n(A[m], rb & 0xffu, 0u); break;
-            case BV_ZEXT: BV_FOR_M r[m] = A[m]; break;
-            case BV_SEXT: BV_FOR_M r[m] = bv_sext(A[m], rb); break;
+            case BV_COPY: r = A; break;
+            case BV_NOT: r = u_not(A); break;
+            case BV_NEG: r = u_neg(A); break;
+            case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
+            case BV_EXTRACT: r = u_shr_n(A, rb & 0xffu, 0u); break;
+            case BV_ZEXT: r = A; break;
+            case BV_SEXT: r = bv_sext(A, rb); break;
             default: {
-                U256 B[M];
-                bv_fetch<M>(c, acc, rb, model, B);
+                U256 B = bv_fetch(c, acc, rb);
                 switch (op) {
-                case BV_ADD: BV_FOR_M r[m] = u_add(A[m], B[m]); break;
-                case BV_SUB: BV_FOR_M r[m] = u_sub(A[m], B[m]); break;
-                case BV_MUL: BV_FOR_M r[m] = u_mul(A[m], B[m]); break;
-                case BV_UDIV: case BV_UREM: case BV_SDIV: case BV_SREM: case BV_SMOD: case BV_MUL_NOOVF_U:
-                    BV_ROLLED(bv_divop(op, a_, b_, width, rc));
+                case BV_ADD: r = u_add(A, B); break;
+                case BV_SUB: r = u_sub(A, B); break;
+                case BV_MUL: r = u_mul(A, B); break;
+                case BV_UDIV: r = z_udiv(A, B); break;
+                case BV_UREM: r = z_urem(A, B); break;
+                case BV_SDIV: r = z_sdiv(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_SREM: r = z_srem(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_SMOD: r = z_smod(bv_sext(A, width), bv_sext(B, width)); break;
+                case BV_AND: r = u_and(A, B); break;
+                case BV_OR: r = u_or(A, B); break;
+                case BV_XOR: r = u_xor(A, B); break;
+                case BV_SHL: r = (u_fits32(B) && B.w[0] < width) ? u_shl_n(A, B.w[0]) : u_zero(); break;
+                case BV_LSHR: r = (u_fits32(B) && B.w[0] < width) ? u_shr_n(A, B.w[0], 0u) : u_zero(); break;
+                case BV_ASHR: {
+                    const U256 sa = bv_sext(A, width);
+                    const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
+                    const uint32_t sh = (u_fits32(B) && B.w[0] < width) ? B.w[0] : 255u;
+                    r = u_shr_n(sa, sh, fill);
                     break;
-                case BV_AND: BV_FOR_M r[m] = u_and(A[m], B[m]); break;
-                case BV_OR: BV_FOR_M r[m] = u_or(A[m], B[m]); break;
-                case BV_XOR: BV_FOR_M r[m] = u_xor(A[m], B[m]); break;
-                case BV_SHL:
-                    BV_FOR_M r[m] = (u_fits32(B[m]) && B[m].w[0] < width) ? u_shl_n(A[m], B[m].w[0]) : u_zero();
-                    break;
-                case BV_LSHR:
-                    BV_FOR_M r[m] = (u_fits32(B[m]) && B[m].w[0] < width) ? u_shr_n(A[m], B[m].w[0], 0u) : u_zero();
-                    break;
-                case BV_ASHR:
-                    BV_FOR_M {
-                        const U256 sa = bv_sext(A[m], width);
-                        const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
-                        const uint32_t sh = (u_fits32(B[m]) && B[m].w[0] < width) ? B[m].w[0] : 255u;
-                        r[m] = u_shr_n(sa, sh, fill);
-                    }
-                    break;
-                case BV_EQ: BV_FOR_M r[m] = u_small(u_eq(A[m], B[m])); break;
-                case BV_NE: BV_FOR_M r[m] = u_small(!u_eq(A[m], B[m])); break;
-                case BV_ULT: BV_FOR_M r[m] = u_small(u_lt(A[m], B[m])); break;
-                case BV_ULE: BV_FOR_M r[m] = u_small(!u_lt(B[m], A[m])); break;
-                case BV_UGT: BV_FOR_M r[m] = u_small(u_lt(B[m], A[m])); break;
-                case BV_UGE: BV_FOR_M r[m] = u_small(!u_lt(A[m], B[m])); break;
-                case BV_SLT: BV_FOR_M r[m] = u_small(u_slt(bv_sext(A[m], rc), bv_sext(B[m], rc))); break;
-                case BV_SLE: BV_FOR_M r[m] = u_small(!u_slt(bv_sext(B[m], rc), bv_sext(A[m], rc))); break;
-                case BV_SGT: BV_FOR_M r[m] = u_small(u_slt(bv_sext(B[m], rc), bv_sext(A[m], rc))); break;
-                case BV_SGE: BV_FOR_M r[m] = u_small(!u_slt(bv_sext(A[m], rc), bv_sext(B[m], rc))); break;
-                case BV_BAND: BV_FOR_M r[m] = u_small(A[m].w[0] & B[m].w[0] & 1u); break;
-                case BV_BOR: BV_FOR_M r[m] = u_small((A[m].w[0] | B[m].w[0]) & 1u); break;
-                case BV_BXOR: BV_FOR_M r[m] = u_small((A[m].w[0] ^ B[m].w[0]) & 1u); break;
-                case BV_BIMPLIES: BV_FOR_M r[m] = u_small(((A[m].w[0] & 1u) ^ 1u) | (B[m].w[0] & 1u)); break;
+                }
+                case BV_EQ: r = u_small(u_eq(A, B)); break;
+                case BV_NE: r = u_small(!u_eq(A, B)); break;
+                case BV_ULT: r = u_small(u_lt(A, B)); break;
+                case BV_ULE: r = u_small(!u_lt(B, A)); break;
+                case BV_UGT: r = u_small(u_lt(B, A)); break;
+                case BV_UGE: r = u_small(!u_lt(A, B)); break;
+                case BV_SLT: r = u_small(u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
+                case BV_SLE: r = u_small(!u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
+                case BV_SGT: r = u_small(u_slt(bv_sext(B, rc), bv_sext(A, rc))); break;
+                case BV_SGE: r = u_small(!u_slt(bv_sext(A, rc), bv_sext(B, rc))); break;
+                case BV_BAND: r = u_small(A.w[0] & B.w[0] & 1u); break;
+                case BV_BOR: r = u_small((A.w[0] | B.w[0]) & 1u); break;
+                case BV_BXOR: r = u_small((A.w[0] ^ B.w[0]) & 1u); break;
+                case BV_BIMPLIES: r = u_small(((A.w[0] & 1u) ^ 1u) | (B.w[0] & 1u)); break;
                 case BV_ITE: {
-                    U256 C[M];
-                    bv_fetch<M>(c, acc, rc, model, C);
-                    BV_FOR_M r[m] = u_select((A[m].w[0] & 1u) != 0u, B[m], C[m]);
+                    const U256 C = bv_fetch(c, acc, rc);
+                    r = u_select((A.w[0] & 1u) != 0u, B, C);
                     break;
                 }
-                case BV_CONCAT: BV_FOR_M r[m] = u_or(u_shl_n(A[m], rc), B[m]); break;
-                case BV_ADD_NOOVF_U:   // top bit of the (w+1)-bit sum is 0
-                    BV_FOR_M {
-                        const U256 s = u_add(A[m], B[m]);
-                        const bool ovf = rc >= 256u ? u_lt(s, A[m]) : !u_iszero(u_shr_n(s, rc, 0u));
-                        r[m] = u_small(!ovf);
+                case BV_CONCAT: r = u_or(u_shl_n(A, rc), B); break;
+                case BV_ADD_NOOVF_U: {  // top bit of the (w+1)-bit sum is 0
+                    const U256 s = u_add(A, B);
+                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_n(s, rc, 0u));
+                    r = u_small(!ovf);
+                    break;
+                }
+                case BV_MUL_NOOVF_U: {  // high w bits of the 2w-bit product are 0
+                    bool ovf;
+                    if (u_iszero(A) || u_iszero(B)) ovf = false;
+                    else {
+                        const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
+                        ovf = u_lt(q, B);   // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
                     }
+                    r = u_small(!ovf);
                     break;
-                case BV_SUB_NOUDF_U: BV_FOR_M r[m] = u_small(!u_lt(A[m], B[m])); break;
-                case BV_TAB: BV_ROLLED(bv_table(c.tab, n_models, model_, a_, b_, rc)); break;
-                default: BV_FOR_M r[m] = u_zero(); break;
+                }
+                case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
+                case BV_TAB: r = bv_table(c, A, B, rc); break;
+                default: r = u_zero(); break;
                 }
             }
             }
-            if (width < 256u) { BV_FOR_M r[m] = bv_mask(r[m], width); }
-            BV_FOR_M acc[m] = r[m];
+            r = bv_mask(r, width);
+            acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;
-                BV_FOR_M {
-                    slots[((ds * 2u) * M + m) * BV_BLOCK + tid] = make_uint4(r[m].w[0], r[m].w[1], r[m].w[2], r[m].w[3]);
-                    slots[((ds * 2u + 1u) * M + m) * BV_BLOCK + tid] = make_uint4(r[m].w[4], r[m].w[5], r[m].w[6], r[m].w[7]);
-                }
+                slots[(ds * 2u) * BV_BLOCK + tid] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+                slots[(ds * 2u + 1u) * BV_BLOCK + tid] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
             }
         }
-        BV_FOR_M {
-            const bool sat = live[m] && (acc[m].w[0] & 1u);
-            const uint64_t bal = __ballot(sat);
-            if ((tid & 63u) == 0u && bal) {
-                const uint32_t base = chunk * CHUNK + (uint32_t)m * BV_BLOCK + tid;   // tid % 64 == 0
-                // optional per-model bitmap (one u64 per wave): lets the host replay
-                // sequential check_quick_sat calls whose LRU bumps reorder the pool
-                if (sat_bits) sat_bits[(size_t)d * bit_words + (base >> 6)] = bal;
-                atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
-                atomicMin(&blk_first[d - d0], base + (uint32_t)(__ffsll((long long)bal) - 1));
-            }
+        const bool sat = live && (acc.w[0] & 1u);
+        const uint64_t bal = __ballot(sat);
+        if ((tid & 63u) == 0u && bal) {
+            // optional per-model bitmap (one u64 per wave): lets the host replay
+            // sequential check_quick_sat calls whose LRU bumps reorder the pool
+            if (sat_bits) sat_bits[(size_t)d * bit_words + ((chunk * BV_BLOCK + tid) >> 6)] = bal;
+            atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
+            atomicMin(&blk_first[d - d0], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
         }
     }
     }
@@ -417,7 +349,7 @@ static int bv_ensure(T *&p, size_t &cap, size_t need) {
 }
 
 static void bv_free(BvState &s) {
-    hipFree(s.timg); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.tile_img);
+    hipFree(s.insns); hipFree(s.prog_off); hipFree(s.tile_dag); hipFree(s.consts);
     hipFree(s.values); hipFree(s.first_sat); hipFree(s.sat_count);
     hipFree(s.tab_start); hipFree(s.tab_count); hipFree(s.tab_entries); hipFree(s.tab_default);
     hipFree(s.sat_bits);
@@ -459,102 +391,27 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
             }
         }
     }
-    // Tiles: consecutive DAGs (at most BV_TILE_DAGS) whose tile image fits the LDS
-    // tile: their instructions plus every constant they use, each constant once
-    // per tile, operand refs rewritten to tile-local constant indices.
-    const size_t slots_b1 = (size_t)std::max<uint32_t>(dags->n_slots, 1) * 2u * BV_BLOCK * sizeof(uint4);
-    const uint32_t img_max = (uint32_t)((BV_LDS_MAX - slots_b1) / sizeof(uint4));
-    auto nrefs = [](uint32_t op) -> int {
-        return (op == BV_ITE) ? 3 : (op == BV_COPY || op == BV_NOT || op == BV_NEG || op == BV_BNOT ||
-                                      op == BV_EXTRACT || op == BV_ZEXT || op == BV_SEXT) ? 1 : 2;
-    };
-    std::vector<uint32_t> stamp(std::max<uint32_t>(dags->n_consts, 1), 0xffffffffu);
-    std::vector<uint32_t> local(std::max<uint32_t>(dags->n_consts, 1), 0u);
-    // per DAG: its own distinct constants (image size alone) -> tile capacity
+    // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
+    // LDS tile capacity: the longest program rounded up, at least BV_TILE_MIN, so
+    // short-program batches keep a small LDS footprint (higher occupancy)
     uint32_t longest = 0;
+    for (uint32_t d = 0; d < n; ++d) longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d]);
+    s.tile_cap = std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u);
+    s.h_tiles.clear();
+    s.h_tiles.push_back(0);
+    uint32_t acc = 0;
     for (uint32_t d = 0; d < n; ++d) {
-        uint32_t uc = 0;
-        for (uint32_t i = dags->prog_off[d]; i < dags->prog_off[d + 1]; ++i) {
-            const uint32_t *w = dags->insns + 4 * (size_t)i;
-            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
-                if ((w[1 + k] >> 30) == BV_REF_CONST) {
-                    const uint32_t g = w[1 + k] & 0x3fffffffu;
-                    if (stamp[g] != d) { stamp[g] = d; ++uc; }
-                }
-        }
-        longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d] + 2u * uc);
+        const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
+        if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= BV_TILE_DAGS) { s.h_tiles.push_back(d); acc = 0; }
+        acc += len;
     }
-    if (longest > img_max) { msg = "program plus its constants exceed the LDS tile"; return MG_EINVAL; }
-    s.tile_cap = std::min(img_max, std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u));
-    std::fill(stamp.begin(), stamp.end(), 0xffffffffu);
-    s.h_tiles.assign(1, 0u);
-    s.h_timg_off.assign(1, 0u);
-    s.h_timg.clear();
-    s.h_timg.reserve((size_t)total * 2);
-    std::vector<uint32_t> tconsts;          // global indices of the current tile's constants
-    uint32_t tile_id = 0, t_insns = 0;
-    auto close_tile = [&](uint32_t d_end) {
-        for (uint32_t g : tconsts) {
-            const uint32_t *c = dags->consts + 8 * (size_t)g;
-            s.h_timg.push_back(make_uint4(c[0], c[1], c[2], c[3]));
-            s.h_timg.push_back(make_uint4(c[4], c[5], c[6], c[7]));
-        }
-        s.h_tiles.push_back(d_end);
-        s.h_timg_off.push_back((uint32_t)s.h_timg.size());
-        tconsts.clear();
-        t_insns = 0;
-        ++tile_id;
-    };
-    for (uint32_t d = 0; d < n; ++d) {
-        const uint32_t a = dags->prog_off[d], b = dags->prog_off[d + 1];
-        uint32_t fresh = 0;                 // constants this DAG adds to the tile
-        for (uint32_t i = a; i < b; ++i) {
-            const uint32_t *w = dags->insns + 4 * (size_t)i;
-            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
-                if ((w[1 + k] >> 30) == BV_REF_CONST) {
-                    const uint32_t g = w[1 + k] & 0x3fffffffu;
-                    if (stamp[g] != tile_id && local[g] != 0xfffffffeu) { local[g] = 0xfffffffeu; ++fresh; }
-                }
-        }
-        for (uint32_t i = a; i < b; ++i) {          // undo the counting marks
-            const uint32_t *w = dags->insns + 4 * (size_t)i;
-            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
-                if ((w[1 + k] >> 30) == BV_REF_CONST && local[w[1 + k] & 0x3fffffffu] == 0xfffffffeu)
-                    local[w[1 + k] & 0x3fffffffu] = 0u;
-        }
-        if (d > s.h_tiles.back() &&
-            (t_insns + (b - a) + 2u * ((uint32_t)tconsts.size() + fresh) > s.tile_cap ||
-             d - s.h_tiles.back() >= BV_TILE_DAGS)) {
-            close_tile(d);
-            // the new tile's image starts with this DAG: instructions come first,
-            // so move nothing -- images are built tile by tile below
-        }
-        for (uint32_t i = a; i < b; ++i) {
-            const uint32_t *w = dags->insns + 4 * (size_t)i;
-            uint32_t x[4] = {w[0], w[1], w[2], w[3]};
-            for (int k = 0; k < nrefs(w[0] & 0xffu); ++k)
-                if ((x[1 + k] >> 30) == BV_REF_CONST) {
-                    const uint32_t g = x[1 + k] & 0x3fffffffu;
-                    if (stamp[g] != tile_id) {
-                        stamp[g] = tile_id;
-                        local[g] = (uint32_t)tconsts.size();
-                        tconsts.push_back(g);
-                    }
-                    x[1 + k] = (BV_REF_CONST << 30) | local[g];
-                }
-            s.h_timg.push_back(make_uint4(x[0], x[1], x[2], x[3]));
-        }
-        t_insns += b - a;
-    }
-    close_tile(n);
-    s.h_tiles.pop_back();                         // close_tile pushed n: keep one n at the end
     s.h_tiles.push_back(n);
     s.n_tiles = (uint32_t)s.h_tiles.size() - 1;
     int rc = 0;
-    if ((rc = bv_ensure(s.timg, s.cap_timg, s.h_timg.size()))) { msg = "alloc tile images"; return rc; }
+    if ((rc = bv_ensure(s.insns, s.cap_insns, total))) { msg = "alloc insns"; return rc; }
     if ((rc = bv_ensure(s.prog_off, s.cap_dags, (size_t)n + 1))) { msg = "alloc offsets"; return rc; }
     if ((rc = bv_ensure(s.tile_dag, s.cap_tiles, s.h_tiles.size()))) { msg = "alloc tiles"; return rc; }
-    if ((rc = bv_ensure(s.tile_img, s.cap_timgoff, s.h_timg_off.size()))) { msg = "alloc tile offsets"; return rc; }
+    if ((rc = bv_ensure(s.consts, s.cap_consts, (size_t)std::max<uint32_t>(dags->n_consts, 1) * 2))) { msg = "alloc consts"; return rc; }
     if ((rc = bv_ensure(s.values, s.cap_values, (size_t)std::max<uint32_t>(models->n_vars, 1) * models->n_models * 2))) { msg = "alloc values"; return rc; }
     if (models->n_tables) {
         if (!models->tab_start || !models->tab_count || !models->tab_default ||
@@ -582,10 +439,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         return MG_ENOMEM;
     }
     hipError_t e = hipSuccess;
-    e = e ? e : hipMemcpyAsync(s.timg, s.h_timg.data(), s.h_timg.size() * 16, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.insns, dags->insns, (size_t)total * 16, hipMemcpyHostToDevice, st);
     e = e ? e : hipMemcpyAsync(s.prog_off, dags->prog_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st);
     e = e ? e : hipMemcpyAsync(s.tile_dag, s.h_tiles.data(), s.h_tiles.size() * 4, hipMemcpyHostToDevice, st);
-    e = e ? e : hipMemcpyAsync(s.tile_img, s.h_timg_off.data(), s.h_timg_off.size() * 4, hipMemcpyHostToDevice, st);
+    if (dags->n_consts) e = e ? e : hipMemcpyAsync(s.consts, dags->consts, (size_t)dags->n_consts * 32, hipMemcpyHostToDevice, st);
     if (models->n_vars)
         e = e ? e : hipMemcpyAsync(s.values, models->values, (size_t)models->n_vars * models->n_models * 32, hipMemcpyHostToDevice, st);
     if (models->n_tables) {
@@ -600,14 +457,8 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     e = e ? e : hipStreamSynchronize(st);
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
     s.n_tables = models->n_tables; s.n_entries = models->n_entries;
-    const char *mv = getenv("MG_BV_MPT");
-    s.mpt = mv ? (uint32_t)atoi(mv) : BV_MPT_DEFAULT;
-    if (s.mpt != 1u && s.mpt != 2u && s.mpt != 4u) s.mpt = BV_MPT_DEFAULT;
-    // a pool smaller than one block of threads gains nothing from more models per thread
-    while (s.mpt > 1u && (size_t)models->n_models <= (size_t)BV_BLOCK * (s.mpt / 2u)) s.mpt /= 2u;
-    // LDS per block (program tile + M register slots per thread) within BV_LDS_MAX
-    const size_t slots_b = (size_t)std::max<uint32_t>(dags->n_slots, 1) * 2u * BV_BLOCK * sizeof(uint4);
-    while (s.mpt > 1u && (size_t)s.tile_cap * sizeof(uint4) + slots_b * s.mpt > BV_LDS_MAX) s.mpt /= 2u;
+    const char *pv = getenv("MG_BV_PROG");
+    s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;
@@ -635,22 +486,17 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t tiles_pad = (nt + 7u) & ~7u;
     // model chunks per block: as many as keep >= BV_GROUP_TARGET blocks in flight,
     // so each program tile is staged once per block instead of once per chunk
-    const uint32_t chunk_models = BV_BLOCK * s.mpt;
-    const uint32_t chunks = (s.n_models + chunk_models - 1) / chunk_models;
+    const uint32_t chunks = (s.n_models + BV_BLOCK - 1) / BV_BLOCK;
     const uint32_t groups_wanted = std::max<uint32_t>(1u, (BV_GROUP_TARGET + tiles_pad - 1u) / tiles_pad);
     const uint32_t cpb = std::max<uint32_t>(1u, chunks / std::min(groups_wanted, chunks));
     const uint32_t groups = (chunks + cpb - 1u) / cpb;
     const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
-    const size_t lds = ((size_t)s.tile_cap + (size_t)s.n_slots * 2 * BV_BLOCK * s.mpt) * sizeof(uint4);
-    auto kern = s.mpt == 4u ? k_bv_eval<4> : s.mpt == 2u ? k_bv_eval<2> : k_bv_eval<1>;
-    if (lds > 65536u) {
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)BV_LDS_MAX);
-        (void)hipGetLastError();
-    }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
-                       s.timg, s.prog_off, s.tile_dag, s.tile_img,
-                       s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
+    const bool lds_prog = s.lds_prog;
+    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
+    hipLaunchKernelGGL(lds_prog ? k_bv_eval<true> : k_bv_eval<false>, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
+                       s.insns, s.prog_off, s.tile_dag,
+                       s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
                        s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,
                        s.tile_cap, cpb, s.first_sat, s.sat_count, s.want_bits ? s.sat_bits : nullptr, bit_words);
     e = hipGetLastError();

@@ -378,7 +378,7 @@ struct StepEnv {
     const uint8_t *a8;
     const uint32_t *a32;
     l_u4 *s_win;
-    const uint2 *s_pd;
+    const uint4 *s_pd;     // pre-decoded code: x, y = decode words, z, w = run table
     const uint4 *s_push;
     uint32_t *s_prof;
     uint32_t *s_kc;      // this wave's Keccak cache (KC_WAVE words)
@@ -865,9 +865,12 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // (MG_K1_RUNS=reg, for A/B runs against the LDS-resident form)
     const uint32_t lpw = lpw_flags & 0xffu;
     const bool lds_runs_on = (lpw_flags & 0x100u) == 0u;
-    // Dynamic LDS: [stack window: win x 2 x lanes-per-block x 16 B][pre-decoded code: pd_cap x 8 B]
-    //              [runs: pd_cap x 8 B][push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B]
-    //              [coverage: pd_cap]
+    // Dynamic LDS: [stack window: win x 2 x lanes-per-block x 16 B]
+    //              [pre-decoded code: pd_cap x 16 B: decode x, y | run table z, w]
+    //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
+    // One ds_read_b128 at FETCH brings a lane both its next instruction's decode
+    // and the straight-line run starting there, so the dispatch head reads the
+    // lead lane's run with v_readlane instead of another dependent LDS read.
     extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
     l_u4 *s_win = (l_u4 *)dyn;
     // Lanes per wave (`lpw` = 64, 32 or 16, launch-uniform): each wave holds lpw
@@ -878,9 +881,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // lanes diverge less).  The idle threads still take part in the wave-wide
     // LDS load of a run's pre-decoded words below.
     const uint32_t lanes_pb = (LANE_BLOCK / 64u) * lpw;
-    uint2 *s_pd = reinterpret_cast<uint2 *>(dyn + (size_t)win * 2u * lanes_pb);
-    uint2 *s_run = s_pd + pd_cap;
-    uint4 *s_push = reinterpret_cast<uint4 *>(s_run + pd_cap);
+    uint4 *s_pd = dyn + (size_t)win * 2u * lanes_pb;
+    uint4 *s_push = s_pd + pd_cap;
     uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + 2u * pd_cap);
     uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_jr + jr_cap);
     __shared__ uint2 s_dec[256];
@@ -939,11 +941,11 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 const uint2 d = kDec[op];
                 const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
                 const uint32_t hook = (uint32_t)((hm >> (op & 63u)) & 1ull);
-                s_pd[i] = make_uint2(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook));
-                s_run[i] = make_uint2(a32[BC.run_off + 2u * i], a32[BC.run_off + 2u * i + 1u]);
+                s_pd[i] = make_uint4(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook),
+                                     a32[BC.run_off + 2u * i], a32[BC.run_off + 2u * i + 1u]);
                 s_cov[i] = 0;
             }
-            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);
+            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint4(0u, ((uint32_t)K_END << 17) | PD_SPECIAL, 0u, 0u);
             const uint4 *gpu4 = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
             for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gpu4[i];
             staged = true;
@@ -973,6 +975,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     uint64_t txlim = 0, glim = 0, gmin = 0, gmax = 0;
     U256 T0 = u_zero(), T1 = u_zero();
     uint2 pd = make_uint2(0u, 0u);
+    uint2 prun = make_uint2(0u, 0u);   // run table entry at pc (staged code only)
     bool live = false;
     if (run0) {
         C = codes[my_code];
@@ -1007,7 +1010,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // hooked opcode, this launch's step budget, host-only opcode.
 #define FETCH() do {                                                                      \
         if (sflag) {                                                                      \
-            pd = s_pd[pc];                    /* s_pd[n_instr] is the END sentinel */     \
+            const uint4 q_ = s_pd[pc];        /* s_pd[n_instr] is the END sentinel */     \
+            pd = make_uint2(q_.x, q_.y); prun = make_uint2(q_.z, q_.w);                   \
         } else if (pc >= C.n_instr) {                                                     \
             pd = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);                    \
         } else {                                                                          \
@@ -1064,12 +1068,14 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (runs_on) {
             uint32_t upc = __builtin_amdgcn_readlane(pc, lead);
             asm volatile("" : "+s"(upc));
-            const uint2 ri = s_run[upc];
-            const uint32_t rx = __builtin_amdgcn_readfirstlane(ri.x);
-            const uint32_t ry = __builtin_amdgcn_readfirstlane(ri.y);
+            // the lead's run entry came with its FETCH (prun): no LDS round trip here
+            const uint32_t rx = __builtin_amdgcn_readlane(prun.x, lead);
+            const uint32_t ry = __builtin_amdgcn_readlane(prun.y, lead);
             const uint32_t rlen = rx & 0xffu;
             if (rlen >= 2u) {
                 const uint32_t rneed = (rx >> 8) & 0xffu, rpeak = (rx >> 16) & 0xffu;
+                // a run may end with a JUMP (rjk 1) or JUMPI (2): rsimple plain steps first
+                const uint32_t rjk = (rx >> 24) & 3u, rsimple = rjk ? rlen - 1u : rlen;
                 const uint32_t rg0 = ry & 0xffffu, rg1 = ry >> 16;
                 // LDS-resident form: when the lead lane's whole run stays inside the
                 // LDS stack window, the lanes at the lead's pc AND stack depth run it
@@ -1097,7 +1103,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                         uint32_t s = usp;
                         if (s >= 1u) V.set_wstack(s - 1u, T0);
                         if (s >= 2u) V.set_wstack(s - 2u, T1);
-                        for (uint32_t k = 0; k < rlen; ++k) {
+                        for (uint32_t k = 0; k < rsimple; ++k) {
                             const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
                             const uint32_t rop = y & 0xffu;
                             switch ((y >> 17) & 31u) {
@@ -1134,13 +1140,36 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                 break;
                             }
                         }
-                        T0 = s >= 1u ? V.wstack(s - 1u) : u_zero();
-                        T1 = s >= 2u ? V.wstack(s - 2u) : u_zero();
-                        sp = s;
-                        pc = upc + rlen; gmin += rg0; gmax += rg1; executed += rlen;
+                        // the closing jump (instructions.py:1520-1636), per lane: a lane
+                        // whose jump would raise or drop its path stops AT the jump and
+                        // the single-instruction path runs it (exceptions, drops)
+                        uint32_t nsp = s, npc = upc + rsimple, nexec = executed + rsimple;
+                        uint32_t jg = 0u;
+                        if (rjk) {
+                            const U256 tgt = V.wstack(s - 1u);
+                            const bool take = rjk == 1u || !u_iszero(V.wstack(s - 2u));
+                            uint32_t idx = MG_JRES_NONE;
+                            if (take && u_fits32(tgt) && tgt.w[0] < C.n_jres) {
+                                if (jflag) { idx = s_jr[tgt.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
+                                else idx = a32[C.jres_off + tgt.w[0]];
+                            }
+                            if (!take || (idx != MG_JRES_NONE && (s_pd[idx].y & 0xffu) == 0x5bu)) {
+                                nsp = s - rjk;
+                                npc = take ? idx : upc + rlen;
+                                nexec = executed + rlen;
+                                jg = rjk == 1u ? 8u : 10u;      // added by hand, no OOG check
+                                if (rjk == 2u) ++depth;
+                            }
+                        }
+                        T0 = nsp >= 1u ? V.wstack(nsp - 1u) : u_zero();
+                        T1 = nsp >= 2u ? V.wstack(nsp - 2u) : u_zero();
+                        sp = nsp;
+                        pc = npc; gmin += rg0 + jg; gmax += rg1 + jg; executed = nexec;
                         FETCH();
                     } else if (in_run) {
-                        for (uint32_t k = 0; k < rlen; ++k) {
+                        // register form: the plain steps only; a closing jump runs as
+                        // its own dispatch
+                        for (uint32_t k = 0; k < rsimple; ++k) {
                             const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
                             const uint32_t rop = y & 0xffu;
                             switch ((y >> 17) & 31u) {
@@ -1186,7 +1215,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                 break;
                             }
                         }
-                        pc = upc + rlen; gmin += rg0; gmax += rg1; executed += rlen;
+                        pc = upc + rsimple; gmin += rg0; gmax += rg1; executed += rsimple;
                         FETCH();
                     }
                     if (cov_on) {

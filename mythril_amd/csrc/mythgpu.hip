@@ -325,13 +325,15 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
     }
     // straight-line runs (kernel 1's block path): from every instruction, the
     // run of simple opcodes (PUSH/DUP/SWAP/POP/JUMPDEST/fast ALU) that follows,
-    // at most RUN_MAX long, with the stack depth it needs, the growth it peaks
-    // at and its table gas, so a lane can check once and execute the run
-    // without per-instruction checks (lane_step.cuh).
+    // at most RUN_MAX long, optionally ended by one JUMP or JUMPI, with the stack
+    // depth it needs, the growth it peaks at and the table gas of its simple
+    // part (jumps add their 8 / 10 by hand), so a lane can check once and
+    // execute the run without per-instruction checks (lane_step.cuh).
+    // rx = len | need << 8 | peak << 16 | jump kind << 24 (1 JUMP, 2 JUMPI).
     {
         const size_t ni = ops.size();
         std::vector<uint32_t> rx(ni + 1, 0u), ry(ni + 1, 0u);
-        std::vector<int> need(ni + 1, 0), peak(ni + 1, 0), len(ni + 1, 0);
+        std::vector<int> need(ni + 1, 0), peak(ni + 1, 0), len(ni + 1, 0), jk(ni + 1, 0);
         std::vector<uint32_t> g0(ni + 1, 0u), g1(ni + 1, 0u);
         for (size_t i = ni; i-- > 0;) {
             const uint32_t b = ops[i];
@@ -344,14 +346,26 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
             else if (b == 0x15 || b == 0x19) { req = 1; d = 0; }
             else if (b <= 0x03 && b >= 0x01) { req = 2; d = -1; }
             else if (b == 0x0b || (b >= 0x10 && b <= 0x1d)) { req = 2; d = -1; }
+            if (b == 0x56 || b == 0x57) {               // a jump ends the run it closes
+                len[i] = 1;
+                need[i] = b == 0x56 ? 1 : 2;
+                peak[i] = 0;
+                jk[i] = b == 0x56 ? 1 : 2;
+                g0[i] = g1[i] = 0u;
+                rx[i] = 1u | ((uint32_t)need[i] << 8) | ((uint32_t)jk[i] << 24);
+                ry[i] = 0u;
+                continue;
+            }
             if (req < 0) continue;                      // not simple: runs end here
             const bool cont = len[i + 1] > 0 && len[i + 1] < RUN_MAX;
             len[i] = 1 + (cont ? len[i + 1] : 0);
             need[i] = std::max(req, (cont ? need[i + 1] : 0) - d);
             peak[i] = std::max(0, d + (cont ? peak[i + 1] : 0));
+            jk[i] = cont ? jk[i + 1] : 0;
             g0[i] = t[b].gmin + (cont ? g0[i + 1] : 0u);
             g1[i] = t[b].gmax + (cont ? g1[i + 1] : 0u);
-            rx[i] = (uint32_t)len[i] | ((uint32_t)need[i] << 8) | ((uint32_t)peak[i] << 16);
+            rx[i] = (uint32_t)len[i] | ((uint32_t)need[i] << 8) | ((uint32_t)peak[i] << 16) |
+                    ((uint32_t)jk[i] << 24);
             ry[i] = g0[i] | (g1[i] << 16);
         }
         dc.run_off = (uint32_t)ctx->a32.size();

@@ -147,6 +147,11 @@ def execute_message_calls(laser_evm, callee_address, caller_address, origin_addr
     rank, world = mdist.rank_world()
     open_states = laser_evm.open_states[:]
     del laser_evm.open_states[:]
+    if getattr(laser_evm, "use_reachability_check", False):
+        # svm.py:244-249: a transaction starts only from open states whose path
+        # constraints are possible (kernel-2 quick-sat, then the SMT backend)
+        from ..smt.solver import Constraints
+        open_states = [ws for ws in open_states if Constraints(ws.constraints).is_possible()]
     local = [(ws, d) for ws in open_states for d in datas]
     if world > 1 and not getattr(laser_evm, "_sharded", False):
         # replicated start: deal pair g to rank g % world

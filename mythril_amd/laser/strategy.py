@@ -101,3 +101,44 @@ class BoundedLoopsStrategy(BasicSearchStrategy):
             count += 1
             j -= size
         return count
+
+
+class DelayConstraintStrategy(BasicSearchStrategy):
+    """constraint_strategy.py:19-47: a state whose path constraints no cached
+    model satisfies (``check_quick_sat`` on the strategy's OWN ModelCache —
+    kernel 2) is parked; parked states run only once the work list is empty,
+    each after ``Constraints.get_model`` (global cache, then the SMT backend)
+    finds it a model, which then joins the strategy's cache.  States pop in
+    work-list order (``pop(0)``).  Batched form: ``drain`` returns every
+    runnable state at once in that order, or the first parked state that gets
+    a model; the quick-sat checks of one drain go to the device in ONE
+    kernel-2 launch (``check_quick_sat_many`` replays them in order)."""
+
+    order = "bfs"
+
+    def __init__(self, work_list, max_depth, **kwargs):
+        super().__init__(work_list, max_depth)
+        from ..smt.solver import ModelCache
+        self.model_cache = ModelCache(device=kwargs.get("device"))
+        self.pending_worklist: List = []
+
+    def drain(self) -> List:
+        from ..smt.expr import And
+        from ..smt.solver import Constraints
+        states = [s for s in self.work_list if s.mstate.depth < self.max_depth]
+        del self.work_list[:]
+        if states:
+            queries = [And(*s.world_state.constraints).raw for s in states]
+            verdicts = self.model_cache.check_quick_sat_many(queries)
+            run = []
+            for s, v in zip(states, verdicts):
+                (run if v is not False else self.pending_worklist).append(s)
+            if run:
+                return run
+        while self.pending_worklist:
+            s = self.pending_worklist.pop(0)
+            model = Constraints(s.world_state.constraints).get_model()
+            if model is not None:
+                self.model_cache.put(model, 1)
+                return [s]
+        return []

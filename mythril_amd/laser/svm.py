@@ -36,6 +36,7 @@ import heapq
 import itertools
 import logging
 import os
+import random
 from collections import defaultdict
 from copy import copy
 from datetime import datetime, timedelta
@@ -53,6 +54,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import symbol_factory
 from ..smt.keccak_manager import keccak_function_manager
+from ..smt.solver import Constraints, args
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
@@ -90,6 +92,7 @@ class LaserEVM:
         self.use_reachability_check = use_reachability_check
 
         self.work_list: List[GlobalState] = []
+        self.device_ms = 0.0            # kernel-1 time of every launch exec() issued
         self.strategy = strategy(self.work_list, max_depth, beam_width=beam_width)
         self.max_depth = max_depth
         self.transaction_count = transaction_count
@@ -453,13 +456,15 @@ class LaserEVM:
         sched = self._sched = _Schedule(lanes, b, bfs)
 
         def launch(run: List[int], horizon: int):
-            for pos in sorted(sched.dirty):
-                dev.upload_range(b, pos, 1)
-                lanes[pos].dirty = False
+            for lo, cnt in _ranges(sorted(sched.dirty)):       # contiguous runs: one copy each
+                dev.upload_range(b, lo, cnt)
+                for pos in range(lo, lo + cnt):
+                    lanes[pos].dirty = False
             sched.dirty.clear()
             st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
                           horizon=horizon)
             self.launches += 1
+            self.device_ms += st.kernel_ms
             self.lane_steps += st.lane_steps
             self.total_states += st.lane_steps      # one successor per executed step
             for lo, cnt in _ranges(run):
@@ -635,6 +640,12 @@ class LaserEVM:
                 log.debug("Encountered unimplemented instruction %s", name)
                 return              # svm.py:314-316: NotImplementedError -> continue
             new_states = self.escape_handler(s)
+            if self.strategy.run_check() and (
+                    len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
+                # svm.py:319-326: a fork keeps the successors whose path
+                # constraints are possible (kernel-2 quick-sat, then the backend)
+                new_states = [st for st in new_states
+                              if Constraints(st.world_state.constraints).is_possible()]
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
             if new_states or not track_gas:

@@ -355,9 +355,13 @@ model_cache = ModelCache()
 
 # ------------------------------------------------------------------ get_model
 class _Args:
-    """support/support_args.py: the solver timeout (ms) get_model uses."""
-    solver_timeout = 25000
+    """support/support_args.py:5-25 (the fields this core reads): solver timeout
+    in ms (get_model), pruning factor (svm.py:319-326 fork filter), the SMT2
+    query log directory (support/model.py:62-73)."""
+    solver_timeout = 10000
+    pruning_factor = 1
     solver_log = None
+    unconstrained_storage = False
 
 
 args = _Args()
@@ -384,9 +388,42 @@ time_handler = TimeHandler()
 
 
 def _no_backend(constraints, minimize, maximize, timeout):
+    """The built-in backend: decides only what needs no search.  A set whose
+    conjunction folds to True is sat with the empty model (what z3's
+    Optimize.check returns for it, support/model.py:76-78), one that folds to
+    False is unsat; anything else needs a real SMT backend."""
+    root = And(*[c for c in constraints if isinstance(c, Bool)]).raw
+    if root is TRUE and not minimize and not maximize:
+        return Model([ModelRef({})])
+    if root.op == "const" and root.param == 0:
+        raise UnsatError
+    if not minimize and not maximize:
+        witness = _keccak_witness()
+        if witness is not None and witness.eval(root, model_completion=True).param == 1:
+            return Model([witness])
     raise SolverBackendMissing(
         "quick-sat found no satisfying model and no SMT backend is installed (z3 is absent "
         "in this image): install one with mythril_amd.smt.solver.set_solver_backend()")
+
+
+def _keccak_witness() -> Optional[ModelRef]:
+    """The model the keccak axioms of concrete inputs admit by construction
+    (keccak_function_manager.py:116-130: f(c) == keccak(c) and inverse(f(c)) == c):
+    keccak256_N and its inverse interpreted exactly at the registered points,
+    every variable 0.  Sound: the caller keeps it only if it satisfies the whole
+    query.  None when there are no registrations."""
+    from .keccak_manager import keccak_function_manager as km
+    from .program import FuncInterp
+    if not km.concrete_hashes:
+        return None
+    fn: Dict[str, FuncInterp] = {}
+    for data, h in km.concrete_hashes.items():
+        n = data.size()
+        f = fn.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
+        inv = fn.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
+        f.entries[(data.value,)] = h.value
+        inv.entries[(h.value,)] = data.value
+    return ModelRef(fn)
 
 
 solver_backend: Callable = _no_backend
@@ -416,9 +453,59 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         ret_model = model_cache.check_quick_sat(simplify(And(*constraints)).raw)
         if ret_model:
             return ret_model
-    model = solver_backend(constraints, minimize, maximize, timeout)
+    if args.solver_log:
+        from .smtlib import log_query, to_smt2
+        log_query(args.solver_log, to_smt2(constraints, minimize, maximize))
+    fut = _speculative.pop(_spec_key(constraints, minimize, maximize), None)
+    model = fut.result() if fut is not None else solver_backend(constraints, minimize, maximize, timeout)
     model_cache.put(model, 1)
     return model
+
+
+# ------------------------------------------------------------------ fallback pool
+_speculative: Dict = {}
+
+
+def _spec_key(constraints, minimize=(), maximize=()):
+    return (tuple(_raw(c) for c in constraints), tuple(minimize), tuple(maximize))
+
+
+def get_models(queries: Sequence, solver_timeout=None, workers: int = 8) -> List[object]:
+    """[get_model(q) for q in queries] with the SMT backend calls overlapped:
+    every query's backend call starts up front on a thread pool (speculation),
+    then the queries are answered strictly in order, exactly as the sequential
+    loop would (quick-sat against the cache as earlier answers left it, memo,
+    LRU moves, backend models cached in order); a speculative answer is used
+    only where the sequential loop reaches the backend, and discarded
+    otherwise.  Each element is a model or the exception get_model raised."""
+    from concurrent.futures import ThreadPoolExecutor
+    timeout = solver_timeout or args.solver_timeout
+    prepared = []
+    for q in queries:
+        cs = q.get_all_constraints() if hasattr(q, "get_all_constraints") else list(q)
+        prepared.append([c for c in cs if type(c) != bool])
+    out: List[object] = []
+    with ThreadPoolExecutor(max_workers=max(1, workers)) as pool:
+        for cs in prepared:
+            key = _spec_key(cs)
+            if key not in _speculative:
+                _speculative[key] = pool.submit(_safe_backend, cs, timeout)
+        try:
+            for q in queries:
+                try:
+                    out.append(get_model(q if isinstance(q, Constraints) else tuple(q),
+                                         solver_timeout=solver_timeout))
+                except (UnsatError, SolverTimeOutException, SolverBackendMissing) as e:
+                    out.append(e)
+        finally:
+            for cs in prepared:
+                _speculative.pop(_spec_key(cs), None)
+    return out
+
+
+def _safe_backend(constraints, timeout):
+    """Speculative backend call: exceptions travel to the sequential replay."""
+    return solver_backend(constraints, (), (), timeout)
 
 
 # ------------------------------------------------------------------ Constraints

@@ -92,12 +92,19 @@ def test_missing_backend_is_loud_not_a_prune(fresh):
     never turned into is_possible() == False (a silent prune)."""
     x = BVS("x", 256)
     solver.set_solver_backend(solver._no_backend)
-    c = Constraints([ULT(x, BVV(11, 256))])
+    c = Constraints([x == BVV(11, 256)])       # no built-in witness (variables 0) satisfies it
     with pytest.raises(solver.SolverBackendMissing):
         c.is_possible()
     with pytest.raises(solver.SolverBackendMissing):
         c.get_model()
     assert not issubclass(solver.SolverBackendMissing, (SolverTimeOutException, UnsatError))
+    # what the built-in backend does decide: folded True / False, concrete keccak axioms
+    assert Constraints([]).is_possible() is True
+    assert Constraints([x == x]).is_possible() is True
+    from mythril_amd.smt.keccak_manager import keccak_function_manager as km
+    km.reset()
+    h = km.create_keccak(BVV(0x1234, 256))
+    assert Constraints([h == h]).is_possible() is True          # f(c) == keccak(c) witness
 
 
 def test_keccak_manager_reference_behaviour():
