@@ -51,9 +51,19 @@ def parse(argv=None):
     ap.add_argument("--hooked-lanes", type=int, default=4096,
                     help="lanes of the hooked-C2 field (0: off): C2 through LaserEVM with the "
                          "default detection modules' opcode hooks registered")
+    ap.add_argument("--unbucketed-steps", type=int, default=10,
+                    help="batches of the C2 lanes in generation order, reported as c2_unbucketed (0: off)")
+    ap.add_argument("--large-steps", type=int, default=10,
+                    help="batches of the large-contract field (c2_large_contract; 0: off)")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
+
+
+def _log(rank: int, what: str) -> None:
+    """Progress on stderr (the JSON line stays alone on stdout)."""
+    if rank == 0:
+        print(f"bench.py: {what} [{time.strftime('%H:%M:%S')}]", file=sys.stderr, flush=True)
 
 
 def _free_port() -> int:
@@ -116,6 +126,14 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         dev = GpuDevice(local)
     else:
         dev = device_factory(local)
+    from mythril_amd import dist as mdist
+
+    def barrier():
+        if dist_on:
+            dist.barrier()
+        if gpu:
+            torch.cuda.synchronize()
+
     code = workloads.bytecode("overflow.sol.o")
     cid = dev.load_code(code)
     batch = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + rank,
@@ -124,18 +142,30 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
     # one function's path (mythril_amd/lanes.py:bucket_order); parity of every
     # lane is independent of its position in the batch
     from mythril_amd.lanes import bucket_order, permuted
-    batch = permuted(batch, bucket_order(batch))
     dev.alloc(batch.shape, coverage=True)
+    unbucketed = None
+    if args.unbucketed_steps and not args.profile_only:
+        # the same lanes in generation order: what bucketing buys (reported
+        # beside `value`, never as it)
+        _log(rank, "C2 unbucketed")
+        dev.upload(workloads.slim_copy(batch))
+        dev.run_batches(1)
+        barrier()
+        t0 = time.perf_counter()
+        ust = dev.run_batches(args.unbucketed_steps)
+        barrier()
+        uel = time.perf_counter() - t0
+        uel, usteps = mdist.reduce_timing(uel, float(sum(st.lane_steps for st in ust)))
+        unbucketed = {"value": usteps / uel, "unit": "lane-steps/s",
+                      "ms_per_step": 1000.0 * uel / args.unbucketed_steps,
+                      "kernel_ms_per_batch": float(np.mean([st.kernel_ms for st in ust])),
+                      "order": "generation order (no bucket_order)"}
+    batch = permuted(batch, bucket_order(batch))
     dev.upload(workloads.slim_copy(batch))
+    _log(rank, "C2 bucketed (timed)")
 
     if args.warmup:
         dev.run_batches(args.warmup)
-
-    def barrier():
-        if dist_on:
-            dist.barrier()
-        if gpu:
-            torch.cuda.synchronize()
 
     # the K batches are enqueued back to back (reset + stepping launch each,
     # mg_run_batches) with one host wait: no host round trip between batches
@@ -150,24 +180,37 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
     elapsed = time.perf_counter() - t0
 
     # coverage all-gather over RCCL (coverage_plugin.py semantics: OR of bits)
-    from mythril_amd import dist as mdist
     cov_union = mdist.allgather_coverage(dev.coverage(cid))
     elapsed, total_steps = mdist.reduce_timing(elapsed, float(lane_steps))
     total_steps = int(total_steps)
 
+    large = None
+    if args.large_steps and not args.profile_only:
+        _log(rank, "C2 on the 3,523-instruction fixture")
+        large = run_large(dev, args, rank, barrier)
+        # back to the C2 batch for the roofline profile below
+        dev.alloc(batch.shape, coverage=True)
+        dev.upload(workloads.slim_copy(batch))
+
+    roof = None
+    if rank == 0 and not args.profile_only and not args.no_roofline:
+        _log(rank, "C2 roofline profile")
+        roof = roofline.lane_step_roofline(dev, batch, cid, kernel_ms=float(np.mean(kernel_ms)) if kernel_ms else 0.0)
+
     hooked = None
-    if args.hooked_lanes and gpu:
+    if args.hooked_lanes and gpu and not args.profile_only:
+        _log(rank, f"hooked C2 ({args.hooked_lanes} lanes)")
         hooked = run_hooked_c2(dev, args.hooked_lanes, rank)
 
     c4 = None
     if not args.no_c4:
+        _log(rank, "C4")
         c4 = run_c4(args, dev, rank, world, barrier, dist_on)
 
     if rank == 0 and not args.profile_only:
         value = total_steps / elapsed
         steps_per_batch = lane_steps / max(args.steps, 1)
         kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
-        roof = None if args.no_roofline else roofline.lane_step_roofline(dev, batch, cid, kernel_ms=kms)
         out = {
             "metric": "EVM lane-steps/s (kernel 1, C2: 65,536 concrete lanes/GPU, token.sol runtime)",
             "value": value,
@@ -190,12 +233,18 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
                        "parallelism": f"lanes sharded x{world}, RCCL coverage all-gather"},
             "roofline": roof,
         }
+        if unbucketed is not None:
+            out["c2_unbucketed"] = unbucketed
+        if large is not None:
+            out["c2_large_contract"] = large
         if not args.no_cpu_baseline:
             from oracle import cpu_baseline
+            _log(rank, "C2 CPU baseline")
             out["cpu_baseline"] = cpu_baseline.c2_lane_steps(code, args.cpu_seconds)
         if c4 is not None:
             if not args.no_cpu_baseline:
                 from oracle import cpu_baseline
+                _log(rank, "C4 CPU baseline")
                 c4["cpu_baseline"] = cpu_baseline.c4_evals(args.c4_models, args.cpu_seconds)
             out["constraint_evals"] = c4
         if hooked is not None:
@@ -261,6 +310,36 @@ def run_hooked_c2(dev, n_lanes, rank):
             "hooked_opcodes": {"pre": DEFAULT_MODULE_PRE, "post": DEFAULT_MODULE_POST}}
 
 
+def run_large(dev, args, rank, barrier):
+    """C2's lane generator on the reference's 3,523-instruction disassembler
+    fixture (workloads.large_code: 16 selectors, bucketed): the pre-decoded
+    code fills LDS with the push immediates left in HBM (parity:
+    tests/test_gpu_lds_plan.py::test_large_code_staged_prefix_with_runs)."""
+    from mythril_amd import dist as mdist, workloads
+    from mythril_amd.lanes import bucket_order, permuted
+    code = workloads.large_code()
+    cid = dev.load_code(code)
+    b = workloads.c2_batch(args.lanes, code_id=cid, seed=workloads.C2_SEED + 0x100 + rank,
+                           stack_cap=1024, mem_cap=4096, rec_cap=args.rec_cap,
+                           selectors=workloads.dispatch_selectors(code))
+    b = permuted(b, bucket_order(b))
+    dev.alloc(b.shape, coverage=True)
+    dev.upload(workloads.slim_copy(b))
+    dev.run_batches(2)
+    barrier()
+    t0 = time.perf_counter()
+    st = dev.run_batches(args.large_steps)
+    barrier()
+    el = time.perf_counter() - t0
+    el, steps = mdist.reduce_timing(el, float(sum(s.lane_steps for s in st)))
+    return {"value": steps / el, "unit": "lane-steps/s", "instructions": dev.n_instr(cid),
+            "lanes_per_gpu": args.lanes,
+            "ms_per_step": 1000.0 * el / args.large_steps,
+            "kernel_ms_per_batch": float(np.mean([s.kernel_ms for s in st])),
+            "escaped_lanes_per_batch": float(np.mean([s.escaped for s in st])),
+            "code": "tests/golden/disassembly.json (disassembler_test.py:8-10)"}
+
+
 def run_c4(args, dev, rank, world, barrier, dist_on):
     """C4 (configs[3]): 1M constraint DAGs x 4096 candidate models, DAGs split
     over ranks (strong scaling), models replicated; kernel 2 only in the timed
@@ -288,6 +367,8 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
     _, n_sat = mdist.reduce_timing(0.0, float(n_sat))
     n_sat = int(n_sat)
     ops, gather_bytes = synth.program_cost(prog)
+    ops_nodiv, _ = synth.program_cost(prog, div_cost=0.0)
+    div_count = synth.division_count(prog)
     k_ms = float(np.mean(kms))
     ops_launch = ops * models.n_models
     tops = ops_launch / (k_ms / 1e3) / 1e12
@@ -306,8 +387,34 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
                      "kernel": "k_bv_eval", "kernel_ms": k_ms,
                      "algorithmic_int32_ops_per_launch": ops_launch,
                      "int32_ops_per_eval": ops / max(prog.n_dags, 1),
+                     # the §8(d) division charge (32 w^2 per 256-bit div/rem) is most of
+                     # `achieved`; without it, and with divisions at the VALU count the
+                     # Knuth-D path executes (SQ_INSTS_VALU of the divrem-only class,
+                     # profiles/r02/k2_div_valu.json):
+                     "without_division_charge": _k2_alt(ops_nodiv, 0.0, models.n_models, k_ms),
+                     "division_at_executed_valu": _k2_alt(ops_nodiv, div_count, models.n_models, k_ms,
+                                                          executed=True),
+                     "divisions_per_eval": div_count / max(prog.n_dags, 1),
                      "model_bytes_per_eval": gather_bytes / max(prog.n_dags, 1)}),
     }
+
+
+def _k2_alt(ops_nodiv, div_count, n_models, k_ms, executed=False):
+    """Kernel 2's INT32 roofline with another division cost: none, or the
+    measured VALU instructions per division (profiles/r02/k2_div_valu.json)."""
+    from mythril_amd.roofline import VALU_PEAK_TOPS, division_valu
+    per_div = 0.0
+    src = None
+    if executed:
+        per_div, src = division_valu()
+        if per_div is None:
+            return None
+    tops = (ops_nodiv + div_count * per_div) * n_models / (k_ms / 1e3) / 1e12
+    out = {"achieved": tops, "peak": VALU_PEAK_TOPS, "frac": tops / VALU_PEAK_TOPS,
+           "unit": "T int32-ops/s"}
+    if executed:
+        out.update({"valu_per_division": per_div, "source": src})
+    return out
 
 
 if __name__ == "__main__":

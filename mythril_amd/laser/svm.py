@@ -32,6 +32,7 @@ order.  Hook-free paths run in one launch.
 """
 from __future__ import annotations
 
+import bisect
 import heapq
 import itertools
 import logging
@@ -63,6 +64,20 @@ from .transaction import ContractCreationTransaction, install_runtime_code
 
 log = logging.getLogger(__name__)
 
+# opcodes _ack_safe may defer, with the number of words the real pop takes
+# (ADDMOD/MULMOD 3, DUPk k, SWAPk k+1: the reference's precheck table says less)
+_ACK_SAFE: Dict[str, int] = {
+    **{op: 2 for op in ("ADD", "MUL", "SUB", "DIV", "SDIV", "MOD", "SMOD", "SIGNEXTEND", "LT", "GT",
+                        "SLT", "SGT", "EQ", "AND", "OR", "XOR", "BYTE", "SHL", "SHR", "SAR",
+                        "MSTORE", "MSTORE8", "SSTORE", "JUMPI")},
+    "ADDMOD": 3, "MULMOD": 3, "ISZERO": 1, "NOT": 1, "POP": 1, "MLOAD": 1, "SLOAD": 1, "JUMP": 1,
+    "JUMPDEST": 0,
+    **{f"PUSH{k}": 0 for k in range(1, 33)},
+    **{f"DUP{k}": k for k in range(1, 17)},
+    **{f"SWAP{k}": k + 1 for k in range(1, 17)},
+}
+
+_MERGE_GAP = 256        # lanes: transfer ranges closer than this merge into one copy
 _EXECUTED_HALTS = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT, MG_VMEXC, MG_HALT_DROPPED)
 _INF = float("inf")
 _NO_GAS_LIMIT = (1 << 64) - 1
@@ -151,6 +166,7 @@ class LaserEVM:
         # coverage the reference's execute_state hook records for states the
         # device never executes (escaped, skipped by a pre hook)
         self._host_cov: Dict[bytes, set] = defaultdict(set)
+        self._jd_addrs: Dict[str, List[int]] = {}     # jump checks of _ack_safe
         # coverage other ranks reported (sharded runs, laser/sharded.py), OR-ed in
         self._peer_cov: Dict[str, np.ndarray] = {}
         self._cap_grow = 1
@@ -456,7 +472,12 @@ class LaserEVM:
         sched = self._sched = _Schedule(lanes, b, bfs)
 
         def launch(run: List[int], horizon: int):
-            for lo, cnt in _ranges(sorted(sched.dirty)):       # contiguous runs: one copy each
+            # Between launches the host image equals the device image for every
+            # lane that is not dirty (every lane the device may change is in
+            # `run` and downloaded right after), so a copy may span clean lanes:
+            # nearby ranges merge into one call (the fixed cost per call is far
+            # above the per-lane bytes of a gap)
+            for lo, cnt in _ranges(sorted(sched.dirty), gap=_MERGE_GAP):
                 dev.upload_range(b, lo, cnt)
                 for pos in range(lo, lo + cnt):
                     lanes[pos].dirty = False
@@ -467,7 +488,7 @@ class LaserEVM:
             self.device_ms += st.kernel_ms
             self.lane_steps += st.lane_steps
             self.total_states += st.lane_steps      # one successor per executed step
-            for lo, cnt in _ranges(run):
+            for lo, cnt in _ranges(run, gap=_MERGE_GAP):
                 dev.download_range(b, lo, cnt)
             self._collect_records(b, run)
             for i in run:
@@ -554,7 +575,11 @@ class LaserEVM:
             b.steps[i] = steps
             b.flags[i] |= MG_LANE_HOOK_ACK | (MG_LANE_STEP1 if post else 0)
             if not post:
-                self._sched.set(i, "paused"); self._sched.mark_dirty(i)
+                # BFS: a resumed instruction that cannot end, escape or register
+                # at its own round joins the round's next launch instead of
+                # forcing one before the round's later events (see _ack_safe)
+                safe = self._sched.bfs and self._ack_safe(name, s, b)
+                self._sched.set(i, "paused", acked=safe); self._sched.mark_dirty(i)
                 return
             self._sched.mark_dirty(i)
             snapshot = copy(pre_state)
@@ -654,6 +679,62 @@ class LaserEVM:
             final_states.append(s)
 
 
+    def _ack_safe(self, name: str, s: GlobalState, b: LaneBatch) -> bool:
+        """True when the hooked instruction of `s`, resumed with HOOK_ACK, can
+        produce no event and no function-manager record at its own round: no
+        halt, VmException, dropped jump, capacity or opcode escape, OOG.  Under
+        BFS the reference runs it right after its hooks (svm.py:369-491) and the
+        next event of the same round comes after it; when it can affect nothing
+        that event sees, the launch that executes it can wait until the round's
+        events are delivered, so one launch serves the whole round.  The test
+        is conservative: any doubt answers False (launch now, as before)."""
+        real_pops = _ACK_SAFE.get(name)
+        if real_pops is None:
+            return False
+        ms, env = s.mstate, s.environment
+        st = ms.stack
+        n = len(st)
+        if n < real_pops:
+            return False                 # the real pop raises (table counts differ)
+        if (name.startswith("PUSH") or name.startswith("DUP")) and n + 1 > min(1024, b.shape.stack_cap):
+            return False
+        extra = 0
+        if name in ("MLOAD", "MSTORE", "MSTORE8"):
+            off = concrete(st[-1])
+            end = off + (1 if name == "MSTORE8" else 32)
+            if end > b.shape.mem_cap:
+                return False             # capacity escape
+            w = (end + 31) // 32
+            extra = 3 * w + w * w // 512
+        elif name == "SSTORE":
+            if env.static:
+                return False
+            store = env.active_account.storage.printable_storage
+            if concrete(st[-1]) not in store and len(store) >= b.shape.storage_cap:
+                return False
+        elif name in ("JUMP", "JUMPI"):
+            if name == "JUMPI" and concrete(st[-2]) == 0:
+                pass
+            elif not self._jumpdest_at(env.code, concrete(st[-1])):
+                return False             # VmException / dropped branch at this round
+        tx = s.current_transaction
+        lim = getattr(tx, "gas_limit", None)
+        lim = 10 ** 9 if lim is None else min(concrete(lim), 10 ** 9)
+        # 50,000 bounds every listed opcode's table gas (SSTORE 20,000 at most)
+        return ms.min_gas_used + extra + 50_000 < lim
+
+    def _jumpdest_at(self, code, target: int) -> bool:
+        """instructions.py:1520-1636 jump check: the first instruction at or above
+        `target` (util.get_instruction_index's >=) is a JUMPDEST."""
+        key = code.bytecode
+        addrs = self._jd_addrs.get(key)
+        if addrs is None:
+            addrs = self._jd_addrs[key] = [ins["address"] for ins in code.instruction_list]
+        if not addrs or target > addrs[-1]:
+            return False
+        k = bisect.bisect_left(addrs, target)
+        return code.instruction_list[k]["opcode"] == "JUMPDEST"
+
     # ------------------------------------------------------------- coverage
     def coverage(self) -> Dict[object, Tuple[int, List[bool]]]:
         """coverage_plugin.py's table {bytecode: (n_instructions, [covered])} from
@@ -706,12 +787,14 @@ def _mask(ops) -> List[int]:
     return m
 
 
-def _ranges(idx: List[int]):
+def _ranges(idx: List[int], gap: int = 0):
+    """[first, count] runs covering the sorted lane indices; runs whose gap is
+    at most `gap` lanes merge (the gap lanes are copied too)."""
     idx = sorted(idx)
     out = []
     for i in idx:
-        if out and out[-1][0] + out[-1][1] == i:
-            out[-1][1] += 1
+        if out and out[-1][0] + out[-1][1] + gap >= i:
+            out[-1][1] = i - out[-1][0] + 1
         else:
             out.append([i, 1])
     return out
@@ -736,6 +819,7 @@ class _Schedule:
         self._ev: List = []
         self._pz: List = []
         self.paused: set = set()
+        self.acked: set = set()       # paused at a deferred hooked instruction (_ack_safe)
         self.dirty: set = set()
 
     def _key(self, pos: int):
@@ -743,15 +827,19 @@ class _Schedule:
         return (r, pos) if self.bfs else (-pos, r)
 
     def _pkey(self, pos: int):
-        return (int(self.b.steps[pos]), pos) if self.bfs else (-pos,)
+        # a deferred hooked instruction has no event before the next round
+        return (int(self.b.steps[pos]) + (pos in self.acked), pos) if self.bfs else (-pos,)
 
-    def set(self, pos: int, phase: str) -> None:
+    def set(self, pos: int, phase: str, acked: bool = False) -> None:
         self.lanes[pos].phase = phase
         self.paused.discard(pos)
+        self.acked.discard(pos)
         if phase == "event":
             heapq.heappush(self._ev, (self._key(pos), pos))
         elif phase == "paused":
             self.paused.add(pos)
+            if acked:
+                self.acked.add(pos)
             heapq.heappush(self._pz, (self._pkey(pos), pos))
 
     def mark_dirty(self, pos: int) -> None:

@@ -139,6 +139,23 @@ def pmc_traffic(kernel: str):
     return None, None
 
 
+def division_valu():
+    """VALU instructions one wave executes per interpreted 256-bit division of
+    kernel 2, minus the interpreter's per-instruction overhead (the add/sub
+    class's VALU per instruction less its 16 useful ops), from the newest
+    profiles/rNN/k2_div_valu.json (scripts/k2_div_valu.py over a rocprofv3
+    SQ_INSTS_VALU pass of scripts/k2_opclass.py).  (value, source) or (None, None)."""
+    for d in sorted(PROFILES.glob("r*"), reverse=True):
+        f = d / "k2_div_valu.json"
+        if f.is_file():
+            try:
+                rec = json.loads(f.read_text())
+                return float(rec["valu_per_division"]), str(f.relative_to(PROFILES.parent))
+            except (OSError, ValueError, KeyError):
+                pass
+    return None, None
+
+
 def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
     """Profile one batch (untimed; the resident image is reset first) and price the
     timed kernel's average launch against the HBM and INT32 VALU peaks."""
@@ -152,15 +169,23 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
     hbm_frac = gbs / HBM_PEAK_GBS
     valu_frac = tops / VALU_PEAK_TOPS
     primary_hbm = hbm_frac >= valu_frac
+    traffic, traffic_src = pmc_traffic("k_lane_step")
     return with_sustained({
+        # SURVEY §8(d) prices a lane-step's stack words as bytes moved; kernel 1
+        # keeps them in registers and LDS, so the HBM fraction below is an
+        # algorithmic one.  `traffic_frac` is the measured HBM fraction, and the
+        # kernel's real bound at C2 is latency (one wave per SIMD): DESIGN.md §3.1.
         "bound": "hbm" if primary_hbm else "valu-int32",
         "achieved": gbs if primary_hbm else tops,
         "peak": HBM_PEAK_GBS if primary_hbm else VALU_PEAK_TOPS,
         "unit": "GB/s" if primary_hbm else "T int32-ops/s",
         "frac": hbm_frac if primary_hbm else valu_frac,
-        "traffic": pmc_traffic("k_lane_step")[0],
+        "traffic": traffic,
         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-        "traffic_source": pmc_traffic("k_lane_step")[1],
+        "traffic_source": traffic_src,
+        "traffic_frac": (traffic / sec / 1e9 / HBM_PEAK_GBS) if traffic else None,
+        "latency_bound": "65,536 lanes = 1,024 waves = one wave per SIMD: the slowest wave's "
+                         "dependent dispatch chain sets the launch time (DESIGN.md §3.1)",
         "kernel": "k_lane_step",
         "kernel_ms": kernel_ms,
         "algorithmic_bytes_per_launch": byts,

@@ -328,16 +328,28 @@ def _insn_cost(op: int, width: int) -> float:
     return 2.0 * 8   # compares / overflow predicates on 256-bit operands
 
 
-def program_cost(batch: ProgramBatch):
-    """(int32 ops per constraint-eval summed over all DAGs, model bytes gathered per eval)."""
+_DIVS = ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")
+
+
+def division_count(batch: ProgramBatch) -> int:
+    """Division / remainder instructions over all DAGs (one per eval each)."""
+    ops = (batch.insns[:, 0] & 0xFF).astype(np.int64)
+    return int(np.isin(ops, [OPCODE[n] for n in _DIVS if n in OPCODE]).sum())
+
+
+def program_cost(batch: ProgramBatch, div_cost=None):
+    """(int32 ops per constraint-eval summed over all DAGs, model bytes gathered per eval).
+    div_cost replaces the §8(d) 32 w^2 charge of each division when given."""
     ops = (batch.insns[:, 0] & 0xFF).astype(np.int64)
     widths = ((batch.insns[:, 0] >> 8) & 0x1FF).astype(np.int64)
     table = {}
     total = 0.0
     key = ops * 512 + widths
     uniq, counts = np.unique(key, return_counts=True)
+    divs = {OPCODE[n] for n in _DIVS if n in OPCODE}
     for k, c in zip(uniq, counts):
-        total += c * _insn_cost(int(k // 512), int(k % 512))
+        op = int(k // 512)
+        total += c * (div_cost if (div_cost is not None and op in divs) else _insn_cost(op, int(k % 512)))
     refs = batch.insns[:, 1:4]
     var_refs = int(((refs >> 30) == REF_VAR).sum())
     return total, 32.0 * var_refs

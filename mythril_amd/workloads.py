@@ -38,6 +38,16 @@ def _words_to_limbs(rows: np.ndarray) -> np.ndarray:
     return dw[:, ::-1].copy()
 
 
+def large_code() -> bytes:
+    """The reference's 3,523-instruction disassembler fixture
+    (tests/disassembler_test.py:8-10, tests/golden/disassembly.json): a solc
+    runtime with 16 dispatcher selectors, past what fits in LDS with its push
+    immediates -- the bench's large-contract field and its parity test."""
+    fx = json.loads((GOLDEN / "disassembly.json").read_text())
+    code = fx["code"]
+    return bytes.fromhex(code[2:] if code.startswith("0x") else code)
+
+
 def _int_limbs(x: int) -> np.ndarray:
     return np.array([(x >> (32 * k)) & 0xFFFFFFFF for k in range(8)], dtype=np.uint32)
 

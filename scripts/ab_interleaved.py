@@ -38,10 +38,13 @@ def k2(dev, variants, rounds, n_dags):
                           "G_evals_s": n_dags * 4096 / min(ms) / 1e6}), flush=True)
 
 
-def k1(dev, variants, rounds):
-    code = workloads.bytecode("overflow.sol.o")
+def k1(dev, variants, rounds, code_name="overflow.sol.o"):
+    """variants: "VAR=value[,VAR2=value]" strings (env switches read per launch)."""
+    code = workloads.bytecode(code_name) if code_name.endswith(".o") else workloads.large_code()
     cid = dev.load_code(code)
-    b = workloads.c2_batch(65536, code_id=cid, stack_cap=1024, mem_cap=1024, rec_cap=128)
+    sels = None if code_name.endswith(".o") else workloads.dispatch_selectors(code)
+    kw = {} if sels is None else {"selectors": sels}
+    b = workloads.c2_batch(65536, code_id=cid, stack_cap=1024, mem_cap=1024, rec_cap=128, **kw)
     b = permuted(b, bucket_order(b))
     dev.alloc(b.shape, coverage=True)
     dev.upload(workloads.slim_copy(b))
@@ -49,15 +52,19 @@ def k1(dev, variants, rounds):
     steps = None
     for _ in range(rounds):
         for v in variants:
-            os.environ["MG_K1_RUNS"] = v
+            for kv in v.split(","):
+                k, _, val = kv.partition("=")
+                os.environ[k] = val
             dev.run_batches(2)
             st = dev.run_batches(10)
             res[v].append(sum(s.kernel_ms for s in st) / len(st))
             n = sum(s.lane_steps for s in st) // len(st)
-            assert steps is None or n == steps
+            assert steps is None or n == steps, (v, n, steps)
             steps = n
+            for kv in v.split(","):
+                os.environ.pop(kv.partition("=")[0], None)
     for v, ms in res.items():
-        print(json.dumps({"kernel": "k_lane_step", "MG_K1_RUNS": v, "min_ms": min(ms),
+        print(json.dumps({"kernel": "k_lane_step", "code": code_name, "variant": v, "min_ms": min(ms),
                           "median_ms": statistics.median(ms),
                           "G_lane_steps_s": steps / min(ms) / 1e6}), flush=True)
 
@@ -65,10 +72,13 @@ def k1(dev, variants, rounds):
 def main():
     dev = GpuDevice(0)
     which = sys.argv[1] if len(sys.argv) > 1 else "both"
-    k2v = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "4"]
-    if which in ("k1", "both"):
-        k1(dev, ["lds", "reg"], 5)
-    if which in ("k2", "both"):
+    if which == "k1":
+        variants = sys.argv[2].split(";") if len(sys.argv) > 2 else ["MG_K1_RUNS=lds", "MG_K1_RUNS=reg"]
+        code = sys.argv[3] if len(sys.argv) > 3 else "overflow.sol.o"
+        rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+        k1(dev, variants, rounds, code)
+    if which == "k2":
+        k2v = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "4"]
         k2(dev, k2v, 4, 1_000_000)
     dev.close()
 

@@ -1,0 +1,122 @@
+"""Hook batching of the BFS event loop (LaserEVM._ack_safe) on CPU with the
+oracle device: deferring the launch that executes a resumed hooked instruction
+to the end of its round must leave every observable event exactly where the
+one-launch-per-event loop puts it (that loop is pinned against single-stepped
+oracle runs by test_gpu_laser.py::test_hooks_fire_in_reference_order).
+
+The batch mixes C2 lanes with lanes whose hooked instruction ends or escapes
+the path at its own round -- the cases _ack_safe must refuse: invalid JUMP,
+JUMPI to a bad target (dropped), a real stack underflow behind the table's
+precheck (DUP3), OOG on a hooked ADD, an MSTORE past the lane's memory page,
+STOP/RETURN/REVERT."""
+import pytest
+
+import bench
+from mythril_amd import workloads
+from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, DepthFirstSearchStrategy,
+                               Disassembly, LaserEVM, MessageCallTransaction, WorldState)
+from mythril_amd.laser import svm as svm_mod
+from mythril_amd.laser.transaction import _setup_global_state_for_execution
+from oracle_device import OracleDevice
+
+ODD_CODES = [
+    ("6001600201600556", 8_000_000),          # ADD, JUMP to 5 (not a JUMPDEST): VmException
+    ("6001602057", 8_000_000),                # JUMPI to 0x20 (past the end): dropped
+    ("600160028200", 8_000_000),              # DUP3 with two words: real underflow
+    ("6001600201600201", 8),                  # the first ADD runs out of gas (limit 8)
+    ("6001620100005200", 8_000_000),          # MSTORE at 0x10000: past the memory page
+    ("600160025b01600456", 8_000_000),         # a JUMP back to the JUMPDEST: ADD then underflow
+    ("600160005260206000f3", 8_000_000),      # MSTORE, RETURN
+    ("60006000fd", 8_000_000),                # REVERT
+]
+
+
+def _states(n_c2=48):
+    b = workloads.c2_batch(n_c2, seed=21, stack_cap=64, mem_cap=1024)
+    code = Disassembly(workloads.bytecode("overflow.sol.o"))
+    txs = []
+    for i in range(n_c2):
+        ws = WorldState()
+        acct = Account(workloads.CONTRACT, code=code)
+        for k, val in b.storage_dict(i, drop_zero=False).items():
+            acct.storage[k] = val
+        ws.put_account(acct)
+        txs.append(MessageCallTransaction(
+            world_state=ws, callee_account=acct, caller=workloads.ATTACKER,
+            call_data=bytes(b.calldata[i, : int(b.calldata_len[i])]), gas_price=1,
+            gas_limit=int(b.gas_limit[i]), origin=workloads.ATTACKER, call_value=0))
+        if i % 6 == 3:                        # odd lanes interleaved with the C2 lanes
+            hexcode, gas = ODD_CODES[(i // 6) % len(ODD_CODES)]
+            ws = WorldState()
+            dis = Disassembly(hexcode)
+            acct = Account(workloads.CONTRACT, code=dis)
+            ws.put_account(acct)
+            txs.append(MessageCallTransaction(
+                world_state=ws, callee_account=acct, caller=workloads.ATTACKER, call_data=b"",
+                gas_price=1, gas_limit=gas, origin=workloads.ATTACKER, call_value=0, code=dis))
+    return txs
+
+
+def _run(strategy, batching, monkeypatch):
+    if batching is False:
+        monkeypatch.setattr(svm_mod.LaserEVM, "_ack_safe", lambda self, name, s, b: False)
+    elif batching:
+        monkeypatch.undo()
+    vm = LaserEVM(device=OracleDevice(), strategy=strategy, execution_timeout=0)
+    log = []
+    tag = {}
+
+    def who(state):
+        return tag.get(id(state), tag.get(id(state.world_state)))
+
+    def pre(name):
+        def f(state):
+            log.append(("pre", name, who(state), state.mstate.pc,
+                        tuple(x.value for x in state.mstate.stack)))
+        return f
+    vm.register_hooks("pre", {op: [pre(op)] for op in bench.DEFAULT_MODULE_PRE + ["DUP3", "SWAP1"]})
+    vm.register_laser_hooks("transaction_end",
+                            lambda s, tx, ret, revert: log.append(("end", who(s), s.mstate.pc, revert)))
+    vm.register_laser_hooks("add_world_state", lambda s: log.append(("ws", who(s))))
+    for k, tx in enumerate(_states()):
+        _setup_global_state_for_execution(vm, tx)
+        tag[id(vm.work_list[-1])] = k
+        tag[id(vm.work_list[-1].world_state)] = k
+    vm.exec()
+    opened = [tag.get(id(ws)) for ws in vm.open_states]
+    return log, opened, vm.launches, vm.lane_steps
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_batched_hook_rounds_keep_the_event_order(strategy, monkeypatch):
+    log0, open0, launches0, steps0 = _run(strategy, False, monkeypatch)
+    log1, open1, launches1, steps1 = _run(strategy, True, monkeypatch)
+    assert steps1 == steps0
+    assert len(log1) == len(log0) > 500
+    assert log1 == log0
+    assert open1 == open0
+    kinds = {e[0] for e in log0}
+    assert {"pre", "end", "ws"} <= kinds
+    if strategy is BreadthFirstSearchStrategy:
+        assert launches1 * 3 < launches0          # rounds share launches
+    else:
+        assert launches1 == launches0             # DFS: unchanged
+
+
+@pytest.mark.parametrize("unguarded", ["DUP3", "ADD"])
+def test_the_batch_exercises_the_guards(unguarded, monkeypatch):
+    """Deferring `unguarded` without _ack_safe's checks (stack underflow behind
+    DUP3's precheck, OOG on ADD) would move an event: the batch above reaches
+    those cases, so its equality is not vacuous."""
+    log0, open0, _, _ = _run(BreadthFirstSearchStrategy, False, monkeypatch)
+    monkeypatch.undo()
+    orig = svm_mod.LaserEVM._ack_safe
+    monkeypatch.setattr(svm_mod.LaserEVM, "_ack_safe",
+                        lambda self, name, s, b: True if name == unguarded else orig(self, name, s, b))
+    log2, open2, _, _ = _run(BreadthFirstSearchStrategy, None, _NoUndo())
+    assert (log2, open2) != (log0, open0)
+
+
+class _NoUndo:
+    def undo(self):
+        pass
