@@ -69,6 +69,7 @@ static_assert(RUN_MAX <= 64u, "a run is read as one pre-decoded word per wave la
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) v4u g_u4;
 typedef __attribute__((address_space(3))) v4u l_u4;
+typedef __attribute__((address_space(3))) uint32_t l_u32;
 template <class T> DEV __attribute__((address_space(1))) T *gp(T *p) {
     return (__attribute__((address_space(1))) T *)p;
 }
@@ -94,6 +95,10 @@ DEV void st_word(g_u4 *base, size_t idx, const U256 &v) {
 }
 // LDS stack window: slots [0, win) of a lane live in LDS as [slot][half][lane of
 // the block] 16-byte pieces (conflict-free ds_read_b128), deeper slots in HBM.
+// LDS memory window: memory dwords [0, mw) of a lane live in LDS as [dword][lane
+// of the block] (conflict-free at a common offset); HBM holds the rest, and the
+// window's bytes once the launch flushes them.  Solidity keeps its scratch words,
+// free-memory pointer and first allocation (0x00-0x9f) there.
 // `ws` = lanes per block (the row stride), `tid` = the lane's index in its block.
 #define LANE_BLOCK 256u
 struct LaneView {
@@ -101,6 +106,8 @@ struct LaneView {
     uint32_t lane;
     l_u4 *win_base;      // LDS window of this block
     uint32_t win, tid, ws;
+    l_u32 *mw_base;      // LDS memory window of this block
+    uint32_t mw;         // memory dwords per lane in it
     DEV size_t row(uint32_t r) const { return (size_t)r * L.N + lane; }
     DEV U256 gstack(uint32_t slot) const { return ld_word(gv(L.stack), row(slot)); }
     DEV void set_gstack(uint32_t slot, const U256 &v) const { st_word(gv(L.stack), row(slot), v); }
@@ -127,9 +134,16 @@ struct LaneView {
         else set_gstack(slot, v);
     }
     DEV U256 env(int w) const { return ld_word(gv(L.env), row((uint32_t)w)); }
-    DEV uint32_t mdw(uint32_t dw) const { return gp(L.mem)[row(dw)]; }
-    DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? gp(L.mem)[row(dw)] : 0u; }
-    DEV void set_mdw(uint32_t dw, uint32_t v) const { gp(L.mem)[row(dw)] = v; }
+    DEV uint32_t lmdw(uint32_t dw) const { return mw_base[dw * ws + tid]; }
+    DEV void set_lmdw(uint32_t dw, uint32_t v) const { mw_base[dw * ws + tid] = v; }
+    DEV uint32_t gmdw(uint32_t dw) const { return gp(L.mem)[row(dw)]; }
+    DEV void set_gmdw(uint32_t dw, uint32_t v) const { gp(L.mem)[row(dw)] = v; }
+    DEV uint32_t mdw(uint32_t dw) const { return dw < mw ? lmdw(dw) : gmdw(dw); }
+    DEV uint32_t mdw_safe(uint32_t dw) const { return dw < L.mem_cap / 4u ? mdw(dw) : 0u; }
+    DEV void set_mdw(uint32_t dw, uint32_t v) const {
+        if (dw < mw) set_lmdw(dw, v);
+        else set_gmdw(dw, v);
+    }
     DEV uint32_t mbyte(uint32_t off) const { return (mdw(off >> 2) >> (24u - 8u * (off & 3u))) & 0xffu; }
     DEV void set_mbyte(uint32_t off, uint32_t b) const {
         const uint32_t sh = 24u - 8u * (off & 3u);
@@ -140,7 +154,10 @@ struct LaneView {
     DEV U256 mword(uint32_t off) const {
         U256 r;
         const uint32_t d0 = off >> 2, s = 8u * (off & 3u);
-        if (s == 0u) {
+        if (s == 0u && d0 + 8u <= mw) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r.w[7 - k] = lmdw(d0 + k);
+        } else if (s == 0u) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) r.w[7 - k] = mdw(d0 + k);
         } else {
@@ -154,7 +171,10 @@ struct LaneView {
     }
     DEV void set_mword(uint32_t off, const U256 &v) const {
         const uint32_t d0 = off >> 2, s = 8u * (off & 3u);
-        if (s == 0u) {
+        if (s == 0u && d0 + 8u <= mw) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) set_lmdw(d0 + k, v.w[7 - k]);
+        } else if (s == 0u) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) set_mdw(d0 + k, v.w[7 - k]);
         } else {
@@ -378,12 +398,15 @@ struct StepEnv {
     const uint8_t *a8;
     const uint32_t *a32;
     l_u4 *s_win;
+    l_u32 *s_mw;           // LDS memory window (mw dwords per lane)
     const uint4 *s_pd;     // pre-decoded code: x, y = decode words, z, w = run table
     const uint4 *s_push;
     uint32_t *s_prof;
     uint32_t *s_kc;      // this wave's Keccak cache (KC_WAVE words)
     uint64_t txlim, glim;
     uint32_t lane, tid, ws, win, flags, sflag, psflag, prof;
+    uint32_t mw;
+    uint32_t sn;         // s_pd holds instructions [0, sn) (the END sentinel included when staged whole)
 };
 
 // Executes the instruction decoded as (uk, ux) for one lane, exactly as the
@@ -398,7 +421,7 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
     const DevLanes &L = *E.L;
     const DevCode &C = E.C;
     const uint32_t lane = E.lane;
-    const LaneView V{L, lane, E.s_win, E.win, E.tid, E.ws};
+    const LaneView V{L, lane, E.s_win, E.win, E.tid, E.ws, E.s_mw, E.mw};
     const uint8_t *__restrict__ a8 = E.a8;
     const uint32_t *__restrict__ a32 = E.a32;
     const uint8_t *__restrict__ gops = a8 + C.op_off;
@@ -429,7 +452,7 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
                                  if (mx_ == MX_OOG) EXCX(EXC_OOG) if (mx_ == MX_ESCAPE) ESCX(ESC_MEMORY) }
 #define ZEROFILL() if (nmsize > msize0) V.mzero(msize0, nmsize);
 #define JUMP_OK(idx_) ((idx_) != MG_JRES_NONE && \
-                       (E.sflag ? (E.s_pd[(idx_)].y & 0xffu) : (uint32_t)gops[(idx_)]) == 0x5bu)
+                       ((E.sflag && (idx_) < E.sn) ? (E.s_pd[(idx_)].y & 0xffu) : (uint32_t)gops[(idx_)]) == 0x5bu)
 
     do {
         // svm.py:391-402 precheck; instructions.py:188-193 write protection;
@@ -862,12 +885,22 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                                           uint32_t horizon, uint32_t loop_bound,
                                                           DevResetImage R, uint32_t lpw_flags) {
     // lpw_flags: lanes per wave in bits 0..7; bit 8 = register-form runs only
-    // (MG_K1_RUNS=reg, for A/B runs against the LDS-resident form)
+    // (MG_K1_RUNS=reg, for A/B runs against the LDS-resident form); bit 9 = the
+    // push immediates are staged in LDS too (otherwise read from the code arena
+    // at wave-uniform addresses)
     const uint32_t lpw = lpw_flags & 0xffu;
     const bool lds_runs_on = (lpw_flags & 0x100u) == 0u;
+    const bool push_lds = (lpw_flags & 0x200u) != 0u;
+    // bits 16..23: LDS memory window per lane in 32-byte words
+    const uint32_t mw = ((lpw_flags >> 16) & 0xffu) * 8u;
     // Dynamic LDS: [stack window: win x 2 x lanes-per-block x 16 B]
+    //              [memory window: mw x lanes-per-block x 4 B]
     //              [pre-decoded code: pd_cap x 16 B: decode x, y | run table z, w]
-    //              [push immediates: pd_cap x 32 B][jump-resolve: jr_cap x 2 B][coverage: pd_cap]
+    //              [push immediates: pd_cap x 32 B, when push_lds][jump-resolve: jr_cap x 2 B]
+    //              [coverage: pd_cap]
+    // A code longer than pd_cap - 1 instructions is staged as its first
+    // pd_cap - 1 instructions (and its first jr_cap jump targets); the lanes
+    // beyond that prefix decode from the code arena and run no straight-line runs.
     // One ds_read_b128 at FETCH brings a lane both its next instruction's decode
     // and the straight-line run starting there, so the dispatch head reads the
     // lead lane's run with v_readlane instead of another dependent LDS read.
@@ -881,9 +914,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // lanes diverge less).  The idle threads still take part in the wave-wide
     // LDS load of a run's pre-decoded words below.
     const uint32_t lanes_pb = (LANE_BLOCK / 64u) * lpw;
-    uint4 *s_pd = dyn + (size_t)win * 2u * lanes_pb;
+    l_u32 *s_mw = (l_u32 *)(dyn + (size_t)win * 2u * lanes_pb);
+    uint4 *s_pd = dyn + (size_t)win * 2u * lanes_pb + (size_t)mw * lanes_pb / 4u;
     uint4 *s_push = s_pd + pd_cap;
-    uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + 2u * pd_cap);
+    uint16_t *s_jr = reinterpret_cast<uint16_t *>(s_push + (push_lds ? 2u * pd_cap : 0u));
     uint8_t *s_cov = reinterpret_cast<uint8_t *>(s_jr + jr_cap);
     __shared__ uint2 s_dec[256];
     __shared__ uint32_t s_code;
@@ -932,11 +966,13 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const uint32_t bcode = s_code;
     const bool mixed = __syncthreads_or(status == ST_RUNNING && my_code != bcode);
     bool staged = false, jstaged = false;
+    uint32_t ns_b = 0u, sn_b = 0u, jn_b = 0u, push_b = 0u;
     if (bcode != 0xffffffffu && !mixed) {
         const DevCode BC = codes[bcode];
-        if (BC.n_instr < pd_cap) {
+        const uint32_t ns = min(BC.n_instr, pd_cap - 1u);   // staged prefix
+        if (ns > 0u) {
             // pre-decode: opcode, gas, stack counts, kind, and the hook bit (bit 31)
-            for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x) {
+            for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
                 const uint32_t op = a8[BC.op_off + i];
                 const uint2 d = kDec[op];
                 const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
@@ -945,16 +981,24 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                      a32[BC.run_off + 2u * i], a32[BC.run_off + 2u * i + 1u]);
                 s_cov[i] = 0;
             }
-            if (threadIdx.x == 0) s_pd[BC.n_instr] = make_uint4(0u, ((uint32_t)K_END << 17) | PD_SPECIAL, 0u, 0u);
-            const uint4 *gpu4 = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
-            for (uint32_t i = threadIdx.x; i < 2u * BC.n_instr; i += blockDim.x) s_push[i] = gpu4[i];
+            if (threadIdx.x == 0 && ns == BC.n_instr)
+                s_pd[ns] = make_uint4(0u, ((uint32_t)K_END << 17) | PD_SPECIAL, 0u, 0u);
+            if (push_lds) {        // the host plans push_lds only for wholly staged codes
+                const uint4 *gpu4 = reinterpret_cast<const uint4 *>(a32 + BC.push_off);
+                for (uint32_t i = threadIdx.x; i < 2u * ns; i += blockDim.x) s_push[i] = gpu4[i];
+            }
             staged = true;
-            if (BC.n_jres <= jr_cap && BC.n_instr < 0xffffu) {
-                for (uint32_t i = threadIdx.x; i < BC.n_jres; i += blockDim.x) {
+            ns_b = ns;
+            sn_b = ns == BC.n_instr ? ns + 1u : ns;
+            push_b = BC.push_off;
+            const uint32_t jn = min(BC.n_jres, jr_cap);
+            if (jn > 0u && BC.n_instr < 0xffffu) {
+                for (uint32_t i = threadIdx.x; i < jn; i += blockDim.x) {
                     const uint32_t t = a32[BC.jres_off + i];
                     s_jr[i] = t == MG_JRES_NONE ? (uint16_t)0xffffu : (uint16_t)t;
                 }
                 jstaged = true;
+                jn_b = jn;
             }
         }
         __syncthreads();
@@ -964,10 +1008,17 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // block-uniform facts in scalar registers
     const uint32_t sflag = __builtin_amdgcn_readfirstlane(staged ? 1u : 0u);
     const uint32_t jflag = __builtin_amdgcn_readfirstlane(jstaged ? 1u : 0u);
+    const uint32_t ns = __builtin_amdgcn_readfirstlane(ns_b);     // staged instructions
+    const uint32_t sn = __builtin_amdgcn_readfirstlane(sn_b);     // + the END sentinel
+    const uint32_t jn = __builtin_amdgcn_readfirstlane(jn_b);     // staged jump targets
+    const uint32_t bpush = __builtin_amdgcn_readfirstlane(push_b);
+    const uint32_t psflag = (staged && push_lds) ? 1u : 0u;
+    // push immediate of instruction i of the staged code (wave-uniform i in runs)
+#define PUSH_IMM(i_) (psflag ? ld_word((const l_u4 *)s_push, (i_)) : ld_word(gv(a32 + bpush), (i_)))
     const uint32_t stack_lim = L.stack_cap < STACK_LIMIT ? L.stack_cap : STACK_LIMIT;
 
     // ---- per-lane machine state (registers) ----
-    const LaneView V{L, lane, s_win, win, tid, lanes_pb};
+    const LaneView V{L, lane, s_win, win, tid, lanes_pb, s_mw, mw};
     DevCode C{};
     uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
     uint32_t tlen = 0;                                    // trace length (BoundedLoops)
@@ -987,6 +1038,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (loop_on) tlen = L.trace_len[lane];
         gmin = L.gas_min[lane]; gmax = L.gas_max[lane];
         for (uint32_t k = 0; k < min(sp, win); ++k) V.set_wstack(k, V.gstack(k));   // window fill
+        for (uint32_t k = 0; k < min(msize >> 2, mw); ++k) V.set_lmdw(k, V.gmdw(k));
         if (sp >= 1u) T0 = V.stack(sp - 1u);
         if (sp >= 2u) T1 = V.stack(sp - 2u);
         live = true;
@@ -1002,19 +1054,21 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         lane_max = min(lane_max, horizon > s0 ? horizon - s0 : 0u);
     }
     const uint8_t *__restrict__ gops = a8 + C.op_off;
-    const StepEnv E{&L, C, a8, a32, s_win, s_pd, s_push, s_prof, s_kc + (threadIdx.x >> 6) * KC_WAVE, txlim, glim,
-                    lane, tid, lanes_pb, win, flags, sflag, staged ? 1u : 0u, prof ? 1u : 0u};
+    const StepEnv E{&L, C, a8, a32, s_win, s_mw, s_pd, s_push, s_prof, s_kc + (threadIdx.x >> 6) * KC_WAVE,
+                    txlim, glim, lane, tid, lanes_pb, win, flags, sflag, psflag, prof ? 1u : 0u, mw, sn};
 
     // Decode the instruction at pc and run the checks svm.execute_state makes
     // before evaluating it (svm.py:369-402): depth cut-off, past-the-end pc,
     // hooked opcode, this launch's step budget, host-only opcode.
 #define FETCH() do {                                                                      \
-        if (sflag) {                                                                      \
+        if (sflag && pc < sn) {                                                           \
             const uint4 q_ = s_pd[pc];        /* s_pd[n_instr] is the END sentinel */     \
             pd = make_uint2(q_.x, q_.y); prun = make_uint2(q_.z, q_.w);                   \
         } else if (pc >= C.n_instr) {                                                     \
             pd = make_uint2(0u, ((uint32_t)K_END << 17) | PD_SPECIAL);                    \
+            prun = make_uint2(0u, 0u);                                                    \
         } else {                                                                          \
+            prun = make_uint2(0u, 0u);        /* no runs beyond the staged prefix */      \
             const uint32_t o_ = gops[pc];                                                 \
             const uint2 d_ = s_dec[o_];                                                   \
             const uint64_t hm_ = o_ < 64u ? m0 : o_ < 128u ? m1 : o_ < 192u ? m2 : m3;    \
@@ -1072,7 +1126,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             const uint32_t rx = __builtin_amdgcn_readlane(prun.x, lead);
             const uint32_t ry = __builtin_amdgcn_readlane(prun.y, lead);
             const uint32_t rlen = rx & 0xffu;
-            if (rlen >= 2u) {
+            if (rlen >= 2u && upc + rlen <= ns) {
                 const uint32_t rneed = (rx >> 8) & 0xffu, rpeak = (rx >> 16) & 0xffu;
                 // a run may end with a JUMP (rjk 1) or JUMPI (2): rsimple plain steps first
                 const uint32_t rjk = (rx >> 24) & 3u, rsimple = rjk ? rlen - 1u : rlen;
@@ -1108,7 +1162,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                             const uint32_t rop = y & 0xffu;
                             switch ((y >> 17) & 31u) {
                             case K_PUSH:
-                                V.set_wstack(s, ld_word((const l_u4 *)s_push, upc + k));
+                                V.set_wstack(s, PUSH_IMM(upc + k));
                                 ++s;
                                 break;
                             case K_DUP:
@@ -1150,10 +1204,11 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                             const bool take = rjk == 1u || !u_iszero(V.wstack(s - 2u));
                             uint32_t idx = MG_JRES_NONE;
                             if (take && u_fits32(tgt) && tgt.w[0] < C.n_jres) {
-                                if (jflag) { idx = s_jr[tgt.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
+                                if (jflag && tgt.w[0] < jn) { idx = s_jr[tgt.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
                                 else idx = a32[C.jres_off + tgt.w[0]];
                             }
-                            if (!take || (idx != MG_JRES_NONE && (s_pd[idx].y & 0xffu) == 0x5bu)) {
+                            if (!take || (idx != MG_JRES_NONE &&
+                                          (idx < sn ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu)) {
                                 nsp = s - rjk;
                                 npc = take ? idx : upc + rlen;
                                 nexec = executed + rlen;
@@ -1174,7 +1229,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                             const uint32_t rop = y & 0xffu;
                             switch ((y >> 17) & 31u) {
                             case K_PUSH: {
-                                const U256 v = ld_word((const l_u4 *)s_push, upc + k);
+                                const U256 v = PUSH_IMM(upc + k);
                                 if (sp >= 2u) V.set_stack(sp - 2u, T1);
                                 T1 = T0; T0 = v; ++sp;
                                 break;
@@ -1236,7 +1291,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
         CLK_MARK(op);
         if (cov_on) {
-            if (sflag) s_cov[pc] = 1;
+            if (sflag && pc < ns) s_cov[pc] = 1;
             else cov[C.cov_off + pc] = 1;
         }
         if (prof) atomicAdd(&s_prof[op], 1u);
@@ -1255,7 +1310,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         switch (kind) {
         case K_PUSH:
             ok = gas_ok && sp + 1u <= stack_lim;
-            if (ok) PUSHV(sflag ? ld_word((const l_u4 *)s_push, pc) : ld_word(gv(a32 + C.push_off), pc));
+            if (ok) PUSHV(psflag ? ld_word((const l_u4 *)s_push, pc) : ld_word(gv(a32 + C.push_off), pc));
             break;
         case K_DUP: {
             const uint32_t k = op - 0x7fu;
@@ -1298,11 +1353,11 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             if (take) {
                 uint32_t idx = MG_JRES_NONE;
                 if (u_fits32(T0) && T0.w[0] < C.n_jres) {
-                    if (jflag) { idx = s_jr[T0.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
+                    if (jflag && T0.w[0] < jn) { idx = s_jr[T0.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
                     else idx = a32[C.jres_off + T0.w[0]];
                 }
                 ok = ok && idx != MG_JRES_NONE &&
-                     (sflag ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu;
+                     ((sflag && idx < sn) ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu;
                 npc = idx;
             }
             if (ok) {
@@ -1407,6 +1462,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (live) FETCH();
     }
 #undef FETCH
+#undef PUSH_IMM
     CLK_MARK(258u);
 
     if (run0) {
@@ -1414,6 +1470,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (sp >= 1u) V.set_stack(sp - 1u, T0);
         if (sp >= 2u) V.set_stack(sp - 2u, T1);
         for (uint32_t k = 0; k < min(sp, win); ++k) V.set_gstack(k, V.wstack(k));
+        for (uint32_t k = 0; k < min(msize >> 2, mw); ++k) V.set_gmdw(k, V.lmdw(k));
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;
@@ -1437,7 +1494,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     if (staged && cov_on) {
         __syncthreads();
         const DevCode BC = codes[bcode];
-        for (uint32_t i = threadIdx.x; i < BC.n_instr; i += blockDim.x)
+        for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x)
             if (s_cov[i]) cov[BC.cov_off + i] = 1;
     }
     if (prof) {

@@ -39,6 +39,7 @@ struct mg_ctx {
     bool have_lanes = false, uploaded = false, init_fresh = false;
     uint32_t loop_bound = 0;             // mg_set_loop_bound (0: BoundedLoops off)
     uint32_t lpw = 64;                   // kernel-1 lanes per wave (MG_LANES_PER_WAVE: 64, 32, 16)
+    std::vector<uint8_t> code_used;      // codes uploaded into the current batch (LDS plan)
     DevLanes L{};
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
@@ -426,6 +427,7 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     HIPX(ctx, hipSetDevice(ctx->device));
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     free_lanes(ctx);
+    ctx->code_used.assign(ctx->codes.size(), 0);
     ctx->cfg = *cfg;
     DevLanes &L = ctx->L;
     L.n = cfg->n_lanes;
@@ -615,8 +617,10 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
     HIPX(ctx, hipSetDevice(ctx->device));
     DevLanes &L = ctx->L;
     // validate code ids and capacities on the host before any kernel sees them
+    if (ctx->code_used.size() < ctx->codes.size()) ctx->code_used.resize(ctx->codes.size(), 0);
     for (uint32_t i = 0; i < n; ++i) {
         if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
+        ctx->code_used[h->code_id[i]] = 1;
         if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
             h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap ||
             (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u) ||
@@ -742,27 +746,83 @@ extern "C" int mg_lanes_reset(mg_ctx *ctx) {
     return MG_OK;
 }
 
-// LDS plan of one launch: the largest loaded code is pre-decoded into LDS (up to
-// 1023 instructions, 41 B each, plus the END sentinel) with its jump-resolve
-// table (2 B per byte address, up to 8192), and the rest of the 160 KiB CU
-// budget share of one block (64 / lpw blocks per CU), minus a margin for the
-// static arrays, holds the stack window (2 x 16 B per lane of the block per
-// slot: 8 KiB at 256 lanes), at most 16 slots.
+// LDS plan of one launch.  One block's share of the 160 KiB CU budget (64 / lpw
+// blocks per CU, one wave per SIMD each) minus a margin for the static arrays
+// holds the stack window (2 x 16 B per lane of the block per slot: 8 KiB at 256
+// lanes, at most 16 slots) and the largest loaded code: pre-decoded entries
+// (16 B per instruction + the END sentinel), coverage bytes (1 B) and the
+// jump-resolve table (2 B per byte address).  When the whole code, its push
+// immediates (32 B per instruction) and a 16-slot window fit, everything is
+// staged (push_lds).  Otherwise the push immediates stay in the code arena
+// (read at wave-uniform addresses), the window shrinks to MIN_WIN slots, and the
+// code gets the rest: a prefix of the instructions and of the jump targets when
+// even that is too little (lane_step.cuh decodes the remainder from HBM).
 // lanes per kernel-1 workgroup: 4 waves of ctx->lpw lanes
 static inline uint32_t lane_block(const mg_ctx *ctx) { return (LANE_BLOCK / 64u) * ctx->lpw; }
 
-static void lds_plan(const mg_ctx *ctx, uint32_t &win, uint32_t &pd_cap, uint32_t &jr_cap, size_t &bytes) {
+struct LdsPlan {
+    uint32_t win, pd_cap, jr_cap, push_lds, mw32;   // mw32: memory window, 32-byte words per lane
+    size_t bytes;
+};
+
+// default LDS memory window per lane (bytes, multiple of 32): Solidity's scratch
+// words, free-memory pointer, zero slot and first allocation (0x00-0x9f)
+#define MEMWIN_DEFAULT 160u
+
+static LdsPlan lds_plan(const mg_ctx *ctx) {
+    static const uint32_t MAX_WIN = 16u, MIN_WIN = 10u;
+    // sized for the largest code the batch's lanes were uploaded with (all codes
+    // when none is marked)
     uint32_t maxn = 0, maxj = 0;
-    for (const DevCode &c : ctx->codes) { maxn = std::max(maxn, c.n_instr); maxj = std::max(maxj, c.n_jres); }
-    pd_cap = (std::min<uint32_t>(maxn, 1023u) + 1u + 15u) & ~15u;   // + END sentinel
-    jr_cap = (std::min<uint32_t>(maxj, 8192u) + 15u) & ~15u;
-    const size_t code_bytes = (size_t)pd_cap * (8 + 8 + 32 + 1) + (size_t)jr_cap * 2;
-    // 64 / lpw blocks share a CU (one wave per SIMD each), so each gets that share
+    bool any = false;
+    for (size_t k = 0; k < ctx->code_used.size() && k < ctx->codes.size(); ++k) any |= ctx->code_used[k] != 0;
+    for (size_t k = 0; k < ctx->codes.size(); ++k) {
+        if (any && (k >= ctx->code_used.size() || !ctx->code_used[k])) continue;
+        maxn = std::max(maxn, ctx->codes[k].n_instr); maxj = std::max(maxj, ctx->codes[k].n_jres);
+    }
     const size_t budget = 160u * 1024u / (64u / ctx->lpw) - 6144u;
     const size_t slot_bytes = 2u * lane_block(ctx) * 16u;
-    win = (uint32_t)std::min<size_t>(16, budget > code_bytes ? (budget - code_bytes) / slot_bytes : 0);
-    win = std::min<uint32_t>(win, ctx->L.stack_cap);
-    bytes = (size_t)win * slot_bytes + code_bytes + 16;
+    const uint32_t win_cap = std::min<uint32_t>(MAX_WIN, ctx->L.stack_cap);
+    LdsPlan p{};
+    const uint32_t pd_full = (std::min<uint32_t>(maxn, 0xfffeu) + 1u + 15u) & ~15u;   // + END sentinel
+    const uint32_t jr_full = (maxj + 15u) & ~15u;
+    const size_t full = (size_t)pd_full * (16 + 32 + 1) + (size_t)jr_full * 2;
+    if (maxn < 0xfffeu && full + (size_t)win_cap * slot_bytes <= budget) {
+        p.pd_cap = pd_full; p.jr_cap = jr_full; p.push_lds = 1u;
+    } else {
+        const size_t min_win = std::min<uint32_t>(MIN_WIN, win_cap);
+        const size_t avail = budget > min_win * slot_bytes ? budget - min_win * slot_bytes : 0;
+        p.pd_cap = (uint32_t)std::min<size_t>(pd_full, (avail / 17u) & ~(size_t)15u);
+        p.jr_cap = (uint32_t)std::min<size_t>(jr_full, ((avail - (size_t)p.pd_cap * 17u) / 2u) & ~(size_t)15u);
+        p.push_lds = 0u;
+    }
+    // test / A/B overrides: MG_K1_PUSH=global, MG_K1_PD_CAP=n, MG_K1_JR_CAP=n (a
+    // smaller staged prefix exercises the HBM-decoded remainder on small codes)
+    const char *ev = getenv("MG_K1_PUSH");
+    if (ev && std::string(ev) == "global") p.push_lds = 0u;
+    if ((ev = getenv("MG_K1_PD_CAP")) != nullptr) {
+        const uint32_t c = (uint32_t)strtoul(ev, nullptr, 10);
+        if (c >= 1u && c < p.pd_cap) { p.pd_cap = c; p.push_lds = 0u; }
+    }
+    if ((ev = getenv("MG_K1_JR_CAP")) != nullptr) {
+        const uint32_t c = (uint32_t)strtoul(ev, nullptr, 10);
+        if (c < p.jr_cap) p.jr_cap = c;
+    }
+    const size_t code_bytes = (size_t)p.pd_cap * (16 + (p.push_lds ? 32 : 0) + 1) + (size_t)p.jr_cap * 2;
+    // memory window (MG_K1_MEMWIN=bytes overrides; 0 = off): taken from the stack
+    // window's share only while that keeps at least MIN_WIN slots
+    uint32_t mwb = MEMWIN_DEFAULT;
+    if ((ev = getenv("MG_K1_MEMWIN")) != nullptr) mwb = (uint32_t)strtoul(ev, nullptr, 10);
+    mwb = std::min<uint32_t>(std::min<uint32_t>(mwb, ctx->L.mem_cap), 255u * 32u) & ~31u;
+    const size_t lanes = lane_block(ctx);
+    size_t left = budget > code_bytes ? budget - code_bytes : 0;
+    const size_t min_stack = (size_t)std::min<uint32_t>(MIN_WIN, win_cap) * slot_bytes;
+    while (mwb > 0u && (size_t)mwb * lanes + min_stack > left) mwb -= 32u;
+    p.mw32 = mwb / 32u;
+    left -= (size_t)mwb * lanes;
+    p.win = (uint32_t)std::min<size_t>(win_cap, left / slot_bytes);
+    p.bytes = (size_t)p.win * slot_bytes + (size_t)mwb * lanes + code_bytes + 16;
+    return p;
 }
 
 // MG_K1_RUNS=reg: straight-line runs in the register form only (A/B switch,
@@ -777,9 +837,7 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        const DevResetImage *reset = nullptr) {
     const uint64_t zero[4] = {0, 0, 0, 0};
     const uint64_t *m = hook_mask ? hook_mask : zero;
-    uint32_t win = 0, pd_cap = 0, jr_cap = 0;
-    size_t lds = 0;
-    lds_plan(ctx, win, pd_cap, jr_cap, lds);
+    const LdsPlan P = lds_plan(ctx);
     if (ctx->loop_bound && ctx->L.trace_cap) {
         // the loop-count hash compares 16-bit byte addresses (EVM code < 64 KiB)
         for (const DevCode &c : ctx->codes)
@@ -799,10 +857,11 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
         return set_err(ctx, MG_EINVAL, "launch of %u blocks exceeds the %u statistics slots",
                        blocks_for(ctx->L.n, lane_block(ctx)), ctx->ctr_cap);
     hipLaunchKernelGGL(loop_bound ? k_lane_step<true> : k_lane_step<false>, dim3(blocks_for(ctx->L.n, lane_block(ctx))),
-                       dim3(LANE_BLOCK), lds, ctx->stream, ctx->L,
+                       dim3(LANE_BLOCK), P.bytes, ctx->stream, ctx->L,
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
-                       m[2], m[3], max_steps, max_depth, ctr, prof, win, pd_cap, jr_cap, horizon,
-                       loop_bound, reset ? *reset : DevResetImage{}, ctx->lpw | k1_flags());
+                       m[2], m[3], max_steps, max_depth, ctr, prof, P.win, P.pd_cap, P.jr_cap, horizon,
+                       loop_bound, reset ? *reset : DevResetImage{},
+                       ctx->lpw | k1_flags() | (P.push_lds ? 0x200u : 0u) | (P.mw32 << 16));
     HIPX(ctx, hipGetLastError());
     return MG_OK;
 }
