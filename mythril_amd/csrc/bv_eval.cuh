@@ -42,6 +42,8 @@ enum BvOp : uint32_t {
     BV_TAB,            // A = key k0, B = key k1, w3 = table | part << 20 | lo << 21:
                        // bits [256 part + lo, +width) of the model's array / function
                        // interpretation at (k0, k1), else its default (lower.py)
+    BV_UMIN, BV_UMAX,  // ite(cmp(A, B), A, B) folded by the compiler (flatten._fold_select)
+    BV_SMIN, BV_SMAX,  // signed at `width`
     BV_NUM_OPS
 };
 
@@ -304,11 +306,15 @@ __global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ 
                 }
                 case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
                 case BV_TAB: r = bv_table(c, A, B, rc); break;
+                case BV_UMIN: r = u_select(u_lt(B, A), B, A); break;
+                case BV_UMAX: r = u_select(u_lt(A, B), B, A); break;
+                case BV_SMIN: r = u_select(u_slt(bv_sext(B, width), bv_sext(A, width)), B, A); break;
+                case BV_SMAX: r = u_select(u_slt(bv_sext(A, width), bv_sext(B, width)), B, A); break;
                 default: r = u_zero(); break;
                 }
             }
             }
-            r = bv_mask(r, width);
+            if (width < 256u) r = bv_mask(r, width);     // width is wave-uniform
             acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;

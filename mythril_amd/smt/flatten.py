@@ -31,6 +31,49 @@ _CMP = {"eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", 
         "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u"}
 
 
+_MINMAX = {  # ite(cmp(x, y), x, y) -> op(x, y); ite(cmp(x, y), y, x) -> the other one
+    "bvult": ("bvumin", "bvumax"), "bvule": ("bvumin", "bvumax"),
+    "bvugt": ("bvumax", "bvumin"), "bvuge": ("bvumax", "bvumin"),
+    "bvslt": ("bvsmin", "bvsmax"), "bvsle": ("bvsmin", "bvsmax"),
+    "bvsgt": ("bvsmax", "bvsmin"), "bvsge": ("bvsmax", "bvsmin"),
+}
+
+
+def _fold_select(root: Node) -> Node:
+    """Peephole over the lowered DAG: a select between the two operands of its
+    own compare is one min/max instruction, and ite(x == y, x, y) is y (with
+    x == y both branches are the same number).  Ties pick either operand: the
+    value is the same.  Every other node is rebuilt only when a child changed."""
+    memo: Dict[Node, Node] = {}
+    stack = [(root, False)]
+    while stack:
+        n, ready = stack.pop()
+        if n in memo:
+            continue
+        if not n.args:
+            memo[n] = n
+            continue
+        if not ready:
+            stack.append((n, True))
+            stack.extend((c, False) for c in n.args if c not in memo)
+            continue
+        args = tuple(memo[c] for c in n.args)
+        out = n if args == n.args else Node(n.op, n.width, args, n.param)
+        if n.op == "ite" and n.width > 1:
+            c, a, b = args
+            if c.op in _MINMAX or c.op == "eq":
+                x, y = c.args
+                if (x, y) == (a, b) or (y, x) == (a, b):
+                    same = (x, y) == (a, b)
+                    if c.op == "eq":
+                        out = b
+                    else:
+                        lo_hi = _MINMAX[c.op]
+                        out = Node(lo_hi[0] if same else lo_hi[1], n.width, (x, y) if same else (x, y))
+        memo[n] = out
+    return memo[root]
+
+
 class _Virt:
     """One device instruction before slot assignment."""
     __slots__ = ("op", "width", "args", "imm", "node")
@@ -137,6 +180,11 @@ class Compiler:
             return
         if op in ("and", "or") and len(x.args) == 1:
             virts.append(_Virt("copy", 1, [arg(x.args[0])]))
+        elif op == "zero_extend" and x.args[0] in vid:
+            # values are kept masked to their width, so zero-extending a computed
+            # value changes no limb: the node aliases its operand's instruction
+            vid[x] = vid[x.args[0]]
+            return
         elif op == "extract":
             virts.append(_Virt("extract", x.width, [arg(x.args[0])], imm=x.param[1]))
         elif op == "sign_extend":
@@ -160,7 +208,7 @@ class Compiler:
 
     # -- slots + encoding -----------------------------------------------------
     def compile(self, root: Node) -> np.ndarray:
-        root = self.lowering.lower(root)
+        root = _fold_select(self.lowering.lower(root))
         virts = self._schedule(root)
         n = len(virts)
         uses: Dict[int, List[Tuple[int, int]]] = {}

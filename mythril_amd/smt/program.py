@@ -17,7 +17,9 @@ OPS = ["copy", "bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem"
        "bvand", "bvor", "bvxor", "bvnot", "bvneg", "bvshl", "bvlshr", "bvashr",
        "eq", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
        "and", "or", "xor", "not", "implies", "ite", "extract", "concat", "zero_extend",
-       "sign_extend", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "distinct", "tab"]
+       "sign_extend", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "distinct", "tab",
+       # compiler-internal: ite(cmp(x, y), x, y) folded by flatten._fold_select
+       "bvumin", "bvumax", "bvsmin", "bvsmax"]
 OPCODE = {name: i for i, name in enumerate(OPS)}
 UNARY = {"copy", "bvnot", "bvneg", "not", "extract", "zero_extend", "sign_extend"}
 REF_ACC, REF_SLOT, REF_VAR, REF_CONST = 0, 1, 2, 3

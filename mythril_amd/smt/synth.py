@@ -100,108 +100,130 @@ def _w0(op, width, store_slot=None):
 
 
 def c4_programs(dr: Draws) -> ProgramBatch:
-    """Kernel-2 programs of every DAG, built with array operations.
+    """Kernel-2 programs of every DAG, built with array operations, in the form
+    flatten.Compiler emits for dag_expr(dr, i) (copy-free operand references,
+    select-of-compare folded to min/max by flatten._fold_select, zero-extension
+    of a computed value aliased) with this generator's own slot schedule, which
+    never needs more than two slots: S0 keeps the spine across a compare that
+    feeds the Bool accumulator, S1 the accumulator.
 
-    Each level is a frame of up to 3 instructions; frames are compacted, then the
-    'save spine to slot 0' store bit is set on the instruction that produced the
-    spine right before an ite/compare level."""
+    The spine of level l is an operand reference `spin`: ACC when the previous
+    level's last instruction left it in the accumulator, S0 when a compare-And
+    level sat in between, or a leaf (the head variable, or the leaf an
+    ite(spine == leaf, spine, leaf) level reduces to)."""
     n, L = dr.n, LEVELS
-    F = 3
-    ins = np.zeros((n, L, F, 4), dtype=np.uint32)
-    valid = np.zeros((n, L, F), dtype=bool)
+    cap = 3 * L + 2
+    out = np.zeros((n, cap, 4), dtype=np.uint32)
+    cnt = np.zeros(n, dtype=np.int64)
+    last = np.full(n, -1, dtype=np.int64)
+    rows_all = np.arange(n)
     leaf = dr.leaf_ref()
     ACC = np.uint32(REF_ACC << 30)
     S0 = np.uint32(REF_SLOT << 30 | 0)
     S1 = np.uint32(REF_SLOT << 30 | 1)
-    cls, sub = dr.cls, dr.sub.astype(np.int64)
 
-    def put(mask, f, op_codes, width, a, b=0, c=0):
-        if not mask.any():
+    def emit(mask, w0, a, b=0, c=0):
+        r = rows_all[mask]
+        if r.size == 0:
             return
-        w0 = (np.asarray(op_codes, dtype=np.uint32) | np.uint32(width << 8))
-        ins[mask, f, 0] = w0 if np.ndim(w0) == 0 else w0[mask]
-        for k, x in ((1, a), (2, b), (3, c)):
-            ins[mask, f, k] = x if np.ndim(x) == 0 else np.asarray(x)[mask]
-        valid[mask, f] = True
+        k = cnt[r]
 
-    # addsub
-    m = cls == ADDSUB
-    put(m, 0, np.where(sub % 2 == 0, OPCODE["bvadd"], OPCODE["bvsub"]), 256, ACC, leaf)
-    # logic: and / or / xor / not
-    m = cls == LOGIC
-    lop = np.choose(sub % 4, [OPCODE["bvand"], OPCODE["bvor"], OPCODE["bvxor"], OPCODE["bvnot"]])
-    put(m, 0, lop, 256, ACC, np.where(sub % 4 == 3, 0, leaf).astype(np.uint32))
-    # mul
-    put(cls == MUL, 0, OPCODE["bvmul"], 256, ACC, leaf)
-    # shifts by constant amounts
-    m = cls == SHIFT
-    sop = np.choose(sub % 3, [OPCODE["bvshl"], OPCODE["bvlshr"], OPCODE["bvashr"]])
-    put(m, 0, sop, 256, ACC, ((REF_CONST << 30) | (C_SMALL + dr.shift)).astype(np.uint32))
-    # extract + zero-extend / concat
-    m_zx = (cls == EXTCAT) & (sub % 2 == 0)
-    put(m_zx, 0, OPCODE["extract"], 128, ACC, dr.lo.astype(np.uint32))
-    put(m_zx, 1, OPCODE["zero_extend"], 256, ACC)
-    m_cc = (cls == EXTCAT) & (sub % 2 == 1)
-    put(m_cc, 0, OPCODE["extract"] | (1 << 17) | (0 << 18), 128, ACC, 0)     # store slot 0
-    put(m_cc, 1, OPCODE["extract"], 128, leaf, 0)
-    put(m_cc, 2, OPCODE["concat"], 256, S0, ACC, 128)
-    # ite: ite(leaf <u spine, spine, leaf)
-    m = cls == ITE
-    put(m, 0, OPCODE["bvult"], 1, leaf, ACC, 256)
-    put(m, 1, OPCODE["ite"], 256, ACC, S0, leaf)
-    # compare -> ite / And
-    m = cls == CMP
-    cop = np.choose(sub % 4, [OPCODE["eq"], OPCODE["bvult"], OPCODE["bvugt"], OPCODE["bvslt"]])
-    m_ite = m & ~dr.use_and
-    put(m_ite, 0, cop, 1, ACC, leaf, 256)
-    put(m_ite, 1, OPCODE["ite"], 256, ACC, S0, leaf)
-    m_and = m & dr.use_and
-    prior_and = np.cumsum(m_and, axis=1) - m_and          # and-uses before this level
-    first = m_and & (prior_and == 0)
-    later = m_and & (prior_and > 0)
-    put(first, 0, cop | (1 << 17) | (1 << 18), 1, ACC, leaf, 256)   # store slot 1
-    put(first, 1, OPCODE["copy"], 256, S0)
-    put(later, 0, cop, 1, ACC, leaf, 256)
-    put(later, 1, OPCODE["and"] | (1 << 17) | (1 << 18), 1, ACC, S1)
-    put(later, 2, OPCODE["copy"], 256, S0)
-    # div / rem
-    m = cls == DIVREM
-    put(m, 0, np.where(sub % 2 == 0, OPCODE["bvudiv"], OPCODE["bvurem"]), 256, ACC, leaf)
+        def pick(x):
+            return x if np.ndim(x) == 0 else np.asarray(x)[mask]
+        out[r, k, 0] = pick(w0)
+        out[r, k, 1] = pick(a)
+        out[r, k, 2] = pick(b)
+        out[r, k, 3] = pick(c)
+        last[r] = k
+        cnt[r] += 1
 
-    # spine saves: the instruction that produced the spine before an ite/cmp level
-    needs_save = (cls == ITE) | (cls == CMP)
-    nvalid = valid.sum(axis=2)                                     # (n, L) 1..3
-    # head: COPY(var spine0)
-    head = np.zeros((n, 1, 4), dtype=np.uint32)
-    head[:, 0, 0] = OPCODE["copy"] | (256 << 8)
-    head[:, 0, 1] = (REF_VAR << 30) | dr.spine0
-    save_head = needs_save[:, 0]
-    head[save_head, 0, 0] |= np.uint32(1 << 17)
-    prev_last = nvalid[:, :-1] - 1                                 # last frame slot of level l-1
-    rows, lv = np.nonzero(needs_save[:, 1:])
-    ins[rows, lv, prev_last[rows, lv], 0] |= np.uint32(1 << 17)    # slot 0
+    def w(op, width):
+        return np.uint32(OPCODE[op] | (width << 8)) if isinstance(op, str) else \
+            (np.asarray(op, dtype=np.uint32) | np.uint32(width << 8))
+
+    # liveness (the compiler only emits what the root reaches): a level's spine
+    # is dead when every path to the root passes an ite(spine == leaf, ..)
+    # level before a compare uses it; a dead level emits nothing
+    live = np.zeros((n, L), dtype=bool)
+    nxt = np.ones(n, dtype=bool)
+    for l in range(L - 1, -1, -1):
+        c = dr.cls[:, l]
+        is_and = (c == CMP) & dr.use_and[:, l]
+        is_eq = (c == CMP) & ~dr.use_and[:, l] & (dr.sub[:, l] % 4 == 0)
+        live[:, l] = ~is_eq & (is_and | nxt)
+        nxt = np.where(is_eq, False, np.where(is_and, True, nxt))
+    spin = ((REF_VAR << 30) | dr.spine0).astype(np.uint32)    # the head variable, no copy
+    spin_acc = np.zeros(n, dtype=bool)
+    n_and = np.zeros(n, dtype=np.int64)
+    for l in range(L):
+        cls, sub, lf = dr.cls[:, l], dr.sub[:, l].astype(np.int64), leaf[:, l]
+        cls = np.where(live[:, l] | (cls == CMP), cls, -1)          # dead levels: nothing
+        A = np.where(spin_acc, ACC, spin).astype(np.uint32)
+        m_cmp = cls == CMP
+        m_and = m_cmp & dr.use_and[:, l]
+        # a compare-And level keeps the spine: save it to S0 if it is in the accumulator
+        sv = m_and & spin_acc
+        out[rows_all[sv], last[sv], 0] |= np.uint32(1 << 17)          # store to slot 0
+        produced = np.zeros(n, dtype=bool)
+        m = cls == ADDSUB
+        emit(m, w(np.where(sub % 2 == 0, OPCODE["bvadd"], OPCODE["bvsub"]), 256), A, lf)
+        produced |= m
+        m = cls == LOGIC
+        lop = np.choose(sub % 4, [OPCODE["bvand"], OPCODE["bvor"], OPCODE["bvxor"], OPCODE["bvnot"]])
+        emit(m, w(lop, 256), A, np.where(sub % 4 == 3, 0, lf).astype(np.uint32))
+        produced |= m
+        m = cls == MUL
+        emit(m, w("bvmul", 256), A, lf)
+        produced |= m
+        m = cls == SHIFT
+        sop = np.choose(sub % 3, [OPCODE["bvshl"], OPCODE["bvlshr"], OPCODE["bvashr"]])
+        emit(m, w(sop, 256), A, ((REF_CONST << 30) | (C_SMALL + dr.shift[:, l])).astype(np.uint32))
+        produced |= m
+        m = (cls == EXTCAT) & (sub % 2 == 0)          # zero_extend(extract): the extract alone
+        emit(m, w("extract", 128), A, dr.lo[:, l].astype(np.uint32))
+        produced |= m
+        m = (cls == EXTCAT) & (sub % 2 == 1)          # concat(low128(spine), low128(leaf))
+        emit(m, np.uint32(OPCODE["extract"] | (128 << 8) | (1 << 17)), A, 0)     # -> S0
+        emit(m, w("extract", 128), lf, 0)
+        emit(m, w("concat", 256), S0, ACC, 128)
+        produced |= m
+        m = cls == ITE                                # ite(leaf <u spine, spine, leaf)
+        emit(m, w("bvumax", 256), A, lf)
+        produced |= m
+        m_sel = m_cmp & ~dr.use_and[:, l]             # ite(cmp(spine, leaf), spine, leaf)
+        cop = sub % 4                                 # eq, ult, ugt, slt
+        fold = np.choose(cop, [0, OPCODE["bvumin"], OPCODE["bvumax"], OPCODE["bvsmin"]])
+        m = m_sel & (cop != 0) & live[:, l]
+        emit(m, w(fold, 256), A, lf)
+        produced |= m
+        m_eq = m_sel & (cop == 0)                     # = leaf: no instruction
+        m = cls == DIVREM
+        emit(m, w(np.where(sub % 2 == 0, OPCODE["bvudiv"], OPCODE["bvurem"]), 256), A, lf)
+        produced |= m
+        # compare feeding the Bool accumulator (slot 1)
+        cmpop = np.choose(cop, [OPCODE["eq"], OPCODE["bvult"], OPCODE["bvugt"], OPCODE["bvslt"]])
+        first = m_and & (n_and == 0)
+        later = m_and & (n_and > 0)
+        emit(first, np.asarray(cmpop, dtype=np.uint32) | np.uint32((1 << 8) | (1 << 17) | (1 << 18)),
+             A, lf, 256)
+        emit(later, w(cmpop, 1), A, lf, 256)
+        emit(later, np.uint32(OPCODE["and"] | (1 << 8) | (1 << 17) | (1 << 18)), ACC, S1)
+        n_and += m_and
+        # the next level's spine
+        spin = np.where(m_and, np.where(spin_acc, S0, spin), spin)
+        spin = np.where(m_eq, lf, spin).astype(np.uint32)
+        spin_acc = np.where(produced, True, np.where(m_and | m_eq, False, spin_acc))
+        spin = np.where(produced, ACC, spin).astype(np.uint32)
     # root: (spine >u leaf_root) [and accumulator]
-    has_and = m_and.any(axis=1)
-    root = np.zeros((n, 2, 4), dtype=np.uint32)
     root_ref = np.where(dr.root_is_var, (REF_VAR << 30) | dr.root_var,
                         (REF_CONST << 30) | dr.root_const).astype(np.uint32)
-    root[:, 0, 0] = OPCODE["bvugt"] | (1 << 8)
-    root[:, 0, 1] = ACC
-    root[:, 0, 2] = root_ref
-    root[:, 0, 3] = 256
-    root[:, 1, 0] = OPCODE["and"] | (1 << 8)
-    root[:, 1, 1] = ACC
-    root[:, 1, 2] = S1
-    root_valid = np.stack([np.ones(n, bool), has_and], axis=1)
-    # compact
-    body = ins.reshape(n, L * F, 4)
-    body_valid = valid.reshape(n, L * F)
-    allins = np.concatenate([head, body, root], axis=1)
-    allvalid = np.concatenate([np.ones((n, 1), bool), body_valid, root_valid], axis=1)
-    counts = allvalid.sum(axis=1)
-    insns = allins[allvalid]
+    A = np.where(spin_acc, ACC, spin).astype(np.uint32)
+    emit(np.ones(n, dtype=bool), w("bvugt", 1), A, root_ref, 256)
+    emit(n_and > 0, w("and", 1), ACC, S1)
+    valid = np.arange(cap)[None, :] < cnt[:, None]
+    insns = out[valid]
     off = np.zeros(n + 1, dtype=np.uint32)
-    off[1:] = np.cumsum(counts)
+    off[1:] = np.cumsum(cnt)
     return ProgramBatch(insns.astype(np.uint32), off, const_pool(), 2,
                         [f"x{i}" for i in range(N_VARS)], [256] * N_VARS)
 
@@ -317,8 +339,8 @@ def _insn_cost(op: int, width: int) -> float:
         return float(w)
     if name in ("bvadd", "bvsub", "bvneg"):
         return 2.0 * w
-    if name in ("bvshl", "bvlshr", "bvashr"):
-        return 3.0 * w
+    if name in ("bvshl", "bvlshr", "bvashr", "bvumin", "bvumax", "bvsmin", "bvsmax"):
+        return 3.0 * w          # min/max: the folded compare (2w) + select (w)
     if name == "bvmul":
         return w * (w + 1) / 2 + w * (w - 1) / 2 + 2.0 * w * w
     if name in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"):

@@ -22,7 +22,8 @@ enum {
     OP_AND, OP_OR, OP_XOR, OP_NOT, OP_NEG, OP_SHL, OP_LSHR, OP_ASHR,
     OP_EQ, OP_ULT, OP_ULE, OP_UGT, OP_UGE, OP_SLT, OP_SLE, OP_SGT, OP_SGE,
     OP_BAND, OP_BOR, OP_BXOR, OP_BNOT, OP_BIMPLIES, OP_ITE, OP_EXTRACT, OP_CONCAT,
-    OP_ZEXT, OP_SEXT, OP_ADD_NOOVF_U, OP_MUL_NOOVF_U, OP_SUB_NOUDF_U, OP_NE, OP_TAB
+    OP_ZEXT, OP_SEXT, OP_ADD_NOOVF_U, OP_MUL_NOOVF_U, OP_SUB_NOUDF_U, OP_NE, OP_TAB,
+    OP_UMIN, OP_UMAX, OP_SMIN, OP_SMAX
 };
 
 static u256 w_mask(u256 v, unsigned w) {
@@ -163,6 +164,10 @@ static int eval_one(const job_t *j, uint32_t d, uint32_t m) {
         }
         case OP_SUB_NOUDF_U: r = w_bool(!u_lt(a, b)); break;
         case OP_TAB: r = table_lookup(j, a, b, w[3], m); break;
+        case OP_UMIN: r = u_lt(b, a) ? b : a; break;
+        case OP_UMAX: r = u_lt(a, b) ? b : a; break;
+        case OP_SMIN: r = u_slt(w_sext(b, width), w_sext(a, width)) ? b : a; break;
+        case OP_SMAX: r = u_slt(w_sext(a, width), w_sext(b, width)) ? b : a; break;
         default: r = u_zero(); break;
         }
         r = w_mask(r, width);

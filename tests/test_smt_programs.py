@@ -35,8 +35,38 @@ def test_c4_full_size_shape_and_determinism():
     b = synth.c4_programs(synth.Draws(1000, seed=synth.C4_SEED))
     assert np.array_equal(a.insns, b.insns) and np.array_equal(a.prog_off, b.prog_off)
     lens = np.diff(a.prog_off.astype(np.int64))
-    assert 33 <= lens.min() and lens.max() <= 2 + 3 * synth.LEVELS + 1
-    assert 40 < lens.mean() < 70          # ~65 nodes per DAG, about 50 instructions
+    # a level an ite(spine == leaf, spine, leaf) discards emits nothing, so a DAG
+    # can shrink to its root compare
+    assert 1 <= lens.min() and lens.max() <= 2 + 3 * synth.LEVELS
+    assert 28 < lens.mean() < 40          # ~65 nodes per DAG, about 34 instructions
+
+
+def test_c4_programs_have_the_compilers_form():
+    """The generator emits what flatten.Compiler emits for the same DAG (no
+    copies, select-of-compare folded, zero-extension aliased, dead levels
+    dropped): per DAG the same multiset of opcodes, except that the compiler
+    also shares a repeated extract of the same leaf across levels (CSE through
+    an extra slot; the generator keeps to two slots), and a min/max of a value
+    with itself may fold either way."""
+    from collections import Counter
+    from mythril_amd.smt.program import OPS
+    norm = {"bvumax": "bvumin", "bvsmax": "bvsmin"}
+    dr = synth.Draws(300, seed=synth.C4_SEED + 5)
+    prog = synth.c4_programs(dr)
+    n = exact = 0
+    for i in range(300):
+        try:
+            p = Compiler().compile(synth.dag_expr(dr, i))
+        except Unsupported:
+            continue
+        a = Counter(OPS[int(w) & 0xFF] for w in p[:, 0])
+        b = Counter(OPS[int(w) & 0xFF] for w in prog.program(i)[:, 0])
+        exact += a == b
+        extra = b - a
+        assert not (a - b) - Counter({k: v for k, v in (a - b).items() if k in norm or k in norm.values()}), i
+        assert set(extra) <= {"extract"} | set(norm) | set(norm.values()), (i, extra)
+        n += 1
+    assert n > 250 and exact > 0.9 * n
 
 
 def _random_constraints(rng, n_terms=6):
