@@ -36,6 +36,15 @@ struct DevLanes {
     uint32_t *rec;       // [rec_cap][N]
 };
 
+// Symbolic planes (mg_sym_alloc): stack tags, expression arena, constants.
+struct DevSym {
+    uint32_t node_cap, const_cap;
+    uint32_t *stag;      // [stack_cap][N]
+    uint4 *node;         // [node_cap][N]
+    uint4 *cval;         // [const_cap][N][2]
+    uint32_t *n_nodes, *n_consts;   // [N]
+};
+
 // Resident initial image of a batch (mg_lanes_reset); passed to the stepping
 // kernel when it re-initialises every lane itself before stepping
 // (mg_run_batches), pc == nullptr otherwise.

@@ -1004,7 +1004,9 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         __syncthreads();
     }
     uint32_t executed = 0;
-    const bool run0 = status == ST_RUNNING;
+    // symbolic lanes (MG_LANE_SYMBOLIC) are k_sym_step's: counted as running, untouched
+    const bool sym_lane = in_range && status == ST_RUNNING && (L.flags[lane] & 16u) != 0u;
+    const bool run0 = status == ST_RUNNING && !sym_lane;
     // block-uniform facts in scalar registers
     const uint32_t sflag = __builtin_amdgcn_readfirstlane(staged ? 1u : 0u);
     const uint32_t jflag = __builtin_amdgcn_readfirstlane(jstaged ? 1u : 0u);

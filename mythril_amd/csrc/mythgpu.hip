@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include "bv_eval.cuh"
 #include "lane_step.cuh"
+#include "sym_step.cuh"
 
 // ------------------------------------------------------------------ context
 struct mg_ctx {
@@ -41,6 +42,7 @@ struct mg_ctx {
     uint32_t lpw = 64;                   // kernel-1 lanes per wave (MG_LANES_PER_WAVE: 64, 32, 16)
     std::vector<uint8_t> code_used;      // codes uploaded into the current batch (LDS plan)
     DevLanes L{};
+    DevSym S{};                          // symbolic planes (mg_sym_alloc), freed with the lanes
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
     uint32_t *i_pc = nullptr, *i_depth = nullptr, *i_status = nullptr, *i_aux = nullptr,
@@ -210,6 +212,7 @@ static void free_lanes(mg_ctx *ctx) {
     ctx->lane_allocs.clear();
     ctx->have_lanes = ctx->uploaded = false;
     ctx->L = DevLanes{};
+    ctx->S = DevSym{};
     ctx->d_ctr = nullptr;
 }
 
@@ -683,6 +686,74 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
     return MG_OK;
 }
 
+// ---- symbolic planes ---------------------------------------------------------
+extern "C" int mg_sym_alloc(mg_ctx *ctx, uint32_t node_cap, uint32_t const_cap) {
+    if (!ctx) return MG_EINVAL;
+    if (!ctx->have_lanes) return set_err(ctx, MG_ESTATE, "mg_sym_alloc before mg_lanes_alloc");
+    if (ctx->S.node) return set_err(ctx, MG_ESTATE, "mg_sym_alloc: already allocated for this batch");
+    if (node_cap == 0u || const_cap == 0u || node_cap >= SYM_CONST || const_cap >= SYM_CONST)
+        return set_err(ctx, MG_EINVAL, "mg_sym_alloc: bad capacities");
+    HIPX(ctx, hipSetDevice(ctx->device));
+    DevSym S{};
+    S.node_cap = node_cap;
+    S.const_cap = const_cap;
+    const size_t N = ctx->L.N;
+    auto get = [&](void **p, size_t bytes) -> int {
+        if (hipMalloc(p, bytes) != hipSuccess) return set_err(ctx, MG_ENOMEM, "mg_sym_alloc: %zu bytes", bytes);
+        ctx->lane_allocs.push_back(*p);
+        return hipMemsetAsync(*p, 0, bytes, ctx->stream) == hipSuccess ? MG_OK : MG_EDEVICE;
+    };
+    int rc;
+    if ((rc = get((void **)&S.stag, (size_t)ctx->L.stack_cap * N * 4))) return rc;
+    if ((rc = get((void **)&S.node, (size_t)node_cap * N * 16))) return rc;
+    if ((rc = get((void **)&S.cval, (size_t)const_cap * N * 32))) return rc;
+    if ((rc = get((void **)&S.n_nodes, N * 4))) return rc;
+    if ((rc = get((void **)&S.n_consts, N * 4))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->S = S;
+    return MG_OK;
+}
+
+static int check_sym_shape(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx->S.node) return set_err(ctx, MG_ESTATE, "mg_sym_alloc first");
+    if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
+        return set_err(ctx, MG_EINVAL, "symbolic lane range [%u,%u) outside batch of %u", first, first + n, ctx->L.n);
+    if (h->stack_cap > ctx->L.stack_cap || h->node_cap > ctx->S.node_cap || h->const_cap > ctx->S.const_cap)
+        return set_err(ctx, MG_EINVAL, "symbolic host image capacities exceed the allocation");
+    return MG_OK;
+}
+
+extern "C" int mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_sym_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    for (uint32_t i = 0; i < n; ++i)
+        if (h->n_nodes[i] > h->node_cap || h->n_consts[i] > h->const_cap)
+            return set_err(ctx, MG_EINVAL, "lane %u: arena exceeds its host capacities", first + i);
+    if ((rc = up_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
+    if ((rc = up_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = up_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
+    if ((rc = up_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
+    if ((rc = up_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
+    return MG_OK;
+}
+
+extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_sym_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    if ((rc = down_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
+    if ((rc = down_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = down_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
+    if ((rc = down_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
+    if ((rc = down_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
+    return MG_OK;
+}
+
 extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n) {
     if (!ctx) return MG_EINVAL;
     int rc;
@@ -863,6 +934,13 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        loop_bound, reset ? *reset : DevResetImage{},
                        ctx->lpw | k1_flags() | (P.push_lds ? 0x200u : 0u) | (P.mw32 << 16));
     HIPX(ctx, hipGetLastError());
+    // symbolic lanes: the concrete stepper left them untouched (counted as running)
+    if (ctx->S.node && !prof && !reset) {
+        hipLaunchKernelGGL(k_sym_step, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, ctx->S,
+                           ctx->d_codes, ctx->d_a8, ctx->d_a32, m[0], m[1], m[2], m[3], max_steps, max_depth,
+                           horizon, ctr, lane_block(ctx));
+        HIPX(ctx, hipGetLastError());
+    }
     return MG_OK;
 }
 

@@ -86,28 +86,45 @@ class GpuDevice:
                                 shape.storage_cap, 1 if coverage else 0, shape.trace_cap,
                                 shape.rec_cap)
         self._check(self.lib.mg_lanes_alloc(self.ctx, ctypes.byref(cfg)), "mg_lanes_alloc")
+        if shape.node_cap:
+            self._check(self.lib.mg_sym_alloc(self.ctx, shape.node_cap, max(shape.const_cap, 1)),
+                        "mg_sym_alloc")
         self.shape = shape
 
     def upload(self, batch: LaneBatch, first: int = 0):
         soa = batch.soa()
         self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, batch.n),
                     "mg_lanes_upload")
+        if batch.symbolic:
+            s = batch.sym_soa_range(0, batch.n)
+            self._check(self.lib.mg_sym_upload(self.ctx, ctypes.addressof(s), first, batch.n), "mg_sym_upload")
 
     def download(self, batch: LaneBatch, first: int = 0):
         soa = batch.soa()
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, batch.n),
                     "mg_lanes_download")
+        if batch.symbolic:
+            s = batch.sym_soa_range(0, batch.n)
+            self._check(self.lib.mg_sym_download(self.ctx, ctypes.addressof(s), first, batch.n),
+                        "mg_sym_download")
 
     def upload_range(self, batch: LaneBatch, first: int, n: int):
         """Upload lanes [first, first + n) of `batch` to the same device lanes."""
         soa = batch.soa_range(first, n)
         self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, n),
                     "mg_lanes_upload")
+        if batch.symbolic:
+            s = batch.sym_soa_range(first, n)
+            self._check(self.lib.mg_sym_upload(self.ctx, ctypes.addressof(s), first, n), "mg_sym_upload")
 
     def download_range(self, batch: LaneBatch, first: int, n: int):
         soa = batch.soa_range(first, n)
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, n),
                     "mg_lanes_download")
+        if batch.symbolic:
+            s = batch.sym_soa_range(first, n)
+            self._check(self.lib.mg_sym_download(self.ctx, ctypes.addressof(s), first, n),
+                        "mg_sym_download")
 
     def set_loop_bound(self, bound: int):
         """BoundedLoopsStrategy on the device (0 = off); needs trace_cap > 0."""

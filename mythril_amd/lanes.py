@@ -21,6 +21,7 @@ import numpy as np
 MG_RUNNING, MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT = 0, 1, 2, 3
 MG_HALT_END, MG_HALT_DROPPED, MG_VMEXC, MG_HOOK, MG_ESCAPE, MG_DEPTH = 4, 5, 6, 7, 8, 9
 MG_LOOP_BOUND = 10
+MG_FORK = 11            # JUMPI on a symbolic condition (symbolic lanes)
 STATUS_NAMES = {
     MG_RUNNING: "running", MG_HALT_STOP: "stop", MG_HALT_RETURN: "return",
     MG_HALT_REVERT: "revert", MG_HALT_END: "end", MG_HALT_DROPPED: "dropped",
@@ -34,10 +35,14 @@ MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
 MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
 MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2, 3, 4, 5
 MG_ESC_RECORD = 6
+MG_ESC_SYMBOLIC, MG_ESC_ARENA = 7, 8
 # function-manager records (include/mythgpu.h MG_REC_*)
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_HEADER = 1, 2, 11
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
+MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT = 16, 32, 6
+MG_SYM_CDLOAD, MG_SYM_CDSIZE, MG_SYM_ENV, MG_SYM_BIN, MG_SYM_UN = 1, 2, 3, 4, 5
+MG_SYM_CONST = 0x80000000
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
 MG_ENV_WORDS = 5
 MG_STACK_LIMIT = 1024
@@ -86,6 +91,14 @@ class MgLaneSoa(ctypes.Structure):
     ]
 
 
+class MgSymSoa(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32), ("node_cap", ctypes.c_uint32),
+                ("const_cap", ctypes.c_uint32), ("stag", ctypes.c_void_p), ("node", ctypes.c_void_p),
+                ("cval", ctypes.c_void_p), ("n_nodes", ctypes.c_void_p), ("n_consts", ctypes.c_void_p)]
+
+
+_SYM_FIELDS = ("stag", "node", "cval", "n_nodes", "n_consts")
+
 _U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
                "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len", "rec_len")
 _U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
@@ -100,6 +113,8 @@ class LaneShape:
     storage_cap: int = 16
     trace_cap: int = 0
     rec_cap: int = 0
+    node_cap: int = 0        # symbolic lanes: arena nodes per lane (0: no symbolic planes)
+    const_cap: int = 0       # symbolic lanes: constant-table entries per lane
 
     def __post_init__(self):
         if self.mem_cap % 32:
@@ -125,6 +140,29 @@ class LaneBatch:
         self.storage = np.zeros((n, shape.storage_cap, 16), dtype=np.uint32)
         self.trace = np.zeros((n, max(shape.trace_cap, 1)), dtype=np.uint32)
         self.rec = np.zeros((n, max(shape.rec_cap, 1)), dtype=np.uint32)
+        if shape.node_cap:
+            self.stag = np.zeros((n, shape.stack_cap), dtype=np.uint32)
+            self.node = np.zeros((n, shape.node_cap, 4), dtype=np.uint32)
+            self.cval = np.zeros((n, max(shape.const_cap, 1), 8), dtype=np.uint32)
+            self.n_nodes = np.zeros(n, dtype=np.uint32)
+            self.n_consts = np.zeros(n, dtype=np.uint32)
+
+    @property
+    def symbolic(self) -> bool:
+        return self.shape.node_cap > 0
+
+    def sym_soa_range(self, first: int, n: int) -> MgSymSoa:
+        """mg_sym_soa over lanes [first, first + n) (symbolic planes)."""
+        if first < 0 or n < 0 or first + n > self.shape.n:
+            raise ValueError("lane range out of bounds")
+        s = MgSymSoa()
+        s.n, s.stack_cap = n, self.shape.stack_cap
+        s.node_cap, s.const_cap = self.shape.node_cap, self.shape.const_cap
+        for f in _SYM_FIELDS:
+            arr = getattr(self, f)
+            setattr(s, f, arr.ctypes.data + first * arr.strides[0])
+        self._keep_sym = s
+        return s
 
     @property
     def n(self) -> int:
@@ -167,7 +205,7 @@ class LaneBatch:
     def copy(self) -> "LaneBatch":
         out = LaneBatch(self.shape)
         for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                              "trace", "rec"):
+                                              "trace", "rec") + (_SYM_FIELDS if self.symbolic else ()):
             getattr(out, f)[...] = getattr(self, f)
         return out
 

@@ -76,9 +76,9 @@ class MachineStack(list):
         super().__init__(default_list or [])
 
     def append(self, element) -> None:
-        if isinstance(element, Bool):
-            element = symbol_factory.BitVecVal(1 if element.value else 0, 256)
-        elif not isinstance(element, BitVec):
+        # machine_state.py:44-56: ints become BitVecVal; Bools (compare results)
+        # and bit-vectors are kept as they are
+        if not isinstance(element, (BitVec, Bool)):
             element = symbol_factory.BitVecVal(int(element), 256)
         if len(self) >= self.STACK_LIMIT:
             raise StackOverflowException("Reached the EVM stack limit of 1024")
@@ -264,7 +264,8 @@ class Environment:
         self.address = active_account.address
         self.code = active_account.code if code is None else code
         self.sender = sender if isinstance(sender, BitVec) else symbol_factory.BitVecVal(concrete(sender), 256)
-        self.calldata = bytes(calldata)
+        # bytes (ConcreteCalldata) or a laser.symbolic.SymbolicCalldata
+        self.calldata = calldata if hasattr(calldata, "get_word_at") else bytes(calldata)
         self.gasprice = gasprice if isinstance(gasprice, BitVec) else symbol_factory.BitVecVal(
             concrete(gasprice), 256)
         self.callvalue = callvalue if isinstance(callvalue, BitVec) else symbol_factory.BitVecVal(

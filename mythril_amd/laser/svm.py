@@ -46,20 +46,22 @@ from typing import Callable, DefaultDict, Dict, List, Optional, Tuple
 import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
-                     MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE,
+                     MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_ESC_ARENA,
+                     MG_FORK, MG_LANE_SYMBOLIC,
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
                      limbs_to_word, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
-from ..smt.expr import symbol_factory
+from ..smt.expr import Expression, symbol_factory
 from ..smt.keccak_manager import keccak_function_manager
 from ..smt.solver import Constraints, args
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
 from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
+from . import symbolic as sym
 from .transaction import ContractCreationTransaction, install_runtime_code
 
 log = logging.getLogger(__name__)
@@ -161,6 +163,7 @@ class LaserEVM:
         self.record_coverage = False        # set by the coverage plugin
         self.lane_steps = 0                 # device instructions executed by exec()
         self.launches = 0
+        self.forks = 0                      # symbolic JUMPIs the device stopped at (MG_FORK)
         self._code_ids: Dict[bytes, int] = {}
         self._code_objs: Dict[bytes, object] = {}
         # coverage the reference's execute_state hook records for states the
@@ -214,12 +217,44 @@ class LaserEVM:
             states = self.strategy.drain()
             if not states:
                 break
+            states = self._host_only(states, final_states, track_gas)
+            if not states:
+                continue
             leftover = self._run_batch(states, final_states, create, track_gas)
             if leftover is not None:       # timeout: the reference returns at once
                 return final_states + leftover if track_gas else None
         for hook in self._stop_exec_hooks:
             hook()
         return final_states if track_gas else None
+
+    def _host_only(self, states, final_states, track_gas):
+        """States a lane cannot carry (a symbolic word the expression arena has
+        no node for, symbolic storage or memory) take one step with the escape
+        handler (the reference's execute_state) and come back through the work
+        list; without a handler they are dropped as svm.py:314-316 drops a
+        NotImplementedError.  Returns the lane-eligible states."""
+        keep = []
+        for st in states:
+            if sym.lane_eligible(st):
+                keep.append(st)
+                continue
+            if self.escape_handler is None:
+                log.debug("state not representable on a lane and no escape handler: dropped")
+                continue
+            new_states = self.escape_handler(st)
+            self._filter_fork(new_states)
+            self.work_list.extend(new_states)
+            self.total_states += len(new_states)
+            if not new_states and track_gas:
+                final_states.append(st)
+        return keep
+
+    def _filter_fork(self, new_states: list) -> None:
+        """svm.py:319-326: a fork keeps the successors whose path constraints are
+        possible (kernel-2 quick-sat over the model cache, then the backend)."""
+        if self.strategy.run_check() and (len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
+            new_states[:] = [st for st in new_states
+                             if Constraints(st.world_state.constraints).is_possible()]
 
     def _add_world_state(self, global_state: GlobalState) -> None:
         """svm.py:339-348."""
@@ -326,7 +361,7 @@ class LaserEVM:
         msz = max((len(s.mstate.memory) for s in states), default=0)
         slots = max((len(s.environment.active_account.storage.printable_storage) for s in states),
                     default=0)
-        cdl = max((len(s.environment.calldata) for s in states), default=0)
+        cdl = max((len(s.environment.calldata) for s in states), default=0)    # 0 when symbolic
         trace_cap = 0
         if self._loop_bound():
             tl = max((len(_trace_of(s)) for s in states), default=0)
@@ -336,10 +371,12 @@ class LaserEVM:
         mem_cap = min(mem_cap, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
         mem_cap = max(mem_cap, (msz + 31) // 32 * 32)
         mem_cap = (mem_cap + 31) // 32 * 32
+        symbolic = any(sym.state_is_symbolic(s) for s in states)
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
                          storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap,
-                         rec_cap=512 * g)
+                         rec_cap=512 * g, node_cap=256 * g if symbolic else 0,
+                         const_cap=128 * g if symbolic else 0)
 
     def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
         env, ms = s.environment, s.mstate
@@ -347,12 +384,19 @@ class LaserEVM:
         gas_limit = getattr(tx, "gas_limit", None)
         b.code_id[i] = self.code_id(env.code)
         b.pc[i] = ms.pc
-        stack = [concrete(x) for x in ms.stack]
-        b.sp[i] = len(stack)
+        sflags = sym.lane_flags(s) if b.symbolic else 0
+        b.sp[i] = len(ms.stack)
         b.stack[i] = 0
-        if stack:
-            b.stack[i, : len(stack)] = np.array(
-                [np.frombuffer(w.to_bytes(32, "little"), dtype="<u4") for w in stack])
+        if b.symbolic:
+            b.stag[i] = 0
+            b.n_nodes[i] = b.n_consts[i] = 0
+            if sym.encode_stack(b, i, list(ms.stack)):
+                sflags |= MG_LANE_SYMBOLIC
+        else:
+            stack = [concrete(x) for x in ms.stack]
+            if stack:
+                b.stack[i, : len(stack)] = np.array(
+                    [np.frombuffer(w.to_bytes(32, "little"), dtype="<u4") for w in stack])
         mem = ms.memory.raw()
         b.msize[i] = len(mem)
         b.memory[i] = 0
@@ -361,17 +405,21 @@ class LaserEVM:
         b.status[i] = MG_RUNNING
         b.aux[i] = 0
         b.flags[i] = (MG_LANE_STATIC if env.static else 0) | (
-            MG_LANE_CREATION if isinstance(tx, ContractCreationTransaction) else 0)
+            MG_LANE_CREATION if isinstance(tx, ContractCreationTransaction) else 0) | sflags
         b.gas_min[i] = ms.min_gas_used
         b.gas_max[i] = ms.max_gas_used
         b.gas_limit[i] = _NO_GAS_LIMIT if gas_limit is None else min(concrete(gas_limit), _NO_GAS_LIMIT)
         cd = env.calldata
         b.calldata[i] = 0
-        b.calldata[i, : len(cd)] = np.frombuffer(cd, dtype=np.uint8)
-        b.calldata_len[i] = len(cd)
+        if sym.is_symbolic_calldata(cd):
+            b.calldata_len[i] = 0                   # MG_LANE_SYMCD: CALLDATA* make arena nodes
+        else:
+            b.calldata[i, : len(cd)] = np.frombuffer(cd, dtype=np.uint8)
+            b.calldata_len[i] = len(cd)
         words = (env.address, env.sender, env.origin, env.callvalue, env.gasprice)
         for k in range(MG_ENV_WORDS):
-            b.env[i, k] = word_to_limbs(concrete(words[k]))
+            w = words[k]
+            b.env[i, k] = 0 if (isinstance(w, Expression) and w.value is None) else word_to_limbs(concrete(w))
         slots = list(env.active_account.storage.printable_storage.items())
         b.storage[i] = 0
         for k, (key, val) in enumerate(slots):
@@ -393,8 +441,11 @@ class LaserEVM:
         ms = s.mstate
         ms.pc = int(b.pc[i])
         sp = int(b.sp[i])
-        ms.stack = MachineStack([symbol_factory.BitVecVal(limbs_to_word(b.stack[i, k]), 256)
-                                 for k in range(sp)])
+        if b.symbolic and int(b.flags[i]) & MG_LANE_SYMBOLIC:
+            ms.stack = MachineStack(sym.decode_stack(b, i, s))
+        else:
+            ms.stack = MachineStack([symbol_factory.BitVecVal(limbs_to_word(b.stack[i, k]), 256)
+                                     for k in range(sp)])
         ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
         ms.depth = int(b.depth[i])
         ms.min_gas_used = int(b.gas_min[i])
@@ -650,9 +701,20 @@ class LaserEVM:
             pass
         elif status in (MG_DEPTH, MG_LOOP_BOUND):
             return                  # the strategy skips it: not a final state
+        elif status == MG_FORK:
+            # instructions.py:1558-1636 on a symbolic condition, then the fork
+            # filter of svm.py:319-326 (kernel 2)
+            self.forks += 1
+            new_states = sym.jumpi_successors(s)
+            self._filter_fork(new_states)
+            self.work_list.extend(new_states)
+            self.total_states += len(new_states)
+            if new_states or not track_gas:
+                return
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
-            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE, MG_ESC_RECORD):
+            if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE, MG_ESC_RECORD,
+                          MG_ESC_ARENA):
                 # rerun with larger lane capacities; the instruction was traced
                 # at its pop but not executed, and will be traced again
                 if reason != MG_ESC_TRACE and b.shape.trace_cap:
@@ -665,12 +727,7 @@ class LaserEVM:
                 log.debug("Encountered unimplemented instruction %s", name)
                 return              # svm.py:314-316: NotImplementedError -> continue
             new_states = self.escape_handler(s)
-            if self.strategy.run_check() and (
-                    len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
-                # svm.py:319-326: a fork keeps the successors whose path
-                # constraints are possible (kernel-2 quick-sat, then the backend)
-                new_states = [st for st in new_states
-                              if Constraints(st.world_state.constraints).is_possible()]
+            self._filter_fork(new_states)
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
             if new_states or not track_gas:
@@ -691,6 +748,9 @@ class LaserEVM:
         real_pops = _ACK_SAFE.get(name)
         if real_pops is None:
             return False
+        if real_pops and any(isinstance(x, Expression) and x.value is None
+                             for x in s.mstate.stack[-real_pops:]):
+            return False             # symbolic operand: a fork or escape at this round
         ms, env = s.mstate, s.environment
         st = ms.stack
         n = len(st)

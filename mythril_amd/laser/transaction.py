@@ -65,7 +65,8 @@ class MessageCallTransaction:
         self.code = code
         self.caller = caller
         self.callee_account = callee_account
-        self.call_data = bytes(call_data)
+        # bytes, or a laser.symbolic.SymbolicCalldata for a symbolic transaction
+        self.call_data = call_data if hasattr(call_data, "get_word_at") else bytes(call_data)
         self.call_value = call_value
         self.static = static
         self.base_fee = base_fee
@@ -77,8 +78,8 @@ class MessageCallTransaction:
                           code=self.code or self.callee_account.code, static=self.static)
         gs = GlobalState(self.world_state, env, None)
         gs.environment.active_function_name = "fallback"
-        value = concrete(self.call_value)
-        if value:
+        value = getattr(self.call_value, "value", self.call_value)
+        if value:      # a symbolic value moves no concrete balance (balances stay concrete here)
             sender, receiver = concrete(env.sender), concrete(env.active_account.address)
             ws = gs.world_state
             if receiver in ws.accounts:
@@ -94,6 +95,43 @@ class MessageCallTransaction:
     def __str__(self):
         return "{} {} from {} to {:#42x}".format(type(self).__name__, self.id, self.caller,
                                                  concrete(self.callee_account.address))
+
+
+# transaction/symbolic.py:28-40 Actors
+ACTORS = {"CREATOR": 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,
+          "ATTACKER": 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+          "SOMEGUY": 0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA}
+
+
+def execute_symbolic_message_call(laser_evm, callee_address, gas_limit: int = 8_000_000) -> None:
+    """transaction/symbolic.py:105-150: one message call per open world state
+    with symbolic calldata (``{id}_calldata``, ``{id}_calldatasize``), a
+    symbolic sender/origin (``sender_{id}``), gas price and call value, plus
+    the constraint that the sender is one of the ACTORS
+    (symbolic.py:202-219); then ``laser_evm.exec()``.  The lanes run on the
+    device as symbolic lanes (mythril_amd/laser/symbolic.py)."""
+    from ..smt.expr import Or, symbol_factory
+    from .symbolic import SymbolicCalldata
+    open_states = laser_evm.open_states[:]
+    del laser_evm.open_states[:]
+    for ws in open_states:
+        acct = ws[callee_address]
+        if getattr(acct, "deleted", False):
+            continue
+        txid = tx_id_manager.get_next_tx_id()
+        sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
+        tx = MessageCallTransaction(
+            world_state=ws, identifier=txid,
+            gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256), gas_limit=gas_limit,
+            origin=sender, caller=sender, callee_account=acct, call_data=SymbolicCalldata(txid),
+            call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+        gs = tx.initial_global_state()
+        gs.transaction_stack.append((tx, None))
+        gs.world_state.constraints.append(
+            Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
+        gs.world_state.transaction_sequence.append(tx)
+        laser_evm.work_list.append(gs)
+    laser_evm.exec()
 
 
 def _rlp_item(b: bytes) -> bytes:

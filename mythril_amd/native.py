@@ -134,6 +134,9 @@ SIGNATURES = {
     "mg_eval_upload": (_I, [_P, ctypes.POINTER(MgDagBatch), ctypes.POINTER(MgModelBatch)]),
     "mg_eval_run": (_I, [_P, _U32, _U32, ctypes.POINTER(ctypes.c_float)]),
     "mg_eval_download": (_I, [_P, _P, _P, _U32, _U32]),
+    "mg_sym_alloc": (_I, [_P, _U32, _U32]),
+    "mg_sym_upload": (_I, [_P, _P, _U32, _U32]),
+    "mg_sym_download": (_I, [_P, _P, _U32, _U32]),
 }
 
 _lib = None

@@ -15,7 +15,8 @@ from typing import Dict, Optional
 import numpy as np
 
 from mythril_amd.device import StepStats
-from mythril_amd.lanes import (_ALL_FIELDS, LaneBatch, MG_ESCAPE, MG_HOOK, MG_RUNNING)
+from mythril_amd.lanes import (_ALL_FIELDS, _SYM_FIELDS, LaneBatch, MG_DEPTH, MG_ESC_SYMBOLIC, MG_ESCAPE,
+                               MG_HALT_END, MG_HOOK, MG_LANE_HOOK_ACK, MG_LANE_SYMBOLIC, MG_RUNNING)
 from oracle.evm_ref import OracleEVM
 
 
@@ -48,7 +49,8 @@ class OracleDevice:
         self._cov_on = bool(coverage)
 
     def _copy(self, src: LaneBatch, dst: LaneBatch, first: int, n: int):
-        for f in _ALL_FIELDS:
+        fields = _ALL_FIELDS + (_SYM_FIELDS if src.symbolic and dst.symbolic else ())
+        for f in fields:
             a, b = getattr(dst, f), getattr(src, f)
             if a.shape[1:] == b.shape[1:]:
                 a[first:first + n] = b[first:first + n]
@@ -91,6 +93,7 @@ class OracleDevice:
         for cid, buf in self._cov.items():
             self.o.set_coverage(cid, buf if self._cov_on else None)
         bound = self._bound if self._img.shape.trace_cap else 0
+        self._park_symbolic(hook_mask, max_depth)
         steps = self.o.run(self._img, hook_mask=hook_mask or (0, 0, 0, 0), max_steps=max_steps,
                            max_depth=max_depth, horizon=horizon, loop_bound=bound)
         for cid in self._cov:
@@ -99,6 +102,27 @@ class OracleDevice:
         return StepStats(steps, int((s == MG_RUNNING).sum()),
                          int(((s != MG_RUNNING) & (s != MG_HOOK) & (s != MG_ESCAPE)).sum()),
                          int((s == MG_HOOK).sum()), int((s == MG_ESCAPE).sum()), 0.0)
+
+    def _park_symbolic(self, hook_mask, max_depth):
+        """The oracle has no symbolic lanes: a running MG_LANE_SYMBOLIC lane stops
+        before its next instruction exactly as k_sym_step stops before one it
+        cannot run (depth cut, past the end, hook, else MG_ESC_SYMBOLIC), so the
+        host's escape handler executes it (test stand-in for k_sym_step)."""
+        img = self._img
+        live = np.nonzero((img.status == MG_RUNNING) & ((img.flags & MG_LANE_SYMBOLIC) != 0))[0]
+        mask = hook_mask or (0, 0, 0, 0)
+        for i in live:
+            ops, _ = self.o.code_table(int(img.code_id[i]))
+            pc = int(img.pc[i])
+            if max_depth and int(img.depth[i]) >= max_depth:
+                img.status[i] = MG_DEPTH
+            elif pc >= ops.size:
+                img.status[i] = MG_HALT_END
+            else:
+                op = int(ops[pc])
+                hooked = (int(mask[op >> 6]) >> (op & 63)) & 1 and not int(img.flags[i]) & MG_LANE_HOOK_ACK
+                img.status[i] = MG_HOOK if hooked else MG_ESCAPE
+                img.aux[i] = op if hooked else op | (MG_ESC_SYMBOLIC << 8)
 
     # -- coverage
     def coverage(self, code_id: int) -> np.ndarray:

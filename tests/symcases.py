@@ -1,0 +1,111 @@
+"""Shared harness of the symbolic-lane tests (CPU with the oracle device,
+MI355X with kernel 1): deploy a reference test contract concretely, run one
+symbolic message call (transaction/symbolic.py:105-150) through the batched
+LaserEVM, and the same call through the CPU restatement (tests/symref.py);
+both sides report every path's outcome with its constraint sequence.
+
+The fork filter is off on both sides (args.pruning_factor = 0): no SMT solver
+exists here to prove a branch infeasible, so every fork is kept, as the
+reference keeps them when the filter does not run (svm.py:319-326)."""
+from __future__ import annotations
+
+from collections import Counter
+
+import symref
+from mythril_amd import workloads
+from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, LaserEVM, MessageCallTransaction,
+                               SymbolicCalldata, WorldState, execute_contract_creation,
+                               execute_symbolic_message_call, generate_contract_address)
+from mythril_amd.laser.transaction import ACTORS, tx_id_manager
+from mythril_amd.smt import solver
+from mythril_amd.smt.expr import Or, symbol_factory
+
+CREATOR = ACTORS["CREATOR"]
+# contract -> (creation code suffix: constructor arguments, call value of the creation)
+CONTRACTS = {
+    "flag_array.sol.o": (b"", 10 ** 17),                              # require(msg.value == 0.1 ether)
+    "symbolic_exec_bytecode.sol.o": ((10).to_bytes(32, "big"), 0),  # _log2Size = 10
+}
+
+
+def deploy(device, name):
+    """Concolic creation (concolic.py:23-72) of a reference test contract;
+    returns (the open world state, the new account's address)."""
+    args, value = CONTRACTS[name]
+    eng = symref.Engine()       # CODESIZE of a creation with arguments escapes: concrete on the oracle
+    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+                     escape_handler=eng.step)
+    ws = WorldState()
+    creator = Account(CREATOR, balances=None)
+    ws.put_account(creator)
+    laser.open_states = [ws]
+    execute_contract_creation(laser, None, CREATOR, CREATOR, workloads.bytecode(name) + args,
+                              8_000_000, 1, value)
+    assert len(laser.open_states) == 1, f"{name}: creation did not complete"
+    out = laser.open_states[0]
+    addr = next(a for a in out.accounts if a != CREATOR)
+    return out, addr
+
+
+def _outcomes_of_restatement(engine):
+    out = Counter()
+    for kind, s in engine.ended:
+        c = tuple(x.raw for x in s.world_state.constraints)
+        if kind in ("stop", "return"):
+            out[("txend", False, c)] += 1
+            out[("ws", c)] += 1
+        elif kind == "exception":
+            out[("txend", False, c)] += 1
+        elif kind == "revert":
+            out[("txend", True, c)] += 1
+        elif kind == "end":
+            out[("ws", c)] += 1
+        else:
+            out[(kind, c)] += 1
+    return out
+
+
+def run_both(device, name, monkeypatch):
+    """(outcomes through LaserEVM + device, outcomes of the restatement, laser)."""
+    monkeypatch.setattr(solver.args, "pruning_factor", 0)
+    ws, addr = deploy(device, name)
+    from copy import copy
+    ws_ref = copy(ws)
+    # --- batched LaserEVM: symbolic lanes on the device, escapes to the restatement
+    handler_engine = symref.Engine()
+
+    def handler(state):
+        try:
+            return handler_engine.step(state)
+        except symref.Unsupported:
+            handler_engine.ended.append(("unsupported", state))
+            return []
+    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+                     escape_handler=handler)
+    got = Counter()
+    laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
+        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
+    laser.register_laser_hooks("add_world_state", lambda s: got.update(
+        [("ws", tuple(x.raw for x in s.world_state.constraints))]))
+    laser.open_states = [ws]
+    tx0 = int(tx_id_manager.get_next_tx_id())
+    tx_id_manager.set_counter(tx0 - 1)
+    execute_symbolic_message_call(laser, addr)
+    got += _outcomes_of_restatement(handler_engine)
+    # --- the restatement alone, from the same world state and transaction id
+    tx_id_manager.set_counter(tx0 - 1)
+    ref_engine = symref.Engine()
+    txid = tx_id_manager.get_next_tx_id()
+    sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
+    acct = ws_ref[addr]
+    tx = MessageCallTransaction(world_state=ws_ref, identifier=txid,
+                                gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256),
+                                gas_limit=8_000_000, origin=sender, caller=sender, callee_account=acct,
+                                call_data=SymbolicCalldata(txid),
+                                call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+    gs = tx.initial_global_state()
+    gs.transaction_stack.append((tx, None))
+    gs.world_state.constraints.append(
+        Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
+    ref_engine.run([gs])
+    return got, _outcomes_of_restatement(ref_engine), laser

@@ -1,0 +1,350 @@
+"""CPU restatement of the reference's symbolic instruction semantics for the
+paths the symbolic lanes run (test infrastructure; parity unpinned against z3:
+z3 and the reference cannot be imported here).
+
+``step(state)`` executes the instruction at ``state.mstate.pc`` the way
+mythril/laser/ethereum/instructions.py does and returns the successor states,
+written independently of mythril_amd/laser/symbolic.py (which turns device
+arena nodes into expressions) so the two meet only in the expression layer:
+
+* symbolic operands: the mutators of instructions.py:356-800 (pop_bitvec's
+  ``If(b, 1, 0)``, Bool-valued compares, ISZERO's If, NOT as 2**256-1 - x, the
+  concrete-zero divisor rules), ``get_word_at`` of SymbolicCalldata
+  (state/calldata.py:214-262) and the symbolic environment words;
+* a JUMPI on a symbolic condition forks as instructions.py:1558-1636 does;
+* every instruction whose operands are all concrete runs on the C oracle
+  (oracle/evm_ref.c, pinned on the reference's VMTests) over a concrete
+  projection of the state.
+
+An instruction with symbolic inputs outside that set raises ``Unsupported``.
+Halts are reported in ``Engine.ended`` as (kind, state); ``Engine.run`` is a
+BFS over paths with the svm.py:319-326 fork filter, the restatement the
+device-driven LaserEVM is compared against."""
+from __future__ import annotations
+
+from copy import copy
+
+import numpy as np
+
+from mythril_amd.lanes import (LaneBatch, LaneShape, MG_HALT_DROPPED, MG_HALT_END, MG_HALT_RETURN,
+                               MG_HALT_REVERT, MG_HALT_STOP, MG_RUNNING, MG_VMEXC, limbs_to_word,
+                               word_to_limbs)
+from mythril_amd.laser.opcodes import ADDRESS_OPCODE_MAPPING
+from mythril_amd.laser.state import Memory, MachineStack
+from mythril_amd.smt.expr import (BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT, URem,
+                                  symbol_factory)
+from oracle.evm_ref import OracleEVM
+
+BVV = symbol_factory.BitVecVal
+
+
+class Unsupported(Exception):
+    pass
+
+
+def _val(x):
+    raw = getattr(x, "raw", None)
+    if isinstance(x, Bool):
+        return None if x.value is None else int(bool(x.value))
+    return int(raw.param) if raw is not None and raw.op == "const" else None
+
+
+def _pop_bitvec(x):
+    """util.pop_bitvec (util.py:75-96)."""
+    if isinstance(x, Bool):
+        return If(x, BVV(1, 256), BVV(0, 256))
+    return x
+
+
+def _word_at(calldata, off):
+    # BaseCalldata.get_word_at -> Concat(self[off: off + 32]); _load is
+    # If(index < size (signed), calldata[index], 0)
+    parts = []
+    for k in range(32):
+        idx = off if k == 0 else off + k
+        parts.append(If(idx < calldata.size, calldata._calldata[idx], BVV(0, 8)))
+    return Concat(*parts)
+
+
+_SYM_ENV = {0x30: "address", 0x33: "sender", 0x32: "origin", 0x34: "callvalue", 0x3A: "gasprice"}
+
+
+class Engine:
+    def __init__(self, pruning=None):
+        self.o = OracleEVM()
+        self.code_ids = {}
+        self.ended = []            # (kind, state): stop / return / revert / exception / end / unsupported
+        self.pruning = pruning     # callable(list of states) -> kept states (the fork filter)
+
+    # ---- concrete instructions on the oracle ---------------------------------
+    def _cid(self, code):
+        cid = self.code_ids.get(code.bytecode)
+        if cid is None:
+            raw = code.bytecode if isinstance(code.bytecode, (bytes, bytearray)) else bytes.fromhex(code.bytecode)
+            cid = self.code_ids[code.bytecode] = self.o.load_code(raw)
+        return cid
+
+    def _oracle_step(self, s):
+        env, ms = s.environment, s.mstate
+        stack = [(_val(x) or 0) for x in ms.stack]
+        mem = ms.memory.raw()
+        store = env.active_account.storage.printable_storage
+        shape = LaneShape(n=1, stack_cap=1024, mem_cap=max(4096, (len(mem) + 31) // 32 * 32 + 4096),
+                          calldata_cap=32, storage_cap=max(16, 2 * len(store) + 4))
+        b = LaneBatch(shape)
+        b.code_id[0] = self._cid(env.code)
+        b.pc[0], b.sp[0] = ms.pc, len(stack)
+        for k, v in enumerate(stack):
+            b.stack[0, k] = word_to_limbs(v)
+        b.msize[0] = len(mem)
+        b.memory[0, :len(mem)] = np.frombuffer(mem, dtype=np.uint8)
+        b.depth[0] = ms.depth
+        b.status[0] = MG_RUNNING
+        b.gas_min[0], b.gas_max[0] = ms.min_gas_used, ms.max_gas_used
+        tx = s.current_transaction
+        gl = getattr(tx, "gas_limit", None)
+        b.gas_limit[0] = (1 << 64) - 1 if gl is None else int(_val(gl) if not isinstance(gl, int) else gl)
+        words = (env.address, env.sender, env.origin, env.callvalue, env.gasprice)
+        for k, w in enumerate(words):
+            b.env[0, k] = word_to_limbs(_val(w) or 0)
+        for k, (key, val) in enumerate(store.items()):
+            b.storage[0, k, :8] = word_to_limbs(key)
+            b.storage[0, k, 8:] = word_to_limbs(val)
+        b.storage_count[0] = len(store)
+        self.o.run(b, max_steps=1)
+        st = int(b.status[0])
+        if st == MG_RUNNING:
+            n = s
+            old = list(ms.stack)
+            new_sp = int(b.sp[0])
+            out = [BVV(limbs_to_word(b.stack[0, k]), 256) for k in range(new_sp)]
+            # words below the instruction's reach keep their (maybe symbolic) objects
+            for k in range(min(new_sp, len(old) - self._touched)):
+                out[k] = old[k]
+            n.mstate.stack = MachineStack(out)
+            n.mstate.pc = int(b.pc[0])
+            n.mstate.memory = Memory(bytes(b.memory[0, :int(b.msize[0])]))
+            n.mstate.depth = int(b.depth[0])
+            n.mstate.min_gas_used, n.mstate.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])
+            store.clear()
+            for k in range(int(b.storage_count[0])):
+                store[limbs_to_word(b.storage[0, k, :8])] = limbs_to_word(b.storage[0, k, 8:])
+            return [n]
+        if st == MG_HALT_RETURN:
+            s.return_data = bytes(b.memory[0, int(b.ret_offset[0]):int(b.ret_offset[0]) + int(b.ret_len[0])])
+        kind = {MG_HALT_STOP: "stop", MG_HALT_RETURN: "return", MG_HALT_REVERT: "revert", MG_VMEXC: "exception",
+                MG_HALT_END: "end", MG_HALT_DROPPED: "dropped"}.get(st, "unsupported")   # oracle escapes
+        if kind != "dropped":
+            self.ended.append((kind, s))
+        return []
+
+    # ---- one instruction ----------------------------------------------------------
+    def step(self, state):
+        s = copy(state)
+        ms, env = s.mstate, s.environment
+        instrs = env.code.instruction_list
+        if ms.pc >= len(instrs):
+            self.ended.append(("end", s))
+            return []
+        name = instrs[ms.pc]["opcode"]
+        op = next(k for k, v in ADDRESS_OPCODE_MAPPING.items() if v == name)
+        st = ms.stack
+        nin = {"DUP": int(name[3:]) if name.startswith("DUP") else 0,
+               "SWAP": int(name[4:]) + 1 if name.startswith("SWAP") else 0}
+        reads = nin["DUP"] or nin["SWAP"] or _POPS.get(op, 0)
+        sym_in = any(_val(x) is None for x in st[-reads:]) if reads and len(st) >= reads else False
+        symcd = not isinstance(env.calldata, (bytes, bytearray))
+        env_attr = _SYM_ENV.get(op)
+        sym_env = env_attr is not None and _val(getattr(env, env_attr)) is None
+        if name.startswith(("DUP", "SWAP")) or name == "POP" or name.startswith("PUSH"):
+            self._touched = reads if not name.startswith("PUSH") else 0
+            if name.startswith("DUP") or name.startswith("SWAP"):
+                return self._stack_op(s, name)
+            return self._oracle_step(s)
+        if not (sym_in or sym_env or (symcd and op in (0x35, 0x36, 0x37))):
+            self._touched = reads
+            return self._oracle_step(s)
+        gmin, gmax = _GAS[op]
+        if op == 0x57:                                          # JUMPI
+            target, cond = st[-1], st[-2]
+            if _val(target) is None:
+                raise Unsupported("symbolic jump target")
+            return self._jumpi(s, _val(target), cond)
+        if op == 0x37 or op not in _SYM_OK and not sym_env and op not in (0x35, 0x36):
+            raise Unsupported(f"{name} with symbolic inputs")
+        if sym_env:
+            res = getattr(env, env_attr)
+        elif op == 0x36:
+            res = env.calldata.size
+        elif op == 0x35:
+            res = _word_at(env.calldata, st.pop())
+        elif op == 0x15:
+            v = st.pop()
+            exp = Not(v) if isinstance(v, Bool) else v == 0
+            res = If(exp, BVV(1, 256), BVV(0, 256))
+        elif op == 0x19:
+            v = st.pop()
+            if isinstance(v, Bool):
+                raise Unsupported("NOT of a Bool")
+            res = BVV((1 << 256) - 1, 256) - v
+        else:
+            a, b = st.pop(), st.pop()
+            res = self._binary(op, a, b)
+        if len(st) + 1 > 1024:
+            raise Unsupported("stack overflow")
+        if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
+            self.ended.append(("exception", state))
+            return []
+        st.append(res)
+        ms.pc += 1
+        ms.min_gas_used += gmin
+        ms.max_gas_used += gmax
+        return [s]
+
+    def _binary(self, op, a, b):
+        if op in (0x04, 0x05, 0x06, 0x07):
+            x, y = _pop_bitvec(a), _pop_bitvec(b)
+            if _val(y) == 0:                                  # `if op1 == 0`: a concrete zero
+                return BVV(0, 256)
+            if op == 0x04:
+                return UDiv(x, y)
+            if op == 0x05:
+                return x / y
+            return URem(x, y) if op == 0x06 else SRem(x, y)
+        if op == 0x01:
+            return _pop_bitvec(a) + _pop_bitvec(b)
+        if op == 0x02:
+            return _pop_bitvec(a) * _pop_bitvec(b)
+        if op == 0x03:
+            return _pop_bitvec(a) - _pop_bitvec(b)
+        if op == 0x10:
+            return ULT(_pop_bitvec(a), _pop_bitvec(b))
+        if op == 0x11:
+            return UGT(_pop_bitvec(a), _pop_bitvec(b))
+        if op == 0x12:
+            return _pop_bitvec(a) < _pop_bitvec(b)
+        if op == 0x13:
+            return _pop_bitvec(a) > _pop_bitvec(b)
+        if op == 0x14:
+            return _pop_bitvec(a) == _pop_bitvec(b)
+        if op == 0x16:
+            return _pop_bitvec(a) & _pop_bitvec(b)
+        if op == 0x17:
+            return _pop_bitvec(a) | _pop_bitvec(b)
+        if op == 0x18:
+            if isinstance(a, Bool) or isinstance(b, Bool):
+                raise Unsupported("XOR of a Bool")
+            return a ^ b
+        if op == 0x1A:
+            idx = _val(a)
+            if idx is None:
+                raise Unsupported("symbolic BYTE index")
+            off = (31 - idx) * 8
+            return BVV(0, 256) if off < 0 else Concat(BVV(0, 248), Extract(off + 7, off, b))
+        shift, value = _pop_bitvec(a), _pop_bitvec(b)
+        if op == 0x1B:
+            return value << shift
+        if op == 0x1C:
+            return LShR(value, shift)
+        return value >> shift
+
+    def _stack_op(self, s, name):
+        st = s.mstate.stack
+        k = int(name[3:]) if name.startswith("DUP") else int(name[4:])
+        need = k if name.startswith("DUP") else k + 1
+        if len(st) < need:
+            self.ended.append(("exception", s))
+            return []
+        gmin, gmax = 3, 3
+        if s.mstate.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
+            self.ended.append(("exception", s))
+            return []
+        if name.startswith("DUP"):
+            if len(st) + 1 > 1024:
+                self.ended.append(("exception", s))
+                return []
+            st.append(st[-k])
+        else:
+            st[-1], st[-1 - k] = st[-1 - k], st[-1]
+        s.mstate.pc += 1
+        s.mstate.min_gas_used += gmin
+        s.mstate.max_gas_used += gmax
+        return [s]
+
+    def _jumpi(self, s, jump_addr, condition):
+        """instructions.py:1558-1636."""
+        gmin, gmax = 10, 10
+        base = copy(s)
+        base.mstate.stack.pop()
+        base.mstate.stack.pop()
+        negated = Not(condition) if isinstance(condition, Bool) else condition == 0
+        condi = condition if isinstance(condition, Bool) else condition != 0
+        out = []
+        if not negated.is_false:
+            n = copy(base)
+            n.mstate.min_gas_used += gmin
+            n.mstate.max_gas_used += gmax
+            n.mstate.depth += 1
+            n.mstate.pc += 1
+            n.world_state.constraints.append(negated)
+            out.append(n)
+        instrs = s.environment.code.instruction_list
+        index = next((k for k, ins in enumerate(instrs) if ins["address"] >= jump_addr), None)
+        if index is None or instrs[index]["opcode"] != "JUMPDEST":
+            return out
+        if not condi.is_false:
+            n = copy(base)
+            n.mstate.min_gas_used += gmin
+            n.mstate.max_gas_used += gmax
+            n.mstate.pc = index
+            n.mstate.depth += 1
+            n.world_state.constraints.append(condi)
+            out.append(n)
+        return out
+
+    # ---- BFS -----------------------------------------------------------------------
+    def run(self, states, max_steps: int = 100000):
+        """All paths in BFS rounds (one instruction per path per round)."""
+        work = list(states)
+        for _ in range(max_steps):
+            if not work:
+                return
+            nxt = []
+            for st in work:
+                try:
+                    succ = self.step(st)
+                except Unsupported as e:
+                    self.ended.append(("unsupported", st))
+                    continue
+                if len(succ) > 1 and self.pruning is not None:
+                    succ = self.pruning(succ)
+                nxt.extend(succ)
+            work = nxt
+        raise RuntimeError("restatement did not finish")
+
+
+def _gas_limit(s):
+    gl = getattr(s.current_transaction, "gas_limit", None)
+    return 1 << 64 if gl is None else (gl if isinstance(gl, int) else _val(gl))
+
+
+# stack words each opcode reads (the mutator's pops)
+_POPS = {**{op: 2 for op in list(range(0x01, 0x08)) + [0x0A, 0x0B] + list(range(0x10, 0x15)) +
+            list(range(0x16, 0x19)) + list(range(0x1A, 0x1E)) + [0x20, 0x52, 0x53, 0x55, 0x57, 0xF3, 0xFD]},
+         0x08: 3, 0x09: 3, 0x15: 1, 0x19: 1, 0x35: 1, 0x37: 3, 0x39: 3, 0x3E: 3, 0x50: 1, 0x51: 1,
+         0x54: 1, 0x56: 1, 0xA0: 2, 0xA1: 3, 0xA2: 4, 0xA3: 5, 0xA4: 6}
+_SYM_OK = set(range(0x01, 0x08)) | set(range(0x10, 0x15)) | {0x15, 0x16, 0x17, 0x18, 0x19, 0x1A, 0x1B, 0x1C, 0x1D}
+
+
+def _gas_table():
+    from mythril_amd.laser.opcodes import get_opcode_gas
+    out = {}
+    for op, name in ADDRESS_OPCODE_MAPPING.items():
+        try:
+            out[op] = tuple(get_opcode_gas(name))
+        except Exception:
+            out[op] = (0, 0)
+    return out
+
+
+_GAS = _gas_table()

@@ -1,0 +1,106 @@
+"""Symbolic lanes on an MI355X: k_sym_step + the expression arena.
+
+* co-simulation: every path of a symbolic message call into the reference's
+  flag_array and symbolic_exec_bytecode contracts is stepped on the device
+  until it stops (MG_FORK at a symbolic JUMPI, MG_ESCAPE, a halt); the CPU
+  restatement (tests/symref.py) steps the same state the same number of
+  instructions, and the decoded device stack must be the restatement's stack
+  node for node (hash-consed expressions), with pc, gas, depth, memory and
+  storage equal; at MG_FORK both sides fork into the same successors;
+* end to end: the batched LaserEVM on kernel 1 ends the calls in the same path
+  outcomes and constraint sequences as the restatement, with the symbolic
+  lanes' instructions executed on the device.
+"""
+from copy import copy
+
+import pytest
+
+import symcases
+import symref
+from mythril_amd.device import GpuDevice
+from mythril_amd.lanes import (MG_ESC_SYMBOLIC, MG_ESCAPE, MG_FORK, MG_LANE_SYMBOLIC, MG_RUNNING,
+                               LaneBatch)
+from mythril_amd.laser import (BreadthFirstSearchStrategy, LaserEVM, MessageCallTransaction,
+                               SymbolicCalldata)
+from mythril_amd.laser import symbolic as sym
+from mythril_amd.laser.transaction import ACTORS
+from mythril_amd.smt.expr import Or, symbol_factory
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    d = GpuDevice(0)
+    yield d
+    d.close()
+
+
+def _initial(ws, addr, txid="50"):
+    sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
+    tx = MessageCallTransaction(world_state=ws, identifier=txid,
+                                gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256),
+                                gas_limit=8_000_000, origin=sender, caller=sender,
+                                callee_account=ws[addr], call_data=SymbolicCalldata(txid),
+                                call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+    gs = tx.initial_global_state()
+    gs.transaction_stack.append((tx, None))
+    gs.world_state.constraints.append(
+        Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
+    return gs
+
+
+@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS))
+def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
+    ws, addr = symcases.deploy(dev, name)
+    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    queue = [_initial(ws, addr)]
+    eng = symref.Engine()
+    forks = device_steps = checked = 0
+    while queue:
+        batch_states = queue[:256]
+        queue = queue[256:]
+        shape = vm._shape(batch_states)
+        b = LaneBatch(shape)
+        for i, s in enumerate(batch_states):
+            vm._pack(b, i, s)
+            b.steps[i] = 0
+        dev.alloc(shape)
+        dev.upload(b)
+        dev.step()
+        dev.download(b)
+        for i, s0 in enumerate(batch_states):
+            n = int(b.steps[i])
+            device_steps += n
+            st = int(b.status[i])
+            got = vm._materialise(b, i, copy(s0))
+            # the restatement: the same state, the same number of instructions
+            ref = s0
+            for _ in range(n):
+                out = eng.step(ref)
+                assert len(out) == 1, (name, "the restatement forked or ended inside a device run")
+                ref = out[0]
+            assert got.mstate.pc == ref.mstate.pc
+            assert [x.raw for x in got.mstate.stack] == [x.raw for x in ref.mstate.stack], (name, got.mstate.pc)
+            assert [type(x) for x in got.mstate.stack] == [type(x) for x in ref.mstate.stack]
+            assert (got.mstate.min_gas_used, got.mstate.max_gas_used, got.mstate.depth) == \
+                (ref.mstate.min_gas_used, ref.mstate.max_gas_used, ref.mstate.depth)
+            assert got.mstate.memory.raw() == ref.mstate.memory.raw()
+            checked += 1
+            if st == MG_FORK:
+                forks += 1
+                mine = sym.jumpi_successors(got)
+                theirs = eng.step(ref)
+                assert [(t.mstate.pc, tuple(c.raw for c in t.world_state.constraints)) for t in mine] == \
+                    [(t.mstate.pc, tuple(c.raw for c in t.world_state.constraints)) for t in theirs]
+                queue.extend(t for t in mine if sym.lane_eligible(t))
+            elif st == MG_ESCAPE:
+                assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
+    assert forks >= 6 and device_steps > 100 and checked > forks
+
+
+@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS))
+def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
+    got, want, laser = symcases.run_both(dev, name, monkeypatch)
+    assert got == want
+    assert laser.forks >= 6 and laser.lane_steps > 100
