@@ -55,6 +55,8 @@ def parse(argv=None):
                     help="batches of the C2 lanes in generation order, reported as c2_unbucketed (0: off)")
     ap.add_argument("--large-steps", type=int, default=10,
                     help="batches of the large-contract field (c2_large_contract; 0: off)")
+    ap.add_argument("--symbolic-calls", type=int, default=1024,
+                    help="symbolic message calls of the symbolic-lane field (0: off)")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
@@ -202,6 +204,11 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         _log(rank, f"hooked C2 ({args.hooked_lanes} lanes)")
         hooked = run_hooked_c2(dev, args.hooked_lanes, rank)
 
+    symb = None
+    if args.symbolic_calls and gpu and not args.profile_only:
+        _log(rank, f"symbolic calls ({args.symbolic_calls})")
+        symb = run_symbolic(dev, args.symbolic_calls)
+
     c4 = None
     if not args.no_c4:
         _log(rank, "C4")
@@ -249,6 +256,8 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["constraint_evals"] = c4
         if hooked is not None:
             out["hooked_c2"] = hooked
+        if symb is not None:
+            out["symbolic_calls"] = symb
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
@@ -338,6 +347,53 @@ def run_large(dev, args, rank, barrier):
             "kernel_ms_per_batch": float(np.mean([s.kernel_ms for s in st])),
             "escaped_lanes_per_batch": float(np.mean([s.escaped for s in st])),
             "code": "tests/golden/disassembly.json (disassembler_test.py:8-10)"}
+
+
+def run_symbolic(dev, n_calls):
+    """Symbolic lanes: n symbolic message calls
+    (transaction/symbolic.py:105-150) into the reference's flag_array contract
+    (deployed concretely with 0.1 ether) through the batched LaserEVM (BFS):
+    the device builds the calldata / call value expressions and stops at
+    every symbolic JUMPI, the host forks (fork filter off: no SMT solver here)
+    and re-packs the successors.  The SLOAD of a symbolic key escapes; with no
+    handler here that path ends.  Reports paths, forks, lane-steps and the
+    host/device split."""
+    from mythril_amd import workloads
+    from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, LaserEVM, WorldState,
+                                   execute_contract_creation, execute_symbolic_message_call)
+    from mythril_amd.laser.transaction import ACTORS
+    from mythril_amd.smt import solver
+    creator = ACTORS["CREATOR"]
+    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    ws = WorldState()
+    ws.put_account(Account(creator))
+    laser.open_states = [ws]
+    execute_contract_creation(laser, None, creator, creator, workloads.bytecode("flag_array.sol.o"),
+                              8_000_000, 1, 10 ** 17)        # require(msg.value == 0.1 ether)
+    if len(laser.open_states) != 1:
+        return {"error": "deployment did not complete"}
+    base = laser.open_states[0]
+    addr = next(a for a in base.accounts if a != creator)
+    from copy import copy
+    old = solver.args.pruning_factor
+    solver.args.pruning_factor = 0
+    try:
+        laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+        ends = [0]
+        laser.register_laser_hooks("transaction_end", lambda *a: ends.__setitem__(0, ends[0] + 1))
+        laser.open_states = [copy(base) for _ in range(n_calls)]
+        t0 = time.perf_counter()
+        execute_symbolic_message_call(laser, addr)
+        wall = time.perf_counter() - t0
+    finally:
+        solver.args.pruning_factor = old
+    dev_s = laser.device_ms / 1e3
+    return {"metric": "symbolic lane-steps/s (symbolic message calls, kernel 1 + host forks)",
+            "calls": n_calls, "contract": "flag_array.sol.o",
+            "paths_ended": ends[0], "open_states": len(laser.open_states), "forks": laser.forks,
+            "lane_steps": int(laser.lane_steps), "launches": int(laser.launches), "wall_s": wall,
+            "device_s": dev_s, "host_s": wall - dev_s, "lane_steps_per_s": laser.lane_steps / wall,
+            "forks_per_s": laser.forks / wall}
 
 
 def run_c4(args, dev, rank, world, barrier, dist_on):

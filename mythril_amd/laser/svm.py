@@ -163,6 +163,7 @@ class LaserEVM:
         self.record_coverage = False        # set by the coverage plugin
         self.lane_steps = 0                 # device instructions executed by exec()
         self.launches = 0
+        self._exec_stop = False
         self.forks = 0                      # symbolic JUMPIs the device stopped at (MG_FORK)
         self._code_ids: Dict[bytes, int] = {}
         self._code_objs: Dict[bytes, object] = {}
@@ -211,6 +212,7 @@ class LaserEVM:
         """svm.py:293-337: drain the work list; returns the final states when
         track_gas, else None."""
         final_states: List[GlobalState] = []
+        self._exec_stop = False
         for hook in self._start_exec_hooks:
             hook()
         while True:
@@ -223,6 +225,10 @@ class LaserEVM:
             leftover = self._run_batch(states, final_states, create, track_gas)
             if leftover is not None:       # timeout: the reference returns at once
                 return final_states + leftover if track_gas else None
+            if self._exec_stop:            # BoundedLoops popped a past-the-end state
+                self._exec_stop = False
+                self.work_list.clear()
+                break
         for hook in self._stop_exec_hooks:
             hook()
         return final_states if track_gas else None
@@ -574,6 +580,8 @@ class LaserEVM:
                     continue
             self._replay_records(lanes, self._event_key(b, ev))
             self._deliver(lanes[ev], b, final_states, track_gas, launch, regrow, single_step)
+            if self._exec_stop:
+                return None           # exec ends here: later events never happen
         self._replay_records(lanes)
         if regrow:
             self._cap_grow *= 4
@@ -690,6 +698,13 @@ class LaserEVM:
             for hook in self._transaction_end_hooks:
                 hook(s, tx, None, True)
         elif status == MG_HALT_END:
+            if self._loop_bound():
+                # BoundedLoopsStrategy.get_strategic_global_state reads the popped
+                # state's current instruction: past the end that IndexError ends the
+                # strategy's iteration (StopIteration), i.e. the whole exec, and this
+                # state is never executed (bounded_loops.py:103-145, strategy/__init__.py)
+                self._exec_stop = True
+                return
             self._add_world_state(s)
         elif status == MG_VMEXC:
             precheck = (int(b.aux[i]) == MG_EXC_STACK_UNDERFLOW and name is not None
