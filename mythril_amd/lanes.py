@@ -52,12 +52,19 @@ M256 = (1 << 256) - 1
 
 
 def word_to_limbs(x: int) -> np.ndarray:
-    x &= M256
-    return np.array([(x >> (32 * k)) & 0xFFFFFFFF for k in range(8)], dtype=np.uint32)
+    return np.frombuffer((int(x) & M256).to_bytes(32, "little"), dtype="<u4").astype(np.uint32)
 
 
 def limbs_to_word(l: Sequence[int]) -> int:
+    if isinstance(l, np.ndarray) and l.dtype == np.uint32 and l.size == 8:
+        return int.from_bytes(l.astype("<u4", copy=False).tobytes(), "little")
     return sum(int(v) << (32 * k) for k, v in enumerate(l))
+
+
+def rows_to_words(rows: np.ndarray) -> list:
+    """(n, 8) uint32 limbs -> n ints (one bytes conversion for the block)."""
+    raw = np.ascontiguousarray(rows, dtype="<u4").tobytes()
+    return [int.from_bytes(raw[32 * k: 32 * k + 32], "little") for k in range(rows.shape[0])]
 
 
 def words_to_limbs(xs: Iterable[int]) -> np.ndarray:

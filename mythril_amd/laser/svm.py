@@ -52,7 +52,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
-                     limbs_to_word, word_to_limbs)
+                     limbs_to_word, rows_to_words, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import Expression, symbol_factory
 from ..smt.keccak_manager import keccak_function_manager
@@ -450,16 +450,18 @@ class LaserEVM:
         if b.symbolic and int(b.flags[i]) & MG_LANE_SYMBOLIC:
             ms.stack = MachineStack(sym.decode_stack(b, i, s))
         else:
-            ms.stack = MachineStack([symbol_factory.BitVecVal(limbs_to_word(b.stack[i, k]), 256)
-                                     for k in range(sp)])
+            ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])
         ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
         ms.depth = int(b.depth[i])
         ms.min_gas_used = int(b.gas_min[i])
         ms.max_gas_used = int(b.gas_max[i])
         store = s.environment.active_account.storage.printable_storage
         store.clear()
-        for k in range(int(b.storage_count[i])):
-            store[limbs_to_word(b.storage[i, k, :8])] = limbs_to_word(b.storage[i, k, 8:])
+        cnt = int(b.storage_count[i])
+        if cnt:
+            kv = rows_to_words(b.storage[i, :cnt].reshape(2 * cnt, 8))
+            for k in range(cnt):
+                store[kv[2 * k]] = kv[2 * k + 1]
         s.lane_steps = int(b.steps[i])
         if b.shape.trace_cap:
             ann = _annotation_of(s)
