@@ -55,6 +55,7 @@ class SymbolicCalldata:
         self.tx_id = str(tx_id)
         self._size = symbol_factory.BitVecSym(f"{tx_id}_calldatasize", 256)
         self._calldata = Array(f"{tx_id}_calldata", 256, 8)
+        self._words = {}            # offset node -> word expression (hash-consed anyway)
 
     @property
     def size(self) -> BitVec:
@@ -71,7 +72,10 @@ class SymbolicCalldata:
     def get_word_at(self, offset) -> BitVec:
         """BaseCalldata.get_word_at: Concat of the 32 loads at offset + k."""
         off = symbol_factory.BitVecVal(offset, 256) if isinstance(offset, int) else offset
-        return Concat(*[self._load(off if k == 0 else off + k) for k in range(32)])
+        w = self._words.get(off.raw)
+        if w is None:
+            w = self._words[off.raw] = Concat(*[self._load(off if k == 0 else off + k) for k in range(32)])
+        return w
 
     def __len__(self):
         return 0
