@@ -19,8 +19,25 @@ __constant__ uint64_t kKeccakRC[24] = {
     0x000000000000800aull, 0x800000008000000aull, 0x8000000080008081ull,
     0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 
+// 64-bit rotate by a compile-time constant as two v_alignbit_b32 funnel shifts
+// on the 32-bit halves (alignbit(a, b, s) = low word of (a:b) >> s).  Written
+// out: the (v << r) | (v >> 64 - r) form lowers to 64-bit shift pairs plus ors,
+// two to three times the instructions, and at one wave per SIMD (kernel 1's C2
+// grid) Keccak-f's instruction count is its latency.
 __device__ __forceinline__ uint64_t krotl(uint64_t v, int r) {
-    return r == 0 ? v : ((v << r) | (v >> (64 - r)));
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    uint32_t nh, nl;
+    if (r == 0) return v;
+    if (r < 32) {
+        nh = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+        nl = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+    } else if (r == 32) {
+        nh = lo; nl = hi;
+    } else {
+        nh = __builtin_amdgcn_alignbit(lo, hi, 64 - r);
+        nl = __builtin_amdgcn_alignbit(hi, lo, 64 - r);
+    }
+    return ((uint64_t)nh << 32) | nl;
 }
 
 // gfx950 v_bitop3_b32: any 3-input bitwise function in one VALU instruction

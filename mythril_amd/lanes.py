@@ -364,6 +364,46 @@ def bucket_order(batch: LaneBatch) -> np.ndarray:
     return np.lexsort((batch.calldata_len, sel, batch.code_id))
 
 
+def wave_aligned_order(batch: LaneBatch, selectors, wave: int = 64) -> np.ndarray:
+    """bucket_order with every bucket of at least one wave starting and ending
+    on a wave boundary.  A wave pays for the union of its lanes' paths (the
+    longest C2 path, 203 steps, shared a wave with a 52-step bucket: 255 serial
+    steps); the slack around a large bucket is filled with lanes whose calldata
+    selects none of `selectors` (the code's dispatcher selectors,
+    workloads.dispatch_selectors) -- calldata shorter than a selector first,
+    then unknown selectors -- which take the dispatcher's fall-through, the
+    shortest paths.  Still a permutation: parity is position independent."""
+    base = bucket_order(batch)
+    sel = np.zeros(batch.n, dtype=np.uint64)
+    for k in range(min(4, batch.shape.calldata_cap)):
+        sel = (sel << np.uint64(8)) | batch.calldata[:, k].astype(np.uint64)
+    length = batch.calldata_len
+    short = length < 4
+    known = np.isin(sel, np.array(sorted(selectors), dtype=np.uint64)) & ~short
+    fillers = np.concatenate([base[short[base]], base[(~known & ~short)[base]]])
+    rest = base[known[base]]
+    key = np.stack([batch.code_id[rest].astype(np.uint64), sel[rest],
+                    length[rest].astype(np.uint64)], axis=1)
+    cut = np.flatnonzero(np.any(key[1:] != key[:-1], axis=1)) + 1
+    out, pos, f = [], 0, 0
+
+    def pad():
+        nonlocal pos, f
+        k = min((-pos) % wave, len(fillers) - f)
+        out.append(fillers[f:f + k])
+        f += k
+        pos += k
+    for g in np.split(rest, cut):
+        if len(g) >= wave:
+            pad()
+        out.append(g)
+        pos += len(g)
+        if len(g) >= wave:
+            pad()
+    out.append(fillers[f:])
+    return np.concatenate(out)
+
+
 def permuted(batch: LaneBatch, order: np.ndarray) -> LaneBatch:
     out = LaneBatch(batch.shape)
     for f in _ALL_FIELDS:
