@@ -26,10 +26,11 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 5u   /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 6u   /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
-                               5: symbolic lanes: expression arena, MG_FORK */
+                               5: symbolic lanes: expression arena, MG_FORK
+                               6: taint lanes: object handles + annotation masks */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -73,6 +74,7 @@ extern "C" {
 #define MG_ESC_RECORD   6u   /* function-manager record log would grow past rec_cap */
 #define MG_ESC_SYMBOLIC 7u   /* symbolic operand the device has no symbolic semantics for */
 #define MG_ESC_ARENA    8u   /* the lane's expression arena / constant table is full */
+#define MG_ESC_TAINT    9u   /* the lane's annotation atoms (64) or object table are full */
 
 /* Function-manager records: what the reference registers with its global
  * function managers while a path runs, logged per lane in execution order so
@@ -91,6 +93,13 @@ extern "C" {
  *                  payload = base limbs then exponent limbs (16 words).             */
 #define MG_REC_KECCAK   1u
 #define MG_REC_EXP      2u
+/*   MG_REC_ANNOT   a batch-safe annotating hook the device applied (taint lanes,
+ *                  mg_taint_program): len = the new atom's index; result = the
+ *                  word at stack[-1] before the instruction; payload = stack[-2]
+ *                  (8 limbs, 0 when absent), then pc (instruction index) and the
+ *                  opcode with MG_TAINT_POST (bit 8) for a post-hook atom.  The host
+ *                  replays the module's own hook on a state built from it.        */
+#define MG_REC_ANNOT    3u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */
@@ -107,6 +116,8 @@ extern "C" {
 #define MG_LANE_SYMCD    32u  /* symbolic calldata (SymbolicCalldata): CALLDATALOAD
                                  and CALLDATASIZE make arena nodes, CALLDATACOPY escapes */
 #define MG_LANE_SYMENV_SHIFT 6 /* bit 6 + MG_ENV_k: environment word k is symbolic  */
+#define MG_LANE_TAINT  2048u  /* taint lane: stack words are objects with annotation
+                                 sets (mg_taint_alloc); stepped by the symbolic stepper */
 
 /* environment words, per lane */
 #define MG_ENV_ADDRESS   0
@@ -221,6 +232,54 @@ typedef struct mg_sym_soa {
 int         mg_sym_alloc(mg_ctx *ctx, uint32_t node_cap, uint32_t const_cap);
 int         mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *host, uint32_t first, uint32_t n);
 int         mg_sym_download(mg_ctx *ctx, mg_sym_soa *host, uint32_t first, uint32_t n);
+
+/* ------------------------------------------------------------ taint lanes
+ * The reference's stack words are Python objects carrying a mutable set of
+ * annotations (laser/smt/expression.py:10-57): ALU results take the union of
+ * their operands' sets (bitvec.py:63-136), DUP pushes the SAME object
+ * (instructions.py:330) so a later annotate() on it shows on every copy, the
+ * environment words are one object each (instructions.py:895-1060), and concrete
+ * memory / storage round trips drop them (memory.py:84-115, account.py:43-87).
+ * A taint lane (MG_LANE_TAINT) reproduces that on the device: every stack slot
+ * holds an object handle (0: an object no other slot shares and that has no
+ * annotations; 1..5: the environment words MG_ENV_k + 1; 6: the symbolic
+ * calldata size; >= 7: the lane's object table), and every object an annotation
+ * mask over the lane's atoms (<= 64; the host maps atom k to annotation objects).
+ *
+ * Batch-safe hooks (mythril_amd/laser/taint.py) become per-opcode actions the
+ * device applies instead of yielding to the host, and log an MG_REC_ANNOT record
+ * per new atom.  Action word per opcode byte (mg_taint_program): */
+#define MG_TAINT_PRE_SHIFT   0   /* bits 0..3: operand k + 1 of a pre-hook that annotates stack[-1-k] */
+#define MG_TAINT_POST       16u  /* a post-hook annotates the pushed word                     */
+#define MG_TAINT_EXPCOND    32u  /* skip the pre-annotation when stack[-2] == 0 or stack[-1] < 2
+                                    (integer.py:161-166)                                        */
+#define MG_TAINT_YCLASS     64u  /* this action's atoms join the lane's yield class            */
+#define MG_TAINT_SINK_SHIFT  8   /* bits 8..11: operand k + 1 whose set a pre-hook adds to the
+                                    state annotation (the lane's sink mask)                    */
+#define MG_TAINT_YIELD_SHIFT 12  /* bits 12..15: operand k + 1: yield (MG_HOOK) only when that
+                                    word carries an atom of the yield class                   */
+#define MG_TAINT_OBJ0        7u  /* first object-table handle                                  */
+
+/* Host image of the taint planes of lanes [first, first + n), lane-major. */
+typedef struct mg_taint_soa {
+    uint32_t n, stack_cap, obj_cap, _pad;
+    uint32_t *sobj;         /* [n][stack_cap] object handle per stack slot      */
+    uint64_t *omask;        /* [n][obj_cap]   annotation mask per object         */
+    uint32_t *n_obj;        /* [n] object handles in use (>= MG_TAINT_OBJ0)     */
+    uint32_t *n_fixed;      /* [n] handles below this are the host's objects: the
+                               device's handle compaction never renumbers them  */
+    uint32_t *n_atoms;      /* [n] atoms in use (<= 64)                          */
+    uint64_t *sink;         /* [n] atoms the sink hooks collected                */
+    uint64_t *ymask;        /* [n] atoms of the yield class                      */
+    uint32_t *tflags;       /* [n] bit 0: a sink hook ran                         */
+} mg_taint_soa;
+
+/* Taint planes for the current batch (after mg_lanes_alloc; freed with it) and
+ * the per-opcode action table (256 words; zeros = no batch-safe hooks). */
+int         mg_taint_alloc(mg_ctx *ctx, uint32_t obj_cap);
+int         mg_taint_program(mg_ctx *ctx, const uint32_t actions[256]);
+int         mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *host, uint32_t first, uint32_t n);
+int         mg_taint_download(mg_ctx *ctx, mg_taint_soa *host, uint32_t first, uint32_t n);
 
 /* ------------------------------------------------------------- lifecycle */
 int         mg_abi_version(void);

@@ -45,6 +45,18 @@ struct DevSym {
     uint32_t *n_nodes, *n_consts;   // [N]
 };
 
+// Taint planes (mg_taint_alloc): object handle per stack slot, annotation mask
+// per object, the lane's atom count, sink and yield-class masks.
+struct DevTaint {
+    uint32_t obj_cap;
+    const uint32_t *prog;              // [256] action word per opcode (mg_taint_program)
+    uint32_t *sobj;                    // [stack_cap][N]
+    unsigned long long *omask;         // [obj_cap][N]
+    uint32_t *oremap;                  // [obj_cap][N] scratch of the handle compaction
+    uint32_t *n_obj, *n_fixed, *n_atoms, *tflags;   // [N] (handles below n_fixed are the host's)
+    unsigned long long *sink, *ymask;          // [N]
+};
+
 // Resident initial image of a batch (mg_lanes_reset); passed to the stepping
 // kernel when it re-initialises every lane itself before stepping
 // (mg_run_batches), pc == nullptr otherwise.

@@ -1004,8 +1004,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         __syncthreads();
     }
     uint32_t executed = 0;
-    // symbolic lanes (MG_LANE_SYMBOLIC) are k_sym_step's: counted as running, untouched
-    const bool sym_lane = in_range && status == ST_RUNNING && (L.flags[lane] & 16u) != 0u;
+    // symbolic and taint lanes (MG_LANE_SYMBOLIC, MG_LANE_TAINT) are k_sym_step's: counted as running, untouched
+    const bool sym_lane = in_range && status == ST_RUNNING && (L.flags[lane] & (16u | 2048u)) != 0u;
     const bool run0 = status == ST_RUNNING && !sym_lane;
     // block-uniform facts in scalar registers
     const uint32_t sflag = __builtin_amdgcn_readfirstlane(staged ? 1u : 0u);

@@ -43,6 +43,8 @@ struct mg_ctx {
     std::vector<uint8_t> code_used;      // codes uploaded into the current batch (LDS plan)
     DevLanes L{};
     DevSym S{};                          // symbolic planes (mg_sym_alloc), freed with the lanes
+    DevTaint T{};                        // taint planes (mg_taint_alloc), freed with the lanes
+    uint32_t *d_tprog = nullptr;         // [256] taint action words (mg_taint_program)
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
     uint32_t *i_pc = nullptr, *i_depth = nullptr, *i_status = nullptr, *i_aux = nullptr,
@@ -213,6 +215,7 @@ static void free_lanes(mg_ctx *ctx) {
     ctx->have_lanes = ctx->uploaded = false;
     ctx->L = DevLanes{};
     ctx->S = DevSym{};
+    ctx->T = DevTaint{};
     ctx->d_ctr = nullptr;
 }
 
@@ -224,6 +227,7 @@ extern "C" void mg_close(mg_ctx *ctx) {
     bv_free(ctx->bv);
     hipFree(ctx->d_codes); hipFree(ctx->d_a8); hipFree(ctx->d_a32); hipFree(ctx->d_cov);
     hipFree(ctx->d_stage);
+    hipFree(ctx->d_tprog);
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
     for (hipEvent_t e : ctx->ev_batch) hipEventDestroy(e);
@@ -754,6 +758,116 @@ extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint3
     return MG_OK;
 }
 
+// ---- taint planes ------------------------------------------------------------
+static int ensure_tprog(mg_ctx *ctx) {
+    if (ctx->d_tprog) return MG_OK;
+    HIPX(ctx, hipMalloc((void **)&ctx->d_tprog, 256 * 4));
+    HIPX(ctx, hipMemsetAsync(ctx->d_tprog, 0, 256 * 4, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+extern "C" int mg_taint_alloc(mg_ctx *ctx, uint32_t obj_cap) {
+    if (!ctx) return MG_EINVAL;
+    if (!ctx->have_lanes) return set_err(ctx, MG_ESTATE, "mg_taint_alloc before mg_lanes_alloc");
+    if (ctx->T.sobj) return set_err(ctx, MG_ESTATE, "mg_taint_alloc: already allocated for this batch");
+    if (obj_cap < MG_TAINT_OBJ0 + 8u || obj_cap > 65536u)
+        return set_err(ctx, MG_EINVAL, "mg_taint_alloc: obj_cap %u outside [%u, 65536]", obj_cap, MG_TAINT_OBJ0 + 8u);
+    HIPX(ctx, hipSetDevice(ctx->device));
+    int rc;
+    if ((rc = ensure_tprog(ctx))) return rc;
+    DevTaint T{};
+    T.obj_cap = obj_cap;
+    T.prog = ctx->d_tprog;
+    const size_t N = ctx->L.N;
+    auto get = [&](void **p, size_t bytes) -> int {
+        if (hipMalloc(p, bytes) != hipSuccess) return set_err(ctx, MG_ENOMEM, "mg_taint_alloc: %zu bytes", bytes);
+        ctx->lane_allocs.push_back(*p);
+        return hipMemsetAsync(*p, 0, bytes, ctx->stream) == hipSuccess ? MG_OK : MG_EDEVICE;
+    };
+    if ((rc = get((void **)&T.sobj, (size_t)ctx->L.stack_cap * N * 4))) return rc;
+    if ((rc = get((void **)&T.omask, (size_t)obj_cap * N * 8))) return rc;
+    if ((rc = get((void **)&T.oremap, (size_t)obj_cap * N * 4))) return rc;
+    if ((rc = get((void **)&T.n_obj, N * 4))) return rc;
+    if ((rc = get((void **)&T.n_fixed, N * 4))) return rc;
+    if ((rc = get((void **)&T.n_atoms, N * 4))) return rc;
+    if ((rc = get((void **)&T.tflags, N * 4))) return rc;
+    if ((rc = get((void **)&T.sink, N * 8))) return rc;
+    if ((rc = get((void **)&T.ymask, N * 8))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->T = T;
+    return MG_OK;
+}
+
+extern "C" int mg_taint_program(mg_ctx *ctx, const uint32_t actions[256]) {
+    if (!ctx || !actions) return MG_EINVAL;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    for (int k = 0; k < 256; ++k) {
+        const uint32_t a = actions[k];
+        if (a & ~0xffffu) return set_err(ctx, MG_EINVAL, "taint action %#x of opcode %#x: unknown bits", a, k);
+        if (((a & 15u) && (a & 15u) > 7u) || ((a >> 8) & 15u) > 7u || ((a >> 12) & 15u) > 7u)
+            return set_err(ctx, MG_EINVAL, "taint action %#x of opcode %#x: operand out of range", a, k);
+    }
+    int rc;
+    if ((rc = ensure_tprog(ctx))) return rc;
+    HIPX(ctx, hipMemcpyAsync(ctx->d_tprog, actions, 256 * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    return MG_OK;
+}
+
+static int check_taint_shape(mg_ctx *ctx, const mg_taint_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx->T.sobj) return set_err(ctx, MG_ESTATE, "mg_taint_alloc first");
+    if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
+        return set_err(ctx, MG_EINVAL, "taint lane range [%u,%u) outside batch of %u", first, first + n, ctx->L.n);
+    if (h->stack_cap > ctx->L.stack_cap || h->obj_cap > ctx->T.obj_cap)
+        return set_err(ctx, MG_EINVAL, "taint host image capacities exceed the allocation");
+    return MG_OK;
+}
+
+extern "C" int mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_taint_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (h->n_obj[i] > h->obj_cap || h->n_fixed[i] < MG_TAINT_OBJ0 || h->n_fixed[i] > h->n_obj[i] ||
+            h->n_atoms[i] > 64u)
+            return set_err(ctx, MG_EINVAL, "lane %u: taint counts outside its capacities", first + i);
+        const uint32_t *so = h->sobj + (size_t)i * h->stack_cap;
+        for (uint32_t k = 0; k < h->stack_cap; ++k)
+            if (so[k] >= h->n_obj[i]) return set_err(ctx, MG_EINVAL, "lane %u slot %u: handle %u past n_obj", first + i, k, so[k]);
+    }
+    DevTaint &T = ctx->T;
+    if ((rc = up_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
+    if ((rc = up_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
+    if ((rc = up_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
+    if ((rc = up_scalar(ctx, h->tflags, 4, n, T.tflags, first))) return rc;
+    if ((rc = up_scalar(ctx, h->sink, 8, n, T.sink, first))) return rc;
+    if ((rc = up_scalar(ctx, h->ymask, 8, n, T.ymask, first))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = up_units(ctx, h->sobj, n, h->stack_cap, 1, T.sobj, first))) return rc;
+    if ((rc = up_units(ctx, h->omask, n, h->obj_cap, 2, T.omask, first))) return rc;
+    return MG_OK;
+}
+
+extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, uint32_t n) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_taint_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    DevTaint &T = ctx->T;
+    if ((rc = down_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
+    if ((rc = down_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
+    if ((rc = down_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
+    if ((rc = down_scalar(ctx, h->tflags, 4, n, T.tflags, first))) return rc;
+    if ((rc = down_scalar(ctx, h->sink, 8, n, T.sink, first))) return rc;
+    if ((rc = down_scalar(ctx, h->ymask, 8, n, T.ymask, first))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    if ((rc = down_units(ctx, h->sobj, n, h->stack_cap, 1, T.sobj, first))) return rc;
+    if ((rc = down_units(ctx, h->omask, n, h->obj_cap, 2, T.omask, first))) return rc;
+    return MG_OK;
+}
+
 extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n) {
     if (!ctx) return MG_EINVAL;
     int rc;
@@ -934,11 +1048,11 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        loop_bound, reset ? *reset : DevResetImage{},
                        ctx->lpw | k1_flags() | (P.push_lds ? 0x200u : 0u) | (P.mw32 << 16));
     HIPX(ctx, hipGetLastError());
-    // symbolic lanes: the concrete stepper left them untouched (counted as running)
-    if (ctx->S.node && !prof && !reset) {
+    // symbolic and taint lanes: the concrete stepper left them untouched (counted as running)
+    if ((ctx->S.node || ctx->T.sobj) && !prof && !reset) {
         hipLaunchKernelGGL(k_sym_step, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, ctx->S,
-                           ctx->d_codes, ctx->d_a8, ctx->d_a32, m[0], m[1], m[2], m[3], max_steps, max_depth,
-                           horizon, ctr, lane_block(ctx));
+                           ctx->T, ctx->d_codes, ctx->d_a8, ctx->d_a32, m[0], m[1], m[2], m[3], max_steps, max_depth,
+                           horizon, loop_bound, ctr, lane_block(ctx));
         HIPX(ctx, hipGetLastError());
     }
     return MG_OK;

@@ -18,6 +18,15 @@
 //
 // One thread per lane, stack rows in HBM (no LDS window): symbolic lanes are the
 // minority of a batch (the concrete ones run in k_lane_step, which skips these).
+//
+// Taint lanes (MG_LANE_TAINT) run here too: every stack slot
+// carries an object handle and every object an annotation mask over the lane's
+// atoms (include/mythgpu.h "taint lanes"), so the reference's annotation sets
+// follow the words exactly as laser/smt/expression.py and bitvec.py move them --
+// unions through the ALU, one shared object per DUP and per environment word,
+// nothing through concrete memory or storage -- and the batch-safe hooks of
+// mythril_amd/laser/taint.py run here as per-opcode actions instead of a host
+// round trip.
 #pragma once
 
 #define ST_FORK 11u
@@ -80,27 +89,164 @@ DEV uint32_t sym_env_word(uint32_t op) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const DevCode *__restrict__ codes,
+
+#define LANE_TAINT 2048u
+#define ESC_TAINT 9u
+#define TOBJ0 7u                  // MG_TAINT_OBJ0
+#define T_POST 16u
+#define T_EXPCOND 32u
+#define T_YCLASS 64u
+#define TREC_WORDS (MG_REC_HEADER + 10u)
+
+DEV uint32_t t_obj(const DevTaint &T, size_t N, uint32_t lane, uint32_t slot) {
+    return T.sobj[(size_t)slot * N + lane];
+}
+DEV void t_set_obj(const DevTaint &T, size_t N, uint32_t lane, uint32_t slot, uint32_t h) {
+    T.sobj[(size_t)slot * N + lane] = h;
+}
+DEV unsigned long long t_mask(const DevTaint &T, size_t N, uint32_t lane, uint32_t h) {
+    return h ? T.omask[(size_t)h * N + lane] : 0ull;
+}
+DEV uint32_t t_new(const DevTaint &T, size_t N, uint32_t lane, uint32_t &nobj, unsigned long long m) {
+    const uint32_t h = nobj++;
+    T.omask[(size_t)h * N + lane] = m;
+    return h;
+}
+// handle compaction: objects no stack slot holds any more are dropped and the
+// device's own handles [fixed, nobj) renumbered in order (new <= old, so the
+// masks move down in place); the host's handles and the environment's stay put
+DEV void t_gc(const DevTaint &T, size_t N, uint32_t lane, uint32_t sp, uint32_t fixed, uint32_t &nobj) {
+    uint32_t *__restrict__ rm = T.oremap + lane;
+    for (uint32_t h = fixed; h < nobj; ++h) rm[(size_t)h * N] = 0u;
+    for (uint32_t s = 0; s < sp; ++s) {
+        const uint32_t h = t_obj(T, N, lane, s);
+        if (h >= fixed) rm[(size_t)h * N] = 1u;
+    }
+    uint32_t next = fixed;
+    for (uint32_t h = fixed; h < nobj; ++h) {
+        if (!rm[(size_t)h * N]) continue;
+        if (next != h) T.omask[(size_t)next * N + lane] = T.omask[(size_t)h * N + lane];
+        rm[(size_t)h * N] = next++;
+    }
+    for (uint32_t s = 0; s < sp; ++s) {
+        const uint32_t h = t_obj(T, N, lane, s);
+        if (h >= fixed) t_set_obj(T, N, lane, s, rm[(size_t)h * N]);
+    }
+    nobj = next;
+}
+// MG_REC_ANNOT: [kind][atom][step][stack[-1]][stack[-2]][pc][op | post << 8]
+DEV void rec_annot(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t atom, uint32_t step, const U256 &v0,
+                   const U256 &v1, uint32_t pc, uint32_t opw) {
+    at = rec_head(L, lane, at, MG_REC_ANNOT, atom, step, v0);
+    uint32_t *__restrict__ q = L.rec + lane;
+    const size_t N = L.N;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[(size_t)(at + k) * N] = v1.w[k];
+    q[(size_t)(at + 8u) * N] = pc;
+    q[(size_t)(at + 9u) * N] = opw;
+}
+// Annotation set of the word an executed opcode pushes (instructions.py:330-1060
+// with bitvec.py's unions): the operands' union for the ALU -- nothing for a
+// concrete zero divisor (DIV/SDIV/MOD/SMOD push a fresh 0) or a BYTE index past
+// the word, only the value's for BYTE (its index is made concrete) -- and a
+// fresh object for every other push.  a, b = stack[-1], stack[-2] before.
+DEV unsigned long long t_result_mask(const DevTaint &T, size_t N, uint32_t lane, uint32_t op, uint32_t sp0,
+                                     const U256 &a, const U256 &b, bool b_sym) {
+    const auto m = [&](uint32_t k) { return sp0 > k ? t_mask(T, N, lane, t_obj(T, N, lane, sp0 - 1u - k)) : 0ull; };
+    switch (op) {
+    case 0x01: case 0x02: case 0x03: case 0x0a: case 0x0b:
+    case 0x10: case 0x11: case 0x12: case 0x13: case 0x14:
+    case 0x16: case 0x17: case 0x18: case 0x1b: case 0x1c: case 0x1d:
+        return m(0) | m(1);
+    case 0x04: case 0x05: case 0x06: case 0x07:
+        return (!b_sym && u_iszero(b)) ? 0ull : (m(0) | m(1));
+    case 0x08: case 0x09:
+        return m(0) | m(1) | m(2);
+    case 0x15: case 0x19:
+        return m(0);
+    case 0x1a:
+        return (u_fits32(a) && a.w[0] < 32u) ? m(1) : 0ull;
+    default:
+        return 0ull;
+    }
+}
+// The taint effects of one executed instruction, in the reference's order: the
+// pre-hook's annotate() on its operand object, the sink hook's collection,
+// the mutator's push (a new object, the DUP'd object, the environment word's
+// object), the post-hook's annotate() on the pushed object.
+DEV void t_commit(const DevTaint &T, size_t N, uint32_t lane, uint32_t op, uint32_t kind, uint32_t tact,
+                  uint32_t sp0, uint32_t nsp, uint32_t nin, bool pushes, bool symcd, const U256 &a, const U256 &b,
+                  bool b_sym, unsigned long long pre_bit, unsigned long long post_bit, uint32_t &nobj,
+                  unsigned long long &sink, uint32_t &tf) {
+    const uint32_t pre_k = tact & 15u, sink_k = (tact >> 8) & 15u;
+    if (pre_bit) {
+        const uint32_t slot = sp0 - pre_k;
+        uint32_t h = t_obj(T, N, lane, slot);
+        if (!h) { h = t_new(T, N, lane, nobj, 0ull); t_set_obj(T, N, lane, slot, h); }
+        T.omask[(size_t)h * N + lane] |= pre_bit;
+    }
+    if (sink_k && sp0 >= sink_k) {
+        sink |= t_mask(T, N, lane, t_obj(T, N, lane, sp0 - sink_k));
+        tf |= 1u;
+    }
+    if (kind == K_DUP) {
+        const uint32_t src = sp0 - nin;
+        uint32_t h = t_obj(T, N, lane, src);
+        if (!h) { h = t_new(T, N, lane, nobj, 0ull); t_set_obj(T, N, lane, src, h); }
+        t_set_obj(T, N, lane, sp0, h);
+    } else if (kind == K_SWAP) {
+        const uint32_t x = t_obj(T, N, lane, sp0 - 1u), y = t_obj(T, N, lane, sp0 - nin);
+        t_set_obj(T, N, lane, sp0 - 1u, y);
+        t_set_obj(T, N, lane, sp0 - nin, x);
+    } else if (pushes) {
+        uint32_t h = 0u;
+        const uint32_t envw = sym_env_word(op);
+        if (envw < 5u) h = envw + 1u;                     // environment.address/sender/... object
+        else if (op == 0x36u && symcd) h = 6u;            // SymbolicCalldata.calldatasize object
+        else {
+            const unsigned long long rm = t_result_mask(T, N, lane, op, sp0, a, b, b_sym);
+            if (rm) h = t_new(T, N, lane, nobj, rm);
+        }
+        t_set_obj(T, N, lane, nsp - 1u, h);
+    }
+    if (post_bit && nsp >= 1u) {
+        uint32_t h = t_obj(T, N, lane, nsp - 1u);
+        if (!h) { h = t_new(T, N, lane, nobj, 0ull); t_set_obj(T, N, lane, nsp - 1u, h); }
+        T.omask[(size_t)h * N + lane] |= post_bit;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint T, const DevCode *__restrict__ codes,
                                                   const uint8_t *__restrict__ a8,
                                                   const uint32_t *__restrict__ a32,
                                                   uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3,
                                                   uint32_t max_steps, uint32_t max_depth, uint32_t horizon,
-                                                  DevCounters *__restrict__ ctr, uint32_t lanes_pb) {
+                                                  uint32_t loop_bound, DevCounters *__restrict__ ctr,
+                                                  uint32_t lanes_pb) {
     __shared__ uint32_t s_kc[(256u / 64u) * KC_WAVE];
     if ((threadIdx.x & 63u) < 2u) s_kc[(threadIdx.x >> 6) * KC_WAVE + KC_E * 24u + (threadIdx.x & 63u)] = 0u;
     __syncthreads();
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= L.n || L.status[lane] != ST_RUNNING) return;
     const uint32_t flags = L.flags[lane];
-    if (!(flags & LANE_SYMBOLIC)) return;
+    if (!(flags & (LANE_SYMBOLIC | LANE_TAINT))) return;
     const size_t N = L.N;
+    // symbolic semantics need the arena planes; taint needs the taint planes
+    const bool symlane = (flags & LANE_SYMBOLIC) && S.stag != nullptr;
+    const bool tl = (flags & LANE_TAINT) && T.sobj != nullptr;
     const DevCode C = codes[L.code_id[lane]];
     const uint8_t *__restrict__ gops = a8 + C.op_off;
     uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
     uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
     const uint64_t txlim = L.gas_limit[lane];
     const uint64_t glim = txlim < MSTATE_GAS_LIMIT + 1ull ? txlim : MSTATE_GAS_LIMIT + 1ull;
-    uint32_t nn = S.n_nodes[lane], nc = S.n_consts[lane];
+    uint32_t nn = symlane ? S.n_nodes[lane] : 0u, nc = symlane ? S.n_consts[lane] : 0u;
+    uint32_t nobj = 0u, tfixed = 0u, natoms = 0u, ttf = 0u;
+    unsigned long long tsink = 0ull, tym = 0ull;
+    if (tl) {
+        nobj = T.n_obj[lane]; tfixed = T.n_fixed[lane]; natoms = T.n_atoms[lane]; ttf = T.tflags[lane];
+        tsink = T.sink[lane]; tym = T.ymask[lane];
+    }
     const bool hook_ack = (flags & LANE_HOOK_ACK) != 0u;
     const bool creation = (flags & LANE_CREATION) != 0u;
     uint32_t lane_max = (flags & LANE_STEP1) ? min(max_steps, 1u) : max_steps;
@@ -109,6 +255,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const De
         lane_max = min(lane_max, horizon > s0 ? horizon - s0 : 0u);
     }
     uint32_t status = ST_RUNNING, aux = 0u, executed = 0u, n_sha3 = 0u, n_exp = 0u;
+    const bool loop_on = loop_bound != 0u && L.trace_cap != 0u;
+    uint32_t tlen = loop_on ? L.trace_len[lane] : 0u;
     const LaneView V{L, lane, nullptr, 0u, threadIdx.x, 256u, nullptr, 0u};
     const StepEnv E{&L, C, a8, a32, nullptr, nullptr, nullptr, nullptr, nullptr,
                     s_kc + (threadIdx.x >> 6) * KC_WAVE, txlim, glim, lane, threadIdx.x, 256u, 0u, flags,
@@ -122,7 +270,18 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const De
         const uint2 d = kDec[op];
         const uint32_t kind = (d.y >> 9) & 31u;
         const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
-        if (((hm >> (op & 63u)) & 1ull) && !(hook_ack && executed == 0u)) { status = ST_HOOK; aux = op; break; }
+        const bool acked = hook_ack && executed == 0u;     // the host ran this instruction's hooks
+        const bool hooked = ((hm >> (op & 63u)) & 1ull) && !acked;
+        if (loop_on && !acked && (hooked || executed < lane_max)) {
+            // BoundedLoopsStrategy: every instruction the path is popped at, as k_lane_step
+            const uint64_t tr = trace_step(L.trace, N, L.trace_cap, lane, tlen, a32[C.addr_off + pc], op == 0x5bu,
+                                           loop_bound, creation ? 1u : 0u);
+            tlen = (uint32_t)tr;
+            const uint32_t res = (uint32_t)(tr >> 60);
+            if (res == 1u) { status = ST_LOOP; aux = (uint32_t)(tr >> 32) & 0x0fffffffu; break; }
+            if (res == 2u) { status = ST_ESCAPE; aux = op | (ESC_TRACE << 8); break; }
+        }
+        if (hooked) { status = ST_HOOK; aux = op; break; }
         if (executed >= lane_max) break;
         const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
         if ((uy & PD_SPECIAL) || (creation && (uy & PD_CREATION))) {
@@ -134,11 +293,62 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const De
         if (kind == K_DUP) nin = op - 0x7fu;
         else if (kind == K_SWAP) nin = op - 0x8fu + 1u;
         bool any_sym = false;
-        for (uint32_t k = 0; k < nin && k < sp; ++k) any_sym |= sym_tag(S, N, lane, sp - 1u - k) != 0u;
+        if (symlane)
+            for (uint32_t k = 0; k < nin && k < sp; ++k) any_sym |= sym_tag(S, N, lane, sp - 1u - k) != 0u;
         const uint32_t envw = sym_env_word(op);
-        const bool env_sym = envw < 5u && ((flags >> (LANE_SYMENV_SHIFT + envw)) & 1u);
-        const bool cd_sym = (flags & LANE_SYMCD) && (op == 0x35u || op == 0x36u || op == 0x37u);
+        const bool env_sym = symlane && envw < 5u && ((flags >> (LANE_SYMENV_SHIFT + envw)) & 1u);
+        const bool cd_sym = symlane && (flags & LANE_SYMCD) && (op == 0x35u || op == 0x36u || op == 0x37u);
         const bool stack_op = kind == K_DUP || kind == K_SWAP || kind == K_POP;
+
+        // ---- taint lanes: this opcode's batch-safe hooks (mythril_amd/laser/taint.py) ----
+        const uint32_t tact = (tl && !acked) ? T.prog[op] : 0u;
+        unsigned long long pre_bit = 0ull, post_bit = 0ull;
+        uint32_t rec_save = 0u;
+        bool rec_pre = false;
+        if (tact) {
+            const uint32_t yk = (tact >> 12) & 15u, pre_k = tact & 15u;
+            // a yield-if hook has work only when its operand carries an atom of the class
+            if (yk && sp >= yk && (t_mask(T, N, lane, t_obj(T, N, lane, sp - yk)) & tym)) {
+                status = ST_HOOK; aux = op; break;
+            }
+            bool do_pre = pre_k != 0u && sp >= pre_k && sp >= req;
+            const bool do_post = (tact & T_POST) != 0u;
+            if (do_pre || do_post) {
+                // the device replays annotating hooks on concrete words only; the host
+                // runs them (MG_HOOK) on symbolic ones and around SHA3/EXP results
+                if (any_sym || env_sym || cd_sym || (do_post && (kind == K_SHA3 || op == 0x0au))) {
+                    status = ST_HOOK; aux = op; break;
+                }
+                if (do_pre && (tact & T_EXPCOND)) {
+                    // integer.py:161-166: no annotation for exponent 0 or base < 2
+                    const U256 base = V.stack(sp - 1u);
+                    const U256 ex = sp >= 2u ? V.stack(sp - 2u) : u_zero();
+                    if (u_iszero(ex) || (u_fits32(base) && base.w[0] < 2u)) do_pre = false;
+                }
+            }
+            const uint32_t need = (do_pre ? 1u : 0u) + (do_post ? 1u : 0u);
+            if (natoms + need > 64u) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
+            if (nobj + 4u > T.obj_cap) {
+                t_gc(T, N, lane, sp, tfixed, nobj);
+                if (nobj + 4u > T.obj_cap) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
+            }
+            if (need && (uint64_t)L.rec_len[lane] + need * TREC_WORDS > L.rec_cap) {
+                status = ST_ESCAPE; aux = op | (ESC_RECORD << 8); break;
+            }
+            if (do_pre) {
+                // logged before the mutator runs: its own records (EXP) follow
+                rec_save = L.rec_len[lane];
+                rec_annot(L, lane, rec_save, natoms, L.steps[lane] + executed, V.stack(sp - 1u),
+                          sp >= 2u ? V.stack(sp - 2u) : u_zero(), pc, op);
+                L.rec_len[lane] = rec_save + TREC_WORDS;
+                rec_pre = true;
+                pre_bit = 1ull << natoms;
+            }
+            if (do_post) post_bit = 1ull << (natoms + (do_pre ? 1u : 0u));
+        } else if (tl && nobj + 4u > T.obj_cap) {
+            t_gc(T, N, lane, sp, tfixed, nobj);
+            if (nobj + 4u > T.obj_cap) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
+        }
 
         if ((any_sym || env_sym || cd_sym) && !stack_op && sp >= max(req, npop)) {
             // ---- symbolic semantics: one arena node (or a concrete result) ----
@@ -182,36 +392,69 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const De
                                         lnn, rtag))
                     arena_full = true;
             }
-            if (esc) { status = ST_ESCAPE; aux = op | (ESC_SYMBOLIC << 8); break; }
-            if (fork) { status = ST_FORK; aux = op; break; }
-            if (arena_full) { status = ST_ESCAPE; aux = op | (ESC_ARENA << 8); break; }
             // StateTransition: table gas after the mutator, OOG, then the push
             const uint32_t nsp = sp - npop;
-            if (pushes && nsp + 1u > STACK_LIMIT) { status = ST_VMEXC; aux = EXC_OVERFLOW; break; }
-            if (pushes && nsp + 1u > L.stack_cap) { status = ST_ESCAPE; aux = op | (ESC_STACK << 8); break; }
             const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
-            if (ngmin >= glim) { status = ST_VMEXC; aux = EXC_OOG; break; }
+            uint32_t stop = ST_RUNNING, sx = 0u;
+            if (esc) { stop = ST_ESCAPE; sx = op | (ESC_SYMBOLIC << 8); }
+            else if (fork) { stop = ST_FORK; sx = op; }
+            else if (arena_full) { stop = ST_ESCAPE; sx = op | (ESC_ARENA << 8); }
+            else if (pushes && nsp + 1u > STACK_LIMIT) { stop = ST_VMEXC; sx = EXC_OVERFLOW; }
+            else if (pushes && nsp + 1u > L.stack_cap) { stop = ST_ESCAPE; sx = op | (ESC_STACK << 8); }
+            else if (ngmin >= glim) { stop = ST_VMEXC; sx = EXC_OOG; }
+            if (stop != ST_RUNNING) {
+                if (rec_pre) L.rec_len[lane] = rec_save;   // the instruction did not run
+                status = stop; aux = sx; break;
+            }
+            if (tl)
+                t_commit(T, N, lane, op, kind, tact, sp, nsp + 1u, nin, pushes, cd_sym, a, b, tb != 0u, pre_bit,
+                         post_bit, nobj, tsink, ttf);
             V.set_stack(nsp, rval);
             sym_set_tag(S, N, lane, nsp, rtag);
             sp = nsp + 1u; ++pc; gmin = ngmin; gmax = ngmax; nn = lnn; nc = lnc;
+            if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }
             ++executed;
             continue;
         }
 
         // ---- concrete semantics (kernel 1's general handler); tags follow the words ----
         uint32_t t_in0 = 0u, t_in1 = 0u;
-        if (kind == K_DUP && sp >= nin) t_in0 = sym_tag(S, N, lane, sp - nin);
-        if (kind == K_SWAP && sp >= nin) { t_in0 = sym_tag(S, N, lane, sp - 1u); t_in1 = sym_tag(S, N, lane, sp - nin); }
+        if (symlane) {
+            if (kind == K_DUP && sp >= nin) t_in0 = sym_tag(S, N, lane, sp - nin);
+            if (kind == K_SWAP && sp >= nin) { t_in0 = sym_tag(S, N, lane, sp - 1u); t_in1 = sym_tag(S, N, lane, sp - nin); }
+        }
         LaneRegs R{sp >= 1u ? V.stack(sp - 1u) : u_zero(), sp >= 2u ? V.stack(sp - 2u) : u_zero(), gmin, gmax,
                    pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed};
+        const U256 pa = R.T0, pb = R.T1;
+        const uint32_t sp0 = sp;
         slow_step(R, E, uy, d.x);
         n_sha3 = R.n_sha3; n_exp = R.n_exp;
-        if (R.stop != ST_RUNNING) { status = R.stop; aux = R.sx; break; }
+        if (R.stop != ST_RUNNING) {
+            if (rec_pre) {
+                // the mutator's own record (EXP) was not published either; drop ours
+                L.rec_len[lane] = rec_save;
+            }
+            status = R.stop; aux = R.sx; break;
+        }
         if (R.sp >= 1u) V.set_stack(R.sp - 1u, R.T0);
         if (R.sp >= 2u) V.set_stack(R.sp - 2u, R.T1);
-        if (kind == K_DUP) sym_set_tag(S, N, lane, R.sp - 1u, t_in0);
-        else if (kind == K_SWAP) { sym_set_tag(S, N, lane, sp - 1u, t_in1); sym_set_tag(S, N, lane, sp - nin, t_in0); }
-        else if (pushes) sym_set_tag(S, N, lane, R.sp - 1u, 0u);
+        if (symlane) {
+            if (kind == K_DUP) sym_set_tag(S, N, lane, R.sp - 1u, t_in0);
+            else if (kind == K_SWAP) { sym_set_tag(S, N, lane, sp - 1u, t_in1); sym_set_tag(S, N, lane, sp - nin, t_in0); }
+            else if (pushes) sym_set_tag(S, N, lane, R.sp - 1u, 0u);
+        }
+        if (tl) {
+            t_commit(T, N, lane, op, kind, tact, sp0, R.sp, nin, pushes, false, pa, pb, false, pre_bit, post_bit,
+                     nobj, tsink, ttf);
+            if (post_bit) {
+                const uint32_t at = L.rec_len[lane];
+                rec_annot(L, lane, at, natoms + (pre_bit ? 1u : 0u), L.steps[lane] + executed, R.T0,
+                          R.sp >= 2u ? R.T1 : u_zero(), pc, op | 0x100u);
+                L.rec_len[lane] = at + TREC_WORDS;
+            }
+            if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }
+            if (post_bit) { ++natoms; if (tact & T_YCLASS) tym |= post_bit; }
+        }
         pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth; gmin = R.gmin; gmax = R.gmax;
         ++executed;
     }
@@ -221,9 +464,14 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, const De
     L.status[lane] = status; L.aux[lane] = aux;
     if (hook_ack && executed > 0u) L.flags[lane] = flags & ~LANE_HOOK_ACK;
     L.steps[lane] += executed;
+    if (loop_on) L.trace_len[lane] = tlen;
     if (n_sha3) L.sha3_count[lane] += n_sha3;
     if (n_exp) L.exp_count[lane] += n_exp;
-    S.n_nodes[lane] = nn; S.n_consts[lane] = nc;
+    if (symlane) { S.n_nodes[lane] = nn; S.n_consts[lane] = nc; }
+    if (tl) {
+        T.n_obj[lane] = nobj; T.n_atoms[lane] = natoms; T.tflags[lane] = ttf;
+        T.sink[lane] = tsink; T.ymask[lane] = tym;
+    }
     if (ctr) {
         DevCounters *c = ctr + lane / lanes_pb;
         atomicAdd(&c->lane_steps, (unsigned long long)executed);

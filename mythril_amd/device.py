@@ -89,42 +89,54 @@ class GpuDevice:
         if shape.node_cap:
             self._check(self.lib.mg_sym_alloc(self.ctx, shape.node_cap, max(shape.const_cap, 1)),
                         "mg_sym_alloc")
+        if shape.obj_cap:
+            self._check(self.lib.mg_taint_alloc(self.ctx, shape.obj_cap), "mg_taint_alloc")
         self.shape = shape
+
+    def set_taint_program(self, actions) -> None:
+        """mg_taint_program: the per-opcode action words of the batch-safe hooks
+        (256 x uint32, mythril_amd/laser/taint.py)."""
+        arr = np.ascontiguousarray(np.asarray(actions, dtype=np.uint32).reshape(256))
+        self._check(self.lib.mg_taint_program(self.ctx, arr.ctypes.data), "mg_taint_program")
+
+    def _planes(self, batch: LaneBatch, first: int, n: int, up: bool, dev_first: Optional[int] = None):
+        """Symbolic / taint planes of host lanes [first, first + n) to or from
+        device lanes [dev_first, dev_first + n) (dev_first defaults to first)."""
+        d = first if dev_first is None else dev_first
+        if batch.symbolic:
+            s = batch.sym_soa_range(first, n)
+            fn = self.lib.mg_sym_upload if up else self.lib.mg_sym_download
+            self._check(fn(self.ctx, ctypes.addressof(s), d, n), "mg_sym_upload" if up else "mg_sym_download")
+        if batch.taint:
+            t = batch.taint_soa_range(first, n)
+            fn = self.lib.mg_taint_upload if up else self.lib.mg_taint_download
+            self._check(fn(self.ctx, ctypes.addressof(t), d, n),
+                        "mg_taint_upload" if up else "mg_taint_download")
 
     def upload(self, batch: LaneBatch, first: int = 0):
         soa = batch.soa()
         self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, batch.n),
                     "mg_lanes_upload")
-        if batch.symbolic:
-            s = batch.sym_soa_range(0, batch.n)
-            self._check(self.lib.mg_sym_upload(self.ctx, ctypes.addressof(s), first, batch.n), "mg_sym_upload")
+        self._planes(batch, 0, batch.n, True, first)
 
     def download(self, batch: LaneBatch, first: int = 0):
         soa = batch.soa()
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, batch.n),
                     "mg_lanes_download")
-        if batch.symbolic:
-            s = batch.sym_soa_range(0, batch.n)
-            self._check(self.lib.mg_sym_download(self.ctx, ctypes.addressof(s), first, batch.n),
-                        "mg_sym_download")
+        self._planes(batch, 0, batch.n, False, first)
 
     def upload_range(self, batch: LaneBatch, first: int, n: int):
         """Upload lanes [first, first + n) of `batch` to the same device lanes."""
         soa = batch.soa_range(first, n)
         self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, n),
                     "mg_lanes_upload")
-        if batch.symbolic:
-            s = batch.sym_soa_range(first, n)
-            self._check(self.lib.mg_sym_upload(self.ctx, ctypes.addressof(s), first, n), "mg_sym_upload")
+        self._planes(batch, first, n, True)
 
     def download_range(self, batch: LaneBatch, first: int, n: int):
         soa = batch.soa_range(first, n)
         self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, n),
                     "mg_lanes_download")
-        if batch.symbolic:
-            s = batch.sym_soa_range(first, n)
-            self._check(self.lib.mg_sym_download(self.ctx, ctypes.addressof(s), first, n),
-                        "mg_sym_download")
+        self._planes(batch, first, n, False)
 
     def set_loop_bound(self, bound: int):
         """BoundedLoopsStrategy on the device (0 = off); needs trace_cap > 0."""

@@ -35,14 +35,21 @@ MG_EXC_STACK_UNDERFLOW, MG_EXC_STACK_OVERFLOW, MG_EXC_INVALID_JUMP = 1, 2, 3
 MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
 MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2, 3, 4, 5
 MG_ESC_RECORD = 6
-MG_ESC_SYMBOLIC, MG_ESC_ARENA = 7, 8
+MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 # function-manager records (include/mythgpu.h MG_REC_*)
-MG_REC_KECCAK, MG_REC_EXP, MG_REC_HEADER = 1, 2, 11
+MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HEADER = 1, 2, 3, 11
+MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT = 16, 32, 6
 MG_SYM_CDLOAD, MG_SYM_CDSIZE, MG_SYM_ENV, MG_SYM_BIN, MG_SYM_UN = 1, 2, 3, 4, 5
 MG_SYM_CONST = 0x80000000
+MG_LANE_TAINT = 2048
+# taint action word (include/mythgpu.h MG_TAINT_*)
+MG_TAINT_POST, MG_TAINT_EXPCOND, MG_TAINT_YCLASS = 16, 32, 64
+MG_TAINT_SINK_SHIFT, MG_TAINT_YIELD_SHIFT = 8, 12
+MG_TAINT_OBJ0 = 7
+MG_TAINT_CDSIZE = 6     # handle of the symbolic calldata-size object
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
 MG_ENV_WORDS = 5
 MG_STACK_LIMIT = 1024
@@ -106,6 +113,16 @@ class MgSymSoa(ctypes.Structure):
 
 _SYM_FIELDS = ("stag", "node", "cval", "n_nodes", "n_consts")
 
+
+class MgTaintSoa(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32), ("obj_cap", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32), ("sobj", ctypes.c_void_p), ("omask", ctypes.c_void_p),
+                ("n_obj", ctypes.c_void_p), ("n_fixed", ctypes.c_void_p), ("n_atoms", ctypes.c_void_p),
+                ("sink", ctypes.c_void_p), ("ymask", ctypes.c_void_p), ("tflags", ctypes.c_void_p)]
+
+
+_TAINT_FIELDS = ("sobj", "omask", "n_obj", "n_fixed", "n_atoms", "sink", "ymask", "tflags")
+
 _U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
                "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len", "rec_len")
 _U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
@@ -122,6 +139,7 @@ class LaneShape:
     rec_cap: int = 0
     node_cap: int = 0        # symbolic lanes: arena nodes per lane (0: no symbolic planes)
     const_cap: int = 0       # symbolic lanes: constant-table entries per lane
+    obj_cap: int = 0         # taint lanes: object handles per lane (0: no taint planes)
 
     def __post_init__(self):
         if self.mem_cap % 32:
@@ -153,10 +171,35 @@ class LaneBatch:
             self.cval = np.zeros((n, max(shape.const_cap, 1), 8), dtype=np.uint32)
             self.n_nodes = np.zeros(n, dtype=np.uint32)
             self.n_consts = np.zeros(n, dtype=np.uint32)
+        if shape.obj_cap:
+            self.sobj = np.zeros((n, shape.stack_cap), dtype=np.uint32)
+            self.omask = np.zeros((n, shape.obj_cap), dtype=np.uint64)
+            self.n_obj = np.full(n, MG_TAINT_OBJ0, dtype=np.uint32)
+            self.n_fixed = np.full(n, MG_TAINT_OBJ0, dtype=np.uint32)
+            self.n_atoms = np.zeros(n, dtype=np.uint32)
+            self.sink = np.zeros(n, dtype=np.uint64)
+            self.ymask = np.zeros(n, dtype=np.uint64)
+            self.tflags = np.zeros(n, dtype=np.uint32)
 
     @property
     def symbolic(self) -> bool:
         return self.shape.node_cap > 0
+
+    @property
+    def taint(self) -> bool:
+        return self.shape.obj_cap > 0
+
+    def taint_soa_range(self, first: int, n: int) -> MgTaintSoa:
+        """mg_taint_soa over lanes [first, first + n) (taint planes)."""
+        if first < 0 or n < 0 or first + n > self.shape.n:
+            raise ValueError("lane range out of bounds")
+        s = MgTaintSoa()
+        s.n, s.stack_cap, s.obj_cap = n, self.shape.stack_cap, self.shape.obj_cap
+        for f in _TAINT_FIELDS:
+            arr = getattr(self, f)
+            setattr(s, f, arr.ctypes.data + first * arr.strides[0])
+        self._keep_taint = s
+        return s
 
     def sym_soa_range(self, first: int, n: int) -> MgSymSoa:
         """mg_sym_soa over lanes [first, first + n) (symbolic planes)."""
@@ -212,7 +255,8 @@ class LaneBatch:
     def copy(self) -> "LaneBatch":
         out = LaneBatch(self.shape)
         for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage",
-                                              "trace", "rec") + (_SYM_FIELDS if self.symbolic else ()):
+                                              "trace", "rec") + (_SYM_FIELDS if self.symbolic else ()) + (
+                                                  _TAINT_FIELDS if self.taint else ()):
             getattr(out, f)[...] = getattr(self, f)
         return out
 
@@ -283,6 +327,12 @@ class LaneBatch:
             elif kind == MG_REC_EXP:
                 out.append((step, "exp", limbs_to_word(q[k: k + 8]), limbs_to_word(q[k + 8: k + 16]), r))
                 k += 16
+            elif kind == MG_REC_ANNOT:
+                # (step, "annot", atom, pc, opcode, post, stack[-1], stack[-2])
+                opw = int(q[k + 9])
+                out.append((step, "annot", ln, int(q[k + 8]), opw & 0xFF, bool(opw & 0x100), r,
+                            limbs_to_word(q[k: k + 8])))
+                k += 10
             else:
                 raise ValueError(f"lane {i}: bad record kind {kind} at word {k - MG_REC_HEADER}")
         return out

@@ -47,7 +47,7 @@ import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
                      MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_ESC_ARENA,
-                     MG_FORK, MG_LANE_SYMBOLIC,
+                     MG_ESC_TAINT, MG_FORK, MG_LANE_SYMBOLIC, MG_LANE_TAINT,
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
@@ -62,6 +62,7 @@ from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
 from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
 from . import symbolic as sym
+from . import taint as tnt
 from .transaction import ContractCreationTransaction, install_runtime_code
 
 log = logging.getLogger(__name__)
@@ -174,6 +175,11 @@ class LaserEVM:
         # coverage other ranks reported (sharded runs, laser/sharded.py), OR-ed in
         self._peer_cov: Dict[str, np.ndarray] = {}
         self._cap_grow = 1
+        # taint lanes (laser/taint.py): force object tracking even without
+        # annotating hooks (a caller that annotates words itself sets this)
+        self.track_objects = False
+        self._plan: Optional[tnt.TaintPlan] = None
+        self._tl: Optional[List[tnt.LaneTaint]] = None
         log.info("LASER EVM (MI355X batched core) initialized")
 
     # ------------------------------------------------------------- device
@@ -354,14 +360,27 @@ class LaserEVM:
             for name, hooks in table.items():
                 if hooks and name in OPCODES:
                     ops.add(OPCODES[name])
+        if self._plan is not None:
+            ops -= self._plan.safe          # batch-safe hooks run on the device (laser/taint.py)
         return ops
+
+    def _annotators_registered(self) -> bool:
+        """A module the taint registry knows (one whose hooks annotate words) is
+        hooked, batch-safe or not: its annotate() calls need object identity."""
+        for table in (self.pre_hooks, self.post_hooks):
+            for hooks in table.values():
+                for h in hooks:
+                    m = tnt._module_of(h)
+                    if m is not None and type(m).__name__ in tnt.BATCH_SAFE:
+                        return True
+        return False
 
     def _has_post(self, name: str) -> bool:
         return bool(self.post_hooks.get(name) or self.instr_post_hook.get(name)
                     or self._execute_state_hooks)
 
     # ------------------------------------------------------------- lanes
-    def _shape(self, states: List[GlobalState]) -> LaneShape:
+    def _shape(self, states: List[GlobalState], taint: bool = False) -> LaneShape:
         n = len(states)
         g = self._cap_grow
         msz = max((len(s.mstate.memory) for s in states), default=0)
@@ -382,7 +401,8 @@ class LaserEVM:
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
                          storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap,
                          rec_cap=512 * g, node_cap=256 * g if symbolic else 0,
-                         const_cap=128 * g if symbolic else 0)
+                         const_cap=128 * g if symbolic else 0,
+                         obj_cap=min(256 * g, 65536) if taint else 0)
 
     def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
         env, ms = s.environment, s.mstate
@@ -441,6 +461,12 @@ class LaserEVM:
         b.rec_len[i] = 0                # records already parsed into the replay queue
         if hasattr(b, "rec_seen"):
             b.rec_seen[i] = 0
+        if b.taint:
+            if tnt.pack(b, i, s, self._tl[i], self._plan):
+                b.flags[i] |= MG_LANE_TAINT
+            else:
+                log.warning("state needs more than %d annotation atoms or objects: its lane drops "
+                            "annotations", tnt.MAX_ATOMS)
 
     def _materialise(self, b: LaneBatch, i: int, s: GlobalState) -> GlobalState:
         """Write lane i of the host image back into its GlobalState (in place)."""
@@ -451,6 +477,8 @@ class LaserEVM:
             ms.stack = MachineStack(sym.decode_stack(b, i, s))
         else:
             ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])
+        if b.taint and int(b.flags[i]) & MG_LANE_TAINT:
+            ms.stack = MachineStack(tnt.materialise(b, i, s, self._tl[i], self._plan, list(ms.stack)))
         ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
         ms.depth = int(b.depth[i])
         ms.min_gas_used = int(b.gas_min[i])
@@ -495,6 +523,8 @@ class LaserEVM:
             _, _, i, r = heapq.heappop(q)
             if r[1] == "keccak":
                 keccak_function_manager.register_concrete(r[2], r[3])
+            elif r[1] == "annot":
+                tnt.note_record(self._tl[i], r, len(lanes[i].state.world_state.constraints))
             else:
                 _, cond = exponent_function_manager.create_condition(
                     symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))
@@ -512,7 +542,12 @@ class LaserEVM:
                    track_gas: bool, single_step: bool = False):
         dev = self.device
         n = len(states)
-        shape = self._shape(states)
+        plan = tnt.TaintPlan(self)
+        taint = (plan.active or self.track_objects or self._annotators_registered()
+                 or any(tnt.state_needs_taint(s) for s in states))
+        self._plan = plan if taint else None
+        self._tl = [tnt.LaneTaint() for _ in states] if taint else None
+        shape = self._shape(states, taint)
         b = LaneBatch(shape)
         b.rec_seen = np.zeros(n, dtype=np.int64)
         lanes = [_Lane(s, i) for i, s in enumerate(states)]
@@ -520,9 +555,12 @@ class LaserEVM:
             self._pack(b, i, s)
             b.steps[i] = 0
         dev.alloc(shape, coverage=self.record_coverage)
+        if taint:
+            dev.set_taint_program(plan.actions)
         dev.upload(b)
         dev.set_loop_bound(self._loop_bound())
         mask = _mask(self._hooked_ops())
+        plan_key = [plan.key()]
         depth = 0 if self.max_depth == _INF else int(self.max_depth)
         bfs = getattr(self.strategy, "order", "bfs") == "bfs"
         regrow: List[GlobalState] = []
@@ -541,6 +579,12 @@ class LaserEVM:
                 for pos in range(lo, lo + cnt):
                     lanes[pos].dirty = False
             sched.dirty.clear()
+            if self._plan is not None and self._plan.key() != plan_key[0]:
+                # a module's issue cache changed: its hooks may no longer be batch-safe
+                self._plan = tnt.TaintPlan(self)
+                plan_key[0] = self._plan.key()
+                dev.set_taint_program(self._plan.actions)
+                mask[:] = _mask(self._hooked_ops())
             st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
                           horizon=horizon)
             self.launches += 1
@@ -629,6 +673,10 @@ class LaserEVM:
             for hook in self.instr_pre_hook.get(name, ()):
                 hook(s)
             post = self._has_post(name) or single_step
+            # the hooks keep the state they saw (the reference's evaluate steps a
+            # copy, instructions.py:121-130): the lane goes on with a copy
+            s = copy(s)
+            ln.state = s
             # hooks may have rewritten the state: repack, then run the hooked
             # instruction alone (STEP1) when post hooks must see its successor
             steps = int(b.steps[i])
@@ -673,6 +721,13 @@ class LaserEVM:
                 if track_gas:
                     final_states.append(snapshot)
                 return
+            if st2 == MG_RUNNING:
+                # post hooks may have rewritten the successor (an annotate() on
+                # the pushed word, say): the lane resumes from the host image
+                steps2 = int(b.steps[i])
+                self._pack(b, i, new)
+                b.steps[i] = steps2
+                self._sched.mark_dirty(i)
             self._sched.set(i, "paused" if st2 == MG_RUNNING else "event")
             return
 
@@ -722,6 +777,15 @@ class LaserEVM:
             # instructions.py:1558-1636 on a symbolic condition, then the fork
             # filter of svm.py:319-326 (kernel 2)
             self.forks += 1
+            if self._plan is not None and OPCODES["JUMPI"] in self._plan.safe:
+                # the device stops before a symbolic JUMPI without its batch-safe
+                # pre-hooks: the reference runs them before the fork
+                try:
+                    self._execute_pre_hook("JUMPI", s)
+                except PluginSkipState:
+                    if track_gas:
+                        final_states.append(s)
+                    return
             new_states = sym.jumpi_successors(s)
             self._filter_fork(new_states)
             self.work_list.extend(new_states)
@@ -731,7 +795,7 @@ class LaserEVM:
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
             if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE, MG_ESC_RECORD,
-                          MG_ESC_ARENA):
+                          MG_ESC_ARENA, MG_ESC_TAINT):
                 # rerun with larger lane capacities; the instruction was traced
                 # at its pop but not executed, and will be traced again
                 if reason != MG_ESC_TRACE and b.shape.trace_cap:

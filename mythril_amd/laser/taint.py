@@ -1,0 +1,428 @@
+"""Annotation (taint) handles on the device and batch-safe hooks — SURVEY §8(f)1.
+
+In the reference every stack word is a Python object with a mutable set of
+annotations (laser/smt/expression.py:10-57).  ALU results take the union of
+their operands' sets (bitvec.py:63-136, bitvec_helper.py), DUP pushes the same
+object again (instructions.py:330), the environment words are one object each
+(instructions.py:895-1060), and concrete memory and storage round trips drop the
+sets (memory.py:84-115, account.py:43-87, array.py:21-28).  Detection modules
+build on that: the integer module's ADD/SUB/MUL/EXP pre-hooks ``annotate()`` the
+first operand with an ``OverUnderflowAnnotation`` and its SSTORE/JUMPI pre-hooks
+collect the annotations that reach them into a state annotation
+(analysis/module/modules/integer.py:133-260); TxOrigin annotates ORIGIN's word
+and inspects JUMPI conditions (dependence_on_origin.py:44-107).
+
+A taint lane (MG_LANE_TAINT, include/mythgpu.h) carries that object graph on
+the device: an object handle per stack slot and an annotation mask per object
+over up to 64 *atoms*, each atom one host-side set of annotation objects.  This
+module is the host half:
+
+* ``BATCH_SAFE``: the reference modules whose hooks the device reproduces, and
+  how (Annotate / AnnotateResult / Sink / YieldIf).  ``TaintPlan`` turns the
+  hooks a LaserEVM has registered into the device's per-opcode action words and
+  the set of opcodes that no longer need to stop the lane;
+* ``LaneTaint``: per lane, handle -> Python object and atom -> annotation set;
+  ``pack`` writes a state's objects into the planes, ``materialise`` rebuilds
+  them (the same Python objects where they existed, so identity and in-place
+  annotation behave as in the reference);
+* the device logs an MG_REC_ANNOT record for every atom it creates; when an atom
+  reaches a materialised state the host replays the module's *own* hook
+  (``module.execute``) on a state built from the record, and the annotations
+  the hook adds become the atom's set.  A sink hook is replayed once per
+  materialisation on the lane's real state with a word carrying everything the
+  sinks collected, so the module's own state annotation receives them.
+
+A module's hooks are batch-safe only while its issue cache is empty (a cached
+address makes DetectionModule.execute return early, base.py:79-86); after that
+its hooks run on the host again.
+"""
+from __future__ import annotations
+
+from collections import Counter
+from copy import copy
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ..lanes import (MG_TAINT_CDSIZE, MG_TAINT_EXPCOND, MG_TAINT_OBJ0, MG_TAINT_POST, MG_TAINT_SINK_SHIFT,
+                     MG_TAINT_YCLASS, MG_TAINT_YIELD_SHIFT)
+from ..smt.expr import Expression, symbol_factory
+from .opcodes import OPCODES
+
+MAX_ATOMS = 64
+_ENV_ATTRS = ("address", "sender", "origin", "callvalue", "gasprice")     # handles 1..5 (MG_ENV_k + 1)
+
+
+@dataclass(frozen=True)
+class Annotate:
+    """A pre-hook that annotate()s stack[-1-operand] (0 or 1); exp_cond: the
+    integer module's EXP early return (integer.py:161-166)."""
+    operand: int = 0
+    exp_cond: bool = False
+    yield_class: bool = False
+
+
+@dataclass(frozen=True)
+class AnnotateResult:
+    """A post-hook that annotate()s the word the opcode pushed."""
+    yield_class: bool = False
+
+
+@dataclass(frozen=True)
+class Sink:
+    """A pre-hook that adds stack[-1-operand]'s annotations to a state annotation."""
+    operand: int
+
+
+@dataclass(frozen=True)
+class YieldIf:
+    """A pre-hook with work only when stack[-1-operand] carries an annotation of
+    one of `types` (class names in the module's own Python module)."""
+    operand: int
+    types: Tuple[str, ...]
+
+
+# The reference's modules (class name) -> {(hook type, opcode): action}
+BATCH_SAFE: Dict[str, Dict[Tuple[str, str], object]] = {
+    # analysis/module/modules/integer.py:75-85, 140-250
+    "IntegerArithmetics": {
+        ("pre", "ADD"): Annotate(0), ("pre", "MUL"): Annotate(0), ("pre", "SUB"): Annotate(0),
+        ("pre", "EXP"): Annotate(0, exp_cond=True),
+        ("pre", "SSTORE"): Sink(1), ("pre", "JUMPI"): Sink(1),
+    },
+    # analysis/module/modules/dependence_on_origin.py:33-34, 53-107
+    "TxOrigin": {
+        ("post", "ORIGIN"): AnnotateResult(yield_class=True),
+        ("pre", "JUMPI"): YieldIf(1, ("TxOriginAnnotation",)),
+    },
+}
+
+
+def register_batch_safe(module_class_name: str, table: Dict[Tuple[str, str], object]) -> None:
+    """Declare another module's hooks batch-safe (same action vocabulary)."""
+    BATCH_SAFE[module_class_name] = dict(table)
+
+
+def _module_of(hook: Callable):
+    mod = getattr(hook, "__self__", None)
+    if mod is None or getattr(hook, "__name__", "") != "execute":
+        return None                    # get_detection_module_hooks registers module.execute
+    return mod
+
+
+def _spec(hook: Callable, hook_type: str, opcode: str):
+    mod = _module_of(hook)
+    if mod is None:
+        return None
+    table = BATCH_SAFE.get(type(mod).__name__)
+    if table is None:
+        return None
+    if getattr(mod, "cache", None) and getattr(mod, "auto_cache", True):
+        return None                    # base.py:79-86 would skip cached addresses
+    return table.get((hook_type, opcode))
+
+
+def _resolve_types(mod, names) -> Tuple[type, ...]:
+    import sys
+    pymod = sys.modules.get(type(mod).__module__)
+    out = []
+    for n in names:
+        t = getattr(pymod, n, None)
+        if isinstance(t, type):
+            out.append(t)
+    return tuple(out)
+
+
+class TaintPlan:
+    """What the device does for a LaserEVM's registered hooks."""
+
+    def __init__(self, laser):
+        self.actions = np.zeros(256, dtype=np.uint32)
+        self.safe: set = set()                         # opcode bytes the device no longer stops at
+        self.pre_replay: Dict[int, List[Callable]] = {}
+        self.post_replay: Dict[int, List[Callable]] = {}
+        self.pre_operand: Dict[int, int] = {}
+        self.sink: Optional[Tuple[Callable, str, int]] = None
+        self.yield_types: Tuple[type, ...] = ()
+        self.modules: List = []
+        if laser._execute_state_hooks:
+            return                                     # every opcode is a host event anyway
+        sink_mod = None
+        for name, op in OPCODES.items():
+            if laser.instr_pre_hook.get(name) or laser.instr_post_hook.get(name):
+                continue
+            pre, post = laser.pre_hooks.get(name, []), laser.post_hooks.get(name, [])
+            if not pre and not post:
+                continue
+            specs_pre = [(h, _spec(h, "pre", name)) for h in pre]
+            specs_post = [(h, _spec(h, "post", name)) for h in post]
+            if any(s is None for _, s in specs_pre + specs_post):
+                continue
+            if any(not isinstance(s, AnnotateResult) for _, s in specs_post):
+                continue
+            ann = [s for _, s in specs_pre if isinstance(s, Annotate)]
+            sinks = [(h, s) for h, s in specs_pre if isinstance(s, Sink)]
+            yields = [(h, s) for h, s in specs_pre if isinstance(s, YieldIf)]
+            if len({a.operand for a in ann}) > 1 or any(a.operand > 1 for a in ann):
+                continue
+            if len({s.operand for _, s in sinks}) > 1 or len({s.operand for _, s in yields}) > 1:
+                continue
+            if sinks and sink_mod is not None and any(_module_of(h) is not sink_mod for h, _ in sinks):
+                continue                                # one sink module per batch
+            if any(s.operand > 6 for _, s in sinks + yields):
+                continue
+            word = 0
+            if ann:
+                word |= ann[0].operand + 1
+                if any(a.exp_cond for a in ann):
+                    if not all(a.exp_cond for a in ann):
+                        continue
+                    word |= MG_TAINT_EXPCOND
+                if any(a.yield_class for a in ann):
+                    word |= MG_TAINT_YCLASS
+                self.pre_replay[op] = [h for h, s in specs_pre if isinstance(s, Annotate)]
+                self.pre_operand[op] = ann[0].operand
+            if specs_post:
+                word |= MG_TAINT_POST
+                if any(s.yield_class for _, s in specs_post):
+                    word |= MG_TAINT_YCLASS
+                self.post_replay[op] = [h for h, _ in specs_post]
+            if sinks:
+                word |= (sinks[0][1].operand + 1) << MG_TAINT_SINK_SHIFT
+                sink_mod = _module_of(sinks[0][0])
+                self.sink = (sinks[0][0], name, sinks[0][1].operand)
+            if yields:
+                word |= (yields[0][1].operand + 1) << MG_TAINT_YIELD_SHIFT
+                for h, s in yields:
+                    self.yield_types += _resolve_types(_module_of(h), s.types)
+            self.actions[op] = word
+            self.safe.add(op)
+            for h, _ in specs_pre + specs_post:
+                m = _module_of(h)
+                if all(m is not x for x in self.modules):
+                    self.modules.append(m)
+
+    @property
+    def active(self) -> bool:
+        return bool(self.safe)
+
+    def key(self):
+        """Changes when a module's issue cache does (the plan must be rebuilt)."""
+        return tuple(len(getattr(m, "cache", ()) or ()) for m in self.modules)
+
+
+class LaneTaint:
+    """Host side of one taint lane: handle -> object, atom -> annotation set,
+    and the records of device atoms not resolved yet."""
+    __slots__ = ("objs", "atoms", "pending")
+
+    def __init__(self):
+        self.objs: Dict[int, Expression] = {}
+        self.atoms: List[Optional[frozenset]] = []
+        self.pending: Dict[int, tuple] = {}
+
+
+def state_needs_taint(state) -> bool:
+    """Whether a state carries annotations a concrete lane would drop."""
+    env = state.environment
+    for w in (getattr(env, a) for a in _ENV_ATTRS):
+        if isinstance(w, Expression) and w.annotations:
+            return True
+    return any(isinstance(x, Expression) and x.annotations for x in state.mstate.stack)
+
+
+def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
+    """Write state's object graph into lane i's taint planes.  False when it needs
+    more than 64 atoms or the object table (the lane cannot carry it)."""
+    lt.objs, lt.atoms, lt.pending = {}, [], {}
+    atom_of: Dict[int, int] = {}
+    keep = []
+
+    def mask(o) -> int:
+        m = 0
+        for a in o.annotations:
+            k = atom_of.get(id(a))
+            if k is None:
+                k = atom_of[id(a)] = len(lt.atoms)
+                lt.atoms.append(frozenset((a,)))
+                keep.append(a)
+            m |= 1 << k
+        return m
+
+    handle: Dict[int, int] = {}
+    row = b.omask[i]
+    env = state.environment
+    for k, attr in enumerate(_ENV_ATTRS):
+        o = getattr(env, attr)
+        row[k + 1] = 0
+        if isinstance(o, Expression):
+            handle[id(o)] = k + 1
+            lt.objs[k + 1] = o
+            row[k + 1] = mask(o)
+    row[MG_TAINT_CDSIZE] = 0
+    cd = env.calldata
+    if hasattr(cd, "calldatasize") and not isinstance(cd, (bytes, bytearray)):
+        o = cd.calldatasize
+        if isinstance(o, Expression):
+            handle[id(o)] = MG_TAINT_CDSIZE
+            lt.objs[MG_TAINT_CDSIZE] = o
+            row[MG_TAINT_CDSIZE] = mask(o)
+    stack = state.mstate.stack
+    counts = Counter(id(x) for x in stack)
+    nxt = MG_TAINT_OBJ0
+    cap = b.shape.obj_cap
+    so = b.sobj[i]
+    so[:] = 0
+    for slot, x in enumerate(stack):
+        h = handle.get(id(x))
+        if h is None:
+            if isinstance(x, Expression) and (counts[id(x)] > 1 or x.annotations):
+                if nxt + 4 > cap:
+                    return False
+                h = handle[id(x)] = nxt
+                nxt += 1
+                lt.objs[h] = x
+                row[h] = mask(x)
+            else:
+                h = 0
+        so[slot] = h
+    if len(lt.atoms) > MAX_ATOMS:
+        return False
+    b.n_obj[i] = b.n_fixed[i] = nxt
+    b.n_atoms[i] = len(lt.atoms)
+    b.sink[i] = 0
+    b.tflags[i] = 0
+    ym = 0
+    if plan is not None and plan.yield_types:
+        for k, s in enumerate(lt.atoms):
+            if any(isinstance(a, plan.yield_types) for a in s):
+                ym |= 1 << k
+    b.ymask[i] = ym
+    return True
+
+
+def _bits(m: int):
+    k = 0
+    while m:
+        if m & 1:
+            yield k
+        m >>= 1
+        k += 1
+
+
+def _snapshot(state, pc: int, stack, n_constraints: int):
+    """The state a replayed hook sees: the lane's environment and transaction,
+    the world state with the path constraints the lane had at that step, pc and
+    the recorded stack words.  Memory and storage are not reproduced (the
+    batch-safe hooks do not read them)."""
+    from .state import GlobalState, MachineState
+    ws = copy(state.world_state)
+    ws.constraints = list(ws.constraints[:n_constraints])
+    ms = MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack, depth=state.mstate.depth)
+    g = GlobalState(ws, state.environment, state.node, ms, transaction_stack=list(state.transaction_stack),
+                    last_return_data=state.last_return_data)
+    return g
+
+
+def note_record(lt: LaneTaint, rec, n_constraints: int) -> None:
+    """An MG_REC_ANNOT record in the lane's execution order (lanes.records)."""
+    _step, _kind, atom, pc, op, post, v0, v1 = rec
+    while len(lt.atoms) <= atom:
+        lt.atoms.append(None)
+    lt.pending[atom] = (pc, op, post, v0, v1, n_constraints)
+
+
+def _resolve(lt: LaneTaint, atom: int, state, plan: TaintPlan) -> frozenset:
+    got = lt.atoms[atom] if atom < len(lt.atoms) else None
+    if got is not None:
+        return got
+    rec = lt.pending.pop(atom, None)
+    if rec is None:
+        raise RuntimeError(f"taint atom {atom} has no record")
+    pc, op, post, v0, v1, ncons = rec
+    o0, o1 = symbol_factory.BitVecVal(v0, 256), symbol_factory.BitVecVal(v1, 256)
+    if post:
+        target = o0
+        hooks = plan.post_replay.get(op, ())
+        pc_at = pc + 1                     # the post-hook state is the successor
+    else:
+        target = o0 if plan.pre_operand.get(op, 0) == 0 else o1
+        hooks = plan.pre_replay.get(op, ())
+        pc_at = pc
+    snap = _snapshot(state, pc_at, [o1, o0], ncons)
+    for h in hooks:
+        h(snap)
+    s = frozenset(target.annotations)
+    lt.atoms[atom] = s
+    return s
+
+
+def atoms_set(lt: LaneTaint, m: int, state, plan: TaintPlan) -> frozenset:
+    out = frozenset()
+    for k in _bits(int(m)):
+        out = out | _resolve(lt, k, state, plan)
+    return out
+
+
+def materialise(b, i: int, state, lt: LaneTaint, plan: TaintPlan, words: list) -> list:
+    """Lane i's stack as objects: `words` are fresh objects for its values; slots
+    that share a handle become one object, handles the host packed become the
+    very objects it packed, each with the annotation set of its mask.  The
+    environment words' sets are updated in place and the sink hook, when one
+    ran, is replayed on `state`.  Every handle is fixed afterwards."""
+    row = b.omask[i]
+    so = b.sobj[i]
+    made: Dict[int, Expression] = {}
+    seen = set()
+    out = []
+    for slot, x in enumerate(words):
+        h = int(so[slot])
+        if h == 0:
+            if x.annotations or id(x) in seen:
+                x = type(x)(x.raw)          # an object of its own, as the reference's push made it
+            seen.add(id(x))
+            out.append(x)
+            continue
+        o = made.get(h)
+        if o is None:
+            ann = atoms_set(lt, int(row[h]), state, plan)
+            o = lt.objs.get(h)
+            if o is None:
+                o = type(x)(x.raw, ann)
+                lt.objs[h] = o
+            elif not ann <= o.annotations:
+                o.annotations = o.annotations | ann
+            made[h] = o
+        out.append(o)
+    for h in range(1, MG_TAINT_CDSIZE + 1):
+        o = lt.objs.get(h)
+        if o is not None and int(row[h]):
+            ann = atoms_set(lt, int(row[h]), state, plan)
+            if not ann <= o.annotations:
+                o.annotations = o.annotations | ann
+    if int(b.tflags[i]) & 1 and plan.sink is not None:
+        replay_sink(state, atoms_set(lt, int(b.sink[i]), state, plan), plan)
+        b.tflags[i] = 0
+        b.sink[i] = 0
+    b.n_fixed[i] = b.n_obj[i]
+    return out
+
+
+def replay_sink(state, ann: frozenset, plan: TaintPlan) -> None:
+    """Run the sink module's own hook once on `state` (sharing its annotation
+    list) with stack[-1-operand] carrying `ann`: the module adds them to its
+    state annotation exactly as its SSTORE/JUMPI pre-hooks would have."""
+    from .state import GlobalState, MachineState
+    hook, opname, operand = plan.sink
+    instrs = state.environment.code.instruction_list
+    pc = next((k for k, ins in enumerate(instrs) if ins["opcode"] == opname), None)
+    if pc is None:
+        return
+    word = symbol_factory.BitVecVal(0, 256, ann)
+    stack = [word] + [symbol_factory.BitVecVal(0, 256) for _ in range(operand)]
+    proxy = GlobalState(state.world_state, state.environment, state.node,
+                        MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack),
+                        transaction_stack=state.transaction_stack, last_return_data=state.last_return_data)
+    proxy._annotations = state._annotations
+    hook(proxy)

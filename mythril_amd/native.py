@@ -137,6 +137,10 @@ SIGNATURES = {
     "mg_sym_alloc": (_I, [_P, _U32, _U32]),
     "mg_sym_upload": (_I, [_P, _P, _U32, _U32]),
     "mg_sym_download": (_I, [_P, _P, _U32, _U32]),
+    "mg_taint_alloc": (_I, [_P, _U32]),
+    "mg_taint_program": (_I, [_P, _P]),
+    "mg_taint_upload": (_I, [_P, _P, _U32, _U32]),
+    "mg_taint_download": (_I, [_P, _P, _U32, _U32]),
 }
 
 _lib = None

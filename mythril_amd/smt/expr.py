@@ -12,7 +12,10 @@ node-for-node onto a program (flatten.py):
   ``BVSubNoUnderflow`` (bitvec_helper.py:200-246).
 
 Annotations (taint sets) are carried as frozensets and unioned the way
-bitvec.py:63-136 does; they never reach the device.
+bitvec.py:63-136 does.  ``annotate`` adds to the set of *this* wrapper object in
+place, as expression.py:37-43 does, so every holder of the object (a DUP'd stack
+slot, an environment word) sees it; kernel 1's taint lanes carry the sets as
+object handles + atom masks (mythril_amd/laser/taint.py).
 """
 from __future__ import annotations
 
@@ -93,6 +96,14 @@ class Expression:
 
     def size(self) -> int:
         return self.raw.width
+
+    def annotate(self, annotation) -> None:
+        """expression.py:37-43: add to this object's annotation set."""
+        self.annotations = self.annotations | {annotation}
+
+    def get_annotations(self, annotation_type):
+        """expression.py:54-55."""
+        return [a for a in self.annotations if isinstance(a, annotation_type)]
 
     @property
     def symbolic(self) -> bool:
@@ -405,7 +416,7 @@ class BaseArray:
         if isinstance(item, slice):
             raise ValueError("Instance of BaseArray, does not support getitem with slices")
         k = _bv(item, self.domain)
-        return BitVec(_select(self.raw, k.raw), k.annotations)
+        return BitVec(_select(self.raw, k.raw))          # array.py:21-28: no annotations
 
     def __setitem__(self, key, value) -> None:
         k = _bv(key, self.domain)

@@ -15,9 +15,12 @@ from typing import Dict, Optional
 import numpy as np
 
 from mythril_amd.device import StepStats
-from mythril_amd.lanes import (_ALL_FIELDS, _SYM_FIELDS, LaneBatch, MG_DEPTH, MG_ESC_SYMBOLIC, MG_ESCAPE,
-                               MG_HALT_END, MG_HOOK, MG_LANE_HOOK_ACK, MG_LANE_SYMBOLIC, MG_RUNNING)
+from mythril_amd.lanes import (_ALL_FIELDS, _SYM_FIELDS, _TAINT_FIELDS, LaneBatch, MG_DEPTH, MG_ESC_SYMBOLIC,
+                               MG_ESCAPE, MG_HALT_END, MG_HOOK, MG_LANE_HOOK_ACK, MG_LANE_SYMBOLIC,
+                               MG_LANE_TAINT, MG_RUNNING)
 from oracle.evm_ref import OracleEVM
+
+from taintref import run_lane
 
 
 class OracleDevice:
@@ -29,6 +32,7 @@ class OracleDevice:
         self._img: Optional[LaneBatch] = None
         self._bound = 0
         self.shape = None
+        self._actions = np.zeros(256, dtype=np.uint32)
 
     # -- codes
     def load_code(self, code: bytes) -> int:
@@ -48,8 +52,12 @@ class OracleDevice:
         self._img = LaneBatch(shape)
         self._cov_on = bool(coverage)
 
+    def set_taint_program(self, actions):
+        self._actions = np.asarray(actions, dtype=np.uint32).reshape(256).copy()
+
     def _copy(self, src: LaneBatch, dst: LaneBatch, first: int, n: int):
-        fields = _ALL_FIELDS + (_SYM_FIELDS if src.symbolic and dst.symbolic else ())
+        fields = _ALL_FIELDS + (_SYM_FIELDS if src.symbolic and dst.symbolic else ()) + (
+            _TAINT_FIELDS if src.taint and dst.taint else ())
         for f in fields:
             a, b = getattr(dst, f), getattr(src, f)
             if a.shape[1:] == b.shape[1:]:
@@ -94,8 +102,18 @@ class OracleDevice:
             self.o.set_coverage(cid, buf if self._cov_on else None)
         bound = self._bound if self._img.shape.trace_cap else 0
         self._park_symbolic(hook_mask, max_depth)
-        steps = self.o.run(self._img, hook_mask=hook_mask or (0, 0, 0, 0), max_steps=max_steps,
+        img = self._img
+        # taint lanes are k_sym_step's: the restatement steps them (tests/taintref.py)
+        tl = np.nonzero((img.status == MG_RUNNING) & ((img.flags & MG_LANE_TAINT) != 0)
+                        & ((img.flags & MG_LANE_SYMBOLIC) == 0))[0] if img.taint else np.zeros(0, dtype=int)
+        img.status[tl] = 0xFF
+        steps = self.o.run(img, hook_mask=hook_mask or (0, 0, 0, 0), max_steps=max_steps,
                            max_depth=max_depth, horizon=horizon, loop_bound=bound)
+        img.status[tl] = MG_RUNNING
+        mask = hook_mask or (0, 0, 0, 0)
+        for i in tl:
+            ops, _ = self.o.code_table(int(img.code_id[i]))
+            steps += run_lane(self.o, ops, img, int(i), self._actions, mask, max_steps, max_depth, horizon, bound)
         for cid in self._cov:
             self.o.set_coverage(cid, None)
         s = self._img.status

@@ -220,7 +220,7 @@ def test_hooks_fire_in_reference_order(dev, strategy):
 
     def rec(kind):
         def f(state):
-            log.append((kind, pos[id(state)] if id(state) in pos else pos[id(state.world_state)],
+            log.append((kind, pos[id(state.current_transaction)],
                         state.mstate.pc, tuple(x.value for x in state.mstate.stack)))
         return f
 
@@ -228,8 +228,7 @@ def test_hooks_fire_in_reference_order(dev, strategy):
     vm.register_hooks("post", {"SLOAD": [rec("post")]})
     for i, tx in enumerate(txs):
         _setup_global_state_for_execution(vm, tx)
-        pos[id(vm.work_list[-1])] = i
-        pos[id(vm.work_list[-1].world_state)] = i
+        pos[id(tx)] = i            # hooked states are the hooks' own: a path is its transaction
     vm.exec()
     # expected global order from per-lane sequences
     flat = [(k, r, i, pc, st) for i, evs in expected.items() for (k, r, pc, st) in evs]
@@ -372,9 +371,13 @@ def test_bounded_loops_strategy_drops_like_the_oracle(dev, hooked):
     final = vm.exec(track_gas=True)
     halted = [i for i in range(len(ns)) if int(b.status[i]) == 1]
     assert len(vm.open_states) == len(halted)
-    assert {id(s) for s in final} == {id(states[i]) for i in halted}
+    # a hooked state stays the hooks' own and its path goes on with a copy (as in
+    # the reference): paths are told apart by their transaction
+    by_tx = {id(s.current_transaction): s for s in final}
+    assert set(by_tx) == {id(states[i].current_transaction) for i in halted}
     for i in halted:
-        ann = [a for a in states[i].annotations if isinstance(a, JumpdestCountAnnotation)]
+        ann = [a for a in by_tx[id(states[i].current_transaction)].annotations
+               if isinstance(a, JumpdestCountAnnotation)]
         assert ann and ann[0].trace == [int(x) for x in b.trace[i, : int(b.trace_len[i])]]
     if hooked:
         # every JUMPDEST pop that survived the bound fired the hook once

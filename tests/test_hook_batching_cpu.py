@@ -67,7 +67,9 @@ def _run(strategy, batching, monkeypatch):
     tag = {}
 
     def who(state):
-        return tag.get(id(state), tag.get(id(state.world_state)))
+        # a hooked state is the hooks' own (the lane goes on with a copy, as the
+        # reference's evaluate does): paths are told apart by their transaction
+        return tag.get(id(state.current_transaction))
 
     def pre(name):
         def f(state):
@@ -80,10 +82,9 @@ def _run(strategy, batching, monkeypatch):
     vm.register_laser_hooks("add_world_state", lambda s: log.append(("ws", who(s))))
     for k, tx in enumerate(_states()):
         _setup_global_state_for_execution(vm, tx)
-        tag[id(vm.work_list[-1])] = k
-        tag[id(vm.work_list[-1].world_state)] = k
+        tag[id(tx)] = k
     vm.exec()
-    opened = [tag.get(id(ws)) for ws in vm.open_states]
+    opened = [tag.get(id(ws.transaction_sequence[-1])) for ws in vm.open_states]
     return log, opened, vm.launches, vm.lane_steps
 
 
