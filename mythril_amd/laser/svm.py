@@ -524,7 +524,7 @@ class LaserEVM:
             if r[1] == "keccak":
                 keccak_function_manager.register_concrete(r[2], r[3])
             elif r[1] == "annot":
-                tnt.note_record(self._tl[i], r, len(lanes[i].state.world_state.constraints))
+                tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
             else:
                 _, cond = exponent_function_manager.create_condition(
                     symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))
@@ -581,7 +581,7 @@ class LaserEVM:
             sched.dirty.clear()
             if self._plan is not None and self._plan.key() != plan_key[0]:
                 # a module's issue cache changed: its hooks may no longer be batch-safe
-                self._plan = tnt.TaintPlan(self)
+                self._plan = tnt.TaintPlan(self, prev=self._plan)
                 plan_key[0] = self._plan.key()
                 dev.set_taint_program(self._plan.actions)
                 mask[:] = _mask(self._hooked_ops())

@@ -25,10 +25,10 @@ module is the host half:
   ``pack`` writes a state's objects into the planes, ``materialise`` rebuilds
   them (the same Python objects where they existed, so identity and in-place
   annotation behave as in the reference);
-* the device logs an MG_REC_ANNOT record for every atom it creates; when an atom
-  reaches a materialised state the host replays the module's *own* hook
-  (``module.execute``) on a state built from the record, and the annotations
-  the hook adds become the atom's set.  A sink hook is replayed once per
+* the device logs an MG_REC_ANNOT record for every atom it creates; when the
+  host replays the lane's records in the reference's global order it runs the
+  module's *own* hook (``module.execute``) on a state built from the record, and
+  the annotations the hook adds become the atom's set.  A sink hook is replayed once per
   materialisation on the lane's real state with a word carrying everything the
   sinks collected, so the module's own state annotation receives them.
 
@@ -135,9 +135,11 @@ def _resolve_types(mod, names) -> Tuple[type, ...]:
 
 
 class TaintPlan:
-    """What the device does for a LaserEVM's registered hooks."""
+    """What the device does for a LaserEVM's registered hooks.  `prev`: the plan
+    this one replaces mid-batch; its replay tables stay (the device may already
+    have applied its actions, and their records and sinks replay later)."""
 
-    def __init__(self, laser):
+    def __init__(self, laser, prev: Optional["TaintPlan"] = None):
         self.actions = np.zeros(256, dtype=np.uint32)
         self.safe: set = set()                         # opcode bytes the device no longer stops at
         self.pre_replay: Dict[int, List[Callable]] = {}
@@ -147,6 +149,7 @@ class TaintPlan:
         self.yield_types: Tuple[type, ...] = ()
         self.modules: List = []
         if laser._execute_state_hooks:
+            prev = None
             return                                     # every opcode is a host event anyway
         sink_mod = None
         for name, op in OPCODES.items():
@@ -202,6 +205,19 @@ class TaintPlan:
                 m = _module_of(h)
                 if all(m is not x for x in self.modules):
                     self.modules.append(m)
+        if prev is not None:
+            for k, v in prev.pre_replay.items():
+                self.pre_replay.setdefault(k, v)
+            for k, v in prev.post_replay.items():
+                self.post_replay.setdefault(k, v)
+            for k, v in prev.pre_operand.items():
+                self.pre_operand.setdefault(k, v)
+            if self.sink is None:
+                self.sink = prev.sink
+            self.yield_types = tuple(dict.fromkeys(self.yield_types + prev.yield_types))
+            for m in prev.modules:
+                if all(m is not x for x in self.modules):
+                    self.modules.append(m)
 
     @property
     def active(self) -> bool:
@@ -213,14 +229,12 @@ class TaintPlan:
 
 
 class LaneTaint:
-    """Host side of one taint lane: handle -> object, atom -> annotation set,
-    and the records of device atoms not resolved yet."""
-    __slots__ = ("objs", "atoms", "pending")
+    """Host side of one taint lane: handle -> object, atom -> annotation set."""
+    __slots__ = ("objs", "atoms")
 
     def __init__(self):
         self.objs: Dict[int, Expression] = {}
         self.atoms: List[Optional[frozenset]] = []
-        self.pending: Dict[int, tuple] = {}
 
 
 def state_needs_taint(state) -> bool:
@@ -235,7 +249,7 @@ def state_needs_taint(state) -> bool:
 def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
     """Write state's object graph into lane i's taint planes.  False when it needs
     more than 64 atoms or the object table (the lane cannot carry it)."""
-    lt.objs, lt.atoms, lt.pending = {}, [], {}
+    lt.objs, lt.atoms = {}, []
     atom_of: Dict[int, int] = {}
     keep = []
 
@@ -325,22 +339,14 @@ def _snapshot(state, pc: int, stack, n_constraints: int):
     return g
 
 
-def note_record(lt: LaneTaint, rec, n_constraints: int) -> None:
-    """An MG_REC_ANNOT record in the lane's execution order (lanes.records)."""
+def note_record(lt: LaneTaint, rec, state, plan: TaintPlan) -> None:
+    """An MG_REC_ANNOT record, replayed in the reference's global execution order
+    (LaserEVM._replay_records): the module's own hook runs now, on a state built
+    from the record, so it sees the module's caches and the path's constraints
+    as they are at that step; what it annotates becomes the atom's set."""
     _step, _kind, atom, pc, op, post, v0, v1 = rec
     while len(lt.atoms) <= atom:
         lt.atoms.append(None)
-    lt.pending[atom] = (pc, op, post, v0, v1, n_constraints)
-
-
-def _resolve(lt: LaneTaint, atom: int, state, plan: TaintPlan) -> frozenset:
-    got = lt.atoms[atom] if atom < len(lt.atoms) else None
-    if got is not None:
-        return got
-    rec = lt.pending.pop(atom, None)
-    if rec is None:
-        raise RuntimeError(f"taint atom {atom} has no record")
-    pc, op, post, v0, v1, ncons = rec
     o0, o1 = symbol_factory.BitVecVal(v0, 256), symbol_factory.BitVecVal(v1, 256)
     if post:
         target = o0
@@ -350,12 +356,17 @@ def _resolve(lt: LaneTaint, atom: int, state, plan: TaintPlan) -> frozenset:
         target = o0 if plan.pre_operand.get(op, 0) == 0 else o1
         hooks = plan.pre_replay.get(op, ())
         pc_at = pc
-    snap = _snapshot(state, pc_at, [o1, o0], ncons)
+    snap = _snapshot(state, pc_at, [o1, o0], len(state.world_state.constraints))
     for h in hooks:
         h(snap)
-    s = frozenset(target.annotations)
-    lt.atoms[atom] = s
-    return s
+    lt.atoms[atom] = frozenset(target.annotations)
+
+
+def _resolve(lt: LaneTaint, atom: int, state, plan: TaintPlan) -> frozenset:
+    got = lt.atoms[atom] if atom < len(lt.atoms) else None
+    if got is None:
+        raise RuntimeError(f"taint atom {atom} has no record")
+    return got
 
 
 def atoms_set(lt: LaneTaint, m: int, state, plan: TaintPlan) -> frozenset:

@@ -1,0 +1,249 @@
+"""Restatements of two reference detection modules -- TEST INFRASTRUCTURE ONLY.
+
+The reference's modules cannot be imported here (z3, eth_abi absent), so the
+taint tests drive LaserEVM with these restatements of their hook logic on the
+repo's expression layer.  Class names match the reference's so the taint
+registry (mythril_amd/laser/taint.py BATCH_SAFE) recognises them as it would
+the originals; the device must produce the same annotations, state annotations
+and issues as running every hook on the host.
+
+* IntegerArithmetics: analysis/module/modules/integer.py:33-339 (annotation
+  classes :33-61, hooks :75-85, handlers :140-306).  Issue reporting keeps the
+  reference's control flow but, with no SMT backend here, decides satisfiability
+  only for constant constraint sets (concrete lanes produce nothing else) and
+  records (swc, ostate address, operator, end address) instead of an Issue.
+* TxOrigin: dependence_on_origin.py:18-107.
+* DetectionModule.execute: analysis/module/base.py:72-96 (the cache check).
+"""
+from __future__ import annotations
+
+from copy import copy
+from math import ceil, log2
+from typing import List, Set
+
+from mythril_amd.smt.expr import (And, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, BitVec, Bool,
+                                  Expression, If, Not, symbol_factory)
+
+
+class _Base:
+    """base.py:30-96 (the parts hooks reach)."""
+    auto_cache = True
+
+    def __init__(self):
+        self.issues: List = []
+        self.cache: Set = set()
+
+    def reset_module(self):
+        self.issues = []
+
+    def update_cache(self, issues=None):
+        for issue in issues or self.issues:
+            self.cache.add((issue[1], issue[-1]))
+
+    def execute(self, target):
+        addr = target.get_current_instruction()["address"]
+        if (addr, target.environment.code.bytecode) in self.cache and self.auto_cache:
+            return []
+        result = self._execute(target)
+        if result:
+            if self.auto_cache:
+                self.update_cache(result)
+            self.issues += result
+        return result
+
+
+def _sat(constraints) -> bool:
+    """solver.get_model on a constant set (concrete lanes): True/False; raises
+    for anything symbolic (no backend in this image)."""
+    for c in constraints:
+        v = c.value if isinstance(c, Bool) else bool(c)
+        if v is None:
+            raise NotImplementedError("symbolic constraint: no SMT backend in the tests")
+        if not v:
+            return False
+    return True
+
+
+# ---------------------------------------------------------------- integer.py
+class OverUnderflowAnnotation:
+    """integer.py:33-46."""
+
+    def __init__(self, overflowing_state, operator: str, constraint) -> None:
+        self.overflowing_state = overflowing_state
+        self.operator = operator
+        self.constraint = constraint
+
+    def __deepcopy__(self, memodict={}):
+        return copy(self)
+
+
+class OverUnderflowStateAnnotation:
+    """integer.py:49-61."""
+
+    def __init__(self) -> None:
+        self.overflowing_state_annotations = set()
+
+    def __copy__(self):
+        new = OverUnderflowStateAnnotation()
+        new.overflowing_state_annotations = copy(self.overflowing_state_annotations)
+        return new
+
+
+class IntegerArithmetics(_Base):
+    """integer.py:64-306."""
+    swc_id = "101"
+    pre_hooks = ["ADD", "MUL", "EXP", "SUB", "SSTORE", "JUMPI", "STOP", "RETURN", "CALL"]
+    post_hooks: List[str] = []
+
+    def __init__(self):
+        super().__init__()
+        self._ostates_satisfiable = set()
+        self._ostates_unsatisfiable = set()
+
+    def _execute(self, state):
+        opcode = state.get_current_instruction()["opcode"]
+        funcs = {
+            "ADD": [self._handle_add], "SUB": [self._handle_sub], "MUL": [self._handle_mul],
+            "SSTORE": [self._handle_sstore], "JUMPI": [self._handle_jumpi], "CALL": [self._handle_call],
+            "RETURN": [self._handle_return, self._handle_transaction_end],
+            "STOP": [self._handle_transaction_end], "EXP": [self._handle_exp],
+        }
+        results = []
+        for func in funcs[opcode]:
+            result = func(state)
+            if result and len(result) > 0:
+                results += result
+        return results
+
+    def _get_args(self, state):
+        stack = state.mstate.stack
+        return self._make_bitvec_if_not(stack, -1), self._make_bitvec_if_not(stack, -2)
+
+    def _handle_add(self, state):
+        op0, op1 = self._get_args(state)
+        c = Not(BVAddNoOverflow(op0, op1, False))
+        op0.annotate(OverUnderflowAnnotation(state, "addition", c))
+
+    def _handle_mul(self, state):
+        op0, op1 = self._get_args(state)
+        c = Not(BVMulNoOverflow(op0, op1, False))
+        op0.annotate(OverUnderflowAnnotation(state, "multiplication", c))
+
+    def _handle_sub(self, state):
+        op0, op1 = self._get_args(state)
+        c = Not(BVSubNoUnderflow(op0, op1, False))
+        op0.annotate(OverUnderflowAnnotation(state, "subtraction", c))
+
+    def _handle_exp(self, state):
+        op0, op1 = self._get_args(state)
+        if (op1.symbolic is False and op1.value == 0) or (op0.symbolic is False and op0.value < 2):
+            return
+        if op0.symbolic and op1.symbolic:
+            constraint = And(op1 > symbol_factory.BitVecVal(256, 256), op0 > symbol_factory.BitVecVal(1, 256))
+        elif op0.symbolic:
+            constraint = op0 >= symbol_factory.BitVecVal(2 ** ceil(256 / op1.value), 256)
+        else:
+            constraint = op1 >= symbol_factory.BitVecVal(ceil(256 / log2(op0.value)), 256)
+        op0.annotate(OverUnderflowAnnotation(state, "exponentiation", constraint))
+
+    @staticmethod
+    def _make_bitvec_if_not(stack, index):
+        value = stack[index]
+        if isinstance(value, BitVec):
+            return value
+        if isinstance(value, Bool):
+            return If(value, 1, 0)
+        stack[index] = symbol_factory.BitVecVal(value, 256)
+        return stack[index]
+
+    @staticmethod
+    def _handle_sstore(state) -> None:
+        value = state.mstate.stack[-2]
+        if not isinstance(value, Expression):
+            return
+        sa = _get_state_annotation(state)
+        for a in value.annotations:
+            if isinstance(a, OverUnderflowAnnotation):
+                sa.overflowing_state_annotations.add(a)
+
+    @staticmethod
+    def _handle_jumpi(state):
+        value = state.mstate.stack[-2]
+        sa = _get_state_annotation(state)
+        for a in value.annotations:
+            if isinstance(a, OverUnderflowAnnotation):
+                sa.overflowing_state_annotations.add(a)
+
+    @staticmethod
+    def _handle_call(state):
+        value = state.mstate.stack[-3]
+        sa = _get_state_annotation(state)
+        for a in value.annotations:
+            if isinstance(a, OverUnderflowAnnotation):
+                sa.overflowing_state_annotations.add(a)
+
+    @staticmethod
+    def _handle_return(state) -> None:
+        # concrete lanes hold bytes (no Expression) in memory: nothing to collect
+        _get_state_annotation(state)
+
+    def _handle_transaction_end(self, state):
+        sa = _get_state_annotation(state)
+        issues = []
+        for annotation in sa.overflowing_state_annotations:
+            ostate = annotation.overflowing_state
+            if ostate in self._ostates_unsatisfiable:
+                continue
+            if ostate not in self._ostates_satisfiable:
+                if _sat(list(ostate.world_state.constraints) + [annotation.constraint]):
+                    self._ostates_satisfiable.add(ostate)
+                else:
+                    self._ostates_unsatisfiable.add(ostate)
+                    continue
+            if not _sat(list(state.world_state.constraints) + [annotation.constraint]):
+                continue
+            issues.append((self.swc_id, ostate.get_current_instruction()["address"], annotation.operator,
+                           state.get_current_instruction()["address"], ostate.environment.code.bytecode))
+        return issues
+
+
+def _get_state_annotation(state) -> OverUnderflowStateAnnotation:
+    """integer.py:326-339."""
+    anns = list(state.get_annotations(OverUnderflowStateAnnotation))
+    if not anns:
+        sa = OverUnderflowStateAnnotation()
+        state.annotate(sa)
+        return sa
+    return anns[0]
+
+
+# ------------------------------------------------------- dependence_on_origin.py
+class TxOriginAnnotation:
+    """dependence_on_origin.py:18-22."""
+
+
+class TxOrigin(_Base):
+    """dependence_on_origin.py:25-107 (an issue is recorded as (swc, address))."""
+    swc_id = "115"
+    pre_hooks = ["JUMPI"]
+    post_hooks = ["ORIGIN"]
+
+    def _execute(self, state):
+        issues = []
+        if state.get_current_instruction()["opcode"] == "JUMPI":
+            for annotation in state.mstate.stack[-2].annotations:
+                if isinstance(annotation, TxOriginAnnotation):
+                    issues.append((self.swc_id, state.get_current_instruction()["address"],
+                                   state.environment.code.bytecode))
+        else:
+            state.mstate.stack[-1].annotate(TxOriginAnnotation())
+        return issues
+
+
+def hooks_of(modules, hook_type="pre"):
+    """module/util.py:13-43 get_detection_module_hooks."""
+    out = {}
+    for m in modules:
+        for op in (m.pre_hooks if hook_type == "pre" else m.post_hooks):
+            out.setdefault(op.upper(), []).append(m.execute)
+    return out

@@ -89,14 +89,16 @@ class RefLane:
                     self.fixed[h] = Obj(_bits(b.omask[i, h]))
                 self.stack.append(self.fixed[h])
         self.n_fixed = int(b.n_fixed[i])
+        self.n_obj = int(b.n_obj[i])
         self.natoms = int(b.n_atoms[i])
         self.sink = _bits(b.sink[i])
         self.tflags = int(b.tflags[i])
         self.ymask = _bits(b.ymask[i])
 
     def write(self, b, i: int) -> None:
-        """Planes for these objects: the host's handles stay, the rest are numbered
-        from n_fixed in order of first appearance."""
+        """Planes for these objects: existing handles stay, new objects get handles
+        from n_obj on in order of first appearance (the device allocates past
+        every handle in use)."""
         b.omask[i] = 0
         for h, o in self.env.items():
             b.omask[i, h] = _mask(o.ann)
@@ -104,11 +106,19 @@ class RefLane:
         for h, o in self.fixed.items():
             handle[id(o)] = h
             b.omask[i, h] = _mask(o.ann)
-        nxt = self.n_fixed
+        nxt = self.n_obj
         b.sobj[i] = 0
         count: Dict[int, int] = {}
         for o in self.stack:
             count[id(o)] = count.get(id(o), 0) + 1
+        new = sum(1 for o in {id(x): x for x in self.stack}.values()
+                  if id(o) not in handle and (count[id(o)] > 1 or o.ann))
+        if nxt + new + 4 > b.shape.obj_cap:
+            # the device's compaction: handles below n_fixed stay, the rest are
+            # renumbered (only their partition is observable)
+            for h in [h for h in self.fixed if h >= self.n_fixed]:
+                del handle[id(self.fixed.pop(h))]
+            nxt = self.n_fixed
         for s, o in enumerate(self.stack):
             h = handle.get(id(o))
             if h is None:
