@@ -55,6 +55,9 @@ def parse(argv=None):
                     help="batches of the C2 lanes in generation order, reported as c2_unbucketed (0: off)")
     ap.add_argument("--large-steps", type=int, default=10,
                     help="batches of the large-contract field (c2_large_contract; 0: off)")
+    ap.add_argument("--taint-lanes", type=int, default=4096,
+                    help="lanes of the taint_c2 field (0: off): C2 through LaserEVM with the integer "
+                         "and TxOrigin modules' hooks as device actions (taint lanes) and on the host")
     ap.add_argument("--symbolic-calls", type=int, default=1024,
                     help="symbolic message calls of the symbolic-lane field (0: off)")
     ap.add_argument("--no-roofline", action="store_true",
@@ -204,6 +207,11 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         _log(rank, f"hooked C2 ({args.hooked_lanes} lanes)")
         hooked = run_hooked_c2(dev, args.hooked_lanes, rank)
 
+    taint = None
+    if args.taint_lanes and gpu and not args.profile_only:
+        _log(rank, f"taint C2 ({args.taint_lanes} lanes)")
+        taint = run_taint_c2(dev, args.taint_lanes, rank)
+
     symb = None
     if args.symbolic_calls and gpu and not args.profile_only:
         _log(rank, f"symbolic calls ({args.symbolic_calls})")
@@ -256,6 +264,8 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["constraint_evals"] = c4
         if hooked is not None:
             out["hooked_c2"] = hooked
+        if taint is not None:
+            out["taint_c2"] = taint
         if symb is not None:
             out["symbolic_calls"] = symb
         print(json.dumps(out), flush=True)
@@ -317,6 +327,71 @@ def run_hooked_c2(dev, n_lanes, rank):
             "host_s": wall - dev_s, "lane_steps_per_s": laser.lane_steps / wall,
             "hook_events_per_s": events[0] / wall,
             "hooked_opcodes": {"pre": DEFAULT_MODULE_PRE, "post": DEFAULT_MODULE_POST}}
+
+
+def _c2_laser_states(laser, n_lanes, seed):
+    from mythril_amd import workloads
+    from mythril_amd.laser import Account, Disassembly, MessageCallTransaction, WorldState
+    from mythril_amd.laser.transaction import _setup_global_state_for_execution
+    from mythril_amd.lanes import limbs_to_word
+    b = workloads.c2_batch(n_lanes, seed=seed)
+    dis = Disassembly(workloads.bytecode("overflow.sol.o"))
+    for i in range(n_lanes):
+        ws = WorldState()
+        acct = Account(workloads.CONTRACT, code=dis, concrete_storage=True)
+        for k in range(int(b.storage_count[i])):
+            acct.storage.printable_storage[limbs_to_word(b.storage[i, k, :8])] = \
+                limbs_to_word(b.storage[i, k, 8:])
+        ws.put_account(acct)
+        tx = MessageCallTransaction(world_state=ws, callee_account=acct, caller=workloads.ATTACKER,
+                                    call_data=bytes(b.calldata[i, :int(b.calldata_len[i])]),
+                                    gas_price=1, gas_limit=8_000_000, origin=workloads.ATTACKER,
+                                    code=dis, call_value=0)
+        _setup_global_state_for_execution(laser, tx)
+
+
+def run_taint_c2(dev, n_lanes, rank):
+    """Taint lanes in situ: C2's lanes through the batched
+    LaserEVM (BFS) with the integer and TxOrigin detection modules registered
+    (their hook logic restated in tests/refmodules.py: the reference's modules
+    cannot be imported here).  `device`: their ADD/SUB/MUL/EXP annotations,
+    SSTORE/JUMPI collections and ORIGIN annotation run as k_sym_step actions
+    (laser/taint.py); `host`: the same hooks as host events.  Same annotations,
+    state annotations and issues either way (tests/test_gpu_taint.py)."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+    from refmodules import IntegerArithmetics, TxOrigin, hooks_of
+    from mythril_amd.laser import LaserEVM
+    from mythril_amd.laser import taint as tnt
+    from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
+    out = {"metric": "lane-steps/s with the integer + TxOrigin modules (kernel 1 taint lanes + host LaserEVM)",
+           "lanes": n_lanes, "modules": "tests/refmodules.py (integer.py, dependence_on_origin.py)"}
+    saved = tnt.BATCH_SAFE
+    try:
+        for mode in ("device", "host"):
+            tnt.BATCH_SAFE = saved if mode == "device" else {}
+            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+            laser.track_objects = True
+            mods = [IntegerArithmetics(), TxOrigin()]
+            laser.register_hooks("pre", hooks_of(mods, "pre"))
+            laser.register_hooks("post", hooks_of(mods, "post"))
+            _c2_laser_states(laser, n_lanes, workloads_seed(rank))
+            t0 = time.perf_counter()
+            laser.exec()
+            wall = time.perf_counter() - t0
+            dev_s = laser.device_ms / 1e3
+            out[mode] = {"lane_steps": int(laser.lane_steps), "launches": int(laser.launches),
+                         "wall_s": wall, "device_s": dev_s, "host_s": wall - dev_s,
+                         "lane_steps_per_s": laser.lane_steps / wall,
+                         "issues": len(mods[0].issues) + len(mods[1].issues)}
+    finally:
+        tnt.BATCH_SAFE = saved
+    out["speedup"] = out["device"]["lane_steps_per_s"] / out["host"]["lane_steps_per_s"]
+    return out
+
+
+def workloads_seed(rank):
+    from mythril_amd import workloads
+    return workloads.C2_SEED + 11 + rank
 
 
 def run_large(dev, args, rank, barrier):

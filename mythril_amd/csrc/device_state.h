@@ -50,6 +50,8 @@ struct DevSym {
 struct DevTaint {
     uint32_t obj_cap;
     const uint32_t *prog;              // [256] action word per opcode (mg_taint_program)
+    const uint8_t *force;              // per code instruction (coverage layout): 1 = the host runs
+                                       // this instruction's hooks (mg_taint_force), or null
     uint32_t *sobj;                    // [stack_cap][N]
     unsigned long long *omask;         // [obj_cap][N]
     uint32_t *oremap;                  // [obj_cap][N] scratch of the handle compaction

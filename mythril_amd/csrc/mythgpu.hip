@@ -45,6 +45,8 @@ struct mg_ctx {
     DevSym S{};                          // symbolic planes (mg_sym_alloc), freed with the lanes
     DevTaint T{};                        // taint planes (mg_taint_alloc), freed with the lanes
     uint32_t *d_tprog = nullptr;         // [256] taint action words (mg_taint_program)
+    uint8_t *d_tforce = nullptr;         // per code instruction (coverage layout): host-run hooks
+    size_t cap_tforce = 0;
     std::vector<void *> lane_allocs;
     // resident initial image for mg_lanes_reset
     uint32_t *i_pc = nullptr, *i_depth = nullptr, *i_status = nullptr, *i_aux = nullptr,
@@ -228,6 +230,7 @@ extern "C" void mg_close(mg_ctx *ctx) {
     hipFree(ctx->d_codes); hipFree(ctx->d_a8); hipFree(ctx->d_a32); hipFree(ctx->d_cov);
     hipFree(ctx->d_stage);
     hipFree(ctx->d_tprog);
+    hipFree(ctx->d_tforce);
     if (ctx->ev0) hipEventDestroy(ctx->ev0);
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
     for (hipEvent_t e : ctx->ev_batch) hipEventDestroy(e);
@@ -779,6 +782,7 @@ extern "C" int mg_taint_alloc(mg_ctx *ctx, uint32_t obj_cap) {
     DevTaint T{};
     T.obj_cap = obj_cap;
     T.prog = ctx->d_tprog;
+    T.force = ctx->d_tforce;
     const size_t N = ctx->L.N;
     auto get = [&](void **p, size_t bytes) -> int {
         if (hipMalloc(p, bytes) != hipSuccess) return set_err(ctx, MG_ENOMEM, "mg_taint_alloc: %zu bytes", bytes);
@@ -815,6 +819,29 @@ extern "C" int mg_taint_program(mg_ctx *ctx, const uint32_t actions[256]) {
     return MG_OK;
 }
 
+extern "C" int mg_taint_force(mg_ctx *ctx, uint32_t code_id, const uint8_t *flags, uint32_t n) {
+    if (!ctx || !flags) return MG_EINVAL;
+    if (code_id >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "unknown code_id %u", code_id);
+    const DevCode &c = ctx->codes[code_id];
+    if (n != c.n_instr) return set_err(ctx, MG_EINVAL, "mg_taint_force: %u flags for %u instructions", n, c.n_instr);
+    HIPX(ctx, hipSetDevice(ctx->device));
+    if (ctx->cov_total > ctx->cap_tforce) {
+        uint8_t *p = nullptr;
+        const size_t ncap = std::max<size_t>(ctx->cov_total, 2 * ctx->cap_tforce + 256);
+        HIPX(ctx, hipMalloc((void **)&p, ncap));
+        HIPX(ctx, hipMemsetAsync(p, 0, ncap, ctx->stream));
+        if (ctx->d_tforce) HIPX(ctx, hipMemcpyAsync(p, ctx->d_tforce, ctx->cap_tforce, hipMemcpyDeviceToDevice, ctx->stream));
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        hipFree(ctx->d_tforce);
+        ctx->d_tforce = p;
+        ctx->cap_tforce = ncap;
+    }
+    HIPX(ctx, hipMemcpyAsync(ctx->d_tforce + c.cov_off, flags, n, hipMemcpyHostToDevice, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->T.force = ctx->d_tforce;
+    return MG_OK;
+}
+
 static int check_taint_shape(mg_ctx *ctx, const mg_taint_soa *h, uint32_t first, uint32_t n) {
     if (!ctx->T.sobj) return set_err(ctx, MG_ESTATE, "mg_taint_alloc first");
     if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
@@ -833,9 +860,12 @@ extern "C" int mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *h, uint32_t firs
         if (h->n_obj[i] > h->obj_cap || h->n_fixed[i] < MG_TAINT_OBJ0 || h->n_fixed[i] > h->n_obj[i] ||
             h->n_atoms[i] > 64u)
             return set_err(ctx, MG_EINVAL, "lane %u: taint counts outside its capacities", first + i);
+        // slots above the lane's sp may hold stale handles (never read before a push
+        // writes them); every handle must index the object table
         const uint32_t *so = h->sobj + (size_t)i * h->stack_cap;
         for (uint32_t k = 0; k < h->stack_cap; ++k)
-            if (so[k] >= h->n_obj[i]) return set_err(ctx, MG_EINVAL, "lane %u slot %u: handle %u past n_obj", first + i, k, so[k]);
+            if (so[k] >= h->obj_cap)
+                return set_err(ctx, MG_EINVAL, "lane %u slot %u: handle %u past obj_cap", first + i, k, so[k]);
     }
     DevTaint &T = ctx->T;
     if ((rc = up_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;

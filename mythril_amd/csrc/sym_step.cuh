@@ -305,6 +305,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         unsigned long long pre_bit = 0ull, post_bit = 0ull;
         uint32_t rec_save = 0u;
         bool rec_pre = false;
+        // an address a module has cached an issue at: its hooks return early there
+        // (base.py:79-86), the host runs them
+        if (tact && T.force && T.force[C.cov_off + pc]) { status = ST_HOOK; aux = op; break; }
         if (tact) {
             const uint32_t yk = (tact >> 12) & 15u, pre_k = tact & 15u;
             // a yield-if hook has work only when its operand carries an atom of the class

@@ -99,6 +99,13 @@ class GpuDevice:
         arr = np.ascontiguousarray(np.asarray(actions, dtype=np.uint32).reshape(256))
         self._check(self.lib.mg_taint_program(self.ctx, arr.ctypes.data), "mg_taint_program")
 
+    def set_taint_force(self, code_id: int, flags) -> None:
+        """mg_taint_force: instructions of a code where taint lanes stop for the
+        host instead of applying the batch-safe actions."""
+        arr = np.ascontiguousarray(np.asarray(flags, dtype=np.uint8))
+        self._check(self.lib.mg_taint_force(self.ctx, int(code_id), arr.ctypes.data, arr.size),
+                    "mg_taint_force")
+
     def _planes(self, batch: LaneBatch, first: int, n: int, up: bool, dev_first: Optional[int] = None):
         """Symbolic / taint planes of host lanes [first, first + n) to or from
         device lanes [dev_first, dev_first + n) (dev_first defaults to first)."""

@@ -364,6 +364,11 @@ class LaserEVM:
             ops -= self._plan.safe          # batch-safe hooks run on the device (laser/taint.py)
         return ops
 
+    def _upload_force(self, dev) -> None:
+        """mg_taint_force for every loaded code (laser/taint.py force_flags)."""
+        for raw, cid in self._code_ids.items():
+            dev.set_taint_force(cid, self._plan.force_flags(self._code_objs[raw]))
+
     def _annotators_registered(self) -> bool:
         """A module the taint registry knows (one whose hooks annotate words) is
         hooked, batch-safe or not: its annotate() calls need object identity."""
@@ -557,6 +562,7 @@ class LaserEVM:
         dev.alloc(shape, coverage=self.record_coverage)
         if taint:
             dev.set_taint_program(plan.actions)
+            self._upload_force(dev)
         dev.upload(b)
         dev.set_loop_bound(self._loop_bound())
         mask = _mask(self._hooked_ops())
@@ -584,6 +590,7 @@ class LaserEVM:
                 self._plan = tnt.TaintPlan(self, prev=self._plan)
                 plan_key[0] = self._plan.key()
                 dev.set_taint_program(self._plan.actions)
+                self._upload_force(dev)
                 mask[:] = _mask(self._hooked_ops())
             st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
                           horizon=horizon)

@@ -32,9 +32,9 @@ module is the host half:
   materialisation on the lane's real state with a word carrying everything the
   sinks collected, so the module's own state annotation receives them.
 
-A module's hooks are batch-safe only while its issue cache is empty (a cached
-address makes DetectionModule.execute return early, base.py:79-86); after that
-its hooks run on the host again.
+A cached issue address makes DetectionModule.execute return early there
+(base.py:79-86): the device stops lanes at those instructions (mg_taint_force)
+and the host runs the hooks.
 """
 from __future__ import annotations
 
@@ -118,8 +118,6 @@ def _spec(hook: Callable, hook_type: str, opcode: str):
     table = BATCH_SAFE.get(type(mod).__name__)
     if table is None:
         return None
-    if getattr(mod, "cache", None) and getattr(mod, "auto_cache", True):
-        return None                    # base.py:79-86 would skip cached addresses
     return table.get((hook_type, opcode))
 
 
@@ -224,8 +222,31 @@ class TaintPlan:
         return bool(self.safe)
 
     def key(self):
-        """Changes when a module's issue cache does (the plan must be rebuilt)."""
+        """Changes when a module's issue cache does (the forced addresses change)."""
         return tuple(len(getattr(m, "cache", ()) or ()) for m in self.modules)
+
+    def force_addresses(self) -> set:
+        """Addresses in a module's issue cache: DetectionModule.execute returns
+        early there (base.py:79-86), so the device must not apply the module's
+        actions; the lane stops and the host runs the hooks (mg_taint_force).
+        Keyed by address only (the cache's code key is the module's own
+        business): a forced stop where no issue was cached is merely a host event."""
+        out = set()
+        for m in self.modules:
+            if getattr(m, "auto_cache", True):
+                for entry in getattr(m, "cache", ()) or ():
+                    out.add(entry[0])
+        return out
+
+    def force_flags(self, code) -> np.ndarray:
+        addrs = self.force_addresses()
+        ins = code.instruction_list
+        flags = np.zeros(len(ins), dtype=np.uint8)
+        if addrs:
+            for k, x in enumerate(ins):
+                if x["address"] in addrs and OPCODES.get(x["opcode"]) in self.safe:
+                    flags[k] = 1
+        return flags
 
 
 class LaneTaint:

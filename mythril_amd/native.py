@@ -139,6 +139,7 @@ SIGNATURES = {
     "mg_sym_download": (_I, [_P, _P, _U32, _U32]),
     "mg_taint_alloc": (_I, [_P, _U32]),
     "mg_taint_program": (_I, [_P, _P]),
+    "mg_taint_force": (_I, [_P, _U32, _P, _U32]),
     "mg_taint_upload": (_I, [_P, _P, _U32, _U32]),
     "mg_taint_download": (_I, [_P, _P, _U32, _U32]),
 }

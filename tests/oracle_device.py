@@ -33,6 +33,7 @@ class OracleDevice:
         self._bound = 0
         self.shape = None
         self._actions = np.zeros(256, dtype=np.uint32)
+        self._force = {}
 
     # -- codes
     def load_code(self, code: bytes) -> int:
@@ -54,6 +55,9 @@ class OracleDevice:
 
     def set_taint_program(self, actions):
         self._actions = np.asarray(actions, dtype=np.uint32).reshape(256).copy()
+
+    def set_taint_force(self, code_id, flags):
+        self._force[int(code_id)] = np.asarray(flags, dtype=np.uint8).copy()
 
     def _copy(self, src: LaneBatch, dst: LaneBatch, first: int, n: int):
         fields = _ALL_FIELDS + (_SYM_FIELDS if src.symbolic and dst.symbolic else ()) + (
@@ -113,7 +117,8 @@ class OracleDevice:
         mask = hook_mask or (0, 0, 0, 0)
         for i in tl:
             ops, _ = self.o.code_table(int(img.code_id[i]))
-            steps += run_lane(self.o, ops, img, int(i), self._actions, mask, max_steps, max_depth, horizon, bound)
+            steps += run_lane(self.o, ops, img, int(i), self._actions, mask, max_steps, max_depth, horizon, bound,
+                              self._force.get(int(img.code_id[i])))
         for cid in self._cov:
             self.o.set_coverage(cid, None)
         s = self._img.status

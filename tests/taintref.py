@@ -160,7 +160,7 @@ def _restore(b, i, snap):
 
 
 def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_mask, max_depth: int,
-              acked: bool, loop_bound: int = 0) -> bool:
+              acked: bool, loop_bound: int = 0, force=None) -> bool:
     """One instruction of taint lane i (its objects in `lane`), in k_sym_step's
     order: depth / end / trace and loop bound / hook / opcode escape, then the
     batch-safe hooks' checks, then the mutator.  Returns whether it executed;
@@ -194,6 +194,9 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
     _restore(b, i, at_op)
     b.status[i], b.aux[i] = MG_RUNNING, 0
     tact = int(actions[op])
+    if tact and force is not None and force[pc]:
+        b.status[i], b.aux[i] = MG_HOOK, op          # a cached issue address: the host's hooks
+        return False
     yk, pre_k = (tact >> 12) & 15, tact & 15
     if yk and sp >= yk and (lane.stack[sp - yk].ann & lane.ymask):
         b.status[i], b.aux[i] = MG_HOOK, op
@@ -284,7 +287,7 @@ def _objects(b, i, lane: RefLane, op, pc, sp0, tact, pre_atom, post_atom, snap):
 
 
 def run_lane(oracle, ops, b, i: int, actions, hook_mask, max_steps: int, max_depth: int, horizon: int,
-             loop_bound: int = 0) -> int:
+             loop_bound: int = 0, force=None) -> int:
     """k_sym_step on one taint lane: steps until it stops or its budget ends.
     Returns instructions executed."""
     if int(b.status[i]) != MG_RUNNING:
@@ -304,7 +307,7 @@ def run_lane(oracle, ops, b, i: int, actions, hook_mask, max_steps: int, max_dep
             # whose pop is traced) can still stop the lane
             oracle.run(b, i, 1, hook_mask=hook_mask, max_steps=0, max_depth=max_depth, loop_bound=loop_bound)
             break
-        if not step_lane(oracle, ops, b, i, lane, actions, hook_mask, max_depth, acked, loop_bound):
+        if not step_lane(oracle, ops, b, i, lane, actions, hook_mask, max_depth, acked, loop_bound, force):
             break
         executed += 1
     if executed and ack:

