@@ -407,6 +407,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             else if (ngmin >= glim) { stop = ST_VMEXC; sx = EXC_OOG; }
             if (stop != ST_RUNNING) {
                 if (rec_pre) L.rec_len[lane] = rec_save;   // the instruction did not run
+                // a VmException counts as an executed step, as in k_lane_step
+                if (stop != ST_ESCAPE && stop != ST_FORK) ++executed;
                 status = stop; aux = sx; break;
             }
             if (tl)
@@ -437,6 +439,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                 // the mutator's own record (EXP) was not published either; drop ours
                 L.rec_len[lane] = rec_save;
             }
+            // halts and VmExceptions count as executed steps (k_lane_step: only an
+            // escape leaves the instruction unexecuted)
+            if (R.stop != ST_ESCAPE) ++executed;
             status = R.stop; aux = R.sx; break;
         }
         if (R.sp >= 1u) V.set_stack(R.sp - 1u, R.T0);

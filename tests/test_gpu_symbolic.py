@@ -74,9 +74,10 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
             device_steps += n
             st = int(b.status[i])
             got = vm._materialise(b, i, copy(s0))
-            # the restatement: the same state, the same number of instructions
+            # the restatement: the same state, the same number of instructions (a
+            # halt or VmException counts as a step but leaves the state at its start)
             ref = s0
-            for _ in range(n):
+            for _ in range(n - (1 if st in (1, 2, 3, 5, 6) else 0)):
                 out = eng.step(ref)
                 assert len(out) == 1, (name, "the restatement forked or ended inside a device run")
                 ref = out[0]
