@@ -52,10 +52,14 @@ NO_PUSH = {0x00, 0x37, 0x39, 0x3E, 0x50, 0x52, 0x53, 0x55, 0x56, 0x57, 0x5B, 0xA
 
 
 class Obj:
-    __slots__ = ("ann",)
+    """A stack word.  `tracked`: the device has given it an object handle (it was
+    DUP'd, annotated, or made with annotations) -- only the object-table
+    capacity check (MG_ESC_TAINT) depends on it."""
+    __slots__ = ("ann", "tracked")
 
-    def __init__(self, ann=()):
+    def __init__(self, ann=(), tracked=None):
         self.ann = set(ann)
+        self.tracked = bool(self.ann) if tracked is None else tracked
 
 
 def _bits(m: int):
@@ -86,7 +90,7 @@ class RefLane:
                 self.stack.append(self.env[h])
             else:
                 if h not in self.fixed:
-                    self.fixed[h] = Obj(_bits(b.omask[i, h]))
+                    self.fixed[h] = Obj(_bits(b.omask[i, h]), tracked=True)
                 self.stack.append(self.fixed[h])
         self.n_fixed = int(b.n_fixed[i])
         self.n_obj = int(b.n_obj[i])
@@ -136,6 +140,15 @@ class RefLane:
         b.ymask[i] = _mask(self.ymask)
 
 
+def _objects_full(lane: RefLane, cap: int) -> bool:
+    """k_sym_step's object-table check before an instruction: after compaction the
+    table holds the host's handles plus one per tracked object on the stack."""
+    host = {id(o) for h, o in lane.fixed.items() if h < lane.n_fixed}
+    env = {id(o) for o in lane.env.values()}
+    live = {id(o) for o in lane.stack if o.tracked and id(o) not in host and id(o) not in env}
+    return lane.n_fixed + len(live) + 4 > cap
+
+
 def _word(b, i, slot) -> int:
     return limbs_to_word(b.stack[i, slot])
 
@@ -171,6 +184,9 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
     snap = _snap(b, i)
     if acked or pc >= ops.size:
         # the host already ran this instruction's hooks: no device actions
+        if acked and pc < ops.size and _objects_full(lane, b.shape.obj_cap):
+            b.status[i], b.aux[i] = MG_ESCAPE, int(ops[pc]) | (MG_ESC_TAINT << 8)
+            return False
         oracle.run(b, i, 1, hook_mask=hook_mask, max_steps=1, max_depth=max_depth, loop_bound=loop_bound)
         if int(b.steps[i]) != steps0 + 1:
             return False
@@ -197,6 +213,9 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
     if tact and force is not None and force[pc]:
         b.status[i], b.aux[i] = MG_HOOK, op          # a cached issue address: the host's hooks
         return False
+    if not tact and _objects_full(lane, b.shape.obj_cap):
+        b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
+        return False
     yk, pre_k = (tact >> 12) & 15, tact & 15
     if yk and sp >= yk and (lane.stack[sp - yk].ann & lane.ymask):
         b.status[i], b.aux[i] = MG_HOOK, op
@@ -208,7 +227,7 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
         if ex == 0 or base < 2:
             do_pre = False
     need = int(do_pre) + int(do_post)
-    if lane.natoms + need > 64:
+    if lane.natoms + need > 64 or _objects_full(lane, b.shape.obj_cap):
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
         return False
     if need and int(b.rec_len[i]) + need * MG_REC_ANNOT_WORDS > b.shape.rec_cap:
@@ -252,11 +271,13 @@ def _objects(b, i, lane: RefLane, op, pc, sp0, tact, pre_atom, post_atom, snap):
     pre_k, sink_k = tact & 15, (tact >> 8) & 15
     if pre_atom is not None:
         st[sp0 - pre_k].ann.add(pre_atom)
+        st[sp0 - pre_k].tracked = True
     if sink_k and sp0 >= sink_k:
         lane.sink |= st[sp0 - sink_k].ann
         lane.tflags |= 1
     before = [limbs_to_word(snap["stack"][s]) for s in range(max(0, sp0 - 3), sp0)][::-1]   # [-1], [-2], [-3]
     if 0x80 <= op <= 0x8F:                      # DUPn
+        st[-(op - 0x7F)].tracked = True
         st.append(st[-(op - 0x7F)])
     elif 0x90 <= op <= 0x9F:                    # SWAPn
         n = op - 0x8F
@@ -284,6 +305,7 @@ def _objects(b, i, lane: RefLane, op, pc, sp0, tact, pre_atom, post_atom, snap):
             st.append(r)
     if post_atom is not None:
         st[-1].ann.add(post_atom)
+        st[-1].tracked = True
 
 
 def run_lane(oracle, ops, b, i: int, actions, hook_mask, max_steps: int, max_depth: int, horizon: int,
