@@ -18,7 +18,7 @@ from typing import Dict, List, Optional, Union
 
 import numpy as np
 
-from ..smt.expr import BitVec, Bool, Expression, symbol_factory
+from ..smt.expr import BitVec, Bool, Expression, If, symbol_factory
 from .disassembly import Disassembly
 
 M256 = (1 << 256) - 1
@@ -76,9 +76,10 @@ class MachineStack(list):
         super().__init__(default_list or [])
 
     def append(self, element) -> None:
-        # machine_state.py:44-56: ints become BitVecVal; Bools (compare results)
-        # and bit-vectors are kept as they are
-        if not isinstance(element, (BitVec, Bool)):
+        # machine_state.py:29-56: ints become BitVecVal, Bools If(b, 1, 0)
+        if isinstance(element, Bool):
+            element = If(element, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
+        elif not isinstance(element, BitVec):
             element = symbol_factory.BitVecVal(int(element), 256)
         if len(self) >= self.STACK_LIMIT:
             raise StackOverflowException("Reached the EVM stack limit of 1024")

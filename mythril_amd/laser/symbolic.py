@@ -91,8 +91,16 @@ _PROV: "weakref.WeakKeyDictionary[Node, tuple]" = weakref.WeakKeyDictionary()
 
 
 def _mark(e, kind: int, imm: int, args: tuple):
+    """Record how node `e` was built.  A Bool result goes on the stack as
+    If(b, 1, 0), as MachineStack.append wraps it (machine_state.py:39-46); the
+    wrapper is what the stack holds and what encode_stack maps back to the
+    (width-1) node."""
+    width = 256
+    if isinstance(e, Bool):
+        e = If(e, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
+        width = 1
     try:
-        _PROV[e.raw] = (kind, imm, args)
+        _PROV[e.raw] = (kind, imm, args, width)
     except TypeError:
         pass
     return e
@@ -245,11 +253,10 @@ def encode_stack(b, i: int, stack: list) -> bool:
         prov = _PROV.get(raw)
         if prov is None:
             raise NotEncodable(f"expression without arena provenance: {raw!r}"[:200])
-        kind, imm, args = prov
+        kind, imm, args, width = prov
         refs = [enc(a) for a in args]
         if nn >= sh.node_cap:
             raise NotEncodable("arena full")
-        width = 1 if isinstance(e, Bool) else 256
         b.node[i, nn] = (kind | (width << 8), refs[0] if refs else 0, refs[1] if len(refs) > 1 else 0, imm)
         nodes[raw] = nn
         nn += 1

@@ -73,11 +73,15 @@ def test_decode_builds_the_restatements_expressions():
     e = symref.Engine()
     lt = e._binary(0x10, cd.size, BVV(4, 256))
     assert isinstance(lt, Bool)
-    from mythril_amd.smt.expr import If, Not
-    iszero = If(Not(lt), BVV(1, 256), BVV(0, 256))
+    from mythril_amd.smt.expr import If
+    # a Bool goes on the stack as If(b, 1, 0) (machine_state.py:39-46), and ISZERO
+    # of that word is If(word == 0, 1, 0) (instructions.py:749-763)
+    lt_w = If(lt, BVV(1, 256), BVV(0, 256))
+    iszero = If(lt_w == 0, BVV(1, 256), BVV(0, 256))
     add = e._binary(0x01, symref._word_at(cd, BVV(4, 256)), s.environment.callvalue)
-    want = [BVV(99, 256), symref._word_at(cd, BVV(4, 256)), cd.size, s.environment.callvalue, lt, iszero,
-            add, e._binary(0x14, add, BVV(4, 256)), BVV((1 << 256) - 1, 256) - symref._word_at(cd, BVV(4, 256)),
+    eq_w = If(e._binary(0x14, add, BVV(4, 256)), BVV(1, 256), BVV(0, 256))
+    want = [BVV(99, 256), symref._word_at(cd, BVV(4, 256)), cd.size, s.environment.callvalue, lt_w, iszero,
+            add, eq_w, BVV((1 << 256) - 1, 256) - symref._word_at(cd, BVV(4, 256)),
             e._binary(0x1C, BVV(224, 256), symref._word_at(cd, BVV(4, 256)))]
     assert [x.raw for x in got] == [x.raw for x in want]
     assert [type(x) for x in got] == [type(x) for x in want]
