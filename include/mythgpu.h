@@ -278,9 +278,10 @@ typedef struct mg_taint_soa {
  * the per-opcode action table (256 words; zeros = no batch-safe hooks). */
 int         mg_taint_alloc(mg_ctx *ctx, uint32_t obj_cap);
 int         mg_taint_program(mg_ctx *ctx, const uint32_t actions[256]);
-/* Instructions of a code (flags[k] != 0, n = its instruction count) at which a
- * lane stops with MG_HOOK instead of applying the opcode's actions: addresses a
- * module's issue cache holds, where its hooks return early (base.py:79-86). */
+/* Per instruction of a code (n = its instruction count): 1 = a taint lane stops
+ * there with MG_HOOK instead of applying the opcode's actions, 2 = it applies
+ * none (addresses in modules' issue caches, where DetectionModule.execute returns
+ * early, base.py:79-86: 2 when every module on the opcode has it cached). */
 int         mg_taint_force(mg_ctx *ctx, uint32_t code_id, const uint8_t *flags, uint32_t n);
 int         mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *host, uint32_t first, uint32_t n);
 int         mg_taint_download(mg_ctx *ctx, mg_taint_soa *host, uint32_t first, uint32_t n);

@@ -301,13 +301,18 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         const bool stack_op = kind == K_DUP || kind == K_SWAP || kind == K_POP;
 
         // ---- taint lanes: this opcode's batch-safe hooks (mythril_amd/laser/taint.py) ----
-        const uint32_t tact = (tl && !acked) ? T.prog[op] : 0u;
+        uint32_t tact = (tl && !acked) ? T.prog[op] : 0u;
         unsigned long long pre_bit = 0ull, post_bit = 0ull;
         uint32_t rec_save = 0u;
         bool rec_pre = false;
-        // an address a module has cached an issue at: its hooks return early there
-        // (base.py:79-86), the host runs them
-        if (tact && T.force && T.force[C.cov_off + pc]) { status = ST_HOOK; aux = op; break; }
+        // an address modules have cached an issue at: their hooks return early there
+        // (base.py:79-86): 2 = all of this opcode's modules (no actions), 1 = some
+        // of them (the host runs the hooks)
+        if (tact && T.force) {
+            const uint8_t f = T.force[C.cov_off + pc];
+            if (f == 1u) { status = ST_HOOK; aux = op; break; }
+            if (f == 2u) tact = 0u;
+        }
         if (tact) {
             const uint32_t yk = (tact >> 12) & 15u, pre_k = tact & 15u;
             // a yield-if hook has work only when its operand carries an atom of the class

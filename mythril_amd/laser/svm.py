@@ -690,6 +690,16 @@ class LaserEVM:
             self._pack(b, i, s)
             b.steps[i] = steps
             b.flags[i] |= MG_LANE_HOOK_ACK | (MG_LANE_STEP1 if post else 0)
+            if not post and self._halts_on_host(name, s, b, i):
+                # a hooked STOP / RETURN whose outcome is certain ends right here, as
+                # the device would report it -- without a launch per such event
+                b.flags[i] = int(b.flags[i]) & ~MG_LANE_HOOK_ACK
+                b.steps[i] = steps + 1
+                self.lane_steps += 1
+                self.total_states += 1
+                self._sched.set(i, "event")
+                self._deliver(ln, b, final_states, track_gas, launch, regrow, single_step)
+                return
             if not post:
                 # BFS: a resumed instruction that cannot end, escape or register
                 # at its own round joins the round's next launch instead of
@@ -823,6 +833,36 @@ class LaserEVM:
         if track_gas:
             final_states.append(s)
 
+
+    def _halts_on_host(self, name: str, s: GlobalState, b: LaneBatch, i: int) -> bool:
+        """Set lane i's halt for a hooked STOP, or a RETURN that needs no memory
+        extension and cannot run out of gas, exactly as kernel 1 would report it
+        (instructions.py:1857-1959: STOP ends before any gas check; RETURN's
+        mem_extend and check_gas_usage_limit, :1864-1872, change nothing here).
+        False when the outcome needs the device."""
+        if name == "STOP":
+            b.status[i] = MG_HALT_STOP
+            return True
+        if name != "RETURN":
+            return False
+        st = s.mstate.stack
+        if len(st) < 2:
+            return False
+        off, ln = st[-1].value, st[-2].value
+        if off is None or ln is None or off + ln >= 1 << 32:
+            return False
+        msize = len(s.mstate.memory)
+        if (ln == 0 and off > msize) or (ln and off + ln > msize):
+            return False                       # mem_extend would extend (and charge gas)
+        tx = s.current_transaction
+        lim = getattr(tx, "gas_limit", None)
+        lim = None if lim is None else (lim.value if isinstance(lim, Expression) else int(lim))
+        gmin = s.mstate.min_gas_used
+        if lim is None or gmin >= lim or gmin > 10 ** 9 or s.mstate.max_gas_used > 10 ** 9:
+            return False
+        b.status[i] = MG_HALT_RETURN
+        b.ret_offset[i], b.ret_len[i] = off, ln
+        return True
 
     def _ack_safe(self, name: str, s: GlobalState, b: LaneBatch) -> bool:
         """True when the hooked instruction of `s`, resumed with HOOK_ACK, can

@@ -146,6 +146,7 @@ class TaintPlan:
         self.sink: Optional[Tuple[Callable, str, int]] = None
         self.yield_types: Tuple[type, ...] = ()
         self.modules: List = []
+        self.op_modules: Dict[int, List] = {}          # safe opcode -> modules hooked on it
         if laser._execute_state_hooks:
             prev = None
             return                                     # every opcode is a host event anyway
@@ -199,10 +200,14 @@ class TaintPlan:
                     self.yield_types += _resolve_types(_module_of(h), s.types)
             self.actions[op] = word
             self.safe.add(op)
+            mods = []
             for h, _ in specs_pre + specs_post:
                 m = _module_of(h)
+                if all(m is not x for x in mods):
+                    mods.append(m)
                 if all(m is not x for x in self.modules):
                     self.modules.append(m)
+            self.op_modules[op] = mods
         if prev is not None:
             for k, v in prev.pre_replay.items():
                 self.pre_replay.setdefault(k, v)
@@ -225,27 +230,34 @@ class TaintPlan:
         """Changes when a module's issue cache does (the forced addresses change)."""
         return tuple(len(getattr(m, "cache", ()) or ()) for m in self.modules)
 
-    def force_addresses(self) -> set:
-        """Addresses in a module's issue cache: DetectionModule.execute returns
-        early there (base.py:79-86), so the device must not apply the module's
-        actions; the lane stops and the host runs the hooks (mg_taint_force).
-        Keyed by address only (the cache's code key is the module's own
-        business): a forced stop where no issue was cached is merely a host event."""
-        out = set()
+    def force_flags(self, code) -> np.ndarray:
+        """Per instruction of `code` (mg_taint_force): DetectionModule.execute
+        returns early at an address in the module's issue cache (base.py:79-86).
+        2 = every module hooked on the opcode has the address cached: the device
+        skips the actions; 1 = some of them have: the lane stops and the host runs
+        the hooks.  The cache's code key is the module's own business, so this is
+        keyed by address only -- a stop where no issue was cached for this code is
+        merely a host event, and a skip only happens where every module's cache
+        names the address (a code whose module hooks would have run there is the
+        case the key cannot separate; modules cache per code hash, so a batch of
+        one code is exact)."""
+        cached = []
         for m in self.modules:
             if getattr(m, "auto_cache", True):
-                for entry in getattr(m, "cache", ()) or ():
-                    out.add(entry[0])
-        return out
-
-    def force_flags(self, code) -> np.ndarray:
-        addrs = self.force_addresses()
+                cached.append((m, {entry[0] for entry in getattr(m, "cache", ()) or ()}))
         ins = code.instruction_list
         flags = np.zeros(len(ins), dtype=np.uint8)
-        if addrs:
-            for k, x in enumerate(ins):
-                if x["address"] in addrs and OPCODES.get(x["opcode"]) in self.safe:
-                    flags[k] = 1
+        if not any(c for _, c in cached):
+            return flags
+        where = {id(m): c for m, c in cached}
+        for k, x in enumerate(ins):
+            op = OPCODES.get(x["opcode"])
+            if op not in self.safe:
+                continue
+            mods = self.op_modules.get(op, ())
+            hit = [m for m in mods if x["address"] in where.get(id(m), ())]
+            if hit:
+                flags[k] = 2 if len(hit) == len(mods) else 1
         return flags
 
 

@@ -210,9 +210,11 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
     _restore(b, i, at_op)
     b.status[i], b.aux[i] = MG_RUNNING, 0
     tact = int(actions[op])
-    if tact and force is not None and force[pc]:
+    if tact and force is not None and force[pc] == 1:
         b.status[i], b.aux[i] = MG_HOOK, op          # a cached issue address: the host's hooks
         return False
+    if tact and force is not None and force[pc] == 2:
+        tact = 0                                     # every module returns early there
     if not tact and _objects_full(lane, b.shape.obj_cap):
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
         return False

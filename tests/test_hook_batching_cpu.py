@@ -121,3 +121,18 @@ def test_the_batch_exercises_the_guards(unguarded, monkeypatch):
 class _NoUndo:
     def undo(self):
         pass
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_host_halts_equal_device_halts(strategy, monkeypatch):
+    """LaserEVM._halts_on_host ends a hooked STOP / RETURN on the host instead of
+    launching the device to report it: the event log, open states and lane-steps
+    must be those of the device run (the batch includes RETURNs of in-memory data
+    and the odd codes' halts)."""
+    log_h, open_h, launches_h, steps_h = _run(strategy, True, monkeypatch)
+    monkeypatch.setattr(svm_mod.LaserEVM, "_halts_on_host", lambda self, name, s, b, i: False)
+    log_d, open_d, launches_d, steps_d = _run(strategy, None, _NoUndo())
+    assert steps_h == steps_d
+    assert log_h == log_d
+    assert open_h == open_d
+    assert launches_h < launches_d

@@ -130,6 +130,13 @@ def test_plan_actions_for_the_reference_modules():
     assert plan.key() != tnt.TaintPlan(vm).key() or True
     flags = tnt.TaintPlan(vm).force_flags(code)
     assert [code.instruction_list[k]["address"] for k in flags.nonzero()[0]] == [sub]
+    assert flags[flags.nonzero()[0][0]] == 2          # the only module on SUB: no actions there
+    # a JUMPI the integer module cached but TxOrigin did not: the host runs the hooks
+    jumpi = next(x["address"] for x in code.instruction_list if x["opcode"] == "JUMPI")
+    mods[0].cache.add((jumpi, "x"))
+    flags = tnt.TaintPlan(vm).force_flags(code)
+    k = next(k for k, x in enumerate(code.instruction_list) if x["address"] == jumpi)
+    assert flags[k] == 1
     # a foreign hook on an opcode keeps it a host event
     vm.register_hooks("pre", {"ADD": [lambda s: None]})
     assert OPCODES["ADD"] not in tnt.TaintPlan(vm).safe
