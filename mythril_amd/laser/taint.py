@@ -148,7 +148,6 @@ class TaintPlan:
         self.modules: List = []
         self.op_modules: Dict[int, List] = {}          # safe opcode -> modules hooked on it
         if laser._execute_state_hooks:
-            prev = None
             return                                     # every opcode is a host event anyway
         sink_mod = None
         for name, op in OPCODES.items():
@@ -395,17 +394,15 @@ def note_record(lt: LaneTaint, rec, state, plan: TaintPlan) -> None:
     lt.atoms[atom] = frozenset(target.annotations)
 
 
-def _resolve(lt: LaneTaint, atom: int, state, plan: TaintPlan) -> frozenset:
-    got = lt.atoms[atom] if atom < len(lt.atoms) else None
-    if got is None:
-        raise RuntimeError(f"taint atom {atom} has no record")
-    return got
-
-
-def atoms_set(lt: LaneTaint, m: int, state, plan: TaintPlan) -> frozenset:
+def atoms_set(lt: LaneTaint, m: int) -> frozenset:
+    """The annotation set of mask `m` (every atom was resolved when its record
+    was replayed, or at pack)."""
     out = frozenset()
     for k in _bits(int(m)):
-        out = out | _resolve(lt, k, state, plan)
+        got = lt.atoms[k] if k < len(lt.atoms) else None
+        if got is None:
+            raise RuntimeError(f"taint atom {k} has no record")
+        out = out | got
     return out
 
 
@@ -430,7 +427,7 @@ def materialise(b, i: int, state, lt: LaneTaint, plan: TaintPlan, words: list) -
             continue
         o = made.get(h)
         if o is None:
-            ann = atoms_set(lt, int(row[h]), state, plan)
+            ann = atoms_set(lt, int(row[h]))
             o = lt.objs.get(h)
             if o is None:
                 o = type(x)(x.raw, ann)
@@ -442,11 +439,11 @@ def materialise(b, i: int, state, lt: LaneTaint, plan: TaintPlan, words: list) -
     for h in range(1, MG_TAINT_CDSIZE + 1):
         o = lt.objs.get(h)
         if o is not None and int(row[h]):
-            ann = atoms_set(lt, int(row[h]), state, plan)
+            ann = atoms_set(lt, int(row[h]))
             if not ann <= o.annotations:
                 o.annotations = o.annotations | ann
     if int(b.tflags[i]) & 1 and plan.sink is not None:
-        replay_sink(state, atoms_set(lt, int(b.sink[i]), state, plan), plan)
+        replay_sink(state, atoms_set(lt, int(b.sink[i])), plan)
         b.tflags[i] = 0
         b.sink[i] = 0
     b.n_fixed[i] = b.n_obj[i]
