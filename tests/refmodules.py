@@ -247,3 +247,119 @@ def hooks_of(modules, hook_type="pre"):
         for op in (m.pre_hooks if hook_type == "pre" else m.post_hooks):
             out.setdefault(op.upper(), []).append(m.execute)
     return out
+
+
+# ------------------------------------------------- more default modules (§8(f)1)
+class PotentialIssuesAnnotation:
+    """analysis/potential_issues.py:65-75 (no __copy__: copies share the list)."""
+
+    def __init__(self):
+        self.potential_issues = []
+
+
+def get_potential_issues_annotation(state) -> PotentialIssuesAnnotation:
+    """potential_issues.py:77-90."""
+    for annotation in state.annotations:
+        if isinstance(annotation, PotentialIssuesAnnotation):
+            return annotation
+    annotation = PotentialIssuesAnnotation()
+    state.annotate(annotation)
+    return annotation
+
+
+class ArbitraryStorage(_Base):
+    """arbitrary_write.py:22-75: every SSTORE files a potential issue whose
+    constraint asks for the slot to hit an attacker-chosen location (recorded as
+    (swc, address, constant-folded constraint value))."""
+    swc_id = "124"
+    pre_hooks = ["SSTORE"]
+    post_hooks: List[str] = []
+
+    def _execute(self, state):
+        issues = self._analyze_state(state)
+        get_potential_issues_annotation(state).potential_issues.extend(issues)
+
+    def _analyze_state(self, state):
+        write_slot = state.mstate.stack[-1]
+        constraints = list(state.world_state.constraints) + [
+            write_slot == symbol_factory.BitVecVal(324345425435, 256)]
+        return [(self.swc_id, state.get_current_instruction()["address"],
+                 tuple(c.value if isinstance(c, Bool) else c for c in constraints))]
+
+
+class ArbitraryJump(_Base):
+    """arbitrary_jump.py:45-112: only a symbolic jump target has work."""
+    swc_id = "127"
+    pre_hooks = ["JUMP", "JUMPI"]
+    post_hooks: List[str] = []
+
+    def _execute(self, state):
+        jump_dest = state.mstate.stack[-1]
+        if jump_dest.symbolic is False:
+            return []
+        return [(self.swc_id, state.get_current_instruction()["address"], state.environment.code.bytecode)]
+
+
+class UserAssertions(_Base):
+    """user_assertions.py:30-126, the MSTORE half: a concrete value carrying the
+    assertion-failed pattern is an issue (the LOG1 half reads memory and stays a
+    host hook)."""
+    swc_id = "110"
+    pre_hooks = ["MSTORE"]
+    post_hooks: List[str] = []
+    mstore_pattern = "0xcafecafecafecafecafecafecafecafecafecafecafecafecafecafecafe"
+
+    def _execute(self, state):
+        value = state.mstate.stack[-2]
+        if value.symbolic:
+            return []
+        if self.mstore_pattern not in hex(value.value)[:126]:
+            return []
+        return [(self.swc_id, state.get_current_instruction()["address"], value.value & 0xFFFF,
+                 state.environment.code.bytecode)]
+
+
+class LastJumpAnnotation:
+    """exceptions.py:21-33."""
+
+    def __init__(self, last_jump=None):
+        self.last_jump = last_jump
+
+    def __copy__(self):
+        return LastJumpAnnotation(self.last_jump)
+
+
+class Exceptions(_Base):
+    """exceptions.py:36-137, the JUMP half: every JUMP records its address in the
+    state's LastJumpAnnotation (INVALID and REVERT end the path: host hooks)."""
+    swc_id = "110"
+    pre_hooks = ["JUMP"]
+    post_hooks: List[str] = []
+
+    def _execute(self, state):
+        address = state.get_current_instruction()["address"]
+        annotations = [a for a in state.get_annotations(LastJumpAnnotation)]
+        if len(annotations) == 0:
+            state.annotate(LastJumpAnnotation())
+            annotations = [a for a in state.get_annotations(LastJumpAnnotation)]
+        annotations[0].last_jump = address
+        return []
+
+
+class StateChangeCallsAnnotation:
+    """state_change_external_calls.py:27-40 (made by the CALL hooks)."""
+
+
+class StateChangeAfterCall(_Base):
+    """state_change_external_calls.py:104-185, the SLOAD/SSTORE half: with no
+    StateChangeCallsAnnotation on the state (no external call yet) they return
+    at once; with one, the host runs them (recorded as an issue per access)."""
+    swc_id = "107"
+    pre_hooks = ["SLOAD", "SSTORE"]
+    post_hooks: List[str] = []
+
+    def _execute(self, state):
+        annotations = list(state.get_annotations(StateChangeCallsAnnotation))
+        if len(annotations) == 0:
+            return []
+        return [(self.swc_id, state.get_current_instruction()["address"], state.environment.code.bytecode)]
