@@ -354,24 +354,29 @@ def run_taint_c2(dev, n_lanes, rank):
     """Taint lanes in situ: C2's lanes through the batched
     LaserEVM (BFS) with the integer and TxOrigin detection modules registered
     (their hook logic restated in tests/refmodules.py: the reference's modules
-    cannot be imported here).  `device`: their ADD/SUB/MUL/EXP annotations,
-    SSTORE/JUMPI collections and ORIGIN annotation run as k_sym_step actions
-    (laser/taint.py); `host`: the same hooks as host events.  Same annotations,
-    state annotations and issues either way (tests/test_gpu_taint.py)."""
+    cannot be imported here) plus ArbitraryStorage, ArbitraryJump, UserAssertions,
+    Exceptions and StateChangeAfterCall.  `device`: their batch-safe hooks run
+    as k_sym_step actions and record replays (laser/taint.py); `host`: the same
+    hooks as host events.  Same annotations, state annotations and issues
+    either way (tests/test_gpu_taint.py)."""
     sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
-    from refmodules import IntegerArithmetics, TxOrigin, hooks_of
+    import refmodules
+    from refmodules import hooks_of
+    names = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJump", "UserAssertions",
+             "Exceptions", "StateChangeAfterCall")
     from mythril_amd.laser import LaserEVM
     from mythril_amd.laser import taint as tnt
     from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
-    out = {"metric": "lane-steps/s with the integer + TxOrigin modules (kernel 1 taint lanes + host LaserEVM)",
-           "lanes": n_lanes, "modules": "tests/refmodules.py (integer.py, dependence_on_origin.py)"}
+    out = {"metric": "lane-steps/s with seven default detection modules (kernel 1 taint lanes + host LaserEVM)",
+           "lanes": n_lanes, "modules": list(names),
+           "modules_source": "tests/refmodules.py (restated: the reference's modules need z3)"}
     saved = tnt.BATCH_SAFE
     try:
         for mode in ("device", "host"):
             tnt.BATCH_SAFE = saved if mode == "device" else {}
             laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
             laser.track_objects = True
-            mods = [IntegerArithmetics(), TxOrigin()]
+            mods = [getattr(refmodules, m)() for m in names]
             laser.register_hooks("pre", hooks_of(mods, "pre"))
             laser.register_hooks("post", hooks_of(mods, "post"))
             _c2_laser_states(laser, n_lanes, workloads_seed(rank))
@@ -382,7 +387,7 @@ def run_taint_c2(dev, n_lanes, rank):
             out[mode] = {"lane_steps": int(laser.lane_steps), "launches": int(laser.launches),
                          "wall_s": wall, "device_s": dev_s, "host_s": wall - dev_s,
                          "lane_steps_per_s": laser.lane_steps / wall,
-                         "issues": len(mods[0].issues) + len(mods[1].issues)}
+                         "issues": sum(len(m.issues) for m in mods)}
     finally:
         tnt.BATCH_SAFE = saved
     out["speedup"] = out["device"]["lane_steps_per_s"] / out["host"]["lane_steps_per_s"]

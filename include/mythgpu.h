@@ -100,6 +100,9 @@ extern "C" {
  *                  opcode with MG_TAINT_POST (bit 8) for a post-hook atom.  The host
  *                  replays the module's own hook on a state built from it.        */
 #define MG_REC_ANNOT    3u
+/*   MG_REC_HOOK    a deferred batch-safe hook (MG_TAINT_DEFER): len = n words; result =
+ *                  stack[-1]; payload = stack[-2..-n] (8 limbs each), pc, opcode.       */
+#define MG_REC_HOOK     4u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */
@@ -258,6 +261,12 @@ int         mg_sym_download(mg_ctx *ctx, mg_sym_soa *host, uint32_t first, uint3
                                     state annotation (the lane's sink mask)                    */
 #define MG_TAINT_YIELD_SHIFT 12  /* bits 12..15: operand k + 1: yield (MG_HOOK) only when that
                                     word carries an atom of the yield class                   */
+#define MG_TAINT_DEFER_SHIFT 16  /* bits 16..19: 1..3: a pre-hook replayed later from a record of
+                                    stack[-1..-n] (MG_REC_HOOK); it reads only those words     */
+#define MG_TAINT_IFSYM_SHIFT 20  /* bits 20..23: operand k + 1: a pre-hook with work only when that
+                                    word is symbolic (yield then)                              */
+#define MG_TAINT_IFLANE     (1u << 24)  /* yield when the lane's tflags bit 1 is set (a state
+                                    annotation the host found at pack)                          */
 #define MG_TAINT_OBJ0        7u  /* first object-table handle                                  */
 
 /* Host image of the taint planes of lanes [first, first + n), lane-major. */
@@ -271,7 +280,7 @@ typedef struct mg_taint_soa {
     uint32_t *n_atoms;      /* [n] atoms in use (<= 64)                          */
     uint64_t *sink;         /* [n] atoms the sink hooks collected                */
     uint64_t *ymask;        /* [n] atoms of the yield class                      */
-    uint32_t *tflags;       /* [n] bit 0: a sink hook ran                         */
+    uint32_t *tflags;       /* [n] bit 0: a sink hook ran; bit 1: MG_TAINT_IFLANE yields */
 } mg_taint_soa;
 
 /* Taint planes for the current batch (after mg_lanes_alloc; freed with it) and

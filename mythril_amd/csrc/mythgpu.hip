@@ -808,8 +808,9 @@ extern "C" int mg_taint_program(mg_ctx *ctx, const uint32_t actions[256]) {
     HIPX(ctx, hipSetDevice(ctx->device));
     for (int k = 0; k < 256; ++k) {
         const uint32_t a = actions[k];
-        if (a & ~0xffffu) return set_err(ctx, MG_EINVAL, "taint action %#x of opcode %#x: unknown bits", a, k);
-        if (((a & 15u) && (a & 15u) > 7u) || ((a >> 8) & 15u) > 7u || ((a >> 12) & 15u) > 7u)
+        if (a & ~0x1ffff7fu) return set_err(ctx, MG_EINVAL, "taint action %#x of opcode %#x: unknown bits", a, k);
+        if ((a & 15u) > 7u || ((a >> 8) & 15u) > 7u || ((a >> 12) & 15u) > 7u || ((a >> 16) & 15u) > 3u ||
+            ((a >> 20) & 15u) > 7u)
             return set_err(ctx, MG_EINVAL, "taint action %#x of opcode %#x: operand out of range", a, k);
     }
     int rc;

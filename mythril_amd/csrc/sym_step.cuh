@@ -97,6 +97,8 @@ DEV uint32_t sym_env_word(uint32_t op) {
 #define T_EXPCOND 32u
 #define T_YCLASS 64u
 #define TREC_WORDS (MG_REC_HEADER + 10u)
+#define T_IFLANE (1u << 24)
+DEV uint32_t hrec_words(uint32_t n) { return MG_REC_HEADER + 8u * (n - 1u) + 2u; }
 
 DEV uint32_t t_obj(const DevTaint &T, size_t N, uint32_t lane, uint32_t slot) {
     return T.sobj[(size_t)slot * N + lane];
@@ -144,6 +146,21 @@ DEV void rec_annot(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t atom,
     for (int k = 0; k < 8; ++k) q[(size_t)(at + k) * N] = v1.w[k];
     q[(size_t)(at + 8u) * N] = pc;
     q[(size_t)(at + 9u) * N] = opw;
+}
+// MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op]
+DEV void rec_hook(const DevLanes &L, const LaneView &V, uint32_t lane, uint32_t at, uint32_t n, uint32_t step,
+                  uint32_t sp, uint32_t pc, uint32_t op) {
+    at = rec_head(L, lane, at, MG_REC_HOOK, n, step, V.stack(sp - 1u));
+    uint32_t *__restrict__ q = L.rec + lane;
+    const size_t N = L.N;
+    for (uint32_t j = 1u; j < n; ++j) {
+        const U256 w = V.stack(sp - 1u - j);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[(size_t)(at + 8u * (j - 1u) + k) * N] = w.w[k];
+    }
+    at += 8u * (n - 1u);
+    q[(size_t)at * N] = pc;
+    q[(size_t)(at + 1u) * N] = op;
 }
 // Annotation set of the word an executed opcode pushes (instructions.py:330-1060
 // with bitvec.py's unions): the operands' union for the ALU -- nothing for a
@@ -315,10 +332,19 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         }
         if (tact) {
             const uint32_t yk = (tact >> 12) & 15u, pre_k = tact & 15u;
+            const uint32_t dk = (tact >> 16) & 15u, sk = (tact >> 20) & 15u;
             // a yield-if hook has work only when its operand carries an atom of the class
             if (yk && sp >= yk && (t_mask(T, N, lane, t_obj(T, N, lane, sp - yk)) & tym)) {
                 status = ST_HOOK; aux = op; break;
             }
+            // hooks with work only on a symbolic operand, or on lanes whose state
+            // carries a given annotation; a deferred hook's words must be concrete
+            bool ysym = false;
+            if (symlane) {
+                if (sk && sp >= sk && sym_tag(S, N, lane, sp - sk)) ysym = true;
+                for (uint32_t j = 0; j < dk && j < sp; ++j) ysym |= sym_tag(S, N, lane, sp - 1u - j) != 0u;
+            }
+            if (ysym || ((tact & T_IFLANE) && (ttf & 2u))) { status = ST_HOOK; aux = op; break; }
             bool do_pre = pre_k != 0u && sp >= pre_k && sp >= req;
             const bool do_post = (tact & T_POST) != 0u;
             if (do_pre || do_post) {
@@ -335,22 +361,31 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                 }
             }
             const uint32_t need = (do_pre ? 1u : 0u) + (do_post ? 1u : 0u);
+            const bool defer = dk != 0u && sp >= dk;
             if (natoms + need > 64u) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
             if (nobj + 4u > T.obj_cap) {
                 t_gc(T, N, lane, sp, tfixed, nobj);
                 if (nobj + 4u > T.obj_cap) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
             }
-            if (need && (uint64_t)L.rec_len[lane] + need * TREC_WORDS > L.rec_cap) {
+            if ((need || defer) && (uint64_t)L.rec_len[lane] + need * TREC_WORDS + (defer ? hrec_words(dk) : 0u) >
+                                       L.rec_cap) {
                 status = ST_ESCAPE; aux = op | (ESC_RECORD << 8); break;
             }
+            rec_save = L.rec_len[lane];
             if (do_pre) {
                 // logged before the mutator runs: its own records (EXP) follow
-                rec_save = L.rec_len[lane];
-                rec_annot(L, lane, rec_save, natoms, L.steps[lane] + executed, V.stack(sp - 1u),
+                rec_annot(L, lane, L.rec_len[lane], natoms, L.steps[lane] + executed, V.stack(sp - 1u),
                           sp >= 2u ? V.stack(sp - 2u) : u_zero(), pc, op);
-                L.rec_len[lane] = rec_save + TREC_WORDS;
+                L.rec_len[lane] += TREC_WORDS;
                 rec_pre = true;
                 pre_bit = 1ull << natoms;
+            }
+            if (defer) {
+                // the deferred hook runs after the annotating ones of the opcode, as
+                // the host replays records in log order
+                rec_hook(L, V, lane, L.rec_len[lane], dk, L.steps[lane] + executed, sp, pc, op);
+                L.rec_len[lane] += hrec_words(dk);
+                rec_pre = true;
             }
             if (do_post) post_bit = 1ull << (natoms + (do_pre ? 1u : 0u));
         } else if (tl && nobj + 4u > T.obj_cap) {

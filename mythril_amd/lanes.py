@@ -37,7 +37,7 @@ MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2,
 MG_ESC_RECORD = 6
 MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 # function-manager records (include/mythgpu.h MG_REC_*)
-MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HEADER = 1, 2, 3, 11
+MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
 MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
@@ -48,6 +48,7 @@ MG_LANE_TAINT = 2048
 # taint action word (include/mythgpu.h MG_TAINT_*)
 MG_TAINT_POST, MG_TAINT_EXPCOND, MG_TAINT_YCLASS = 16, 32, 64
 MG_TAINT_SINK_SHIFT, MG_TAINT_YIELD_SHIFT = 8, 12
+MG_TAINT_DEFER_SHIFT, MG_TAINT_IFSYM_SHIFT, MG_TAINT_IFLANE = 16, 20, 1 << 24
 MG_TAINT_OBJ0 = 7
 MG_TAINT_CDSIZE = 6     # handle of the symbolic calldata-size object
 ENV_ADDRESS, ENV_CALLER, ENV_ORIGIN, ENV_CALLVALUE, ENV_GASPRICE = range(5)
@@ -327,6 +328,12 @@ class LaneBatch:
             elif kind == MG_REC_EXP:
                 out.append((step, "exp", limbs_to_word(q[k: k + 8]), limbs_to_word(q[k + 8: k + 16]), r))
                 k += 16
+            elif kind == MG_REC_HOOK:
+                # (step, "hook", [stack[-1], stack[-2], ...], pc, opcode)
+                words = [r] + [limbs_to_word(q[k + 8 * j: k + 8 * j + 8]) for j in range(ln - 1)]
+                k += 8 * (ln - 1)
+                out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF))
+                k += 2
             elif kind == MG_REC_ANNOT:
                 # (step, "annot", atom, pc, opcode, post, stack[-1], stack[-2])
                 opw = int(q[k + 9])

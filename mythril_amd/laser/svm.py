@@ -405,7 +405,9 @@ class LaserEVM:
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
                          storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap,
-                         rec_cap=512 * g, node_cap=256 * g if symbolic else 0,
+                         # taint lanes log a record per annotating / deferred hook: a
+                         # log that fills escapes and regrows (a later batch, §7)
+                         rec_cap=(4096 if taint else 512) * g, node_cap=256 * g if symbolic else 0,
                          const_cap=128 * g if symbolic else 0,
                          obj_cap=min(256 * g, 65536) if taint else 0)
 
@@ -530,6 +532,8 @@ class LaserEVM:
                 keccak_function_manager.register_concrete(r[2], r[3])
             elif r[1] == "annot":
                 tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
+            elif r[1] == "hook":
+                tnt.replay_deferred(r, lanes[i].state, self._plan)
             else:
                 _, cond = exponent_function_manager.create_condition(
                     symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))

@@ -45,8 +45,9 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 
-from ..lanes import (MG_TAINT_CDSIZE, MG_TAINT_EXPCOND, MG_TAINT_OBJ0, MG_TAINT_POST, MG_TAINT_SINK_SHIFT,
-                     MG_TAINT_YCLASS, MG_TAINT_YIELD_SHIFT)
+from ..lanes import (MG_TAINT_CDSIZE, MG_TAINT_DEFER_SHIFT, MG_TAINT_EXPCOND, MG_TAINT_IFLANE,
+                     MG_TAINT_IFSYM_SHIFT, MG_TAINT_OBJ0, MG_TAINT_POST, MG_TAINT_SINK_SHIFT, MG_TAINT_YCLASS,
+                     MG_TAINT_YIELD_SHIFT)
 from ..smt.expr import Expression, symbol_factory
 from .opcodes import OPCODES
 
@@ -83,6 +84,30 @@ class YieldIf:
     types: Tuple[str, ...]
 
 
+@dataclass(frozen=True)
+class Deferred:
+    """A pre-hook that changes nothing the path executes (it files issues or
+    updates state annotations) and reads only stack[-1..-words], the pc, the
+    environment and the path constraints: the device logs those words
+    (MG_REC_HOOK) and the host runs the hook on them when it replays the lane's
+    records, in the reference's order."""
+    words: int = 1
+
+
+@dataclass(frozen=True)
+class IfSymbolic:
+    """A pre-hook with work only when stack[-1-operand] is symbolic."""
+    operand: int
+
+
+@dataclass(frozen=True)
+class IfStateAnnotation:
+    """A pre-hook with work only when the state carries an annotation of one of
+    `types` (class names in the module's Python module); such annotations come
+    from host events, so the host knows them when it packs the lane."""
+    types: Tuple[str, ...]
+
+
 # The reference's modules (class name) -> {(hook type, opcode): action}
 BATCH_SAFE: Dict[str, Dict[Tuple[str, str], object]] = {
     # analysis/module/modules/integer.py:75-85, 140-250
@@ -96,6 +121,24 @@ BATCH_SAFE: Dict[str, Dict[Tuple[str, str], object]] = {
         ("post", "ORIGIN"): AnnotateResult(yield_class=True),
         ("pre", "JUMPI"): YieldIf(1, ("TxOriginAnnotation",)),
     },
+    # dependence_on_predictable_vars.py:47-48, 66-75: JUMPI has work only on a
+    # PredictableValueAnnotation (its block-value post hooks run on the host:
+    # those opcodes escape the device anyway)
+    "PredictableVariables": {("pre", "JUMPI"): YieldIf(1, ("PredictableValueAnnotation",))},
+    # arbitrary_jump.py:50, 74-77: a concrete target returns at once
+    "ArbitraryJump": {("pre", "JUMP"): IfSymbolic(0), ("pre", "JUMPI"): IfSymbolic(0)},
+    # arbitrary_write.py:28, 37-75: every SSTORE files a potential issue on the
+    # state's PotentialIssuesAnnotation from the slot, pc and constraints
+    "ArbitraryStorage": {("pre", "SSTORE"): Deferred(1)},
+    # user_assertions.py:38, 55-64: MSTORE reads only the stored value (LOG1 reads
+    # memory: a host hook)
+    "UserAssertions": {("pre", "MSTORE"): Deferred(2)},
+    # exceptions.py:43, 66-82: JUMP records its address in the LastJumpAnnotation
+    "Exceptions": {("pre", "JUMP"): Deferred(1)},
+    # state_change_external_calls.py:112, 148-160: SLOAD/SSTORE return at once
+    # while the state has no StateChangeCallsAnnotation (made by CALL hooks)
+    "StateChangeAfterCall": {("pre", "SLOAD"): IfStateAnnotation(("StateChangeCallsAnnotation",)),
+                             ("pre", "SSTORE"): IfStateAnnotation(("StateChangeCallsAnnotation",))},
 }
 
 
@@ -147,6 +190,8 @@ class TaintPlan:
         self.yield_types: Tuple[type, ...] = ()
         self.modules: List = []
         self.op_modules: Dict[int, List] = {}          # safe opcode -> modules hooked on it
+        self.deferred: Dict[int, List[Callable]] = {}    # opcode -> Deferred hooks, in order
+        self.iflane_types: Tuple[type, ...] = ()
         if laser._execute_state_hooks:
             return                                     # every opcode is a host event anyway
         sink_mod = None
@@ -165,6 +210,13 @@ class TaintPlan:
             ann = [s for _, s in specs_pre if isinstance(s, Annotate)]
             sinks = [(h, s) for h, s in specs_pre if isinstance(s, Sink)]
             yields = [(h, s) for h, s in specs_pre if isinstance(s, YieldIf)]
+            defers = [(h, s) for h, s in specs_pre if isinstance(s, Deferred)]
+            ifsyms = [s for _, s in specs_pre if isinstance(s, IfSymbolic)]
+            iflanes = [(h, s) for h, s in specs_pre if isinstance(s, IfStateAnnotation)]
+            if len({s.operand for s in ifsyms}) > 1 or any(s.operand > 6 for s in ifsyms):
+                continue
+            if any(not 1 <= s.words <= 3 for _, s in defers):
+                continue
             if len({a.operand for a in ann}) > 1 or any(a.operand > 1 for a in ann):
                 continue
             if len({s.operand for _, s in sinks}) > 1 or len({s.operand for _, s in yields}) > 1:
@@ -197,6 +249,15 @@ class TaintPlan:
                 word |= (yields[0][1].operand + 1) << MG_TAINT_YIELD_SHIFT
                 for h, s in yields:
                     self.yield_types += _resolve_types(_module_of(h), s.types)
+            if defers:
+                word |= max(s.words for _, s in defers) << MG_TAINT_DEFER_SHIFT
+                self.deferred[op] = [h for h, _ in defers]
+            if ifsyms:
+                word |= (ifsyms[0].operand + 1) << MG_TAINT_IFSYM_SHIFT
+            if iflanes:
+                word |= MG_TAINT_IFLANE
+                for h, s in iflanes:
+                    self.iflane_types += _resolve_types(_module_of(h), s.types)
             self.actions[op] = word
             self.safe.add(op)
             mods = []
@@ -216,6 +277,8 @@ class TaintPlan:
                 self.pre_operand.setdefault(k, v)
             if self.sink is None:
                 self.sink = prev.sink
+            for k, v in prev.deferred.items():
+                self.deferred.setdefault(k, v)
             self.yield_types = tuple(dict.fromkeys(self.yield_types + prev.yield_types))
             for m in prev.modules:
                 if all(m is not x for x in self.modules):
@@ -345,6 +408,9 @@ def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
             if any(isinstance(a, plan.yield_types) for a in s):
                 ym |= 1 << k
     b.ymask[i] = ym
+    if plan is not None and plan.iflane_types and any(
+            isinstance(a, plan.iflane_types) for a in state.annotations):
+        b.tflags[i] = 2                    # MG_TAINT_IFLANE hooks have work on this path
     return True
 
 
@@ -392,6 +458,26 @@ def note_record(lt: LaneTaint, rec, state, plan: TaintPlan) -> None:
     for h in hooks:
         h(snap)
     lt.atoms[atom] = frozenset(target.annotations)
+
+
+def replay_deferred(rec, state, plan: TaintPlan) -> None:
+    """An MG_REC_HOOK record, in the reference's global execution order: the
+    opcode's deferred hooks (the modules' own `execute`) run on a state with the
+    recorded words, pc and path constraints as of that step, sharing the lane's
+    state and world-state annotations, so what they file lands where the
+    reference's hooks put it."""
+    from .state import GlobalState, MachineState
+    _step, _kind, words, pc, op = rec
+    ws = copy(state.world_state)
+    ws._annotations = state.world_state._annotations
+    stack = [symbol_factory.BitVecVal(w, 256) for w in reversed(words)]
+    snap = GlobalState(ws, state.environment, state.node,
+                       MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack,
+                                    depth=state.mstate.depth),
+                       transaction_stack=list(state.transaction_stack), last_return_data=state.last_return_data)
+    snap._annotations = state._annotations
+    for h in plan.deferred.get(op, ()):
+        h(snap)
 
 
 def atoms_set(lt: LaneTaint, m: int) -> frozenset:

@@ -38,7 +38,8 @@ from typing import Dict, List
 import numpy as np
 
 from mythril_amd.lanes import (MG_ESC_OPCODE, MG_ESC_RECORD, MG_ESC_TAINT, MG_ESCAPE, MG_HOOK,
-                               MG_LANE_HOOK_ACK, MG_LANE_STEP1, MG_REC_ANNOT, MG_REC_ANNOT_WORDS,
+                               MG_LANE_HOOK_ACK, MG_LANE_STEP1, MG_REC_ANNOT, MG_REC_ANNOT_WORDS, MG_REC_HOOK,
+                               MG_TAINT_IFLANE,
                                MG_REC_HEADER, MG_RUNNING, MG_TAINT_CDSIZE, MG_TAINT_EXPCOND,
                                MG_TAINT_OBJ0, MG_TAINT_POST, MG_TAINT_YCLASS, limbs_to_word,
                                word_to_limbs)
@@ -162,6 +163,19 @@ def _write_annot(b, i, at, atom, step, v0, v1, pc, opw):
     q[at + MG_REC_HEADER + 9] = opw
 
 
+def _write_hook(b, i, at, words, step, pc, op):
+    """MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op]."""
+    q = b.rec[i]
+    q[at], q[at + 1], q[at + 2] = MG_REC_HOOK, len(words), step
+    q[at + 3: at + 11] = word_to_limbs(words[0])
+    k = at + MG_REC_HEADER
+    for w in words[1:]:
+        q[k: k + 8] = word_to_limbs(w)
+        k += 8
+    q[k], q[k + 1] = pc, op
+    return k + 2 - at
+
+
 def _snap(b, i):
     from mythril_amd.lanes import _ALL_FIELDS
     return {f: getattr(b, f)[i].copy() for f in _ALL_FIELDS}
@@ -219,7 +233,13 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
         return False
     yk, pre_k = (tact >> 12) & 15, tact & 15
+    dk = (tact >> 16) & 15
     if yk and sp >= yk and (lane.stack[sp - yk].ann & lane.ymask):
+        b.status[i], b.aux[i] = MG_HOOK, op
+        return False
+    # concrete lanes: an if-symbolic hook never has work; an if-annotation hook
+    # has work when the host flagged the lane (tflags bit 1)
+    if tact & MG_TAINT_IFLANE and lane.tflags & 2:
         b.status[i], b.aux[i] = MG_HOOK, op
         return False
     do_pre = pre_k != 0 and sp >= pre_k
@@ -229,10 +249,12 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
         if ex == 0 or base < 2:
             do_pre = False
     need = int(do_pre) + int(do_post)
+    defer = dk != 0 and sp >= dk
+    hook_words = MG_REC_HEADER + 8 * (dk - 1) + 2 if defer else 0
     if lane.natoms + need > 64 or _objects_full(lane, b.shape.obj_cap):
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
         return False
-    if need and int(b.rec_len[i]) + need * MG_REC_ANNOT_WORDS > b.shape.rec_cap:
+    if (need or defer) and int(b.rec_len[i]) + need * MG_REC_ANNOT_WORDS + hook_words > b.shape.rec_cap:
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_RECORD << 8)
         return False
     pre_atom = post_atom = None
@@ -242,6 +264,9 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
                      pc, op)
         b.rec_len[i] = rec0 + MG_REC_ANNOT_WORDS
         pre_atom = lane.natoms
+    if defer:
+        at = int(b.rec_len[i])
+        b.rec_len[i] = at + _write_hook(b, i, at, [_word(b, i, sp - 1 - j) for j in range(dk)], steps0, pc, op)
     b.flags[i] = flags0 | MG_LANE_HOOK_ACK          # run the mutator, not the trace again
     oracle.run(b, i, 1, hook_mask=(0, 0, 0, 0), max_steps=1, max_depth=max_depth, loop_bound=loop_bound)
     if int(b.steps[i]) != steps0 + 1:

@@ -37,6 +37,13 @@ ACTIONS[OPCODES["EXP"]] = 1 | 32
 ACTIONS[OPCODES["SSTORE"]] = 2 << 8
 ACTIONS[OPCODES["JUMPI"]] = (2 << 8) | (2 << 12)
 ACTIONS[OPCODES["ORIGIN"]] = 16 | 64
+# deferred hooks (ArbitraryStorage SSTORE, UserAssertions MSTORE, Exceptions JUMP),
+# ArbitraryJump's if-symbolic JUMP/JUMPI, StateChangeAfterCall's if-annotation SLOAD
+ACTIONS[OPCODES["SSTORE"]] |= 1 << 16
+ACTIONS[OPCODES["MSTORE"]] = 2 << 16
+ACTIONS[OPCODES["JUMP"]] = (1 << 16) | (1 << 20)
+ACTIONS[OPCODES["JUMPI"]] |= 1 << 20
+ACTIONS[OPCODES["SLOAD"]] = 1 << 24
 
 CRAFTED = [
     # PUSH 3, PUSH 5, DUP2, ADD (annotates the DUP'd 3: slot 0 too), PUSH 0, SSTORE, STOP
@@ -81,6 +88,7 @@ def _batch(n_c2=48, obj_cap=64):
     b.flags[:] |= MG_LANE_TAINT
     b.n_obj[:] = MG_TAINT_OBJ0
     b.n_fixed[:] = MG_TAINT_OBJ0
+    b.tflags[::5] = 2                 # these lanes' states carry the if-annotation class
     return b, codes, n_c2
 
 
@@ -149,13 +157,15 @@ def test_device_taint_planes_match_the_restatement(obj_cap):
 
 
 @pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
-def test_laser_taint_on_the_gpu_matches_host_hooks(strategy, monkeypatch):
+@pytest.mark.parametrize("modules", ["integer+origin", "default"])
+def test_laser_taint_on_the_gpu_matches_host_hooks(strategy, modules, monkeypatch):
     import test_taint_cpu as t
+    mods = t.DEFAULT_SET if modules == "default" else ("IntegerArithmetics", "TxOrigin")
     gpu = GpuDevice(0)
     try:
-        ends_d, issues_d, launches_d, steps_d = t._run(strategy, "device", monkeypatch, device=gpu)
-        ends_h, issues_h, launches_h, steps_h = t._run(strategy, "host", monkeypatch, device=gpu)
-        ends_c, issues_c, _, steps_c = t._run(strategy, "device", monkeypatch)     # oracle device
+        ends_d, issues_d, launches_d, steps_d = t._run(strategy, "device", monkeypatch, device=gpu, modules=mods)
+        ends_h, issues_h, launches_h, steps_h = t._run(strategy, "host", monkeypatch, device=gpu, modules=mods)
+        ends_c, issues_c, _, steps_c = t._run(strategy, "device", monkeypatch, modules=mods)   # oracle device
     finally:
         gpu.close()
     assert steps_d == steps_h == steps_c

@@ -15,7 +15,11 @@ from mythril_amd.laser import taint as tnt
 from mythril_amd.laser.opcodes import OPCODES
 from mythril_amd.laser.transaction import _setup_global_state_for_execution
 from oracle_device import OracleDevice
+import refmodules
 from refmodules import IntegerArithmetics, OverUnderflowStateAnnotation, TxOrigin, hooks_of
+
+DEFAULT_SET = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJump", "UserAssertions",
+               "Exceptions", "StateChangeAfterCall")
 
 
 def _txs(n_c2=24, n_under=8, n_origin=8):
@@ -53,7 +57,7 @@ def _txs(n_c2=24, n_under=8, n_origin=8):
     return out
 
 
-def _run(strategy, mode, monkeypatch, device=None):
+def _run(strategy, mode, monkeypatch, device=None, modules=("IntegerArithmetics", "TxOrigin")):
     """mode: "device" (batch-safe hooks as device actions), "host" (every module
     hook on the host), "every" (every opcode a host event)."""
     monkeypatch.undo()
@@ -61,7 +65,7 @@ def _run(strategy, mode, monkeypatch, device=None):
         monkeypatch.setattr(tnt, "BATCH_SAFE", {})
     vm = LaserEVM(device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
     vm.track_objects = True
-    mods = [IntegerArithmetics(), TxOrigin()]
+    mods = [getattr(refmodules, m)() for m in modules]
     vm.register_hooks("pre", hooks_of(mods, "pre"))
     vm.register_hooks("post", hooks_of(mods, "post"))
     if mode == "every":
@@ -74,7 +78,11 @@ def _run(strategy, mode, monkeypatch, device=None):
                       a.constraint.value) for s in sa for a in s.overflowing_state_annotations)
         stack = [sorted((type(a).__name__, getattr(a, "operator", "")) for a in x.annotations)
                  for x in state.mstate.stack]
-        ends.append((tag[id(tx)], state.mstate.pc, revert, bool(sa), tuple(got), str(stack)))
+        pots = [tuple(p.potential_issues) for p in state.annotations
+                if isinstance(p, refmodules.PotentialIssuesAnnotation)]
+        jumps = [a.last_jump for a in state.annotations if isinstance(a, refmodules.LastJumpAnnotation)]
+        ends.append((tag[id(tx)], state.mstate.pc, revert, bool(sa), tuple(got), str(stack), str(pots),
+                     tuple(jumps)))
     vm.register_laser_hooks("transaction_end", end)
     for k, tx in enumerate(_txs()):
         _setup_global_state_for_execution(vm, tx)
@@ -104,6 +112,20 @@ def test_device_taint_matches_every_opcode_on_the_host(monkeypatch):
     assert steps_d == steps_e
     assert ends_d == ends_e
     assert issues_d == issues_e
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_default_module_set_on_the_device_matches_host_hooks(strategy, monkeypatch):
+    """The wider set (deferred potential issues of ArbitraryStorage, the
+    LastJumpAnnotation of Exceptions, UserAssertions' MSTORE check, ArbitraryJump
+    and StateChangeAfterCall's early returns) besides integer and TxOrigin."""
+    ends_d, issues_d, launches_d, steps_d = _run(strategy, "device", monkeypatch, modules=DEFAULT_SET)
+    ends_h, issues_h, launches_h, steps_h = _run(strategy, "host", monkeypatch, modules=DEFAULT_SET)
+    assert steps_d == steps_h
+    assert ends_d == ends_h
+    assert issues_d == issues_h
+    assert any(e[6] != "[]" for e in ends_d) and any(e[7] for e in ends_d)     # not vacuous
+    assert launches_d < launches_h
 
 
 def test_plan_actions_for_the_reference_modules():
