@@ -1,0 +1,12 @@
+#!/bin/bash
+# Taint lanes: their GPU parity tests first, then the full GPU suite, smoke, bench.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/r02t
+mkdir -p $OUT
+echo "== taint" && timeout -k 10 600 python -u -m pytest tests/test_gpu_taint.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_taint.log 2>&1 && \
+echo "== gpu suite" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+echo "== smoke" && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
+echo "== bench" && timeout -k 10 900 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err && \
+echo "== done"
