@@ -423,14 +423,23 @@ def _bits(m: int):
         k += 1
 
 
+def _world_view(ws, n_constraints: int):
+    """The world state a replayed hook sees: the lane's (accounts, transaction
+    sequence and annotations shared -- the batch-safe hooks only read them) with
+    the path constraints it had at the hooked step."""
+    view = object.__new__(type(ws))
+    view.__dict__.update(ws.__dict__)
+    view.constraints = list(ws.constraints[:n_constraints])
+    return view
+
+
 def _snapshot(state, pc: int, stack, n_constraints: int):
     """The state a replayed hook sees: the lane's environment and transaction,
     the world state with the path constraints the lane had at that step, pc and
     the recorded stack words.  Memory and storage are not reproduced (the
     batch-safe hooks do not read them)."""
     from .state import GlobalState, MachineState
-    ws = copy(state.world_state)
-    ws.constraints = list(ws.constraints[:n_constraints])
+    ws = _world_view(state.world_state, n_constraints)
     ms = MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack, depth=state.mstate.depth)
     g = GlobalState(ws, state.environment, state.node, ms, transaction_stack=list(state.transaction_stack),
                     last_return_data=state.last_return_data)
@@ -468,8 +477,7 @@ def replay_deferred(rec, state, plan: TaintPlan) -> None:
     reference's hooks put it."""
     from .state import GlobalState, MachineState
     _step, _kind, words, pc, op = rec
-    ws = copy(state.world_state)
-    ws._annotations = state.world_state._annotations
+    ws = _world_view(state.world_state, len(state.world_state.constraints))
     stack = [symbol_factory.BitVecVal(w, 256) for w in reversed(words)]
     snap = GlobalState(ws, state.environment, state.node,
                        MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack,
