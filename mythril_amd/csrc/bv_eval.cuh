@@ -54,7 +54,9 @@ enum BvOp : uint32_t {
 #define BV_MAX_SLOTS 8u
 #define BV_BLOCK 256u
 #define BV_TILE_INSNS 2048u   // longest program (LDS tile upper bound: 32 KiB)
+#ifndef BV_TILE_MIN
 #define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
+#endif
 #define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
 
@@ -175,8 +177,19 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     return r;
 }
 
+// MG_BV_WAVES (A/B builds only): minimum waves per SIMD the register allocation
+// must allow; 0 leaves the compiler's choice
+#ifndef MG_BV_WAVES
+#define MG_BV_WAVES 0
+#endif
+#if MG_BV_WAVES
+#define BV_BOUNDS __launch_bounds__(BV_BLOCK, MG_BV_WAVES)
+#else
+#define BV_BOUNDS __launch_bounds__(BV_BLOCK)
+#endif
+
 template <bool kLdsProg>
-__global__ __launch_bounds__(BV_BLOCK) void k_bv_eval(const uint4 *__restrict__ insns,
+__global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
                                                       const uint4 *__restrict__ consts,
