@@ -55,7 +55,7 @@ enum BvOp : uint32_t {
 #define BV_BLOCK 256u
 #define BV_TILE_INSNS 2048u   // longest program (LDS tile upper bound: 32 KiB)
 #ifndef BV_TILE_MIN
-#define BV_TILE_MIN 512u      // smallest LDS tile (8 KiB)
+#define BV_TILE_MIN 256u      // smallest program tile (4 KiB in LDS)
 #endif
 #define BV_TILE_DAGS 64u      // most DAGs per tile (per-block result accumulators)
 #define BV_GROUP_TARGET 4096u // blocks wanted per launch (16 per CU)
@@ -79,7 +79,7 @@ struct BvState {
     bool want_bits = false;
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
     size_t cap_entries = 0;
-    bool lds_prog = true;            // MG_BV_PROG=scalar selects the scalar-load program variant
+    bool lds_prog = false;           // MG_BV_PROG=lds stages the program tile in LDS
     std::vector<uint32_t> h_tiles;
 };
 
@@ -177,10 +177,12 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     return r;
 }
 
-// MG_BV_WAVES (A/B builds only): minimum waves per SIMD the register allocation
-// must allow; 0 leaves the compiler's choice
+// MG_BV_WAVES: minimum waves per SIMD the register allocation must allow (0
+// leaves the compiler's choice).  8 caps the kernel at 64 VGPRs (a few spill to
+// scratch); with the scalar-load instruction fetch the block's LDS is its 16 KiB of
+// slots, so 8 blocks fit a CU: C4 249 -> 220 ms (profiles/r02/ab_k2_occupancy.log)
 #ifndef MG_BV_WAVES
-#define MG_BV_WAVES 0
+#define MG_BV_WAVES 8
 #endif
 #if MG_BV_WAVES
 #define BV_BOUNDS __launch_bounds__(BV_BLOCK, MG_BV_WAVES)
@@ -477,7 +479,9 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
     s.n_tables = models->n_tables; s.n_entries = models->n_entries;
     const char *pv = getenv("MG_BV_PROG");
-    s.lds_prog = !(pv && std::string(pv) == "scalar");   // A/B: lds 501 ms, scalar 508 ms (C4)
+    // scalar-load fetch by default: at 8 waves per SIMD the LDS tile would cost
+    // occupancy (C4: scalar 220 ms, LDS 232 ms); MG_BV_PROG=lds selects the other
+    s.lds_prog = pv && std::string(pv) == "lds";
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;

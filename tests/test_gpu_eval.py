@@ -92,3 +92,23 @@ def test_arrays_functions_device_equals_oracle(dev):
 def ULT_x():
     from mythril_amd.smt.expr import ULT, symbol_factory
     return ULT(symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecVal(3, 256))
+
+
+@pytest.mark.parametrize("fetch", ["lds", "scalar"])
+def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
+    """The scalar-load fetch is the default; MG_BV_PROG=lds stages the program tile
+    in LDS.  Both read at upload, both equal the oracle (plain ops and tables)."""
+    from test_smt_programs import _random_table_constraints, _random_table_models
+    monkeypatch.setenv("MG_BV_PROG", fetch)
+    prog = synth.c4_programs(synth.Draws(900, seed=synth.C4_SEED + 9))
+    models = synth.c4_models(333, seed=19)
+    fs, sc, _ = dev.eval(prog, models)
+    rfs, rsc = eval_batch(prog, models)
+    assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
+    rng = random.Random(31)
+    prog, _ = compile_sets([_random_table_constraints(rng) for _ in range(200)])
+    pool = ModelPool.from_dicts(_random_table_models(random.Random(3), 300, prog), prog.var_names,
+                                prog.var_widths, prog.tables)
+    fs, sc, _ = dev.eval(prog, pool)
+    rfs, rsc = eval_batch(prog, pool)
+    assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
