@@ -261,6 +261,28 @@ class LaneBatch:
             getattr(out, f)[...] = getattr(self, f)
         return out
 
+    def regrown(self, shape: "LaneShape") -> "LaneBatch":
+        """The same lanes in a batch of larger capacities (same n, calldata_cap,
+        and symbolic / taint planes): every per-lane table is copied as a prefix
+        (stack, memory, storage, trace, records, arena and object tables are
+        filled from index 0 up), so the lanes continue where they stopped."""
+        if shape.n != self.shape.n or shape.calldata_cap != self.shape.calldata_cap or \
+                bool(shape.node_cap) != self.symbolic or bool(shape.obj_cap) != self.taint:
+            raise ValueError("regrown: only capacities may change")
+        out = LaneBatch(shape)
+        for f in _U32_FIELDS + _U64_FIELDS + ("calldata", "env", "stack", "memory", "storage", "trace",
+                                              "rec") + (_SYM_FIELDS if self.symbolic else ()) + (
+                                                  _TAINT_FIELDS if self.taint else ()):
+            src, dst = getattr(self, f), getattr(out, f)
+            if src.ndim == 1:
+                dst[...] = src
+            else:
+                k = min(src.shape[1], dst.shape[1])
+                if k < src.shape[1]:
+                    raise ValueError(f"regrown: {f} would shrink")
+                dst[:, :k] = src[:, :k]
+        return out
+
     # ---- per-lane construction ----------------------------------------
     def set_lane(self, i: int, *, code_id: int = 0, calldata: bytes = b"",
                  address: int = 0, caller: int = 0, origin: int = 0, callvalue: int = 0,

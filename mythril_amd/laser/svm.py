@@ -33,6 +33,7 @@ order.  Hook-free paths run in one launch.
 from __future__ import annotations
 
 import bisect
+import dataclasses
 import heapq
 import itertools
 import logging
@@ -52,6 +53,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
+                     MG_STACK_LIMIT,
                      limbs_to_word, rows_to_words, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import Expression, symbol_factory
@@ -166,6 +168,7 @@ class LaserEVM:
         self.launches = 0
         self._exec_stop = False
         self.forks = 0                      # symbolic JUMPIs the device stopped at (MG_FORK)
+        self.regrows = 0                    # capacity escapes resumed in a regrown batch
         self._code_ids: Dict[bytes, int] = {}
         self._code_objs: Dict[bytes, object] = {}
         # coverage the reference's execute_state hook records for states the
@@ -639,11 +642,68 @@ class LaserEVM:
             self._deliver(lanes[ev], b, final_states, track_gas, launch, regrow, single_step)
             if self._exec_stop:
                 return None           # exec ends here: later events never happen
+            if regrow:
+                grown = self._regrow_in_place(b, regrow, lanes)
+                if grown is not None:
+                    b = sched.b = grown
+                    regrow.clear()
         self._replay_records(lanes)
         if regrow:
             self._cap_grow *= 4
-            self.work_list.extend(regrow)
+            self.work_list.extend(ln.state for ln, _ in regrow)
         return None
+
+    def _regrow_in_place(self, b: LaneBatch, regrow, lanes) -> Optional[LaneBatch]:
+        """A lane stopped by a full per-lane table (capacity escape): grow that
+        capacity 4x for the whole batch, copy every lane into the new image
+        (LaneBatch.regrown), re-allocate and re-upload, and resume the lane at the
+        instruction it stopped before -- inside this batch, so its later events
+        keep their place in the strategy's order and a hook it already passed is
+        not run again.  None when the capacity is already at its limit (or the
+        taint escape was the 64-atom limit): the caller re-queues the state for a
+        later batch, where packing compacts it."""
+        sh = b.shape
+        grow = {}
+        for ln, reason in regrow:
+            need = _capacity_growth(sh, reason, b, ln.pos)
+            if need is None:
+                return None
+            grow.update(need)
+        if any(v <= getattr(sh, k) for k, v in grow.items()):
+            return None
+        # lanes of the same launch that escaped for a capacity this growth covers
+        # resume too (their escape events are artifacts of the old shape)
+        resume = [(ln.pos, reason) for ln, reason in regrow]
+        for ln in lanes:
+            i = ln.pos
+            if ln.phase == "event" and int(b.status[i]) == MG_ESCAPE:
+                need = _capacity_growth(sh, int(b.aux[i]) >> 8, b, i)
+                if need and all(k in grow for k in need):
+                    resume.append((i, int(b.aux[i]) >> 8))
+        b2 = b.regrown(dataclasses.replace(sh, **grow))
+        b2.rec_seen = b.rec_seen.copy()
+        for i, reason in resume:
+            b2.status[i] = MG_RUNNING
+            b2.aux[i] = 0
+            if reason != MG_ESC_TRACE and sh.trace_cap and int(b2.trace_len[i]):
+                b2.trace_len[i] -= 1          # traced at its pop, traced again when it runs
+        dev = self.device
+        dev.alloc(b2.shape, coverage=self.record_coverage)
+        if self._plan is not None:
+            dev.set_taint_program(self._plan.actions)
+            self._upload_force(dev)
+        dev.upload(b2)
+        dev.set_loop_bound(self._loop_bound())
+        self.regrows += 1
+        sched = self._sched
+        for pos in sched.dirty:
+            lanes[pos].dirty = False
+        sched.dirty.clear()
+        sched.b = b2
+        for i, _ in resume:
+            sched.set(i, "paused")
+        return b2
+
 
     def _deliver(self, ln: _Lane, b: LaneBatch, final_states, track_gas, launch, regrow,
                  single_step: bool = False):
@@ -823,7 +883,7 @@ class LaserEVM:
                     ann = _annotation_of(s)
                     if ann.trace:
                         ann.trace.pop()
-                regrow.append(s)
+                regrow.append((ln, reason))
                 return
             if self.escape_handler is None:
                 log.debug("Encountered unimplemented instruction %s", name)
@@ -996,6 +1056,27 @@ def _event_round(b: LaneBatch, i: int) -> int:
     st = int(b.status[i])
     s = int(b.steps[i])
     return s - 1 if st in _EXECUTED_HALTS else s
+
+def _capacity_growth(sh: LaneShape, reason: int, b: LaneBatch, i: int) -> Optional[Dict[str, int]]:
+    """The capacities (4x) a lane's capacity escape asks for; None when growing
+    cannot help (the 64-atom limit of a taint lane) or it is no capacity escape."""
+    n = sh.n
+    if reason == MG_ESC_MEMORY:
+        cap = min(sh.mem_cap * 4, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
+        return {"mem_cap": (cap + 31) // 32 * 32}
+    if reason == MG_ESC_STORAGE:
+        return {"storage_cap": sh.storage_cap * 4}
+    if reason == MG_ESC_STACK:
+        return {"stack_cap": min(MG_STACK_LIMIT, sh.stack_cap * 4)}
+    if reason == MG_ESC_TRACE:
+        return {"trace_cap": sh.trace_cap * 4}
+    if reason == MG_ESC_RECORD:
+        return {"rec_cap": sh.rec_cap * 4}
+    if reason == MG_ESC_ARENA:
+        return {"node_cap": sh.node_cap * 4, "const_cap": sh.const_cap * 4}
+    if reason == MG_ESC_TAINT and sh.obj_cap and int(b.n_obj[i]) + 4 > sh.obj_cap:
+        return {"obj_cap": min(sh.obj_cap * 4, 65536)}
+    return None
 
 
 class _Schedule:

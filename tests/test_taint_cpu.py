@@ -162,3 +162,34 @@ def test_plan_actions_for_the_reference_modules():
     # a foreign hook on an opcode keeps it a host event
     vm.register_hooks("pre", {"ADD": [lambda s: None]})
     assert OPCODES["ADD"] not in tnt.TaintPlan(vm).safe
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_taint_capacity_escapes_resume_in_place(strategy, monkeypatch):
+    """Record logs and object tables that fill (MG_ESC_RECORD, MG_ESC_TAINT)
+    regrow the batch in place: with both started small the device-action run
+    still equals the host-hook run on the default module set."""
+    from mythril_amd.laser import svm as svm_mod
+    import dataclasses
+    orig_shape, orig_regrow = svm_mod.LaserEVM._shape, svm_mod.LaserEVM._regrow_in_place
+    seen = []
+
+    def small(self, states, taint=False):
+        sh = orig_shape(self, states, taint)
+        # small in the first batch only (a state re-queued at a limit gets the usual shapes)
+        return dataclasses.replace(sh, rec_cap=64, obj_cap=16) if taint and self._cap_grow == 1 else sh
+
+    def counting(self, b, regrow, lanes):
+        out = orig_regrow(self, b, regrow, lanes)
+        seen.append(out is not None)
+        return out
+    ends_h, issues_h, _, steps_h = _run(strategy, "host", monkeypatch, modules=DEFAULT_SET)
+    svm_mod.LaserEVM._shape, svm_mod.LaserEVM._regrow_in_place = small, counting
+    try:
+        ends_d, issues_d, _, steps_d = _run(strategy, "device", monkeypatch, modules=DEFAULT_SET)
+    finally:
+        svm_mod.LaserEVM._shape, svm_mod.LaserEVM._regrow_in_place = orig_shape, orig_regrow
+    assert seen and all(seen)
+    assert steps_d == steps_h
+    assert ends_d == ends_h
+    assert issues_d == issues_h
