@@ -51,6 +51,9 @@ def parse(argv=None):
     ap.add_argument("--hooked-lanes", type=int, default=4096,
                     help="lanes of the hooked-C2 field (0: off): C2 through LaserEVM with the "
                          "default detection modules' opcode hooks registered")
+    ap.add_argument("--overlap-steps", type=int, default=40,
+                    help="batches per stream of the C2 lanes on two library contexts at once, "
+                         "reported as c2_two_streams (0: off)")
     ap.add_argument("--unbucketed-steps", type=int, default=10,
                     help="batches of the C2 lanes in generation order, reported as c2_unbucketed (0: off)")
     ap.add_argument("--large-steps", type=int, default=10,
@@ -189,6 +192,11 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
     elapsed, total_steps = mdist.reduce_timing(elapsed, float(lane_steps))
     total_steps = int(total_steps)
 
+    overlap = None
+    if args.overlap_steps and gpu and not args.profile_only:
+        _log(rank, "C2 on two streams")
+        overlap = run_two_streams(dev, batch, code, args.overlap_steps, local, barrier)
+
     large = None
     if args.large_steps and not args.profile_only:
         _log(rank, "C2 on the 3,523-instruction fixture")
@@ -250,6 +258,8 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         }
         if unbucketed is not None:
             out["c2_unbucketed"] = unbucketed
+        if overlap is not None:
+            out["c2_two_streams"] = overlap
         if large is not None:
             out["c2_large_contract"] = large
         if not args.no_cpu_baseline:
@@ -397,6 +407,54 @@ def run_taint_c2(dev, n_lanes, rank):
 def workloads_seed(rank):
     from mythril_amd import workloads
     return workloads.C2_SEED + 11 + rank
+
+
+def run_two_streams(dev, batch, code, steps, local, barrier):
+    """The same 65,536-lane C2 batch on a second library context (its own HIP
+    stream and lane buffers) while the first runs it too: K batches per stream,
+    issued from two host threads (ctypes drops the GIL inside mg_run_batches).
+    A block owns its CU's LDS, so the second stream's blocks start on the CUs
+    the first batch's short waves free while its slowest waves (the sendeth
+    path) still run: the tail of one batch is filled by the next.  Reported
+    beside `value`, never as it (`value` keeps one batch in flight)."""
+    import threading
+    from mythril_amd import workloads
+    from mythril_amd.device import GpuDevice
+    dev2 = GpuDevice(local)
+    try:
+        cid2 = dev2.load_code(code)
+        b2 = workloads.slim_copy(batch)
+        if cid2 != int(batch.code_id[0]):
+            b2.code_id[:] = cid2
+        dev2.alloc(batch.shape, coverage=True)
+        dev2.upload(b2)
+        # warm up at the timed batch count: a larger statistics buffer is re-allocated
+        # on first use, and hipFree waits for the whole device (both streams)
+        dev.run_batches(steps)
+        dev2.run_batches(steps)
+        res = [None, None]
+
+        def go(k, d):
+            res[k] = d.run_batches(steps)
+        barrier()
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=go, args=(k, d)) for k, d in enumerate((dev, dev2))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        barrier()
+        el = time.perf_counter() - t0
+        lane_steps = sum(st.lane_steps for r in res for st in r)
+        if any(st.running for r in res for st in r):
+            raise RuntimeError("a two-stream C2 batch ended with lanes still running")
+        per = [sum(st.lane_steps for st in r) for r in res]
+        return {"value": lane_steps / el, "unit": "lane-steps/s", "streams": 2, "batches_per_stream": steps,
+                "lanes_per_batch": batch.n, "ms_per_batch": 1000.0 * el / (2 * steps),
+                "lane_steps_per_stream": per,
+                "kernel_ms_per_batch": float(np.mean([st.kernel_ms for r in res for st in r]))}
+    finally:
+        dev2.close()
 
 
 def run_large(dev, args, rank, barrier):
