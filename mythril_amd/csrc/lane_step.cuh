@@ -57,6 +57,9 @@ struct OpInfo {
 #define LANE_STEP1 8u
 
 #define MSTATE_GAS_LIMIT 1000000000ull
+#ifndef MG_K1_PF
+#define MG_K1_PF 0
+#endif
 #define RUN_MAX 64u   // longest straight-line run executed as one block
 static_assert(RUN_MAX <= 64u, "a run is read as one pre-decoded word per wave lane");
 #define STACK_LIMIT 1024u
@@ -1062,7 +1065,16 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     // Decode the instruction at pc and run the checks svm.execute_state makes
     // before evaluating it (svm.py:369-402): depth cut-off, past-the-end pc,
     // hooked opcode, this launch's step budget, host-only opcode.
-#define FETCH() do {                                                                      \
+#define FETCH() do { FETCH_LOAD(); FETCH_CHECK(); } while (0)
+    // MG_K1_PF (A/B builds): the single-instruction path loads the entry of pc + 1
+    // before its handler runs and FETCH_PF uses it when the lane fell through
+#define FETCH_PF(q_pf, pc_pf) do {                                                        \
+        if (sflag && pc == (pc_pf) && pc < sn) {                                          \
+            pd = make_uint2((q_pf).x, (q_pf).y); prun = make_uint2((q_pf).z, (q_pf).w);   \
+        } else FETCH_LOAD();                                                              \
+        FETCH_CHECK();                                                                    \
+    } while (0)
+#define FETCH_LOAD() do {                                                                 \
         if (sflag && pc < sn) {                                                           \
             const uint4 q_ = s_pd[pc];        /* s_pd[n_instr] is the END sentinel */     \
             pd = make_uint2(q_.x, q_.y); prun = make_uint2(q_.z, q_.w);                   \
@@ -1077,6 +1089,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             pd = make_uint2(d_.x, o_ | (d_.y << 8) |                                      \
                             pd_flags(o_, d_.y, (uint32_t)((hm_ >> (o_ & 63u)) & 1ull)));  \
         }                                                                                 \
+    } while (0)
+#define FETCH_CHECK() do {                                                                \
         const uint32_t k_ = (pd.y >> 17) & 31u, o_ = pd.y & 0xffu;                       \
         const bool hk_ = (pd.y >> 31) && !(hook_ack && executed == 0u);                  \
         bool lstop_ = false;                                                              \
@@ -1291,6 +1305,10 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         if (!(live && pd.y == uy)) continue;
 
         const uint32_t op = uk & 0xffu, kind = (uk >> 17) & 31u;
+#if MG_K1_PF
+        const uint32_t pc_pf = pc + 1u;
+        const uint4 q_pf = s_pd[min(pc_pf, sn - 1u)];
+#endif
         CLK_MARK(op);
         if (cov_on) {
             if (sflag && pc < ns) s_cov[pc] = 1;
@@ -1461,8 +1479,15 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             }
         }
         CLK_MARK(261u);
+#if MG_K1_PF
+        if (live) FETCH_PF(q_pf, pc_pf);
+#else
         if (live) FETCH();
+#endif
     }
+#undef FETCH_PF
+#undef FETCH_LOAD
+#undef FETCH_CHECK
 #undef FETCH
 #undef PUSH_IMM
     CLK_MARK(258u);
