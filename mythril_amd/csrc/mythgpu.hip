@@ -62,6 +62,7 @@ struct mg_ctx {
     // mg_run_batches: per-batch statistics slots and per-launch events
     DevCounters *d_ctr_multi = nullptr;
     size_t ctr_multi_cap = 0;            // slots
+    std::vector<void *> retired;          // outgrown buffers, freed by mg_close
     std::vector<hipEvent_t> ev_batch;
     // kernel 2
     BvState bv{};
@@ -235,6 +236,7 @@ extern "C" void mg_close(mg_ctx *ctx) {
     if (ctx->ev1) hipEventDestroy(ctx->ev1);
     for (hipEvent_t e : ctx->ev_batch) hipEventDestroy(e);
     hipFree(ctx->d_ctr_multi);
+    for (void *p : ctx->retired) hipFree(p);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1154,13 +1156,17 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
     const uint32_t nb = blocks_for(ctx->L.n, lane_block(ctx));
     const size_t slots = (size_t)nb * n_batches;
     if (slots > ctx->ctr_multi_cap) {
+        // grow geometrically and retire the old buffer instead of freeing it: hipFree
+        // waits for the whole device, which would serialise another context's
+        // stream running on the same GPU (two contexts per GPU)
         HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        hipFree(ctx->d_ctr_multi);
-        ctx->d_ctr_multi = nullptr;
-        ctx->ctr_multi_cap = 0;
-        if (hipMalloc(&ctx->d_ctr_multi, slots * sizeof(DevCounters)) != hipSuccess)
-            return set_err(ctx, MG_ENOMEM, "hipMalloc %zu statistics slots", slots);
-        ctx->ctr_multi_cap = slots;
+        const size_t cap = std::max(slots, std::max(2 * ctx->ctr_multi_cap, (size_t)nb * 64u));
+        DevCounters *p = nullptr;
+        if (hipMalloc(&p, cap * sizeof(DevCounters)) != hipSuccess)
+            return set_err(ctx, MG_ENOMEM, "hipMalloc %zu statistics slots", cap);
+        if (ctx->d_ctr_multi) ctx->retired.push_back(ctx->d_ctr_multi);
+        ctx->d_ctr_multi = p;
+        ctx->ctr_multi_cap = cap;
     }
     while (ctx->ev_batch.size() < 2u * n_batches) {
         hipEvent_t e = nullptr;
