@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Two library contexts on one GPU after a one-batch warm-up only: the C2 batch
-K times per context from two threads, against K times on one context.  Before
-the statistics buffers were retired instead of freed, the first larger call's
-hipFree waited for the whole device and serialised the two streams."""
+K times per context from two threads, against K times on one context.  The
+first call with more batches than before allocates statistics slots and events;
+measured on the MI355X (r02z) those first-use allocations serialise the two
+streams (two contexts slower than one), which is why bench.run_two_streams
+warms each context up at the timed batch count."""
 import json
 import sys
 import threading
