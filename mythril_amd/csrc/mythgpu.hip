@@ -1168,7 +1168,9 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
         ctx->d_ctr_multi = p;
         ctx->ctr_multi_cap = cap;
     }
-    while (ctx->ev_batch.size() < 2u * n_batches) {
+    // events in a block of at least 128 (64 batches): like the statistics slots,
+    // created before they are needed rather than on a larger call's first use
+    while (ctx->ev_batch.size() < std::max<size_t>(2u * n_batches, 128u)) {
         hipEvent_t e = nullptr;
         HIPX(ctx, hipEventCreate(&e));
         ctx->ev_batch.push_back(e);
