@@ -26,11 +26,13 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 6u   /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 7u   /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
-                               6: taint lanes: object handles + annotation masks */
+                               6: taint lanes: object handles + annotation masks
+                               7: symbolic memory bytes, storage chains, symbolic
+                                  SHA3 (MG_SYM_SLOAD..CONCAT, MG_REC_SYMKECCAK) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -103,6 +105,11 @@ extern "C" {
 /*   MG_REC_HOOK    a deferred batch-safe hook (MG_TAINT_DEFER): len = n words; result =
  *                  stack[-1]; payload = stack[-2..-n] (8 limbs each), pc, opcode.       */
 #define MG_REC_HOOK     4u
+/*   MG_REC_SYMKECCAK  SHA3 of a symbolic input (symbolic lanes): len = input bytes,
+ *                  result limbs unused; payload = the MG_SYM_KECCAK node's index.
+ *                  The host registers the input with create_keccak in the
+ *                  reference's global order (symbolic_inputs).                 */
+#define MG_REC_SYMKECCAK 5u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */
@@ -121,6 +128,10 @@ extern "C" {
 #define MG_LANE_SYMENV_SHIFT 6 /* bit 6 + MG_ENV_k: environment word k is symbolic  */
 #define MG_LANE_TAINT  2048u  /* taint lane: stack words are objects with annotation
                                  sets (mg_taint_alloc); stepped by the symbolic stepper */
+#define MG_LANE_SYMSTORE 4096u /* symbolic lane whose storage base is the symbolic
+                                 Array("Storage{address}") (account.py:26-29), not K(0) */
+#define MG_LANE_MEMTAG 8192u  /* symbolic lane whose memory may hold symbolic bytes
+                                 (mtag); set by the host or by the device on a write */
 
 /* environment words, per lane */
 #define MG_ENV_ADDRESS   0
@@ -215,11 +226,28 @@ typedef struct mg_ctx mg_ctx;
 #define MG_SYM_ENV    3u  /* environment word w (MG_ENV_*)                       */
 #define MG_SYM_BIN    4u  /* binary EVM opcode w on (y = first pop, z = second)  */
 #define MG_SYM_UN     5u  /* unary EVM opcode w (ISZERO, NOT) on y               */
+#define MG_SYM_SLOAD  6u  /* simplify(Select(store chain after its first z entries, y))
+                             (account.py:43-75, instructions.py:1496-1506)        */
+#define MG_SYM_KECCAK 7u  /* keccak256_w(y): create_keccak of a symbolic input of w bits
+                             (keccak_function_manager.py:95-114, instructions.py:1013-1051) */
+#define MG_SYM_EXTRACT 8u /* Extract(w >> 16, w & 0xffff, y) of a node's word      */
+#define MG_SYM_CONCAT 9u  /* Concat(y, z), widths w & 0xffff and w >> 16: the parts of
+                             a memory read, simplify(Concat(bytes)) (memory.py:56-82) */
+#define MG_SYM_TERM  10u  /* an opaque term of the host's expression layer, index w in
+                             the host's term table (anything a handler or the caller
+                             built); compared by identity                          */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */
 
-/* Host image of the symbolic planes of lanes [first, first + n), lane-major. */
+/* Host image of the symbolic planes of lanes [first, first + n), lane-major.
+ * Memory bytes and storage entries carry tags too (ABI v7): a memory byte tag is
+ * 0 (the byte in `memory` is the value) or 1 + (node << 5 | j): byte j (0 = most
+ * significant) of that node's word, i.e. Extract(255 - 8j, 248 - 8j, word) as
+ * write_word_at stores it (memory.py:84-115).  In a symbolic lane the storage
+ * table is the reference's store chain, one entry per SSTORE in order (over K(0),
+ * or the symbolic Array with MG_LANE_SYMSTORE); an entry's key / value tag is 0
+ * (the limbs are the value) or 1 + node. */
 typedef struct mg_sym_soa {
     uint32_t n, stack_cap, node_cap, const_cap;
     uint32_t *stag;         /* [n][stack_cap]                                 */
@@ -227,6 +255,9 @@ typedef struct mg_sym_soa {
     uint32_t *cval;         /* [n][const_cap][8] little-endian limbs          */
     uint32_t *n_nodes;      /* [n]                                            */
     uint32_t *n_consts;     /* [n]                                            */
+    uint32_t mem_cap, storage_cap;   /* the lane image's capacities               */
+    uint32_t *mtag;         /* [n][mem_cap] memory byte tags                  */
+    uint32_t *sttag;        /* [n][storage_cap][2] storage entry (key, value) tags */
 } mg_sym_soa;
 
 /* Symbolic planes for the current batch (after mg_lanes_alloc; freed with it).

@@ -43,6 +43,8 @@ struct DevSym {
     uint4 *node;         // [node_cap][N]
     uint4 *cval;         // [const_cap][N][2]
     uint32_t *n_nodes, *n_consts;   // [N]
+    uint32_t *mtag;      // [mem_cap][N]  memory byte tags: 0, or 1 + (node << 5 | byte j)
+    uint2 *sttag;        // [storage_cap][N]  storage chain entry (key, value) tags: 0 or 1 + node
 };
 
 // Taint planes (mg_taint_alloc): object handle per stack slot, annotation mask

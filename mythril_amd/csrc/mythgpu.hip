@@ -718,6 +718,8 @@ extern "C" int mg_sym_alloc(mg_ctx *ctx, uint32_t node_cap, uint32_t const_cap) 
     if ((rc = get((void **)&S.cval, (size_t)const_cap * N * 32))) return rc;
     if ((rc = get((void **)&S.n_nodes, N * 4))) return rc;
     if ((rc = get((void **)&S.n_consts, N * 4))) return rc;
+    if ((rc = get((void **)&S.mtag, (size_t)ctx->L.mem_cap * N * 4))) return rc;
+    if ((rc = get((void **)&S.sttag, (size_t)ctx->L.storage_cap * N * 8))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     ctx->S = S;
     return MG_OK;
@@ -727,7 +729,8 @@ static int check_sym_shape(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, uin
     if (!ctx->S.node) return set_err(ctx, MG_ESTATE, "mg_sym_alloc first");
     if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
         return set_err(ctx, MG_EINVAL, "symbolic lane range [%u,%u) outside batch of %u", first, first + n, ctx->L.n);
-    if (h->stack_cap > ctx->L.stack_cap || h->node_cap > ctx->S.node_cap || h->const_cap > ctx->S.const_cap)
+    if (h->stack_cap > ctx->L.stack_cap || h->node_cap > ctx->S.node_cap || h->const_cap > ctx->S.const_cap ||
+        h->mem_cap > ctx->L.mem_cap || h->storage_cap > ctx->L.storage_cap)
         return set_err(ctx, MG_EINVAL, "symbolic host image capacities exceed the allocation");
     return MG_OK;
 }
@@ -746,6 +749,8 @@ extern "C" int mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, u
     if ((rc = up_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
     if ((rc = up_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
     if ((rc = up_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
+    if ((rc = up_units(ctx, h->mtag, n, h->mem_cap, 1, ctx->S.mtag, first))) return rc;
+    if ((rc = up_units(ctx, h->sttag, n, h->storage_cap, 2, ctx->S.sttag, first))) return rc;
     return MG_OK;
 }
 
@@ -760,6 +765,8 @@ extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint3
     if ((rc = down_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
     if ((rc = down_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
     if ((rc = down_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
+    if ((rc = down_units(ctx, h->mtag, n, h->mem_cap, 1, ctx->S.mtag, first))) return rc;
+    if ((rc = down_units(ctx, h->sttag, n, h->storage_cap, 2, ctx->S.sttag, first))) return rc;
     return MG_OK;
 }
 

@@ -71,6 +71,135 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
     return true;
 }
 
+// ---- symbolic memory, storage and SHA3 (ABI v7) ----------------------------------
+#define LANE_SYMSTORE 4096u
+#define LANE_MEMTAG 8192u
+#define SYM_SLOAD 6u
+#define SYM_KECCAK 7u
+#define SYM_EXTRACT 8u
+#define SYM_CONCAT 9u
+#define SYM_TERM 10u
+#define SYM_NONE 0xffffffffu
+
+DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
+DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
+    S.mtag[(size_t)off * N + lane] = t;
+}
+// any symbolic byte in memory [off, off + len) (bytes past msize are zero)
+DEV bool mtag_any(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t len, uint32_t msize) {
+    const uint32_t end = min(off + len, msize);
+    for (uint32_t p = off; p < end; ++p)
+        if (mtag_at(S, N, lane, p)) return true;
+    return false;
+}
+
+// Whether operand refs x and y denote the same term.  z3 terms are hash-consed,
+// so the Select-over-Store rewrites of simplify (storage reads, account.py:75)
+// compare indices by identity; here: equal refs, equal constants, or nodes with
+// equal headers whose operands are the same terms, walked with an explicit
+// stack.  A comparison deeper than the stack answers false, so the device keeps
+// a Select node the host's decode then folds (decoding decides the term).
+__device__ __noinline__ bool sym_same(const DevSym &S, size_t N, uint32_t lane, uint32_t x, uint32_t y) {
+    uint32_t st[32];
+    int top = 0;
+    st[top++] = x;
+    st[top++] = y;
+    while (top) {
+        const uint32_t b = st[--top], a = st[--top];
+        if (a == b) continue;
+        const bool ca = (a & SYM_CONST) != 0u, cb = (b & SYM_CONST) != 0u;
+        if (ca || cb) {
+            if (!(ca && cb)) return false;
+            if (!u_eq(ld_word(gv(S.cval), (size_t)(a & ~SYM_CONST) * N + lane),
+                      ld_word(gv(S.cval), (size_t)(b & ~SYM_CONST) * N + lane)))
+                return false;
+            continue;
+        }
+        const uint4 na = S.node[(size_t)a * N + lane], nb = S.node[(size_t)b * N + lane];
+        if (na.x != nb.x || na.w != nb.w) return false;
+        const uint32_t kind = na.x & 0xffu;
+        const bool yref = kind != SYM_CDSIZE && kind != SYM_ENV && kind != SYM_TERM;
+        const bool zref = kind == SYM_BIN || kind == SYM_CONCAT;
+        if (!yref && na.y != nb.y) return false;
+        if (!zref && na.z != nb.z) return false;      // SLOAD: the chain length
+        if (top + 4 > 32) return false;
+        if (yref) { st[top++] = na.y; st[top++] = nb.y; }
+        if (zref) { st[top++] = na.z; st[top++] = nb.z; }
+    }
+    return true;
+}
+
+// Memory [off, off + len) as one operand, the parts of simplify(Concat(bytes))
+// (memory.py:56-82, instructions.py:1032-1039): constant runs (<= 32 bytes each),
+// runs of consecutive bytes of one node's word (an EXTRACT node, or the node
+// itself for its 32 bytes in order), joined left to right by CONCAT nodes.  The
+// host's decode joins the parts the same way expr.simplify_concat joins bytes.
+// False when the arena or the constant table is full.
+__device__ __noinline__ bool sym_mem_ref(const DevSym &S, const DevLanes &L, size_t N, uint32_t lane,
+                                         uint32_t off, uint32_t len, uint32_t msize, uint32_t &nn, uint32_t &nc,
+                                         uint32_t &ref) {
+    const LaneView V{L, lane, nullptr, 0u, 0u, 256u, nullptr, 0u};
+    uint32_t acc = SYM_NONE, accw = 0u, k = 0u;
+    while (k < len) {
+        const uint32_t p = off + k;
+        const uint32_t tag = p < msize ? mtag_at(S, N, lane, p) : 0u;
+        uint32_t part, pw;
+        if (tag == 0u) {
+            U256 v = u_zero();
+            uint32_t run = 0u;
+            while (k < len && run < 32u) {
+                const uint32_t q = off + k;
+                if (q < msize && mtag_at(S, N, lane, q) != 0u) break;
+                v = u_shl_n(v, 8u);
+                v.w[0] |= q < msize ? V.mbyte(q) : 0u;
+                ++run;
+                ++k;
+            }
+            if (nc >= S.const_cap) return false;
+            st_word(gv(S.cval), (size_t)nc * N + lane, v);
+            part = SYM_CONST | nc;
+            ++nc;
+            pw = 8u * run;
+        } else {
+            const uint32_t t = (tag - 1u) >> 5, j0 = (tag - 1u) & 31u;
+            const uint32_t w = S.node[(size_t)t * N + lane].x >> 8;
+            uint32_t run = 1u;
+            ++k;
+            if (w != 8u) {
+                while (k < len && j0 + run <= 31u) {
+                    const uint32_t q = off + k;
+                    if (q >= msize || mtag_at(S, N, lane, q) != tag + run) break;
+                    ++run;
+                    ++k;
+                }
+            }
+            if (w == 8u || run == 32u) {
+                part = t;
+                pw = w == 8u ? 8u : 256u;
+            } else {
+                const uint32_t hi = 255u - 8u * j0, lo = 248u - 8u * (j0 + run - 1u);
+                uint32_t et;
+                if (!sym_node_push(S, N, lane, SYM_EXTRACT | ((hi - lo + 1u) << 8), t, 0u, (hi << 16) | lo, nn, et))
+                    return false;
+                part = et - 1u;
+                pw = hi - lo + 1u;
+            }
+        }
+        if (acc == SYM_NONE) {
+            acc = part;
+            accw = pw;
+        } else {
+            uint32_t ct;
+            if (!sym_node_push(S, N, lane, SYM_CONCAT | ((accw + pw) << 8), acc, part, accw | (pw << 16), nn, ct))
+                return false;
+            acc = ct - 1u;
+            accw += pw;
+        }
+    }
+    ref = acc;
+    return true;
+}
+
 // binary ALU opcodes with symbolic semantics; compares push Bools (width 1)
 DEV bool sym_bin_ok(uint32_t op) {
     return (op >= 0x01u && op <= 0x07u) || (op >= 0x10u && op <= 0x14u) || (op >= 0x16u && op <= 0x18u) ||
@@ -247,6 +376,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
     if (lane >= L.n || L.status[lane] != ST_RUNNING) return;
     const uint32_t flags = L.flags[lane];
     if (!(flags & (LANE_SYMBOLIC | LANE_TAINT))) return;
+    uint32_t lflags = flags;                 // + LANE_MEMTAG once a symbolic byte is written
     const size_t N = L.N;
     // symbolic semantics need the arena planes; taint needs the taint planes
     const bool symlane = (flags & LANE_SYMBOLIC) && S.stag != nullptr;
@@ -393,6 +523,180 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (nobj + 4u > T.obj_cap) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
         }
 
+        // ---- symbolic lanes: storage chain, memory byte tags, symbolic SHA3 ----
+        // (instructions.py:1013-1051, 1437-1518; account.py:43-87; memory.py:56-115).
+        // Storage of a symbolic lane is the reference's store chain (one entry per
+        // SSTORE), so every SLOAD / SSTORE runs here; memory operations run here
+        // when a byte they read is symbolic or the word they write is, or to clear
+        // the tags of bytes a concrete write replaces.
+        bool memlane = false;
+        const bool memop = kind == K_SLOAD || kind == K_SSTORE || kind == K_MLOAD || kind == K_MSTORE ||
+                           kind == K_MSTORE8 || kind == K_SHA3;      // each pops >= 1 word
+        if (symlane && memop && sp >= max(max(req, npop), 1u)) {
+            const uint32_t ta0 = sym_tag(S, N, lane, sp - 1u);
+            const uint32_t tb0 = npop >= 2u ? sym_tag(S, N, lane, sp - 2u) : 0u;
+            if (kind == K_SLOAD || kind == K_SSTORE) memlane = true;
+            else if (kind == K_MLOAD || kind == K_MSTORE || kind == K_MSTORE8)
+                memlane = ta0 != 0u || tb0 != 0u || (lflags & LANE_MEMTAG);
+            else if (kind == K_SHA3) {
+                const U256 a0 = V.stack(sp - 1u), b0 = V.stack(sp - 2u);
+                memlane = ta0 != 0u || tb0 != 0u ||
+                          ((lflags & LANE_MEMTAG) && u_fits32(a0) && u_fits32(b0) && b0.w[0] != 0u &&
+                           mtag_any(S, N, lane, a0.w[0], b0.w[0], msize));
+            }
+        }
+        if (memlane) {
+            const uint32_t ta = sym_tag(S, N, lane, sp - 1u);
+            const uint32_t tb = npop >= 2u ? sym_tag(S, N, lane, sp - 2u) : 0u;
+            const U256 a = V.stack(sp - 1u);
+            const U256 b = npop >= 2u ? V.stack(sp - 2u) : u_zero();
+            const uint32_t nsp = sp - npop;
+            uint32_t lnn = nn, lnc = nc, rtag = 0u, nmsize = msize, rec_new = 0u, stop = ST_RUNNING, sx = 0u;
+            uint64_t ngmin = gmin, ngmax = gmax;
+            U256 rval = u_zero();
+            bool wrote_tag = false;
+            const uint64_t gtmin = d.x & 0xffffu, gtmax = d.x >> 16;
+            // a taint lane's annotating hooks on these opcodes run on the host, and
+            // symbolic memory words carry annotation sets the lane does not track
+            const bool tbusy = tl && (pre_bit != 0ull || post_bit != 0ull);
+            const bool memsym = kind != K_SLOAD && kind != K_SSTORE;
+            do {
+                if (tbusy) { stop = ST_HOOK; sx = op; break; }
+#define MSTOPX(s_, x_) { stop = (s_); sx = (x_); break; }
+#define MGAS() { ngmin += gtmin; ngmax += gtmax; if (ngmin >= glim) MSTOPX(ST_VMEXC, EXC_OOG) }
+#define MPUSHCHK() { if (nsp + 1u > STACK_LIMIT) MSTOPX(ST_VMEXC, EXC_OVERFLOW) \
+                     if (nsp + 1u > L.stack_cap) MSTOPX(ST_ESCAPE, op | (ESC_STACK << 8)) }
+#define MMEMX(st_, sz_, later_) { const int mx_ = mem_extend((st_), (sz_), nmsize, ngmin, ngmax, L.mem_cap, \
+                                                             (later_), txlim); \
+                                  if (mx_ == MX_OOG) MSTOPX(ST_VMEXC, EXC_OOG) \
+                                  if (mx_ == MX_ESCAPE) MSTOPX(ST_ESCAPE, op | (ESC_MEMORY << 8)) }
+                if (memsym && ta) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))      // symbolic offset
+                if (kind == K_SLOAD) {
+                    // simplify(Select(chain, index)): from the newest store, the same
+                    // index term answers, a distinct constant index (both constant) is
+                    // skipped, anything else stops the walk (expr._select)
+                    const uint32_t cnt = L.storage_count[lane];
+                    int32_t e = (int32_t)cnt - 1;
+                    bool hit = false;
+                    for (; e >= 0; --e) {
+                        const uint2 tg = S.sttag[(size_t)e * N + lane];
+                        if (!ta && !tg.x) {
+                            if (u_eq(ld_word(gv(L.storage), V.row((uint32_t)e) * 2), a)) { hit = true; break; }
+                            continue;
+                        }
+                        if (ta && tg.x && sym_same(S, N, lane, ta - 1u, tg.x - 1u)) hit = true;
+                        break;
+                    }
+                    MPUSHCHK()
+                    MGAS()
+                    if (hit) {
+                        const uint2 tg = S.sttag[(size_t)e * N + lane];
+                        if (tg.y) rtag = tg.y;
+                        else rval = ld_word(gv(L.storage), V.row((uint32_t)e) * 2 + 1);
+                    } else if (e < 0 && !(lflags & LANE_SYMSTORE)) {
+                        rval = u_zero();                             // K(256, 256, 0): its default
+                    } else {
+                        uint32_t ya;
+                        if (!sym_ref(S, N, lane, ta, a, lnc, ya) ||
+                            !sym_node_push(S, N, lane, SYM_SLOAD | (256u << 8), ya, cnt, 0u, lnn, rtag))
+                            MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                    }
+                } else if (kind == K_SSTORE) {
+                    // a new Store on the chain (account.py:77-87), never in place
+                    if (flags & LANE_STATIC) MSTOPX(ST_VMEXC, EXC_WRITEPROT)
+                    const uint32_t cnt = L.storage_count[lane];
+                    if (cnt >= L.storage_cap) MSTOPX(ST_ESCAPE, op | (ESC_STORAGE << 8))
+                    MGAS()
+                    st_word(gv(L.storage), V.row(cnt) * 2, ta ? u_zero() : a);
+                    st_word(gv(L.storage), V.row(cnt) * 2 + 1, tb ? u_zero() : b);
+                    S.sttag[(size_t)cnt * N + lane] = make_uint2(ta, tb);
+                    L.storage_count[lane] = cnt + 1u;
+                } else if (kind == K_MLOAD) {
+                    MMEMX(a, u_small(32), (int64_t)gtmin)
+                    MPUSHCHK()
+                    MGAS()
+                    if (nmsize > msize) V.mzero(msize, nmsize);
+                    if ((lflags & LANE_MEMTAG) && mtag_any(S, N, lane, a.w[0], 32u, nmsize)) {
+                        if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                        uint32_t r;
+                        if (!sym_mem_ref(S, L, N, lane, a.w[0], 32u, nmsize, lnn, lnc, r))
+                            MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                        rtag = r + 1u;
+                    } else {
+                        rval = V.mword(a.w[0]);
+                    }
+                } else if (kind == K_MSTORE || kind == K_MSTORE8) {
+                    const bool m8 = kind == K_MSTORE8;
+                    if (tb && tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    MMEMX(a, u_small(m8 ? 1u : 32u), (int64_t)gtmin)
+                    MGAS()
+                    if (nmsize > msize) V.mzero(msize, nmsize);
+                    const uint32_t off = a.w[0];
+                    if (tb) {
+                        // write_word_at: byte j = Extract(255 - 8j, 248 - 8j, value);
+                        // MSTORE8: Extract(7, 0, value) (memory.py:102-115, instructions.py:1472-1493)
+                        const uint32_t base = (tb - 1u) << 5;
+                        if (m8) {
+                            V.set_mbyte(off, 0u);
+                            set_mtag(S, N, lane, off, 1u + (base | 31u));
+                        } else {
+                            V.set_mword(off, u_zero());
+                            for (uint32_t j = 0; j < 32u; ++j) set_mtag(S, N, lane, off + j, 1u + (base | j));
+                        }
+                        wrote_tag = true;
+                    } else {
+                        if (m8) V.set_mbyte(off, b.w[0] & 0xffu);
+                        else V.set_mword(off, b);
+                        if (lflags & LANE_MEMTAG)
+                            for (uint32_t j = 0; j < (m8 ? 1u : 32u); ++j) set_mtag(S, N, lane, off + j, 0u);
+                    }
+                } else {  // K_SHA3 over symbolic bytes: keccak256_<8 len>(data), create_keccak
+                    if (tb) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))   // symbolic length
+                    if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    const uint32_t len = b.w[0];
+                    if (!L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    const uint64_t g = 30ull + 6ull * (((uint64_t)len + 31ull) >> 5);
+                    ngmin += g; ngmax += g;
+                    if (ngmin >= glim) MSTOPX(ST_VMEXC, EXC_OOG)
+                    MMEMX(a, b, -1)
+                    const uint32_t rec_at = L.rec_len[lane];
+                    if ((uint64_t)rec_at + MG_REC_HEADER + 1u > L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_RECORD << 8))
+                    if (nmsize > msize) V.mzero(msize, nmsize);
+                    MPUSHCHK()
+                    uint32_t r;
+                    if (!sym_mem_ref(S, L, N, lane, a.w[0], len, nmsize, lnn, lnc, r) ||
+                        !sym_node_push(S, N, lane, SYM_KECCAK | (256u << 8), r, 0u, 8u * len, lnn, rtag))
+                        MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                    rec_new = rec_head(L, lane, rec_at, MG_REC_SYMKECCAK, len, L.steps[lane] + executed, u_zero());
+                    L.rec[(size_t)rec_new * N + lane] = rtag - 1u;
+                    ++rec_new;
+                    ++n_sha3;
+                }
+#undef MSTOPX
+#undef MGAS
+#undef MPUSHCHK
+#undef MMEMX
+            } while (0);
+            if (stop != ST_RUNNING) {
+                if (rec_pre) L.rec_len[lane] = rec_save;   // the instruction did not run
+                if (stop != ST_ESCAPE && stop != ST_HOOK) ++executed;
+                status = stop; aux = sx; break;
+            }
+            if (rec_new) L.rec_len[lane] = rec_new;
+            if (wrote_tag) lflags |= LANE_MEMTAG;
+            if (tl)
+                t_commit(T, N, lane, op, kind, tact, sp, nsp + (pushes ? 1u : 0u), nin, pushes, false, a, b, tb != 0u,
+                         pre_bit, post_bit, nobj, tsink, ttf);
+            if (pushes) {
+                V.set_stack(nsp, rval);
+                sym_set_tag(S, N, lane, nsp, rtag);
+            }
+            sp = nsp + (pushes ? 1u : 0u); ++pc; msize = nmsize; gmin = ngmin; gmax = ngmax; nn = lnn; nc = lnc;
+            if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }
+            ++executed;
+            continue;
+        }
+
         if ((any_sym || env_sym || cd_sym) && !stack_op && sp >= max(req, npop)) {
             // ---- symbolic semantics: one arena node (or a concrete result) ----
             const U256 a = sp >= 1u ? V.stack(sp - 1u) : u_zero();
@@ -484,6 +788,15 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (R.stop != ST_ESCAPE) ++executed;
             status = R.stop; aux = R.sx; break;
         }
+        if (symlane && (lflags & LANE_MEMTAG) && (kind == K_CDCOPY || kind == K_CODECOPY)) {
+            // the bytes a copy wrote are concrete now (CODECOPY stops at the end of
+            // the code: the bytes after it keep what they held, symbolic or not)
+            const U256 c = V.stack(sp0 - 3u);
+            uint32_t n = 0u;
+            if (kind == K_CDCOPY) n = u_iszero(c) ? 0u : c.w[0];
+            else if (u_fits32(pb) && pb.w[0] < C.n_bytes) n = min(C.n_bytes - pb.w[0], c.w[0]);
+            for (uint32_t j = 0; j < n; ++j) set_mtag(S, N, lane, pa.w[0] + j, 0u);
+        }
         if (R.sp >= 1u) V.set_stack(R.sp - 1u, R.T0);
         if (R.sp >= 2u) V.set_stack(R.sp - 2u, R.T1);
         if (symlane) {
@@ -510,7 +823,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
     L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
     L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
     L.status[lane] = status; L.aux[lane] = aux;
-    if (hook_ack && executed > 0u) L.flags[lane] = flags & ~LANE_HOOK_ACK;
+    if (hook_ack && executed > 0u) lflags &= ~LANE_HOOK_ACK;
+    if (lflags != flags) L.flags[lane] = lflags;
     L.steps[lane] += executed;
     if (loop_on) L.trace_len[lane] = tlen;
     if (n_sha3) L.sha3_count[lane] += n_sha3;

@@ -38,11 +38,14 @@ MG_ESC_RECORD = 6
 MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 # function-manager records (include/mythgpu.h MG_REC_*)
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
+MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
 MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT = 16, 32, 6
 MG_SYM_CDLOAD, MG_SYM_CDSIZE, MG_SYM_ENV, MG_SYM_BIN, MG_SYM_UN = 1, 2, 3, 4, 5
+MG_SYM_SLOAD, MG_SYM_KECCAK, MG_SYM_EXTRACT, MG_SYM_CONCAT, MG_SYM_TERM = 6, 7, 8, 9, 10
+MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
 MG_SYM_CONST = 0x80000000
 MG_LANE_TAINT = 2048
 # taint action word (include/mythgpu.h MG_TAINT_*)
@@ -109,10 +112,12 @@ class MgLaneSoa(ctypes.Structure):
 class MgSymSoa(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint32), ("stack_cap", ctypes.c_uint32), ("node_cap", ctypes.c_uint32),
                 ("const_cap", ctypes.c_uint32), ("stag", ctypes.c_void_p), ("node", ctypes.c_void_p),
-                ("cval", ctypes.c_void_p), ("n_nodes", ctypes.c_void_p), ("n_consts", ctypes.c_void_p)]
+                ("cval", ctypes.c_void_p), ("n_nodes", ctypes.c_void_p), ("n_consts", ctypes.c_void_p),
+                ("mem_cap", ctypes.c_uint32), ("storage_cap", ctypes.c_uint32),
+                ("mtag", ctypes.c_void_p), ("sttag", ctypes.c_void_p)]
 
 
-_SYM_FIELDS = ("stag", "node", "cval", "n_nodes", "n_consts")
+_SYM_FIELDS = ("stag", "node", "cval", "n_nodes", "n_consts", "mtag", "sttag")
 
 
 class MgTaintSoa(ctypes.Structure):
@@ -172,6 +177,10 @@ class LaneBatch:
             self.cval = np.zeros((n, max(shape.const_cap, 1), 8), dtype=np.uint32)
             self.n_nodes = np.zeros(n, dtype=np.uint32)
             self.n_consts = np.zeros(n, dtype=np.uint32)
+            # byte tags of memory (0 = concrete, else 1 + (node << 5 | j): byte j of
+            # the node's word) and (key, value) tags of the storage chain entries
+            self.mtag = np.zeros((n, shape.mem_cap), dtype=np.uint32)
+            self.sttag = np.zeros((n, shape.storage_cap, 2), dtype=np.uint32)
         if shape.obj_cap:
             self.sobj = np.zeros((n, shape.stack_cap), dtype=np.uint32)
             self.omask = np.zeros((n, shape.obj_cap), dtype=np.uint64)
@@ -209,6 +218,7 @@ class LaneBatch:
         s = MgSymSoa()
         s.n, s.stack_cap = n, self.shape.stack_cap
         s.node_cap, s.const_cap = self.shape.node_cap, self.shape.const_cap
+        s.mem_cap, s.storage_cap = self.shape.mem_cap, self.shape.storage_cap
         for f in _SYM_FIELDS:
             arr = getattr(self, f)
             setattr(s, f, arr.ctypes.data + first * arr.strides[0])
@@ -356,6 +366,10 @@ class LaneBatch:
                 k += 8 * (ln - 1)
                 out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF))
                 k += 2
+            elif kind == MG_REC_SYMKECCAK:
+                # (step, "symkeccak", KECCAK node index, input bytes)
+                out.append((step, "symkeccak", int(q[k]), ln))
+                k += 1
             elif kind == MG_REC_ANNOT:
                 # (step, "annot", atom, pc, opcode, post, stack[-1], stack[-2])
                 opw = int(q[k + 9])

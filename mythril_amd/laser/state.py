@@ -18,7 +18,8 @@ from typing import Dict, List, Optional, Union
 
 import numpy as np
 
-from ..smt.expr import BitVec, Bool, Expression, If, symbol_factory
+from ..smt.expr import (Array, BitVec, Bool, Expression, Extract, If, K, Node, _select, simplify_concat,
+                        symbol_factory)
 from .disassembly import Disassembly
 
 M256 = (1 << 256) - 1
@@ -99,11 +100,16 @@ class MachineStack(list):
 
 
 class Memory:
-    """memory.py:28-208 for concrete bytes: reads of unset bytes give 0, writes at
-    index >= msize are dropped (memory.py:202-203)."""
+    """memory.py:28-208 at concrete offsets: a byte is an int or, for a symbolic
+    byte, an 8-bit expression (``Extract(i + 7, i, value)`` of a symbolic word
+    written with write_word_at, memory.py:102-115); reads of unset bytes give 0,
+    writes at index >= msize are dropped (memory.py:202-203), and a word read
+    with a symbolic byte in it is ``simplify(Concat(bytes))`` (memory.py:70-82,
+    expr.simplify_concat).  Symbolic offsets stay with the host's handler."""
 
-    def __init__(self, data: bytes = b""):
+    def __init__(self, data: bytes = b"", sym: Optional[Dict[int, BitVec]] = None):
         self._m = bytearray(data)
+        self._sym: Dict[int, BitVec] = dict(sym) if sym else {}
 
     def __len__(self):
         return len(self._m)
@@ -111,27 +117,64 @@ class Memory:
     def extend(self, size: int):
         self._m.extend(b"\x00" * size)
 
+    def _byte(self, k: int):
+        if k >= len(self._m):
+            return 0
+        s = self._sym.get(k) if self._sym else None
+        return self._m[k] if s is None else s
+
     def __getitem__(self, item):
         if isinstance(item, slice):
             start, stop = item.start or 0, item.stop if item.stop is not None else len(self._m)
-            return [self._m[k] if k < len(self._m) else 0 for k in range(start, stop)]
-        return self._m[item] if item < len(self._m) else 0
+            return [self._byte(k) for k in range(start, stop)]
+        return self._byte(item)
 
-    def __setitem__(self, key: int, value: int):
-        if key < len(self._m):
-            self._m[key] = concrete(value) & 0xFF
+    def __setitem__(self, key: int, value):
+        if key >= len(self._m):
+            return
+        if isinstance(value, Expression) and value.symbolic:
+            if value.size() != 8:
+                raise ValueError("a memory byte is an 8-bit expression")
+            self._sym[key] = value
+            self._m[key] = 0                 # the byte's concrete image (as a lane holds it)
+            return
+        self._m[key] = concrete(value) & 0xFF
+        if self._sym:
+            self._sym.pop(key, None)
+
+    @property
+    def symbolic(self) -> bool:
+        return bool(self._sym)
+
+    def symbolic_bytes(self) -> Dict[int, BitVec]:
+        """{offset: 8-bit expression} of the symbolic bytes."""
+        return self._sym
 
     def get_word_at(self, index: int) -> BitVec:
-        b = bytes(self[index: index + 32])
+        if self._sym and any(k in self._sym for k in range(index, index + 32)):
+            return simplify_concat(self[index: index + 32])
+        b = bytes(self._m[index: index + 32]).ljust(32, b"\x00") if index < len(self._m) else bytes(32)
         return symbol_factory.BitVecVal(int.from_bytes(b, "big"), 256)
 
     def write_word_at(self, index: int, value) -> None:
+        if isinstance(value, Expression) and value.symbolic:
+            if isinstance(value, Bool):
+                value = If(value, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
+            for i in range(0, 256, 8):
+                self[index + 31 - i // 8] = Extract(i + 7, i, value)
+            return
         v = concrete(value).to_bytes(32, "big")
         for k in range(32):
             self[index + k] = v[k]
 
     def raw(self) -> bytes:
+        """Concrete bytes (a symbolic byte reads as 0)."""
         return bytes(self._m)
+
+    def copy(self) -> "Memory":
+        return Memory(self._m, self._sym)
+
+    __copy__ = copy
 
 
 class MachineState:
@@ -159,7 +202,7 @@ class MachineState:
         return values[0] if amount == 1 else values
 
     def __copy__(self):
-        return MachineState(self.gas_limit, self.pc, list(self.stack), Memory(self.memory.raw()),
+        return MachineState(self.gas_limit, self.pc, list(self.stack), self.memory.copy(),
                             self.depth, self.max_gas_used, self.min_gas_used)
 
     __deepcopy__ = lambda self, memo=None: self.__copy__()  # noqa: E731
@@ -167,24 +210,129 @@ class MachineState:
 
 # --------------------------------------------------------------- accounts
 class Storage:
-    """account.py:18-99 for concrete storage (K(256,256,0) + stores): absent keys read 0."""
+    """account.py:18-99.  Two representations of the same array:
+
+    * slot mode: concrete keys and values over K(256, 256, 0) as
+      ``printable_storage`` {int: int} (what a concrete lane carries);
+    * chain mode: the reference's ``_standard_storage`` itself -- the base array
+      (K(256, 256, 0), or ``Array("Storage{address}")`` for an account without
+      concrete storage) with one Store per ``__setitem__`` in order, and
+      ``printable_storage`` {key: value} as expressions.  A read is
+      ``simplify(Select(chain, key))`` (expr._select).  Symbolic lanes carry
+      this chain (mythril_amd/laser/symbolic.py).
+
+    A symbolic key or value, or a symbolic base, switches to chain mode; the
+    slots become Stores in insertion order (the store history of keys
+    overwritten while concrete is not kept: the same array, not the same
+    term)."""
 
     def __init__(self, concrete: bool = True, address=None, slots: Optional[Dict[int, int]] = None):
         self.concrete = concrete
         self.address = address
-        self.printable_storage: Dict[int, int] = dict(slots or {})
+        self.printable_storage: Dict = dict(slots or {})
+        self._chain: Optional[List] = None       # [(key, value)] in store order (chain mode)
+        self._raws: Optional[List] = None        # _raws[m]: the array after m stores
+        if not concrete:
+            self._chain, self._raws = [], [self._base_raw()]
+
+    def _base_raw(self):
+        if self.concrete:
+            return K(256, 256, 0).raw
+        return Array(f"Storage{concrete(self.address) if self.address is not None else None}", 256, 256).raw
+
+    @property
+    def is_chain(self) -> bool:
+        return self._chain is not None
+
+    def to_chain(self) -> "Storage":
+        if self._chain is None:
+            slots = list(self.printable_storage.items())
+            self._chain, self._raws, self.printable_storage = [], [self._base_raw()], {}
+            for k, v in slots:
+                self._append(symbol_factory.BitVecVal(k, 256), symbol_factory.BitVecVal(v, 256))
+        return self
+
+    @classmethod
+    def from_chain(cls, concrete: bool, address, entries) -> "Storage":
+        """Chain-mode storage with the given [(key, value)] stores in order."""
+        s = cls(concrete, address)
+        s._chain, s._raws, s.printable_storage = [], [s._base_raw()], {}
+        for k, v in entries:
+            s._append(k, v)
+        return s
+
+    def _append(self, key: BitVec, value: BitVec) -> None:
+        self._chain.append((key, value))
+        self._raws.append(Node("store", 0, (self._raws[-1], key.raw, value.raw), (256, 256)))
+        self.printable_storage[key] = value
+
+    def chain(self) -> List:
+        """[(key, value)] Stores in order (slot mode: its slots in insertion order)."""
+        if self._chain is not None:
+            return list(self._chain)
+        return [(symbol_factory.BitVecVal(k, 256), symbol_factory.BitVecVal(v, 256))
+                for k, v in self.printable_storage.items()]
+
+    def chain_raw(self, m: Optional[int] = None):
+        """The array term after the first m stores (all when None)."""
+        self.to_chain()
+        return self._raws[-1 if m is None else m]
+
+    @property
+    def base_raw(self):
+        return self._raws[0] if self._raws else self._base_raw()
 
     def __getitem__(self, item) -> BitVec:
-        return symbol_factory.BitVecVal(self.printable_storage.get(concrete(item), 0), 256)
+        if self._chain is None:
+            if not (isinstance(item, Expression) and item.symbolic):
+                return symbol_factory.BitVecVal(self.printable_storage.get(concrete(item), 0), 256)
+            self.to_chain()
+        key = item if isinstance(item, BitVec) else symbol_factory.BitVecVal(concrete(item), 256)
+        return BitVec(_select(self._raws[-1], key.raw))        # array.py:21-28: no annotations
 
     def __setitem__(self, key, value) -> None:
-        self.printable_storage[concrete(key)] = concrete(value)
+        sym = any(isinstance(x, Expression) and x.symbolic for x in (key, value))
+        if self._chain is None and not sym:
+            self.printable_storage[concrete(key)] = concrete(value)
+            return
+        self.to_chain()
+        if isinstance(value, Bool):
+            value = If(value, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
+        k = key if isinstance(key, BitVec) else symbol_factory.BitVecVal(concrete(key), 256)
+        v = value if isinstance(value, BitVec) else symbol_factory.BitVecVal(concrete(value), 256)
+        self._append(k, v)
 
     def items(self):
         return self.printable_storage.items()
 
+    def n_entries(self) -> int:
+        return len(self._chain) if self._chain is not None else len(self.printable_storage)
+
+    def slots(self) -> Dict[int, int]:
+        """{key: value} of concrete storage (a chain of concrete stores over
+        K(0), latest store per key); raises for symbolic storage."""
+        if self._chain is None:
+            return self.printable_storage
+        if not self.concrete:
+            raise ValueError("symbolic storage cannot be placed in a concrete lane")
+        out: Dict[int, int] = {}
+        for k, v in self._chain:
+            out[concrete(k)] = concrete(v)
+        return out
+
+    def set_slots(self, slots: Dict[int, int]) -> None:
+        """Replace the contents by concrete slots (slot mode)."""
+        self._chain = self._raws = None
+        self.printable_storage = dict(slots)
+
     def __copy__(self):
-        return Storage(self.concrete, self.address, self.printable_storage)
+        s = Storage(self.concrete, self.address, None)
+        s.printable_storage = dict(self.printable_storage)
+        if self._chain is not None:
+            s._chain, s._raws = list(self._chain), list(self._raws)
+        else:
+            s._chain = s._raws = None
+        return s
 
 
 class Account:

@@ -392,8 +392,7 @@ class LaserEVM:
         n = len(states)
         g = self._cap_grow
         msz = max((len(s.mstate.memory) for s in states), default=0)
-        slots = max((len(s.environment.active_account.storage.printable_storage) for s in states),
-                    default=0)
+        slots = max((s.environment.active_account.storage.n_entries() for s in states), default=0)
         cdl = max((len(s.environment.calldata) for s in states), default=0)    # 0 when symbolic
         trace_cap = 0
         if self._loop_bound():
@@ -404,14 +403,23 @@ class LaserEVM:
         mem_cap = min(mem_cap, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
         mem_cap = max(mem_cap, (msz + 31) // 32 * 32)
         mem_cap = (mem_cap + 31) // 32 * 32
-        symbolic = any(sym.state_is_symbolic(s) for s in states)
+        # symbolic lanes: their arena encodings (reused by _pack) size the planes
+        self._encodings = {}
+        n_nodes = n_consts = 0
+        for s in states:
+            if sym.state_is_symbolic(s):
+                le = self._encodings[id(s)] = sym.encode_state(s)
+                n_nodes = max(n_nodes, len(le.enc.nodes))
+                n_consts = max(n_consts, len(le.enc.consts))
+        symbolic = bool(self._encodings)
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),
                          storage_cap=max(64 * g, 2 * slots + 16), trace_cap=trace_cap,
                          # taint lanes log a record per annotating / deferred hook: a
                          # log that fills escapes and regrows (a later batch, §7)
-                         rec_cap=(4096 if taint else 512) * g, node_cap=256 * g if symbolic else 0,
-                         const_cap=128 * g if symbolic else 0,
+                         rec_cap=(4096 if taint else 512) * g,
+                         node_cap=max(256 * g, 2 * n_nodes) if symbolic else 0,
+                         const_cap=max(128 * g, 2 * n_consts) if symbolic else 0,
                          obj_cap=min(256 * g, 65536) if taint else 0)
 
     def _pack(self, b: LaneBatch, i: int, s: GlobalState) -> None:
@@ -420,15 +428,23 @@ class LaserEVM:
         gas_limit = getattr(tx, "gas_limit", None)
         b.code_id[i] = self.code_id(env.code)
         b.pc[i] = ms.pc
-        sflags = sym.lane_flags(s) if b.symbolic else 0
+        sflags = 0
+        le = None
         b.sp[i] = len(ms.stack)
         b.stack[i] = 0
         if b.symbolic:
             b.stag[i] = 0
             b.n_nodes[i] = b.n_consts[i] = 0
-            if sym.encode_stack(b, i, list(ms.stack)):
-                sflags |= MG_LANE_SYMBOLIC
-        else:
+            b.mtag[i] = 0
+            b.sttag[i] = 0
+            le = self._encodings.pop(id(s), None) if getattr(self, "_encodings", None) else None
+            if le is None:
+                le = sym.encode_state(s, b.shape.node_cap, b.shape.const_cap)
+            if le.symbolic:
+                sflags = le.flags
+            else:
+                le = None
+        if le is None:
             stack = [concrete(x) for x in ms.stack]
             if stack:
                 b.stack[i, : len(stack)] = np.array(
@@ -456,12 +472,15 @@ class LaserEVM:
         for k in range(MG_ENV_WORDS):
             w = words[k]
             b.env[i, k] = 0 if (isinstance(w, Expression) and w.value is None) else word_to_limbs(concrete(w))
-        slots = list(env.active_account.storage.printable_storage.items())
-        b.storage[i] = 0
-        for k, (key, val) in enumerate(slots):
-            b.storage[i, k, :8] = word_to_limbs(key)
-            b.storage[i, k, 8:] = word_to_limbs(val)
-        b.storage_count[i] = len(slots)
+        if le is not None:
+            le.write(b, i)            # stack, arena, memory tags and the storage chain
+        else:
+            slots = list(env.active_account.storage.slots().items())
+            b.storage[i] = 0
+            for k, (key, val) in enumerate(slots):
+                b.storage[i, k, :8] = word_to_limbs(key)
+                b.storage[i, k, 8:] = word_to_limbs(val)
+            b.storage_count[i] = len(slots)
         b.ret_offset[i] = b.ret_len[i] = 0
         if b.shape.trace_cap:
             tr = _trace_of(s)
@@ -483,23 +502,29 @@ class LaserEVM:
         ms = s.mstate
         ms.pc = int(b.pc[i])
         sp = int(b.sp[i])
-        if b.symbolic and int(b.flags[i]) & MG_LANE_SYMBOLIC:
-            ms.stack = MachineStack(sym.decode_stack(b, i, s))
+        symlane = b.symbolic and int(b.flags[i]) & MG_LANE_SYMBOLIC
+        if symlane:
+            stack, memory, storage = sym.decode_lane(b, i, s)
+            ms.stack = MachineStack(stack)
         else:
             ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])
         if b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack(tnt.materialise(b, i, s, self._tl[i], self._plan, list(ms.stack)))
-        ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
         ms.depth = int(b.depth[i])
         ms.min_gas_used = int(b.gas_min[i])
         ms.max_gas_used = int(b.gas_max[i])
-        store = s.environment.active_account.storage.printable_storage
-        store.clear()
-        cnt = int(b.storage_count[i])
-        if cnt:
-            kv = rows_to_words(b.storage[i, :cnt].reshape(2 * cnt, 8))
-            for k in range(cnt):
-                store[kv[2 * k]] = kv[2 * k + 1]
+        acct = s.environment.active_account
+        if symlane:
+            # the lane's store chain and memory bytes (symbolic ones included)
+            ms.memory = memory
+            acct.storage = storage
+        else:
+            ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
+            acct.storage.set_slots({})
+            cnt = int(b.storage_count[i])
+            if cnt:
+                kv = rows_to_words(b.storage[i, :cnt].reshape(2 * cnt, 8))
+                acct.storage.set_slots({kv[2 * k]: kv[2 * k + 1] for k in range(cnt)})
         s.lane_steps = int(b.steps[i])
         if b.shape.trace_cap:
             ann = _annotation_of(s)
@@ -518,6 +543,9 @@ class LaserEVM:
             if end <= seen:
                 continue
             for r in b.records(i, seen):
+                if r[1] == "symkeccak":
+                    # the input as the lane's arena holds it now (its node is final)
+                    r = (r[0], "symkeccak", sym.keccak_input(b, i, self._rec_lanes[i].state, r[2]))
                 key = (r[0], i) if self._rec_bfs else (-i, r[0])
                 heapq.heappush(self._recq, (key, next(self._rec_seq), i, r))
             b.rec_seen[i] = end
@@ -533,6 +561,8 @@ class LaserEVM:
             _, _, i, r = heapq.heappop(q)
             if r[1] == "keccak":
                 keccak_function_manager.register_concrete(r[2], r[3])
+            elif r[1] == "symkeccak":
+                keccak_function_manager.create_keccak(r[2])      # symbolic_inputs, in order
             elif r[1] == "annot":
                 tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
             elif r[1] == "hook":

@@ -35,10 +35,13 @@ import numpy as np
 
 from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_CALLVALUE as MG_ENV_CALLVALUE, ENV_GASPRICE as MG_ENV_GASPRICE,
-                     ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT, MG_SYM_BIN, MG_SYM_CDLOAD,
-                     MG_SYM_CDSIZE, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_UN, limbs_to_word, word_to_limbs)
-from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, If, LShR, Node, Not, UDiv, UGT, ULT, URem,
-                        SRem, symbol_factory)
+                     ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
+                     MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDLOAD, MG_SYM_CDSIZE,
+                     MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
+from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
+                        URem, SRem, _select, simplify_concat, symbol_factory)
+from .state import Memory, Storage
 
 TT256M1 = (1 << 256) - 1
 
@@ -74,7 +77,8 @@ class SymbolicCalldata:
         off = symbol_factory.BitVecVal(offset, 256) if isinstance(offset, int) else offset
         w = self._words.get(off.raw)
         if w is None:
-            w = self._words[off.raw] = Concat(*[self._load(off if k == 0 else off + k) for k in range(32)])
+            w = self._words[off.raw] = _mark(Concat(*[self._load(off if k == 0 else off + k) for k in range(32)]),
+                                             MG_SYM_CDLOAD, 0, (off,))
         return w
 
     def __len__(self):
@@ -173,44 +177,168 @@ def source(kind: int, imm: int, arg, state):
 
 
 # ----------------------------------------------------------- decode / encode
-def decode_stack(b, i: int, state) -> list:
-    """Lane i's stack as the reference would hold it: BitVecVal for concrete
-    words, the node's expression for symbolic ones."""
-    sp = int(b.sp[i])
-    n_nodes = int(b.n_nodes[i])
-    memo: List[Optional[object]] = [None] * n_nodes
+class _Decoder:
+    """The expressions of one lane's planes: its stack words, memory bytes and
+    storage chain (the arena is shared by all three, nodes memoised)."""
 
-    def ref(r: int):
+    def __init__(self, b, i: int, state):
+        self.b, self.i, self.state = b, i, state
+        self.n_nodes = int(b.n_nodes[i])
+        self.memo: List[Optional[object]] = [None] * self.n_nodes
+        self._entries = None
+        self._raws = None
+
+    # -- operands
+    def const(self, r: int, width: int = 256):
+        v = limbs_to_word(self.b.cval[self.i, r & ~MG_SYM_CONST])
+        return symbol_factory.BitVecVal(v & ((1 << width) - 1), width)
+
+    def ref(self, r: int):
+        return self.const(r) if r & MG_SYM_CONST else self.node(r)
+
+    def parts(self, r: int, width: int) -> list:
+        """The memory parts an operand of a CONCAT / KECCAK stands for."""
         if r & MG_SYM_CONST:
-            return symbol_factory.BitVecVal(limbs_to_word(b.cval[i, r & ~MG_SYM_CONST]), 256)
-        return node(r)
-
-    def node(k: int):
-        if k >= n_nodes:
-            raise ValueError(f"lane {i}: arena reference {k} past its {n_nodes} nodes")
-        if memo[k] is not None:
-            return memo[k]
-        x, y, z, w = (int(v) for v in b.node[i, k])
+            return [self.const(r, width)]
+        x = int(self.b.node[self.i, r, 0])
         kind = x & 0xFF
-        if kind == MG_SYM_BIN:
-            a, c = ref(y), ref(z)
-            e = _mark(binary(w, a, c), kind, w, (a, c))
-        elif kind == MG_SYM_UN:
-            a = ref(y)
-            e = _mark(unary(w, a), kind, w, (a,))
-        elif kind == MG_SYM_CDLOAD:
-            a = ref(y)
-            e = _mark(source(kind, w, a, state), kind, w, (a,))
-        else:
-            e = _mark(source(kind, w, None, state), kind, w, ())
-        memo[k] = e
+        if kind == MG_SYM_CONCAT:
+            _, y, z, w = (int(v) for v in self.b.node[self.i, r])
+            return self.parts(y, w & 0xFFFF) + self.parts(z, w >> 16)
+        return [self.node(r)]
+
+    # -- nodes
+    def node(self, k: int):
+        if k >= self.n_nodes:
+            raise ValueError(f"lane {self.i}: arena reference {k} past its {self.n_nodes} nodes")
+        e = self.memo[k]
+        if e is None:
+            e = self.memo[k] = self._build(k)
         return e
 
+    def _build(self, k: int):
+        x, y, z, w = (int(v) for v in self.b.node[self.i, k])
+        kind = x & 0xFF
+        if kind == MG_SYM_BIN:
+            a, c = self.ref(y), self.ref(z)
+            return _mark(binary(w, a, c), kind, w, (a, c))
+        if kind == MG_SYM_UN:
+            a = self.ref(y)
+            return _mark(unary(w, a), kind, w, (a,))
+        if kind == MG_SYM_CDLOAD:
+            a = self.ref(y)
+            return _mark(source(kind, w, a, self.state), kind, w, (a,))
+        if kind in (MG_SYM_CDSIZE, MG_SYM_ENV):
+            return _mark(source(kind, w, None, self.state), kind, w, ())
+        if kind == MG_SYM_SLOAD:
+            # Storage.__getitem__: simplify(Select(chain after z stores, index))
+            return BitVec(_select(self.chain_raw(z), self.ref(y).raw))
+        if kind == MG_SYM_EXTRACT:
+            return Extract(w >> 16, w & 0xFFFF, self.node(y))
+        if kind == MG_SYM_CONCAT:
+            return simplify_concat(self.parts(k, x >> 8))
+        if kind == MG_SYM_KECCAK:
+            return keccak_of(simplify_concat(self.parts(y, w)))
+        if kind == MG_SYM_TERM:
+            return term(w)
+        raise NotEncodable(f"unknown arena node kind {kind}")
+
+    # -- memory and storage
+    def memory(self):
+        """The lane's memory: concrete bytes plus the symbolic ones (memory.py
+        bytes: Extract(255 - 8j, 248 - 8j, word) of a node's word)."""
+        b, i = self.b, self.i
+        msize = int(b.msize[i])
+        symb = {}
+        if hasattr(b, "mtag") and msize:
+            tags = b.mtag[i, :msize]
+            for p in np.flatnonzero(tags):
+                t = int(tags[p]) - 1
+                node, j = t >> 5, t & 31
+                word = self.node(node)
+                symb[int(p)] = word if word.size() == 8 else Extract(255 - 8 * j, 248 - 8 * j, word)
+        return Memory(bytes(b.memory[i, :msize]), symb)
+
+    def entry(self, e: int):
+        """Storage chain entry e as (key, value).  Entries decode one at a time:
+        a stored value may be a read of the chain before it (x -= v)."""
+        if self._entries is None:
+            self._entries = []
+        b, i = self.b, self.i
+        while len(self._entries) <= e:
+            k = len(self._entries)
+            kt, vt = (int(v) for v in b.sttag[i, k])
+            key = self.node(kt - 1) if kt else symbol_factory.BitVecVal(limbs_to_word(b.storage[i, k, :8]), 256)
+            val = self.node(vt - 1) if vt else symbol_factory.BitVecVal(limbs_to_word(b.storage[i, k, 8:]), 256)
+            self._entries.append((key, val))
+        return self._entries[e]
+
+    def entries(self) -> list:
+        """The storage chain: [(key, value)] per device entry, in store order."""
+        n = int(self.b.storage_count[self.i])
+        if n:
+            self.entry(n - 1)
+        return list(self._entries or [])[:n]
+
+    def base_raw(self):
+        acct = self.state.environment.active_account
+        symstore = bool(int(self.b.flags[self.i]) & MG_LANE_SYMSTORE)
+        return Storage(not symstore, acct.address).base_raw
+
+    def chain_raw(self, m: int):
+        if self._raws is None:
+            self._raws = [self.base_raw()]
+        while len(self._raws) <= m:
+            k, v = self.entry(len(self._raws) - 1)
+            self._raws.append(Node("store", 0, (self._raws[-1], k.raw, v.raw), (256, 256)))
+        return self._raws[m]
+
+    def storage(self):
+        acct = self.state.environment.active_account
+        symstore = bool(int(self.b.flags[self.i]) & MG_LANE_SYMSTORE)
+        return Storage.from_chain(not symstore, acct.address, self.entries())
+
+
+def keccak_of(data):
+    """KeccakFunctionManager.create_keccak's value for `data` without its
+    registration: the concrete hash, or keccak256_<bits>(data)."""
+    if not data.symbolic:
+        from ..keccak import keccak256
+        n = data.size() // 8
+        return symbol_factory.BitVecVal(int.from_bytes(keccak256(data.value.to_bytes(n, "big")), "big"), 256)
+    w = data.size()
+    return Function(f"keccak256_{w}", [w], 256)(data)
+
+
+def decode_stack(b, i: int, state, dec: Optional[_Decoder] = None) -> list:
+    """Lane i's stack as the reference would hold it: BitVecVal for concrete
+    words, the node's expression for symbolic ones."""
+    dec = dec or _Decoder(b, i, state)
+    sp = int(b.sp[i])
     out = []
     for s in range(sp):
         t = int(b.stag[i, s])
-        out.append(node(t - 1) if t else symbol_factory.BitVecVal(limbs_to_word(b.stack[i, s]), 256))
+        out.append(dec.node(t - 1) if t else symbol_factory.BitVecVal(limbs_to_word(b.stack[i, s]), 256))
     return out
+
+
+def decode_lane(b, i: int, state):
+    """(stack, memory, storage) of a symbolic lane."""
+    dec = _Decoder(b, i, state)
+    return decode_stack(b, i, state, dec), dec.memory(), dec.storage()
+
+
+def decode_node(b, i: int, state, k: int):
+    return _Decoder(b, i, state).node(k)
+
+
+def keccak_input(b, i: int, state, k: int):
+    """The input of lane i's KECCAK node k (an MG_REC_SYMKECCAK record):
+    simplify(Concat(bytes)) of the hashed memory, as sha3_ passes it to
+    create_keccak (instructions.py:1032-1048)."""
+    dec = _Decoder(b, i, state)
+    _, y, _, w = (int(v) for v in b.node[i, k])
+    return simplify_concat(dec.parts(y, w))
 
 
 def _concrete_value(x) -> Optional[int]:
@@ -222,61 +350,209 @@ def _concrete_value(x) -> Optional[int]:
     return None
 
 
+class _Encoder:
+    """One lane's arena built from expressions: nodes for expressions decode
+    produced (recorded provenance) or that have the structure of a memory read,
+    a keccak application or a storage read over this lane's chain; constants
+    in the constant table; repeated subterms shared."""
+
+    def __init__(self, node_cap: int = 1 << 30, const_cap: int = 1 << 30):
+        self.node_cap, self.const_cap = node_cap, const_cap
+        self.nodes: list = []             # (x, y, z, w)
+        self.consts: list = []            # ints
+        self._cref: dict = {}
+        self._nref: dict = {}             # raw -> node index
+        self.raws: list = []              # this lane's chain prefixes (encode_storage)
+
+    def cref(self, v: int) -> int:
+        r = self._cref.get(v)
+        if r is None:
+            if len(self.consts) >= self.const_cap:
+                raise NotEncodable("constant table full")
+            r = self._cref[v] = MG_SYM_CONST | len(self.consts)
+            self.consts.append(v)
+        return r
+
+    def _push(self, raw, x, y=0, z=0, w=0) -> int:
+        if len(self.nodes) >= self.node_cap:
+            raise NotEncodable("arena full")
+        self.nodes.append((x, y, z, w))
+        self._nref[raw] = len(self.nodes) - 1
+        return len(self.nodes) - 1
+
+    def enc(self, raw) -> int:
+        """Operand ref of a raw term (a node index or a constant ref)."""
+        if raw.op == "const":
+            return self.cref(int(raw.param))
+        r = self._nref.get(raw)
+        if r is not None:
+            return r
+        prov = _PROV.get(raw)
+        if prov is not None:
+            kind, imm, args, width = prov
+            refs = [self.enc(a.raw) for a in args]
+            return self._push(raw, kind | (width << 8), refs[0] if refs else 0, refs[1] if len(refs) > 1 else 0,
+                              imm)
+        op = raw.op
+        if op == "extract":
+            src = raw.args[0]
+            y = self.enc(src)
+            if y & MG_SYM_CONST:
+                raise NotEncodable("extract of a constant")
+            hi, lo = raw.param
+            return self._push(raw, MG_SYM_EXTRACT | (raw.width << 8), y, 0, (hi << 16) | lo)
+        if op == "concat":
+            l, r_ = raw.args
+            return self._push(raw, MG_SYM_CONCAT | (raw.width << 8), self.enc(l), self.enc(r_),
+                              l.width | (r_.width << 16))
+        if op == "uf" and len(raw.args) == 1 and raw.param[0].startswith("keccak256_") \
+                and not raw.param[0].endswith("-1") and raw.width == 256:
+            return self._push(raw, MG_SYM_KECCAK | (256 << 8), self.enc(raw.args[0]), 0, raw.args[0].width)
+        if op == "select" and raw.width == 256:
+            arr = raw.args[0]
+            for m, a in enumerate(self.raws):
+                if a is arr:
+                    return self._push(raw, MG_SYM_SLOAD | (256 << 8), self.enc(raw.args[1]), m, 0)
+        # any other term rides on the lane as an opaque node: the device builds on
+        # it and compares it by identity, the host decodes it to the same term
+        if raw.width > 0xFFFFFF:
+            raise NotEncodable("term too wide for an arena node")
+        return self._push(raw, MG_SYM_TERM | (raw.width << 8), 0, 0, register_term(raw))
+
+    def word(self, x) -> Tuple[int, int]:
+        """(concrete value, tag) of a stack word / storage key or value."""
+        v = _concrete_value(x)
+        if v is not None and not isinstance(x, Bool):
+            return v, 0
+        if isinstance(x, Bool) and x.value is not None:
+            return int(bool(x.value)), 0
+        r = self.enc(x.raw)
+        if r & MG_SYM_CONST:                    # a Bool folded to a constant, say
+            return self.consts[r & ~MG_SYM_CONST], 0
+        return 0, r + 1
+
+    def byte(self, e) -> int:
+        """Tag of a symbolic memory byte."""
+        raw = e.raw
+        if raw.op == "extract" and raw.width == 8 and raw.args[0].width == 256:
+            hi, lo = raw.param
+            if hi % 8 == 7:
+                r = self.enc(raw.args[0])
+                if not r & MG_SYM_CONST:
+                    return 1 + ((r << 5) | ((255 - hi) // 8))
+        r = self.enc(raw)
+        if r & MG_SYM_CONST or raw.width != 8:
+            raise NotEncodable("memory byte without arena provenance")
+        return 1 + ((r << 5) | 31)
+
+
+# Opaque terms of the host's expression layer carried by lanes (MG_SYM_TERM):
+# index -> term, interned by identity, so equal indices are the same term.
+_TERMS: List[object] = []
+_TERM_IDX: dict = {}
+
+
+def register_term(raw) -> int:
+    k = _TERM_IDX.get(raw)
+    if k is None:
+        k = _TERM_IDX[raw] = len(_TERMS)
+        _TERMS.append(raw)
+    return k
+
+
+def term(k: int):
+    raw = _TERMS[k]
+    return Bool(raw) if raw.width == 1 and raw.op not in ("const",) and _is_bool_op(raw) else BitVec(raw)
+
+
+def _is_bool_op(raw) -> bool:
+    return raw.op in ("eq", "distinct", "and", "or", "not", "xor", "implies", "bvult", "bvugt", "bvslt", "bvsgt",
+                      "bvsle", "bvsge", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u") or \
+        (raw.op == "var" and raw.width == 1)
+
+
+class LaneEncoding:
+    """Everything encode_state wrote for one state (lists, written by write())."""
+
+    def __init__(self, enc: _Encoder, stack, mem, store, flags: int):
+        self.enc, self.stack, self.mem, self.store, self.flags = enc, stack, mem, store, flags
+
+    @property
+    def symbolic(self) -> bool:
+        return bool(self.flags & MG_LANE_SYMBOLIC)
+
+    def write(self, b, i: int) -> None:
+        sh = b.shape
+        enc = self.enc
+        if len(enc.nodes) > sh.node_cap or len(enc.consts) > sh.const_cap:
+            raise NotEncodable("arena larger than the batch's capacities")
+        b.stag[i] = 0
+        for s, (v, t) in enumerate(self.stack):
+            b.stack[i, s] = word_to_limbs(v)
+            b.stag[i, s] = t
+        if enc.nodes:
+            b.node[i, :len(enc.nodes)] = np.array(enc.nodes, dtype=np.uint64).astype(np.uint32)
+        for k, v in enumerate(enc.consts):
+            b.cval[i, k] = word_to_limbs(v)
+        b.n_nodes[i], b.n_consts[i] = len(enc.nodes), len(enc.consts)
+        b.mtag[i] = 0
+        for p, t in self.mem.items():
+            b.mtag[i, p] = t
+        if self.store is not None:
+            if len(self.store) > sh.storage_cap:
+                raise NotEncodable("storage chain longer than the batch's capacity")
+            b.storage[i] = 0
+            b.sttag[i] = 0
+            for e, (kv, kt, vv, vt) in enumerate(self.store):
+                b.storage[i, e, :8] = word_to_limbs(kv)
+                b.storage[i, e, 8:] = word_to_limbs(vv)
+                b.sttag[i, e] = (kt, vt)
+            b.storage_count[i] = len(self.store)
+
+
+def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> LaneEncoding:
+    """A state's stack, symbolic memory bytes and (for a symbolic lane) storage
+    chain in arena form; raises NotEncodable for an expression the arena cannot
+    represent.  The lane is symbolic when any of them is, or its calldata or
+    environment words are, or its storage base is the symbolic Array."""
+    enc = _Encoder(node_cap, const_cap)
+    flags = lane_flags(state)
+    storage = state.environment.active_account.storage
+    symstore = not storage.concrete or (storage.is_chain and any(
+        k.symbolic or v.symbolic for k, v in storage.chain()))
+    store = None
+    if flags or symstore or state.mstate.memory.symbolic or not all(
+            _concrete_value(x) is not None or (isinstance(x, Bool) and x.value is not None)
+            for x in state.mstate.stack):
+        flags |= MG_LANE_SYMBOLIC
+        # the chain first: storage reads on the stack refer to its prefixes
+        enc.raws = [storage.base_raw]
+        store = []
+        for k, v in storage.chain():
+            kv, kt = enc.word(k)
+            vv, vt = enc.word(v)
+            store.append((kv, kt, vv, vt))
+            enc.raws.append(Node("store", 0, (enc.raws[-1], k.raw, v.raw), (256, 256)))
+        if not storage.concrete:
+            flags |= MG_LANE_SYMSTORE
+    stack = [enc.word(x) for x in state.mstate.stack]
+    mem = {}
+    if state.mstate.memory.symbolic:
+        for p, e in state.mstate.memory.symbolic_bytes().items():
+            mem[p] = enc.byte(e)
+        flags |= MG_LANE_MEMTAG
+    return LaneEncoding(enc, stack, mem, store, flags)
+
+
 def encode_stack(b, i: int, stack: list) -> bool:
     """Write `stack` into lane i's stack rows and symbolic planes.  Returns
     whether any word is symbolic; raises NotEncodable for an expression that no
     arena node produced, or a full arena."""
     sh = b.shape
-    nodes: dict = {}
-    consts: dict = {}
-    nn = nc = 0
-
-    def cref(v: int) -> int:
-        nonlocal nc
-        if v in consts:
-            return consts[v]
-        if nc >= sh.const_cap:
-            raise NotEncodable("constant table full")
-        b.cval[i, nc] = word_to_limbs(v)
-        consts[v] = MG_SYM_CONST | nc
-        nc += 1
-        return consts[v]
-
-    def enc(e) -> int:
-        nonlocal nn
-        v = _concrete_value(e)
-        if v is not None and not isinstance(e, Bool):
-            return cref(v)
-        raw = e.raw
-        if raw in nodes:
-            return nodes[raw]
-        prov = _PROV.get(raw)
-        if prov is None:
-            raise NotEncodable(f"expression without arena provenance: {raw!r}"[:200])
-        kind, imm, args, width = prov
-        refs = [enc(a) for a in args]
-        if nn >= sh.node_cap:
-            raise NotEncodable("arena full")
-        b.node[i, nn] = (kind | (width << 8), refs[0] if refs else 0, refs[1] if len(refs) > 1 else 0, imm)
-        nodes[raw] = nn
-        nn += 1
-        return nodes[raw]
-
-    sym = False
-    for s, x in enumerate(stack):
-        v = _concrete_value(x)
-        if v is not None and not isinstance(x, Bool):
-            b.stack[i, s] = word_to_limbs(v)
-            b.stag[i, s] = 0
-        elif isinstance(x, Bool) and x.value is not None:
-            b.stack[i, s] = word_to_limbs(int(bool(x.value)))
-            b.stag[i, s] = 0
-        else:
-            b.stag[i, s] = enc(x) + 1
-            b.stack[i, s] = 0
-            sym = True
-    b.n_nodes[i], b.n_consts[i] = nn, nc
-    return sym
+    enc = _Encoder(sh.node_cap, sh.const_cap)
+    words = [enc.word(x) for x in stack]
+    LaneEncoding(enc, words, {}, None, 0).write(b, i)
+    return any(t for _, t in words)
 
 
 def lane_flags(state) -> int:
@@ -293,7 +569,13 @@ def lane_flags(state) -> int:
 
 
 def state_is_symbolic(state) -> bool:
-    if lane_flags(state):
+    """Whether the state needs a symbolic lane: symbolic calldata or environment
+    words, a symbolic stack word or memory byte, or storage over the symbolic
+    Array or with symbolic stores."""
+    if lane_flags(state) or state.mstate.memory.symbolic:
+        return True
+    st = state.environment.active_account.storage
+    if not st.concrete or (st.is_chain and any(k.symbolic or v.symbolic for k, v in st.chain())):
         return True
     return any(_concrete_value(x) is None for x in state.mstate.stack)
 
@@ -350,16 +632,13 @@ def _fork_copy(state):
 
 
 def lane_eligible(state) -> bool:
-    """Whether a lane can carry the state: every symbolic stack word has arena
-    provenance, calldata is bytes or a SymbolicCalldata, and the active
-    account's storage is concrete."""
-    acct = state.environment.active_account
-    if not getattr(acct.storage, "concrete", True):
+    """Whether a lane can carry the state: every symbolic stack word, memory
+    byte and storage key or value is an expression the arena represents
+    (encode_state succeeds)."""
+    try:
+        encode_state(state)
+    except NotEncodable:
         return False
-    for x in state.mstate.stack:
-        if _concrete_value(x) is None and not (isinstance(x, Bool) and x.value is not None):
-            if x.raw not in _PROV:
-                return False
     return True
 
 

@@ -315,6 +315,50 @@ def Concat(*args) -> BitVec:
     return acc
 
 
+def simplify_concat(parts) -> BitVec:
+    """``simplify(Concat(parts))`` as the reference builds memory words and SHA3
+    inputs (memory.py:56-82, instructions.py:1032-1039): z3's concat rewrites
+    restated on the part sequence -- adjacent constants join into one constant,
+    adjacent extracts of the same term over contiguous bit ranges join into one
+    extract, and an extract of a term's full width is the term.  A part that is
+    neither a constant nor an extract counts as the full-width extract of itself
+    (parts are never taken apart).  The result depends only on the part
+    sequence after these joins, so parts that were joined in advance (device
+    runs, mythril_amd/laser/symbolic.py) give the same expression as the bytes
+    they cover."""
+    atoms: list = []              # ["c", value, width] | ["x", term, hi, lo]
+    ann = frozenset()
+    for p in parts:
+        p = _bv(p, 8)
+        ann = ann | p.annotations
+        r = p.raw
+        if r.op == "const":
+            a = ["c", r.param, r.width]
+        elif r.op == "extract":
+            a = ["x", r.args[0], r.param[0], r.param[1]]
+        else:
+            a = ["x", r, r.width - 1, 0]
+        if atoms:
+            b = atoms[-1]
+            if a[0] == "c" and b[0] == "c":
+                b[1], b[2] = (b[1] << a[2]) | a[1], b[2] + a[2]
+                continue
+            if a[0] == "x" and b[0] == "x" and a[1] is b[1] and b[3] == a[2] + 1:
+                b[3] = a[3]
+                continue
+        atoms.append(a)
+    acc = None
+    for a in atoms:
+        if a[0] == "c":
+            n = const(a[1], a[2])
+        elif a[2] == a[1].width - 1 and a[3] == 0:
+            n = a[1]
+        else:
+            n = _fold("extract", a[2] - a[3] + 1, (a[1],), (a[2], a[3]))
+        acc = n if acc is None else _fold("concat", acc.width + n.width, (acc, n))
+    return BitVec(acc, ann)
+
+
 def Extract(hi: int, lo: int, a) -> BitVec:
     a = _bv(a)
     return BitVec(_fold("extract", hi - lo + 1, (a.raw,), (hi, lo)), a.annotations)
@@ -381,19 +425,26 @@ symbol_factory = _SymbolFactory()
 #   store: args (array, index, value)
 # select(array, index) and uf(args...) are bit-vector nodes of the range width.
 def _select(arr: Node, idx: Node) -> Node:
-    """Select with the folding z3's simplify applies to concrete indices:
-    a store at an equal constant index answers, an unequal one is skipped, and
-    a K array answers its default."""
+    """Select with the rewrites z3's simplify applies (the reference reads
+    storage as ``simplify(storage[item])``, account.py:75): walking the store
+    chain from the newest store, a store at the same index term answers (the
+    terms are hash-consed: identical means the same node), a store at a
+    distinct constant index is skipped when the index is a constant too, and a
+    constant array answers its default for any index; the first store neither
+    rule decides stops the walk, and the select stays over the rest of the
+    chain."""
     a = arr
     while True:
-        if a.op == "store" and idx.op == "const" and a.args[1].op == "const":
-            if a.args[1].param == idx.param:
+        if a.op == "store":
+            key = a.args[1]
+            if key is idx:
                 return a.args[2]
-            a = a.args[0]
-            continue
+            if idx.op == "const" and key.op == "const":
+                a = a.args[0]
+                continue
+            break
         if a.op == "K":
-            if idx.op == "const":
-                return a.args[0]
+            return a.args[0]
         break
     return Node("select", a.param[-1], (a, idx))
 

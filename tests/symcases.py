@@ -13,7 +13,7 @@ from collections import Counter
 
 import symref
 from mythril_amd import workloads
-from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, LaserEVM, MessageCallTransaction,
+from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, Disassembly, LaserEVM, MessageCallTransaction,
                                SymbolicCalldata, WorldState, execute_contract_creation,
                                execute_symbolic_message_call, generate_contract_address)
 from mythril_amd.laser.transaction import ACTORS, tx_id_manager
@@ -28,9 +28,22 @@ CONTRACTS = {
 }
 
 
+# runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
+# an account at a fixed address with the code and symbolic storage
+# (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o")
+
+
 def deploy(device, name):
-    """Concolic creation (concolic.py:23-72) of a reference test contract;
-    returns (the open world state, the new account's address)."""
+    """Concolic creation (concolic.py:23-72) of a reference test contract (a
+    RUNTIME code: the account holding it, with symbolic storage); returns (the
+    open world state, the account's address)."""
+    if name in RUNTIME:
+        ws = WorldState()
+        ws.put_account(Account(CREATOR, balances=None))
+        acct = Account(workloads.CONTRACT, code=Disassembly(workloads.bytecode(name)), concrete_storage=False)
+        ws.put_account(acct)
+        return ws, workloads.CONTRACT
     args, value = CONTRACTS[name]
     eng = symref.Engine()       # CODESIZE of a creation with arguments escapes: concrete on the oracle
     laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,

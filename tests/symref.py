@@ -32,7 +32,8 @@ from mythril_amd.lanes import (LaneBatch, LaneShape, MG_HALT_DROPPED, MG_HALT_EN
 from mythril_amd.laser.opcodes import ADDRESS_OPCODE_MAPPING
 from mythril_amd.laser.state import Memory, MachineStack
 from mythril_amd.smt.expr import (BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT, URem,
-                                  symbol_factory)
+                                  simplify_concat, symbol_factory)
+from mythril_amd.smt.keccak_manager import keccak_function_manager
 from oracle.evm_ref import OracleEVM
 
 BVV = symbol_factory.BitVecVal
@@ -84,11 +85,17 @@ class Engine:
             cid = self.code_ids[code.bytecode] = self.o.load_code(raw)
         return cid
 
-    def _oracle_step(self, s):
+    def _oracle_run(self, s):
+        """One instruction of the concrete projection of `s` on the oracle
+        (symbolic words, memory bytes and storage read as 0 / empty): its
+        status, pc, gas, depth and memory size are the instruction's whatever
+        the symbolic values are (only symbolic offsets would change them, and
+        those stay Unsupported)."""
         env, ms = s.environment, s.mstate
         stack = [(_val(x) or 0) for x in ms.stack]
         mem = ms.memory.raw()
-        store = env.active_account.storage.printable_storage
+        st = env.active_account.storage
+        store = {} if st.is_chain else st.printable_storage
         shape = LaneShape(n=1, stack_cap=1024, mem_cap=max(4096, (len(mem) + 31) // 32 * 32 + 4096),
                           calldata_cap=32, storage_cap=max(16, 2 * len(store) + 4))
         b = LaneBatch(shape)
@@ -112,24 +119,10 @@ class Engine:
             b.storage[0, k, 8:] = word_to_limbs(val)
         b.storage_count[0] = len(store)
         self.o.run(b, max_steps=1)
+        return b
+
+    def _ended(self, s, b):
         st = int(b.status[0])
-        if st == MG_RUNNING:
-            n = s
-            old = list(ms.stack)
-            new_sp = int(b.sp[0])
-            out = [BVV(limbs_to_word(b.stack[0, k]), 256) for k in range(new_sp)]
-            # words below the instruction's reach keep their (maybe symbolic) objects
-            for k in range(min(new_sp, len(old) - self._touched)):
-                out[k] = old[k]
-            n.mstate.stack = MachineStack(out)
-            n.mstate.pc = int(b.pc[0])
-            n.mstate.memory = Memory(bytes(b.memory[0, :int(b.msize[0])]))
-            n.mstate.depth = int(b.depth[0])
-            n.mstate.min_gas_used, n.mstate.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])
-            store.clear()
-            for k in range(int(b.storage_count[0])):
-                store[limbs_to_word(b.storage[0, k, :8])] = limbs_to_word(b.storage[0, k, 8:])
-            return [n]
         if st == MG_HALT_RETURN:
             s.return_data = bytes(b.memory[0, int(b.ret_offset[0]):int(b.ret_offset[0]) + int(b.ret_len[0])])
         kind = {MG_HALT_STOP: "stop", MG_HALT_RETURN: "return", MG_HALT_REVERT: "revert", MG_VMEXC: "exception",
@@ -137,6 +130,100 @@ class Engine:
         if kind != "dropped":
             self.ended.append((kind, s))
         return []
+
+    def _advance(self, s, b):
+        """pc, gas, depth and memory size of a completed oracle step."""
+        ms = s.mstate
+        ms.pc = int(b.pc[0])
+        ms.depth = int(b.depth[0])
+        ms.min_gas_used, ms.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])
+        grow = int(b.msize[0]) - len(ms.memory)
+        if grow > 0:
+            ms.memory.extend(grow)
+
+    def _oracle_step(self, s):
+        env, ms = s.environment, s.mstate
+        b = self._oracle_run(s)
+        if int(b.status[0]) != MG_RUNNING:
+            return self._ended(s, b)
+        n = s
+        old = list(ms.stack)
+        new_sp = int(b.sp[0])
+        out = [BVV(limbs_to_word(b.stack[0, k]), 256) for k in range(new_sp)]
+        # words below the instruction's reach keep their (maybe symbolic) objects
+        for k in range(min(new_sp, len(old) - self._touched)):
+            out[k] = old[k]
+        n.mstate.stack = MachineStack(out)
+        # memory: the oracle's bytes; symbolic bytes stay unless the instruction
+        # wrote over them (CALLDATACOPY, CODECOPY: the bytes they copied)
+        sym = dict(ms.memory.symbolic_bytes())
+        if sym:
+            name = env.code.instruction_list[ms.pc]["opcode"]
+            lo = n_w = 0
+            if name in ("CALLDATACOPY", "CODECOPY"):
+                lo, src, size = (_val(x) or 0 for x in (old[-1], old[-2], old[-3]))
+                if name == "CALLDATACOPY":
+                    n_w = size
+                else:
+                    code_len = len(env.code.raw)
+                    n_w = min(code_len - src, size) if src < code_len else 0
+            for p in range(lo, lo + n_w):
+                sym.pop(p, None)
+        n.mstate.memory = Memory(bytes(b.memory[0, :int(b.msize[0])]), sym)
+        n.mstate.pc = int(b.pc[0])
+        n.mstate.depth = int(b.depth[0])
+        n.mstate.min_gas_used, n.mstate.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])
+        st = env.active_account.storage
+        if not st.is_chain:
+            st.set_slots({limbs_to_word(b.storage[0, k, :8]): limbs_to_word(b.storage[0, k, 8:])
+                          for k in range(int(b.storage_count[0]))})
+        return [n]
+
+    # ---- memory, storage and SHA3 of a symbolic state ----------------------------
+    def _memstore(self, s, op):
+        """instructions.py:1013-1051 (sha3_), 1437-1518 (mload_ .. sstore_) on the
+        host's Memory / Storage restatements (memory.py, account.py): the
+        oracle's projection decides status, gas and memory size, the values are
+        the reference's expressions."""
+        ms, env = s.mstate, s.environment
+        st = ms.stack
+        if op in (0x20, 0x51, 0x52, 0x53) and _val(st[-1]) is None:
+            raise Unsupported("symbolic memory offset")
+        if op == 0x20 and _val(st[-2]) is None:
+            raise Unsupported("symbolic SHA3 length")
+        b = self._oracle_run(s)
+        if int(b.status[0]) != MG_RUNNING:
+            return self._ended(s, b)
+        self._advance(s, b)
+        storage = env.active_account.storage
+        if op == 0x54:
+            idx = st.pop()
+            st.append(storage[idx])
+        elif op == 0x55:
+            key, value = st.pop(), st.pop()
+            storage[key] = value
+        elif op == 0x51:
+            off = _val(st.pop())
+            st.append(ms.memory.get_word_at(off))
+        elif op == 0x52:
+            off, value = _val(st.pop()), st.pop()
+            ms.memory.write_word_at(off, value)
+        elif op == 0x53:
+            off, value = _val(st.pop()), st.pop()
+            v = _val(value)
+            ms.memory[off] = (v % 256) if v is not None else Extract(7, 0, value)
+        else:
+            off, length = _val(st.pop()), _val(st.pop())
+            data_list = [x if isinstance(x, BitVec) else BVV(x, 8) for x in ms.memory[off: off + length]]
+            if len(data_list) > 1:
+                data = simplify_concat(data_list)
+            elif len(data_list) == 1:
+                data = data_list[0]
+            else:
+                st.append(keccak_function_manager.get_empty_keccak_hash())
+                return [s]
+            st.append(keccak_function_manager.create_keccak(data))
+        return [s]
 
     # ---- one instruction ----------------------------------------------------------
     def step(self, state):
@@ -156,6 +243,9 @@ class Engine:
         symcd = not isinstance(env.calldata, (bytes, bytearray))
         env_attr = _SYM_ENV.get(op)
         sym_env = env_attr is not None and _val(getattr(env, env_attr)) is None
+        if op in (0x20, 0x51, 0x52, 0x53, 0x54, 0x55) and _symbolic_state(s) and len(st) >= _POPS[op]:
+            s.environment.active_account.storage.to_chain()
+            return self._memstore(s, op)
         if name.startswith(("DUP", "SWAP")) or name == "POP" or name.startswith("PUSH"):
             self._touched = reads if not name.startswith("PUSH") else 0
             if name.startswith("DUP") or name.startswith("SWAP"):
@@ -321,6 +411,20 @@ class Engine:
                 nxt.extend(succ)
             work = nxt
         raise RuntimeError("restatement did not finish")
+
+
+def _symbolic_state(s) -> bool:
+    """A state whose memory and storage follow the symbolic restatement (a
+    symbolic lane's): symbolic calldata, environment, stack, memory or storage."""
+    env = s.environment
+    if not isinstance(env.calldata, (bytes, bytearray)) or s.mstate.memory.symbolic:
+        return True
+    if any(_val(getattr(env, a)) is None for a in _SYM_ENV.values()):
+        return True
+    st = env.active_account.storage
+    if not st.concrete or (st.is_chain and any(_val(k) is None or _val(v) is None for k, v in st.chain())):
+        return True
+    return any(_val(x) is None for x in s.mstate.stack)
 
 
 def _gas_limit(s):

@@ -105,9 +105,13 @@ def test_encode_decode_round_trip_and_sharing():
     assert int(c.n_nodes[0]) == 3            # x shared by both operands of x + x
     again = sym.decode_stack(c, 0, s)
     assert [x.raw for x in again] == [x.raw for x in stack]
-    with pytest.raises(sym.NotEncodable):
-        sym.encode_stack(c, 0, [BVS("fresh_from_elsewhere", 256)])
-    assert not sym.lane_eligible(_with_stack(s, [BVS("fresh_from_elsewhere", 256)]))
+    # a term no node produced rides on the lane as an opaque node (MG_SYM_TERM)
+    fresh = [BVS("fresh_from_elsewhere", 256), stack[1] + BVS("fresh_from_elsewhere", 256)]
+    d = _batch()
+    d.sp[0] = 2
+    assert sym.encode_stack(d, 0, fresh)
+    assert [x.raw for x in sym.decode_stack(d, 0, s)] == [x.raw for x in fresh]
+    assert sym.lane_eligible(_with_stack(s, fresh))
     assert sym.lane_eligible(_with_stack(s, stack))
 
 
@@ -145,8 +149,85 @@ def test_jumpi_successors_follow_the_reference():
     assert jump.world_state.constraints[-1].raw is (cond < BVV(3, 256)).raw
 
 
-@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS))
+@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
 def test_symbolic_call_outcomes_equal_the_restatement(name, monkeypatch):
     got, want, laser = symcases.run_both(OracleDevice(), name, monkeypatch)
     assert sum(want.values()) >= 7
     assert got == want
+
+
+# ---- symbolic memory, storage chains and SHA3 (ABI v7) -----------------------------
+def _run_restatement(code_hex, steps):
+    s = _state(code_hex)
+    s.environment.active_account.storage.to_chain()
+    e = symref.Engine()
+    for _ in range(steps):
+        (s,) = e.step(s)
+    return s
+
+
+# PUSH1 4 CALLDATALOAD | PUSH1 0 MSTORE | PUSH1 0x20 PUSH1 0 SHA3 | DUP1 PUSH1 1 SSTORE |
+# SLOAD | PUSH1 0x10 MLOAD | STOP
+_MEMPROG = "600435" "600052" "6020600020" "80600155" "54" "601051" "00"
+
+
+def test_restated_memory_storage_and_sha3_follow_the_reference():
+    s = _run_restatement(_MEMPROG, 13)
+    cd = s.environment.calldata
+    x = cd.get_word_at(BVV(4, 256))
+    from mythril_amd.smt.expr import Concat, Extract, Function, K, Node, _select
+    k = Function("keccak256_256", [256], 256)(x)                 # 32 bytes of one word: x itself
+    chain = Node("store", 0, (K(256, 256, 0).raw, BVV(1, 256).raw, k.raw), (256, 256))
+    sel = _select(chain, k.raw)
+    assert sel.op == "select" and sel.args[0] is chain           # 1 vs k: z3 cannot decide
+    word = Concat(Extract(127, 0, x), BVV(0, 128))               # bytes 16..47: half of x, then zeros
+    assert [w.raw for w in s.mstate.stack] == [sel, word.raw]
+    assert s.mstate.memory.get_word_at(0).raw is x.raw
+    st = s.environment.active_account.storage
+    assert [(a.raw, b.raw) for a, b in st.chain()] == [(BVV(1, 256).raw, k.raw)]
+    assert st[BVV(1, 256)].raw is k.raw and st[k].raw is sel and st[BVV(2, 256)].value == 0
+
+
+def test_lane_encoding_of_memory_and_storage_round_trips():
+    s = _run_restatement(_MEMPROG, 13)
+    le = sym.encode_state(s)
+    assert le.symbolic and le.store is not None and len(le.mem) == 32
+    b = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=64, const_cap=32))
+    le.write(b, 0)
+    b.sp[0] = len(s.mstate.stack)
+    b.msize[0] = len(s.mstate.memory)
+    b.flags[0] = le.flags
+    stack, mem, storage = sym.decode_lane(b, 0, s)
+    assert [w.raw for w in stack] == [w.raw for w in s.mstate.stack]
+    assert {p: e.raw for p, e in mem.symbolic_bytes().items()} == \
+        {p: e.raw for p, e in s.mstate.memory.symbolic_bytes().items()}
+    assert [(a.raw, c.raw) for a, c in storage.chain()] == \
+        [(a.raw, c.raw) for a, c in s.environment.active_account.storage.chain()]
+    assert storage.chain_raw() is s.environment.active_account.storage.chain_raw()
+
+
+def test_device_memory_parts_decode_to_the_reference_word():
+    """The parts kernel 1 builds for a memory read (EXTRACT / CONCAT nodes, a
+    constant run) decode to simplify(Concat(bytes)) of the same bytes."""
+    s = _state()
+    b = _batch()
+    C = MG_SYM_CONST
+    from mythril_amd.lanes import MG_SYM_CONCAT, MG_SYM_EXTRACT, MG_SYM_KECCAK
+    b.cval[0, 0] = word_to_limbs(4)
+    b.cval[0, 1] = word_to_limbs(0xABCD)
+    b.node[0, 0] = (MG_SYM_CDLOAD | 256 << 8, C | 0, 0, 0)
+    b.node[0, 1] = (MG_SYM_EXTRACT | 128 << 8, 0, 0, (127 << 16) | 0)        # bytes 16..31 of x
+    b.node[0, 2] = (MG_SYM_CONCAT | 256 << 8, 1, C | 1, 128 | (128 << 16))   # then 16 bytes 0..0abcd
+    b.node[0, 3] = (MG_SYM_KECCAK | 256 << 8, 2, 0, 256)
+    b.n_nodes[0], b.n_consts[0] = 4, 2
+    b.sp[0] = 2
+    b.stag[0, 0], b.stag[0, 1] = 3, 4
+    word, h = sym.decode_stack(b, 0, s)
+    mem = s.mstate.memory
+    mem.extend(64)
+    x = s.environment.calldata.get_word_at(BVV(4, 256))
+    mem.write_word_at(0, x)
+    mem.write_word_at(32, BVV(0xABCD << 128, 256))           # bytes 32..47 end in ab cd
+    assert word.raw is mem.get_word_at(16).raw
+    from mythril_amd.smt.keccak_manager import KeccakFunctionManager
+    assert h.raw is KeccakFunctionManager().create_keccak(mem.get_word_at(16)).raw
