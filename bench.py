@@ -61,8 +61,11 @@ def parse(argv=None):
     ap.add_argument("--taint-lanes", type=int, default=4096,
                     help="lanes of the taint_c2 field (0: off): C2 through LaserEVM with the integer "
                          "and TxOrigin modules' hooks as device actions (taint lanes) and on the host")
-    ap.add_argument("--symbolic-calls", type=int, default=1024,
-                    help="symbolic message calls of the symbolic-lane field (0: off)")
+    ap.add_argument("--symbolic-replicas", type=int, default=64,
+                    help="replicas of each contract in the symbolic_tx field (0: off)")
+    ap.add_argument("--symbolic-tx", type=int, default=2, help="transactions of the symbolic_tx field (-t)")
+    ap.add_argument("--seed-models", type=int, default=1024,
+                    help="witness seed models beside the LRU cache in the symbolic_tx field")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
@@ -221,9 +224,10 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         taint = run_taint_c2(dev, args.taint_lanes, rank)
 
     symb = None
-    if args.symbolic_calls and gpu and not args.profile_only:
-        _log(rank, f"symbolic calls ({args.symbolic_calls})")
-        symb = run_symbolic(dev, args.symbolic_calls)
+    if args.symbolic_replicas and gpu and not args.profile_only:
+        _log(rank, f"symbolic transactions (-t {args.symbolic_tx}, {args.symbolic_replicas} replicas)")
+        symb = run_symbolic_tx(dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models,
+                               log=lambda m: _log(rank, m))
 
     c4 = None
     if not args.no_c4:
@@ -277,7 +281,7 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         if taint is not None:
             out["taint_c2"] = taint
         if symb is not None:
-            out["symbolic_calls"] = symb
+            out["symbolic_tx"] = symb
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
@@ -487,51 +491,101 @@ def run_large(dev, args, rank, barrier):
             "code": "tests/golden/disassembly.json (disassembler_test.py:8-10)"}
 
 
-def run_symbolic(dev, n_calls):
-    """Symbolic lanes: n symbolic message calls
-    (transaction/symbolic.py:105-150) into the reference's flag_array contract
-    (deployed concretely with 0.1 ether) through the batched LaserEVM (BFS):
-    the device builds the calldata / call value expressions and stops at
-    every symbolic JUMPI, the host forks (fork filter off: no SMT solver here)
-    and re-packs the successors.  The SLOAD of a symbolic key escapes; with no
-    handler here that path ends.  Reports paths, forks, lane-steps and the
-    host/device split."""
-    from mythril_amd import workloads
-    from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, LaserEVM, WorldState,
-                                   execute_contract_creation, execute_symbolic_message_call)
-    from mythril_amd.laser.transaction import ACTORS
-    from mythril_amd.smt import solver
-    creator = ACTORS["CREATOR"]
-    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
-    ws = WorldState()
-    ws.put_account(Account(creator))
-    laser.open_states = [ws]
-    execute_contract_creation(laser, None, creator, creator, workloads.bytecode("flag_array.sol.o"),
-                              8_000_000, 1, 10 ** 17)        # require(msg.value == 0.1 ether)
-    if len(laser.open_states) != 1:
-        return {"error": "deployment did not complete"}
-    base = laser.open_states[0]
-    addr = next(a for a in base.accounts if a != creator)
+SYMBOLIC_TX_CODES = ("overflow.sol.o", "exceptions.sol.o", "flag_array.sol.o")
+
+
+def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_handler=None, log=None):
+    """C3 in situ (BASELINE configs[2] needs solc for BECToken; the reference's
+    own precompiled contracts stand in): `-t tx_count` symbolic transactions
+    (svm.py:214-275, transaction/symbolic.py:105-150) through the batched
+    LaserEVM with the fork filter ON (svm.py:319-326) and the per-transaction
+    reachability filter (svm.py:244-249).  Symbolic lanes run on kernel 1
+    (store chains, symbolic memory, symbolic SHA3); every fork filter group and
+    reachability round is one kernel-2 launch over the model cache plus
+    `n_seeds` witness seeds (laser/witness.py).  No SMT backend exists in the
+    image, so a query no candidate satisfies is an UNKNOWN and its path is kept
+    (mode "prefilter-only"); escaped paths (no host handler) are dropped and
+    counted.  Runtime codes are analysed as `myth analyze -f` does (symbolic
+    storage); flag_array is deployed concretely first.  `replicas` copies of the
+    deployed world state run together (one contract per replica, independent
+    paths) for a batch that fills the GPU; replicas=1 is one analysis."""
     from copy import copy
-    old = solver.args.pruning_factor
-    solver.args.pruning_factor = 0
+    from mythril_amd import workloads
+    from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, Disassembly, LaserEVM, WorldState,
+                                   execute_contract_creation)
+    from mythril_amd.laser.transaction import ACTORS, tx_id_manager
+    from mythril_amd.laser.witness import WitnessSeeds
+    from mythril_amd.smt import solver
+    from mythril_amd.smt.keccak_manager import keccak_function_manager
+    creator = ACTORS["CREATOR"]
+    out = {"metric": "in-situ constraint-evals/s of the fork and reachability filters (kernel 2) "
+                     "+ symbolic lane-steps/s (kernel 1)",
+           "mode": "prefilter-only: no SMT backend in the image; queries no candidate satisfies "
+                   "are UNKNOWN and their paths kept; escaped paths dropped (counted)",
+           "transactions": tx_count, "replicas": replicas, "seed_models": n_seeds, "contracts": {}}
+    saved_cache = solver.model_cache
     try:
-        laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
-        ends = [0]
-        laser.register_laser_hooks("transaction_end", lambda *a: ends.__setitem__(0, ends[0] + 1))
-        laser.open_states = [copy(base) for _ in range(n_calls)]
-        t0 = time.perf_counter()
-        execute_symbolic_message_call(laser, addr)
-        wall = time.perf_counter() - t0
+        for name in SYMBOLIC_TX_CODES:
+            keccak_function_manager.reset()
+            tx_id_manager.restart_counter()
+            solver.get_model.cache_clear()
+            code = workloads.bytecode(name)
+            ws = WorldState()
+            ws.put_account(Account(creator))
+            if name == "flag_array.sol.o":
+                laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+                laser.open_states = [ws]
+                execute_contract_creation(laser, None, creator, creator, code, 8_000_000, 1, 10 ** 17)
+                if len(laser.open_states) != 1:
+                    out["contracts"][name] = {"error": "deployment did not complete"}
+                    continue
+                ws = laser.open_states[0]
+                addr = next(a for a in ws.accounts if a != creator)
+            else:
+                addr = workloads.CONTRACT
+                ws.put_account(Account(addr, code=Disassembly(code), concrete_storage=False))
+            mc = solver.ModelCache(device=dev)
+            seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"])
+            mc.seed_source = seeds
+            solver.model_cache = mc
+            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+                             transaction_count=tx_count, escape_handler=escape_handler)
+            laser.unknown_forks = "keep"
+            if log:
+                log(f"symbolic_tx {name}")
+                laser.register_laser_hooks("start_sym_trans", lambda: log(
+                    f"symbolic_tx {name}: transaction with {len(laser.open_states)} open states"))
+            ends = {"return_or_stop": 0, "revert": 0}
+            laser.register_laser_hooks("transaction_end", lambda s, tx, r, revert: ends.__setitem__(
+                "revert" if revert else "return_or_stop", ends["revert" if revert else "return_or_stop"] + 1))
+            laser.open_states = [copy(ws) for _ in range(replicas)]
+            t0 = time.perf_counter()
+            laser.execute_transactions(addr)
+            wall = time.perf_counter() - t0
+            k1_s, k2_s = laser.device_ms / 1e3, mc.device_ms / 1e3
+            st = mc.stats
+            answered = st["lru_hits"] + st["seed_hits"]
+            out["contracts"][name] = {
+                "wall_s": wall, "kernel1_s": k1_s, "kernel2_s": k2_s, "host_s": wall - k1_s - k2_s,
+                "lane_steps": int(laser.lane_steps), "lane_steps_per_s": laser.lane_steps / wall,
+                "launches_kernel1": int(laser.launches), "forks": laser.forks,
+                "tx_ends": ends, "open_states": len(laser.open_states),
+                "escapes_dropped": laser.escapes_dropped,
+                "fork_filter": dict(laser.fork_stats),
+                "queries": st["queries"], "lru_hits": st["lru_hits"], "seed_hits": st["seed_hits"],
+                "unknown": st["misses"],
+                "prefilter_hit_rate": answered / st["queries"] if st["queries"] else None,
+                "constraint_evals": int(mc.device_evals), "launches_kernel2": int(mc.launches),
+                "constraint_evals_per_s_kernel": mc.device_evals / k2_s if k2_s else None,
+                "constraint_evals_per_s_wall": mc.device_evals / wall,
+                "keccak_symbolic_inputs": sum(len(v) for v in keccak_function_manager.symbolic_inputs.values()),
+            }
     finally:
-        solver.args.pruning_factor = old
-    dev_s = laser.device_ms / 1e3
-    return {"metric": "symbolic lane-steps/s (symbolic message calls, kernel 1 + host forks)",
-            "calls": n_calls, "contract": "flag_array.sol.o",
-            "paths_ended": ends[0], "open_states": len(laser.open_states), "forks": laser.forks,
-            "lane_steps": int(laser.lane_steps), "launches": int(laser.launches), "wall_s": wall,
-            "device_s": dev_s, "host_s": wall - dev_s, "lane_steps_per_s": laser.lane_steps / wall,
-            "forks_per_s": laser.forks / wall}
+        solver.model_cache = saved_cache
+        keccak_function_manager.reset()
+        tx_id_manager.restart_counter()
+        solver.get_model.cache_clear()
+    return out
 
 
 def run_c4(args, dev, rank, world, barrier, dist_on):

@@ -58,7 +58,8 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import Expression, symbol_factory
 from ..smt.keccak_manager import keccak_function_manager
-from ..smt.solver import Constraints, args
+from ..smt import solver as solver_mod
+from ..smt.solver import Constraints, SnapshotConstraints, SolverBackendMissing, args, query_raw
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, Memory, MachineStack, concrete
@@ -168,6 +169,7 @@ class LaserEVM:
         self.launches = 0
         self._exec_stop = False
         self.forks = 0                      # symbolic JUMPIs the device stopped at (MG_FORK)
+        self.escapes_dropped = 0            # escaped states dropped for want of an escape handler
         self.regrows = 0                    # capacity escapes resumed in a regrown batch
         self._code_ids: Dict[bytes, int] = {}
         self._code_objs: Dict[bytes, object] = {}
@@ -183,6 +185,14 @@ class LaserEVM:
         self.track_objects = False
         self._plan: Optional[tnt.TaintPlan] = None
         self._tl: Optional[List[tnt.LaneTaint]] = None
+        # fork filters of consecutive MG_FORK events, evaluated together (one
+        # kernel-2 launch per group) before anything else can observe them
+        self._pending_forks: List = []
+        # a fork-filter query no quick-sat candidate answers and no SMT backend
+        # can decide: "raise" (SolverBackendMissing) or "keep" the successor
+        # (prefilter-only runs: the image has no solver; counted in fork_stats)
+        self.unknown_forks = "raise"
+        self.fork_stats = {"groups": 0, "queries": 0, "kept": 0, "pruned": 0, "unknown": 0, "flushes": 0}
         log.info("LASER EVM (MI355X batched core) initialized")
 
     # ------------------------------------------------------------- device
@@ -242,6 +252,50 @@ class LaserEVM:
             hook()
         return final_states if track_gas else None
 
+    # ------------------------------------------------------------- transactions
+    def execute_transactions(self, address) -> None:
+        """svm.py:214-228: plugins may order transactions themselves
+        (executed_transactions); otherwise transaction_count symbolic message
+        calls."""
+        for hook in self._start_exec_trans_hooks:
+            hook()
+        if self.executed_transactions is False:
+            self._execute_transactions(address)
+        for hook in self._stop_exec_trans_hooks:
+            hook()
+
+    def _execute_transactions(self, address) -> None:
+        """svm.py:230-275: per transaction, the open states whose constraints
+        are still possible (all queries of the round in one kernel-2 launch,
+        answered in order), then one symbolic message call per open state."""
+        from .transaction import execute_symbolic_message_call
+        self.time = datetime.now()
+        for _ in range(self.transaction_count):
+            if len(self.open_states) == 0:
+                break
+            if self.use_reachability_check:
+                self.open_states = self.reachable(self.open_states)
+            for hook in self._start_sym_trans_hooks:
+                hook()
+            execute_symbolic_message_call(self, address)
+            for hook in self._stop_sym_trans_hooks:
+                hook()
+        self.executed_transactions = True
+
+    def reachable(self, world_states: list) -> list:
+        """[ws for ws in world_states if ws.constraints.is_possible()] with the
+        queries prefetched together (svm.py:244-249)."""
+        self._flush_forks()
+        if not world_states:
+            return []
+        kc = keccak_function_manager.create_conditions()
+        qs = [SnapshotConstraints(ws.constraints, kc) for ws in world_states]
+        solver_mod.model_cache.prefetch([query_raw(q.get_all_constraints()) for q in qs])
+        try:
+            return [ws for ws, q in zip(world_states, qs) if self._possible(q)]
+        finally:
+            solver_mod.model_cache.clear_prefetch()
+
     def _host_only(self, states, final_states, track_gas):
         """States a lane cannot carry (a symbolic word the expression arena has
         no node for, symbolic storage or memory) take one step with the escape
@@ -253,6 +307,7 @@ class LaserEVM:
             if sym.lane_eligible(st):
                 keep.append(st)
                 continue
+            self._flush_forks()
             if self.escape_handler is None:
                 log.debug("state not representable on a lane and no escape handler: dropped")
                 continue
@@ -267,9 +322,55 @@ class LaserEVM:
     def _filter_fork(self, new_states: list) -> None:
         """svm.py:319-326: a fork keeps the successors whose path constraints are
         possible (kernel-2 quick-sat over the model cache, then the backend)."""
+        self._flush_forks()
         if self.strategy.run_check() and (len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
             new_states[:] = [st for st in new_states
-                             if Constraints(st.world_state.constraints).is_possible()]
+                             if self._possible(Constraints(st.world_state.constraints))]
+
+    def _possible(self, constraints) -> bool:
+        self.fork_stats["queries"] += 1
+        try:
+            ok = constraints.is_possible()
+        except SolverBackendMissing:
+            if self.unknown_forks != "keep":
+                raise
+            self.fork_stats["unknown"] += 1
+            ok = True
+        self.fork_stats["kept" if ok else "pruned"] += 1
+        return ok
+
+    def _queue_fork(self, s: GlobalState, new_states: list, track_gas: bool, final_states: list) -> None:
+        """svm.py:319-326 for an MG_FORK event, deferred: the decision to filter
+        (and its random draw) and each successor's query -- the keccak conjunct
+        as of now -- are taken here; the queries of consecutive forks are then
+        evaluated together (_flush_forks) in the same order, so answers and
+        model-cache moves are the sequential loop's."""
+        queries = None
+        if self.strategy.run_check() and (len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
+            kc = keccak_function_manager.create_conditions()
+            queries = [SnapshotConstraints(st.world_state.constraints, kc) for st in new_states]
+        self._pending_forks.append((s, new_states, queries, track_gas, final_states))
+
+    def _flush_forks(self) -> None:
+        pend = self._pending_forks
+        if not pend:
+            return
+        self._pending_forks = []
+        raws = [query_raw(q.get_all_constraints()) for _, _, qs, _, _ in pend if qs for q in qs]
+        self.fork_stats["flushes"] += 1
+        self.fork_stats["groups"] += len(pend)
+        if raws:
+            solver_mod.model_cache.prefetch(raws)
+        try:
+            for s, new_states, qs, track_gas, final_states in pend:
+                if qs is not None:
+                    new_states = [st for st, q in zip(new_states, qs) if self._possible(q)]
+                self.work_list.extend(new_states)
+                self.total_states += len(new_states)
+                if not new_states and track_gas:
+                    final_states.append(s)
+        finally:
+            solver_mod.model_cache.clear_prefetch()
 
     def _add_world_state(self, global_state: GlobalState) -> None:
         """svm.py:339-348."""
@@ -618,7 +719,7 @@ class LaserEVM:
             # nearby ranges merge into one call (the fixed cost per call is far
             # above the per-lane bytes of a gap)
             for lo, cnt in _ranges(sorted(sched.dirty), gap=_MERGE_GAP):
-                dev.upload_range(b, lo, cnt)
+                dev.upload_range(sched.b, lo, cnt)
                 for pos in range(lo, lo + cnt):
                     lanes[pos].dirty = False
             sched.dirty.clear()
@@ -636,12 +737,19 @@ class LaserEVM:
             self.lane_steps += st.lane_steps
             self.total_states += st.lane_steps      # one successor per executed step
             for lo, cnt in _ranges(run, gap=_MERGE_GAP):
-                dev.download_range(b, lo, cnt)
-            self._collect_records(b, run)
+                dev.download_range(sched.b, lo, cnt)
+            self._collect_records(sched.b, run)
             for i in run:
-                sched.set(i, "paused" if b.status[i] == MG_RUNNING else "event")
+                sched.set(i, "paused" if sched.b.status[i] == MG_RUNNING else "event")
 
         launch(list(range(n)), 0)
+        try:
+            return self._event_loop(b, lanes, sched, launch, final_states, create, track_gas, single_step, regrow)
+        finally:
+            self._flush_forks()
+
+    def _event_loop(self, b, lanes, sched, launch, final_states, create, track_gas, single_step, regrow):
+        bfs = sched.bfs
         while True:
             if (create and self._check_create_termination()) or (
                     not create and self._check_execution_termination()):
@@ -651,6 +759,7 @@ class LaserEVM:
                 return left
             ev = sched.next_event()
             if single_step:
+                self._flush_forks()
                 for i in sorted(sched.paused):
                     ln = lanes[i]
                     self._materialise(b, i, ln.state)
@@ -678,6 +787,7 @@ class LaserEVM:
                     b = sched.b = grown
                     regrow.clear()
         self._replay_records(lanes)
+        self._flush_forks()
         if regrow:
             self._cap_grow *= 4
             self.work_list.extend(ln.state for ln, _ in regrow)
@@ -740,6 +850,8 @@ class LaserEVM:
         """Run the host side of one device event, as execute_state would."""
         i, s = ln.pos, ln.state
         status = int(b.status[i])
+        if status != MG_FORK:
+            self._flush_forks()        # queued fork filters come first (reference order)
         self._materialise(b, i, s)
         instrs = s.environment.code.instruction_list
         name = instrs[s.mstate.pc]["opcode"] if s.mstate.pc < len(instrs) else None
@@ -897,12 +1009,8 @@ class LaserEVM:
                     if track_gas:
                         final_states.append(s)
                     return
-            new_states = sym.jumpi_successors(s)
-            self._filter_fork(new_states)
-            self.work_list.extend(new_states)
-            self.total_states += len(new_states)
-            if new_states or not track_gas:
-                return
+            self._queue_fork(s, sym.jumpi_successors(s), track_gas, final_states)
+            return
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
             if reason in (MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE, MG_ESC_RECORD,
@@ -917,6 +1025,7 @@ class LaserEVM:
                 return
             if self.escape_handler is None:
                 log.debug("Encountered unimplemented instruction %s", name)
+                self.escapes_dropped += 1
                 return              # svm.py:314-316: NotImplementedError -> continue
             new_states = self.escape_handler(s)
             self._filter_fork(new_states)

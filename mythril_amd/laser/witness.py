@@ -1,0 +1,270 @@
+"""Witness seeds: concrete transaction inputs as candidate models for kernel 2.
+
+The reference's quick-sat (support_utils.py:34-68) can only answer with one of
+the <= 100 models its SMT backend returned earlier.  Kernel 2 evaluates
+thousands of candidates per constraint set for the price of a few, so a pool of
+*concrete transaction inputs* -- the calldata, sender, call value and initial
+storage a concrete run of the contract would use -- proves "SAT" for every path
+such an input drives, before any solver is asked (the prefilter
+may only answer SAT with a model; a miss falls through unchanged).  The pool is
+consulted only where get_model would call the backend (solver.ModelCache
+.check_seeds), and a seed it returns is checked against the whole query, the
+keccak conjunct included, on the device.
+
+A seed assigns, for every symbolic transaction id N the queries mention,
+``N_calldata`` (a byte array: a dispatcher selector of the code, then argument
+words drawn from zero / small / actor address / random address / random word /
+all-ones), ``N_calldatasize``, ``sender_N`` (one of the ACTORS,
+transaction/symbolic.py:28-40), ``call_valueN`` (mostly 0) and ``gas_priceN``;
+the symbolic storage arrays start at 0.  Keccak functions are completed per
+seed so the KeccakFunctionManager axioms hold (keccak_function_manager.py:
+116-179): each registered symbolic input x evaluates under the seed to v, and
+keccak256_N(v) is keccak(c) when v is a registered concrete input c, else a
+fresh multiple of 64 inside N's interval, with the inverse mapping back; and
+Power is the true power at every concrete EXP registered (the constraints
+exponent_function_manager.py:32-60 adds, with its 256**i table).
+"""
+from __future__ import annotations
+
+import re
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import numpy as np
+
+from ..smt.expr import Node
+from ..smt.keccak_manager import PART, KeccakFunctionManager, keccak_function_manager
+from ..smt.program import ArrayInterp, FuncInterp
+from ..smt.solver import Model, ModelRef
+from .transaction import ACTORS
+
+M256 = (1 << 256) - 1
+_TX_VAR = re.compile(r"^(?:sender_(\d+)|call_value(\d+)|gas_price(\d+)|(\d+)_calldata(?:size)?)$")
+
+
+def dispatch_selectors(code: bytes) -> List[int]:
+    """The 4-byte constants a Solidity dispatcher compares the selector with
+    (PUSH4 x; EQ)."""
+    out, k = [], 0
+    while k < len(code):
+        op = code[k]
+        if op == 0x63 and k + 6 <= len(code) and code[k + 5] == 0x14:
+            out.append(int.from_bytes(code[k + 1:k + 5], "big"))
+        k += 1 + (op - 0x5F if 0x60 <= op <= 0x7F else 0)
+    return sorted(set(out))
+
+
+class WitnessSeeds:
+    """A fixed pool of `n` seed models over the transactions the queries name.
+
+    ``models()`` returns the pool as solver Models, extended with the
+    variables of newly seen transaction ids and completed for the keccak
+    inputs registered so far (incrementally: values already computed are
+    kept)."""
+
+    def __init__(self, codes: Sequence[bytes], n: int = 1024, seed: int = 0x5EED5EED,
+                 storage_names: Iterable[str] = (), manager: KeccakFunctionManager = keccak_function_manager):
+        self.n = n
+        self.rng = np.random.default_rng(seed)
+        sel = []
+        for c in codes:
+            sel.extend(dispatch_selectors(bytes(c)))
+        self.selectors = sorted(set(sel)) or [0]
+        self.storage_names = list(storage_names)
+        self.km = manager
+        self.assign: List[Dict[str, object]] = [{} for _ in range(n)]
+        for a in self.assign:
+            for name in self.storage_names:
+                a[name] = ArrayInterp(0, {})
+        self.tx_ids: List[str] = []
+        self._done: List[Dict[Node, int]] = [{} for _ in range(n)]   # keccak input -> value, per seed
+        self._next: List[Dict[int, int]] = [{} for _ in range(n)]    # next free slot per input size
+        self._models: Optional[List[Model]] = None
+        self._epoch = None
+        self._rev: Dict[str, int] = {}           # interpretation changes per name (PoolColumns)
+
+    def revision(self, name: str) -> int:
+        return self._rev.get(name, 0)
+
+    def _touch(self, name: str) -> None:
+        self._rev[name] = self._rev.get(name, 0) + 1
+
+    # -- transactions ------------------------------------------------------------------
+    def add_tx(self, txid: str) -> None:
+        if txid in self.tx_ids:
+            return
+        self.tx_ids.append(txid)
+        actors = list(ACTORS.values())
+        r = self.rng
+        for m, a in enumerate(self.assign):
+            nargs = int(r.integers(0, 4))
+            data = bytearray()
+            if r.random() < 0.9:
+                data += self.selectors[int(r.integers(0, len(self.selectors)))].to_bytes(4, "big")
+            else:
+                data += bytes(r.integers(0, 256, 4, dtype=np.uint8))
+            for _ in range(nargs):
+                data += self._arg(actors).to_bytes(32, "big")
+            if r.random() < 0.05 and data:
+                data = data[:int(r.integers(0, len(data)))]
+            a[f"{txid}_calldata"] = ArrayInterp(0, {k: b for k, b in enumerate(data)})
+            a[f"{txid}_calldatasize"] = len(data)
+            a[f"sender_{txid}"] = actors[m % len(actors)]
+            a[f"call_value{txid}"] = 0 if r.random() < 0.85 else int(r.integers(1, 1 << 20))
+            a[f"gas_price{txid}"] = int(r.integers(0, 1 << 40))
+
+    def _arg(self, actors) -> int:
+        r = self.rng
+        u = r.random()
+        if u < 0.15:
+            return 0
+        if u < 0.40:
+            return int(r.integers(0, 1 << 16))
+        if u < 0.60:
+            return actors[int(r.integers(0, len(actors)))]
+        if u < 0.75:
+            return int.from_bytes(bytes(r.integers(0, 256, 20, dtype=np.uint8)), "big")
+        if u < 0.90:
+            return int.from_bytes(bytes(r.integers(0, 256, 32, dtype=np.uint8)), "big")
+        return M256
+
+    def note_query_vars(self, names: Iterable[str]) -> None:
+        for name in names:
+            mt = _TX_VAR.match(name)
+            if mt:
+                self.add_tx(next(g for g in mt.groups() if g is not None))
+
+    # -- keccak completion --------------------------------------------------------------
+    def _complete(self) -> None:
+        km = self.km
+        inputs = [x for xs in km.symbolic_inputs.values() for x in xs]
+        concrete = {}
+        for c, h in km.concrete_hashes.items():
+            concrete[(c.size(), c.value)] = h.value
+        if inputs:
+            km.create_conditions()          # assigns the intervals in the reference's order
+        from ..smt.exponent_manager import exponent_function_manager
+        power = exponent_function_manager.concrete_points
+        self._touch("Power")
+        for (n, _), _h in concrete.items():
+            self._touch(f"keccak256_{n}")
+            self._touch(f"keccak256_{n}-1")
+        for x in inputs:
+            self._touch(f"keccak256_{x.size()}")
+            self._touch(f"keccak256_{x.size()}-1")
+        for m, a in enumerate(self.assign):
+            pw = a.setdefault("Power", FuncInterp(0, {}))
+            for (b, e), v in power.items():
+                pw.entries.setdefault((b, e), v)
+            for (n, cv), h in concrete.items():
+                a.setdefault(f"keccak256_{n}", FuncInterp(0, {})).entries.setdefault((cv,), h)
+                a.setdefault(f"keccak256_{n}-1", FuncInterp(0, {})).entries.setdefault((h,), cv)
+        # inputs in registration order (an input may hash an earlier one's hash):
+        # each evaluated under every seed at once, then entered into the seeds'
+        # keccak tables
+        for x in inputs:
+            n = x.size()
+            todo = [m for m in range(self.n) if x.raw not in self._done[m]]
+            if not todo:
+                continue
+            vals = eval_all(x.raw, [self.assign[m] for m in todo])
+            for m, v in zip(todo, vals):
+                self._done[m][x.raw] = v
+                a, nxt = self.assign[m], self._next[m]
+                f = a.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
+                inv = a.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
+                if (v,) in f.entries:
+                    continue
+                h = concrete.get((n, v))
+                if h is None:
+                    k = nxt.get(n, 0) + 1
+                    nxt[n] = k
+                    lo = km.interval_hook_for_size.get(n, 0) * PART
+                    h = (lo + 63) // 64 * 64 + 64 * (k - 1)     # in [lo, lo + PART), % 64 == 0
+                f.entries[(v,)] = h
+                inv.entries[(h,)] = v
+
+    @property
+    def epoch(self):
+        return self._epoch
+
+    def models(self) -> List[Model]:
+        """The pool, covering every transaction id issued so far.  The Model
+        objects keep their identity (the model cache's LRU holds seeds it
+        returned): completion only adds entries, so every query a seed answered
+        before stays answered."""
+        from .transaction import tx_id_manager
+        for k in range(1, int(tx_id_manager._next_transaction_id) + 1):
+            self.add_tx(str(k))
+        from ..smt.exponent_manager import exponent_function_manager
+        epoch = (len(self.tx_ids), sum(len(v) for v in self.km.symbolic_inputs.values()),
+                 len(self.km.concrete_hashes), len(exponent_function_manager.concrete_points))
+        if self._models is None or epoch != self._epoch:
+            self._complete()
+            if self._models is None:
+                self._models = []
+                for a in self.assign:
+                    ref = ModelRef()
+                    ref.assignment = a          # shared: completion updates it in place
+                    self._models.append(Model([ref]))
+            self._epoch = epoch
+        return self._models
+
+
+def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
+    """Value of a bit-vector / Bool term under every assignment (model
+    completion: absent variables 0, arrays and functions their default /
+    else value), one pass over the DAG with a value list per node."""
+    from ..smt.semantics import apply_op
+    n = len(assigns)
+    memo: Dict[int, object] = {}
+
+    def arr(node):
+        """Per model: (default, {index: value}) of an array term."""
+        got = memo.get(id(node))
+        if got is not None:
+            return got
+        if node.op == "array":
+            name = node.param[0]
+            out = []
+            for a in assigns:
+                it = a.get(name)
+                out.append((it.default, it.entries) if isinstance(it, ArrayInterp) else (0, {}))
+        elif node.op == "K":
+            d = val(node.args[0])
+            out = [(d[m], {}) for m in range(n)]
+        elif node.op == "store":
+            base, idx, v = arr(node.args[0]), val(node.args[1]), val(node.args[2])
+            out = [(base[m][0], {**base[m][1], idx[m]: v[m]}) for m in range(n)]
+        else:
+            raise ValueError(f"array term {node.op}")
+        memo[id(node)] = out
+        return out
+
+    def val(node):
+        got = memo.get(id(node))
+        if got is not None:
+            return got
+        op = node.op
+        if op == "const":
+            out = [node.param] * n
+        elif op == "var":
+            out = [(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns]
+        elif op == "select":
+            ar, idx = arr(node.args[0]), val(node.args[1])
+            out = [ar[m][1].get(idx[m], ar[m][0]) for m in range(n)]
+        elif op == "uf":
+            args = [val(x) for x in node.args]
+            name = node.param[0]
+            out = []
+            for m, a in enumerate(assigns):
+                it = a.get(name)
+                key = tuple(col[m] for col in args)
+                out.append(it.entries.get(key, it.else_value) if isinstance(it, FuncInterp) else 0)
+        else:
+            args = [val(x) for x in node.args]
+            ws = [x.width for x in node.args]
+            out = [apply_op(op, node.width, [col[m] for col in args], ws, node.param) for m in range(n)]
+        memo[id(node)] = out
+        return out
+
+    return val(raw)

@@ -18,6 +18,9 @@ from .expr import And, BitVec, Bool, Function, URem, symbol_factory
 
 class ExponentFunctionManager:
     def __init__(self):
+        # concrete (base, exponent) -> power of every EXP registered so far (what
+        # a model must interpret Power as; laser/witness.py completes seeds with it)
+        self.concrete_points = {(256, i): 256 ** i for i in range(32)}
         power = Function("Power", [256, 256], 256)
         n256 = symbol_factory.BitVecVal(256, 256)
         self.concrete_constraints = And(*[
@@ -30,6 +33,7 @@ class ExponentFunctionManager:
         if exponent.symbolic is False and base.symbolic is False:
             const = symbol_factory.BitVecVal(pow(base.value, exponent.value, 2 ** 256), 256,
                                              annotations=base.annotations.union(exponent.annotations))
+            self.concrete_points[(base.value, exponent.value)] = const.value
             return const, const == exponentiation
         constraint = And(exponentiation > 0, self.concrete_constraints)
         if base.value == 256:

@@ -177,3 +177,96 @@ class ModelPool:
 
 def limbs(x: int) -> np.ndarray:
     return np.frombuffer((x & ((1 << 256) - 1)).to_bytes(32, "little"), dtype="<u4").copy()
+
+
+def concat_pools(a: ModelPool, b: ModelPool) -> ModelPool:
+    """Pool a's models followed by pool b's (same variables and tables)."""
+    out = ModelPool(np.concatenate([a.values, b.values], axis=1))
+    if a.n_tables:
+        shift = np.uint32(a.tab_entries.shape[0])
+        out.tab_start = np.concatenate([a.tab_start, b.tab_start + shift], axis=1)
+        out.tab_count = np.concatenate([a.tab_count, b.tab_count], axis=1)
+        out.tab_entries = np.concatenate([a.tab_entries, b.tab_entries], axis=0)
+        out.tab_default = np.concatenate([a.tab_default, b.tab_default], axis=1)
+    return out
+
+
+class PoolColumns:
+    """A fixed list of model assignments, laid out once per variable and per
+    table: ``pool(var_names, var_widths, tables)`` assembles a ModelPool from
+    cached columns (the witness seeds are rebuilt only when they change)."""
+
+    def __init__(self, assigns: List[Dict[str, object]], revision=None):
+        self.assigns = assigns
+        self._vars: Dict[tuple, np.ndarray] = {}
+        self._tabs: Dict[tuple, tuple] = {}
+        # revision(name) -> a value that changes whenever any assignment's
+        # interpretation of `name` changes (None: interpretations never change)
+        self.revision = revision or (lambda name: 0)
+
+    def _var(self, name: str, w: int) -> np.ndarray:
+        col = self._vars.get((name, w))
+        if col is None:
+            raw = bytearray()
+            for a in self.assigns:
+                x = a.get(name, 0)
+                x = (x if isinstance(x, int) else 0) & ((1 << w) - 1)
+                raw += x.to_bytes(32, "little")
+            col = self._vars[(name, w)] = np.frombuffer(bytes(raw), dtype="<u4").reshape(-1, 8).astype(np.uint32)
+        return col
+
+    def _tab(self, sig) -> tuple:
+        key = (sig.name, sig.kind, sig.domain, sig.range)
+        rev = self.revision(sig.name)
+        got = self._tabs.get(key)
+        if got is None or got[0] != rev:
+            nm = len(self.assigns)
+            start = np.zeros(nm, dtype=np.uint32)
+            count = np.zeros(nm, dtype=np.uint32)
+            dflt = bytearray()
+            rows = bytearray()
+            n_rows = 0
+            M256_, M512_ = (1 << 256) - 1, (1 << 512) - 1
+            for m, a in enumerate(self.assigns):
+                interp = a.get(sig.name)
+                start[m] = n_rows
+                if isinstance(interp, ArrayInterp):
+                    d = interp.default
+                    items = [((k,), v) for k, v in interp.entries.items()]
+                elif isinstance(interp, FuncInterp):
+                    d = interp.else_value
+                    items = interp.entries.items()
+                else:
+                    d, items = 0, ()
+                dflt += (d & M512_).to_bytes(64, "little")
+                for args, v in items:
+                    k0, k1 = sig.key_chunks(tuple(args))
+                    rows += (k0 & M256_).to_bytes(32, "little") + (k1 & M256_).to_bytes(32, "little") + \
+                        (v & M512_).to_bytes(64, "little")
+                    n_rows += 1
+                count[m] = n_rows - start[m]
+            entries = np.frombuffer(bytes(rows), dtype="<u4").reshape(-1, 32).astype(np.uint32)
+            default = np.frombuffer(bytes(dflt), dtype="<u4").reshape(nm, 16).astype(np.uint32)
+            got = self._tabs[key] = (rev, (start, count, entries, default))
+        return got[1]
+
+    def pool(self, var_names: List[str], var_widths: List[int], tables: Optional[List] = None) -> ModelPool:
+        nm = len(self.assigns)
+        vals = np.zeros((max(len(var_names), 1), max(nm, 1), 8), dtype=np.uint32)
+        for v, (name, w) in enumerate(zip(var_names, var_widths)):
+            vals[v, :nm] = self._var(name, w)
+        out = ModelPool(vals)
+        if tables:
+            parts = [self._tab(sig) for sig in tables]
+            starts, counts, defaults, ents, off = [], [], [], [], 0
+            for st, ct, en, df in parts:
+                starts.append(st + np.uint32(off))
+                counts.append(ct)
+                defaults.append(df)
+                ents.append(en)
+                off += en.shape[0]
+            out.tab_start = np.stack(starts)
+            out.tab_count = np.stack(counts)
+            out.tab_default = np.stack(defaults)
+            out.tab_entries = np.concatenate(ents, axis=0) if off else np.zeros((0, 32), dtype=np.uint32)
+        return out

@@ -38,7 +38,7 @@ import numpy as np
 
 from .expr import And, BitVec, Bool, Node, TRUE, _fold, _select, const, symbol_factory
 from .flatten import compile_sets
-from .program import ArrayInterp, FuncInterp, ModelPool
+from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, concat_pools
 
 NO_MODEL = 0xFFFFFFFF
 
@@ -239,6 +239,17 @@ class ModelCache:
         self._fresh: List = []          # models this rank found since the last exchange
         self.device_evals = 0          # constraint-evals run on kernel 2
         self.launches = 0
+        self.device_ms = 0.0           # kernel-2 time of those launches
+        # candidate models beyond the LRU (witness seeds, SURVEY §8(b): kernel 2
+        # evaluates thousands where the reference keeps 100): consulted only
+        # where the reference would call its SMT backend, see get_model
+        self.seeds: List = []
+        # an object with models() and epoch (laser/witness.WitnessSeeds), or None
+        self.seed_source = None
+        self._seed_cols = None               # (epoch, PoolColumns) of the seeds
+        # quick-sat bitmaps computed ahead for a group of queries (prefetch)
+        self._bits: Dict[Node, tuple] = {}
+        self.stats = {"queries": 0, "lru_hits": 0, "seed_hits": 0, "misses": 0}
 
     @property
     def device(self):
@@ -275,6 +286,21 @@ class ModelCache:
             self._memo.popitem(last=False)
 
     def _pool(self, models: List[Model], prog, key: Optional[Node] = None) -> ModelPool:
+        seeds = self.seeds
+        n = len(models) - len(seeds)
+        if seeds and n >= 0 and all(a is b for a, b in zip(models[n:], seeds)):
+            # the seed block comes from cached columns (rebuilt when the seeds change)
+            if self._seed_cols is None or self._seed_cols[0] is not self.seed_source or \
+                    len(self._seed_cols[1].assigns) != len(seeds):
+                cols = PoolColumns([_view(m, None) for m in seeds],
+                                   getattr(self.seed_source, "revision", None))
+                self._seed_cols = (self.seed_source, cols)
+            block = self._seed_cols[1].pool(prog.var_names, prog.var_widths, prog.tables)
+            if n == 0:
+                return block
+            head = ModelPool.from_dicts([_view(m, key) for m in models[:n]], prog.var_names,
+                                        prog.var_widths, prog.tables)
+            return concat_pools(head, block)
         return ModelPool.from_dicts([_view(m, key) for m in models], prog.var_names,
                                     prog.var_widths, prog.tables)
 
@@ -288,17 +314,87 @@ class ModelCache:
         if hit:
             return val
         result = False
+        if self.seed_source is not None:
+            self._seed_models()          # seeds in the LRU are completed for every input first
         models = list(reversed(self.model_cache.lru_cache.keys()))      # MRU first
-        if models:
+        pre = self._bits.get(key)
+        if models and pre is not None and all(id(m) in pre[0] for m in models):
+            pos, row = pre                       # prefetched: no launch of its own
+            for m in models:
+                p = pos[id(m)]
+                if (int(row[p >> 6]) >> (p & 63)) & 1:
+                    result = self._select(m)
+                    break
+        elif models:
             prog, kept = compile_sets([[key]])
             if kept:
-                fs, _, _ = self.device.eval(prog, self._pool(models, prog, key))
+                fs, _, ms = self.device.eval(prog, self._pool(models, prog, key))
                 self.device_evals += len(models)
+                self.device_ms += float(ms or 0.0)
                 self.launches += 1
                 if int(fs[0]) != NO_MODEL:
                     result = self._select(models[int(fs[0])])
         self._memo_put(key, result)
         return result
+
+    # -- witness seeds and prefetched groups ------------------------------------
+    def _seed_models(self) -> List:
+        if self.seed_source is not None:
+            self.seeds = list(self.seed_source.models())
+        return self.seeds
+
+    def prefetch(self, raws: Sequence[Node]) -> None:
+        """Quick-sat bitmaps of a group of queries (the fork filters of one BFS
+        round) against the current LRU models and the seeds, in ONE kernel-2
+        launch; check_quick_sat / check_seeds then replay the sequential
+        reference order from them (LRU moves exactly as query by query)."""
+        seeds = self._seed_models()
+        lru = list(reversed(self.model_cache.lru_cache.keys()))
+        pool = lru + seeds          # a seed the LRU holds appears twice: same bits
+        fresh = list(OrderedDict.fromkeys(k for k in raws if k not in self._memo and k not in self._bits))
+        if not pool or not fresh:
+            return
+        if any(_decl(k) is not None for k in fresh) and any(isinstance(m, Model) and len(m.raw) > 1 for m in pool):
+            return                            # per-query internal models: sequential path
+        prog, kept = compile_sets([[k] for k in fresh])
+        if not kept:
+            return
+        _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
+        self.device_evals += len(kept) * len(pool)
+        self.device_ms += float(ms or 0.0)
+        self.launches += 1
+        pos = {}
+        for i, m in enumerate(pool):
+            pos.setdefault(id(m), i)
+        for row, k in enumerate(kept):
+            self._bits[fresh[k]] = (pos, bits[row])
+
+    def clear_prefetch(self) -> None:
+        self._bits.clear()
+
+    def check_seeds(self, key: Node):
+        """The first seed model (pool order) satisfying `key`, or None: where
+        the reference asks its SMT backend for a model, a seed that satisfies
+        the query is such a model (sound: it is checked, not guessed)."""
+        seeds = self._seed_models()
+        if not seeds:
+            return None
+        pre = self._bits.get(key)
+        if pre is not None and all(id(m) in pre[0] for m in seeds):
+            pos, row = pre
+            for m in seeds:
+                p = pos[id(m)]
+                if (int(row[p >> 6]) >> (p & 63)) & 1:
+                    return m
+            return None
+        prog, kept = compile_sets([[key]])
+        if not kept:
+            return None
+        fs, _, ms = self.device.eval(prog, self._pool(seeds, prog, key))
+        self.device_evals += len(seeds)
+        self.device_ms += float(ms or 0.0)
+        self.launches += 1
+        return seeds[int(fs[0])] if int(fs[0]) != NO_MODEL else None
 
     def check_quick_sat_many(self, queries: Sequence) -> List[object]:
         """[check_quick_sat(q) for q in queries], with every query not already
@@ -450,9 +546,19 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         constraints = constraints.get_all_constraints()
     constraints = [c for c in constraints if type(c) != bool]
     if len(maximize) + len(minimize) == 0:
-        ret_model = model_cache.check_quick_sat(simplify(And(*constraints)).raw)
+        key = simplify(And(*constraints)).raw
+        model_cache.stats["queries"] += 1
+        ret_model = model_cache.check_quick_sat(key)
         if ret_model:
+            model_cache.stats["lru_hits"] += 1
             return ret_model
+        seed = model_cache.check_seeds(key)
+        if seed is not None:
+            # a model of the query, as the backend would have returned one
+            model_cache.stats["seed_hits"] += 1
+            model_cache.put(seed, 1)
+            return seed
+        model_cache.stats["misses"] += 1
     if args.solver_log:
         from .smtlib import log_query, to_smt2
         log_query(args.solver_log, to_smt2(constraints, minimize, maximize))
@@ -514,6 +620,12 @@ def _keccak_conditions():
     return keccak_function_manager.create_conditions()
 
 
+def query_raw(all_constraints) -> Node:
+    """The conjunction get_model's quick-sat evaluates for a constraint list
+    (support/model.py:48-56): And of every non-bool constraint."""
+    return simplify(And(*[c for c in all_constraints if type(c) != bool])).raw
+
+
 class Constraints(list):
     def __init__(self, constraint_list: Optional[List] = None):
         super().__init__(self._get_smt_bool_list(constraint_list or []))
@@ -571,3 +683,23 @@ class Constraints(list):
     def __eq__(self, other):
         return isinstance(other, list) and len(self) == len(other) and all(
             _raw(a) is _raw(b) for a, b in zip(self, other))
+
+
+class SnapshotConstraints(Constraints):
+    """A path's constraints with the keccak conjunct as it was when the query
+    was posed (a fork filter evaluated later in a batch sees the function
+    manager of its own time); hashed and compared as the plain Constraints, so
+    get_model's cache is shared with them."""
+
+    def __init__(self, constraint_list, keccak_conjunct):
+        super().__init__(list(constraint_list))
+        self._kc = keccak_conjunct
+
+    def get_all_constraints(self):
+        return self[:] + [self._kc]
+
+    @property
+    def as_list(self):
+        return self.get_all_constraints()
+
+    __hash__ = Constraints.__hash__

@@ -16,7 +16,7 @@ import numpy as np
 
 from mythril_amd.device import StepStats
 from mythril_amd.lanes import (_ALL_FIELDS, _SYM_FIELDS, _TAINT_FIELDS, LaneBatch, MG_DEPTH, MG_ESC_SYMBOLIC,
-                               MG_ESCAPE, MG_HALT_END, MG_HOOK, MG_LANE_HOOK_ACK, MG_LANE_SYMBOLIC,
+                               MG_ESCAPE, MG_FORK, MG_HALT_END, MG_HOOK, MG_LANE_HOOK_ACK, MG_LANE_SYMBOLIC,
                                MG_LANE_TAINT, MG_RUNNING)
 from oracle.evm_ref import OracleEVM
 
@@ -144,6 +144,12 @@ class OracleDevice:
             else:
                 op = int(ops[pc])
                 hooked = (int(mask[op >> 6]) >> (op & 63)) & 1 and not int(img.flags[i]) & MG_LANE_HOOK_ACK
+                sp = int(img.sp[i])
+                fork = (op == 0x57 and not hooked and sp >= 2 and img.symbolic and int(img.stag[i, sp - 2])
+                        and not int(img.stag[i, sp - 1]))
+                if fork:                        # k_sym_step: a JUMPI on a symbolic condition
+                    img.status[i], img.aux[i] = MG_FORK, op
+                    continue
                 img.status[i] = MG_HOOK if hooked else MG_ESCAPE
                 img.aux[i] = op if hooked else op | (MG_ESC_SYMBOLIC << 8)
 
@@ -154,3 +160,39 @@ class OracleDevice:
     def coverage_clear(self):
         for buf in self._cov.values():
             buf[:] = 0
+
+
+class OracleK2:
+    """Test stand-in for kernel 2's entry points (mg_eval / mg_eval_bits),
+    backed by the C evaluator oracle/bv_ref.c."""
+
+    def __init__(self):
+        self.launches = 0
+
+    def eval(self, prog, pool):
+        from oracle.bv_ref import eval_batch
+        self.launches += 1
+        fs, sc = eval_batch(prog, pool)
+        return fs, sc, 0.0
+
+    def eval_bits(self, prog, pool):
+        from oracle.bv_ref import eval_batch
+        from mythril_amd.smt.program import ModelPool
+        self.launches += 1
+        n, m = prog.n_dags, pool.n_models
+        bits = np.zeros((n, (m + 63) // 64), dtype=np.uint64)
+        for k in range(m):
+            one = ModelPool(pool.values[:, k:k + 1])
+            if pool.n_tables:
+                one.tab_start, one.tab_count = pool.tab_start[:, k:k + 1], pool.tab_count[:, k:k + 1]
+                one.tab_entries, one.tab_default = pool.tab_entries, pool.tab_default[:, k:k + 1]
+            _, sc = eval_batch(prog, one)
+            for d in np.flatnonzero(sc):
+                bits[d, k >> 6] |= np.uint64(1) << np.uint64(k & 63)
+        fs = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+        sc = np.zeros(n, dtype=np.uint32)
+        for d in range(n):
+            hit = [k for k in range(m) if (int(bits[d, k >> 6]) >> (k & 63)) & 1]
+            if hit:
+                fs[d], sc[d] = hit[0], len(hit)
+        return fs, sc, bits, 0.0
