@@ -66,6 +66,9 @@ def parse(argv=None):
     ap.add_argument("--symbolic-tx", type=int, default=2, help="transactions of the symbolic_tx field (-t)")
     ap.add_argument("--seed-models", type=int, default=1024,
                     help="witness seed models beside the LRU cache in the symbolic_tx field")
+    ap.add_argument("--host-profile", default=None,
+                    help="directory: cProfile the LaserEVM fields (hooked_c2, taint_c2, symbolic_tx) "
+                         "and write each one's cumulative-time table there")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
@@ -213,21 +216,40 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         _log(rank, "C2 roofline profile")
         roof = roofline.lane_step_roofline(dev, batch, cid, kernel_ms=float(np.mean(kernel_ms)) if kernel_ms else 0.0)
 
+    def host_profiled(name, fn):
+        """fn(), under cProfile when --host-profile is set (rank 0)."""
+        if not args.host_profile or rank != 0:
+            return fn()
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            return fn()
+        finally:
+            pr.disable()
+            os.makedirs(args.host_profile, exist_ok=True)
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(60)
+            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(40)
+            Path(args.host_profile, f"{name}.txt").write_text(buf.getvalue())
+
     hooked = None
     if args.hooked_lanes and gpu and not args.profile_only:
         _log(rank, f"hooked C2 ({args.hooked_lanes} lanes)")
-        hooked = run_hooked_c2(dev, args.hooked_lanes, rank)
+        hooked = host_profiled("hooked_c2", lambda: run_hooked_c2(dev, args.hooked_lanes, rank))
 
     taint = None
     if args.taint_lanes and gpu and not args.profile_only:
         _log(rank, f"taint C2 ({args.taint_lanes} lanes)")
-        taint = run_taint_c2(dev, args.taint_lanes, rank)
+        taint = host_profiled("taint_c2", lambda: run_taint_c2(dev, args.taint_lanes, rank))
 
     symb = None
     if args.symbolic_replicas and gpu and not args.profile_only:
         _log(rank, f"symbolic transactions (-t {args.symbolic_tx}, {args.symbolic_replicas} replicas)")
-        symb = run_symbolic_tx(dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models,
-                               log=lambda m: _log(rank, m))
+        symb = host_profiled("symbolic_tx", lambda: run_symbolic_tx(
+            dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models, log=lambda m: _log(rank, m)))
 
     c4 = None
     if not args.no_c4:

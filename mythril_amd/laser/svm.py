@@ -288,7 +288,7 @@ class LaserEVM:
         self._flush_forks()
         if not world_states:
             return []
-        kc = keccak_function_manager.create_conditions()
+        kc = _keccak_conjunct()
         qs = [SnapshotConstraints(ws.constraints, kc) for ws in world_states]
         solver_mod.model_cache.prefetch([query_raw(q.get_all_constraints()) for q in qs])
         try:
@@ -347,7 +347,7 @@ class LaserEVM:
         model-cache moves are the sequential loop's."""
         queries = None
         if self.strategy.run_check() and (len(new_states) > 1 and random.uniform(0, 1) < args.pruning_factor):
-            kc = keccak_function_manager.create_conditions()
+            kc = _keccak_conjunct()
             queries = [SnapshotConstraints(st.world_state.constraints, kc) for st in new_states]
         self._pending_forks.append((s, new_states, queries, track_gas, final_states))
 
@@ -1153,6 +1153,24 @@ class LaserEVM:
             if old is not None and old.size == bits.size:
                 bits = old | bits
             self._peer_cov[code] = bits
+
+
+_KC = [None, None]
+
+
+def _keccak_conjunct():
+    """keccak_function_manager.create_conditions(), rebuilt only when an input
+    or a hash was registered since the last call (it depends on nothing else:
+    the intervals are assigned once per input size)."""
+    km = keccak_function_manager
+    def key():
+        return (id(km), id(km.symbolic_inputs), id(km.concrete_hashes),
+                tuple(len(v) for v in km.symbolic_inputs.values()), len(km.concrete_hashes),
+                len(km.interval_hook_for_size))
+    if _KC[0] != key():
+        _KC[1] = km.create_conditions()
+        _KC[0] = key()            # after the call: it may assign intervals
+    return _KC[1]
 
 
 def _annotation_of(state: GlobalState) -> JumpdestCountAnnotation:

@@ -81,6 +81,7 @@ class WitnessSeeds:
         self._models: Optional[List[Model]] = None
         self._epoch = None
         self._rev: Dict[str, int] = {}           # interpretation changes per name (PoolColumns)
+        self._tx_top = -1
 
     def revision(self, name: str) -> int:
         return self._rev.get(name, 0)
@@ -93,6 +94,7 @@ class WitnessSeeds:
         if txid in self.tx_ids:
             return
         self.tx_ids.append(txid)
+        self._touch(f"{txid}_calldata")
         actors = list(ACTORS.values())
         r = self.rng
         for m, a in enumerate(self.assign):
@@ -193,8 +195,11 @@ class WitnessSeeds:
         returned): completion only adds entries, so every query a seed answered
         before stays answered."""
         from .transaction import tx_id_manager
-        for k in range(1, int(tx_id_manager._next_transaction_id) + 1):
-            self.add_tx(str(k))
+        top = int(tx_id_manager._next_transaction_id)
+        if top != self._tx_top:
+            for k in range(1, top + 1):
+                self.add_tx(str(k))
+            self._tx_top = top
         from ..smt.exponent_manager import exponent_function_manager
         epoch = (len(self.tx_ids), sum(len(v) for v in self.km.symbolic_inputs.values()),
                  len(self.km.concrete_hashes), len(exponent_function_manager.concrete_points))

@@ -285,3 +285,23 @@ def compile_sets(sets: Sequence[Sequence], compiler: Compiler = None) -> Tuple[P
         tables[t] = c.lowering.tables[name]
     return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths),
                         tables), kept
+
+
+def batch_from(c: "Compiler", progs: List[np.ndarray]) -> ProgramBatch:
+    """A ProgramBatch of programs compiled by one (persistent) Compiler: its
+    variable, constant and table index spaces only grow, so programs compiled
+    for earlier batches stay valid in later ones."""
+    off = np.zeros(len(progs) + 1, dtype=np.uint32)
+    if progs:
+        off[1:] = np.cumsum([p.shape[0] for p in progs])
+        insns = np.concatenate(progs)
+    else:
+        insns = np.zeros((0, 4), dtype=np.uint32)
+    consts = np.stack([limbs(x) for x in c.consts]) if c.consts else np.zeros((0, 8), np.uint32)
+    names = [None] * len(c.var_widths)
+    for name, i in c.var_index.items():
+        names[i] = name
+    tables = [None] * len(c.table_index)
+    for name, t in c.table_index.items():
+        tables[t] = c.lowering.tables[name]
+    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths), tables)

@@ -8,6 +8,7 @@ refs kind<<30 | index, or immediates).
 from __future__ import annotations
 
 import ctypes
+import itertools
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -216,39 +217,50 @@ class PoolColumns:
         return col
 
     def _tab(self, sig) -> tuple:
+        """(start, count, entries, default) of one table over every model.
+        Interpretations only grow (witness seeds gain entries, never change
+        one), so a revision serialises only each model's new entries."""
         key = (sig.name, sig.kind, sig.domain, sig.range)
         rev = self.revision(sig.name)
         got = self._tabs.get(key)
-        if got is None or got[0] != rev:
-            nm = len(self.assigns)
-            start = np.zeros(nm, dtype=np.uint32)
-            count = np.zeros(nm, dtype=np.uint32)
-            dflt = bytearray()
-            rows = bytearray()
-            n_rows = 0
-            M256_, M512_ = (1 << 256) - 1, (1 << 512) - 1
-            for m, a in enumerate(self.assigns):
-                interp = a.get(sig.name)
-                start[m] = n_rows
-                if isinstance(interp, ArrayInterp):
-                    d = interp.default
-                    items = [((k,), v) for k, v in interp.entries.items()]
-                elif isinstance(interp, FuncInterp):
-                    d = interp.else_value
-                    items = interp.entries.items()
-                else:
-                    d, items = 0, ()
-                dflt += (d & M512_).to_bytes(64, "little")
-                for args, v in items:
-                    k0, k1 = sig.key_chunks(tuple(args))
-                    rows += (k0 & M256_).to_bytes(32, "little") + (k1 & M256_).to_bytes(32, "little") + \
+        if got is not None and got[0] == rev:
+            return got[1]
+        nm = len(self.assigns)
+        if got is None:
+            ser = [bytearray() for _ in range(nm)]      # per model: serialised rows
+            done = [0] * nm                              # entries serialised
+            dflt = [None] * nm
+        else:
+            ser, done, dflt = got[2]
+        M256_, M512_ = (1 << 256) - 1, (1 << 512) - 1
+        for m, a in enumerate(self.assigns):
+            interp = a.get(sig.name)
+            if isinstance(interp, ArrayInterp):
+                d, ent, arr = interp.default, interp.entries, True
+            elif isinstance(interp, FuncInterp):
+                d, ent, arr = interp.else_value, interp.entries, False
+            else:
+                d, ent, arr = 0, {}, False
+            if len(ent) < done[m] or dflt[m] != d:       # not append-only: start over
+                ser[m], done[m] = bytearray(), 0
+            dflt[m] = d
+            if len(ent) > done[m]:
+                buf = ser[m]
+                for k, v in itertools.islice(ent.items(), done[m], None):
+                    k0, k1 = sig.key_chunks((k,) if arr else tuple(k))
+                    buf += (k0 & M256_).to_bytes(32, "little") + (k1 & M256_).to_bytes(32, "little") + \
                         (v & M512_).to_bytes(64, "little")
-                    n_rows += 1
-                count[m] = n_rows - start[m]
-            entries = np.frombuffer(bytes(rows), dtype="<u4").reshape(-1, 32).astype(np.uint32)
-            default = np.frombuffer(bytes(dflt), dtype="<u4").reshape(nm, 16).astype(np.uint32)
-            got = self._tabs[key] = (rev, (start, count, entries, default))
-        return got[1]
+                done[m] = len(ent)
+        count = np.array(done, dtype=np.uint32)
+        start = np.zeros(nm, dtype=np.uint32)
+        if nm > 1:
+            start[1:] = np.cumsum(count[:-1])
+        entries = np.frombuffer(b"".join(ser), dtype="<u4").reshape(-1, 32).astype(np.uint32)
+        default = np.frombuffer(b"".join(((x or 0) & M512_).to_bytes(64, "little") for x in dflt),
+                                dtype="<u4").reshape(nm, 16).astype(np.uint32)
+        out = (start, count, entries, default)
+        self._tabs[key] = (rev, out, (ser, done, dflt))
+        return out
 
     def pool(self, var_names: List[str], var_widths: List[int], tables: Optional[List] = None) -> ModelPool:
         nm = len(self.assigns)

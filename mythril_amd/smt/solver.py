@@ -37,7 +37,8 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence
 import numpy as np
 
 from .expr import And, BitVec, Bool, Node, TRUE, _fold, _select, const, symbol_factory
-from .flatten import compile_sets
+from .flatten import Compiler, batch_from, compile_sets
+from .lower import Unsupported
 from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, concat_pools
 
 NO_MODEL = 0xFFFFFFFF
@@ -225,6 +226,9 @@ class LRUCache:
         self.lru_cache[key] = value
 
 
+_MISSING = object()
+
+
 def _raw(expr) -> Node:
     return expr.raw if isinstance(expr, Bool) else expr
 
@@ -249,6 +253,10 @@ class ModelCache:
         self._seed_cols = None               # (epoch, PoolColumns) of the seeds
         # quick-sat bitmaps computed ahead for a group of queries (prefetch)
         self._bits: Dict[Node, tuple] = {}
+        self._seed_memo: Dict[Node, object] = {}
+        self._compiler = None                 # persistent: conjunct programs are compiled once
+        self._progs: Dict[Node, object] = {}
+        self.part_evals = 0            # conjunct programs x models run on kernel 2
         self.stats = {"queries": 0, "lru_hits": 0, "seed_hits": 0, "misses": 0}
 
     @property
@@ -317,25 +325,96 @@ class ModelCache:
         if self.seed_source is not None:
             self._seed_models()          # seeds in the LRU are completed for every input first
         models = list(reversed(self.model_cache.lru_cache.keys()))      # MRU first
-        pre = self._bits.get(key)
-        if models and pre is not None and all(id(m) in pre[0] for m in models):
-            pos, row = pre                       # prefetched: no launch of its own
-            for m in models:
-                p = pos[id(m)]
-                if (int(row[p >> 6]) >> (p & 63)) & 1:
-                    result = self._select(m)
-                    break
-        elif models:
-            prog, kept = compile_sets([[key]])
-            if kept:
-                fs, _, ms = self.device.eval(prog, self._pool(models, prog, key))
-                self.device_evals += len(models)
-                self.device_ms += float(ms or 0.0)
-                self.launches += 1
-                if int(fs[0]) != NO_MODEL:
-                    result = self._select(models[int(fs[0])])
+        if models:
+            pre = self._bits.get(key)
+            if pre is None or not all(id(m) in pre[0] for m in models):
+                pre = self._eval_keys([key], self._full_pool(models), keep=False).get(key)
+            if pre is not None:
+                pos, row = pre
+                for m in models:
+                    p = pos[id(m)]
+                    if (int(row[p >> 6]) >> (p & 63)) & 1:
+                        result = self._select(m)
+                        break
         self._memo_put(key, result)
         return result
+
+    # -- evaluation by conjuncts ----------------------------------------------------
+    def _eval_keys(self, keys: Sequence[Node], pool: List, keep: bool = True) -> Dict[Node, tuple]:
+        """Per key, (position of each pool model, satisfied-model bitmap), from ONE
+        kernel-2 launch.  A key is a conjunction (get_model's And of the path
+        constraints and the keccak conjunct): it is taken apart into its
+        conjuncts, each distinct conjunct of the whole group is compiled and
+        evaluated once, and a key's bitmap is the AND of its conjuncts' -- the
+        same truth as the conjunction evaluated whole, for a fraction of the
+        compile work (sibling paths share most conjuncts, and every query of a
+        group shares the keccak conjunct).  Keys with a conjunct the device does
+        not evaluate get no entry (they stay with the backend)."""
+        out: Dict[Node, tuple] = {}
+        if not pool or not keys:
+            return out
+        if any(_decl(k) is not None for k in keys) and any(isinstance(m, Model) and len(m.raw) > 1 for m in pool):
+            return out                        # a per-query internal model: evaluate on the host path
+        parts_of = {}
+        distinct: "OrderedDict[Node, None]" = OrderedDict()
+        for k in keys:
+            cs = _conjuncts(k)
+            parts_of[k] = cs
+            for c in cs:
+                distinct[c] = None
+        plist = [c for c in distinct if c.op != "const"]
+        words = (len(pool) + 63) // 64
+        rows: Dict[Node, np.ndarray] = {}
+        if plist:
+            # every conjunct is compiled once per cache, by one compiler whose
+            # index spaces only grow (flatten.batch_from)
+            if self._compiler is None:
+                self._compiler = Compiler()
+            progs, kept = [], []
+            for c in plist:
+                pr = self._progs.get(c, _MISSING)
+                if pr is _MISSING:
+                    try:
+                        pr = self._compiler.compile(c)
+                    except Unsupported:
+                        pr = None
+                    self._progs[c] = pr
+                if pr is not None:
+                    progs.append(pr)
+                    kept.append(c)
+            if kept:
+                prog = batch_from(self._compiler, progs)
+                _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
+                self.part_evals += len(kept) * len(pool)
+                self.device_ms += float(ms or 0.0)
+                self.launches += 1
+                for row, c in enumerate(kept):
+                    rows[c] = bits[row]
+        ones = np.zeros(words, dtype=np.uint64)
+        for i in range(len(pool)):
+            ones[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
+        pos = {}
+        for i, m in enumerate(pool):
+            pos.setdefault(id(m), i)
+        for k in keys:
+            acc = ones.copy()
+            ok = True
+            for c in parts_of[k]:
+                if c.op == "const":
+                    if not c.param:
+                        acc[:] = 0
+                    continue
+                r = rows.get(c)
+                if r is None:
+                    ok = False
+                    break
+                acc &= r
+            if ok:
+                out[k] = (pos, acc)
+                self.device_evals += len(pool)
+        if keep:
+            self._bits.update(out)
+        return out
 
     # -- witness seeds and prefetched groups ------------------------------------
     def _seed_models(self) -> List:
@@ -345,29 +424,23 @@ class ModelCache:
 
     def prefetch(self, raws: Sequence[Node]) -> None:
         """Quick-sat bitmaps of a group of queries (the fork filters of one BFS
-        round) against the current LRU models and the seeds, in ONE kernel-2
-        launch; check_quick_sat / check_seeds then replay the sequential
-        reference order from them (LRU moves exactly as query by query)."""
-        seeds = self._seed_models()
-        lru = list(reversed(self.model_cache.lru_cache.keys()))
-        pool = lru + seeds          # a seed the LRU holds appears twice: same bits
-        fresh = list(OrderedDict.fromkeys(k for k in raws if k not in self._memo and k not in self._bits))
-        if not pool or not fresh:
-            return
-        if any(_decl(k) is not None for k in fresh) and any(isinstance(m, Model) and len(m.raw) > 1 for m in pool):
-            return                            # per-query internal models: sequential path
-        prog, kept = compile_sets([[k] for k in fresh])
-        if not kept:
-            return
-        _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
-        self.device_evals += len(kept) * len(pool)
-        self.device_ms += float(ms or 0.0)
-        self.launches += 1
-        pos = {}
-        for i, m in enumerate(pool):
-            pos.setdefault(id(m), i)
-        for row, k in enumerate(kept):
-            self._bits[fresh[k]] = (pos, bits[row])
+        round, a transaction's reachability filter) against the current LRU
+        models and the seeds, in ONE kernel-2 launch; check_quick_sat /
+        check_seeds then replay the sequential reference order from them (LRU
+        moves exactly as query by query)."""
+        self._seed_models()
+        pool = self._full_pool(list(reversed(self.model_cache.lru_cache.keys())))
+        fresh = list(OrderedDict.fromkeys(
+            k for k in raws if k not in self._bits and not (k in self._memo and k in self._seed_memo)))
+        self._eval_keys(fresh, pool)
+
+    def _full_pool(self, lru: List) -> List:
+        """The LRU's models that are not seeds, then every seed (a pool's order
+        only places bits: answers follow the LRU's MRU order, then the seeds')."""
+        if not self.seeds:
+            return lru
+        ids = {id(m) for m in self.seeds}
+        return [m for m in lru if id(m) not in ids] + self.seeds
 
     def clear_prefetch(self) -> None:
         self._bits.clear()
@@ -375,26 +448,27 @@ class ModelCache:
     def check_seeds(self, key: Node):
         """The first seed model (pool order) satisfying `key`, or None: where
         the reference asks its SMT backend for a model, a seed that satisfies
-        the query is such a model (sound: it is checked, not guessed)."""
+        the query is such a model (sound: it is checked, not guessed).  The
+        answer is memoised: seeds only gain interpretations of inputs a query
+        registered later, which it does not mention."""
+        if key in self._seed_memo:
+            return self._seed_memo[key]
         seeds = self._seed_models()
         if not seeds:
             return None
         pre = self._bits.get(key)
-        if pre is not None and all(id(m) in pre[0] for m in seeds):
+        if pre is None or not all(id(m) in pre[0] for m in seeds):
+            pre = self._eval_keys([key], seeds, keep=False).get(key)
+        found = None
+        if pre is not None:
             pos, row = pre
             for m in seeds:
                 p = pos[id(m)]
                 if (int(row[p >> 6]) >> (p & 63)) & 1:
-                    return m
-            return None
-        prog, kept = compile_sets([[key]])
-        if not kept:
-            return None
-        fs, _, ms = self.device.eval(prog, self._pool(seeds, prog, key))
-        self.device_evals += len(seeds)
-        self.device_ms += float(ms or 0.0)
-        self.launches += 1
-        return seeds[int(fs[0])] if int(fs[0]) != NO_MODEL else None
+                    found = m
+                    break
+        self._seed_memo[key] = found
+        return found
 
     def check_quick_sat_many(self, queries: Sequence) -> List[object]:
         """[check_quick_sat(q) for q in queries], with every query not already
@@ -433,6 +507,20 @@ class ModelCache:
             self._memo_put(k, result)
             out.append(result)
         return out
+
+
+def _conjuncts(key: Node) -> List[Node]:
+    """The leaf conjuncts of a Bool term (nested ``and`` nodes flattened, each
+    distinct conjunct once, in first-seen order)."""
+    out: "OrderedDict[Node, None]" = OrderedDict()
+    stack = [key]
+    while stack:
+        n = stack.pop()
+        if n.op == "and":
+            stack.extend(reversed(n.args))
+        elif n is not TRUE:
+            out[n] = None
+    return list(out)
 
 
 def _view(model, key: Optional[Node]) -> Dict[str, object]:
