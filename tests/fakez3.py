@@ -150,3 +150,86 @@ def ZeroExt(k, a):
 
 def SignExt(k, a):
     return Expr("SIGN_EXT", BitVecSort(a.size() + k), [a], params=(k,))
+
+
+# ---- the constructors mythril_amd.bridge.from_dag calls (z3py's names) ----------
+def _bool(op, *args):
+    return Expr(op, BoolSort(), args)
+
+
+def _w(x):
+    return x.sort().size()
+
+
+def UDiv(a, b): return bv("BUDIV", a, b)
+def URem(a, b): return bv("BUREM", a, b)
+def SRem(a, b): return bv("BSREM", a, b)
+def LShR(a, b): return bv("BLSHR", a, b)
+def ULT(a, b): return _bool("ULT", a, b)
+def UGT(a, b): return _bool("UGT", a, b)
+def ULE(a, b): return _bool("ULEQ", a, b)
+def UGE(a, b): return _bool("UGEQ", a, b)
+def And(*a): return _bool("AND", *a)
+def Or(*a): return _bool("OR", *a)
+def Not(a): return _bool("NOT", a)
+def Xor(a, b): return _bool("XOR", a, b)
+def Implies(a, b): return _bool("IMPLIES", a, b)
+def Distinct(a, b): return _bool("DISTINCT", a, b)
+
+
+def _function(name, *sorts):
+    rng = sorts[-1]
+    if isinstance(rng, int):              # this fake's older form: (name, domain widths, range width)
+        rng = BitVecSort(rng)
+
+    def app(*args):
+        return Expr("UNINTERPRETED", rng, args, name=name)
+    return app
+
+
+Function = _function          # z3py: Function(name, *domain_sorts, range_sort)
+
+
+def Array(name, dom, rng):  # noqa: F811  (z3py: Array(name, domain_sort, range_sort))
+    if isinstance(dom, int):
+        dom, rng = BitVecSort(dom), BitVecSort(rng)
+    return Expr("UNINTERPRETED", ArraySort(dom, rng), name=name)
+
+
+def K(dom, v):  # noqa: F811
+    if isinstance(dom, int):
+        dom = BitVecSort(dom)
+    return Expr("CONST_ARRAY", ArraySort(dom, v.sort()), [v])
+
+
+def _op(name):
+    def f(self, other):
+        return bv(name, self, other)
+    return f
+
+
+def _cmp(name):
+    def f(self, other):
+        return _bool(name, self, other)
+    return f
+
+
+Expr.__add__ = _op("BADD")
+Expr.__sub__ = _op("BSUB")
+Expr.__mul__ = _op("BMUL")
+Expr.__truediv__ = _op("BSDIV")
+Expr.__mod__ = _op("BSMOD")
+Expr.__and__ = _op("BAND")
+Expr.__or__ = _op("BOR")
+Expr.__xor__ = _op("BXOR")
+Expr.__lshift__ = _op("BSHL")
+Expr.__rshift__ = _op("BASHR")
+Expr.__invert__ = lambda self: bv("BNOT", self)
+Expr.__neg__ = lambda self: bv("BNEG", self)
+Expr.__lt__ = _cmp("SLT")
+Expr.__gt__ = _cmp("SGT")
+Expr.__le__ = _cmp("SLEQ")
+Expr.__ge__ = _cmp("SGEQ")
+Expr.__eq__ = _cmp("EQ")
+Expr.__ne__ = _cmp("DISTINCT")
+Expr.__hash__ = lambda self: self._id

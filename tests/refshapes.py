@@ -9,9 +9,18 @@ transaction_stack.  The reference itself is not importable here (z3, eth_abi
 and py-evm are absent), so these stand in for it."""
 
 
+import fakez3 as _z
+
+
 class BitVec:
-    def __init__(self, value=None, size=256, name=None):
+    """value (None when symbolic) and, for a symbolic word, ``raw``: its z3
+    term (the fake z3's), as the reference's BitVec.raw."""
+
+    def __init__(self, value=None, size=256, name=None, raw=None):
         self.value, self._size, self.name = value, size, name
+        if raw is None and value is None and name is not None:
+            raw = _z.BitVec(name, size)
+        self.raw = raw
 
     @property
     def symbolic(self):
@@ -21,10 +30,32 @@ class BitVec:
         return self._size
 
     def __hash__(self):
-        return hash((self.value, self.name))
+        return hash((self.value, self.name, id(self.raw) if self.value is None else 0))
 
     def __eq__(self, other):
-        return isinstance(other, BitVec) and (self.value, self.name) == (other.value, other.name)
+        return isinstance(other, BitVec) and (self.value, self.name) == (other.value, other.name) and (
+            self.value is not None or self.raw is other.raw)
+
+
+class Bool:
+    def __init__(self, raw):
+        self.raw = raw
+        self.value = None
+
+
+class Smt:                                      # the mythril.laser.smt surface unpack uses
+    @staticmethod
+    def BitVec(raw):
+        return BitVec(None, raw.sort().size(), raw=raw)
+
+    Bool = Bool
+
+
+smt = Smt()
+
+
+def _raw(x, w=256):
+    return _z.BitVecVal(x.value, w) if x.value is not None else x.raw
 
 
 class SymbolFactory:
@@ -60,23 +91,27 @@ class Memory:                                   # memory.py:28-208
         self._memory[BitVec(key)] = value
 
 
-class K:                                       # array.py:73-86 (marker)
-    pass
+class K:                                       # array.py:73-86
+    def __init__(self):
+        self.raw = _z.K(256, _z.BitVecVal(0, 256))
 
 
-class Array:
-    pass
+class Array:                                   # array.py:56-70
+    def __init__(self, name):
+        self.raw = _z.Array(name, 256, 256)
 
 
 class Storage:                                 # account.py:18-99
-    def __init__(self, concrete=True):
-        self._standard_storage = K() if concrete else Array()
+    def __init__(self, concrete=True, address=0):
+        self._standard_storage = K() if concrete else Array(f"Storage{address}")
         self.printable_storage = {}
         self.keys_set = set()
 
     def __setitem__(self, key, value):
         self.printable_storage[key] = value
         self.keys_set.add(key)
+        std = self._standard_storage
+        std.raw = _z.Store(std.raw, _raw(key), _raw(value))
 
 
 class Disassembly:
@@ -88,7 +123,7 @@ class Account:
     def __init__(self, address, code_hex, concrete_storage=True, balance=0):
         self.address = BitVec(address)
         self.code = Disassembly(code_hex)
-        self.storage = Storage(concrete_storage)
+        self.storage = Storage(concrete_storage, address)
         self.nonce = 0
         self.contract_name = "Test"
         self._balance = BitVec(balance)
@@ -102,8 +137,9 @@ class ConcreteCalldata:
         self._concrete_calldata = list(data)
 
 
-class SymbolicCalldata:
-    pass
+class SymbolicCalldata:                        # calldata.py:214-262 (tx_id)
+    def __init__(self, tx_id="1"):
+        self.tx_id = tx_id
 
 
 class Environment:

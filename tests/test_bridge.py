@@ -137,14 +137,24 @@ def _ref_state(calldata: bytes, symbolic=False):
     return R.GlobalState(R.WorldState(), env, R.MachineState(), R.MessageCallTransaction(8_000_000))
 
 
-def test_pack_rejects_symbolic_state():
+def test_concrete_filter_and_what_stays_with_the_reference():
     assert bridge.is_concrete(_ref_state(bytes.fromhex("18160ddd")))
     assert not bridge.is_concrete(_ref_state(b"", symbolic=True))
     s = _ref_state(bytes.fromhex("18160ddd"))
     s.mstate.stack.append(R.BitVec(None, 256, "calldatasize"))
     assert not bridge.is_concrete(s)
-    with pytest.raises(bridge.NotConcrete):
+    with pytest.raises(bridge.NotConcrete):             # symbolic: needs the z3 module
         bridge.pack_global_state(s)
+    bridge.pack_global_state(s, z)                      # with it, the word is lowered
+    t = _ref_state(bytes.fromhex("18160ddd"))
+    t.mstate.memory.extend(64)
+    t.mstate.memory._memory[R.BitVec(None, 256, "off")] = 7    # a symbolic memory offset
+    with pytest.raises(bridge.NotConcrete):
+        bridge.pack_global_state(t, z)
+    u = _ref_state(bytes.fromhex("18160ddd"))
+    u.current_transaction.gas_limit = R.BitVec(None, 256, "gas")
+    with pytest.raises(bridge.NotConcrete):
+        bridge.pack_global_state(u, z)
 
 
 def _integration_blocks():
@@ -173,3 +183,91 @@ def test_integration_snippets_execute():
     assert int.from_bytes(word, "big") == 10 ** 6
     assert ref_states[2].mstate.pc == 0                      # symbolic: left to the reference
     assert ns["query"].raw.op == "bvult"
+
+
+# ---- the symbolic half (round 3): from_dag, symbolic pack / unpack -------------------
+def test_from_dag_inverts_to_dag():
+    """from_dag builds z3 terms with z3py's constructors; lowering them again
+    lands on the very same nodes (random terms and the reference's shapes:
+    store chains, keccak applications, Bool structure)."""
+    rng = random.Random(11)
+    x, y = z.BitVec("x", 256), z.BitVec("y", 256)
+    for _ in range(150):
+        node = bridge.to_dag(_rand_z3(rng, rng.randrange(1, 4), x, y), z)
+        assert bridge.to_dag(bridge.from_dag(node, z), z) is node
+    a, b = BVS("a", 256), BVS("b", 256)
+    st = K(256, 256, 0)
+    st[a] = b + 1
+    st[BVV(3, 256)] = a
+    kec = Function("keccak256_512", [512], 256)(Concat(a, BVV(0, 256)))
+    for e in [st[b], kec, And(ULT(a, b), Not(a == b), Or(ULT(b, BVV(9, 256)), a == kec)),
+              If(ULT(a, b), a, SRem(b, a)), Extract(7, 0, a), SignExt(8, Extract(7, 0, a)),
+              UDiv(a, b) ^ URem(a, b), LShR(a, BVV(3, 256)), (a >> BVV(1, 256)) < b]:
+        assert bridge.to_dag(bridge.from_dag(e.raw, z), z) is e.raw
+
+
+def _symbolic_ref_state():
+    """A reference-shaped state in the middle of a symbolic call: symbolic
+    calldata and sender, a symbolic stack word, a symbolic memory byte,
+    symbolic storage with a symbolic store, a path constraint."""
+    code = workloads.bytecode("overflow.sol.o").hex()
+    acct = R.Account(workloads.CONTRACT, code, concrete_storage=False)
+    sender = R.BitVec(None, 256, "sender_5")
+    acct.storage[R.BitVec(1)] = sender                          # Store(Storage{addr}, 1, sender)
+    env = R.Environment(acct, workloads.ATTACKER, R.SymbolicCalldata("5"), 1, 0, workloads.ATTACKER)
+    env.sender = env.origin = sender
+    ms = R.MachineState()
+    ms.memory.extend(0x60)
+    ms.memory[0x40] = R.BitVec(None, 8, raw=z.Extract(7, 0, sender.raw))
+    ms.memory[0x41] = 0xAB
+    ms.stack = [R.BitVec(4), R.BitVec(None, 256, raw=sender.raw + z.BitVecVal(1, 256))]
+    ms.pc, ms.min_gas_used, ms.max_gas_used = 0, 21, 24
+    ws = R.WorldState()
+    ws.constraints.append(R.Bool(z.ULT(sender.raw, z.BitVecVal(1 << 160, 256))))
+    return R.GlobalState(ws, env, ms, R.MessageCallTransaction(8_000_000))
+
+
+def test_symbolic_state_packs_encodes_and_writes_back():
+    from copy import copy
+    from mythril_amd.laser import symbolic as sym
+    from mythril_amd.lanes import LaneBatch, LaneShape
+    ref = _symbolic_ref_state()
+    m = bridge.pack_global_state(ref, z)
+    sender = bridge.to_dag(ref.environment.sender.raw, z)
+    assert m.environment.sender.raw is sender and sym.is_symbolic_calldata(m.environment.calldata)
+    assert m.environment.calldata.tx_id == "5"
+    assert [w.raw for w in m.mstate.stack] == [BVV(4, 256).raw, (E_bv(sender) + 1).raw]
+    assert m.mstate.memory.symbolic_bytes()[0x40].raw is Extract(7, 0, E_bv(sender)).raw
+    assert m.mstate.memory[0x41] == 0xAB
+    st = m.environment.active_account.storage
+    assert not st.concrete and [(k.raw, v.raw) for k, v in st.chain()] == [(BVV(1, 256).raw, sender)]
+    assert st[BVV(1, 256)].raw is sender                   # the Store answers its own key
+    assert [c.raw for c in m.world_state.constraints] == [ULT(E_bv(sender), BVV(1 << 160, 256)).raw]
+    # the lane carries all of it: encode -> lane planes -> decode is the identity
+    le = sym.encode_state(m)
+    b = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=64, const_cap=32))
+    le.write(b, 0)
+    b.sp[0], b.msize[0], b.flags[0] = len(m.mstate.stack), len(m.mstate.memory), le.flags
+    stack, mem, storage = sym.decode_lane(b, 0, m)
+    assert [w.raw for w in stack] == [w.raw for w in m.mstate.stack]
+    assert {p: e.raw for p, e in mem.symbolic_bytes().items()} == {0x40: Extract(7, 0, E_bv(sender)).raw}
+    assert storage.chain_raw() is st.chain_raw()
+    # write-back: a new Store, a new constraint, a new symbolic word, a new symbolic byte
+    m2 = copy(m)
+    m2.ref_state, m2.ref_n_constraints, m2.ref_n_stores = ref, m.ref_n_constraints, m.ref_n_stores
+    k = E_bv(sender) * 3
+    m2.environment.active_account.storage[k] = BVV(9, 256)
+    m2.world_state.constraints.append(ULT(k, BVV(77, 256)))
+    m2.mstate.stack.append(k)
+    m2.mstate.memory[0x42] = Extract(15, 8, k)
+    bridge.unpack_global_state(m2, ref, R.symbol_factory, R.smt, z)
+    assert bridge.to_dag(ref.mstate.stack[-1].raw, z) is k.raw
+    assert bridge.to_dag(ref.mstate.memory[0x42].raw, z) is Extract(15, 8, k).raw
+    assert bridge.to_dag(ref.world_state.constraints[-1].raw, z) is ULT(k, BVV(77, 256)).raw
+    chain = bridge.to_dag(ref.environment.active_account.storage._standard_storage.raw, z)
+    assert chain.op == "store" and chain.args[1] is k.raw and chain.args[0].args[2] is sender
+
+
+def E_bv(node):
+    from mythril_amd.smt.expr import BitVec
+    return BitVec(node)
