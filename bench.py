@@ -61,7 +61,7 @@ def parse(argv=None):
     ap.add_argument("--taint-lanes", type=int, default=4096,
                     help="lanes of the taint_c2 field (0: off): C2 through LaserEVM with the integer "
                          "and TxOrigin modules' hooks as device actions (taint lanes) and on the host")
-    ap.add_argument("--symbolic-replicas", type=int, default=64,
+    ap.add_argument("--symbolic-replicas", type=int, default=8,
                     help="replicas of each contract in the symbolic_tx field (0: off)")
     ap.add_argument("--symbolic-tx", type=int, default=2, help="transactions of the symbolic_tx field (-t)")
     ap.add_argument("--seed-models", type=int, default=1024,

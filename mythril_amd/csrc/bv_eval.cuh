@@ -177,6 +177,59 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     return r;
 }
 
+// The division-class ops (UDIV UREM SDIV SREM SMOD MUL_NOOVF_U) share ONE
+// inlined u_divmod_nz: operands are prepared per op (sign-extend + magnitude
+// for the signed ops; (2^w-1, A) for the overflow test), divided once, and the
+// quotient / remainder post-processed per op.  Six inlined copies of Knuth D
+// made the kernel's code ~4x larger than its hot loop (instruction-cache
+// misses, SQ_WAIT_INST_ANY).  z3 semantics for a zero divisor are kept:
+// udiv -> ones, urem/srem/smod -> a, sdiv -> (a < 0 ? 1 : -1).
+DEV bool bv_is_div(uint32_t op) {
+    return op == BV_UDIV || op == BV_UREM || op == BV_SDIV || op == BV_SREM || op == BV_SMOD ||
+           op == BV_MUL_NOOVF_U;
+}
+DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const U256 &B) {
+    const bool sgn = op == BV_SDIV || op == BV_SREM || op == BV_SMOD;   // wave-uniform
+    U256 a = A, b = B;
+    bool na = false, nb = false;
+    if (sgn) {                                  // magnitudes of the width-bit signed operands
+        a = bv_sext(A, width);
+        b = bv_sext(B, width);
+        na = u_isneg(a);
+        nb = u_isneg(b);
+        if (na) a = u_neg(a);
+        if (nb) b = u_neg(b);
+    }
+    U256 keep = b;                              // divisor magnitude (SMOD) / B (MUL_NOOVF_U)
+    if (op == BV_MUL_NOOVF_U) { keep = B; b = A; a = bv_mask(u_ones(), rc); }
+    const bool bz = u_iszero(b);
+    U256 q = u_ones(), r = a;                   // b == 0: q = ones, r = a
+    if (!bz) u_divmod_nz(a, b, q, r);
+    switch (op) {
+    case BV_UDIV: return q;
+    case BV_UREM: return r;
+    case BV_SDIV: return bz ? (na ? u_small(1) : u_ones()) : ((na != nb) ? u_neg(q) : q);
+    case BV_SREM: return na ? u_neg(r) : r;     // b == 0: the signed dividend
+    case BV_SMOD: {
+        const U256 s = na ? u_neg(r) : r;       // srem: sign of the dividend
+        if (bz || u_iszero(s) || u_isneg(s) == nb) return s;
+        return u_add(s, nb ? u_neg(keep) : keep);   // smod: sign of the divisor
+    }
+    default:                                    // MUL_NOOVF_U: a*b <= 2^w-1 <=> b <= floor((2^w-1)/a)
+        return u_small(!u_lt(q, keep));         // a == 0: q = ones; b == 0: never less
+    }
+}
+
+// ops whose 256-bit result may have bits at or above `width`: only these are
+// masked (the comparisons, Boolean connectives and overflow tests produce 0/1)
+#define BV_MASK_OPS ((1ull << BV_COPY) | (1ull << BV_ADD) | (1ull << BV_SUB) | (1ull << BV_MUL) | \
+                     (1ull << BV_UDIV) | (1ull << BV_SDIV) | (1ull << BV_SREM) | (1ull << BV_SMOD) | \
+                     (1ull << BV_NOT) | (1ull << BV_NEG) | (1ull << BV_SHL) | (1ull << BV_ASHR) | \
+                     (1ull << BV_EXTRACT) | (1ull << BV_CONCAT) | (1ull << BV_SEXT) | (1ull << BV_ITE) | \
+                     (1ull << BV_TAB) | (1ull << BV_SMIN) | (1ull << BV_SMAX) | (1ull << BV_ZEXT) | \
+                     (1ull << BV_AND) | (1ull << BV_OR) | (1ull << BV_XOR) | (1ull << BV_LSHR) | \
+                     (1ull << BV_UREM) | (1ull << BV_UMIN) | (1ull << BV_UMAX))
+
 // MG_BV_WAVES: minimum waves per SIMD the register allocation must allow (0
 // leaves the compiler's choice).  8 caps the kernel at 64 VGPRs (a few spill to
 // scratch); with the scalar-load instruction fetch the block's LDS is its 16 KiB of
@@ -240,14 +293,19 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     for (uint32_t d = d0; d < d1; ++d) {
         const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
         U256 acc = u_zero();
+        // scalar fetch one instruction ahead: the s_load of instruction p+1 is in
+        // flight while instruction p executes
+        uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
+        if (!kLdsProg && p0 < p1) nxt = insns[i0 + uni(p0)];
         for (uint32_t p = p0; p < p1; ++p) {
             uint32_t w0, ra, rb, rc;
             if (kLdsProg) {
                 const uint4 ins = prog[p];
                 w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
             } else {
-                const uint4 ins = insns[i0 + uni(p)];
+                const uint4 ins = nxt;
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
+                if (p + 1u < p1) nxt = insns[i0 + uni(p + 1u)];
             }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
             U256 A = bv_fetch(c, acc, ra);
@@ -262,15 +320,11 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             case BV_SEXT: r = bv_sext(A, rb); break;
             default: {
                 U256 B = bv_fetch(c, acc, rb);
+                if (bv_is_div(op)) { r = bv_divop(op, width, rc, A, B); break; }
                 switch (op) {
                 case BV_ADD: r = u_add(A, B); break;
                 case BV_SUB: r = u_sub(A, B); break;
                 case BV_MUL: r = u_mul(A, B); break;
-                case BV_UDIV: r = z_udiv(A, B); break;
-                case BV_UREM: r = z_urem(A, B); break;
-                case BV_SDIV: r = z_sdiv(bv_sext(A, width), bv_sext(B, width)); break;
-                case BV_SREM: r = z_srem(bv_sext(A, width), bv_sext(B, width)); break;
-                case BV_SMOD: r = z_smod(bv_sext(A, width), bv_sext(B, width)); break;
                 case BV_AND: r = u_and(A, B); break;
                 case BV_OR: r = u_or(A, B); break;
                 case BV_XOR: r = u_xor(A, B); break;
@@ -309,16 +363,6 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     r = u_small(!ovf);
                     break;
                 }
-                case BV_MUL_NOOVF_U: {  // high w bits of the 2w-bit product are 0
-                    bool ovf;
-                    if (u_iszero(A) || u_iszero(B)) ovf = false;
-                    else {
-                        const U256 q = z_udiv(bv_mask(u_ones(), rc), A);
-                        ovf = u_lt(q, B);   // a*b > 2^w - 1  <=>  b > floor((2^w-1)/a)
-                    }
-                    r = u_small(!ovf);
-                    break;
-                }
                 case BV_SUB_NOUDF_U: r = u_small(!u_lt(A, B)); break;
                 case BV_TAB: r = bv_table(c, A, B, rc); break;
                 case BV_UMIN: r = u_select(u_lt(B, A), B, A); break;
@@ -329,7 +373,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
             }
             }
-            if (width < 256u) r = bv_mask(r, width);     // width is wave-uniform
+            if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);   // uniform
             acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;

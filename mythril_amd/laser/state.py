@@ -98,6 +98,12 @@ class MachineStack(list):
         except IndexError:
             raise StackUnderflowException("Trying to access a stack element which doesn't exist")
 
+    def __add__(self, other):
+        raise NotImplementedError("Implement this if needed")      # machine_state.py:80-92
+
+    def __iadd__(self, other):
+        raise NotImplementedError("Implement this if needed")
+
 
 class Memory:
     """memory.py:28-208 at concrete offsets: a byte is an int or, for a symbolic
@@ -193,6 +199,35 @@ class MachineState:
     @property
     def memory_size(self) -> int:
         return len(self.memory)
+
+    def calculate_extension_size(self, start: int, size: int) -> int:
+        """machine_state.py:132-146 (the old size rounds DOWN to words)."""
+        if self.memory_size > start + size:
+            return 0
+        return ((start + size + 31) // 32 - self.memory_size // 32) * 32
+
+    def calculate_memory_gas(self, start: int, size: int) -> int:
+        """machine_state.py:148-166 (GAS_MEMORY 3, quadratic denominator 512)."""
+        old = self.memory_size // 32
+        new = (start + size + 31) // 32
+        return (new * 3 + new * new // 512) - (old * 3 + old * old // 512)
+
+    def check_gas(self) -> None:
+        if self.min_gas_used > self.gas_limit:
+            raise OutOfGasException()
+
+    def mem_extend(self, start, size) -> None:
+        """machine_state.py:171-191: a symbolic start or size extends nothing."""
+        if any(isinstance(x, Expression) and x.symbolic for x in (start, size)):
+            return
+        start, size = concrete(start), concrete(size)
+        m_extend = self.calculate_extension_size(start, size)
+        if m_extend:
+            gas = self.calculate_memory_gas(start, size)
+            self.min_gas_used += gas
+            self.max_gas_used += gas
+            self.check_gas()
+            self.memory.extend(m_extend)
 
     def pop(self, amount: int = 1):
         if amount > len(self.stack):

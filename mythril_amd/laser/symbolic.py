@@ -72,6 +72,11 @@ class SymbolicCalldata:
         item = symbol_factory.BitVecVal(item, 256) if isinstance(item, int) else item
         return If(item < self._size, self._calldata[item], symbol_factory.BitVecVal(0, 8))
 
+    def __getitem__(self, item) -> BitVec:
+        """calldata.py:57-64 for an int or expression index: one byte,
+        If(index < calldatasize, calldata[index], 0) (calldata.py:253-262)."""
+        return self._load(item)
+
     def get_word_at(self, offset) -> BitVec:
         """BaseCalldata.get_word_at: Concat of the 32 loads at offset + k."""
         off = symbol_factory.BitVecVal(offset, 256) if isinstance(offset, int) else offset

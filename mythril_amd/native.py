@@ -38,7 +38,7 @@ def _command(out: str):
     # -structurizecfg-skip-uniform-regions: the interpreters' opcode switches
     # branch on wave-uniform values (readfirstlane); left unstructured they are
     # plain scalar branches instead of an exec-masked flag chain through every
-    # case.  A/B on MI355X (scripts/gpu_ab_skip.sh): kernel 2 C4 8.0 -> 11.9 G
+    # case.  A/B on MI355X (scripts/archive/gpu_ab_skip.sh): kernel 2 C4 8.0 -> 11.9 G
     # constraint-evals/s (VGPRs 101 -> 69), kernel 1 C2 36.6 -> 38.4 G lane-steps/s.
     return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
             "-mllvm", "-structurizecfg-skip-uniform-regions=true",

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel 2 on the C4 op mix only (65,536 DAGs x 4,096 models, 3 timed runs):
 the short, fixed workload behind the rocprofv3 counter passes of kernel-2
-A/Bs (scripts/gpu_r02c.sh).  Prints ms per launch and G constraint-evals/s."""
+A/Bs (scripts/archive/gpu_r02c.sh).  Prints ms per launch and G constraint-evals/s."""
 import json
 import sys
 from pathlib import Path

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-pattern SQ instruction counts per wave of kernel 1 (scripts/gpu_pmc_op.sh)."""
+"""Per-pattern SQ instruction counts per wave of kernel 1 (scripts/archive/gpu_pmc_op.sh)."""
 import csv
 import sys
 from collections import defaultdict

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of the SQ counter passes written by scripts/gpu_pmc.sh."""
+"""Per-kernel averages of the SQ counter passes written by scripts/archive/gpu_pmc.sh."""
 import csv
 import sys
 from collections import defaultdict

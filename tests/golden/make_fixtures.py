@@ -19,6 +19,9 @@ and expected outputs taken from the reference's test suite — never source text
 * keccak_cases.json <- tests/laser/keccak_tests.py:7-145 (inputs and expected sat/unsat)
 * disassembly.json  <- tests/disassembler_test.py:8-10 (code, 3,523 instructions)
 * model_cases.json  <- tests/laser/smt/model_test.py:5-56
+* state_cases.json  <- tests/laser/state/{calldata,storage,mstate,mstack}_test.py: the
+                       module-level parametrize tables (ast.literal_eval) and the
+                       fixed cases' literal inputs / expected values
 
 Usage:  python tests/golden/make_fixtures.py [--reference /root/reference]
 """
@@ -278,6 +281,66 @@ def make_shift_rows(ref: Path):
     return out
 
 
+def _module_tables(path: Path, names):
+    """Module-level `name = <literal>` assignments of a test file."""
+    out = {}
+    for node in ast.parse(path.read_text()).body:
+        if isinstance(node, ast.Assign) and len(node.targets) == 1 and \
+                getattr(node.targets[0], "id", None) in names:
+            out[node.targets[0].id] = ast.literal_eval(node.value)
+    return out
+
+
+def make_state_cases(ref: Path):
+    st = ref / "tests/laser/state"
+    cd = _module_tables(st / "calldata_test.py", {"uninitialized_test_data"})
+    sto = _module_tables(st / "storage_test.py", {"storage_uninitialized_test_data"})
+    ms = _module_tables(st / "mstate_test.py", {"memory_extension_test_data", "stack_pop_too_many_test_data",
+                                               "stack_pop_test_data"})
+    return {
+        "calldata": {
+            # calldata_test.py:8-25: calldata[100] == 0 and get_word_at(200) == 0
+            "uninitialized": [list(x) for x in cd["uninitialized_test_data"]],
+            "uninitialized_reads": {"index": 100, "word_at": 200, "expected": 0},
+            # calldata_test.py:28-39: calldatasize of 7 concrete bytes evaluates to 7
+            "calldatasize": {"data": [1, 4, 7, 3, 7, 2, 9], "expected": 7},
+            # calldata_test.py:42-55: calldata[2] == 3 is unsat (the byte is 7)
+            "constrain_index": {"data": [1, 4, 7, 3, 7, 2, 9], "index": 2, "value": 3, "sat": False},
+            # calldata_test.py:58-73: symbolic calldata[51] == 1 with calldatasize == 50 is unsat
+            "symbolic_index": {"index": 51, "size": 50, "value": 1, "sat": False},
+            # calldata_test.py:76-91: index_a == index_b and calldata[a] != calldata[b] is unsat
+            "symbolic_equal_indices": {"sat": False},
+        },
+        "storage": {
+            # storage_test.py:9-38: (initial {key: value}, read key): concrete -> 0, symbolic -> an Expression
+            "uninitialized": [[{str(k): v for k, v in init.items()}, key]
+                              for init, key in sto["storage_uninitialized_test_data"]],
+            # storage_test.py:41-61
+            "set_item": {"key": 1, "value": 13},
+            "change_item": {"key": 1, "values": [12, 14], "expected": 14},
+        },
+        "mstate": {
+            # mstate_test.py:9-26: (initial size, start, extension size) -> max(initial, ceil32(start + ext))
+            "memory_extension": [list(x) for x in ms["memory_extension_test_data"]],
+            # mstate_test.py:29-39: (initial stack size, overflow) -> StackUnderflowException
+            "stack_pop_too_many": [list(x) for x in ms["stack_pop_too_many_test_data"]],
+            # mstate_test.py:42-63: (stack, amount, expected popped)
+            "stack_pop": [[list(a), n, list(e)] for a, n, e in ms["stack_pop_test_data"]],
+            # mstate_test.py:90-103: zeroed memory around writes
+            "memory_zeroed": {"extend": 2032, "byte": [11, 10], "word": [2000, 0x12345],
+                              "zero_bytes": [10, 100], "zero_word": 1000},
+            # mstate_test.py:106-127
+            "memory_write": {"extend": 232, "byte": [11, 10], "sym_byte": 12, "word": [200, 0x12345],
+                             "sym_word": 100, "expect_byte": [[0, 0], [11, 10], [231, 0x45]]},
+        },
+        "mstack": {
+            # mstack_test.py:8-56: constructor, append, STACK_LIMIT overflow, pop underflow,
+            # `+` / `+=` unsupported
+            "constructor": [1, 2], "limit": 1024, "pop": {"stack": [2], "value": 2},
+        },
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
@@ -293,6 +356,7 @@ def main():
         "model_cases.json": make_model_cases(ref),
         "loop_count.json": make_loop_counts(ref),
         "bytecodes.json": make_bytecodes(ref),
+        "state_cases.json": make_state_cases(ref),
         "keccak_kat.json": {
             # keccak_function_manager.py:92 — keccak256(b"") as a decimal integer
             "empty": "89477152217924674838424037953991966239322087453347756267410168184682657981552",

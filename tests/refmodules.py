@@ -13,6 +13,9 @@ and issues as running every hook on the host.
   only for constant constraint sets (concrete lanes produce nothing else) and
   records (swc, ostate address, operator, end address) instead of an Issue.
 * TxOrigin: dependence_on_origin.py:18-107.
+* UserAssertions, Exceptions: user_assertions.py:30-126, exceptions.py:36-151,
+  with the issue-filing tail (get_transaction_sequence stubbed over the
+  constant constraint sets of concrete lanes; UnsatError drops the issue).
 * DetectionModule.execute: analysis/module/base.py:72-96 (the cache check).
 """
 from __future__ import annotations
@@ -300,23 +303,79 @@ class ArbitraryJump(_Base):
         return [(self.swc_id, state.get_current_instruction()["address"], state.environment.code.bytecode)]
 
 
+class UnsatError(Exception):
+    """mythril/exceptions.py UnsatError."""
+
+
+class IssueAnnotation:
+    """analysis/issue_annotation.py: the issue a detector filed on a state."""
+
+    def __init__(self, conditions, issue, detector):
+        self.conditions = conditions
+        self.issue = issue
+        self.detector = detector
+
+
+def get_transaction_sequence(state, constraints):
+    """analysis/solver.py get_transaction_sequence, stubbed: UnsatError when the
+    (constant) constraint set is unsat, else the ids of the path's transactions
+    (the concrete model the reference would minimise is not rebuilt here)."""
+    if not _sat(constraints):
+        raise UnsatError()
+    return {"steps": [str(getattr(tx, "id", tx)) for tx in state.world_state.transaction_sequence]}
+
+
+def _abi_string(data: bytes):
+    """eth_abi.decode_single("string", data) for a well-formed head + tail."""
+    off = int.from_bytes(data[:32], "big")
+    n = int.from_bytes(data[off:off + 32], "big")
+    if off + 32 + n > len(data):
+        raise ValueError("short string")
+    return data[off + 32: off + 32 + n].decode("utf8")
+
+
 class UserAssertions(_Base):
-    """user_assertions.py:30-126, the MSTORE half: a concrete value carrying the
-    assertion-failed pattern is an issue (the LOG1 half reads memory and stays a
-    host hook)."""
+    """user_assertions.py:30-126: an MSTORE of a value carrying the
+    assertion-failed pattern, or a LOG1 with the AssertionFailed(string) topic,
+    files an issue when the path's constraints have a model (the MSTORE hook is
+    device-deferred, LOG1 reads memory: a host hook).  An issue is recorded as
+    (swc, address, description tail, bytecode) and annotated on the state."""
     swc_id = "110"
-    pre_hooks = ["MSTORE"]
+    pre_hooks = ["LOG1", "MSTORE"]
     post_hooks: List[str] = []
     mstore_pattern = "0xcafecafecafecafecafecafecafecafecafecafecafecafecafecafecafe"
+    assertion_failed_hash = 0xB42604CB105A16C8F6DB8A41E6B00C0C1B4826465E8BC504B3EB3E88B3E6A4A0
 
     def _execute(self, state):
-        value = state.mstate.stack[-2]
-        if value.symbolic:
+        opcode = state.get_current_instruction()["opcode"]
+        message = None
+        if opcode == "MSTORE":
+            value = state.mstate.stack[-2]
+            if value.symbolic:
+                return []
+            if self.mstore_pattern not in hex(value.value)[:126]:
+                return []
+            message = "Failed property id {}".format(value.value & 0xFFFF)
+        else:
+            topic, size, mem_start = state.mstate.stack[-3:]
+            if topic.symbolic or topic.value != self.assertion_failed_hash:
+                return []
+            if not mem_start.symbolic and not size.symbolic:
+                try:
+                    message = _abi_string(bytes(state.mstate.memory[mem_start.value + 32:
+                                                                    mem_start.value + size.value]))
+                except Exception:
+                    pass
+        try:
+            seq = get_transaction_sequence(state, state.world_state.constraints)
+        except UnsatError:
             return []
-        if self.mstore_pattern not in hex(value.value)[:126]:
-            return []
-        return [(self.swc_id, state.get_current_instruction()["address"], value.value & 0xFFFF,
-                 state.environment.code.bytecode)]
+        tail = ("A user-provided assertion failed with the message '{}'".format(message) if message
+                else "A user-provided assertion failed.")
+        issue = (self.swc_id, state.get_current_instruction()["address"], tail, state.environment.code.bytecode)
+        state.annotate(IssueAnnotation(conditions=[And(*state.world_state.constraints)], issue=(issue, seq),
+                                       detector=self))
+        return [issue]
 
 
 class LastJumpAnnotation:
@@ -329,21 +388,58 @@ class LastJumpAnnotation:
         return LastJumpAnnotation(self.last_jump)
 
 
+PANIC_SIGNATURE = [78, 72, 123, 113]          # exceptions.py:20: Panic(uint256)
+
+
+def is_assertion_failure(state) -> bool:
+    """exceptions.py:140-151."""
+    offset, length = state.mstate.stack[-1], state.mstate.stack[-2]
+    if offset.symbolic or length.symbolic:
+        return False
+    data = state.mstate.memory[offset.value: (offset.value + length.value) & ((1 << 256) - 1)]
+    return list(data[:4]) == PANIC_SIGNATURE and len(data) > 0 and data[-1] == 1
+
+
 class Exceptions(_Base):
-    """exceptions.py:36-137, the JUMP half: every JUMP records its address in the
-    state's LastJumpAnnotation (INVALID and REVERT end the path: host hooks)."""
+    """exceptions.py:36-137: JUMP records its address in the state's
+    LastJumpAnnotation (device-deferred); INVALID and an assertion-failure
+    REVERT (host hooks) file an issue at the last jump's address when the path
+    has a model, unless (last jump, code) is cached (auto_cache off: the module
+    caches by source location itself)."""
     swc_id = "110"
-    pre_hooks = ["JUMP"]
+    pre_hooks = ["INVALID", "JUMP", "REVERT"]
     post_hooks: List[str] = []
+    auto_cache = False
 
     def _execute(self, state):
+        issues = self._analyze_state(state)
+        for issue in issues:
+            self.cache.add((issue[2], issue[-1]))          # (source_location, code)
+        return issues
+
+    def _analyze_state(self, state):
+        opcode = state.get_current_instruction()["opcode"]
         address = state.get_current_instruction()["address"]
         annotations = [a for a in state.get_annotations(LastJumpAnnotation)]
         if len(annotations) == 0:
             state.annotate(LastJumpAnnotation())
             annotations = [a for a in state.get_annotations(LastJumpAnnotation)]
-        annotations[0].last_jump = address
-        return []
+        if opcode == "JUMP":
+            annotations[0].last_jump = address
+            return []
+        if opcode == "REVERT" and not is_assertion_failure(state):
+            return []
+        cache_address = annotations[0].last_jump
+        if (cache_address, state.environment.code.bytecode) in self.cache:
+            return []
+        try:
+            seq = get_transaction_sequence(state, state.world_state.constraints)
+        except UnsatError:
+            return []
+        issue = (self.swc_id, address, cache_address, state.environment.code.bytecode)
+        state.annotate(IssueAnnotation(conditions=[And(*state.world_state.constraints)], issue=(issue, seq),
+                                       detector=self))
+        return [issue]
 
 
 class StateChangeCallsAnnotation:

@@ -112,3 +112,39 @@ def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
     fs, sc, _ = dev.eval(prog, pool)
     rfs, rsc = eval_batch(prog, pool)
     assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
+
+
+@pytest.mark.parametrize("w", [8, 64, 255, 256])
+def test_division_class_ops_at_every_width(dev, w):
+    """UDIV UREM SDIV SREM SMOD and the unsigned multiply-overflow test share one
+    division site in the kernel (bv_divop): each op at width w, against values
+    at the sign / zero / all-ones edges (z3 zero-divisor semantics)."""
+    from mythril_amd.smt.expr import (BVMulNoOverflow, SDiv, SMod, SRem, UDiv, URem,
+                                      symbol_factory)
+    BVS = symbol_factory.BitVecSym
+    x, y, z = BVS("x", w), BVS("y", w), BVS("z", w)
+    sets = []
+    for f in (UDiv, URem, SDiv, SRem, SMod):
+        sets.append([f(x, y) == z])
+        sets.append([f(y, x) == z])
+    sets.append([BVMulNoOverflow(x, y, False)])
+    sets.append([BVMulNoOverflow(y, z, False)])
+    prog, kept = compile_sets(sets)
+    assert len(kept) == len(sets)
+    m = (1 << w) - 1
+    edges = [0, 1, 2, 3, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1, (1 << (w - 1)) + 1]
+    rng = random.Random(w)
+    from mythril_amd.smt import semantics
+    models = []
+    for k in range(1024):
+        a = rng.choice(edges) if k % 3 else rng.getrandbits(w)
+        b = rng.choice(edges) if k % 2 else rng.getrandbits(rng.choice([1, 5, w // 2 + 1, w]))
+        op = ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")[k % 5]
+        # every 4th model makes the first constraint of op k % 5 true
+        c = semantics.apply_op(op, w, [a, b], [w, w], None) if k % 4 == 0 else rng.getrandbits(w)
+        models.append({"x": a, "y": b, "z": c & m})
+    pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
+    fs, sc, _ = dev.eval(prog, pool)
+    rfs, rsc = eval_batch(prog, pool)
+    assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
+    assert (sc[:10] > 0).all()

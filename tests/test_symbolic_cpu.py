@@ -192,7 +192,7 @@ def test_lane_encoding_of_memory_and_storage_round_trips():
     s = _run_restatement(_MEMPROG, 13)
     le = sym.encode_state(s)
     assert le.symbolic and le.store is not None and len(le.mem) == 32
-    b = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=64, const_cap=32))
+    b = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=128, const_cap=32))
     le.write(b, 0)
     b.sp[0] = len(s.mstate.stack)
     b.msize[0] = len(s.mstate.memory)

@@ -22,7 +22,7 @@ DEFAULT_SET = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJ
                "Exceptions", "StateChangeAfterCall")
 
 
-def _txs(n_c2=24, n_under=8, n_origin=8):
+def _txs(n_c2=24, n_under=8, n_origin=8, extra=()):
     out = []
     b = workloads.c2_batch(n_c2, seed=33, stack_cap=64, mem_cap=1024)
     code = Disassembly(workloads.bytecode("overflow.sol.o"))
@@ -38,7 +38,7 @@ def _txs(n_c2=24, n_under=8, n_origin=8):
             gas_limit=int(b.gas_limit[i]), origin=workloads.ATTACKER, call_value=0))
     import random
     rnd = random.Random(7)
-    for name, n in (("underflow.sol.o", n_under), ("origin.sol.o", n_origin)):
+    for name, n in (("underflow.sol.o", n_under), ("origin.sol.o", n_origin)) + tuple(extra):
         dis = Disassembly(workloads.bytecode(name))
         sels = sorted({ins["argument"] for ins in dis.instruction_list
                        if ins["opcode"] == "PUSH4" and isinstance(ins.get("argument"), str)})
@@ -57,7 +57,7 @@ def _txs(n_c2=24, n_under=8, n_origin=8):
     return out
 
 
-def _run(strategy, mode, monkeypatch, device=None, modules=("IntegerArithmetics", "TxOrigin")):
+def _run(strategy, mode, monkeypatch, device=None, modules=("IntegerArithmetics", "TxOrigin"), extra=()):
     """mode: "device" (batch-safe hooks as device actions), "host" (every module
     hook on the host), "every" (every opcode a host event)."""
     monkeypatch.undo()
@@ -84,7 +84,7 @@ def _run(strategy, mode, monkeypatch, device=None, modules=("IntegerArithmetics"
         ends.append((tag[id(tx)], state.mstate.pc, revert, bool(sa), tuple(got), str(stack), str(pots),
                      tuple(jumps)))
     vm.register_laser_hooks("transaction_end", end)
-    for k, tx in enumerate(_txs()):
+    for k, tx in enumerate(_txs(extra=extra)):
         _setup_global_state_for_execution(vm, tx)
         tag[id(tx)] = k
     vm.exec()
@@ -193,3 +193,18 @@ def test_taint_capacity_escapes_resume_in_place(strategy, monkeypatch):
     assert steps_d == steps_h
     assert ends_d == ends_h
     assert issues_d == issues_h
+
+
+def test_exception_issues_filed_at_the_last_jump(monkeypatch):
+    """Exceptions' issue tail (exceptions.py:89-137): concrete calls into
+    exceptions.sol.o reach INVALID; the issue is filed at the LastJumpAnnotation
+    the device kept, once per (last jump, code), the same as with host hooks."""
+    extra = (("exceptions.sol.o", 16),)
+    ends_d, issues_d, _, steps_d = _run(BreadthFirstSearchStrategy, "device", monkeypatch,
+                                        modules=DEFAULT_SET, extra=extra)
+    ends_h, issues_h, _, steps_h = _run(BreadthFirstSearchStrategy, "host", monkeypatch,
+                                        modules=DEFAULT_SET, extra=extra)
+    assert (steps_d, ends_d, issues_d) == (steps_h, ends_h, issues_h)
+    ex = [i for i in issues_d if i[0] == "110"]
+    assert ex and all(i[2] is not None for i in ex)
+    assert len({(i[2], i[3]) for i in ex}) == len(ex)
