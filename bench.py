@@ -530,11 +530,17 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     counted.  Runtime codes are analysed as `myth analyze -f` does (symbolic
     storage); flag_array is deployed concretely first.  `replicas` copies of the
     deployed world state run together (one contract per replica, independent
-    paths) for a batch that fills the GPU; replicas=1 is one analysis."""
+    paths) for a batch that fills the GPU; replicas=1 is one analysis.  With
+    N ranks, replicas x N copies are dealt over the ranks and the open states
+    are rebalanced at every transaction boundary (laser/sharded.py
+    execute_symbolic_transactions): per-GPU work is fixed (weak scaling); the
+    whole-job rates sum the ranks' work over the slowest rank's wall time."""
     from copy import copy
     from mythril_amd import workloads
     from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, Disassembly, LaserEVM, WorldState,
                                    execute_contract_creation)
+    from mythril_amd import dist as mdist
+    from mythril_amd.laser.sharded import execute_symbolic_transactions
     from mythril_amd.laser.transaction import ACTORS, tx_id_manager
     from mythril_amd.laser.witness import WitnessSeeds
     from mythril_amd.smt import solver
@@ -544,7 +550,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
                      "+ symbolic lane-steps/s (kernel 1)",
            "mode": "prefilter-only: no SMT backend in the image; queries no candidate satisfies "
                    "are UNKNOWN and their paths kept; escaped paths dropped (counted)",
-           "transactions": tx_count, "replicas": replicas, "seed_models": n_seeds, "contracts": {}}
+           "transactions": tx_count, "replicas_per_gpu": replicas, "seed_models": n_seeds, "contracts": {}}
     saved_cache = solver.model_cache
     try:
         for name in SYMBOLIC_TX_CODES:
@@ -580,10 +586,13 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
             ends = {"return_or_stop": 0, "revert": 0}
             laser.register_laser_hooks("transaction_end", lambda s, tx, r, revert: ends.__setitem__(
                 "revert" if revert else "return_or_stop", ends["revert" if revert else "return_or_stop"] + 1))
-            laser.open_states = [copy(ws) for _ in range(replicas)]
+            rank, world = mdist.rank_world()
+            laser.open_states = [copy(ws) for _ in range(replicas * world)]
             t0 = time.perf_counter()
-            laser.execute_transactions(addr)
+            execute_symbolic_transactions(laser, addr)
             wall = time.perf_counter() - t0
+            job_wall, job_steps = mdist.reduce_timing(wall, float(laser.lane_steps))
+            _, job_evals = mdist.reduce_timing(wall, float(mc.device_evals))
             k1_s, k2_s = laser.device_ms / 1e3, mc.device_ms / 1e3
             st = mc.stats
             answered = st["lru_hits"] + st["seed_hits"]
@@ -601,6 +610,8 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
                 "constraint_evals_per_s_kernel": mc.device_evals / k2_s if k2_s else None,
                 "constraint_evals_per_s_wall": mc.device_evals / wall,
                 "keccak_symbolic_inputs": sum(len(v) for v in keccak_function_manager.symbolic_inputs.values()),
+                "ranks": world, "job_lane_steps_per_s": job_steps / job_wall,
+                "job_constraint_evals_per_s_wall": job_evals / job_wall,
             }
     finally:
         solver.model_cache = saved_cache

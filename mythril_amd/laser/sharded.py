@@ -77,62 +77,158 @@ def exchange_coverage(laser_evm) -> Dict[str, np.ndarray]:
     return union
 
 
-def _encode_model(model) -> list:
-    """A Model as plain data (every internal ModelRef's assignment)."""
+# ---------------------------------------------------------------- models over a tensor
+# A model travels as a stream of u32 words (no pickled objects): the stream of
+# every rank rides one RCCL all-gather (dist.allgather_models, [k, 1, 8] rows).
+#   stream  := n_models model*
+#   model   := n_refs ref*
+#   ref     := n_items item*
+#   item    := name kind (int: big | array: big(default) n (big big)* |
+#                         func: big(else) n (n_args big* big)*)
+#   name    := n_bytes word*   (utf-8, zero padded)
+#   big     := n_limbs limb*   (little-endian u32 limbs)
+def _put_big(out: list, v: int) -> None:
+    v = int(v)
+    limbs = []
+    while v:
+        limbs.append(v & 0xFFFFFFFF)
+        v >>= 32
+    out.append(len(limbs))
+    out.extend(limbs)
+
+
+def _put_name(out: list, name: str) -> None:
+    b = name.encode()
+    out.append(len(b))
+    b = b + b"\0" * (-len(b) % 4)
+    out.extend(int.from_bytes(b[k:k + 4], "little") for k in range(0, len(b), 4))
+
+
+def _models_to_words(models) -> np.ndarray:
     from ..smt.program import ArrayInterp, FuncInterp
-    out = []
-    for ref in getattr(model, "raw", [model]):
-        asg = {}
-        for name, v in ref.assignment.items():
-            if isinstance(v, ArrayInterp):
-                asg[name] = ("A", v.default, dict(v.entries))
-            elif isinstance(v, FuncInterp):
-                asg[name] = ("F", v.else_value, dict(v.entries))
-            else:
-                asg[name] = int(v)
-        out.append(asg)
-    return out
+    out = [len(models)]
+    for m in models:
+        refs = getattr(m, "raw", [m])
+        out.append(len(refs))
+        for ref in refs:
+            items = list(ref.assignment.items())
+            out.append(len(items))
+            for name, v in items:
+                _put_name(out, name)
+                if isinstance(v, ArrayInterp):
+                    out.append(1)
+                    _put_big(out, v.default)
+                    out.append(len(v.entries))
+                    for k, x in v.entries.items():
+                        _put_big(out, k)
+                        _put_big(out, x)
+                elif isinstance(v, FuncInterp):
+                    out.append(2)
+                    _put_big(out, v.else_value)
+                    out.append(len(v.entries))
+                    for args, x in v.entries.items():
+                        out.append(len(args))
+                        for a in args:
+                            _put_big(out, a)
+                        _put_big(out, x)
+                else:
+                    out.append(0)
+                    _put_big(out, v)
+    return np.asarray(out, dtype=np.uint32)
 
 
-def _decode_model(refs: list):
+class _Words:
+    def __init__(self, w):
+        self.w, self.k = w, 0
+
+    def u(self) -> int:
+        x = int(self.w[self.k])
+        self.k += 1
+        return x
+
+    def big(self) -> int:
+        n = self.u()
+        v = 0
+        for j in range(n):
+            v |= int(self.w[self.k + j]) << (32 * j)
+        self.k += n
+        return v
+
+    def name(self) -> str:
+        n = self.u()
+        nw = (n + 3) // 4
+        b = b"".join(int(x).to_bytes(4, "little") for x in self.w[self.k:self.k + nw])
+        self.k += nw
+        return b[:n].decode()
+
+
+def _words_to_models(words: np.ndarray) -> list:
     from ..smt.program import ArrayInterp, FuncInterp
     from ..smt.solver import Model, ModelRef
+    r = _Words(words)
     models = []
-    for asg in refs:
-        d = {}
-        for name, v in asg.items():
-            if isinstance(v, tuple) and v[0] == "A":
-                d[name] = ArrayInterp(v[1], v[2])
-            elif isinstance(v, tuple) and v[0] == "F":
-                d[name] = FuncInterp(v[1], v[2])
-            else:
-                d[name] = v
-        models.append(ModelRef(d))
-    return Model(models)
+    for _ in range(r.u()):
+        refs = []
+        for _ in range(r.u()):
+            d = {}
+            for _ in range(r.u()):
+                name, kind = r.name(), r.u()
+                if kind == 1:
+                    dflt = r.big()
+                    d[name] = ArrayInterp(dflt, {r.big(): r.big() for _ in range(r.u())})
+                elif kind == 2:
+                    els = r.big()
+                    ent = {}
+                    for _ in range(r.u()):
+                        args = tuple(r.big() for _ in range(r.u()))
+                        ent[args] = r.big()
+                    d[name] = FuncInterp(els, ent)
+                else:
+                    d[name] = r.big()
+            refs.append(ModelRef(d))
+        models.append(Model(refs))
+    return models
+
+
+def _allgather_words(words: np.ndarray) -> List[np.ndarray]:
+    """Every rank's u32 stream (rank order) through one tensor all-gather."""
+    from .. import dist as mdist
+    rank, world = mdist.rank_world()
+    n = int(words.size)
+    rows = np.zeros(((n + 1 + 7) // 8, 1, 8), dtype=np.uint32)
+    flat = rows.reshape(-1)
+    flat[0] = n
+    flat[1:n + 1] = words
+    got = mdist.allgather_models(rows)
+    counts = _allgather_ints(rows.shape[0])
+    out, at = [], 0
+    for c in counts:
+        f = got[at:at + c].reshape(-1)
+        out.append(f[1:1 + int(f[0])] if c else np.zeros(0, dtype=np.uint32))
+        at += c
+    return out
 
 
 def exchange_models(model_cache=None) -> int:
     """the satisfying models every rank found since the last
-    exchange (z3 fallback answers cached by get_model, support/model.py:76-78)
-    join every other rank's candidate pool — kernel 2's ModelCache — in rank
-    order, each with count 1 as a fresh backend model gets.  One all-gather per
-    transaction round; returns the number of peer models received."""
+    exchange (backend answers cached by get_model, support/model.py:76-78)
+    join every other rank's candidate pool -- kernel 2's ModelCache -- in rank
+    order, each with count 1 as a fresh backend model gets.  The models ride a
+    u32 tensor all-gather (dist.allgather_models), one per transaction round;
+    returns the number of peer models received."""
     from .. import dist as mdist
     from ..smt import solver
     cache = model_cache or solver.model_cache
     rank, world = mdist.rank_world()
-    mine = [_encode_model(m) for m in cache.take_fresh()]
+    mine = _models_to_words(cache.take_fresh())
     if world == 1:
         return 0
-    import torch.distributed as dist
-    parts: List[Optional[list]] = [None] * world
-    dist.all_gather_object(parts, mine)
     got = 0
-    for r, models in enumerate(parts):
-        if r == rank:
+    for r, words in enumerate(_allgather_words(mine)):
+        if r == rank or words.size == 0:
             continue
-        for enc in models or []:
-            cache.put(_decode_model(enc), 1, peer=True)
+        for m in _words_to_models(words):
+            cache.put(m, 1, peer=True)
             got += 1
     return got
 
@@ -193,3 +289,234 @@ def execute_message_calls(laser_evm, callee_address, caller_address, origin_addr
 def open_state_counts(laser_evm) -> List[int]:
     """Every rank's number of open world states (rank order)."""
     return _allgather_ints(len(laser_evm.open_states))
+
+
+# ---------------------------------------------------------------- world states across ranks
+class _NodeTable:
+    """Expression DAG nodes as a flat post-order table (op, width, arg indices,
+    param): shared subterms once, no recursion, re-interned on load (Node is
+    hash-consed, so a received term IS the local term wherever both exist)."""
+
+    def __init__(self):
+        self.rows: List[tuple] = []
+        self.index: Dict[int, int] = {}
+        self._keep: List = []
+
+    def add(self, node) -> int:
+        got = self.index.get(id(node))
+        if got is not None:
+            return got
+        stack = [(node, False)]
+        while stack:
+            n, done = stack.pop()
+            if id(n) in self.index:
+                continue
+            if not done:
+                stack.append((n, True))
+                stack.extend((a, False) for a in n.args if id(a) not in self.index)
+                continue
+            self.index[id(n)] = len(self.rows)
+            self._keep.append(n)
+            self.rows.append((n.op, n.width, tuple(self.index[id(a)] for a in n.args), n.param))
+        return self.index[id(node)]
+
+    @staticmethod
+    def load(rows) -> list:
+        from ..smt.expr import Node
+        out: list = []
+        for op, width, args, param in rows:
+            out.append(Node(op, width, tuple(out[a] for a in args), param))
+        return out
+
+
+def _dumps_states(items, shared: Dict[int, int]) -> bytes:
+    """Pickle [(position, world state)] with expression nodes as table rows and
+    rank-global objects (detection modules, the LaserEVM) as references."""
+    import io
+    import pickle
+    from ..smt.expr import Node
+    table = _NodeTable()
+
+    class P(pickle.Pickler):
+        def persistent_id(self, obj):
+            if type(obj) is Node:
+                return ("N", table.add(obj))
+            k = shared.get(id(obj))
+            return None if k is None else ("S", k)
+
+    buf = io.BytesIO()
+    P(buf, protocol=pickle.HIGHEST_PROTOCOL).dump(items)
+    return pickle.dumps((table.rows, buf.getvalue()), protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def _loads_states(blob: bytes, shared_objs: list):
+    import io
+    import pickle
+    rows, payload = pickle.loads(blob)
+    nodes = _NodeTable.load(rows)
+
+    class U(pickle.Unpickler):
+        def persistent_load(self, pid):
+            kind, k = pid
+            return nodes[k] if kind == "N" else shared_objs[k]
+
+    return U(io.BytesIO(payload)).load()
+
+
+def _shared_objects(laser_evm) -> list:
+    """Objects every rank holds once and states only refer to: the LaserEVM and
+    the detection modules whose hooks it runs (an IssueAnnotation's detector)."""
+    objs, seen = [laser_evm], {id(laser_evm)}
+    for table in (getattr(laser_evm, "pre_hooks", {}), getattr(laser_evm, "post_hooks", {})):
+        for hooks in table.values():
+            for h in hooks:
+                m = getattr(h, "__self__", None)
+                if m is not None and id(m) not in seen:
+                    seen.add(id(m))
+                    objs.append(m)
+    return objs
+
+
+def rebalance(laser_evm) -> List[int]:
+    """SURVEY §8(e) rebalancing at a transaction boundary: the open world
+    states of all ranks, in rank-major order, are re-dealt in equal contiguous
+    runs (rank r gets positions [t_r, t_r + n_r), n_r = total // world, the
+    first total % world ranks one more).  Only states that change owner move
+    (one all-gather of pickled states; expression nodes as flat tables).
+    Returns the per-rank counts before the move."""
+    from .. import dist as mdist
+    rank, world = mdist.rank_world()
+    counts = _allgather_ints(len(laser_evm.open_states))
+    if world == 1:
+        return counts
+    total = sum(counts)
+    target = [total // world + (1 if r < total % world else 0) for r in range(world)]
+    tstart = [sum(target[:r]) for r in range(world)]
+    off = sum(counts[:rank])
+
+    def owner(g):
+        for q in range(world):
+            if g < tstart[q] + target[q]:
+                return q
+        return world - 1
+
+    keep, send = [], {}
+    for j, ws in enumerate(laser_evm.open_states):
+        g = off + j
+        q = owner(g)
+        (keep if q == rank else send.setdefault(q, [])).append((g, ws))
+    objs = _shared_objects(laser_evm)
+    shared = {id(o): k for k, o in enumerate(objs)}
+    blob = _dumps_states(send, shared) if send else b""
+    import torch.distributed as dist
+    parts: List[Optional[bytes]] = [None] * world
+    dist.all_gather_object(parts, blob)
+    got = list(keep)
+    for r, b in enumerate(parts):
+        if r == rank or not b:
+            continue
+        got.extend(_loads_states(b, objs).get(rank, []))
+    got.sort(key=lambda x: x[0])
+    laser_evm.open_states = [ws for _, ws in got]
+    return counts
+
+
+def sync_function_managers() -> int:
+    """Every rank registers the keccak inputs (symbolic and concrete) and the
+    concrete EXP points the other ranks registered, so the axioms
+    create_conditions adds cover every term a (moved) state's constraints
+    mention (keccak_function_manager.py:116-179, exponent_function_manager.py:
+    32-60).  Returns the number of entries received."""
+    from .. import dist as mdist
+    from ..smt.exponent_manager import exponent_function_manager as em
+    from ..smt.expr import BitVec
+    from ..smt.keccak_manager import keccak_function_manager as km
+    rank, world = mdist.rank_world()
+    if world == 1:
+        return 0
+    table = _NodeTable()
+    sym = [table.add(x.raw) for xs in km.symbolic_inputs.values() for x in xs]
+    conc = [(table.add(k.raw), table.add(h.raw)) for k, h in km.concrete_hashes.items()]
+    pts = sorted(em.concrete_points.items())
+    import torch.distributed as dist
+    parts: List[Optional[tuple]] = [None] * world
+    dist.all_gather_object(parts, (table.rows, sym, conc, pts))
+    have = {id(x.raw) for xs in km.symbolic_inputs.values() for x in xs}
+    have_c = {id(k.raw) for k in km.concrete_hashes}
+    got = 0
+    for r, part in enumerate(parts):
+        if r == rank or not part:
+            continue
+        rows, s_idx, c_idx, p = part
+        nodes = _NodeTable.load(rows)
+        for i in s_idx:
+            n = nodes[i]
+            if id(n) not in have:
+                have.add(id(n))
+                km.get_function(n.width)
+                x = BitVec(n)
+                func, _ = km.get_function(n.width)
+                km.symbolic_inputs.setdefault(n.width, []).append(x)
+                km.hash_result_store[n.width].append(func(x))
+                got += 1
+        for ki, hi in c_idx:
+            k = nodes[ki]
+            if id(k) not in have_c:
+                have_c.add(id(k))
+                km.get_function(k.width)
+                km.concrete_hashes[BitVec(k)] = BitVec(nodes[hi])
+                got += 1
+        for key, v in p:
+            if tuple(key) not in em.concrete_points:
+                em.concrete_points[tuple(key)] = v
+                got += 1
+    return got
+
+
+def execute_symbolic_transactions(laser_evm, callee_address, tx_count: Optional[int] = None,
+                                  gas_limit: int = 8_000_000, balance: bool = True) -> None:
+    """svm.py:230-275 ``_execute_transactions`` with the open states sharded
+    over the ranks: per transaction round, the states are
+    rebalanced (``rebalance``), filtered for reachability, and each rank runs
+    one symbolic message call per state it owns -- one ``exec()``, its lanes on
+    this rank's GPU.  Transaction ids are the global positions (rank-major),
+    so every rank's counter advances by the global count (transaction_models.py
+    :21-36); after the round the function managers, coverage and fresh models
+    are exchanged.  With one rank this is exactly the single-process loop.
+    The first round deals a replicated start round-robin."""
+    from .. import dist as mdist
+    from .transaction import execute_symbolic_message_call
+    from datetime import datetime
+    rank, world = mdist.rank_world()
+    n = laser_evm.transaction_count if tx_count is None else tx_count
+    for hook in laser_evm._start_exec_trans_hooks:       # svm.py:214-228 execute_transactions
+        hook()
+    laser_evm.time = datetime.now()
+    if world > 1 and not getattr(laser_evm, "_sharded", False):
+        laser_evm.open_states = mdist.shard(laser_evm.open_states, rank, world)
+        laser_evm._sharded = True
+    for _ in range(n):
+        if balance:
+            rebalance(laser_evm)
+        if laser_evm.use_reachability_check:
+            laser_evm.open_states = laser_evm.reachable(laser_evm.open_states)
+        counts = _allgather_ints(len(laser_evm.open_states))
+        if sum(counts) == 0:
+            break
+        base = tx_id_manager._next_transaction_id
+        off = sum(counts[:rank])
+        ids = [str(base + off + j + 1) for j in range(counts[rank])]
+        for hook in laser_evm._start_sym_trans_hooks:
+            hook()
+        execute_symbolic_message_call(laser_evm, callee_address, gas_limit, ids=ids)
+        tx_id_manager.set_counter(base + sum(counts))
+        for hook in laser_evm._stop_sym_trans_hooks:
+            hook()
+        if world > 1:
+            sync_function_managers()
+            if laser_evm.record_coverage:
+                exchange_coverage(laser_evm)
+            exchange_models()
+    laser_evm.executed_transactions = True
+    for hook in laser_evm._stop_exec_trans_hooks:
+        hook()

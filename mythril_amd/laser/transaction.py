@@ -103,22 +103,25 @@ ACTORS = {"CREATOR": 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,
           "SOMEGUY": 0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA}
 
 
-def execute_symbolic_message_call(laser_evm, callee_address, gas_limit: int = 8_000_000) -> None:
+def execute_symbolic_message_call(laser_evm, callee_address, gas_limit: int = 8_000_000,
+                                  ids=None) -> None:
     """transaction/symbolic.py:105-150: one message call per open world state
     with symbolic calldata (``{id}_calldata``, ``{id}_calldatasize``), a
     symbolic sender/origin (``sender_{id}``), gas price and call value, plus
     the constraint that the sender is one of the ACTORS
     (symbolic.py:202-219); then ``laser_evm.exec()``.  The lanes run on the
-    device as symbolic lanes (mythril_amd/laser/symbolic.py)."""
+    device as symbolic lanes (mythril_amd/laser/symbolic.py).  ``ids``: the
+    transaction ids to use, one per open state (sharded runs: the states'
+    global positions), instead of the counter's next ones."""
     from ..smt.expr import Or, symbol_factory
     from .symbolic import SymbolicCalldata
     open_states = laser_evm.open_states[:]
     del laser_evm.open_states[:]
-    for ws in open_states:
+    for k, ws in enumerate(open_states):
         acct = ws[callee_address]
         if getattr(acct, "deleted", False):
             continue
-        txid = tx_id_manager.get_next_tx_id()
+        txid = tx_id_manager.get_next_tx_id() if ids is None else ids[k]
         sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
         tx = MessageCallTransaction(
             world_state=ws, identifier=txid,
