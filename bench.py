@@ -61,6 +61,8 @@ def parse(argv=None):
     ap.add_argument("--taint-lanes", type=int, default=4096,
                     help="lanes of the taint_c2 field (0: off): C2 through LaserEVM with the integer "
                          "and TxOrigin modules' hooks as device actions (taint lanes) and on the host")
+    ap.add_argument("--symbolic-lanes", type=int, default=65536,
+                    help="symbolic lanes for the k_sym_step field (0: skip)")
     ap.add_argument("--symbolic-replicas", type=int, default=8,
                     help="replicas of each contract in the symbolic_tx field (0: off)")
     ap.add_argument("--symbolic-tx", type=int, default=2, help="transactions of the symbolic_tx field (-t)")
@@ -245,6 +247,16 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         _log(rank, f"taint C2 ({args.taint_lanes} lanes)")
         taint = host_profiled("taint_c2", lambda: run_taint_c2(dev, args.taint_lanes, rank))
 
+    symlanes = None
+    if args.symbolic_lanes and gpu and not args.profile_only:
+        _log(rank, f"symbolic lanes ({args.symbolic_lanes}) on k_sym_step")
+        symlanes = run_symbolic_lanes(dev, args.symbolic_lanes)
+
+    taintlanes = None
+    if args.symbolic_lanes and gpu and not args.profile_only:
+        _log(rank, f"taint lanes ({args.symbolic_lanes}) on k_sym_step")
+        taintlanes = run_taint_lanes(dev, args.symbolic_lanes, rank)
+
     symb = None
     if args.symbolic_replicas and gpu and not args.profile_only:
         _log(rank, f"symbolic transactions (-t {args.symbolic_tx}, {args.symbolic_replicas} replicas)")
@@ -302,6 +314,10 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["hooked_c2"] = hooked
         if taint is not None:
             out["taint_c2"] = taint
+        if symlanes is not None:
+            out["symbolic_lanes"] = symlanes
+        if taintlanes is not None:
+            out["taint_lanes"] = taintlanes
         if symb is not None:
             out["symbolic_tx"] = symb
         print(json.dumps(out), flush=True)
@@ -514,6 +530,178 @@ def run_large(dev, args, rank, barrier):
 
 
 SYMBOLIC_TX_CODES = ("overflow.sol.o", "exceptions.sol.o", "flag_array.sol.o")
+
+
+def symbolic_lane_batch(dev, lanes: int):
+    """`lanes` symbolic lanes: the initial state of a symbolic message call
+    (transaction/symbolic.py:105-150: symbolic calldata, sender, value, gas
+    price; symbolic storage, as `myth analyze -f` analyses a runtime code) into
+    each of the reference's precompiled contracts, dealt round-robin.  Returns
+    (LaserEVM, batch)."""
+    from dataclasses import replace
+    from mythril_amd import workloads
+    from mythril_amd.lanes import _ALL_FIELDS, _SYM_FIELDS, LaneBatch, LaneShape
+    from mythril_amd.laser import (Account, BreadthFirstSearchStrategy, Disassembly, LaserEVM,
+                                   MessageCallTransaction, SymbolicCalldata, WorldState)
+    from mythril_amd.laser.transaction import ACTORS
+    from mythril_amd.smt.expr import Or, symbol_factory
+    codes = json.loads((ROOT / "tests" / "golden" / "bytecodes.json").read_text())
+    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    states = []
+    for k, name in enumerate(sorted(codes)):
+        ws = WorldState()
+        ws.put_account(Account(ACTORS["CREATOR"]))
+        acct = Account(workloads.CONTRACT, code=Disassembly(workloads.bytecode(name)), concrete_storage=False)
+        ws.put_account(acct)
+        txid = str(k + 1)
+        sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
+        tx = MessageCallTransaction(world_state=ws, identifier=txid,
+                                    gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256),
+                                    gas_limit=8_000_000, origin=sender, caller=sender, callee_account=acct,
+                                    call_data=SymbolicCalldata(txid),
+                                    call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+        gs = tx.initial_global_state()
+        gs.transaction_stack.append((tx, None))
+        gs.world_state.constraints.append(
+            Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
+        states.append(gs)
+    shape = laser._shape(states)
+    # 65,536 lanes: a 128-word stack and 1 KiB of memory per lane keep the
+    # planes (memory byte tags included) within a few hundred MB
+    shape = replace(shape, stack_cap=128, mem_cap=1024, storage_cap=64, rec_cap=512)
+    small = LaneBatch(shape)
+    for i, gs in enumerate(states):
+        laser._pack(small, i, gs)
+    big = LaneBatch(replace(shape, n=lanes))
+    idx = np.arange(lanes) % len(states)
+    for f in _ALL_FIELDS + _SYM_FIELDS:
+        src = getattr(small, f, None)
+        if src is not None:
+            getattr(big, f)[...] = src[idx]
+    return laser, big
+
+
+def run_symbolic_lanes(dev, lanes: int, reps: int = 5):
+    """k_sym_step at `lanes` lanes: every lane runs from the
+    start of its symbolic message call to its first stop -- MG_FORK at a
+    symbolic JUMPI (the dispatcher's selector compare), an escape or a halt --
+    in one launch.  Timed per launch with the device's HIP events (the events
+    bracket kernel 1's no-op pass over the symbolic lanes too: k_lane_step
+    leaves them to k_sym_step); the image is re-uploaded before each launch,
+    outside the timed region.  The roofline prices the opcode histogram a
+    profiling pass of k_sym_step counts (mg_step_profile) with §8(d)'s table,
+    plus 4 bytes of tag per stack word moved and 16 bytes per arena node
+    created."""
+    from mythril_amd import roofline
+    from mythril_amd.lanes import MG_FORK, STATUS_NAMES, LaneBatch
+    laser, b = symbolic_lane_batch(dev, lanes)
+    n0 = int(b.n_nodes.sum())
+    dev.alloc(b.shape)
+    dev.upload(b)
+    dev.step()
+    ms, steps = [], 0
+    for _ in range(reps):
+        dev.upload(b)
+        st = dev.step()
+        ms.append(st.kernel_ms)
+        steps = st.lane_steps
+    out_b = LaneBatch(b.shape)
+    dev.download(out_b)
+    created = int(out_b.n_nodes.sum()) - n0
+    statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
+                for k, v in zip(*np.unique(out_b.status, return_counts=True))}
+    dev.upload(b)
+    op_counts, extra = dev.step_profile()
+    ops, byts, psteps = roofline.algorithmic_work(op_counts, extra)
+    words = float((op_counts.astype(np.float64) * roofline.WORDS).sum())
+    byts += 4.0 * words + 16.0 * created
+    kms = float(np.median(ms))
+    sec = kms / 1e3
+    gbs, tops = byts / sec / 1e9, ops / sec / 1e12
+    hbm = gbs / roofline.HBM_PEAK_GBS >= tops / roofline.VALU_PEAK_TOPS
+    roof = roofline.with_sustained({
+        "bound": "hbm" if hbm else "valu-int32",
+        "achieved": gbs if hbm else tops,
+        "peak": roofline.HBM_PEAK_GBS if hbm else roofline.VALU_PEAK_TOPS,
+        "unit": "GB/s" if hbm else "T int32-ops/s",
+        "frac": gbs / roofline.HBM_PEAK_GBS if hbm else tops / roofline.VALU_PEAK_TOPS,
+        "traffic": roofline.pmc_traffic("k_sym_step")[0],
+        "kernel": "k_sym_step", "kernel_ms": kms,
+        "algorithmic_bytes_per_launch": byts, "algorithmic_int32_ops_per_launch": ops,
+        "bytes_per_lane_step": byts / max(psteps, 1.0), "int32_ops_per_lane_step": ops / max(psteps, 1.0),
+        "arena_nodes_created": created,
+    })
+    return {"metric": "symbolic lane-steps/s (k_sym_step)", "lanes": lanes, "codes": int(len(set(b.code_id.tolist()))),
+            "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
+            "lane_steps_per_s": steps / sec, "forked": int((out_b.status == MG_FORK).sum()),
+            "statuses": statuses, "roofline": roof,
+            "workload": "symbolic message call into each of the 18 precompiled reference contracts "
+                        "(symbolic calldata/sender/value, symbolic storage), dealt round-robin; "
+                        "each lane runs to its first fork, escape or halt"}
+
+
+def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5):
+    """k_sym_step at `lanes` taint lanes, the kernel alone: the
+    first launch of `taint_c2`'s batch -- C2's lanes with the seven modules'
+    batch-safe hooks as device actions -- packed by the batched LaserEVM for
+    4,096 distinct C2 calls and dealt round-robin to `lanes` lanes, then run to
+    the first host event (a non-batch-safe hook, a halt, an escape) in one
+    launch.  The host replay of the records (what `taint_c2` adds on top) is
+    not part of this figure."""
+    from dataclasses import replace
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+    import refmodules
+    from refmodules import hooks_of
+    from mythril_amd.lanes import _ALL_FIELDS, _TAINT_FIELDS, LaneBatch, MG_RUNNING, STATUS_NAMES
+    from mythril_amd.laser import LaserEVM
+    from mythril_amd.laser import svm as svm_mod
+    from mythril_amd.laser import taint as tnt
+    from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
+    names = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJump", "UserAssertions",
+             "Exceptions", "StateChangeAfterCall")
+    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    laser.track_objects = True
+    mods = [getattr(refmodules, m)() for m in names]
+    laser.register_hooks("pre", hooks_of(mods, "pre"))
+    laser.register_hooks("post", hooks_of(mods, "post"))
+    distinct = min(4096, lanes)
+    _c2_laser_states(laser, distinct, workloads_seed(rank))
+    states = laser.work_list[:]
+    plan = tnt.TaintPlan(laser)
+    laser._plan = plan
+    laser._tl = [tnt.LaneTaint() for _ in states]
+    shape = laser._shape(states, True)
+    small = LaneBatch(shape)
+    for i, st in enumerate(states):
+        laser._pack(small, i, st)
+        small.steps[i] = 0
+    big = LaneBatch(replace(shape, n=lanes))
+    idx = np.arange(lanes) % distinct
+    for f in _ALL_FIELDS + _TAINT_FIELDS:
+        src = getattr(small, f, None)
+        if src is not None:
+            getattr(big, f)[...] = src[idx]
+    mask = svm_mod._mask(laser._hooked_ops())
+    dev.alloc(big.shape)
+    dev.set_taint_program(plan.actions)
+    laser._upload_force(dev)
+    ms, steps = [], 0
+    for _ in range(reps + 1):
+        dev.upload(big)
+        st = dev.step(mask)
+        ms.append(st.kernel_ms)
+        steps = st.lane_steps
+    ms = ms[1:]
+    out_b = LaneBatch(big.shape)
+    dev.download(out_b)
+    statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
+                for k, v in zip(*np.unique(out_b.status, return_counts=True))}
+    kms = float(np.median(ms))
+    return {"metric": "taint lane-steps/s (k_sym_step, device actions; host replay excluded)",
+            "lanes": lanes, "distinct_calls": distinct, "modules": list(names),
+            "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
+            "lane_steps_per_s": steps / (kms / 1e3) if kms else None, "statuses": statuses,
+            "running_after": int((out_b.status == MG_RUNNING).sum())}
 
 
 def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_handler=None, log=None):

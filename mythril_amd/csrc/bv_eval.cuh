@@ -120,12 +120,20 @@ struct BvTables {
     const uint4 *__restrict__ dflt;
 };
 
+// Per lane, the whole context is ONE VGPR: m = chunk * BV_BLOCK + tid (the model
+// this thread evaluates, unclamped).  tid = m % BV_BLOCK addresses the LDS slots;
+// the value / table rows use min(m, n_models - 1) (a dead lane past the pool
+// reads the last model; its result is masked).  Keeping model, tid and the
+// live flag as separate VGPRs spilled them at 64 VGPRs inside the DAG loop
+// (12.6 GB of scratch traffic per C4 launch, profiles/r02/traffic.json).
 struct BvCtx {
     const uint4 *__restrict__ values;
     const uint4 *__restrict__ consts;
     uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
-    uint32_t n_models, model, tid;
+    uint32_t n_models, m;
     BvTables tab;
+    DEV uint32_t model() const { return min(m, n_models - 1u); }
+    DEV uint32_t tid() const { return m & (BV_BLOCK - 1u); }
 };
 
 DEV U256 ld2(const uint4 *p) {
@@ -139,7 +147,7 @@ DEV U256 ld2(const uint4 *p) {
 // model interpretation lookup (entries are unique keys: first match wins)
 DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) {
     const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
-    const size_t tm = (size_t)t * c.n_models + c.model;
+    const size_t tm = (size_t)t * c.n_models + c.model();
     const uint32_t s0 = c.tab.start[tm], cnt = c.tab.count[tm];
     U256 v = ld2(c.tab.dflt + tm * 4u + part * 2u);
     for (uint32_t k = 0; k < cnt; ++k) {
@@ -157,14 +165,14 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     U256 r;
     if (kind == BV_REF_ACC) return acc;
     if (kind == BV_REF_SLOT) {
-        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid];
-        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid];
+        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid()];
+        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid()];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
         return r;
     }
     if (kind == BV_REF_VAR) {
-        const size_t row = (size_t)idx * c.n_models + c.model;
+        const size_t row = (size_t)idx * c.n_models + c.model();
         const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
@@ -177,17 +185,22 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
     return r;
 }
 
-// The division-class ops (UDIV UREM SDIV SREM SMOD MUL_NOOVF_U) share ONE
-// inlined u_divmod_nz: operands are prepared per op (sign-extend + magnitude
-// for the signed ops; (2^w-1, A) for the overflow test), divided once, and the
-// quotient / remainder post-processed per op.  Six inlined copies of Knuth D
-// made the kernel's code ~4x larger than its hot loop (instruction-cache
-// misses, SQ_WAIT_INST_ANY).  z3 semantics for a zero divisor are kept:
+// The division-class ops go through TWO inlined u_divmod_nz sites instead of
+// six: UDIV/UREM (bv_udivrem), and SDIV SREM SMOD MUL_NOOVF_U (bv_divop:
+// operands prepared per op -- sign-extend + magnitude for the signed ops,
+// (2^w-1, A) for the overflow test -- divided once, the quotient / remainder
+// post-processed per op).  Six inlined copies of Knuth D doubled the kernel's
+// code; one shared site kept the divisor live across the division and spilled
+// inside it (divrem class 83 -> 92 ms, profiles/r03/k2).  z3 semantics for a zero divisor are kept:
 // udiv -> ones, urem/srem/smod -> a, sdiv -> (a < 0 ? 1 : -1).
-DEV bool bv_is_div(uint32_t op) {
-    return op == BV_UDIV || op == BV_UREM || op == BV_SDIV || op == BV_SREM || op == BV_SMOD ||
-           op == BV_MUL_NOOVF_U;
+// UDIV/UREM (C4's division class) keep nothing live across the division; the
+// signed ops and the overflow test share the second site
+DEV U256 bv_udivrem(bool quotient, const U256 &A, const U256 &B) {
+    U256 q = u_ones(), r = A;                   // b == 0: bvudiv -> ones, bvurem -> a
+    if (!u_iszero(B)) u_divmod_nz(A, B, q, r);
+    return quotient ? q : r;
 }
+#define BV_DIV_OPS ((1ull << BV_SDIV) | (1ull << BV_SREM) | (1ull << BV_SMOD) | (1ull << BV_MUL_NOOVF_U))
 DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const U256 &B) {
     const bool sgn = op == BV_SDIV || op == BV_SREM || op == BV_SMOD;   // wave-uniform
     U256 a = A, b = B;
@@ -282,30 +295,29 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
         for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
     __syncthreads();
 
-    const uint32_t tid = threadIdx.x;
     const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
     const uint32_t c_lo = group * chunks_per_block, c_hi = min(c_lo + chunks_per_block, n_chunks);
+    // thread index = the wave's first (an SGPR) + the lane id (v_mbcnt): nothing
+    // keeps threadIdx.x alive across the loops
+    const uint32_t wave0 = uni(threadIdx.x) & ~63u;
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-    const uint32_t model = chunk * BV_BLOCK + tid;
-    const bool live = model < n_models;
-    BvCtx c{values, consts, slots, n_models, live ? model : 0u, tid, tab};
+    BvCtx c{values, consts, slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
 
     for (uint32_t d = d0; d < d1; ++d) {
         const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
         U256 acc = u_zero();
-        // scalar fetch one instruction ahead: the s_load of instruction p+1 is in
-        // flight while instruction p executes
-        uint4 nxt = make_uint4(0u, 0u, 0u, 0u);
-        if (!kLdsProg && p0 < p1) nxt = insns[i0 + uni(p0)];
         for (uint32_t p = p0; p < p1; ++p) {
+            // c.m is the only per-lane context: hide its loop invariance so the
+            // compiler recomputes min(m, n - 1) / m % 256 at each use instead of
+            // keeping them in extra VGPRs across the loop (they spilled)
+            asm volatile("" : "+v"(c.m));
             uint32_t w0, ra, rb, rc;
             if (kLdsProg) {
                 const uint4 ins = prog[p];
                 w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
             } else {
-                const uint4 ins = nxt;
+                const uint4 ins = insns[i0 + uni(p)];
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
-                if (p + 1u < p1) nxt = insns[i0 + uni(p + 1u)];
             }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
             U256 A = bv_fetch(c, acc, ra);
@@ -320,7 +332,14 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             case BV_SEXT: r = bv_sext(A, rb); break;
             default: {
                 U256 B = bv_fetch(c, acc, rb);
-                if (bv_is_div(op)) { r = bv_divop(op, width, rc, A, B); break; }
+                if (op == BV_UDIV || op == BV_UREM) {        // the unsigned division site
+                    r = bv_udivrem(op == BV_UDIV, A, B);
+                    break;
+                }
+                if ((BV_DIV_OPS >> op) & 1ull) {             // the signed / overflow site
+                    r = bv_divop(op, width, rc, A, B);
+                    break;
+                }
                 switch (op) {
                 case BV_ADD: r = u_add(A, B); break;
                 case BV_SUB: r = u_sub(A, B); break;
@@ -377,22 +396,26 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;
-                slots[(ds * 2u) * BV_BLOCK + tid] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
-                slots[(ds * 2u + 1u) * BV_BLOCK + tid] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
+                slots[(ds * 2u) * BV_BLOCK + c.tid()] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+                slots[(ds * 2u + 1u) * BV_BLOCK + c.tid()] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
             }
         }
-        const bool sat = live && (acc.w[0] & 1u);
+        const bool sat = c.m < n_models && (acc.w[0] & 1u);
         const uint64_t bal = __ballot(sat);
-        if ((tid & 63u) == 0u && bal) {
+        // the wave's first model, wave-uniform (an SGPR: nothing per lane stays live
+        // across the DAG loop but c.m and the accumulator)
+        const uint32_t wm = uni(c.m) & ~63u;
+        if (bal && __lane_id() == 0u) {
             // optional per-model bitmap (one u64 per wave): lets the host replay
             // sequential check_quick_sat calls whose LRU bumps reorder the pool
-            if (sat_bits) sat_bits[(size_t)d * bit_words + ((chunk * BV_BLOCK + tid) >> 6)] = bal;
+            if (sat_bits) sat_bits[(size_t)d * bit_words + (wm >> 6)] = bal;
             atomicAdd(&blk_cnt[d - d0], (uint32_t)__popcll(bal));
-            atomicMin(&blk_first[d - d0], chunk * BV_BLOCK + (tid & ~63u) + (uint32_t)(__ffsll((long long)bal) - 1));
+            atomicMin(&blk_first[d - d0], wm + (uint32_t)(__ffsll((long long)bal) - 1));
         }
     }
     }
     __syncthreads();
+    const uint32_t tid = wave0 + __lane_id();
     if (tid < d1 - d0) {
         const uint32_t n = blk_cnt[tid], f = blk_first[tid];
         if (n) {

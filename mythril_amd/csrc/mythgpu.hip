@@ -1089,10 +1089,11 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        ctx->lpw | k1_flags() | (P.push_lds ? 0x200u : 0u) | (P.mw32 << 16));
     HIPX(ctx, hipGetLastError());
     // symbolic and taint lanes: the concrete stepper left them untouched (counted as running)
-    if ((ctx->S.node || ctx->T.sobj) && !prof && !reset) {
+    // (a profiling pass counts their opcodes into the same histogram)
+    if ((ctx->S.node || ctx->T.sobj) && !reset) {
         hipLaunchKernelGGL(k_sym_step, dim3(blocks_for(ctx->L.n)), dim3(256), 0, ctx->stream, ctx->L, ctx->S,
                            ctx->T, ctx->d_codes, ctx->d_a8, ctx->d_a32, m[0], m[1], m[2], m[3], max_steps, max_depth,
-                           horizon, loop_bound, ctr, lane_block(ctx));
+                           horizon, loop_bound, ctr, lane_block(ctx), prof);
         HIPX(ctx, hipGetLastError());
     }
     return MG_OK;

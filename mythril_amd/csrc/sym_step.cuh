@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                                                   uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3,
                                                   uint32_t max_steps, uint32_t max_depth, uint32_t horizon,
                                                   uint32_t loop_bound, DevCounters *__restrict__ ctr,
-                                                  uint32_t lanes_pb) {
+                                                  uint32_t lanes_pb, unsigned long long *__restrict__ prof) {
     __shared__ uint32_t s_kc[(256u / 64u) * KC_WAVE];
     if ((threadIdx.x & 63u) < 2u) s_kc[(threadIdx.x >> 6) * KC_WAVE + KC_E * 24u + (threadIdx.x & 63u)] = 0u;
     __syncthreads();
@@ -409,11 +409,16 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     s_kc + (threadIdx.x >> 6) * KC_WAVE, txlim, glim, lane, threadIdx.x, 256u, 0u, flags,
                     0u, 0u, 0u, 0u, 0u};
 
+    // optional opcode histogram (mg_step_profile; profiling passes only): the
+    // previous instruction is counted once `executed` shows it completed
+    uint32_t pexec = 0u, pop = 0u;
     for (;;) {
+        if (prof && executed != pexec) { atomicAdd(&prof[pop], 1ull); pexec = executed; }
         // the checks svm.execute_state makes before an instruction (svm.py:369-402)
         if (max_depth != 0u && depth >= max_depth) { status = ST_DEPTH; break; }
         if (pc >= C.n_instr) { status = ST_END; break; }
         const uint32_t op = gops[pc];
+        pop = op;
         const uint2 d = kDec[op];
         const uint32_t kind = (d.y >> 9) & 31u;
         const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
@@ -819,6 +824,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth; gmin = R.gmin; gmax = R.gmax;
         ++executed;
     }
+    if (prof && executed != pexec) atomicAdd(&prof[pop], 1ull);
 
     L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
     L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;

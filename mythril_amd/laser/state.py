@@ -116,11 +116,13 @@ class Memory:
     def __init__(self, data: bytes = b"", sym: Optional[Dict[int, BitVec]] = None):
         self._m = bytearray(data)
         self._sym: Dict[int, BitVec] = dict(sym) if sym else {}
+        self._ver = 0            # bumped by every mutation (LaserEVM's unchanged-after-hooks test)
 
     def __len__(self):
         return len(self._m)
 
     def extend(self, size: int):
+        self._ver += 1
         self._m.extend(b"\x00" * size)
 
     def _byte(self, k: int):
@@ -138,6 +140,7 @@ class Memory:
     def __setitem__(self, key: int, value):
         if key >= len(self._m):
             return
+        self._ver += 1
         if isinstance(value, Expression) and value.symbolic:
             if value.size() != 8:
                 raise ValueError("a memory byte is an 8-bit expression")
@@ -265,6 +268,7 @@ class Storage:
         self.concrete = concrete
         self.address = address
         self.printable_storage: Dict = dict(slots or {})
+        self._ver = 0                            # bumped by every mutation
         self._chain: Optional[List] = None       # [(key, value)] in store order (chain mode)
         self._raws: Optional[List] = None        # _raws[m]: the array after m stores
         if not concrete:
@@ -281,6 +285,7 @@ class Storage:
 
     def to_chain(self) -> "Storage":
         if self._chain is None:
+            self._ver += 1
             slots = list(self.printable_storage.items())
             self._chain, self._raws, self.printable_storage = [], [self._base_raw()], {}
             for k, v in slots:
@@ -297,6 +302,7 @@ class Storage:
         return s
 
     def _append(self, key: BitVec, value: BitVec) -> None:
+        self._ver += 1
         self._chain.append((key, value))
         self._raws.append(Node("store", 0, (self._raws[-1], key.raw, value.raw), (256, 256)))
         self.printable_storage[key] = value
@@ -327,6 +333,7 @@ class Storage:
 
     def __setitem__(self, key, value) -> None:
         sym = any(isinstance(x, Expression) and x.symbolic for x in (key, value))
+        self._ver += 1
         if self._chain is None and not sym:
             self.printable_storage[concrete(key)] = concrete(value)
             return
@@ -357,6 +364,7 @@ class Storage:
 
     def set_slots(self, slots: Dict[int, int]) -> None:
         """Replace the contents by concrete slots (slot mode)."""
+        self._ver += 1
         self._chain = self._raws = None
         self.printable_storage = dict(slots)
 

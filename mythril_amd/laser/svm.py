@@ -499,7 +499,7 @@ class LaserEVM:
         if self._loop_bound():
             tl = max((len(_trace_of(s)) for s in states), default=0)
             trace_cap = max(4096 * g, 2 * tl)
-        stack_cap = 1024 if n <= 4096 else min(1024, 128 * g)
+        stack_cap = min(1024, 128 * g)        # deeper stacks escape and regrow in place
         mem_cap = max(4096 * g, 2 * msz)
         mem_cap = min(mem_cap, max(1024, ((1 << 30) // max(n, 1)) // 32 * 32), 1 << 24)
         mem_cap = max(mem_cap, (msz + 31) // 32 * 32)
@@ -862,6 +862,8 @@ class LaserEVM:
         if status in _EXECUTED_HALTS:
             self.total_states -= 1                  # the halting step had no successor
         if status == MG_HOOK:
+            # plain concrete lanes: a state the hooks leave untouched needs no repack
+            sig0 = _hook_sig(s) if not (b.taint or b.symbolic or b.shape.trace_cap) else None
             # execute_state returning [] puts the popped state in final_states
             # when track_gas (svm.py:328-334), whatever the reason
             try:
@@ -893,7 +895,10 @@ class LaserEVM:
             # hooks may have rewritten the state: repack, then run the hooked
             # instruction alone (STEP1) when post hooks must see its successor
             steps = int(b.steps[i])
-            self._pack(b, i, s)
+            if sig0 is not None and sig0 == _hook_sig(pre_state):
+                _rearm(b, i)             # the lane image is still the state's: only resume it
+            else:
+                self._pack(b, i, s)
             b.steps[i] = steps
             b.flags[i] |= MG_LANE_HOOK_ACK | (MG_LANE_STEP1 if post else 0)
             if not post and self._halts_on_host(name, s, b, i):
@@ -1187,6 +1192,29 @@ def _trace_of(state: GlobalState) -> List[int]:
         if isinstance(a, JumpdestCountAnnotation):
             return a.trace
     return []
+
+
+def _hook_sig(s: GlobalState):
+    """What _pack reads from a concrete state, by identity and mutation count:
+    equal before and after the hooks means the lane image is still the state's."""
+    ms, env = s.mstate, s.environment
+    acct = env.active_account
+    stack = ms.stack
+    return (ms.pc, id(stack), len(stack), tuple(map(id, stack)), id(ms.memory), ms.memory._ver,
+            ms.depth, ms.min_gas_used, ms.max_gas_used, id(env), id(env.code), env.static, id(env.calldata),
+            id(env.address), id(env.sender), id(env.origin), id(env.callvalue), id(env.gasprice),
+            id(acct), id(acct.storage), acct.storage._ver, id(s.current_transaction))
+
+
+def _rearm(b: LaneBatch, i: int) -> None:
+    """The per-launch fields _pack resets, for a lane whose image is unchanged."""
+    b.status[i] = MG_RUNNING
+    b.aux[i] = 0
+    b.flags[i] = int(b.flags[i]) & ~(MG_LANE_HOOK_ACK | MG_LANE_STEP1) & 0xFFFFFFFF
+    b.ret_offset[i] = b.ret_len[i] = 0
+    b.rec_len[i] = 0
+    if hasattr(b, "rec_seen"):
+        b.rec_seen[i] = 0
 
 
 def _mask(ops) -> List[int]:

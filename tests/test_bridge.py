@@ -171,7 +171,7 @@ def test_integration_snippets_execute():
     ref_states = [_ref_state(bytes.fromhex("18160ddd")),
                   _ref_state(bytes.fromhex("70a08231") + workloads.ATTACKER.to_bytes(32, "big")),
                   _ref_state(b"", symbolic=True)]
-    ns = {"ref_states": ref_states, "device": OracleDevice(), "symbol_factory": R.symbol_factory,
+    ns = {"ref_states": ref_states, "device": OracleDevice(), "symbol_factory": R.symbol_factory, "smt": R.smt,
           "z3": z, "ref_constraints": [z.pred("ULT", z.BitVec("x", 256), z.BitVecVal(9, 256))]}
     for b in blocks:
         exec(compile(b, "INTEGRATION.md", "exec"), ns)
