@@ -621,11 +621,12 @@ class LaserEVM:
             acct.storage = storage
         else:
             ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
-            acct.storage.set_slots({})
             cnt = int(b.storage_count[i])
             if cnt:
                 kv = rows_to_words(b.storage[i, :cnt].reshape(2 * cnt, 8))
                 acct.storage.set_slots({kv[2 * k]: kv[2 * k + 1] for k in range(cnt)})
+            else:
+                acct.storage.set_slots({})
         s.lane_steps = int(b.steps[i])
         if b.shape.trace_cap:
             ann = _annotation_of(s)
