@@ -56,7 +56,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_STACK_LIMIT,
                      limbs_to_word, rows_to_words, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
-from ..smt.expr import Expression, symbol_factory
+from ..smt.expr import ConstWord, Expression, symbol_factory
 from ..smt.keccak_manager import keccak_function_manager
 from ..smt import solver as solver_mod
 from ..smt.solver import Constraints, SnapshotConstraints, SolverBackendMissing, args, query_raw
@@ -607,8 +607,10 @@ class LaserEVM:
         if symlane:
             stack, memory, storage = sym.decode_lane(b, i, s)
             ms.stack = MachineStack(stack)
-        else:
+        elif b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])
+        else:
+            ms.stack = MachineStack([ConstWord(w) for w in rows_to_words(b.stack[i, :sp])])
         if b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack(tnt.materialise(b, i, s, self._tl[i], self._plan, list(ms.stack)))
         ms.depth = int(b.depth[i])

@@ -395,6 +395,45 @@ def BVSubNoUnderflow(a, b, signed: bool) -> Bool:
     return Bool(_fold("bvsub_noudfl_u", 1, (a.raw, b.raw)), _ann(a, b))
 
 
+class ConstWord(BitVec):
+    """A concrete 256-bit word read back from a lane (LaserEVM._materialise):
+    `BitVecVal(v, 256)` with its DAG node built on first use of `.raw`.  Most
+    words a hook event materialises are only compared, read for `.value` or
+    passed along, so the interning of a fresh constant is skipped for them."""
+    __slots__ = ("_v", "_n")
+
+    def __init__(self, v: int):
+        self._v = v
+        self._n = None
+        self.annotations = _NO_ANN
+
+    @property
+    def raw(self) -> Node:
+        n = self._n
+        if n is None:
+            n = self._n = const(self._v, 256)
+        return n
+
+    @raw.setter
+    def raw(self, node: Node) -> None:            # unpickling / copy.copy
+        self._n = node
+        self._v = node.param
+
+    @property
+    def symbolic(self) -> bool:
+        return False
+
+    @property
+    def value(self):
+        return self._v
+
+    def size(self) -> int:
+        return 256
+
+
+_NO_ANN = frozenset()
+
+
 class _SymbolFactory:
     """mythril/laser/smt/__init__.py:37-154 symbol_factory surface."""
 

@@ -124,3 +124,57 @@ def check(results):
         assert status[0] in WORLD_STATE_KEPT, (name, status)
         got = {k: storage.get(k, 0) for k in exp}
         assert got == exp, (name, got, exp)
+
+
+# ---- symbolic lanes: the fixture's symbolic cases as programs ------------------------------
+def symbolic_programs():
+    """[(name, code)] run on a symbolic lane (symbolic calldata, storage): the
+    calldata byte at the fixture's index past its size (calldata_test.py:58-73),
+    two loads at the same symbolic index (:76-91), and an uninitialised read of
+    symbolic storage after the fixture's stores (storage_test.py:27-38)."""
+    c, st = CASES["calldata"]["symbolic_index"], CASES["storage"]["uninitialized"]
+    out = [("cd_index", push(c["index"]) + CALLDATALOAD + byte_at_top() + STOP),
+           # index_a == index_b: the index is one calldata word loaded twice
+           ("cd_equal", push(0) + CALLDATALOAD + CALLDATALOAD + push(0) + CALLDATALOAD + CALLDATALOAD + STOP)]
+    for init, key in st:
+        code = b"".join(push(v) + push(int(k)) + SSTORE for k, v in init.items())
+        out.append((f"sym_storage{len(init)}_{key}", code + push(key) + SLOAD + STOP))
+    return out
+
+
+def symbolic_state(code: bytes, txid: str = "7"):
+    """A symbolic message call's initial state into `code`, with symbolic storage."""
+    from mythril_amd import workloads
+    from mythril_amd.laser import Account, Disassembly, MessageCallTransaction, SymbolicCalldata, WorldState
+    from mythril_amd.smt.expr import symbol_factory
+    ws = WorldState()
+    acct = Account(workloads.CONTRACT, code=Disassembly(code), concrete_storage=False)
+    ws.put_account(acct)
+    sender = symbol_factory.BitVecSym(f"sender_{txid}", 256)
+    tx = MessageCallTransaction(world_state=ws, identifier=txid, gas_limit=8_000_000, origin=sender,
+                                caller=sender, callee_account=acct, call_data=SymbolicCalldata(txid),
+                                call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256),
+                                gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256))
+    gs = tx.initial_global_state()
+    gs.transaction_stack.append((tx, None))
+    return gs
+
+
+def check_symbolic_stack(name: str, stack, txid: str = "7"):
+    """The reference tests' verdicts on the final stack of a symbolic program."""
+    import random
+    from mythril_amd.laser.witness import eval_all
+    from mythril_amd.smt.expr import Expression
+    from mythril_amd.smt.program import ArrayInterp
+    rng = random.Random(5)
+    if name == "cd_index":
+        c = CASES["calldata"]["symbolic_index"]
+        models = [{f"{txid}_calldatasize": c["size"],
+                   f"{txid}_calldata": ArrayInterp(rng.getrandbits(8), {c["index"]: rng.getrandbits(8)})}
+                  for _ in range(32)]
+        assert all(v != c["value"] for v in eval_all(stack[-1].raw, models)) and not c["sat"]
+    elif name == "cd_equal":
+        assert stack[-1].raw is stack[-2].raw                 # the same term: a != b is unsat
+    else:
+        got = stack[-1]
+        assert isinstance(got, Expression) and got.symbolic   # storage_test.py:27-38

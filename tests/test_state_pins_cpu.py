@@ -151,3 +151,19 @@ def test_machine_stack():
     with pytest.raises(NotImplementedError):
         st = MachineStack()
         st += st
+
+
+@pytest.mark.parametrize("name,code", state_pins.symbolic_programs())
+def test_symbolic_fixture_programs_on_the_restatement(name, code):
+    """The same symbolic programs through the CPU restatement (tests/symref.py),
+    the oracle the GPU test compares kernel 1 with."""
+    import symref
+    s, eng = state_pins.symbolic_state(code), symref.Engine()
+    while True:
+        out = eng.step(s)
+        if not out:
+            break
+        s = out[0]
+    kind, last = eng.ended[-1]
+    assert kind == "stop"
+    state_pins.check_symbolic_stack(name, last.mstate.stack)
