@@ -506,10 +506,13 @@ def execute_symbolic_transactions(laser_evm, callee_address, tx_count: Optional[
         base = tx_id_manager._next_transaction_id
         off = sum(counts[:rank])
         ids = [str(base + off + j + 1) for j in range(counts[rank])]
+        # the counter covers the round's ids before the calls run, as the
+        # reference's get_next_tx_id per call leaves it (witness seeds and the
+        # solver read it while the transactions execute)
+        tx_id_manager.set_counter(base + sum(counts))
         for hook in laser_evm._start_sym_trans_hooks:
             hook()
         execute_symbolic_message_call(laser_evm, callee_address, gas_limit, ids=ids)
-        tx_id_manager.set_counter(base + sum(counts))
         for hook in laser_evm._stop_sym_trans_hooks:
             hook()
         if world > 1:

@@ -325,11 +325,12 @@ class TaintPlan:
 
 class LaneTaint:
     """Host side of one taint lane: handle -> object, atom -> annotation set."""
-    __slots__ = ("objs", "atoms")
+    __slots__ = ("objs", "atoms", "msets")
 
     def __init__(self):
         self.objs: Dict[int, Expression] = {}
         self.atoms: List[Optional[frozenset]] = []
+        self.msets: Dict[int, frozenset] = {}     # mask -> union of its (final) atom sets
 
 
 def state_needs_taint(state) -> bool:
@@ -344,7 +345,7 @@ def state_needs_taint(state) -> bool:
 def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
     """Write state's object graph into lane i's taint planes.  False when it needs
     more than 64 atoms or the object table (the lane cannot carry it)."""
-    lt.objs, lt.atoms = {}, []
+    lt.objs, lt.atoms, lt.msets = {}, [], {}
     atom_of: Dict[int, int] = {}
     keep = []
 
@@ -490,13 +491,19 @@ def replay_deferred(rec, state, plan: TaintPlan) -> None:
 
 def atoms_set(lt: LaneTaint, m: int) -> frozenset:
     """The annotation set of mask `m` (every atom was resolved when its record
-    was replayed, or at pack)."""
+    was replayed, or at pack).  An atom's set never changes once resolved, so
+    the union is memoised per mask until the next pack renumbers the atoms."""
+    m = int(m)
+    got = lt.msets.get(m)
+    if got is not None:
+        return got
     out = frozenset()
-    for k in _bits(int(m)):
+    for k in _bits(m):
         got = lt.atoms[k] if k < len(lt.atoms) else None
         if got is None:
             raise RuntimeError(f"taint atom {k} has no record")
         out = out | got
+    lt.msets[m] = out
     return out
 
 
