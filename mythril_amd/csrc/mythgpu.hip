@@ -63,6 +63,11 @@ struct mg_ctx {
     DevCounters *d_ctr_multi = nullptr;
     size_t ctr_multi_cap = 0;            // slots
     std::vector<void *> retired;          // outgrown buffers, freed by mg_close
+    // pinned host copy of the multi-batch statistics slots (a pageable D2H copy
+    // is staged through a bounce buffer: ~0.1 ms for 20 C2 batches' slots)
+    DevCounters *h_ctr_pin = nullptr;
+    size_t h_ctr_pin_cap = 0;
+    std::vector<void *> retired_host;
     std::vector<hipEvent_t> ev_batch;
     // kernel 2
     BvState bv{};
@@ -237,6 +242,8 @@ extern "C" void mg_close(mg_ctx *ctx) {
     for (hipEvent_t e : ctx->ev_batch) hipEventDestroy(e);
     hipFree(ctx->d_ctr_multi);
     for (void *p : ctx->retired) hipFree(p);
+    if (ctx->h_ctr_pin) hipHostFree(ctx->h_ctr_pin);
+    for (void *p : ctx->retired_host) hipHostFree(p);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1057,12 +1064,16 @@ static uint32_t k1_flags() {
     return (r && std::string(r) == "reg") ? 0x100u : 0u;
 }
 
+// plan / kflags: a caller launching many batches computes the LDS plan and the
+// environment switches once (getenv scans the environment: ~1-2 us a call, five
+// calls per launch were most of the gap between C2 batches)
 static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_steps, uint32_t max_depth,
                        DevCounters *ctr, unsigned long long *prof = nullptr, uint32_t horizon = 0,
-                       const DevResetImage *reset = nullptr) {
+                       const DevResetImage *reset = nullptr, const LdsPlan *plan = nullptr,
+                       int64_t kflags = -1) {
     const uint64_t zero[4] = {0, 0, 0, 0};
     const uint64_t *m = hook_mask ? hook_mask : zero;
-    const LdsPlan P = lds_plan(ctx);
+    const LdsPlan P = plan ? *plan : lds_plan(ctx);
     if (ctx->loop_bound && ctx->L.trace_cap) {
         // the loop-count hash compares 16-bit byte addresses (EVM code < 64 KiB)
         for (const DevCode &c : ctx->codes)
@@ -1086,7 +1097,8 @@ static int launch_step(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t max_st
                        ctx->d_codes, ctx->d_a8, ctx->d_a32, ctx->d_cov, ctx->cfg.coverage ? 1u : 0u, m[0], m[1],
                        m[2], m[3], max_steps, max_depth, ctr, prof, P.win, P.pd_cap, P.jr_cap, horizon,
                        loop_bound, reset ? *reset : DevResetImage{},
-                       ctx->lpw | k1_flags() | (P.push_lds ? 0x200u : 0u) | (P.mw32 << 16));
+                       ctx->lpw | (kflags >= 0 ? (uint32_t)kflags : k1_flags()) | (P.push_lds ? 0x200u : 0u) |
+                       (P.mw32 << 16));
     HIPX(ctx, hipGetLastError());
     // symbolic and taint lanes: the concrete stepper left them untouched (counted as running)
     // (a profiling pass counts their opcodes into the same histogram)
@@ -1175,6 +1187,12 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
         if (ctx->d_ctr_multi) ctx->retired.push_back(ctx->d_ctr_multi);
         ctx->d_ctr_multi = p;
         ctx->ctr_multi_cap = cap;
+        DevCounters *hp = nullptr;
+        if (hipHostMalloc((void **)&hp, cap * sizeof(DevCounters), hipHostMallocDefault) != hipSuccess)
+            return set_err(ctx, MG_ENOMEM, "hipHostMalloc %zu statistics slots", cap);
+        if (ctx->h_ctr_pin) ctx->retired_host.push_back(ctx->h_ctr_pin);
+        ctx->h_ctr_pin = hp;
+        ctx->h_ctr_pin_cap = cap;
     }
     // events in a block of at least 128 (64 batches): like the statistics slots,
     // created before they are needed rather than on a larger call's first use
@@ -1186,6 +1204,8 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
     // the stepping kernel re-initialises its lanes itself (reset_lane in its
     // prologue): one launch per batch
     const DevResetImage R = reset_image(ctx);
+    const LdsPlan plan = lds_plan(ctx);
+    const int64_t kflags = (int64_t)k1_flags();
     // one event pair around the whole sequence, each batch reporting the mean:
     // timing events between the launches cost ~8 us per batch on MI355X (C2
     // 0.1765 -> 0.1688 ms per batch, scripts/gpu_ab_events.sh).  The mean includes
@@ -1196,29 +1216,29 @@ extern "C" int mg_run_batches(mg_ctx *ctx, const uint64_t hook_mask[4], uint32_t
     for (uint32_t b = 0; b < n_batches; ++b) {
         if (per_batch_events || b == 0u) HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b], ctx->stream));
         int rc = launch_step(ctx, hook_mask, max_steps, max_depth, ctx->d_ctr_multi + (size_t)b * nb,
-                             nullptr, 0u, &R);
+                             nullptr, 0u, &R, &plan, kflags);
         if (rc) return rc;
         if (per_batch_events || b + 1u == n_batches)
             HIPX(ctx, hipEventRecord(ctx->ev_batch[2u * b + 1u], ctx->stream));
     }
-    ctx->h_ctr.resize(slots);
-    HIPX(ctx, hipMemcpyAsync(ctx->h_ctr.data(), ctx->d_ctr_multi, slots * sizeof(DevCounters),
+    HIPX(ctx, hipMemcpyAsync(ctx->h_ctr_pin, ctx->d_ctr_multi, slots * sizeof(DevCounters),
                              hipMemcpyDeviceToHost, ctx->stream));
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    float ms_all = 0.f;
+    if (!per_batch_events) {
+        HIPX(ctx, hipEventElapsedTime(&ms_all, ctx->ev_batch[0], ctx->ev_batch[2u * n_batches - 1u]));
+        ms_all /= (float)n_batches;
+    }
     for (uint32_t b = 0; b < n_batches; ++b) {
         DevCounters c{};
         for (uint32_t k = 0; k < nb; ++k) {
-            const DevCounters &x = ctx->h_ctr[(size_t)b * nb + k];
+            const DevCounters &x = ctx->h_ctr_pin[(size_t)b * nb + k];
             c.lane_steps += x.lane_steps; c.running += x.running; c.halted += x.halted;
             c.hooked += x.hooked; c.escaped += x.escaped;
         }
-        float ms = 0.f;
-        if (per_batch_events) {
+        float ms = ms_all;
+        if (per_batch_events)
             HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[2u * b], ctx->ev_batch[2u * b + 1u]));
-        } else {
-            HIPX(ctx, hipEventElapsedTime(&ms, ctx->ev_batch[0], ctx->ev_batch[2u * n_batches - 1u]));
-            ms /= (float)n_batches;
-        }
         stats[b].lane_steps = c.lane_steps;
         stats[b].running = c.running;
         stats[b].halted = c.halted;
