@@ -18,6 +18,10 @@
 //               or immediates (EXTRACT lo, SEXT source width, CONCAT low width,
 //               compare operand width), per op.
 // The result always lands in the accumulator; `store` also writes slot dst.
+// Only operand A may refer to the accumulator (the host flattener swaps or
+// spills, bv_upload checks): A is then loaded INTO the accumulator's registers
+// and the accumulator is dead for the rest of the instruction, so no operand
+// copy of the 256-bit accumulator is needed per instruction.
 #pragma once
 #include <string>
 
@@ -44,6 +48,8 @@ enum BvOp : uint32_t {
                        // interpretation at (k0, k1), else its default (lower.py)
     BV_UMIN, BV_UMAX,  // ite(cmp(A, B), A, B) folded by the compiler (flatten._fold_select)
     BV_SMIN, BV_SMAX,  // signed at `width`
+    BV_RSUB,           // B - A           (operand-swapped forms: the accumulator is only
+    BV_RCONCAT,        // A low, B high,   ever operand A; w3 = width of A)
     BV_NUM_OPS
 };
 
@@ -160,15 +166,24 @@ DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) 
     return lo ? u_shr_n(v, lo, 0u) : v;
 }
 
-DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
+// An operand's 256 bits from a slot (LDS), a variable (the model's value row)
+// or a constant (uniform address: scalar loads).  Each path ends in its own
+// opaque asm: the three paths' loads are then no longer identical trailing
+// instructions, so the compiler cannot sink them into one generic-pointer
+// load after the branch (it did, as eight per-dword flat_loads, once A's fetch
+// wrote the accumulator's registers).  The accumulator itself is never
+// fetched here (operand A = the accumulator is handled by the caller).
+#define BV_PIN(tag_, r_) asm volatile(tag_ : "+v"((r_).w[0]), "+v"((r_).w[1]), "+v"((r_).w[2]), "+v"((r_).w[3]), \
+                                      "+v"((r_).w[4]), "+v"((r_).w[5]), "+v"((r_).w[6]), "+v"((r_).w[7]))
+DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
     const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
     U256 r;
-    if (kind == BV_REF_ACC) return acc;
-    if (kind == BV_REF_SLOT) {
+    if (kind <= BV_REF_SLOT) {
         const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid()];
         const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid()];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        BV_PIN("; slot operand", r);
         return r;
     }
     if (kind == BV_REF_VAR) {
@@ -176,12 +191,14 @@ DEV U256 bv_fetch(const BvCtx &c, const U256 &acc, uint32_t ref) {
         const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        BV_PIN("; variable operand", r);
         return r;
     }
     // constant: uniform address -> scalar loads
     const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
     r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
     r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+    BV_PIN("; constant operand", r);
     return r;
 }
 
@@ -241,7 +258,8 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
                      (1ull << BV_EXTRACT) | (1ull << BV_CONCAT) | (1ull << BV_SEXT) | (1ull << BV_ITE) | \
                      (1ull << BV_TAB) | (1ull << BV_SMIN) | (1ull << BV_SMAX) | (1ull << BV_ZEXT) | \
                      (1ull << BV_AND) | (1ull << BV_OR) | (1ull << BV_XOR) | (1ull << BV_LSHR) | \
-                     (1ull << BV_UREM) | (1ull << BV_UMIN) | (1ull << BV_UMAX))
+                     (1ull << BV_UREM) | (1ull << BV_UMIN) | (1ull << BV_UMAX) | (1ull << BV_RSUB) | \
+                     (1ull << BV_RCONCAT))
 
 // MG_BV_WAVES: minimum waves per SIMD the register allocation must allow (0
 // leaves the compiler's choice).  8 caps the kernel at 64 VGPRs (a few spill to
@@ -320,7 +338,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
             }
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
-            U256 A = bv_fetch(c, acc, ra);
+            if ((ra >> 30) != BV_REF_ACC) acc = bv_fetch(c, ra);    // A in the accumulator's registers
+            const U256 A = acc;
             U256 r;
             switch (op) {
             case BV_COPY: r = A; break;
@@ -331,7 +350,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             case BV_ZEXT: r = A; break;
             case BV_SEXT: r = bv_sext(A, rb); break;
             default: {
-                U256 B = bv_fetch(c, acc, rb);
+                U256 B = bv_fetch(c, rb);
                 if (op == BV_UDIV || op == BV_UREM) {        // the unsigned division site
                     r = bv_udivrem(op == BV_UDIV, A, B);
                     break;
@@ -371,7 +390,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_BXOR: r = u_small((A.w[0] ^ B.w[0]) & 1u); break;
                 case BV_BIMPLIES: r = u_small(((A.w[0] & 1u) ^ 1u) | (B.w[0] & 1u)); break;
                 case BV_ITE: {
-                    const U256 C = bv_fetch(c, acc, rc);
+                    const U256 C = bv_fetch(c, rc);
                     r = u_select((A.w[0] & 1u) != 0u, B, C);
                     break;
                 }
@@ -388,6 +407,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_UMAX: r = u_select(u_lt(A, B), B, A); break;
                 case BV_SMIN: r = u_select(u_slt(bv_sext(B, width), bv_sext(A, width)), B, A); break;
                 case BV_SMAX: r = u_select(u_slt(bv_sext(A, width), bv_sext(B, width)), B, A); break;
+                case BV_RSUB: r = u_sub(B, A); break;
+                case BV_RCONCAT: r = u_or(u_shl_n(B, rc), A); break;
                 default: r = u_zero(); break;
                 }
             }
@@ -472,6 +493,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
                                                op == BV_EXTRACT || op == BV_ZEXT || op == BV_SEXT) ? 1 : 2;
         for (int k = 0; k < nref; ++k) {
             const uint32_t ref = w[1 + k], kind = ref >> 30, idx = ref & 0x3fffffffu;
+            if (k > 0 && kind == BV_REF_ACC) {
+                msg = "accumulator operand past position A at instruction " + std::to_string(i);
+                return MG_EINVAL;
+            }
             if ((kind == BV_REF_SLOT && idx >= dags->n_slots) || (kind == BV_REF_VAR && idx >= models->n_vars) ||
                 (kind == BV_REF_CONST && idx >= dags->n_consts)) {
                 msg = "operand out of range at instruction " + std::to_string(i);

@@ -29,6 +29,20 @@ from .program import (MAX_SLOTS, OPCODE, REF_ACC, REF_CONST, REF_SLOT, REF_VAR, 
 _MAP = {"and": "and", "or": "or", "not": "not", "xor": "xor", "implies": "implies"}
 _CMP = {"eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
         "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u"}
+# The accumulator is only ever operand A (bv_eval.cuh keeps A in the
+# accumulator's registers).  A previous result needed as operand B is swapped
+# into A for these ops (the op itself, or its operand-swapped form), otherwise
+# it goes through a slot.
+_COMMUTATIVE = {"bvadd", "bvmul", "bvand", "bvor", "bvxor", "eq", "distinct", "and", "or", "xor",
+                "bvadd_noovfl_u", "bvumul_noovfl", "bvumin", "bvumax", "bvsmin", "bvsmax"}
+_SWAPPED = {"bvult": "bvugt", "bvugt": "bvult", "bvule": "bvuge", "bvuge": "bvule",
+            "bvslt": "bvsgt", "bvsgt": "bvslt", "bvsle": "bvsge", "bvsge": "bvsle",
+            "bvsub": "bvrsub", "bvrsub": "bvsub", "concat": "rconcat", "rconcat": "concat"}
+
+
+def _acc_ok(op: str, k: int) -> bool:
+    """Can operand k of `op` be the accumulator (after a swap when k == 1)?"""
+    return k == 0 or (k == 1 and (op in _COMMUTATIVE or op in _SWAPPED))
 
 
 _MINMAX = {  # ite(cmp(x, y), x, y) -> op(x, y); ite(cmp(x, y), y, x) -> the other one
@@ -216,7 +230,10 @@ class Compiler:
             for k, a in enumerate(v.args):
                 if isinstance(a, tuple):
                     uses.setdefault(a[1], []).append((i, k))
-        needs_slot = {j for j, us in uses.items() if any(i != j + 1 for i, _ in us)}
+        # a result lives only in the accumulator when its single reader is the next
+        # instruction, at a position the accumulator may take (_acc_ok)
+        needs_slot = {j for j, us in uses.items()
+                      if len(us) > 1 or any(i != j + 1 or not _acc_ok(virts[i].op, k) for i, k in us)}
         last_use = {j: max(i for i, _ in uses[j]) for j in needs_slot}
         slot_of: Dict[int, int] = {}
         free = list(range(MAX_SLOTS - 1, -1, -1))
@@ -235,19 +252,25 @@ class Compiler:
         out = np.zeros((n, 4), dtype=np.uint32)
         for i, v in enumerate(virts):
             refs = []
-            for a in v.args:
+            op = v.op
+            for k, a in enumerate(v.args):
                 if isinstance(a, tuple):
                     j = a[1]
-                    # the previous instruction's result is still in the accumulator
-                    refs.append(ref(REF_ACC, 0) if j == i - 1 else ref(REF_SLOT, slot_of[j]))
+                    # the previous instruction's result, still in the accumulator
+                    acc = j == i - 1 and (k == 0 or j not in slot_of)
+                    refs.append(ref(REF_ACC, 0) if acc else ref(REF_SLOT, slot_of[j]))
                 else:
                     refs.append(self._leaf_ref(a))
-            w = [enc_w0(v.op, v.width, slot_of.get(i)), 0, 0, 0]
+            if len(refs) > 1 and refs[1] >> 30 == REF_ACC:
+                refs[0], refs[1] = refs[1], refs[0]          # the accumulator becomes operand A
+                op = op if op in _COMMUTATIVE else _SWAPPED[op]
+            assert all(r >> 30 != REF_ACC for r in refs[1:]), "accumulator past operand A"
+            w = [enc_w0(op, v.width, slot_of.get(i)), 0, 0, 0]
             for k, r in enumerate(refs):
                 w[1 + k] = r
             if v.op in ("extract", "sign_extend"):
                 w[2] = v.imm
-            elif v.op == "concat" or v.op in _CMP or v.op == "tab":
+            elif v.op in ("concat", "rconcat") or v.op in _CMP or v.op == "tab":
                 w[3] = v.imm
             out[i] = w
         if n > TILE_INSNS:

@@ -20,7 +20,11 @@ OPS = ["copy", "bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem"
        "and", "or", "xor", "not", "implies", "ite", "extract", "concat", "zero_extend",
        "sign_extend", "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "distinct", "tab",
        # compiler-internal: ite(cmp(x, y), x, y) folded by flatten._fold_select
-       "bvumin", "bvumax", "bvsmin", "bvsmax"]
+       "bvumin", "bvumax", "bvsmin", "bvsmax",
+       # compiler-internal operand-swapped forms (the accumulator is only ever
+       # operand A, bv_eval.cuh): bvrsub(a, b) = b - a; rconcat(a, b) = concat(b, a)
+       # with the immediate the width of a
+       "bvrsub", "rconcat"]
 OPCODE = {name: i for i, name in enumerate(OPS)}
 UNARY = {"copy", "bvnot", "bvneg", "not", "extract", "zero_extend", "sign_extend"}
 REF_ACC, REF_SLOT, REF_VAR, REF_CONST = 0, 1, 2, 3

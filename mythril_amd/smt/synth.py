@@ -22,6 +22,8 @@ same draws so tests can evaluate it independently.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from .expr import Node, const as cnode, var as vnode
@@ -185,7 +187,10 @@ def c4_programs(dr: Draws) -> ProgramBatch:
         m = (cls == EXTCAT) & (sub % 2 == 1)          # concat(low128(spine), low128(leaf))
         emit(m, np.uint32(OPCODE["extract"] | (128 << 8) | (1 << 17)), A, 0)     # -> S0
         emit(m, w("extract", 128), lf, 0)
-        emit(m, w("concat", 256), S0, ACC, 128)
+        if _LEGACY_CONCAT:                            # A/B runs against builds before rconcat
+            emit(m, w("concat", 256), S0, ACC, 128)
+        else:
+            emit(m, w("rconcat", 256), ACC, S0, 128)  # concat(S0, acc): the accumulator stays operand A
         produced |= m
         m = cls == ITE                                # ite(leaf <u spine, spine, leaf)
         emit(m, w("bvumax", 256), A, lf)
@@ -331,13 +336,18 @@ def model_dict(pool: ModelPool, m: int) -> dict:
 
 # ---------------------------------------------------------------- algorithmic cost
 # SURVEY §8(d) cost table per instruction (int32 ops at w = ceil(width/32) limbs)
+# MYTH_C4_LEGACY_CONCAT=1 (scripts/ab_k2.py `lib:legacy`): emit concat(S0, acc),
+# the form library builds before the accumulator-in-A rule accept
+_LEGACY_CONCAT = os.environ.get("MYTH_C4_LEGACY_CONCAT") == "1"
+
+
 def _insn_cost(op: int, width: int) -> float:
     w = max(1, (width + 31) // 32)
     name = [k for k, v in OPCODE.items() if v == op][0]
-    if name in ("bvand", "bvor", "bvxor", "bvnot", "ite", "extract", "concat", "zero_extend",
+    if name in ("bvand", "bvor", "bvxor", "bvnot", "ite", "extract", "concat", "rconcat", "zero_extend",
                 "sign_extend", "copy"):
         return float(w)
-    if name in ("bvadd", "bvsub", "bvneg"):
+    if name in ("bvadd", "bvsub", "bvrsub", "bvneg"):
         return 2.0 * w
     if name in ("bvshl", "bvlshr", "bvashr", "bvumin", "bvumax", "bvsmin", "bvsmax"):
         return 3.0 * w          # min/max: the folded compare (2w) + select (w)

@@ -23,7 +23,7 @@ enum {
     OP_EQ, OP_ULT, OP_ULE, OP_UGT, OP_UGE, OP_SLT, OP_SLE, OP_SGT, OP_SGE,
     OP_BAND, OP_BOR, OP_BXOR, OP_BNOT, OP_BIMPLIES, OP_ITE, OP_EXTRACT, OP_CONCAT,
     OP_ZEXT, OP_SEXT, OP_ADD_NOOVF_U, OP_MUL_NOOVF_U, OP_SUB_NOUDF_U, OP_NE, OP_TAB,
-    OP_UMIN, OP_UMAX, OP_SMIN, OP_SMAX
+    OP_UMIN, OP_UMAX, OP_SMIN, OP_SMAX, OP_RSUB, OP_RCONCAT
 };
 
 static u256 w_mask(u256 v, unsigned w) {
@@ -168,6 +168,8 @@ static int eval_one(const job_t *j, uint32_t d, uint32_t m) {
         case OP_UMAX: r = u_lt(a, b) ? b : a; break;
         case OP_SMIN: r = u_slt(w_sext(b, width), w_sext(a, width)) ? b : a; break;
         case OP_SMAX: r = u_slt(w_sext(a, width), w_sext(b, width)) ? b : a; break;
+        case OP_RSUB: r = u_sub(b, a); break;
+        case OP_RCONCAT: r = u_or(u_shl(b, u_from64(ow)), a); break;   /* a low (ow bits), b high */
         default: r = u_zero(); break;
         }
         r = w_mask(r, width);

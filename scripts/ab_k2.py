@@ -3,7 +3,8 @@
 the instruction fetch (MG_BV_PROG=lds|scalar, read at upload) for the in-tree
 library and for every other library build given, each in a child process
 (MYTHGPU_LIB).  Every variant's (first_sat, sat_count) must equal the first's.
-usage: ab_k2.py [rounds] [other_lib.so ...]"""
+usage: ab_k2.py [rounds] [other_lib.so[:legacy] ...] (legacy: C4 with concat(S0, acc),
+for builds before the accumulator-in-A rule)"""
 import json
 import os
 import subprocess
@@ -44,11 +45,14 @@ def main():
     res, ref = {}, None
     for r in range(rounds):
         for lib in (libs if r % 2 == 0 else libs[::-1]):
-            name = Path(lib).stem if lib else "in-tree"
+            path, _, tag = (lib or "").partition(":")
+            name = Path(path).stem if lib else "in-tree"
             out = f"/tmp/ab_k2_{name}"
             env = dict(os.environ, AB_K2_CHILD=out)
             if lib:
-                env["MYTHGPU_LIB"] = str(Path(lib).resolve())
+                env["MYTHGPU_LIB"] = str(Path(path).resolve())
+            if tag == "legacy":           # a build before rconcat: C4's concat in the old form
+                env["MYTH_C4_LEGACY_CONCAT"] = "1"
             t = time.time()
             p = subprocess.run([sys.executable, __file__], env=env, capture_output=True, text=True, timeout=900)
             line = [x for x in p.stdout.splitlines() if x.startswith("{")]

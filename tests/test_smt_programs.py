@@ -51,6 +51,9 @@ def test_c4_programs_have_the_compilers_form():
     from collections import Counter
     from mythril_amd.smt.program import OPS
     norm = {"bvumax": "bvumin", "bvsmax": "bvsmin"}
+    # operand-swapped forms (flatten._SWAPPED: the accumulator is only operand A)
+    canon = {"rconcat": "concat", "bvrsub": "bvsub", "bvugt": "bvult", "bvuge": "bvule",
+             "bvsgt": "bvslt", "bvsge": "bvsle"}
     dr = synth.Draws(300, seed=synth.C4_SEED + 5)
     prog = synth.c4_programs(dr)
     n = exact = 0
@@ -59,8 +62,8 @@ def test_c4_programs_have_the_compilers_form():
             p = Compiler().compile(synth.dag_expr(dr, i))
         except Unsupported:
             continue
-        a = Counter(OPS[int(w) & 0xFF] for w in p[:, 0])
-        b = Counter(OPS[int(w) & 0xFF] for w in prog.program(i)[:, 0])
+        a = Counter(canon.get(OPS[int(w) & 0xFF], OPS[int(w) & 0xFF]) for w in p[:, 0])
+        b = Counter(canon.get(OPS[int(w) & 0xFF], OPS[int(w) & 0xFF]) for w in prog.program(i)[:, 0])
         exact += a == b
         extra = b - a
         assert not (a - b) - Counter({k: v for k, v in (a - b).items() if k in norm or k in norm.values()}), i
@@ -239,3 +242,26 @@ def test_select_store_folding_follows_z3_simplify():
     assert a[BVV(1, 256)].raw is x.raw
     # a store at a different constant index is skipped: select(S, 2)
     assert a[BVV(2, 256)].raw.args[0].op == "array"
+
+
+def test_accumulator_is_only_operand_a():
+    """bv_eval.cuh loads operand A into the accumulator's registers, so the
+    compiler never leaves the accumulator in operand B or C: it swaps
+    commutative ops, reverses compares, uses bvrsub / rconcat, or spills to a
+    slot (flatten._acc_ok).  Checked on random sets and on the C4 generator."""
+    from mythril_amd.smt.program import OPCODE, REF_ACC
+    rng = random.Random(99)
+    sets = [_random_constraints(rng, rng.randrange(1, 10)) for _ in range(300)]
+    prog, kept = compile_sets(sets)
+    assert len(kept) > 250
+    ops = prog.insns[:, 0] & 0xFF
+    unary = {OPCODE[o] for o in ("copy", "bvnot", "bvneg", "not", "extract", "zero_extend", "sign_extend")}
+    for w, op in zip(prog.insns, ops):
+        nref = 3 if op == OPCODE["ite"] else (1 if op in unary else 2)
+        assert all(int(w[1 + k]) >> 30 != REF_ACC for k in range(1, nref))
+    assert (ops == OPCODE["bvrsub"]).any() or (ops == OPCODE["bvugt"]).any()
+    c4 = synth.c4_programs(synth.Draws(2000, seed=synth.C4_SEED))
+    ops4 = c4.insns[:, 0] & 0xFF
+    for w, op in zip(c4.insns, ops4):
+        nref = 3 if op == OPCODE["ite"] else (1 if op in unary else 2)
+        assert all(int(w[1 + k]) >> 30 != REF_ACC for k in range(1, nref))
