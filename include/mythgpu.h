@@ -26,13 +26,15 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 7u   /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 8u   /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
                                6: taint lanes: object handles + annotation masks
                                7: symbolic memory bytes, storage chains, symbolic
-                                  SHA3 (MG_SYM_SLOAD..CONCAT, MG_REC_SYMKECCAK) */
+                                  SHA3 (MG_SYM_SLOAD..CONCAT, MG_REC_SYMKECCAK)
+                               8: mg_lanes_download_live; kernel-2 programs keep
+                                  the accumulator in operand A (bvrsub, rconcat) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -352,6 +354,15 @@ int         mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg);
  * upload also becomes the batch's resident initial image (see mg_lanes_reset). */
 int         mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *host, uint32_t first, uint32_t n);
 int         mg_lanes_download(mg_ctx *ctx, mg_lane_soa *host, uint32_t first, uint32_t n);
+/* mg_lanes_download of what the lanes can have changed, for a host image that
+ * was uploaded from the same buffers: the scalars, then each lane's stack rows
+ * below the largest sp of the range, memory below the largest msize, storage
+ * entries below the largest storage_count, records below the largest rec_len
+ * and trace entries below the largest trace_len.  calldata and the environment
+ * words (never written by a step) and everything above those bounds keep the
+ * host's contents.  The batched LaserEVM's per-launch copy-back
+ * (svm.py:293-337 drain) -- a full download moves every lane's whole stack.  */
+int         mg_lanes_download_live(mg_ctx *ctx, mg_lane_soa *host, uint32_t first, uint32_t n);
 /* Re-initialise every lane from the resident initial image on the device
  * (no host traffic): pc, sp, msize, gas, status, storage, steps.            */
 int         mg_lanes_reset(mg_ctx *ctx);
@@ -409,7 +420,12 @@ int         mg_event_counts(mg_ctx *ctx, uint32_t *sha3_count, uint32_t *exp_cou
 /* -------------------------------------------------- constraint prefilter */
 /* A batch of constraint sets, each compiled by the host into a register
  * program over 256-bit values (mythril_amd/smt/flatten.py).  Replaces the
- * model loop of ModelCache.check_quick_sat (support_utils.py:60-68).        */
+ * model loop of ModelCache.check_quick_sat (support_utils.py:60-68).
+ * Instruction: op | width << 8 | store << 17 | slot << 18, then three operand
+ * refs (kind << 30 | index; kind 0 = the accumulator, 1 slot, 2 variable,
+ * 3 constant) or immediates.  Since ABI 8 only operand A may be the
+ * accumulator (the flattener swaps / reverses / spills): a program with the
+ * accumulator in operand B or C is refused with MG_EINVAL.                   */
 typedef struct mg_dag_batch {
     uint32_t n_dags;
     uint32_t n_slots;       /* register slots a program may use (<= 16)       */

@@ -566,15 +566,24 @@ static int up_units(mg_ctx *ctx, const void *host, uint32_t n, uint32_t Uh, uint
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     return MG_OK;
 }
-static int down_units(mg_ctx *ctx, void *host, uint32_t n, uint32_t Uh, uint32_t W, const void *src, uint32_t first) {
+// Uc (<= Uh): units copied per lane (the rest of each host row is left as is)
+static int down_units(mg_ctx *ctx, void *host, uint32_t n, uint32_t Uh, uint32_t W, const void *src, uint32_t first,
+                      uint32_t Uc = 0xffffffffu) {
     if (!host || Uh == 0) return MG_OK;
-    const size_t bytes = (size_t)n * Uh * W * 4;
+    Uc = std::min(Uc, Uh);
+    if (Uc == 0 || n == 0) return MG_OK;
+    const size_t bytes = (size_t)n * Uc * W * 4;
     int rc;
     if ((rc = ensure_stage(ctx, bytes))) return rc;
-    hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)n * Uh * W)), dim3(256), 0, ctx->stream,
-                       (const uint32_t *)src, n, Uh, W, (uint32_t *)ctx->d_stage, ctx->L.N, first);
+    hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)n * Uc * W)), dim3(256), 0, ctx->stream,
+                       (const uint32_t *)src, n, Uc, W, (uint32_t *)ctx->d_stage, ctx->L.N, first);
     HIPX(ctx, hipGetLastError());
-    HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (Uc == Uh) {
+        HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    } else {
+        HIPX(ctx, hipMemcpy2DAsync(host, (size_t)Uh * W * 4, ctx->d_stage, (size_t)Uc * W * 4, (size_t)Uc * W * 4,
+                                   n, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     return MG_OK;
 }
@@ -591,16 +600,25 @@ static int up_bytes(mg_ctx *ctx, const uint8_t *host, uint32_t n, uint32_t bytes
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     return MG_OK;
 }
-static int down_bytes(mg_ctx *ctx, uint8_t *host, uint32_t n, uint32_t bytes_h, const uint32_t *src, uint32_t first) {
+// Dc (<= bytes_h / 4): dwords copied per lane (the rest of each host row is left as is)
+static int down_bytes(mg_ctx *ctx, uint8_t *host, uint32_t n, uint32_t bytes_h, const uint32_t *src, uint32_t first,
+                      uint32_t Dc = 0xffffffffu) {
     if (!host || bytes_h == 0) return MG_OK;
     const uint32_t Dh = bytes_h / 4;
-    const size_t bytes = (size_t)n * bytes_h;
+    Dc = std::min(Dc, Dh);
+    if (Dc == 0 || n == 0) return MG_OK;
+    const size_t bytes = (size_t)n * Dc * 4;
     int rc;
     if ((rc = ensure_stage(ctx, bytes))) return rc;
-    hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)n * Dh)), dim3(256), 0, ctx->stream,
-                       src, n, Dh, (uint8_t *)ctx->d_stage, ctx->L.N, first);
+    hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)n * Dc)), dim3(256), 0, ctx->stream,
+                       src, n, Dc, (uint8_t *)ctx->d_stage, ctx->L.N, first);
     HIPX(ctx, hipGetLastError());
-    HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (Dc == Dh) {
+        HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    } else {
+        HIPX(ctx, hipMemcpy2DAsync(host, (size_t)bytes_h, ctx->d_stage, (size_t)Dc * 4, (size_t)Dc * 4, n,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     return MG_OK;
 }
@@ -915,7 +933,23 @@ extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, u
     return MG_OK;
 }
 
+static uint32_t max_of(const uint32_t *v, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i) m = std::max(m, v[i]);
+    return m;
+}
+
+static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n, bool live);
+
 extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n) {
+    return lanes_download(ctx, h, first, n, false);
+}
+
+extern "C" int mg_lanes_download_live(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n) {
+    return lanes_download(ctx, h, first, n, true);
+}
+
+static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n, bool live) {
     if (!ctx) return MG_EINVAL;
     int rc;
     if ((rc = check_host_shape(ctx, h, first, n))) return rc;
@@ -939,20 +973,27 @@ extern "C" int mg_lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, ui
     if ((rc = down_scalar(ctx, h->gas_max, S8, n, L.gas_max, first))) return rc;
     if ((rc = down_scalar(ctx, h->gas_limit, S8, n, L.gas_limit, first))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = down_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first))) return rc;
-    if ((rc = down_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
-    if ((rc = down_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first))) return rc;
-    if ((rc = down_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
-    if ((rc = down_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
+    // live: only what a step can have written, below the range's largest bound
+    const uint32_t ALL = 0xffffffffu;
+    const uint32_t u_st = live ? max_of(h->sp, n) : ALL;
+    const uint32_t u_sto = live ? max_of(h->storage_count, n) : ALL;
+    const uint32_t d_mem = live ? (max_of(h->msize, n) + 3u) / 4u : ALL;
+    if ((rc = down_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first, u_st))) return rc;
+    if (!live && (rc = down_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
+    if ((rc = down_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first, u_sto))) return rc;
+    if ((rc = down_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first, d_mem))) return rc;
+    if (!live && (rc = down_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
     if (h->trace_cap) {
         if ((rc = down_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
         HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        if ((rc = down_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first))) return rc;
+        if ((rc = down_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first,
+                             live ? max_of(h->trace_len, n) : ALL))) return rc;
     }
     if (h->rec_cap) {
         if ((rc = down_scalar(ctx, h->rec_len, S4, n, L.rec_len, first))) return rc;
         HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        if ((rc = down_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first))) return rc;
+        if ((rc = down_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first, live ? max_of(h->rec_len, n) : ALL)))
+            return rc;
     }
     return MG_OK;
 }

@@ -139,10 +139,15 @@ class GpuDevice:
                     "mg_lanes_upload")
         self._planes(batch, first, n, True)
 
-    def download_range(self, batch: LaneBatch, first: int, n: int):
+    def download_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):
+        """Download lanes [first, first + n).  live=True (the host image was
+        uploaded from `batch`): only what a step can have changed, below the
+        range's largest sp / msize / storage count / record length
+        (mg_lanes_download_live)."""
         soa = batch.soa_range(first, n)
-        self._check(self.lib.mg_lanes_download(self.ctx, ctypes.addressof(soa), first, n),
-                    "mg_lanes_download")
+        fn = self.lib.mg_lanes_download_live if live else self.lib.mg_lanes_download
+        self._check(fn(self.ctx, ctypes.addressof(soa), first, n),
+                    "mg_lanes_download_live" if live else "mg_lanes_download")
         self._planes(batch, first, n, False)
 
     def set_loop_bound(self, bound: int):

@@ -740,7 +740,7 @@ class LaserEVM:
             self.lane_steps += st.lane_steps
             self.total_states += st.lane_steps      # one successor per executed step
             for lo, cnt in _ranges(run, gap=_MERGE_GAP):
-                dev.download_range(sched.b, lo, cnt)
+                dev.download_range(sched.b, lo, cnt, live=True)
             self._collect_records(sched.b, run)
             sched.set_after_launch(run)
 

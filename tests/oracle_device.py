@@ -94,7 +94,7 @@ class OracleDevice:
     def upload_range(self, batch: LaneBatch, first: int, n: int):
         self._copy(batch, self._img, first, n)
 
-    def download_range(self, batch: LaneBatch, first: int, n: int):
+    def download_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):
         self._copy(self._img, batch, first, n)
 
     def set_loop_bound(self, bound: int):
