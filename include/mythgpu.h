@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 8u   /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 9u   /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -34,7 +34,9 @@ extern "C" {
                                7: symbolic memory bytes, storage chains, symbolic
                                   SHA3 (MG_SYM_SLOAD..CONCAT, MG_REC_SYMKECCAK)
                                8: mg_lanes_download_live; kernel-2 programs keep
-                                  the accumulator in operand A (bvrsub, rconcat) */
+                                  the accumulator in operand A (bvrsub, rconcat)
+                               9: mg_lanes_upload_live; lane transfers batched
+                                  through one pinned DMA per phase */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -363,6 +365,14 @@ int         mg_lanes_download(mg_ctx *ctx, mg_lane_soa *host, uint32_t first, ui
  * host's contents.  The batched LaserEVM's per-launch copy-back
  * (svm.py:293-337 drain) -- a full download moves every lane's whole stack.  */
 int         mg_lanes_download_live(mg_ctx *ctx, mg_lane_soa *host, uint32_t first, uint32_t n);
+/* mg_lanes_upload of what a step reads: the scalars, calldata and environment
+ * words whole, each lane's stack rows below the largest sp of the range,
+ * memory below the largest msize (a step zero-fills memory it extends),
+ * storage entries below the largest storage_count, trace entries below the
+ * largest trace_len and records below the largest rec_len; device rows above
+ * those bounds keep their contents.  The batched LaserEVM's per-launch upload
+ * of the lanes its host hooks touched (svm.py:369-491 resume).               */
+int         mg_lanes_upload_live(mg_ctx *ctx, const mg_lane_soa *host, uint32_t first, uint32_t n);
 /* Re-initialise every lane from the resident initial image on the device
  * (no host traffic): pc, sp, msize, gas, status, storage, steps.            */
 int         mg_lanes_reset(mg_ctx *ctx);

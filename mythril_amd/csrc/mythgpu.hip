@@ -56,6 +56,10 @@ struct mg_ctx {
     // staging for upload/download (lane-major)
     void *d_stage = nullptr;
     size_t stage_bytes = 0;
+    // pinned host side of the batched transfers (XferPlan): one DMA per phase
+    uint8_t *h_xfer = nullptr;
+    size_t h_xfer_bytes = 0;
+    bool xfer_legacy = false;            // MG_XFER=legacy: one pageable copy + sync per field (A/B)
     DevCounters *d_ctr = nullptr;        // [blocks] per-block statistics of the last launch
     uint32_t ctr_cap = 0;
     std::vector<DevCounters> h_ctr;
@@ -211,6 +215,8 @@ extern "C" int mg_open(int device, mg_ctx **out) {
             if (v != 64 && v != 32 && v != 16) { rc = MG_EINVAL; break; }
             ctx->lpw = (uint32_t)v;
         }
+        const char *xf = getenv("MG_XFER");
+        ctx->xfer_legacy = xf && std::string(xf) == "legacy";
     } while (0);
     if (rc != MG_OK) { mg_close(ctx); return rc; }
     *out = ctx;
@@ -244,6 +250,7 @@ extern "C" void mg_close(mg_ctx *ctx) {
     for (void *p : ctx->retired) hipFree(p);
     if (ctx->h_ctr_pin) hipHostFree(ctx->h_ctr_pin);
     for (void *p : ctx->retired_host) hipHostFree(p);
+    if (ctx->h_xfer) hipHostFree(ctx->h_xfer);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -635,6 +642,145 @@ static int down_scalar(mg_ctx *ctx, void *host, size_t elem, uint32_t n, const v
     return MG_OK;
 }
 
+// ---- batched transfers ---------------------------------------------------------
+// One host<->device transfer of many lane fields.  Download: every field is
+// gathered (lane-major) into the device stage, ONE DMA copies the stage into a
+// pinned host buffer, ONE stream synchronisation, then the host copies the
+// rows into the caller's arrays.  Upload: the rows are packed into the pinned
+// buffer, ONE DMA, then scatter kernels / device copies (the caller syncs once).
+// The per-field form (pageable copy + synchronisation per field, kept as
+// MG_XFER=legacy) cost ~2.5 ms per LaserEVM launch (profiles/r03/hostprof).
+struct XferPlan {
+    enum Kind { SCALAR, UNITS, BYTES };
+    struct Item {
+        Kind kind;
+        void *host;             // caller's array (lane-major rows)
+        void *dev, *dev2;       // device field (dev2: a second destination on upload)
+        size_t elem;            // SCALAR: bytes per lane
+        uint32_t Uh, W, Uc;     // UNITS: host row of Uh units x W dwords, Uc units copied; BYTES: W = 0, Uh/Uc dwords
+        size_t off, len;        // in the stage
+    };
+    std::vector<Item> items;
+    size_t total = 0;
+    uint32_t n = 0, first = 0;
+    XferPlan(uint32_t n_, uint32_t first_) : n(n_), first(first_) {}
+    void add(Item it) {
+        if (!it.host) return;
+        if (it.kind == SCALAR) it.len = (size_t)n * it.elem;
+        else {
+            it.Uc = std::min(it.Uc, it.Uh);
+            if (it.Uc == 0 || n == 0) return;
+            it.len = (size_t)n * it.Uc * (it.kind == UNITS ? it.W : 1u) * 4u;
+        }
+        it.off = total;
+        total += (it.len + 15u) & ~(size_t)15u;
+        items.push_back(it);
+    }
+    void scalar(void *host, void *dev, size_t elem, void *dev2 = nullptr) {
+        add(Item{SCALAR, host, dev, dev2, elem, 0, 0, 0, 0, 0});
+    }
+    void units(void *host, uint32_t Uh, uint32_t W, void *dev, uint32_t Uc = 0xffffffffu, void *dev2 = nullptr) {
+        if (Uh) add(Item{UNITS, host, dev, dev2, 0, Uh, W, Uc, 0, 0});
+    }
+    void bytes(void *host, uint32_t bytes_h, void *dev, uint32_t Dc = 0xffffffffu) {
+        if (bytes_h) add(Item{BYTES, host, dev, nullptr, 0, bytes_h / 4u, 0, Dc, 0, 0});
+    }
+};
+
+static uint32_t max_of(const uint32_t *v, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i) m = std::max(m, v[i]);
+    return m;
+}
+
+static int ensure_hxfer(mg_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->h_xfer_bytes) return MG_OK;
+    if (ctx->h_xfer) hipHostFree(ctx->h_xfer);
+    ctx->h_xfer = nullptr;
+    ctx->h_xfer_bytes = 0;
+    const size_t cap = std::max<size_t>(bytes, 2 * ctx->h_xfer_bytes + (1u << 20));
+    if (hipHostMalloc((void **)&ctx->h_xfer, cap, hipHostMallocDefault) != hipSuccess)
+        return set_err(ctx, MG_ENOMEM, "hipHostMalloc transfer buffer %zu", cap);
+    ctx->h_xfer_bytes = cap;
+    return MG_OK;
+}
+
+// a row of `row_c` bytes out of every `row_h`-byte host row: one copy when whole
+static void rows_copy(uint8_t *dst, size_t dst_row, const uint8_t *src, size_t src_row, size_t row, uint32_t n) {
+    if (dst_row == row && src_row == row) { std::memcpy(dst, src, row * n); return; }
+    for (uint32_t i = 0; i < n; ++i) std::memcpy(dst + i * dst_row, src + i * src_row, row);
+}
+
+static int xfer_down(mg_ctx *ctx, const XferPlan &x) {
+    if (x.items.empty()) return MG_OK;
+    int rc;
+    if ((rc = ensure_stage(ctx, x.total)) || (rc = ensure_hxfer(ctx, x.total))) return rc;
+    uint8_t *ds = (uint8_t *)ctx->d_stage;
+    const uint32_t N = ctx->L.N;
+    for (const auto &it : x.items) {
+        if (it.kind == XferPlan::SCALAR) {
+            HIPX(ctx, hipMemcpyAsync(ds + it.off, (const uint8_t *)it.dev + (size_t)x.first * it.elem, it.len,
+                                     hipMemcpyDeviceToDevice, ctx->stream));
+        } else if (it.kind == XferPlan::UNITS) {
+            hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)x.n * it.Uc * it.W)), dim3(256), 0, ctx->stream,
+                               (const uint32_t *)it.dev, x.n, it.Uc, it.W, (uint32_t *)(ds + it.off), N, x.first);
+        } else {
+            hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)x.n * it.Uc)), dim3(256), 0, ctx->stream,
+                               (const uint32_t *)it.dev, x.n, it.Uc, ds + it.off, N, x.first);
+        }
+    }
+    HIPX(ctx, hipGetLastError());
+    HIPX(ctx, hipMemcpyAsync(ctx->h_xfer, ds, x.total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    for (const auto &it : x.items) {
+        const uint8_t *src = ctx->h_xfer + it.off;
+        if (it.kind == XferPlan::SCALAR) {
+            std::memcpy(it.host, src, it.len);
+        } else {
+            const size_t unit = it.kind == XferPlan::UNITS ? (size_t)it.W * 4u : 4u;
+            rows_copy((uint8_t *)it.host, it.Uh * unit, src, it.Uc * unit, it.Uc * unit, x.n);
+        }
+    }
+    return MG_OK;
+}
+
+// enqueues the upload; the caller synchronises the stream (h_xfer is reused)
+static int xfer_up(mg_ctx *ctx, const XferPlan &x) {
+    if (x.items.empty()) return MG_OK;
+    int rc;
+    if ((rc = ensure_stage(ctx, x.total)) || (rc = ensure_hxfer(ctx, x.total))) return rc;
+    for (const auto &it : x.items) {
+        uint8_t *dst = ctx->h_xfer + it.off;
+        if (it.kind == XferPlan::SCALAR) {
+            std::memcpy(dst, it.host, it.len);
+        } else {
+            const size_t unit = it.kind == XferPlan::UNITS ? (size_t)it.W * 4u : 4u;
+            rows_copy(dst, it.Uc * unit, (const uint8_t *)it.host, it.Uh * unit, it.Uc * unit, x.n);
+        }
+    }
+    uint8_t *ds = (uint8_t *)ctx->d_stage;
+    HIPX(ctx, hipMemcpyAsync(ds, ctx->h_xfer, x.total, hipMemcpyHostToDevice, ctx->stream));
+    const uint32_t N = ctx->L.N;
+    for (const auto &it : x.items) {
+        for (void *dev : {it.dev, it.dev2}) {
+            if (!dev) continue;
+            if (it.kind == XferPlan::SCALAR) {
+                HIPX(ctx, hipMemcpyAsync((uint8_t *)dev + (size_t)x.first * it.elem, ds + it.off, it.len,
+                                         hipMemcpyDeviceToDevice, ctx->stream));
+            } else if (it.kind == XferPlan::UNITS) {
+                hipLaunchKernelGGL(k_scatter_units, dim3(blocks_for((size_t)x.n * it.Uc * it.W)), dim3(256), 0,
+                                   ctx->stream, (const uint32_t *)(ds + it.off), x.n, it.Uc, it.W, (uint32_t *)dev,
+                                   N, x.first);
+            } else {
+                hipLaunchKernelGGL(k_scatter_bytes, dim3(blocks_for((size_t)x.n * it.Uc)), dim3(256), 0, ctx->stream,
+                                   ds + it.off, x.n, it.Uc, (uint32_t *)dev, N, x.first);
+            }
+        }
+    }
+    HIPX(ctx, hipGetLastError());
+    return MG_OK;
+}
+
 static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
     if (!ctx->have_lanes) return set_err(ctx, MG_ESTATE, "mg_lanes_alloc first");
     if (!h || h->n != n || first + (uint64_t)n > ctx->L.n)
@@ -647,27 +793,10 @@ static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, u
     return MG_OK;
 }
 
-extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
-    if (!ctx) return MG_EINVAL;
-    int rc;
-    if ((rc = check_host_shape(ctx, h, first, n))) return rc;
-    HIPX(ctx, hipSetDevice(ctx->device));
+// MG_XFER=legacy: the per-field upload (one pageable copy + synchronisation per field)
+static int lanes_upload_legacy(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
     DevLanes &L = ctx->L;
-    // validate code ids and capacities on the host before any kernel sees them
-    if (ctx->code_used.size() < ctx->codes.size()) ctx->code_used.resize(ctx->codes.size(), 0);
-    for (uint32_t i = 0; i < n; ++i) {
-        if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
-        ctx->code_used[h->code_id[i]] = 1;
-        if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
-            h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap ||
-            (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u) ||
-            (h->rec_cap ? h->rec_len[i] > h->rec_cap : 0u))
-            return set_err(ctx, MG_EINVAL, "lane %u: state exceeds its host capacities", first + i);
-    }
-    bool fresh = true;
-    for (uint32_t i = 0; i < n && fresh; ++i)
-        fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0) &&
-                (!h->rec_cap || h->rec_len[i] == 0);
+    int rc;
     const size_t S4 = 4, S8 = 8;
     if ((rc = up_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
     if ((rc = up_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
@@ -714,6 +843,82 @@ extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first
         if ((rc = up_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first))) return rc;
     } else {
         HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
+    }
+    return MG_OK;
+}
+
+static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n, bool live);
+
+extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
+    return lanes_upload(ctx, h, first, n, false);
+}
+
+extern "C" int mg_lanes_upload_live(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
+    return lanes_upload(ctx, h, first, n, true);
+}
+
+static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n, bool live) {
+    if (!ctx) return MG_EINVAL;
+    int rc;
+    if ((rc = check_host_shape(ctx, h, first, n))) return rc;
+    HIPX(ctx, hipSetDevice(ctx->device));
+    DevLanes &L = ctx->L;
+    // validate code ids and capacities on the host before any kernel sees them
+    if (ctx->code_used.size() < ctx->codes.size()) ctx->code_used.resize(ctx->codes.size(), 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (h->code_id[i] >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "lane %u: unknown code_id", first + i);
+        ctx->code_used[h->code_id[i]] = 1;
+        if (h->sp[i] > h->stack_cap || h->msize[i] > h->mem_cap || h->msize[i] % 32 ||
+            h->calldata_len[i] > h->calldata_cap || h->storage_count[i] > h->storage_cap ||
+            (h->trace_cap ? h->trace_len[i] > h->trace_cap : 0u) ||
+            (h->rec_cap ? h->rec_len[i] > h->rec_cap : 0u))
+            return set_err(ctx, MG_EINVAL, "lane %u: state exceeds its host capacities", first + i);
+    }
+    bool fresh = true;
+    for (uint32_t i = 0; i < n && fresh; ++i)
+        fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0) &&
+                (!h->rec_cap || h->rec_len[i] == 0);
+    if (ctx->xfer_legacy) {
+        if ((rc = lanes_upload_legacy(ctx, h, first, n))) return rc;
+    } else {
+        const uint32_t ALL = 0xffffffffu;
+        XferPlan x(n, first);
+        x.scalar(h->code_id, L.code_id, 4);
+        x.scalar(h->pc, L.pc, 4, ctx->i_pc);
+        x.scalar(h->sp, L.sp, 4);
+        x.scalar(h->msize, L.msize, 4);
+        x.scalar(h->depth, L.depth, 4, ctx->i_depth);
+        x.scalar(h->status, L.status, 4, ctx->i_status);
+        x.scalar(h->aux, L.aux, 4, ctx->i_aux);
+        x.scalar(h->steps, L.steps, 4, ctx->i_steps);
+        x.scalar(h->flags, L.flags, 4);
+        x.scalar(h->calldata_len, L.calldata_len, 4);
+        x.scalar(h->storage_count, L.storage_count, 4, ctx->i_storage_count);
+        x.scalar(h->ret_offset, L.ret_offset, 4);
+        x.scalar(h->ret_len, L.ret_len, 4);
+        x.scalar(h->gas_min, L.gas_min, 8, ctx->i_gas_min);
+        x.scalar(h->gas_max, L.gas_max, 8, ctx->i_gas_max);
+        x.scalar(h->gas_limit, L.gas_limit, 8);
+        x.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
+        x.units(h->env, MG_ENV_WORDS, 8, L.env);
+        x.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL,
+                ctx->i_storage);
+        x.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
+        x.bytes(h->calldata, h->calldata_cap, L.calldata);
+        if (h->trace_cap) {
+            x.scalar(h->trace_len, L.trace_len, 4);
+            x.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
+        }
+        if (h->rec_cap) {
+            x.scalar(h->rec_len, L.rec_len, 4);
+            x.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
+        }
+        HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
+        HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
+        if (!h->trace_cap) HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
+        if (!h->rec_cap) HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
+        if ((rc = xfer_up(ctx, x))) return rc;
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->uploaded = true;
     ctx->init_fresh = (first == 0 && n == L.n) ? fresh : (ctx->init_fresh && fresh);
@@ -768,6 +973,19 @@ extern "C" int mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, u
     for (uint32_t i = 0; i < n; ++i)
         if (h->n_nodes[i] > h->node_cap || h->n_consts[i] > h->const_cap)
             return set_err(ctx, MG_EINVAL, "lane %u: arena exceeds its host capacities", first + i);
+    if (!ctx->xfer_legacy) {
+        XferPlan x(n, first);
+        x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
+        x.scalar(h->n_consts, ctx->S.n_consts, 4);
+        x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
+        x.units(h->node, h->node_cap, 4, ctx->S.node);
+        x.units(h->cval, h->const_cap, 8, ctx->S.cval);
+        x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
+        x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
+        if ((rc = xfer_up(ctx, x))) return rc;
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        return MG_OK;
+    }
     if ((rc = up_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
     if ((rc = up_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
@@ -784,6 +1002,17 @@ extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint3
     int rc;
     if ((rc = check_sym_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
+    if (!ctx->xfer_legacy) {
+        XferPlan x(n, first);
+        x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
+        x.scalar(h->n_consts, ctx->S.n_consts, 4);
+        x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
+        x.units(h->node, h->node_cap, 4, ctx->S.node);
+        x.units(h->cval, h->const_cap, 8, ctx->S.cval);
+        x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
+        x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
+        return xfer_down(ctx, x);
+    }
     if ((rc = down_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
     if ((rc = down_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
@@ -903,6 +1132,20 @@ extern "C" int mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *h, uint32_t firs
                 return set_err(ctx, MG_EINVAL, "lane %u slot %u: handle %u past obj_cap", first + i, k, so[k]);
     }
     DevTaint &T = ctx->T;
+    if (!ctx->xfer_legacy) {
+        XferPlan x(n, first);
+        x.scalar(h->n_obj, T.n_obj, 4);
+        x.scalar(h->n_fixed, T.n_fixed, 4);
+        x.scalar(h->n_atoms, T.n_atoms, 4);
+        x.scalar(h->tflags, T.tflags, 4);
+        x.scalar(h->sink, T.sink, 8);
+        x.scalar(h->ymask, T.ymask, 8);
+        x.units(h->sobj, h->stack_cap, 1, T.sobj);
+        x.units(h->omask, h->obj_cap, 2, T.omask);
+        if ((rc = xfer_up(ctx, x))) return rc;
+        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+        return MG_OK;
+    }
     if ((rc = up_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
     if ((rc = up_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
     if ((rc = up_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
@@ -921,6 +1164,18 @@ extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, u
     if ((rc = check_taint_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
     DevTaint &T = ctx->T;
+    if (!ctx->xfer_legacy) {
+        XferPlan x(n, first);
+        x.scalar(h->n_obj, T.n_obj, 4);
+        x.scalar(h->n_fixed, T.n_fixed, 4);
+        x.scalar(h->n_atoms, T.n_atoms, 4);
+        x.scalar(h->tflags, T.tflags, 4);
+        x.scalar(h->sink, T.sink, 8);
+        x.scalar(h->ymask, T.ymask, 8);
+        x.units(h->sobj, h->stack_cap, 1, T.sobj);
+        x.units(h->omask, h->obj_cap, 2, T.omask);
+        return xfer_down(ctx, x);
+    }
     if ((rc = down_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
     if ((rc = down_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
     if ((rc = down_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
@@ -933,11 +1188,6 @@ extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, u
     return MG_OK;
 }
 
-static uint32_t max_of(const uint32_t *v, uint32_t n) {
-    uint32_t m = 0;
-    for (uint32_t i = 0; i < n; ++i) m = std::max(m, v[i]);
-    return m;
-}
 
 static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t n, bool live);
 
@@ -955,6 +1205,41 @@ static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t 
     if ((rc = check_host_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
     DevLanes &L = ctx->L;
+    if (!ctx->xfer_legacy) {
+        // phase 1: the per-lane scalars (they bound phase 2's rows)
+        XferPlan x(n, first);
+        x.scalar(h->code_id, L.code_id, 4);
+        x.scalar(h->pc, L.pc, 4);
+        x.scalar(h->sp, L.sp, 4);
+        x.scalar(h->msize, L.msize, 4);
+        x.scalar(h->depth, L.depth, 4);
+        x.scalar(h->status, L.status, 4);
+        x.scalar(h->aux, L.aux, 4);
+        x.scalar(h->steps, L.steps, 4);
+        x.scalar(h->flags, L.flags, 4);
+        x.scalar(h->calldata_len, L.calldata_len, 4);
+        x.scalar(h->storage_count, L.storage_count, 4);
+        x.scalar(h->ret_offset, L.ret_offset, 4);
+        x.scalar(h->ret_len, L.ret_len, 4);
+        x.scalar(h->gas_min, L.gas_min, 8);
+        x.scalar(h->gas_max, L.gas_max, 8);
+        x.scalar(h->gas_limit, L.gas_limit, 8);
+        if (h->trace_cap) x.scalar(h->trace_len, L.trace_len, 4);
+        if (h->rec_cap) x.scalar(h->rec_len, L.rec_len, 4);
+        if ((rc = xfer_down(ctx, x))) return rc;
+        // phase 2: rows; live: only what a step can have written, below the
+        // range's largest sp / storage count / msize / trace and record length
+        const uint32_t ALL = 0xffffffffu;
+        XferPlan y(n, first);
+        y.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
+        if (!live) y.units(h->env, MG_ENV_WORDS, 8, L.env);
+        y.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL);
+        y.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
+        if (!live) y.bytes(h->calldata, h->calldata_cap, L.calldata);
+        if (h->trace_cap) y.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
+        if (h->rec_cap) y.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
+        return xfer_down(ctx, y);
+    }
     const size_t S4 = 4, S8 = 8;
     if ((rc = down_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
     if ((rc = down_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;

@@ -132,11 +132,14 @@ class GpuDevice:
                     "mg_lanes_download")
         self._planes(batch, 0, batch.n, False, first)
 
-    def upload_range(self, batch: LaneBatch, first: int, n: int):
-        """Upload lanes [first, first + n) of `batch` to the same device lanes."""
+    def upload_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):
+        """Upload lanes [first, first + n) of `batch` to the same device lanes.
+        live=True: only what a step reads, below the range's largest sp /
+        msize / storage count / record and trace length (mg_lanes_upload_live)."""
         soa = batch.soa_range(first, n)
-        self._check(self.lib.mg_lanes_upload(self.ctx, ctypes.addressof(soa), first, n),
-                    "mg_lanes_upload")
+        fn = self.lib.mg_lanes_upload_live if live else self.lib.mg_lanes_upload
+        self._check(fn(self.ctx, ctypes.addressof(soa), first, n),
+                    "mg_lanes_upload_live" if live else "mg_lanes_upload")
         self._planes(batch, first, n, True)
 
     def download_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):

@@ -18,8 +18,8 @@ from typing import Dict, List, Optional, Union
 
 import numpy as np
 
-from ..smt.expr import (Array, BitVec, Bool, Expression, Extract, If, K, Node, _select, simplify_concat,
-                        symbol_factory)
+from ..smt.expr import (Array, BitVec, Bool, ConstWord, Expression, Extract, If, K, Node, _select,
+                        simplify_concat, symbol_factory)
 from .disassembly import Disassembly
 
 M256 = (1 << 256) - 1
@@ -103,6 +103,145 @@ class MachineStack(list):
 
     def __iadd__(self, other):
         raise NotImplementedError("Implement this if needed")
+
+
+class LazyStack(MachineStack):
+    """A MachineStack read back from a lane (LaserEVM._materialise): the words
+    stay the lane's raw little-endian bytes until something reads an element,
+    and `mut` records whether anything changed it since.  Most hook events
+    never look at the stack, so they build no word objects; the raw bytes are a
+    copy, so the lane's later steps cannot show through."""
+
+    def __init__(self, raw: bytes):
+        list.__init__(self)
+        self._raw = raw
+        self.mut = False
+
+    def _fill(self) -> None:
+        raw = self._raw
+        if raw is not None:
+            self._raw = None
+            fb = int.from_bytes
+            list.extend(self, [ConstWord(fb(raw[k: k + 32], "little")) for k in range(0, len(raw), 32)])
+
+    def __len__(self):
+        raw = self._raw
+        return len(raw) >> 5 if raw is not None else list.__len__(self)
+
+    def top_int(self, k: int) -> int:
+        """int of the k-th word from the top (1 = top), without building words."""
+        raw = self._raw
+        if raw is not None:
+            e = len(raw) - 32 * (k - 1)
+            if k < 1 or e < 32:
+                raise StackUnderflowException("Trying to access a stack element which doesn't exist")
+            return int.from_bytes(raw[e - 32: e], "little")
+        return concrete(self[-k])
+
+    def __bool__(self):
+        return len(self) > 0
+
+    def __getitem__(self, item):
+        self._fill()
+        return MachineStack.__getitem__(self, item)
+
+    def __iter__(self):
+        self._fill()
+        return list.__iter__(self)
+
+    def __reversed__(self):
+        self._fill()
+        return list.__reversed__(self)
+
+    def __contains__(self, x):
+        self._fill()
+        return list.__contains__(self, x)
+
+    def __eq__(self, other):
+        self._fill()
+        return list.__eq__(self, other)
+
+    def __ne__(self, other):
+        self._fill()
+        return list.__ne__(self, other)
+
+    __hash__ = None
+
+    def __repr__(self):
+        self._fill()
+        return list.__repr__(self)
+
+    def index(self, *a):
+        self._fill()
+        return list.index(self, *a)
+
+    def count(self, x):
+        self._fill()
+        return list.count(self, x)
+
+    def copy(self):
+        self._fill()
+        return MachineStack(list.__iter__(self))
+
+    def __copy__(self):
+        return self.copy()
+
+    def __deepcopy__(self, memo=None):
+        return self.copy()
+
+    def __reduce_ex__(self, protocol):
+        return (MachineStack, (self.copy(),))
+
+    # mutators: fill, mark, then the MachineStack / list behaviour
+    def append(self, element) -> None:
+        self._fill()
+        self.mut = True
+        MachineStack.append(self, element)
+
+    def pop(self, index=-1):
+        self._fill()
+        self.mut = True
+        return MachineStack.pop(self, index)
+
+    def __setitem__(self, key, value):
+        self._fill()
+        self.mut = True
+        list.__setitem__(self, key, value)
+
+    def __delitem__(self, key):
+        self._fill()
+        self.mut = True
+        list.__delitem__(self, key)
+
+    def extend(self, it):
+        self._fill()
+        self.mut = True
+        list.extend(self, it)
+
+    def insert(self, i, x):
+        self._fill()
+        self.mut = True
+        list.insert(self, i, x)
+
+    def remove(self, x):
+        self._fill()
+        self.mut = True
+        list.remove(self, x)
+
+    def clear(self):
+        self._fill()
+        self.mut = True
+        list.clear(self)
+
+    def sort(self, *a, **k):
+        self._fill()
+        self.mut = True
+        list.sort(self, *a, **k)
+
+    def reverse(self):
+        self._fill()
+        self.mut = True
+        list.reverse(self)
 
 
 class Memory:
@@ -366,7 +505,26 @@ class Storage:
         """Replace the contents by concrete slots (slot mode)."""
         self._ver += 1
         self._chain = self._raws = None
+        self.__dict__.pop("_pending", None)
         self.printable_storage = dict(slots)
+
+    def set_slots_raw(self, raw: bytes) -> None:
+        """set_slots from a lane's storage rows (64 bytes per slot: key then value,
+        little-endian limbs); the dict is built on first use of printable_storage."""
+        self._ver += 1
+        self._chain = self._raws = None
+        self.__dict__.pop("printable_storage", None)
+        self._pending = raw
+
+    def __getattr__(self, name):
+        if name == "printable_storage":
+            raw = self.__dict__.pop("_pending", None)
+            if raw is not None:
+                fb = int.from_bytes
+                d = self.printable_storage = {fb(raw[k: k + 32], "little"): fb(raw[k + 32: k + 64], "little")
+                                              for k in range(0, len(raw), 64)}
+                return d
+        raise AttributeError(name)
 
     def __copy__(self):
         s = Storage(self.concrete, self.address, None)

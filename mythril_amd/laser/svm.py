@@ -39,6 +39,7 @@ import itertools
 import logging
 import os
 import random
+import sys
 from collections import defaultdict
 from copy import copy
 from datetime import datetime, timedelta
@@ -62,7 +63,7 @@ from ..smt import solver as solver_mod
 from ..smt.solver import Constraints, SnapshotConstraints, SolverBackendMissing, args, query_raw
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
-from .state import GlobalState, Memory, MachineStack, concrete
+from .state import GlobalState, LazyStack, Memory, MachineStack, concrete
 from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
 from . import symbolic as sym
 from . import taint as tnt
@@ -610,7 +611,7 @@ class LaserEVM:
         elif b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])
         else:
-            ms.stack = MachineStack([ConstWord(w) for w in rows_to_words(b.stack[i, :sp])])
+            ms.stack = LazyStack(b.stack[i, :sp].tobytes())
         if b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack(tnt.materialise(b, i, s, self._tl[i], self._plan, list(ms.stack)))
         ms.depth = int(b.depth[i])
@@ -623,12 +624,7 @@ class LaserEVM:
             acct.storage = storage
         else:
             ms.memory = Memory(bytes(b.memory[i, : int(b.msize[i])]))
-            cnt = int(b.storage_count[i])
-            if cnt:
-                kv = rows_to_words(b.storage[i, :cnt].reshape(2 * cnt, 8))
-                acct.storage.set_slots({kv[2 * k]: kv[2 * k + 1] for k in range(cnt)})
-            else:
-                acct.storage.set_slots({})
+            acct.storage.set_slots_raw(b.storage[i, :int(b.storage_count[i])].tobytes())
         s.lane_steps = int(b.steps[i])
         if b.shape.trace_cap:
             ann = _annotation_of(s)
@@ -722,7 +718,7 @@ class LaserEVM:
             # nearby ranges merge into one call (the fixed cost per call is far
             # above the per-lane bytes of a gap)
             for lo, cnt in _ranges(sorted(sched.dirty), gap=_MERGE_GAP):
-                dev.upload_range(sched.b, lo, cnt)
+                dev.upload_range(sched.b, lo, cnt, live=True)
                 for pos in range(lo, lo + cnt):
                     lanes[pos].dirty = False
             sched.dirty.clear()
@@ -866,6 +862,8 @@ class LaserEVM:
         if status == MG_HOOK:
             # plain concrete lanes: a state the hooks leave untouched needs no repack
             sig0 = _hook_sig(s) if not (b.taint or b.symbolic or b.shape.trace_cap) else None
+            pre_state = s
+            refs0 = _held(pre_state)
             # execute_state returning [] puts the popped state in final_states
             # when track_gas (svm.py:328-334), whatever the reason
             try:
@@ -886,14 +884,16 @@ class LaserEVM:
                 if track_gas:
                     final_states.append(s)
                 return
-            pre_state = s
             for hook in self.instr_pre_hook.get(name, ()):
                 hook(s)
             post = self._has_post(name) or single_step
             # the hooks keep the state they saw (the reference's evaluate steps a
-            # copy, instructions.py:121-130): the lane goes on with a copy
-            s = copy(s)
-            ln.state = s
+            # copy, instructions.py:121-130): the lane goes on with a copy -- unless
+            # no hook kept a reference to the state or to any part of it the lane
+            # changes later (_held), when nothing can observe the difference
+            if post or _held(pre_state) != refs0:
+                s = copy(s)
+                ln.state = s
             # hooks may have rewritten the state: repack, then run the hooked
             # instruction alone (STEP1) when post hooks must see its successor
             steps = int(b.steps[i])
@@ -1086,19 +1086,24 @@ class LaserEVM:
         real_pops = _ACK_SAFE.get(name)
         if real_pops is None:
             return False
-        if real_pops and any(isinstance(x, Expression) and x.value is None
-                             for x in s.mstate.stack[-real_pops:]):
-            return False             # symbolic operand: a fork or escape at this round
         ms, env = s.mstate, s.environment
         st = ms.stack
         n = len(st)
         if n < real_pops:
             return False                 # the real pop raises (table counts differ)
+        if type(st) is LazyStack:
+            top = st.top_int             # a concrete lane's words, read without building them
+        else:
+            if real_pops and any(isinstance(x, Expression) and x.value is None for x in st[-real_pops:]):
+                return False             # symbolic operand: a fork or escape at this round
+
+            def top(k):
+                return concrete(st[-k])
         if (name.startswith("PUSH") or name.startswith("DUP")) and n + 1 > min(1024, b.shape.stack_cap):
             return False
         extra = 0
         if name in ("MLOAD", "MSTORE", "MSTORE8"):
-            off = concrete(st[-1])
+            off = top(1)
             end = off + (1 if name == "MSTORE8" else 32)
             if end > b.shape.mem_cap:
                 return False             # capacity escape
@@ -1108,12 +1113,12 @@ class LaserEVM:
             if env.static:
                 return False
             store = env.active_account.storage.printable_storage
-            if concrete(st[-1]) not in store and len(store) >= b.shape.storage_cap:
+            if top(1) not in store and len(store) >= b.shape.storage_cap:
                 return False
         elif name in ("JUMP", "JUMPI"):
-            if name == "JUMPI" and concrete(st[-2]) == 0:
+            if name == "JUMPI" and top(2) == 0:
                 pass
-            elif not self._jumpdest_at(env.code, concrete(st[-1])):
+            elif not self._jumpdest_at(env.code, top(1)):
                 return False             # VmException / dropped branch at this round
         tx = s.current_transaction
         lim = getattr(tx, "gas_limit", None)
@@ -1202,10 +1207,28 @@ def _hook_sig(s: GlobalState):
     ms, env = s.mstate, s.environment
     acct = env.active_account
     stack = ms.stack
-    return (ms.pc, id(stack), len(stack), tuple(map(id, stack)), id(ms.memory), ms.memory._ver,
+    # a lane's LazyStack records its own changes: no element is built to compare
+    st = (stack.mut,) if type(stack) is LazyStack else (len(stack), tuple(map(id, stack)))
+    return (ms.pc, id(stack), st, id(ms.memory), ms.memory._ver,
             ms.depth, ms.min_gas_used, ms.max_gas_used, id(env), id(env.code), env.static, id(env.calldata),
             id(env.address), id(env.sender), id(env.origin), id(env.callvalue), id(env.gasprice),
             id(acct), id(acct.storage), acct.storage._ver, id(s.current_transaction))
+
+
+def _held(s: GlobalState) -> Tuple[int, ...]:
+    """Reference counts of a state and of the parts of it a lane's next
+    materialisation or host step changes in place (machine state, world state,
+    its constraint and annotation lists, the environment, the active account and
+    its storage, the transaction stack, the annotations): equal before and after
+    the hooks means no hook kept any of them."""
+    ws, env = s.world_state, s.environment
+    acct = env.active_account
+    rc = sys.getrefcount
+    out = (rc(s), rc(s.mstate), rc(ws), rc(ws.constraints), rc(ws._annotations), rc(env), rc(acct),
+           rc(acct.storage), rc(s.transaction_stack), rc(s._annotations))
+    if s._annotations:
+        out += tuple(rc(a) for a in s._annotations)
+    return out
 
 
 def _rearm(b: LaneBatch, i: int) -> None:

@@ -117,6 +117,7 @@ SIGNATURES = {
     "mg_lanes_upload": (_I, [_P, _P, _U32, _U32]),
     "mg_lanes_download": (_I, [_P, _P, _U32, _U32]),
     "mg_lanes_download_live": (_I, [_P, _P, _U32, _U32]),
+    "mg_lanes_upload_live": (_I, [_P, _P, _U32, _U32]),
     "mg_lanes_reset": (_I, [_P]),
     "mg_step": (_I, [_P, _P, _U32, _U32, ctypes.POINTER(MgStepStats)]),
     "mg_step_async": (_I, [_P, _P, _U32, _U32]),

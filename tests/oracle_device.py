@@ -91,7 +91,7 @@ class OracleDevice:
     def download(self, batch: LaneBatch, first: int = 0):
         self._copy(self._img, batch, first, batch.n)
 
-    def upload_range(self, batch: LaneBatch, first: int, n: int):
+    def upload_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):
         self._copy(batch, self._img, first, n)
 
     def download_range(self, batch: LaneBatch, first: int, n: int, live: bool = False):

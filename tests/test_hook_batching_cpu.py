@@ -136,3 +136,63 @@ def test_host_halts_equal_device_halts(strategy, monkeypatch):
     assert log_h == log_d
     assert open_h == open_d
     assert launches_h < launches_d
+
+
+@pytest.mark.parametrize("keep", ["state", "mstate", "world_state", "storage", "nothing"])
+def test_a_kept_state_stays_the_one_the_hook_saw(keep, monkeypatch):
+    """The lane goes on with the hooked state itself when no hook kept it or a
+    part of it the lane changes later (svm._held); a hook that keeps the state
+    (or its machine state, world state or storage) must find it exactly as it
+    saw it after exec, as with the reference's copy per evaluate
+    (instructions.py:121-130) -- and the event log must not depend on it."""
+    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    kept, seen, log = [], [], []
+
+    def part(state):
+        return {"state": state, "mstate": state.mstate, "world_state": state.world_state,
+                "storage": state.environment.active_account.storage, "nothing": None}[keep]
+
+    def view(state):
+        st = state.environment.active_account.storage
+        return (state.mstate.pc, tuple(x.value for x in state.mstate.stack), state.mstate.min_gas_used,
+                len(state.world_state.constraints), tuple(sorted(st.printable_storage.items())))
+
+    def hook(state):
+        log.append(view(state))
+        p = part(state)
+        if p is not None and len(kept) < 400:
+            kept.append(p)
+            seen.append(view(state))
+    vm.register_hooks("pre", {op: [hook] for op in ("ADD", "SSTORE", "SLOAD", "JUMPI", "MSTORE")})
+    for tx in _states(24):
+        _setup_global_state_for_execution(vm, tx)
+    vm.exec()
+    if keep != "nothing":
+        assert len(kept) > 50
+    for k, obj in enumerate(kept):
+        if keep == "state":
+            assert view(obj) == seen[k]
+        elif keep == "mstate":
+            assert (obj.pc, tuple(x.value for x in obj.stack), obj.min_gas_used) == seen[k][:3]
+        elif keep == "world_state":
+            st = obj[workloads.CONTRACT].storage
+            assert (len(obj.constraints), tuple(sorted(st.printable_storage.items()))) == seen[k][3:]
+        else:
+            assert tuple(sorted(obj.printable_storage.items())) == seen[k][4]
+    ref = _log_without_keeping()
+    assert log == ref
+
+
+def _log_without_keeping():
+    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    log = []
+
+    def hook(state):
+        st = state.environment.active_account.storage
+        log.append((state.mstate.pc, tuple(x.value for x in state.mstate.stack), state.mstate.min_gas_used,
+                    len(state.world_state.constraints), tuple(sorted(st.printable_storage.items()))))
+    vm.register_hooks("pre", {op: [hook] for op in ("ADD", "SSTORE", "SLOAD", "JUMPI", "MSTORE")})
+    for tx in _states(24):
+        _setup_global_state_for_execution(vm, tx)
+    vm.exec()
+    return log
