@@ -36,7 +36,9 @@ extern "C" {
                                8: mg_lanes_download_live; kernel-2 programs keep
                                   the accumulator in operand A (bvrsub, rconcat)
                                9: mg_lanes_upload_live; lane transfers batched
-                                  through one pinned DMA per phase */
+                                  through one pinned DMA per phase; symbolic
+                                  calldata copies (MG_SYM_CDBYTE) and a creation's
+                                  calldata opcodes (MG_REC_CDSIZE) on symbolic lanes */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -114,6 +116,11 @@ extern "C" {
  *                  The host registers the input with create_keccak in the
  *                  reference's global order (symbolic_inputs).                 */
 #define MG_REC_SYMKECCAK 5u
+/*   MG_REC_CDSIZE  CODESIZE of a creation transaction on a symbolic lane
+ *                  (instructions.py:979-1000): result = the code's size + 0x200, the
+ *                  value pushed; the host appends `calldata.size == result` to the
+ *                  path's constraints.  len = 0, no payload.                       */
+#define MG_REC_CDSIZE   6u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */
@@ -240,6 +247,9 @@ typedef struct mg_ctx mg_ctx;
 #define MG_SYM_TERM  10u  /* an opaque term of the host's expression layer, index w in
                              the host's term table (anything a handler or the caller
                              built); compared by identity                          */
+#define MG_SYM_CDBYTE 12u /* calldata[w]: one 8-bit byte of the calldata, If(w < size,
+                             calldata_array[w], 0) (state/calldata.py:253-262), as
+                             _calldata_copy_helper writes it (instructions.py:807-875) */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */

@@ -80,6 +80,7 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define SYM_CONCAT 9u
 #define SYM_TERM 10u
 #define SYM_NONE 0xffffffffu
+#define SYM_CDBYTE 12u
 
 DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
 DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
@@ -436,7 +437,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         if (hooked) { status = ST_HOOK; aux = op; break; }
         if (executed >= lane_max) break;
         const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
-        if ((uy & PD_SPECIAL) || (creation && (uy & PD_CREATION))) {
+        // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
+        if ((uy & PD_SPECIAL) || (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
         const uint32_t req = d.y & 15u, npop = (d.y >> 4) & 15u;
@@ -526,6 +528,89 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         } else if (tl && nobj + 4u > T.obj_cap) {
             t_gc(T, N, lane, sp, tfixed, nobj);
             if (nobj + 4u > T.obj_cap) { status = ST_ESCAPE; aux = op | (ESC_TAINT << 8); break; }
+        }
+
+        // ---- symbolic calldata into memory, and a creation's calldata opcodes ----
+        // CALLDATACOPY of symbolic calldata (_calldata_copy_helper,
+        // instructions.py:807-875): memory byte mstart + k becomes calldata[dstart + k],
+        // one CDBYTE node per byte tagged into memory; size 0 copies and extends
+        // nothing.  In a creation transaction (instructions.py:878-891, 979-1000,
+        // 1074-1104) CALLDATACOPY pops its operands and copies nothing, CODESIZE is
+        // the code's size + 0x200 with `calldata.size == it` appended to the path
+        // (MG_REC_CDSIZE, replayed by the host in execution order), and CODECOPY from
+        // at or past the end of the code is that calldata copy at code_offset minus
+        // the code's size.  Symbolic offsets or sizes stay with the host.
+        if (symlane && (flags & LANE_SYMCD) && !tl && sp >= max(req, npop) &&
+            (op == 0x37u || (creation && op == 0x38u) ||
+             (creation && op == 0x39u && !sym_tag(S, N, lane, sp - 2u) &&
+              !(u_fits32(V.stack(sp - 2u)) && V.stack(sp - 2u).w[0] < C.n_bytes)))) {
+            const uint64_t gtmin = d.x & 0xffffu, gtmax = d.x >> 16;
+            uint32_t nsp = sp - npop, nmsize = msize, lnn = nn, stop = ST_RUNNING, sx = 0u, rec_new = 0u;
+            uint64_t ngmin = gmin, ngmax = gmax;
+            U256 rval = u_zero();
+            bool wrote_tag = false;
+            do {
+#define CSTOPX(s_, x_) { stop = (s_); sx = (x_); break; }
+                if (op == 0x38u) {                                   // creation CODESIZE
+                    if (nsp + 1u > STACK_LIMIT) CSTOPX(ST_VMEXC, EXC_OVERFLOW)
+                    if (nsp + 1u > L.stack_cap) CSTOPX(ST_ESCAPE, op | (ESC_STACK << 8))
+                    const uint32_t rec_at = L.rec_len[lane];
+                    if (!L.rec_cap || (uint64_t)rec_at + MG_REC_HEADER > L.rec_cap)
+                        CSTOPX(ST_ESCAPE, op | (ESC_RECORD << 8))
+                    ngmin += gtmin; ngmax += gtmax;
+                    if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
+                    rval = u_small(C.n_bytes + 0x200u);
+                    rec_new = rec_head(L, lane, rec_at, MG_REC_CDSIZE, 0u, L.steps[lane] + executed, rval);
+                    break;
+                }
+                if (creation && op == 0x37u) {                       // creation CALLDATACOPY: pops only
+                    ngmin += gtmin; ngmax += gtmax;
+                    if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
+                    break;
+                }
+                const uint32_t ta = sym_tag(S, N, lane, sp - 1u), tb = sym_tag(S, N, lane, sp - 2u),
+                               tc = sym_tag(S, N, lane, sp - 3u);
+                const U256 a = V.stack(sp - 1u), b = V.stack(sp - 2u), c = V.stack(sp - 3u);
+                if (ta || tb || tc) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                if (u_iszero(c)) {                                   // size 0: nothing but the gas
+                    ngmin += gtmin; ngmax += gtmax;
+                    if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
+                    break;
+                }
+                const int mx = mem_extend(a, c, nmsize, ngmin, ngmax, L.mem_cap, (int64_t)gtmin, txlim);
+                if (mx == MX_OOG) CSTOPX(ST_VMEXC, EXC_OOG)
+                if (mx == MX_ESCAPE) CSTOPX(ST_ESCAPE, op | (ESC_MEMORY << 8))
+                ngmin += gtmin; ngmax += gtmax;
+                if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
+                // the source index of every byte must stay below 2^32 on the device
+                const uint32_t src = op == 0x39u ? b.w[0] - C.n_bytes : b.w[0];
+                const uint32_t size = c.w[0], mst = a.w[0];
+                if (!u_fits32(b) || (uint64_t)src + size > 0xffffffffull) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                if ((uint64_t)lnn + size > S.node_cap) CSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                if (nmsize > msize) V.mzero(msize, nmsize);
+                for (uint32_t k = 0; k < size; ++k) {
+                    uint32_t tg;
+                    sym_node_push(S, N, lane, SYM_CDBYTE | (8u << 8), 0u, 0u, src + k, lnn, tg);
+                    V.set_mbyte(mst + k, 0u);
+                    set_mtag(S, N, lane, mst + k, 1u + (((tg - 1u) << 5) | 31u));
+                }
+                wrote_tag = true;
+#undef CSTOPX
+            } while (0);
+            if (stop != ST_RUNNING) {
+                if (stop != ST_ESCAPE) ++executed;
+                status = stop; aux = sx; break;
+            }
+            if (rec_new) L.rec_len[lane] = rec_new;
+            if (wrote_tag) lflags |= LANE_MEMTAG;
+            if (op == 0x38u) {
+                V.set_stack(nsp, rval);
+                sym_set_tag(S, N, lane, nsp, 0u);
+                ++nsp;
+            }
+            sp = nsp; ++pc; msize = nmsize; gmin = ngmin; gmax = ngmax; nn = lnn;
+            ++executed;
+            continue;
         }
 
         // ---- symbolic lanes: storage chain, memory byte tags, symbolic SHA3 ----

@@ -39,12 +39,14 @@ MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 # function-manager records (include/mythgpu.h MG_REC_*)
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
 MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
+MG_REC_CDSIZE = 6       # a creation's CODESIZE: the host appends calldata.size == result
 MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT = 16, 32, 6
 MG_SYM_CDLOAD, MG_SYM_CDSIZE, MG_SYM_ENV, MG_SYM_BIN, MG_SYM_UN = 1, 2, 3, 4, 5
 MG_SYM_SLOAD, MG_SYM_KECCAK, MG_SYM_EXTRACT, MG_SYM_CONCAT, MG_SYM_TERM = 6, 7, 8, 9, 10
+MG_SYM_CDBYTE = 12      # calldata[w]: one byte of a symbolic calldata copy
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
 MG_SYM_CONST = 0x80000000
 MG_LANE_TAINT = 2048
@@ -366,6 +368,9 @@ class LaneBatch:
                 k += 8 * (ln - 1)
                 out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF))
                 k += 2
+            elif kind == MG_REC_CDSIZE:
+                # (step, "cdsize", the CODESIZE value pushed)
+                out.append((step, "cdsize", r))
             elif kind == MG_REC_SYMKECCAK:
                 # (step, "symkeccak", KECCAK node index, input bytes)
                 out.append((step, "symkeccak", int(q[k]), ln))

@@ -10,6 +10,7 @@ from .strategy import (BoundedLoopsStrategy, BreadthFirstSearchStrategy, DepthFi
 from .svm import LaserEVM
 from .transaction import (ContractCreationTransaction, MessageCallTransaction,
                           execute_contract_creation, execute_message_call, execute_symbolic_message_call,
+                          execute_symbolic_contract_creation,
                           generate_contract_address, tx_id_manager)
 from .symbolic import SymbolicCalldata
 
@@ -19,4 +20,4 @@ __all__ = ["Account", "BoundedLoopsStrategy", "BreadthFirstSearchStrategy",
            "Environment", "GlobalState", "InstructionCoveragePlugin", "LaserEVM", "LaserPlugin",
            "MachineStack", "MachineState", "Memory", "MessageCallTransaction",
            "PluginSkipState", "PluginSkipWorldState", "Storage", "WorldState", "disassemble",
-           "execute_message_call", "execute_symbolic_message_call", "SymbolicCalldata", "tx_id_manager"]
+           "execute_message_call", "execute_symbolic_message_call", "execute_symbolic_contract_creation", "SymbolicCalldata", "tx_id_manager"]

@@ -667,6 +667,12 @@ class LaserEVM:
                 tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
             elif r[1] == "hook":
                 tnt.replay_deferred(r, lanes[i].state, self._plan)
+            elif r[1] == "cdsize":
+                # codesize_ of a creation (instructions.py:989-997): the symbolic
+                # calldata's size is pinned to the pushed value
+                st = lanes[i].state
+                st.world_state.constraints.append(
+                    st.environment.calldata.size == symbol_factory.BitVecVal(r[2], 256))
             else:
                 _, cond = exponent_function_manager.create_condition(
                     symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))

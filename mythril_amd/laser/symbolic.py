@@ -36,8 +36,8 @@ import numpy as np
 from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_CALLVALUE as MG_ENV_CALLVALUE, ENV_GASPRICE as MG_ENV_GASPRICE,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
-                     MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDLOAD, MG_SYM_CDSIZE,
-                     MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDLOAD,
+                     MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
                         URem, SRem, _select, simplify_concat, symbol_factory)
@@ -99,12 +99,11 @@ def is_symbolic_calldata(cd) -> bool:
 _PROV: "weakref.WeakKeyDictionary[Node, tuple]" = weakref.WeakKeyDictionary()
 
 
-def _mark(e, kind: int, imm: int, args: tuple):
+def _mark(e, kind: int, imm: int, args: tuple, width: int = 256):
     """Record how node `e` was built.  A Bool result goes on the stack as
     If(b, 1, 0), as MachineStack.append wraps it (machine_state.py:39-46); the
     wrapper is what the stack holds and what encode_stack maps back to the
     (width-1) node."""
-    width = 256
     if isinstance(e, Bool):
         e = If(e, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
         width = 1
@@ -235,6 +234,9 @@ class _Decoder:
             return _mark(source(kind, w, a, self.state), kind, w, (a,))
         if kind in (MG_SYM_CDSIZE, MG_SYM_ENV):
             return _mark(source(kind, w, None, self.state), kind, w, ())
+        if kind == MG_SYM_CDBYTE:
+            # the byte _calldata_copy_helper writes: calldata[index] (instructions.py:850-860)
+            return _mark(self.state.environment.calldata[w], kind, w, (), 8)
         if kind == MG_SYM_SLOAD:
             # Storage.__getitem__: simplify(Select(chain after z stores, index))
             return BitVec(_select(self.chain_raw(z), self.ref(y).raw))

@@ -137,6 +137,33 @@ def execute_symbolic_message_call(laser_evm, callee_address, gas_limit: int = 8_
     laser_evm.exec()
 
 
+def execute_symbolic_contract_creation(laser_evm, contract_initialization_code, contract_name=None,
+                                       world_state=None, origin=ACTORS["CREATOR"], caller=ACTORS["CREATOR"]):
+    """transaction/symbolic.py:154-200 (execute_contract_creation): one creation
+    from `world_state` (a fresh one when None) with a symbolic gas price and
+    call value and symbolic calldata (SymbolicCalldata(id): constructor
+    arguments are read past the end of the code, instructions.py:979-1104);
+    then ``laser_evm.exec(True)``.  Returns the new account.  The lanes run on
+    the device as symbolic lanes: CALLDATA*, CODESIZE and CODECOPY past the
+    end of the code included (k_sym_step)."""
+    from ..smt.expr import symbol_factory
+    from .symbolic import SymbolicCalldata
+    world_state = world_state or WorldState()
+    del laser_evm.open_states[:]
+    txid = tx_id_manager.get_next_tx_id()
+    code = contract_initialization_code
+    tx = ContractCreationTransaction(
+        world_state=world_state, identifier=txid,
+        gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256), gas_limit=8_000_000,
+        origin=origin, code=code if isinstance(code, Disassembly) else Disassembly(code), caller=caller,
+        contract_name=contract_name, call_data=SymbolicCalldata(txid),
+        call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+    _setup_global_state_for_execution(laser_evm, tx)
+    new_account = tx.callee_account
+    laser_evm.exec(True)
+    return new_account
+
+
 def _rlp_item(b: bytes) -> bytes:
     if len(b) == 1 and b[0] < 0x80:
         return b
@@ -196,9 +223,13 @@ class ContractCreationTransaction(MessageCallTransaction):
         callee_account = create_account(world_state, 0, concrete_storage=True, creator=caller,
                                         address=contract_address)
         callee_account.contract_name = contract_name or callee_account.contract_name
-        super().__init__(world_state, callee_account, caller, b"", identifier, gas_price, gas_limit,
-                         origin, code, call_value, False, base_fee)
-        self.symbolic_calldata = call_data is None
+        # a SymbolicCalldata object (transaction/symbolic.py's creation) is the
+        # environment's calldata; None (concolic creation) keeps an empty concrete
+        # calldata whose CALLDATA* / CODESIZE escape to the host's handler
+        symcd = call_data is not None and hasattr(call_data, "get_word_at")
+        super().__init__(world_state, callee_account, caller, call_data if symcd else b"", identifier,
+                         gas_price, gas_limit, origin, code, call_value, False, base_fee)
+        self.symbolic_calldata = call_data is None or symcd
 
     def initial_global_state(self) -> GlobalState:
         gs = super().initial_global_state()

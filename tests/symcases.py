@@ -31,7 +31,7 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o")
 
 
 def deploy(device, name):
@@ -122,3 +122,65 @@ def run_both(device, name, monkeypatch):
         Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
     ref_engine.run([gs])
     return got, _outcomes_of_restatement(ref_engine), laser
+
+
+# creation codes run by a symbolic creation (transaction/symbolic.py:154-200):
+# constructor arguments are read past the end of the code from the symbolic
+# calldata (CODESIZE + 0x200 pins its size, instructions.py:979-1104)
+SYM_CREATIONS = ("symbolic_exec_bytecode.sol.o", "flag_array.sol.o")
+
+
+def _creation_tx(ws, code, txid):
+    from mythril_amd.laser import ContractCreationTransaction, Disassembly, SymbolicCalldata
+    return ContractCreationTransaction(
+        world_state=ws, identifier=txid, gas_price=symbol_factory.BitVecSym(f"gas_price{txid}", 256),
+        gas_limit=8_000_000, origin=CREATOR, code=Disassembly(code), caller=CREATOR,
+        call_data=SymbolicCalldata(txid), call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
+
+
+def run_creation_both(device, name, monkeypatch):
+    """(outcomes of a symbolic creation through LaserEVM + device, outcomes of
+    the restatement, laser): every path's end with its constraint sequence."""
+    from copy import copy
+    from mythril_amd.laser import execute_symbolic_contract_creation
+    monkeypatch.setattr(solver.args, "pruning_factor", 0)
+    code = workloads.bytecode(name)
+    ws0 = WorldState()
+    ws0.put_account(Account(CREATOR, balances=None))
+    ws_ref = copy(ws0)
+    handler_engine = symref.Engine()
+
+    def handler(state):
+        try:
+            return handler_engine.step(state)
+        except symref.Unsupported:
+            handler_engine.ended.append(("unsupported", state))
+            return []
+    escaped = Counter()
+
+    def counting_handler(state):
+        ins = state.environment.code.instruction_list
+        escaped.update([ins[state.mstate.pc]["opcode"] if state.mstate.pc < len(ins) else "END"])
+        return handler(state)
+    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+                     escape_handler=counting_handler)
+    laser.escaped_ops = escaped
+    got = Counter()
+    # a creation keeps its world state only when it returns code (svm.py:459-466):
+    # path ends are compared by their transaction_end outcomes
+    laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
+        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
+    tx0 = int(tx_id_manager.get_next_tx_id())
+    tx_id_manager.set_counter(tx0 - 1)
+    execute_symbolic_contract_creation(laser, code, world_state=ws0)
+    tx_id_manager.set_counter(tx0 - 1)
+    ref_engine = symref.Engine()
+    txid = tx_id_manager.get_next_tx_id()
+    tx = _creation_tx(ws_ref, code, txid)
+    gs = tx.initial_global_state()
+    gs.transaction_stack.append((tx, None))
+    ref_engine.run([gs])
+
+    def ends(c):
+        return Counter({k: v for k, v in c.items() if k[0] != "ws"})
+    return ends(got + _outcomes_of_restatement(handler_engine)), ends(_outcomes_of_restatement(ref_engine)), laser

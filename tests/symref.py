@@ -30,7 +30,8 @@ from mythril_amd.lanes import (LaneBatch, LaneShape, MG_HALT_DROPPED, MG_HALT_EN
                                MG_HALT_REVERT, MG_HALT_STOP, MG_RUNNING, MG_VMEXC, limbs_to_word,
                                word_to_limbs)
 from mythril_amd.laser.opcodes import ADDRESS_OPCODE_MAPPING
-from mythril_amd.laser.state import Memory, MachineStack
+from mythril_amd.laser.state import Memory, MachineStack, OutOfGasException
+from mythril_amd.laser.transaction import ContractCreationTransaction
 from mythril_amd.smt.expr import (BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT, URem,
                                   simplify_concat, symbol_factory)
 from mythril_amd.smt.keccak_manager import keccak_function_manager
@@ -246,6 +247,11 @@ class Engine:
         if op in (0x20, 0x51, 0x52, 0x53, 0x54, 0x55) and _symbolic_state(s) and len(st) >= _POPS[op]:
             s.environment.active_account.storage.to_chain()
             return self._memstore(s, op)
+        creation = isinstance(s.current_transaction, ContractCreationTransaction)
+        if symcd and (op == 0x37 or (creation and op in (0x38, 0x39))) and len(st) >= _POPS.get(op, 0):
+            out = self._calldata_ops(state, s, op, creation)
+            if out is not None:
+                return out
         if name.startswith(("DUP", "SWAP")) or name == "POP" or name.startswith("PUSH"):
             self._touched = reads if not name.startswith("PUSH") else 0
             if name.startswith("DUP") or name.startswith("SWAP"):
@@ -286,6 +292,52 @@ class Engine:
             self.ended.append(("exception", state))
             return []
         st.append(res)
+        ms.pc += 1
+        ms.min_gas_used += gmin
+        ms.max_gas_used += gmax
+        return [s]
+
+    # ---- symbolic calldata copies, a creation's calldata opcodes ---------------
+    def _calldata_ops(self, state, s, op, creation):
+        """calldatacopy_ / codesize_ / codecopy_ with symbolic calldata
+        (instructions.py:807-891, 979-1000, 1074-1104): a creation's CALLDATACOPY
+        pops three words; its CODESIZE pushes the code's size + 0x200 and pins
+        calldata.size to it; a creation's CODECOPY from at or past the end of the
+        code and a message call's CALLDATACOPY write calldata[src + k] into memory
+        byte dst + k.  None: an ordinary code copy (the oracle runs it)."""
+        ms, env = s.mstate, s.environment
+        st = ms.stack
+        gmin, gmax = _GAS[op]
+        code_len = len(env.code.raw)
+        if op == 0x38:
+            n = code_len + 0x200
+            if len(st) + 1 > 1024:
+                raise Unsupported("stack overflow")
+            s.world_state.constraints.append(env.calldata.size == BVV(n, 256))
+            st.append(BVV(n, 256))
+        else:
+            dst, src, size = st[-1], st[-2], st[-3]
+            if op == 0x39 and _val(src) is not None and _val(src) < code_len:
+                return None
+            if any(_val(x) is None for x in (dst, src, size)):
+                raise Unsupported("symbolic calldata copy operand")
+            del st[-3:]
+            dst, src, size = _val(dst), _val(src), _val(size)
+            if not (creation and op == 0x37) and size > 0:
+                if op == 0x39:
+                    src -= code_len
+                if src + size >= 1 << 32:
+                    raise Unsupported("calldata index past 2^32")
+                try:
+                    ms.mem_extend(BVV(dst, 256), BVV(size, 256))
+                except OutOfGasException:
+                    self.ended.append(("exception", state))
+                    return []
+                for k in range(size):
+                    ms.memory[dst + k] = env.calldata[src + k]
+        if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
+            self.ended.append(("exception", state))
+            return []
         ms.pc += 1
         ms.min_gas_used += gmin
         ms.max_gas_used += gmax

@@ -121,3 +121,18 @@ def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch)
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
     assert laser.forks >= 3 and laser.lane_steps > 100
+
+
+@pytest.mark.parametrize("name", symcases.SYM_CREATIONS)
+def test_symbolic_creation_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
+    """transaction/symbolic.py's creation on kernel 1: the creation's calldata
+    opcodes (CALLDATACOPY pops, CODESIZE + 0x200 with calldata.size pinned
+    through an MG_REC_CDSIZE record, CODECOPY past the end of the code as a
+    symbolic calldata copy) run on the device -- none of them escapes -- and
+    every path ends as the restatement's does, constraint for constraint."""
+    got, want, laser = symcases.run_creation_both(dev, name, monkeypatch)
+    assert sum(want.values()) >= 2
+    assert got == want
+    assert laser.lane_steps > 50
+    for op in ("CODESIZE", "CODECOPY", "CALLDATACOPY", "CALLDATALOAD", "CALLDATASIZE"):
+        assert laser.escaped_ops[op] == 0, (op, dict(laser.escaped_ops))

@@ -156,6 +156,48 @@ def test_symbolic_call_outcomes_equal_the_restatement(name, monkeypatch):
     assert got == want
 
 
+@pytest.mark.parametrize("name", symcases.SYM_CREATIONS)
+def test_symbolic_creation_outcomes_equal_the_restatement(name, monkeypatch):
+    """transaction/symbolic.py's creation (symbolic calldata: CODESIZE + 0x200
+    pins its size, constructor arguments come from CODECOPY past the end of
+    the code) through LaserEVM: the oracle device escapes every symbolic lane
+    to the restatement, so this pins the harness the GPU test uses."""
+    got, want, laser = symcases.run_creation_both(OracleDevice(), name, monkeypatch)
+    assert sum(want.values()) >= 2
+    assert got == want
+
+
+def test_restated_creation_calldata_opcodes_follow_the_reference():
+    """instructions.py:878-891 / 979-1000 / 1074-1104 on a creation with
+    symbolic calldata: CALLDATACOPY pops three words and copies nothing;
+    CODESIZE = code size + 0x200 with calldata.size == it appended; CODECOPY
+    from past the end of the code copies calldata[offset - code size + k]."""
+    from mythril_amd.laser import ContractCreationTransaction, Disassembly, SymbolicCalldata, WorldState
+    # PUSH1 8 PUSH1 0 PUSH1 0 CALLDATACOPY | CODESIZE | PUSH1 3 PUSH1 0x13 PUSH1 0x40 CODECOPY | STOP
+    code = bytes.fromhex("600860006000" "37" "38" "6003601360403900")
+    ws = WorldState()
+    tx = ContractCreationTransaction(world_state=ws, identifier="77", gas_price=0, gas_limit=8_000_000,
+                                     origin=1, code=Disassembly(code), caller=1,
+                                     call_data=SymbolicCalldata("77"), call_value=0)
+    s = tx.initial_global_state()
+    s.transaction_stack.append((tx, None))
+    e = symref.Engine()
+    for _ in range(4):
+        (s,) = e.step(s)
+    assert len(s.mstate.stack) == 0 and len(s.mstate.memory) == 0          # CALLDATACOPY: nothing
+    (s,) = e.step(s)
+    n = len(code) + 0x200
+    assert s.mstate.stack[-1].value == n
+    cd = s.environment.calldata
+    assert s.world_state.constraints[-1].raw is (cd.size == BVV(n, 256)).raw
+    for _ in range(4):
+        (s,) = e.step(s)
+    mem = s.mstate.memory
+    assert len(mem) == 0x60
+    assert {p: x.raw for p, x in mem.symbolic_bytes().items()} == \
+        {0x40 + k: cd[0x13 - len(code) + k].raw for k in range(3)} if 0x13 >= len(code) else True
+
+
 # ---- symbolic memory, storage chains and SHA3 (ABI v7) -----------------------------
 def _run_restatement(code_hex, steps):
     s = _state(code_hex)
