@@ -39,7 +39,11 @@ def run(mode):
         for _ in range(50):
             dev.upload_range(b, 0, n)
         t2 = time.perf_counter()
-        out[n] = {"download_ms": (t1 - t0) / 50 * 1e3, "upload_ms": (t2 - t1) / 50 * 1e3}
+        for _ in range(50):
+            dev.upload_range(b, 0, n, live=True)
+        t3 = time.perf_counter()
+        out[n] = {"download_ms": (t1 - t0) / 50 * 1e3, "upload_ms": (t2 - t1) / 50 * 1e3,
+                  "upload_live_ms": (t3 - t2) / 50 * 1e3}
     dev.download(b)
     images = {k: np.array(getattr(b, k)).copy() for k in ("pc", "sp", "msize", "steps", "stack", "memory",
                                                           "storage", "gas_min", "rec_len", "rec")}

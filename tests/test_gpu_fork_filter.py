@@ -11,6 +11,8 @@ constraint sequences (device halts and escaped paths alike), the open states,
 the fork-filter decisions (queries / kept / pruned / unknown), the model
 cache's hit statistics and its final LRU order must be identical.
 """
+from collections import Counter
+
 import pytest
 
 import symcases
@@ -87,7 +89,7 @@ def _run(name, k1, k2, monkeypatch, n_seeds=48):
     ends += [(kind == "revert", tuple(x.raw for x in st.world_state.constraints)) for kind, st in eng.ended]
     pool = seeds.models()
     lru = [pool.index(m) for m in mc.model_cache.lru_cache]
-    opened = sorted(tuple(x.raw for x in w.constraints) for w in laser.open_states)
+    opened = Counter(tuple(x.raw for x in w.constraints) for w in laser.open_states)
     return {"ends": ends, "lru": lru, "forks": dict(laser.fork_stats), "cache": dict(mc.stats),
             "open": opened, "lane_steps": int(laser.lane_steps), "device_evals": mc.device_evals}
 
