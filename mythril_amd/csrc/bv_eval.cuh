@@ -318,11 +318,14 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     // thread index = the wave's first (an SGPR) + the lane id (v_mbcnt): nothing
     // keeps threadIdx.x alive across the loops
     const uint32_t wave0 = uni(threadIdx.x) & ~63u;
-    for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-    BvCtx c{values, consts, slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
-
+    // DAG-major: one DAG's program (tens of instructions) is evaluated for all of
+    // the block's model chunks while it is hot in the scalar cache; chunk-major
+    // re-read the whole tile (up to 32 KiB) once per chunk, which the scalar
+    // cache cannot hold and a CU's resident blocks' tiles overflow L2 with
     for (uint32_t d = d0; d < d1; ++d) {
-        const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
+    const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
+    for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
+        BvCtx c{values, consts, slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
         U256 acc = u_zero();
         for (uint32_t p = p0; p < p1; ++p) {
             // c.m is the only per-lane context: hide its loop invariance so the

@@ -34,6 +34,7 @@ from mythril_amd.laser.state import Memory, MachineStack, OutOfGasException
 from mythril_amd.laser.transaction import ContractCreationTransaction
 from mythril_amd.smt.expr import (BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT, URem,
                                   simplify_concat, symbol_factory)
+from mythril_amd.smt.exponent_manager import exponent_function_manager
 from mythril_amd.smt.keccak_manager import keccak_function_manager
 from oracle.evm_ref import OracleEVM
 
@@ -144,6 +145,8 @@ class Engine:
 
     def _oracle_step(self, s):
         env, ms = s.environment, s.mstate
+        ins = env.code.instruction_list
+        op_name = ins[ms.pc]["opcode"] if ms.pc < len(ins) else None
         b = self._oracle_run(s)
         if int(b.status[0]) != MG_RUNNING:
             return self._ended(s, b)
@@ -174,6 +177,11 @@ class Engine:
         n.mstate.pc = int(b.pc[0])
         n.mstate.depth = int(b.depth[0])
         n.mstate.min_gas_used, n.mstate.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])
+        if op_name == "EXP":
+            # exp_ appends exponent_function_manager's condition for every EXP,
+            # concrete operands included (instructions.py:624-638)
+            _, cond = exponent_function_manager.create_condition(_pop_bitvec(old[-1]), _pop_bitvec(old[-2]))
+            n.world_state.constraints.append(cond)
         st = env.active_account.storage
         if not st.is_chain:
             st.set_slots({limbs_to_word(b.storage[0, k, :8]): limbs_to_word(b.storage[0, k, 8:])

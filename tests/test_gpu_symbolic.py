@@ -132,7 +132,8 @@ def test_symbolic_creation_on_kernel1_equals_the_restatement(dev, name, monkeypa
     every path ends as the restatement's does, constraint for constraint."""
     got, want, laser = symcases.run_creation_both(dev, name, monkeypatch)
     assert sum(want.values()) >= 2
-    assert got == want
+    assert got == want, ([(k[:2], [str(c) for c in k[2]], v) for k, v in (got - want).items()],
+                         [(k[:2], [str(c) for c in k[2]], v) for k, v in (want - got).items()])
     assert laser.lane_steps > 50
     for op in ("CODESIZE", "CODECOPY", "CALLDATACOPY", "CALLDATALOAD", "CALLDATASIZE"):
         assert laser.escaped_ops[op] == 0, (op, dict(laser.escaped_ops))
