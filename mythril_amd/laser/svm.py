@@ -1306,7 +1306,13 @@ class _Schedule:
     def __init__(self, lanes: List[_Lane], b: LaneBatch, bfs: bool):
         self.lanes, self.b, self.bfs = lanes, b, bfs
         self._ev: List = []
-        self._pz: List = []
+        self._pz: List = []           # DFS: (-pos,) heap of paused lanes, lazy deletion
+        # BFS: only the smallest paused round is ever asked for, so paused lanes
+        # are counted per round (steps + acked) with a heap of the rounds: a
+        # launch of thousands of lanes costs one count per lane, not one heap entry
+        self._pround: Dict[int, int] = {}      # paused pos -> its round
+        self._pcount: Dict[int, int] = {}      # round -> paused lanes
+        self._prounds: List[int] = []          # heap of rounds (lazy: zero counts popped)
         self.paused: set = set()
         self.acked: set = set()       # paused at a deferred hooked instruction (_ack_safe)
         self.dirty: set = set()
@@ -1315,12 +1321,22 @@ class _Schedule:
         r = _event_round(self.b, pos)
         return (r, pos) if self.bfs else (-pos, r)
 
-    def _pkey(self, pos: int):
-        # a deferred hooked instruction has no event before the next round
-        return (int(self.b.steps[pos]) + (pos in self.acked), pos) if self.bfs else (-pos,)
+    def _punpause(self, pos: int) -> None:
+        r = self._pround.pop(pos, None)
+        if r is not None:
+            self._pcount[r] -= 1
+
+    def _ppause(self, pos: int, r: int) -> None:
+        self._pround[pos] = r
+        c = self._pcount.get(r, 0)
+        if not c:
+            heapq.heappush(self._prounds, r)
+        self._pcount[r] = c + 1
 
     def set(self, pos: int, phase: str, acked: bool = False) -> None:
         self.lanes[pos].phase = phase
+        if self.bfs:
+            self._punpause(pos)
         self.paused.discard(pos)
         self.acked.discard(pos)
         if phase == "event":
@@ -1329,7 +1345,11 @@ class _Schedule:
             self.paused.add(pos)
             if acked:
                 self.acked.add(pos)
-            heapq.heappush(self._pz, (self._pkey(pos), pos))
+            if self.bfs:
+                # a deferred hooked instruction has no event before the next round
+                self._ppause(pos, int(self.b.steps[pos]) + (1 if acked else 0))
+            else:
+                heapq.heappush(self._pz, ((-pos,), pos))
 
     def set_after_launch(self, run: List[int]) -> None:
         """set(i, "paused" | "event") for every lane of a launch, from one vector
@@ -1339,13 +1359,20 @@ class _Schedule:
         steps = self.b.steps[idx].tolist()
         lanes, paused, acked, bfs = self.lanes, self.paused, self.acked, self.bfs
         ev, pz, push = self._ev, self._pz, heapq.heappush
+        if bfs:
+            for i in run:
+                self._punpause(i)
+        acked.difference_update(run)
         for i, s_, k_ in zip(run, st, steps):
-            lanes[i].phase = "paused" if s_ == MG_RUNNING else "event"
-            acked.discard(i)
             if s_ == MG_RUNNING:
+                lanes[i].phase = "paused"
                 paused.add(i)
-                push(pz, ((k_, i) if bfs else (-i,), i))
+                if bfs:
+                    self._ppause(i, k_)
+                else:
+                    push(pz, ((-i,), i))
             else:
+                lanes[i].phase = "event"
                 paused.discard(i)
                 r = k_ - 1 if s_ in _EXECUTED_HALTS else k_
                 push(ev, ((r, i) if bfs else (-i, r), i))
@@ -1363,10 +1390,18 @@ class _Schedule:
         return None
 
     def paused_first(self):
-        """Key of the first paused lane: (steps, pos) under BFS, (-pos,) under DFS."""
+        """Key of the first paused lane: (round,) under BFS (its cumulative steps,
+        + 1 at a deferred hooked instruction), (-pos,) under DFS."""
+        if self.bfs:
+            h, cnt = self._prounds, self._pcount
+            while h:
+                if cnt.get(h[0]):
+                    return (h[0],)
+                heapq.heappop(h)
+            return None
         while self._pz:
             key, pos = self._pz[0]
-            if pos in self.paused and key == self._pkey(pos):
+            if pos in self.paused and key == (-pos,):
                 return key
             heapq.heappop(self._pz)
         return None
