@@ -23,7 +23,7 @@ def child():
     prog, models = synth.c4_batch(1_000_000, 4096)
     dev = GpuDevice(0)
     out = {}
-    for mode in ("lds", "scalar"):
+    for mode in os.environ.get("AB_K2_MODES", "lds,scalar").split(","):
         os.environ["MG_BV_PROG"] = mode
         dev.eval_upload(prog, models)
         dev.eval_run()

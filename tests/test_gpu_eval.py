@@ -94,10 +94,12 @@ def ULT_x():
     return ULT(symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecVal(3, 256))
 
 
-@pytest.mark.parametrize("fetch", ["lds", "scalar"])
+@pytest.mark.parametrize("fetch", ["lds", "scalar", "pair"])
 def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
     """The scalar-load fetch is the default; MG_BV_PROG=lds stages the program tile
-    in LDS.  Both read at upload, both equal the oracle (plain ops and tables)."""
+    in LDS, MG_BV_PROG=pair evaluates two models per thread (k_bv_eval_pair).
+    All read at upload, all equal the oracle (plain ops and tables; 333 and 300
+    models: a partial second model half in pair mode)."""
     from test_smt_programs import _random_table_constraints, _random_table_models
     monkeypatch.setenv("MG_BV_PROG", fetch)
     prog = synth.c4_programs(synth.Draws(900, seed=synth.C4_SEED + 9))
@@ -114,14 +116,16 @@ def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
     assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
 
 
+@pytest.mark.parametrize("mode", ["scalar", "pair"])
 @pytest.mark.parametrize("w", [8, 64, 255, 256])
-def test_division_class_ops_at_every_width(dev, w):
+def test_division_class_ops_at_every_width(dev, w, mode, monkeypatch):
     """UDIV UREM SDIV SREM SMOD and the unsigned multiply-overflow test share one
     division site in the kernel (bv_divop): each op at width w, against values
     at the sign / zero / all-ones edges (z3 zero-divisor semantics)."""
     from mythril_amd.smt.expr import (BVMulNoOverflow, SDiv, SMod, SRem, UDiv, URem,
                                       symbol_factory)
     BVS = symbol_factory.BitVecSym
+    monkeypatch.setenv("MG_BV_PROG", mode)
     x, y, z = BVS("x", w), BVS("y", w), BVS("z", w)
     sets = []
     for f in (UDiv, URem, SDiv, SRem, SMod):
@@ -148,3 +152,18 @@ def test_division_class_ops_at_every_width(dev, w):
     rfs, rsc = eval_batch(prog, pool)
     assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
     assert (sc[:10] > 0).all()
+
+
+def test_pair_mode_bitmaps_equal_single_mode(dev, monkeypatch):
+    """mg_eval_bits in pair mode: per-model bitmaps (the LRU replay input) equal
+    the single-model kernel's, with a model count that leaves the second half
+    of the last pair partly empty."""
+    prog = synth.c4_programs(synth.Draws(700, seed=synth.C4_SEED + 13))
+    models = synth.c4_models(1100, seed=23)
+    out = {}
+    for mode in ("scalar", "pair"):
+        monkeypatch.setenv("MG_BV_PROG", mode)
+        out[mode] = dev.eval_bits(prog, models)
+    for k in range(3):
+        assert np.array_equal(out["scalar"][k], out["pair"][k])
+    assert int(out["pair"][1].sum()) > 0
