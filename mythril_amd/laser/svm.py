@@ -103,6 +103,8 @@ class _Lane:
 class LaserEVM:
     """The LASER engine with kernel 1 stepping every path of the work list."""
 
+    _fast_hooks = True      # plain lanes' pre-hook events take _deliver_plain_hook
+
     def __init__(self, dynamic_loader=None, max_depth=float("inf"), execution_timeout=60,
                  create_timeout=10, strategy=DepthFirstSearchStrategy, transaction_count=2,
                  requires_statespace=True, iprof=None, use_reachability_check=True,
@@ -797,6 +799,65 @@ class LaserEVM:
             self.work_list.extend(ln.state for ln, _ in regrow)
         return None
 
+    def _deliver_plain_hook(self, ln: _Lane, b: LaneBatch, i: int, s: GlobalState, name: str, final_states,
+                            track_gas, launch, regrow) -> None:
+        """The MG_HOOK branch of _deliver for a plain concrete lane (its stack a
+        LazyStack: no taint, symbolic or trace planes) with only pre hooks: the
+        same steps (precheck, svm pre hooks, instruction pre hooks, copy if a hook
+        kept the state, resume or repack, host halt, deferred launch), with the
+        "hooks left the lane image alone" test reduced to the objects
+        _materialise just made and the scalars it set."""
+        ms, env = s.mstate, s.environment
+        acct = env.active_account
+        stack, mem, storage = ms.stack, ms.memory, acct.storage
+        mver, sver = mem._ver, storage._ver
+        scal = (ms.pc, ms.depth, ms.min_gas_used, ms.max_gas_used)
+        ids = (id(env), id(acct), id(env.code), id(env.calldata), id(env.address), id(env.sender),
+               id(env.origin), id(env.callvalue), id(env.gasprice), id(s.current_transaction), env.static)
+        refs0 = _held(s)
+        if len(stack) < get_required_stack_elements(name):
+            # svm.py:391-402: precheck underflow -- no pre hooks, no tx-end hooks
+            if track_gas:
+                final_states.append(s)
+            return
+        try:
+            self._execute_pre_hook(name, s)
+        except PluginSkipState:
+            if track_gas:
+                final_states.append(s)
+            return
+        for hook in self.instr_pre_hook.get(name, ()):
+            hook(s)
+        pre_state = s
+        if _held(s) != refs0:
+            s = copy(s)                    # a hook kept the state: the lane goes on with a copy
+            ln.state = s
+        pm, pe = pre_state.mstate, pre_state.environment
+        steps = int(b.steps[i])
+        if (pm is ms and pm.stack is stack and not stack.mut and pm.memory is mem and mem._ver == mver
+                and pe.active_account is acct and acct.storage is storage and storage._ver == sver
+                and (pm.pc, pm.depth, pm.min_gas_used, pm.max_gas_used) == scal
+                and (id(pe), id(pe.active_account), id(pe.code), id(pe.calldata), id(pe.address),
+                     id(pe.sender), id(pe.origin), id(pe.callvalue), id(pe.gasprice),
+                     id(pre_state.current_transaction), pe.static) == ids):
+            _rearm(b, i)                   # the lane image is still the state's: only resume it
+        else:
+            self._pack(b, i, s)
+            b.steps[i] = steps
+        b.flags[i] |= MG_LANE_HOOK_ACK
+        if self._halts_on_host(name, s, b, i):
+            b.flags[i] = int(b.flags[i]) & ~MG_LANE_HOOK_ACK
+            b.steps[i] = steps + 1
+            self.lane_steps += 1
+            self.total_states += 1
+            self._sched.set(i, "event")
+            self._deliver(ln, b, final_states, track_gas, launch, regrow, False)
+            return
+        sched = self._sched
+        safe = sched.bfs and self._ack_safe(name, s, b)
+        sched.set(i, "paused", acked=safe)
+        sched.mark_dirty(i)
+
     def _regrow_in_place(self, b: LaneBatch, regrow, lanes) -> Optional[LaneBatch]:
         """A lane stopped by a full per-lane table (capacity escape): grow that
         capacity 4x for the whole batch, copy every lane into the new image
@@ -865,6 +926,11 @@ class LaserEVM:
 
         if status in _EXECUTED_HALTS:
             self.total_states -= 1                  # the halting step had no successor
+        if status == MG_HOOK and self._fast_hooks and type(s.mstate.stack) is LazyStack \
+                and not self._execute_state_hooks \
+                and not single_step and not self._has_post(name):
+            self._deliver_plain_hook(ln, b, i, s, name, final_states, track_gas, launch, regrow)
+            return
         if status == MG_HOOK:
             # plain concrete lanes: a state the hooks leave untouched needs no repack
             sig0 = _hook_sig(s) if not (b.taint or b.symbolic or b.shape.trace_cap) else None

@@ -196,3 +196,51 @@ def _log_without_keeping():
         _setup_global_state_for_execution(vm, tx)
     vm.exec()
     return log
+
+
+@pytest.mark.parametrize("strategy", [BreadthFirstSearchStrategy, DepthFirstSearchStrategy])
+def test_plain_hook_fast_path_equals_the_general_path(strategy, monkeypatch):
+    """LaserEVM._deliver_plain_hook (plain lanes, pre hooks only) against the
+    general MG_HOOK branch, with hooks that leave the state alone, rewrite a
+    stack word, write memory, write storage, and keep the state: the same event
+    log, open states and lane-steps."""
+    def run(fast):
+        monkeypatch.setattr(svm_mod.LaserEVM, "_fast_hooks", fast)
+        vm = LaserEVM(device=OracleDevice(), strategy=strategy, execution_timeout=0)
+        log, kept = [], []
+
+        def view(state):
+            st = state.environment.active_account.storage
+            return (state.mstate.pc, tuple(x.value for x in state.mstate.stack), state.mstate.min_gas_used,
+                    bytes(state.mstate.memory.raw()), tuple(sorted(st.printable_storage.items())))
+
+        def on_add(state):
+            log.append(("ADD",) + view(state))
+            if state.mstate.pc % 3 == 0:
+                state.mstate.stack[-1] = state.mstate.stack[-1] + 1      # rewrite an operand
+
+        def on_mstore(state):
+            log.append(("MSTORE",) + view(state))
+            if len(state.mstate.memory) >= 32 and state.mstate.pc % 2:
+                state.mstate.memory[5] = 0x42                              # write memory
+
+        def on_sload(state):
+            log.append(("SLOAD",) + view(state))
+            state.environment.active_account.storage[0x99] = 7              # write storage
+
+        def on_jumpi(state):
+            log.append(("JUMPI",) + view(state))
+            if len(kept) < 50:
+                kept.append(state)
+        vm.register_hooks("pre", {"ADD": [on_add], "MSTORE": [on_mstore], "SLOAD": [on_sload],
+                                  "JUMPI": [on_jumpi], "SSTORE": [lambda st: log.append(("SSTORE",) + view(st))]})
+        vm.register_laser_hooks("transaction_end", lambda st, tx, ret, revert: log.append(("end", revert) + view(st)))
+        for tx in _states(30):
+            _setup_global_state_for_execution(vm, tx)
+        vm.exec()
+        return log, [view(k) for k in kept], sorted(view(w) for w in
+                                                   [s for s in vm.open_states] if hasattr(w, "mstate")), vm.lane_steps
+    fast = run(True)
+    slow = run(False)
+    assert fast == slow
+    assert len(fast[0]) > 300
