@@ -40,7 +40,7 @@ import logging
 import os
 import random
 import sys
-from collections import defaultdict
+from collections import Counter, defaultdict
 from copy import copy
 from datetime import datetime, timedelta
 from typing import Callable, DefaultDict, Dict, List, Optional, Tuple
@@ -1421,27 +1421,39 @@ class _Schedule:
         """set(i, "paused" | "event") for every lane of a launch, from one vector
         read of their status and steps (the per-lane form cost ~2 us a lane)."""
         idx = np.asarray(run, dtype=np.int64)
-        st = self.b.status[idx].tolist()
-        steps = self.b.steps[idx].tolist()
+        st = self.b.status[idx]
+        steps = self.b.steps[idx]
+        running = st == MG_RUNNING
+        run_p, steps_p = idx[running].tolist(), steps[running].tolist()
+        run_e, st_e, steps_e = idx[~running].tolist(), st[~running].tolist(), steps[~running].tolist()
         lanes, paused, acked, bfs = self.lanes, self.paused, self.acked, self.bfs
-        ev, pz, push = self._ev, self._pz, heapq.heappush
-        if bfs:
-            for i in run:
-                self._punpause(i)
+        ev, push = self._ev, heapq.heappush
         acked.difference_update(run)
-        for i, s_, k_ in zip(run, st, steps):
-            if s_ == MG_RUNNING:
-                lanes[i].phase = "paused"
-                paused.add(i)
-                if bfs:
-                    self._ppause(i, k_)
-                else:
-                    push(pz, ((-i,), i))
-            else:
-                lanes[i].phase = "event"
-                paused.discard(i)
-                r = k_ - 1 if s_ in _EXECUTED_HALTS else k_
-                push(ev, ((r, i) if bfs else (-i, r), i))
+        paused.difference_update(run_e)
+        paused.update(run_p)
+        if bfs:
+            # every lane of the launch leaves its paused round; the running ones
+            # join their new round (counts in bulk)
+            pround, pcount = self._pround, self._pcount
+            for r in (pround.pop(i, None) for i in run):
+                if r is not None:
+                    pcount[r] -= 1
+            for r, c in Counter(steps_p).items():
+                old = pcount.get(r, 0)
+                if not old:
+                    push(self._prounds, r)
+                pcount[r] = old + c
+            pround.update(zip(run_p, steps_p))
+        else:
+            pz = self._pz
+            for i in run_p:
+                push(pz, ((-i,), i))
+        for i in run_p:
+            lanes[i].phase = "paused"
+        for i, s_, k_ in zip(run_e, st_e, steps_e):
+            lanes[i].phase = "event"
+            r = k_ - 1 if s_ in _EXECUTED_HALTS else k_
+            push(ev, ((r, i) if bfs else (-i, r), i))
 
     def mark_dirty(self, pos: int) -> None:
         self.lanes[pos].dirty = True
