@@ -814,6 +814,7 @@ class LaserEVM:
         scal = (ms.pc, ms.depth, ms.min_gas_used, ms.max_gas_used)
         ids = (id(env), id(acct), id(env.code), id(env.calldata), id(env.address), id(env.sender),
                id(env.origin), id(env.callvalue), id(env.gasprice), id(s.current_transaction), env.static)
+        pre_state = s              # every local reference exists before the baseline counts
         refs0 = _held(s)
         if len(stack) < get_required_stack_elements(name):
             # svm.py:391-402: precheck underflow -- no pre hooks, no tx-end hooks
@@ -828,7 +829,6 @@ class LaserEVM:
             return
         for hook in self.instr_pre_hook.get(name, ()):
             hook(s)
-        pre_state = s
         if _held(s) != refs0:
             s = copy(s)                    # a hook kept the state: the lane goes on with a copy
             ln.state = s

@@ -244,3 +244,34 @@ def test_plain_hook_fast_path_equals_the_general_path(strategy, monkeypatch):
     slow = run(False)
     assert fast == slow
     assert len(fast[0]) > 300
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_hooks_that_keep_nothing_cost_no_state_copy(fast, monkeypatch):
+    """A pre hook that keeps no reference lets the lane go on with the hooked
+    state itself (no GlobalState copy per event), on the fast path and on the
+    general branch; a hook that keeps the state gets one copy per event."""
+    from mythril_amd.laser import state as state_mod
+    monkeypatch.setattr(svm_mod.LaserEVM, "_fast_hooks", fast)
+    copies = [0]
+    orig = state_mod.GlobalState.__copy__
+
+    def counting(self):
+        copies[0] += 1
+        return orig(self)
+    monkeypatch.setattr(state_mod.GlobalState, "__copy__", counting)
+    for keep, want_copies in ((False, False), (True, True)):
+        copies[0] = 0
+        kept, events = [], [0]
+        vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+
+        def hook(st):
+            events[0] += 1
+            if keep:
+                kept.append(st)
+        vm.register_hooks("pre", {op: [hook] for op in ("ADD", "SLOAD", "JUMPI", "MSTORE")})
+        for tx in _states(12):
+            _setup_global_state_for_execution(vm, tx)
+        vm.exec()
+        assert events[0] > 100
+        assert (copies[0] >= events[0]) if want_copies else copies[0] == 0, (keep, copies[0], events[0])
