@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import bisect
 import dataclasses
+import gc
 import heapq
 import itertools
 import logging
@@ -232,7 +233,21 @@ class LaserEVM:
     # ------------------------------------------------------------- exec
     def exec(self, create=False, track_gas=False) -> Optional[List[GlobalState]]:
         """svm.py:293-337: drain the work list; returns the final states when
-        track_gas, else None."""
+        track_gas, else None.  Objects that exist when the drain starts are
+        frozen out of the cyclic collector until it ends (gc.freeze): the event
+        loop allocates a few objects per event, and every full collection it
+        triggered walked the whole heap (the caller's states and everything
+        else alive) again."""
+        frozen = gc.get_freeze_count() == 0      # nested or caller-frozen: leave it to them
+        if frozen:
+            gc.freeze()
+        try:
+            return self._exec(create, track_gas)
+        finally:
+            if frozen:
+                gc.unfreeze()
+
+    def _exec(self, create=False, track_gas=False) -> Optional[List[GlobalState]]:
         final_states: List[GlobalState] = []
         self._exec_stop = False
         for hook in self._start_exec_hooks:
