@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 3 final: host A/B in one process, suite, smoke, default bench line.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/r03${1:-h}
+mkdir -p $OUT
+timeout -k 10 600 python -u scripts/r03/host_ab.py > $OUT/host_ab.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
