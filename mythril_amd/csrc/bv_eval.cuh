@@ -164,7 +164,7 @@ DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) 
             break;
         }
     }
-    return lo ? u_shr_n(v, lo, 0u) : v;
+    return lo ? u_shr_u(v, lo, 0u) : v;      // lo: uniform immediate
 }
 
 // An operand's 256 bits from a slot (LDS), a variable (the model's value row)
@@ -350,7 +350,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             case BV_NOT: r = u_not(A); break;
             case BV_NEG: r = u_neg(A); break;
             case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
-            case BV_EXTRACT: r = u_shr_n(A, rb & 0xffu, 0u); break;
+            case BV_EXTRACT: r = u_shr_u(A, rb & 0xffu, 0u); break;          // rb: uniform immediate
             case BV_ZEXT: r = A; break;
             case BV_SEXT: r = bv_sext(A, rb); break;
             default: {
@@ -370,13 +370,26 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_AND: r = u_and(A, B); break;
                 case BV_OR: r = u_or(A, B); break;
                 case BV_XOR: r = u_xor(A, B); break;
-                case BV_SHL: r = (u_fits32(B) && B.w[0] < width) ? u_shl_n(A, B.w[0]) : u_zero(); break;
-                case BV_LSHR: r = (u_fits32(B) && B.w[0] < width) ? u_shr_n(A, B.w[0], 0u) : u_zero(); break;
-                case BV_ASHR: {
-                    const U256 sa = bv_sext(A, width);
-                    const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
-                    const uint32_t sh = (u_fits32(B) && B.w[0] < width) ? B.w[0] : 255u;
-                    r = u_shr_n(sa, sh, fill);
+                case BV_SHL: case BV_LSHR: case BV_ASHR: {
+                    // a constant shift amount is wave-uniform: scalar-branch shifts
+                    const bool ub = (rb >> 30) == BV_REF_CONST;
+                    const bool in = u_fits32(B) && B.w[0] < width;
+                    if (op == BV_ASHR) {
+                        const U256 sa = bv_sext(A, width);
+                        const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
+                        if (ub) {
+                            const uint32_t sh = uni(in ? B.w[0] : 255u);
+                            r = u_shr_u(sa, sh, fill);
+                        } else {
+                            r = u_shr_n(sa, in ? B.w[0] : 255u, fill);
+                        }
+                    } else if (ub) {
+                        if (!uni(in ? 1u : 0u)) r = u_zero();
+                        else if (op == BV_SHL) r = u_shl_u(A, uni(B.w[0]));
+                        else r = u_shr_u(A, uni(B.w[0]), 0u);
+                    } else {
+                        r = !in ? u_zero() : op == BV_SHL ? u_shl_n(A, B.w[0]) : u_shr_n(A, B.w[0], 0u);
+                    }
                     break;
                 }
                 case BV_EQ: r = u_small(u_eq(A, B)); break;
@@ -398,10 +411,10 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     r = u_select((A.w[0] & 1u) != 0u, B, C);
                     break;
                 }
-                case BV_CONCAT: r = u_or(u_shl_n(A, rc), B); break;
+                case BV_CONCAT: r = u_or(u_shl_u(A, rc), B); break;                 // rc: uniform
                 case BV_ADD_NOOVF_U: {  // top bit of the (w+1)-bit sum is 0
                     const U256 s = u_add(A, B);
-                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_n(s, rc, 0u));
+                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_u(s, rc, 0u));
                     r = u_small(!ovf);
                     break;
                 }
@@ -412,7 +425,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_SMIN: r = u_select(u_slt(bv_sext(B, width), bv_sext(A, width)), B, A); break;
                 case BV_SMAX: r = u_select(u_slt(bv_sext(A, width), bv_sext(B, width)), B, A); break;
                 case BV_RSUB: r = u_sub(B, A); break;
-                case BV_RCONCAT: r = u_or(u_shl_n(B, rc), A); break;
+                case BV_RCONCAT: r = u_or(u_shl_u(B, rc), A); break;
                 default: r = u_zero(); break;
                 }
             }

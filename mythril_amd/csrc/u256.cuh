@@ -196,6 +196,47 @@ DEV U256 u_shr_n(U256 a, uint32_t n, uint32_t fill) {
     o.w[7] = fsr(fill, a.w[7], r);
     return o;
 }
+// Shifts by a wave-uniform amount n < 256 (an instruction immediate, a constant
+// operand): the limb move is a scalar branch over n / 32 with one static
+// permutation per case (8 moves) instead of the three-stage v_cndmask barrel
+// (24 VALU); the funnel shift is the same 8 v_alignbit.  n must be uniform
+// across the wave (the caller guarantees it: the branches are scalar).
+#define U_LIMB_CASES(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+DEV U256 u_shl_u(const U256 &a, uint32_t n) {
+    U256 t;
+    switch (n >> 5) {
+#define U_SHL_CASE(Q) case Q: _Pragma("unroll") for (int i = 0; i < 8; ++i) t.w[i] = i >= Q ? a.w[i - Q] : 0u; break;
+    U_LIMB_CASES(U_SHL_CASE)
+#undef U_SHL_CASE
+    default: t = u_zero(); break;
+    }
+    const uint32_t r = n & 31u;
+    if (r == 0u) return t;
+    U256 o;
+#pragma unroll
+    for (int i = 7; i >= 1; --i) o.w[i] = __builtin_amdgcn_alignbit(t.w[i], t.w[i - 1], 32u - r);
+    o.w[0] = t.w[0] << r;
+    return o;
+}
+// (a >> n) with `fill` shifted in (0, or 0xffffffff for an arithmetic shift)
+DEV U256 u_shr_u(const U256 &a, uint32_t n, uint32_t fill) {
+    U256 t;
+    switch (n >> 5) {
+#define U_SHR_CASE(Q) case Q: _Pragma("unroll") for (int i = 0; i < 8; ++i) t.w[i] = i + Q < 8 ? a.w[i + Q] : fill; break;
+    U_LIMB_CASES(U_SHR_CASE)
+#undef U_SHR_CASE
+    default: t = u_zero(); break;
+    }
+    const uint32_t r = n & 31u;
+    if (r == 0u) return t;
+    U256 o;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) o.w[i] = __builtin_amdgcn_alignbit(t.w[i + 1], t.w[i], r);
+    o.w[7] = __builtin_amdgcn_alignbit(fill, t.w[7], r);
+    return o;
+}
+#undef U_LIMB_CASES
+
 // z3 bvshl / bvlshr / bvashr (shift >= 256 -> 0 / sign fill)
 DEV U256 u_shl(const U256 &a, const U256 &s) {
     if (!u_fits32(s) || s.w[0] >= 256u) return u_zero();
