@@ -38,7 +38,8 @@ extern "C" {
                                9: mg_lanes_upload_live; lane transfers batched
                                   through one pinned DMA per phase; symbolic
                                   calldata copies (MG_SYM_CDBYTE) and a creation's
-                                  calldata opcodes (MG_REC_CDSIZE) on symbolic lanes */
+                                  calldata opcodes (MG_REC_CDSIZE) on symbolic lanes;
+                                  symbolic EXP (MG_SYM_BIN 0x0a, MG_REC_SYMEXP) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -121,6 +122,11 @@ extern "C" {
  *                  value pushed; the host appends `calldata.size == result` to the
  *                  path's constraints.  len = 0, no payload.                       */
 #define MG_REC_CDSIZE   6u
+/*   MG_REC_SYMEXP  EXP with a symbolic operand (symbolic lanes, instructions.py:624-638):
+ *                  payload = the MG_SYM_BIN node (immediate 0x0a) pushed as the result,
+ *                  Power(base, exponent); the host appends exponent_function_manager's
+ *                  condition for (base, exponent) to the path.  len = 0.            */
+#define MG_REC_SYMEXP   7u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */

@@ -797,9 +797,23 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             U256 rval = u_zero();
             bool esc = false, arena_full = false, fork = false;
             uint32_t ya = 0u, yb = 0u;
+            uint32_t exp_rec = 0xffffffffu;         // EXP: where its MG_REC_SYMEXP record goes
             if (kind == K_JUMPI) {
                 if (ta) esc = true;                 // symbolic jump target
                 else fork = true;                   // symbolic condition: the host forks
+            } else if (op == 0x0au && !env_sym && !cd_sym) {
+                // EXP with a symbolic operand (instructions.py:624-638): Power(base,
+                // exponent), the uninterpreted function, and the manager's condition
+                // on it appended to the path (the host replays the record in order)
+                const uint32_t rec_at = L.rec_len[lane];
+                if (tl || !L.rec_cap || (uint64_t)rec_at + MG_REC_HEADER + 1u > L.rec_cap ||
+                    sym_width(S, N, lane, ta) == 1u || sym_width(S, N, lane, tb) == 1u)
+                    esc = true;                     // Bool operands, taint lanes: the host
+                else if (!sym_ref(S, N, lane, ta, a, lnc, ya) || !sym_ref(S, N, lane, tb, b, lnc, yb) ||
+                         !sym_node_push(S, N, lane, SYM_BIN | (256u << 8), ya, yb, op, lnn, rtag))
+                    arena_full = true;
+                else
+                    exp_rec = rec_at;
             } else if (op == 0x37u || kind == K_SHA3 || !(sym_bin_ok(op) || op == 0x15u || op == 0x19u ||
                                                           env_sym || cd_sym)) {
                 esc = true;
@@ -848,6 +862,11 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (tl)
                 t_commit(T, N, lane, op, kind, tact, sp, nsp + 1u, nin, pushes, cd_sym, a, b, tb != 0u, pre_bit,
                          post_bit, nobj, tsink, ttf);
+            if (exp_rec != 0xffffffffu) {
+                uint32_t at = rec_head(L, lane, exp_rec, MG_REC_SYMEXP, 0u, L.steps[lane] + executed, u_zero());
+                L.rec[(size_t)at * N + lane] = rtag - 1u;
+                L.rec_len[lane] = at + 1u;
+            }
             V.set_stack(nsp, rval);
             sym_set_tag(S, N, lane, nsp, rtag);
             sp = nsp + 1u; ++pc; gmin = ngmin; gmax = ngmax; nn = lnn; nc = lnc;

@@ -40,6 +40,7 @@ MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
 MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
 MG_REC_CDSIZE = 6       # a creation's CODESIZE: the host appends calldata.size == result
+MG_REC_SYMEXP = 7       # EXP with a symbolic operand: payload = the Power node's index
 MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
@@ -368,6 +369,10 @@ class LaneBatch:
                 k += 8 * (ln - 1)
                 out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF))
                 k += 2
+            elif kind == MG_REC_SYMEXP:
+                # (step, "symexp", Power node index)
+                out.append((step, "symexp", int(q[k])))
+                k += 1
             elif kind == MG_REC_CDSIZE:
                 # (step, "cdsize", the CODESIZE value pushed)
                 out.append((step, "cdsize", r))

@@ -663,6 +663,8 @@ class LaserEVM:
                 if r[1] == "symkeccak":
                     # the input as the lane's arena holds it now (its node is final)
                     r = (r[0], "symkeccak", sym.keccak_input(b, i, self._rec_lanes[i].state, r[2]))
+                elif r[1] == "symexp":
+                    r = (r[0], "symexp", sym.exp_operands(b, i, self._rec_lanes[i].state, r[2]))
                 key = (r[0], i) if self._rec_bfs else (-i, r[0])
                 heapq.heappush(self._recq, (key, next(self._rec_seq), i, r))
             b.rec_seen[i] = end
@@ -684,6 +686,11 @@ class LaserEVM:
                 tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
             elif r[1] == "hook":
                 tnt.replay_deferred(r, lanes[i].state, self._plan)
+            elif r[1] == "symexp":
+                # exp_ of a symbolic operand (instructions.py:624-638): the manager's
+                # condition on Power(base, exponent)
+                _, cond = exponent_function_manager.create_condition(*r[2])
+                lanes[i].state.world_state.constraints.append(cond)
             elif r[1] == "cdsize":
                 # codesize_ of a creation (instructions.py:989-997): the symbolic
                 # calldata's size is pinned to the pushed value

@@ -157,6 +157,9 @@ def binary(op: int, a, b):
         return LShR(as_bitvec(b), as_bitvec(a))
     if op == 0x1D:
         return as_bitvec(b) >> as_bitvec(a)
+    if op == 0x0A:                                          # EXP: Power(base, exponent)
+        from ..smt.exponent_manager import exponent_function_manager
+        return exponent_function_manager.create_condition(as_bitvec(a), as_bitvec(b))[0]
     raise NotEncodable(f"no symbolic semantics for opcode {op:#x}")
 
 
@@ -337,6 +340,13 @@ def decode_lane(b, i: int, state):
 
 def decode_node(b, i: int, state, k: int):
     return _Decoder(b, i, state).node(k)
+
+
+def exp_operands(b, i: int, state, k: int):
+    """(base, exponent) of lane i's EXP node k (an MG_REC_SYMEXP record)."""
+    dec = _Decoder(b, i, state)
+    _, y, z, _ = (int(v) for v in b.node[i, k])
+    return as_bitvec(dec.ref(y)), as_bitvec(dec.ref(z))
 
 
 def keccak_input(b, i: int, state, k: int):

@@ -274,9 +274,15 @@ class Engine:
             if _val(target) is None:
                 raise Unsupported("symbolic jump target")
             return self._jumpi(s, _val(target), cond)
-        if op == 0x37 or op not in _SYM_OK and not sym_env and op not in (0x35, 0x36):
+        if op == 0x37 or op not in _SYM_OK and not sym_env and op not in (0x35, 0x36, 0x0A):
             raise Unsupported(f"{name} with symbolic inputs")
-        if sym_env:
+        cond_after = None
+        if op == 0x0A:                                          # exp_, instructions.py:624-638
+            base, exponent = st.pop(), st.pop()
+            if isinstance(base, Bool) or isinstance(exponent, Bool):
+                raise Unsupported("EXP of a Bool")
+            res, cond_after = exponent_function_manager.create_condition(base, exponent)
+        elif sym_env:
             res = getattr(env, env_attr)
         elif op == 0x36:
             res = env.calldata.size
@@ -299,6 +305,8 @@ class Engine:
         if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
             self.ended.append(("exception", state))
             return []
+        if cond_after is not None:
+            s.world_state.constraints.append(cond_after)
         st.append(res)
         ms.pc += 1
         ms.min_gas_used += gmin

@@ -56,7 +56,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
     vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
     queue = [_initial(ws, addr)]
     eng = symref.Engine()
-    forks = device_steps = checked = sym_sha3 = halts_past_sha3 = 0
+    forks = device_steps = checked = sym_sha3 = halts_past_sha3 = sym_exp = 0
     while queue:
         batch_states = queue[:256]
         queue = queue[256:]
@@ -96,6 +96,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                 assert gst.slots() == rst.slots()
             recs = b.records(i)
             sym_sha3 += sum(1 for r in recs if r[1] == "symkeccak")
+            sym_exp += sum(1 for r in recs if r[1] == "symexp")
             if st in (1, 2, 3) and any(r[1] == "symkeccak" for r in recs):
                 halts_past_sha3 += 1
             checked += 1
@@ -109,6 +110,9 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
             elif st == MG_ESCAPE:
                 assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
     assert forks >= 3 and device_steps > 100 and checked > forks
+    if name == "flag_array.sol.o":
+        # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
+        assert sym_exp > 0
     if name == "overflow.sol.o":
         # symbolic storage and mapping slots: paths hash a symbolic caller (a
         # SHA3 of symbolic memory), read and write the symbolic storage and halt

@@ -198,6 +198,24 @@ def test_restated_creation_calldata_opcodes_follow_the_reference():
         {0x40 + k: cd[0x13 - len(code) + k].raw for k in range(3)} if 0x13 >= len(code) else True
 
 
+def test_restated_symbolic_exp_follows_the_reference():
+    """exp_ (instructions.py:624-638) of a symbolic exponent: Power(256, x) on the
+    stack and exponent_function_manager's condition (Power > 0, the 256**i table,
+    periodicity mod 32 for base 256) appended; the device's EXP node decodes to
+    the same term and re-encodes as SYM_BIN 0x0a."""
+    from mythril_amd.smt.exponent_manager import exponent_function_manager
+    s = _state("600035" "610100" "0a" "00")          # PUSH1 0 CALLDATALOAD PUSH2 0x100 EXP STOP
+    e = symref.Engine()
+    for _ in range(4):
+        (s,) = e.step(s)
+    x = s.environment.calldata.get_word_at(0)
+    want, cond = exponent_function_manager.create_condition(BVV(256, 256), x)
+    assert s.mstate.stack[-1].raw is want.raw
+    assert s.world_state.constraints[-1].raw is cond.raw
+    got = sym.binary(0x0A, BVV(256, 256), x)
+    assert got.raw is want.raw
+
+
 # ---- symbolic memory, storage chains and SHA3 (ABI v7) -----------------------------
 def _run_restatement(code_hex, steps):
     s = _state(code_hex)
