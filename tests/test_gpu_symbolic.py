@@ -24,6 +24,7 @@ from mythril_amd.laser import (BreadthFirstSearchStrategy, LaserEVM, MessageCall
                                SymbolicCalldata)
 from mythril_amd.laser import symbolic as sym
 from mythril_amd.laser.transaction import ACTORS
+from mythril_amd.smt.exponent_manager import exponent_function_manager
 from mythril_amd.smt.expr import Or, symbol_factory
 
 pytestmark = pytest.mark.gpu
@@ -74,6 +75,16 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
             device_steps += n
             st = int(b.status[i])
             got = vm._materialise(b, i, copy(s0))
+            # the path constraints LaserEVM's record replay appends (EXP: the
+            # exponent manager's condition, instructions.py:624-638), in order
+            for r in b.records(i):
+                if r[1] == "symexp":
+                    _, cond = exponent_function_manager.create_condition(*sym.exp_operands(b, i, got, r[2]))
+                    got.world_state.constraints.append(cond)
+                elif r[1] == "exp":
+                    _, cond = exponent_function_manager.create_condition(
+                        symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))
+                    got.world_state.constraints.append(cond)
             # the restatement: the same state, the same number of instructions (a
             # halt or VmException counts as a step but leaves the state at its start)
             ref = s0
