@@ -133,3 +133,24 @@ def test_vmtests_keccak_records_hash_their_inputs():
                 n_exp += 1
                 assert pow(r[2], r[3], 2 ** 256) == r[4]
     assert n_kec >= 5 and n_exp >= 10, (n_kec, n_exp)
+
+
+def test_symbolic_record_kinds_parse_in_log_order():
+    """MG_REC_SYMEXP (payload: the Power node) and MG_REC_CDSIZE (result: the
+    CODESIZE value pushed) between an EXP record, as k_sym_step writes them
+    (include/mythgpu.h): LaneBatch.records returns them in log order."""
+    from mythril_amd.lanes import MG_REC_CDSIZE, MG_REC_EXP, MG_REC_SYMEXP, word_to_limbs
+    b = LaneBatch(LaneShape(n=2, stack_cap=8, mem_cap=64, calldata_cap=32, storage_cap=4, rec_cap=64))
+    words = []
+
+    def head(kind, ln, step, r):
+        words.extend([kind, ln, step] + [int(x) for x in word_to_limbs(r)])
+    head(MG_REC_CDSIZE, 0, 3, 0x2c9)
+    head(MG_REC_SYMEXP, 0, 7, 0)
+    words.append(5)
+    head(MG_REC_EXP, 0, 9, 256 ** 3)
+    words.extend([int(x) for x in word_to_limbs(256)] + [int(x) for x in word_to_limbs(3)])
+    b.rec[1, :len(words)] = words
+    b.rec_len[1] = len(words)
+    assert b.records(1) == [(3, "cdsize", 0x2c9), (7, "symexp", 5), (9, "exp", 256, 3, 256 ** 3)]
+    assert b.records(0) == []
