@@ -50,7 +50,15 @@ enum BvOp : uint32_t {
     BV_SMIN, BV_SMAX,  // signed at `width`
     BV_RSUB,           // B - A           (operand-swapped forms: the accumulator is only
     BV_RCONCAT,        // A low, B high,   ever operand A; w3 = width of A)
-    BV_NUM_OPS
+    BV_NUM_OPS,
+    // fused pairs, formed by bv_upload from adjacent instructions (never accepted
+    // at the C-ABI): the first's result feeds only the second's accumulator, so one
+    // dispatch does both and the 0/1 or 128-bit intermediate is never widened to
+    // a 256-bit accumulator.  MG_BV_FUSE=0 uploads the programs unfused.
+    BV_CMP_BAND = BV_NUM_OPS,   // cmp(A, B) & C: w0 bits 22..27 = the comparison, width = its
+                                // operand width (w3 of the comparison); C = the and's B
+    BV_EXT_RCAT,                // rconcat(extract(A, lo, ew), B): w3 = shift | lo << 9 | ew << 17
+    BV_NUM_INTERNAL
 };
 
 #define BV_REF_ACC 0u
@@ -88,6 +96,7 @@ struct BvState {
     bool lds_prog = false;           // MG_BV_PROG=lds stages the program tile in LDS
     bool pair = false;               // MG_BV_PROG=pair: two models per thread (k_bv_eval_pair)
     std::vector<uint32_t> h_tiles;
+    std::vector<uint32_t> h_insns, h_off;   // the fused programs (bv_fuse)
 };
 
 DEV U256 bv_mask(U256 v, uint32_t width) {
@@ -260,7 +269,7 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
                      (1ull << BV_TAB) | (1ull << BV_SMIN) | (1ull << BV_SMAX) | (1ull << BV_ZEXT) | \
                      (1ull << BV_AND) | (1ull << BV_OR) | (1ull << BV_XOR) | (1ull << BV_LSHR) | \
                      (1ull << BV_UREM) | (1ull << BV_UMIN) | (1ull << BV_UMAX) | (1ull << BV_RSUB) | \
-                     (1ull << BV_RCONCAT))
+                     (1ull << BV_RCONCAT) | (1ull << BV_EXT_RCAT))
 
 // MG_BV_WAVES: minimum waves per SIMD the register allocation must allow (0
 // leaves the compiler's choice).  8 caps the kernel at 64 VGPRs (a few spill to
@@ -426,6 +435,32 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_SMAX: r = u_select(u_slt(bv_sext(A, width), bv_sext(B, width)), B, A); break;
                 case BV_RSUB: r = u_sub(B, A); break;
                 case BV_RCONCAT: r = u_or(u_shl_u(B, rc), A); break;
+                case BV_CMP_BAND: {
+                    const uint32_t sub = (w0 >> 22) & 0x3fu;
+                    bool t;
+                    switch (sub) {
+                    case BV_EQ: t = u_eq(A, B); break;
+                    case BV_NE: t = !u_eq(A, B); break;
+                    case BV_ULT: t = u_lt(A, B); break;
+                    case BV_ULE: t = !u_lt(B, A); break;
+                    case BV_UGT: t = u_lt(B, A); break;
+                    case BV_UGE: t = !u_lt(A, B); break;
+                    case BV_SLT: t = u_slt(bv_sext(A, width), bv_sext(B, width)); break;
+                    case BV_SLE: t = !u_slt(bv_sext(B, width), bv_sext(A, width)); break;
+                    case BV_SGT: t = u_slt(bv_sext(B, width), bv_sext(A, width)); break;
+                    default: t = !u_slt(bv_sext(A, width), bv_sext(B, width)); break;   // BV_SGE
+                    }
+                    const U256 C = bv_fetch(c, rc);
+                    r = u_small((t ? 1u : 0u) & C.w[0]);
+                    break;
+                }
+                case BV_EXT_RCAT: {
+                    const uint32_t ew = (rc >> 17) & 0x1ffu;
+                    U256 lo = u_shr_u(A, (rc >> 9) & 0xffu, 0u);
+                    if (ew < 256u) lo = bv_mask(lo, ew);
+                    r = u_or(u_shl_u(B, rc & 0x1ffu), lo);
+                    break;
+                }
                 default: r = u_zero(); break;
                 }
             }
@@ -687,6 +722,53 @@ static void bv_free(BvState &s) {
     s = BvState{};
 }
 
+// Superinstructions: rewrite each DAG's program, fusing an instruction whose
+// result is not stored into the next one when that one reads it as its
+// accumulator and the pair is one of the flattener's common shapes (C4: 10 % of
+// instructions are a comparison feeding a Boolean and, 3 % a 128-bit extract
+// feeding an rconcat).  The fused program computes the same value bit for bit
+// (tests/test_gpu_eval.py checks every program against the oracle, which runs
+// the unfused program); it only saves a dispatch and the widening of the
+// intermediate to a 256-bit accumulator.
+static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off) {
+    const uint32_t n = dags->n_dags;
+    out.clear();
+    out.reserve((size_t)dags->prog_off[n] * 4);
+    off.assign((size_t)n + 1, 0u);
+    for (uint32_t d = 0; d < n; ++d) {
+        off[d] = (uint32_t)(out.size() / 4);
+        const uint32_t a = dags->prog_off[d], b = dags->prog_off[d + 1];
+        for (uint32_t i = a; i < b; ++i) {
+            const uint32_t *p = dags->insns + 4 * (size_t)i;
+            const uint32_t op = p[0] & 0xffu;
+            if (i + 1 < b && ((p[0] >> 17) & 1u) == 0u) {
+                const uint32_t *q = p + 4;
+                const uint32_t op2 = q[0] & 0xffu, w2 = (q[0] >> 8) & 0x1ffu;
+                const uint32_t keep2 = q[0] & (0x1fu << 17);          // the second's store bit + slot
+                const bool acc2 = (q[1] >> 30) == BV_REF_ACC;
+                const bool cmp = (op >= BV_EQ && op <= BV_SGE) || op == BV_NE;
+                if (acc2 && cmp && op2 == BV_BAND && p[3] >= 1u && p[3] <= 256u) {
+                    const uint32_t w = (p[3] & 0x1ffu);
+                    const uint32_t f[4] = {BV_CMP_BAND | (w << 8) | keep2 | (op << 22), p[1], p[2], q[2]};
+                    out.insert(out.end(), f, f + 4);
+                    ++i;
+                    continue;
+                }
+                if (acc2 && op == BV_EXTRACT && op2 == BV_RCONCAT && q[3] < 512u) {
+                    const uint32_t ew = (p[0] >> 8) & 0x1ffu;
+                    const uint32_t f[4] = {BV_EXT_RCAT | (w2 << 8) | keep2, p[1], q[2],
+                                           q[3] | ((p[2] & 0xffu) << 9) | (ew << 17)};
+                    out.insert(out.end(), f, f + 4);
+                    ++i;
+                    continue;
+                }
+            }
+            out.insert(out.end(), p, p + 4);
+        }
+    }
+    off[n] = (uint32_t)(out.size() / 4);
+}
+
 static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch *models, hipStream_t st,
                      std::string &msg) {
     if (dags->n_dags == 0 || !dags->prog_off || !dags->insns) { msg = "empty DAG batch"; return MG_EINVAL; }
@@ -726,24 +808,38 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
             }
         }
     }
+    const char *pv = getenv("MG_BV_PROG");
+    // scalar-load fetch by default: at 8 waves per SIMD the LDS tile would cost
+    // occupancy (C4: scalar 220 ms, LDS 232 ms); MG_BV_PROG=lds selects the other
+    s.lds_prog = pv && std::string(pv) == "lds";
+    s.pair = pv && std::string(pv) == "pair";
+    const char *fv = getenv("MG_BV_FUSE");
+    const uint32_t *insns = dags->insns, *prog_off = dags->prog_off;
+    uint32_t total_up = total;
+    if (!s.pair && !(fv && fv[0] == '0')) {
+        bv_fuse(dags, s.h_insns, s.h_off);
+        insns = s.h_insns.data();
+        prog_off = s.h_off.data();
+        total_up = s.h_off[n];
+    }
     // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
     // LDS tile capacity: the longest program rounded up, at least BV_TILE_MIN, so
     // short-program batches keep a small LDS footprint (higher occupancy)
     uint32_t longest = 0;
-    for (uint32_t d = 0; d < n; ++d) longest = std::max(longest, dags->prog_off[d + 1] - dags->prog_off[d]);
+    for (uint32_t d = 0; d < n; ++d) longest = std::max(longest, prog_off[d + 1] - prog_off[d]);
     s.tile_cap = std::max<uint32_t>(BV_TILE_MIN, (longest + 255u) & ~255u);
     s.h_tiles.clear();
     s.h_tiles.push_back(0);
     uint32_t acc = 0;
     for (uint32_t d = 0; d < n; ++d) {
-        const uint32_t len = dags->prog_off[d + 1] - dags->prog_off[d];
+        const uint32_t len = prog_off[d + 1] - prog_off[d];
         if (acc + len > s.tile_cap || (d - s.h_tiles.back()) >= BV_TILE_DAGS) { s.h_tiles.push_back(d); acc = 0; }
         acc += len;
     }
     s.h_tiles.push_back(n);
     s.n_tiles = (uint32_t)s.h_tiles.size() - 1;
     int rc = 0;
-    if ((rc = bv_ensure(s.insns, s.cap_insns, total))) { msg = "alloc insns"; return rc; }
+    if ((rc = bv_ensure(s.insns, s.cap_insns, total_up))) { msg = "alloc insns"; return rc; }
     if ((rc = bv_ensure(s.prog_off, s.cap_dags, (size_t)n + 1))) { msg = "alloc offsets"; return rc; }
     if ((rc = bv_ensure(s.tile_dag, s.cap_tiles, s.h_tiles.size()))) { msg = "alloc tiles"; return rc; }
     if ((rc = bv_ensure(s.consts, s.cap_consts, (size_t)std::max<uint32_t>(dags->n_consts, 1) * 2))) { msg = "alloc consts"; return rc; }
@@ -774,8 +870,8 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         return MG_ENOMEM;
     }
     hipError_t e = hipSuccess;
-    e = e ? e : hipMemcpyAsync(s.insns, dags->insns, (size_t)total * 16, hipMemcpyHostToDevice, st);
-    e = e ? e : hipMemcpyAsync(s.prog_off, dags->prog_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.insns, insns, (size_t)total_up * 16, hipMemcpyHostToDevice, st);
+    e = e ? e : hipMemcpyAsync(s.prog_off, prog_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st);
     e = e ? e : hipMemcpyAsync(s.tile_dag, s.h_tiles.data(), s.h_tiles.size() * 4, hipMemcpyHostToDevice, st);
     if (dags->n_consts) e = e ? e : hipMemcpyAsync(s.consts, dags->consts, (size_t)dags->n_consts * 32, hipMemcpyHostToDevice, st);
     if (models->n_vars)
@@ -792,11 +888,6 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     e = e ? e : hipStreamSynchronize(st);
     if (e != hipSuccess) { msg = std::string("bv upload: ") + hipGetErrorString(e); return MG_EDEVICE; }
     s.n_tables = models->n_tables; s.n_entries = models->n_entries;
-    const char *pv = getenv("MG_BV_PROG");
-    // scalar-load fetch by default: at 8 waves per SIMD the LDS tile would cost
-    // occupancy (C4: scalar 220 ms, LDS 232 ms); MG_BV_PROG=lds selects the other
-    s.lds_prog = pv && std::string(pv) == "lds";
-    s.pair = pv && std::string(pv) == "pair";
     s.n_dags = n; s.n_models = models->n_models; s.n_vars = models->n_vars;
     s.n_slots = std::max<uint32_t>(dags->n_slots, 1); s.n_consts = dags->n_consts;
     return 0;

@@ -24,7 +24,9 @@ def child():
     dev = GpuDevice(0)
     out = {}
     for mode in os.environ.get("AB_K2_MODES", "lds,scalar").split(","):
-        os.environ["MG_BV_PROG"] = mode
+        # "<fetch>-nofuse": the same fetch with the programs uploaded unfused
+        os.environ["MG_BV_PROG"] = mode.removesuffix("-nofuse")
+        os.environ["MG_BV_FUSE"] = "0" if mode.endswith("-nofuse") else "1"
         dev.eval_upload(prog, models)
         dev.eval_run()
         ms = min(dev.eval_run() for _ in range(3))

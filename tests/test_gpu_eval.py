@@ -167,3 +167,75 @@ def test_pair_mode_bitmaps_equal_single_mode(dev, monkeypatch):
     for k in range(3):
         assert np.array_equal(out["scalar"][k], out["pair"][k])
     assert int(out["pair"][1].sum()) > 0
+
+
+def _fusable_programs(n_dags, seed):
+    """Random programs made of the two fused shapes (bv_fuse in bv_eval.cuh):
+    comparison -> Boolean and, and extract -> rconcat, with every comparison kind,
+    signed widths 1..256, accumulator and slot operands, stored and unstored
+    intermediates (a stored first instruction must stay unfused)."""
+    from mythril_amd.smt.program import ProgramBatch
+    O = synth.OPCODE
+    rng = random.Random(seed)
+    cmps = ["eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge"]
+    widths = [256, 64, 8]
+    var = lambda i: (2 << 30) | i
+    slot = lambda i: (1 << 30) | i
+    const = lambda i: (3 << 30) | i
+
+    def w0(op, width, store=None):
+        return O[op] | (width << 8) | ((1 << 17) | (store << 18) if store is not None else 0)
+
+    insns, off = [], [0]
+    for _ in range(n_dags):
+        prog = [[w0("copy", 256, 0), var(rng.randrange(3)), 0, 0]]          # slot 0: a variable
+        prog.append([w0("extract", 1, 1), var(rng.randrange(3)), rng.randrange(256), 0])  # slot 1: a bit
+        for _ in range(rng.randrange(2, 6)):
+            if rng.random() < 0.6:
+                # two sw-bit operands (slot 2 and the accumulator), compared, and-ed with slot 1
+                k = rng.choice(cmps)
+                sw = rng.choice([1, 7, 8, 64, 128, 255, 256])
+                prog.append([w0("extract", sw, 2), var(rng.randrange(3)), rng.randrange(257 - sw), 0])
+                prog.append([w0("extract", sw), var(rng.randrange(3)), rng.randrange(257 - sw), 0])
+                prog.append([w0(k, 1, 2 if rng.random() < 0.2 else None), 0, slot(2), sw])
+                prog.append([w0("and", 1, 1 if rng.random() < 0.5 else None), 0, slot(1), 0])
+            else:
+                # an hw-bit high part in slot 3, an ew-bit extract, rconcat'ed
+                ew = rng.choice([1, 8, 100, 128, 255])
+                hw = rng.choice([1, 8, 128, 256 - ew]) if ew < 256 else 0
+                hw = max(1, min(hw, 256 - ew))
+                prog.append([w0("extract", hw, 3), var(rng.randrange(3)), rng.randrange(257 - hw), 0])
+                prog.append([w0("extract", ew, 2 if rng.random() < 0.2 else None), var(rng.randrange(3)),
+                             rng.randrange(257 - ew), 0])
+                prog.append([w0("rconcat", ew + hw, 0 if rng.random() < 0.5 else None), 0, slot(3), ew])
+            prog.append([w0("and", 1), slot(1), slot(1), 0] if rng.random() < 0.3 else
+                        [w0("bvugt", 1), slot(0), var(0), 256])
+        insns += prog
+        off.append(len(insns))
+    consts = np.zeros((2, 8), dtype=np.uint32)
+    consts[1, :] = 0xFFFFFFFF
+    consts[1, 7] = 0x7FFFFFFF
+    return ProgramBatch(np.asarray(insns, dtype=np.uint32), np.asarray(off, dtype=np.uint32), consts, 4,
+                        ["x0", "x1", "x2"], [256, 256, 256])
+
+
+def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
+    """Superinstructions (MG_BV_FUSE, on by default): on programs dense in the
+    fused shapes, and on C4's own, per-model bitmaps equal the unfused upload's and
+    first/count equal the oracle, which always interprets the unfused program."""
+    mr = random.Random(9)
+    specials = [0, 1, (1 << 255), (1 << 256) - 1, (1 << 127), (1 << 63) - 1]
+    models = [{n: mr.choice(specials) if mr.random() < 0.4 else mr.getrandbits(256) for n in ("x0", "x1", "x2")}
+              for _ in range(320)]
+    for prog, pool in ((_fusable_programs(600, 3), None),
+                       (synth.c4_programs(synth.Draws(500, seed=synth.C4_SEED + 29)), synth.c4_models(300, seed=31))):
+        pool = pool or ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
+        out = {}
+        for fuse in ("1", "0"):
+            monkeypatch.setenv("MG_BV_FUSE", fuse)
+            out[fuse] = dev.eval_bits(prog, pool)
+        for k in range(3):
+            assert np.array_equal(out["1"][k], out["0"][k])
+        rfs, rsc = eval_batch(prog, pool)
+        assert np.array_equal(out["1"][0], rfs) and np.array_equal(out["1"][1], rsc)
+        assert 0 < int(out["1"][1].sum()) < prog.n_dags * pool.n_models
