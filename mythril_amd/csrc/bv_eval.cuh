@@ -58,6 +58,8 @@ enum BvOp : uint32_t {
     BV_CMP_BAND = BV_NUM_OPS,   // cmp(A, B) & C: w0 bits 22..27 = the comparison, width = its
                                 // operand width (w3 of the comparison); C = the and's B
     BV_EXT_RCAT,                // rconcat(extract(A, lo, ew), B): w3 = shift | lo << 9 | ew << 17
+    BV_BIN2,                    // op2(op1(A, B), C) for two 256-bit ops of bv_simple: w0 bits
+                                // 22..25 = op1, 26..29 = op2 (bv_simple indices); C = op2's B
     BV_NUM_INTERNAL
 };
 
@@ -284,6 +286,23 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
 #define BV_BOUNDS __launch_bounds__(BV_BLOCK)
 #endif
 
+// the 256-bit binary ops BV_BIN2 fuses (index = position in kBvSimple), each
+// exactly as the unfused switch computes it
+__device__ __forceinline__ U256 bv_simple(uint32_t k, const U256 &a, const U256 &b) {
+    switch (k) {                                   // wave-uniform
+    case 0: return u_add(a, b);
+    case 1: return u_sub(a, b);
+    case 2: return u_mul(a, b);
+    case 3: return u_and(a, b);
+    case 4: return u_or(a, b);
+    case 5: return u_xor(a, b);
+    case 6: return u_select(u_lt(a, b), b, a);     // BV_UMAX
+    case 7: return u_select(u_lt(b, a), b, a);     // BV_UMIN
+    default: return u_sub(b, a);                   // BV_RSUB
+    }
+}
+static const uint32_t kBvSimple[9] = {BV_ADD, BV_SUB, BV_MUL, BV_AND, BV_OR, BV_XOR, BV_UMAX, BV_UMIN, BV_RSUB};
+
 template <bool kLdsProg>
 __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
@@ -452,6 +471,12 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     }
                     const U256 C = bv_fetch(c, rc);
                     r = u_small((t ? 1u : 0u) & C.w[0]);
+                    break;
+                }
+                case BV_BIN2: {
+                    const U256 t = bv_simple((w0 >> 22) & 0xfu, A, B);
+                    const U256 C = bv_fetch(c, rc);
+                    r = bv_simple((w0 >> 26) & 0xfu, t, C);
                     break;
                 }
                 case BV_EXT_RCAT: {
@@ -724,13 +749,20 @@ static void bv_free(BvState &s) {
 
 // Superinstructions: rewrite each DAG's program, fusing an instruction whose
 // result is not stored into the next one when that one reads it as its
-// accumulator and the pair is one of the flattener's common shapes (C4: 10 % of
-// instructions are a comparison feeding a Boolean and, 3 % a 128-bit extract
-// feeding an rconcat).  The fused program computes the same value bit for bit
+// accumulator and the pair is one of the flattener's common shapes (of C4's
+// instructions, 10 % are a comparison feeding a Boolean and, 17 % a 256-bit
+// add/sub/mul/and/or/xor/umax/umin/rsub feeding another, 3 % a 128-bit extract
+// feeding an rconcat; MG_BV_FUSE=1 leaves out the second shape, =0 all three).  The fused program computes the same value bit for bit
 // (tests/test_gpu_eval.py checks every program against the oracle, which runs
 // the unfused program); it only saves a dispatch and the widening of the
 // intermediate to a 256-bit accumulator.
-static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off) {
+static int bv_simple_index(uint32_t op) {
+    for (int k = 0; k < 9; ++k)
+        if (kBvSimple[k] == op) return k;
+    return -1;
+}
+static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off,
+                    bool bin2) {
     const uint32_t n = dags->n_dags;
     out.clear();
     out.reserve((size_t)dags->prog_off[n] * 4);
@@ -750,6 +782,15 @@ static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::v
                 if (acc2 && cmp && op2 == BV_BAND && p[3] >= 1u && p[3] <= 256u) {
                     const uint32_t w = (p[3] & 0x1ffu);
                     const uint32_t f[4] = {BV_CMP_BAND | (w << 8) | keep2 | (op << 22), p[1], p[2], q[2]};
+                    out.insert(out.end(), f, f + 4);
+                    ++i;
+                    continue;
+                }
+                const int s1 = bv_simple_index(op), s2 = bv_simple_index(op2);
+                const uint32_t w1 = (p[0] >> 8) & 0x1ffu;
+                if (acc2 && s1 >= 0 && s2 >= 0 && w1 == 256u && w2 == 256u && bin2) {
+                    const uint32_t f[4] = {BV_BIN2 | (256u << 8) | keep2 | ((uint32_t)s1 << 22) | ((uint32_t)s2 << 26),
+                                           p[1], p[2], q[2]};
                     out.insert(out.end(), f, f + 4);
                     ++i;
                     continue;
@@ -817,7 +858,8 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     const uint32_t *insns = dags->insns, *prog_off = dags->prog_off;
     uint32_t total_up = total;
     if (!s.pair && !(fv && fv[0] == '0')) {
-        bv_fuse(dags, s.h_insns, s.h_off);
+        // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes
+        bv_fuse(dags, s.h_insns, s.h_off, !(fv && fv[0] == '1'));
         insns = s.h_insns.data();
         prog_off = s.h_off.data();
         total_up = s.h_off[n];

@@ -24,9 +24,11 @@ def child():
     dev = GpuDevice(0)
     out = {}
     for mode in os.environ.get("AB_K2_MODES", "lds,scalar").split(","):
-        # "<fetch>-nofuse": the same fetch with the programs uploaded unfused
-        os.environ["MG_BV_PROG"] = mode.removesuffix("-nofuse")
-        os.environ["MG_BV_FUSE"] = "0" if mode.endswith("-nofuse") else "1"
+        # "<fetch>-fuse<k>": the same fetch with MG_BV_FUSE=k (0: programs uploaded
+        # unfused, 1: two fused shapes, 2: all, the default)
+        fetch, _, fuse = mode.partition("-fuse")
+        os.environ["MG_BV_PROG"] = fetch
+        os.environ["MG_BV_FUSE"] = fuse or "2"
         dev.eval_upload(prog, models)
         dev.eval_run()
         ms = min(dev.eval_run() for _ in range(3))

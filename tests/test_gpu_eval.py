@@ -191,7 +191,14 @@ def _fusable_programs(n_dags, seed):
         prog = [[w0("copy", 256, 0), var(rng.randrange(3)), 0, 0]]          # slot 0: a variable
         prog.append([w0("extract", 1, 1), var(rng.randrange(3)), rng.randrange(256), 0])  # slot 1: a bit
         for _ in range(rng.randrange(2, 6)):
-            if rng.random() < 0.6:
+            if rng.random() < 0.3:
+                # a chain of 256-bit binary ops over variables, constants and slot 0
+                simple = ["bvadd", "bvsub", "bvmul", "bvand", "bvor", "bvxor", "bvumax", "bvumin", "bvrsub"]
+                for k in range(rng.randrange(2, 6)):
+                    a = var(rng.randrange(3)) if k == 0 else 0
+                    prog.append([w0(rng.choice(simple), 256, 0 if rng.random() < 0.15 else None), a,
+                                 rng.choice([var(rng.randrange(3)), const(rng.randrange(2)), slot(0)]), 0])
+            elif rng.random() < 0.6:
                 # two sw-bit operands (slot 2 and the accumulator), compared, and-ed with slot 1
                 k = rng.choice(cmps)
                 sw = rng.choice([1, 7, 8, 64, 128, 255, 256])
@@ -220,8 +227,8 @@ def _fusable_programs(n_dags, seed):
 
 
 def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
-    """Superinstructions (MG_BV_FUSE, on by default): on programs dense in the
-    fused shapes, and on C4's own, per-model bitmaps equal the unfused upload's and
+    """Superinstructions (MG_BV_FUSE, all three shapes by default): on programs
+    dense in the fused shapes, and on C4's own, per-model bitmaps equal the unfused upload's and
     first/count equal the oracle, which always interprets the unfused program."""
     mr = random.Random(9)
     specials = [0, 1, (1 << 255), (1 << 256) - 1, (1 << 127), (1 << 63) - 1]
@@ -231,11 +238,11 @@ def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
                        (synth.c4_programs(synth.Draws(500, seed=synth.C4_SEED + 29)), synth.c4_models(300, seed=31))):
         pool = pool or ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
         out = {}
-        for fuse in ("1", "0"):
+        for fuse in ("2", "1", "0"):         # all shapes (the default), two shapes, none
             monkeypatch.setenv("MG_BV_FUSE", fuse)
             out[fuse] = dev.eval_bits(prog, pool)
         for k in range(3):
-            assert np.array_equal(out["1"][k], out["0"][k])
+            assert np.array_equal(out["2"][k], out["0"][k]) and np.array_equal(out["1"][k], out["0"][k])
         rfs, rsc = eval_batch(prog, pool)
-        assert np.array_equal(out["1"][0], rfs) and np.array_equal(out["1"][1], rsc)
-        assert 0 < int(out["1"][1].sum()) < prog.n_dags * pool.n_models
+        assert np.array_equal(out["2"][0], rfs) and np.array_equal(out["2"][1], rsc)
+        assert 0 < int(out["2"][1].sum()) < prog.n_dags * pool.n_models
