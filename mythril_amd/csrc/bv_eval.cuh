@@ -60,6 +60,8 @@ enum BvOp : uint32_t {
     BV_EXT_RCAT,                // rconcat(extract(A, lo, ew), B): w3 = shift | lo << 9 | ew << 17
     BV_BIN2,                    // op2(op1(A, B), C) for two 256-bit ops of bv_simple: w0 bits
                                 // 22..25 = op1, 26..29 = op2 (bv_simple indices); C = op2's B
+    BV_BINX,                    // a chain of 3 or 4 such ops, two instruction slots: w0 bits
+                                // 22..24 = the count, A, B1, B2; then {kinds 4 bits each, B3, B4, 0}
     BV_NUM_INTERNAL
 };
 
@@ -479,6 +481,27 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     r = bv_simple((w0 >> 26) & 0xfu, t, C);
                     break;
                 }
+                case BV_BINX: {
+                    uint32_t e0, e1, e2;
+                    if (kLdsProg) {
+                        const uint4 x = prog[p + 1];
+                        e0 = uni(x.x); e1 = uni(x.y); e2 = uni(x.z);
+                    } else {
+                        const uint4 x = insns[i0 + uni(p + 1u)];
+                        e0 = x.x; e1 = x.y; e2 = x.z;
+                    }
+                    ++p;                                     // the extension slot
+                    const uint32_t k = (w0 >> 22) & 0x7u;
+                    U256 t = bv_simple(e0 & 0xfu, A, B);
+#pragma unroll 1
+                    for (uint32_t j = 1; j < k; ++j) {
+                        const uint32_t ref = j == 1u ? rc : j == 2u ? e1 : e2;
+                        const U256 C = bv_fetch(c, ref);
+                        t = bv_simple((e0 >> (4u * j)) & 0xfu, t, C);
+                    }
+                    r = t;
+                    break;
+                }
                 case BV_EXT_RCAT: {
                     const uint32_t ew = (rc >> 17) & 0x1ffu;
                     U256 lo = u_shr_u(A, (rc >> 9) & 0xffu, 0u);
@@ -751,8 +774,9 @@ static void bv_free(BvState &s) {
 // result is not stored into the next one when that one reads it as its
 // accumulator and the pair is one of the flattener's common shapes (of C4's
 // instructions, 10 % are a comparison feeding a Boolean and, 17 % a 256-bit
-// add/sub/mul/and/or/xor/umax/umin/rsub feeding another, 3 % a 128-bit extract
-// feeding an rconcat; MG_BV_FUSE=1 leaves out the second shape, =0 all three).  The fused program computes the same value bit for bit
+// add/sub/mul/and/or/xor/umax/umin/rsub feeding another (chains of 3 or 4 in one
+// two-slot BV_BINX), 3 % a 128-bit extract feeding an rconcat; MG_BV_FUSE=2 stops
+// at pairs, =1 leaves out the binary-op shape, =0 all of them).  The fused program computes the same value bit for bit
 // (tests/test_gpu_eval.py checks every program against the oracle, which runs
 // the unfused program); it only saves a dispatch and the widening of the
 // intermediate to a 256-bit accumulator.
@@ -762,7 +786,7 @@ static int bv_simple_index(uint32_t op) {
     return -1;
 }
 static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off,
-                    bool bin2) {
+                    bool bin2, bool binx) {
     const uint32_t n = dags->n_dags;
     out.clear();
     out.reserve((size_t)dags->prog_off[n] * 4);
@@ -789,6 +813,25 @@ static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::v
                 const int s1 = bv_simple_index(op), s2 = bv_simple_index(op2);
                 const uint32_t w1 = (p[0] >> 8) & 0x1ffu;
                 if (acc2 && s1 >= 0 && s2 >= 0 && w1 == 256u && w2 == 256u && bin2) {
+                    // the longest chain (up to 4) of such ops, each feeding the next's
+                    // accumulator unstored
+                    uint32_t L = 2, kinds = (uint32_t)s1 | ((uint32_t)s2 << 4);
+                    while (binx && L < 4 && i + L < b && ((dags->insns[4 * (size_t)(i + L - 1)] >> 17) & 1u) == 0u) {
+                        const uint32_t *x = dags->insns + 4 * (size_t)(i + L);
+                        const int sx = bv_simple_index(x[0] & 0xffu);
+                        if (sx < 0 || ((x[0] >> 8) & 0x1ffu) != 256u || (x[1] >> 30) != BV_REF_ACC) break;
+                        kinds |= (uint32_t)sx << (4 * L);
+                        ++L;
+                    }
+                    if (L > 2) {
+                        const uint32_t *last = dags->insns + 4 * (size_t)(i + L - 1);
+                        const uint32_t f[8] = {BV_BINX | (256u << 8) | (last[0] & (0x1fu << 17)) | (L << 22),
+                                               p[1], p[2], q[2],
+                                               kinds, p[10], L > 3 ? p[14] : 0u, 0u};
+                        out.insert(out.end(), f, f + 8);
+                        i += L - 1;
+                        continue;
+                    }
                     const uint32_t f[4] = {BV_BIN2 | (256u << 8) | keep2 | ((uint32_t)s1 << 22) | ((uint32_t)s2 << 26),
                                            p[1], p[2], q[2]};
                     out.insert(out.end(), f, f + 4);
@@ -859,7 +902,7 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     uint32_t total_up = total;
     if (!s.pair && !(fv && fv[0] == '0')) {
         // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes
-        bv_fuse(dags, s.h_insns, s.h_off, !(fv && fv[0] == '1'));
+        bv_fuse(dags, s.h_insns, s.h_off, !(fv && fv[0] == '1'), !(fv && (fv[0] == '1' || fv[0] == '2')));
         insns = s.h_insns.data();
         prog_off = s.h_off.data();
         total_up = s.h_off[n];

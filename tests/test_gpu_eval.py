@@ -227,7 +227,7 @@ def _fusable_programs(n_dags, seed):
 
 
 def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
-    """Superinstructions (MG_BV_FUSE, all three shapes by default): on programs
+    """Superinstructions (MG_BV_FUSE, all shapes and chains by default): on programs
     dense in the fused shapes, and on C4's own, per-model bitmaps equal the unfused upload's and
     first/count equal the oracle, which always interprets the unfused program."""
     mr = random.Random(9)
@@ -238,11 +238,13 @@ def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
                        (synth.c4_programs(synth.Draws(500, seed=synth.C4_SEED + 29)), synth.c4_models(300, seed=31))):
         pool = pool or ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
         out = {}
-        for fuse in ("2", "1", "0"):         # all shapes (the default), two shapes, none
+        # all shapes (the default), pairs only, no binary-op shape, none
+        for fuse in ("3", "2", "1", "0"):
             monkeypatch.setenv("MG_BV_FUSE", fuse)
             out[fuse] = dev.eval_bits(prog, pool)
         for k in range(3):
-            assert np.array_equal(out["2"][k], out["0"][k]) and np.array_equal(out["1"][k], out["0"][k])
+            for fuse in ("3", "2", "1"):
+                assert np.array_equal(out[fuse][k], out["0"][k]), fuse
         rfs, rsc = eval_batch(prog, pool)
-        assert np.array_equal(out["2"][0], rfs) and np.array_equal(out["2"][1], rsc)
-        assert 0 < int(out["2"][1].sum()) < prog.n_dags * pool.n_models
+        assert np.array_equal(out["3"][0], rfs) and np.array_equal(out["3"][1], rsc)
+        assert 0 < int(out["3"][1].sum()) < prog.n_dags * pool.n_models
