@@ -513,6 +513,26 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
             }
             }
+            if (w0 >> 31) {
+                // fused tail (bv_fuse): 1-3 bv_simple ops applied to this 256-bit
+                // result, from an extension slot {kinds | count << 28, B1, B2, B3}
+                uint32_t e0, e1, e2, e3;
+                if (kLdsProg) {
+                    const uint4 x = prog[p + 1];
+                    e0 = uni(x.x); e1 = uni(x.y); e2 = uni(x.z); e3 = uni(x.w);
+                } else {
+                    const uint4 x = insns[i0 + uni(p + 1u)];
+                    e0 = x.x; e1 = x.y; e2 = x.z; e3 = x.w;
+                }
+                ++p;
+                const uint32_t k = e0 >> 28;
+#pragma unroll 1
+                for (uint32_t j = 0; j < k; ++j) {
+                    const uint32_t ref = j == 0u ? e1 : j == 1u ? e2 : e3;
+                    const U256 C = bv_fetch(c, ref);
+                    r = bv_simple((e0 >> (4u * j)) & 0xfu, r, C);
+                }
+            }
             if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);   // uniform
             acc = r;
             if ((w0 >> 17) & 1u) {
@@ -775,8 +795,8 @@ static void bv_free(BvState &s) {
 // accumulator and the pair is one of the flattener's common shapes (of C4's
 // instructions, 10 % are a comparison feeding a Boolean and, 17 % a 256-bit
 // add/sub/mul/and/or/xor/umax/umin/rsub feeding another (chains of 3 or 4 in one
-// two-slot BV_BINX), 3 % a 128-bit extract feeding an rconcat; MG_BV_FUSE=2 stops
-// at pairs, =1 leaves out the binary-op shape, =0 all of them).  The fused program computes the same value bit for bit
+// two-slot BV_BINX), 3 % a 128-bit extract feeding an rconcat; any other 256-bit
+// op feeding 1-3 such binary ops takes them as a tail in an extension slot).  The fused program computes the same value bit for bit
 // (tests/test_gpu_eval.py checks every program against the oracle, which runs
 // the unfused program); it only saves a dispatch and the widening of the
 // intermediate to a 256-bit accumulator.
@@ -786,7 +806,7 @@ static int bv_simple_index(uint32_t op) {
     return -1;
 }
 static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off,
-                    bool bin2, bool binx) {
+                    bool bin2, bool binx, bool tail) {
     const uint32_t n = dags->n_dags;
     out.clear();
     out.reserve((size_t)dags->prog_off[n] * 4);
@@ -838,6 +858,25 @@ static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::v
                     ++i;
                     continue;
                 }
+                if (acc2 && tail && s1 < 0 && op < BV_NUM_OPS && w1 == 256u && s2 >= 0 && w2 == 256u) {
+                    // any other 256-bit op whose result feeds 1-3 bv_simple ops: the
+                    // op keeps its own encoding, w0 bit 31 marks an extension slot
+                    uint32_t L = 1, kinds = (uint32_t)s2;
+                    while (L < 3 && i + L + 1 < b && ((dags->insns[4 * (size_t)(i + L)] >> 17) & 1u) == 0u) {
+                        const uint32_t *x = dags->insns + 4 * (size_t)(i + L + 1);
+                        const int sx = bv_simple_index(x[0] & 0xffu);
+                        if (sx < 0 || ((x[0] >> 8) & 0x1ffu) != 256u || (x[1] >> 30) != BV_REF_ACC) break;
+                        kinds |= (uint32_t)sx << (4 * L);
+                        ++L;
+                    }
+                    const uint32_t *last = dags->insns + 4 * (size_t)(i + L);
+                    const uint32_t f[8] = {(p[0] & ~(0x1fu << 17)) | (last[0] & (0x1fu << 17)) | (1u << 31),
+                                           p[1], p[2], p[3],
+                                           kinds | (L << 28), q[2], L > 1 ? p[10] : 0u, L > 2 ? p[14] : 0u};
+                    out.insert(out.end(), f, f + 8);
+                    i += L;
+                    continue;
+                }
                 if (acc2 && op == BV_EXTRACT && op2 == BV_RCONCAT && q[3] < 512u) {
                     const uint32_t ew = (p[0] >> 8) & 0x1ffu;
                     const uint32_t f[4] = {BV_EXT_RCAT | (w2 << 8) | keep2, p[1], q[2],
@@ -868,7 +907,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     for (uint32_t i = 0; i < total; ++i) {
         const uint32_t *w = dags->insns + 4 * (size_t)i;
         const uint32_t op = w[0] & 0xffu, width = (w[0] >> 8) & 0x1ffu;
-        if (op >= BV_NUM_OPS || width == 0 || width > 256) { msg = "bad instruction " + std::to_string(i); return MG_EINVAL; }
+        if (op >= BV_NUM_OPS || width == 0 || width > 256 || (w[0] >> 22) != 0u) {
+            msg = "bad instruction " + std::to_string(i);   // bits 22..31 are the fused forms'
+            return MG_EINVAL;
+        }
         if (((w[0] >> 17) & 1u) && ((w[0] >> 18) & 0xfu) >= dags->n_slots) { msg = "slot out of range"; return MG_EINVAL; }
         if (op == BV_TAB) {
             const uint32_t imm = w[3], t = imm & 0xfffffu, lo = (imm >> 21) & 0xffu;
@@ -901,8 +943,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     const uint32_t *insns = dags->insns, *prog_off = dags->prog_off;
     uint32_t total_up = total;
     if (!s.pair && !(fv && fv[0] == '0')) {
-        // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes
-        bv_fuse(dags, s.h_insns, s.h_off, !(fv && fv[0] == '1'), !(fv && (fv[0] == '1' || fv[0] == '2')));
+        // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes, 2: and
+        // binary-op pairs, 3: and their chains, unset (4): and fused tails
+        const char lvl = fv && fv[0] >= '1' && fv[0] <= '3' ? fv[0] : '4';
+        bv_fuse(dags, s.h_insns, s.h_off, lvl >= '2', lvl >= '3', lvl >= '4');
         insns = s.h_insns.data();
         prog_off = s.h_off.data();
         total_up = s.h_off[n];
