@@ -451,7 +451,10 @@ int         mg_event_counts(mg_ctx *ctx, uint32_t *sha3_count, uint32_t *exp_cou
  * refs (kind << 30 | index; kind 0 = the accumulator, 1 slot, 2 variable,
  * 3 constant) or immediates.  Since ABI 8 only operand A may be the
  * accumulator (the flattener swaps / reverses / spills): a program with the
- * accumulator in operand B or C is refused with MG_EINVAL.                   */
+ * accumulator in operand B or C is refused with MG_EINVAL, and so is one
+ * with any of bits 22..31 of the first word set (the library's own fused
+ * forms use them: it rewrites common instruction pairs and chains into
+ * superinstructions at upload, bit-identical results; MG_BV_FUSE=0 disables). */
 typedef struct mg_dag_batch {
     uint32_t n_dags;
     uint32_t n_slots;       /* register slots a program may use (<= 16)       */
