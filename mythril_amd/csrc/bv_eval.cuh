@@ -513,9 +513,12 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
             }
             }
-            if (w0 >> 31) {
-                // fused tail (bv_fuse): 1-3 bv_simple ops applied to this 256-bit
-                // result, from an extension slot {kinds | count << 28, B1, B2, B3}
+            const bool tail = (w0 >> 31) != 0u;
+            if (tail) {
+                // fused tail (bv_fuse): 1-3 bv_simple ops applied to this result
+                // (masked to its own width first), from an extension slot
+                // {kinds | count << 28, B1, B2, B3}
+                if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);
                 uint32_t e0, e1, e2, e3;
                 if (kLdsProg) {
                     const uint4 x = prog[p + 1];
@@ -533,7 +536,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     r = bv_simple((e0 >> (4u * j)) & 0xfu, r, C);
                 }
             }
-            if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);   // uniform
+            // uniform; a tail's ops are 256-bit
+            if (!tail && width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);
             acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;
@@ -806,7 +810,7 @@ static int bv_simple_index(uint32_t op) {
     return -1;
 }
 static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::vector<uint32_t> &off,
-                    bool bin2, bool binx, bool tail) {
+                    bool bin2, bool binx, bool tail, bool narrow_tail) {
     const uint32_t n = dags->n_dags;
     out.clear();
     out.reserve((size_t)dags->prog_off[n] * 4);
@@ -858,8 +862,9 @@ static void bv_fuse(const mg_dag_batch *dags, std::vector<uint32_t> &out, std::v
                     ++i;
                     continue;
                 }
-                if (acc2 && tail && s1 < 0 && op < BV_NUM_OPS && w1 == 256u && s2 >= 0 && w2 == 256u) {
-                    // any other 256-bit op whose result feeds 1-3 bv_simple ops: the
+                if (acc2 && tail && (s1 < 0 || w1 != 256u) && (w1 == 256u || narrow_tail) && op < BV_NUM_OPS &&
+                    s2 >= 0 && w2 == 256u) {
+                    // any other op whose result feeds 1-3 256-bit bv_simple ops: the
                     // op keeps its own encoding, w0 bit 31 marks an extension slot
                     uint32_t L = 1, kinds = (uint32_t)s2;
                     while (L < 3 && i + L + 1 < b && ((dags->insns[4 * (size_t)(i + L)] >> 17) & 1u) == 0u) {
@@ -945,8 +950,8 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     if (!s.pair && !(fv && fv[0] == '0')) {
         // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes, 2: and
         // binary-op pairs, 3: and their chains, unset (4): and fused tails
-        const char lvl = fv && fv[0] >= '1' && fv[0] <= '3' ? fv[0] : '4';
-        bv_fuse(dags, s.h_insns, s.h_off, lvl >= '2', lvl >= '3', lvl >= '4');
+        const char lvl = fv && fv[0] >= '1' && fv[0] <= '4' ? fv[0] : '5';
+        bv_fuse(dags, s.h_insns, s.h_off, lvl >= '2', lvl >= '3', lvl >= '4', lvl >= '5');
         insns = s.h_insns.data();
         prog_off = s.h_off.data();
         total_up = s.h_off[n];

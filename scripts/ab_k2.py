@@ -25,10 +25,11 @@ def child():
     out = {}
     for mode in os.environ.get("AB_K2_MODES", "lds,scalar").split(","):
         # "<fetch>-fuse<k>": the same fetch with MG_BV_FUSE=k (0: programs uploaded
-        # unfused, 1: no binary-op shape, 2: pairs only, 3: no tails, 4: all, the default)
+        # unfused, 1: no binary-op shape, 2: pairs only, 3: no tails, 4: wide tails only,
+        # 5: all, the default)
         fetch, _, fuse = mode.partition("-fuse")
         os.environ["MG_BV_PROG"] = fetch
-        os.environ["MG_BV_FUSE"] = fuse or "4"
+        os.environ["MG_BV_FUSE"] = fuse or "5"
         dev.eval_upload(prog, models)
         dev.eval_run()
         ms = min(dev.eval_run() for _ in range(3))

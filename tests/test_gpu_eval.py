@@ -199,6 +199,9 @@ def _fusable_programs(n_dags, seed):
                 for k in range(rng.randrange(2, 6)):
                     a = var(rng.randrange(3)) if k == 0 else 0
                     op = rng.choice(heads) if k == 0 and rng.random() < 0.5 else rng.choice(simple)
+                    if k == 0 and rng.random() < 0.2:      # a narrower head: a 128-bit extract
+                        prog.append([w0("extract", 128), a, rng.randrange(129), 0])
+                        continue
                     prog.append([w0(op, 256, 0 if rng.random() < 0.15 else None), a,
                                  rng.choice([var(rng.randrange(3)), const(rng.randrange(2)), slot(0)]), 0])
             elif rng.random() < 0.6:
@@ -241,13 +244,14 @@ def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
                        (synth.c4_programs(synth.Draws(500, seed=synth.C4_SEED + 29)), synth.c4_models(300, seed=31))):
         pool = pool or ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
         out = {}
-        # all shapes (the default), no tails, pairs only, no binary-op shape, none
-        for fuse in ("4", "3", "2", "1", "0"):
+        # all shapes (the default), wide tails only, no tails, pairs only, no binary-op
+        # shape, none
+        for fuse in ("5", "4", "3", "2", "1", "0"):
             monkeypatch.setenv("MG_BV_FUSE", fuse)
             out[fuse] = dev.eval_bits(prog, pool)
         for k in range(3):
-            for fuse in ("4", "3", "2", "1"):
+            for fuse in ("5", "4", "3", "2", "1"):
                 assert np.array_equal(out[fuse][k], out["0"][k]), fuse
         rfs, rsc = eval_batch(prog, pool)
-        assert np.array_equal(out["4"][0], rfs) and np.array_equal(out["4"][1], rsc)
-        assert 0 < int(out["4"][1].sum()) < prog.n_dags * pool.n_models
+        assert np.array_equal(out["5"][0], rfs) and np.array_equal(out["5"][1], rsc)
+        assert 0 < int(out["5"][1].sum()) < prog.n_dags * pool.n_models
