@@ -695,10 +695,12 @@ static uint32_t max_of(const uint32_t *v, uint32_t n) {
 
 static int ensure_hxfer(mg_ctx *ctx, size_t bytes) {
     if (bytes <= ctx->h_xfer_bytes) return MG_OK;
+    // geometric growth: a slowly growing transfer reallocates pinned memory
+    // (milliseconds per hipHostFree + hipHostMalloc) only O(log n) times
+    const size_t cap = std::max<size_t>(bytes, 2 * ctx->h_xfer_bytes + (1u << 20));
     if (ctx->h_xfer) hipHostFree(ctx->h_xfer);
     ctx->h_xfer = nullptr;
     ctx->h_xfer_bytes = 0;
-    const size_t cap = std::max<size_t>(bytes, 2 * ctx->h_xfer_bytes + (1u << 20));
     if (hipHostMalloc((void **)&ctx->h_xfer, cap, hipHostMallocDefault) != hipSuccess)
         return set_err(ctx, MG_ENOMEM, "hipHostMalloc transfer buffer %zu", cap);
     ctx->h_xfer_bytes = cap;

@@ -85,6 +85,7 @@ _ACK_SAFE: Dict[str, int] = {
     **{f"SWAP{k}": k + 1 for k in range(1, 17)},
 }
 
+_EXEC_DEPTH = 0         # nesting of LaserEVM.exec drains (the outermost resets the lane term table)
 _MERGE_GAP = 256        # lanes: transfer ranges closer than this merge into one copy
 _EXECUTED_HALTS = (MG_HALT_STOP, MG_HALT_RETURN, MG_HALT_REVERT, MG_VMEXC, MG_HALT_DROPPED)
 _INF = float("inf")
@@ -105,6 +106,16 @@ class LaserEVM:
     """The LASER engine with kernel 1 stepping every path of the work list."""
 
     _fast_hooks = True      # plain lanes' pre-hook events take _deliver_plain_hook
+    # The reference's evaluate() steps a copy of every hooked state
+    # (instructions.py:121-130).  The batched core copies only when a hook kept
+    # a reference to the state or to a part the lane changes in place (_held:
+    # the state, machine state, stack, memory, world state, constraint and
+    # annotation lists, environment, active account, storage, transaction
+    # stack, annotations).  Contract for hooks: keep what you need by
+    # reference to one of those objects (or copy it); a hook that swaps one
+    # kept reference for another of the same objects, or keeps an inner word
+    # it later mutates in place, must run with always_copy_hooked = True.
+    always_copy_hooked = False
 
     def __init__(self, dynamic_loader=None, max_depth=float("inf"), execution_timeout=60,
                  create_timeout=10, strategy=DepthFirstSearchStrategy, transaction_count=2,
@@ -241,9 +252,14 @@ class LaserEVM:
         frozen = gc.get_freeze_count() == 0      # nested or caller-frozen: leave it to them
         if frozen:
             gc.freeze()
+        global _EXEC_DEPTH
+        if _EXEC_DEPTH == 0:
+            sym.reset_terms()                    # no lane image outlives a drain
+        _EXEC_DEPTH += 1
         try:
             return self._exec(create, track_gas)
         finally:
+            _EXEC_DEPTH -= 1
             if frozen:
                 gc.unfreeze()
 
@@ -851,7 +867,7 @@ class LaserEVM:
             return
         for hook in self.instr_pre_hook.get(name, ()):
             hook(s)
-        if _held(s) != refs0:
+        if self.always_copy_hooked or _held(s) != refs0:
             s = copy(s)                    # a hook kept the state: the lane goes on with a copy
             ln.state = s
         pm, pe = pre_state.mstate, pre_state.environment
@@ -985,7 +1001,7 @@ class LaserEVM:
             # copy, instructions.py:121-130): the lane goes on with a copy -- unless
             # no hook kept a reference to the state or to any part of it the lane
             # changes later (_held), when nothing can observe the difference
-            if post or _held(pre_state) != refs0:
+            if post or self.always_copy_hooked or _held(pre_state) != refs0:
                 s = copy(s)
                 ln.state = s
             # hooks may have rewritten the state: repack, then run the hooked
@@ -1317,9 +1333,10 @@ def _held(s: GlobalState) -> Tuple[int, ...]:
     the hooks means no hook kept any of them."""
     ws, env = s.world_state, s.environment
     acct = env.active_account
+    ms = s.mstate
     rc = sys.getrefcount
-    out = (rc(s), rc(s.mstate), rc(ws), rc(ws.constraints), rc(ws._annotations), rc(env), rc(acct),
-           rc(acct.storage), rc(s.transaction_stack), rc(s._annotations))
+    out = (rc(s), rc(ms), rc(ms.stack), rc(ms.memory), rc(ws), rc(ws.constraints), rc(ws._annotations),
+           rc(env), rc(acct), rc(acct.storage), rc(s.transaction_stack), rc(s._annotations))
     if s._annotations:
         out += tuple(rc(a) for a in s._annotations)
     return out

@@ -465,8 +465,16 @@ class _Encoder:
 
 # Opaque terms of the host's expression layer carried by lanes (MG_SYM_TERM):
 # index -> term, interned by identity, so equal indices are the same term.
+# Lane images live only inside one LaserEVM.exec drain (states between drains
+# are host objects, re-encoded when packed), so the outermost exec() clears the
+# table when it starts: terms of finished transactions are not kept alive.
 _TERMS: List[object] = []
 _TERM_IDX: dict = {}
+
+
+def reset_terms() -> None:
+    _TERMS.clear()
+    _TERM_IDX.clear()
 
 
 def register_term(raw) -> int:

@@ -18,14 +18,20 @@ from .expr import And, BitVec, Bool, Function, URem, symbol_factory
 
 class ExponentFunctionManager:
     def __init__(self):
-        # concrete (base, exponent) -> power of every EXP registered so far (what
-        # a model must interpret Power as; laser/witness.py completes seeds with it)
-        self.concrete_points = {(256, i): 256 ** i for i in range(32)}
+        self.reset()
         power = Function("Power", [256, 256], 256)
         n256 = symbol_factory.BitVecVal(256, 256)
         self.concrete_constraints = And(*[
             power(n256, symbol_factory.BitVecVal(i, 256)) == symbol_factory.BitVecVal(256 ** i, 256)
             for i in range(0, 32)])
+
+    def reset(self) -> None:
+        """Forget the points registered by earlier runs (host bookkeeping only:
+        the reference's manager keeps no per-run state, so this changes no
+        constraint)."""
+        # concrete (base, exponent) -> power of every EXP registered so far (what
+        # a model must interpret Power as; laser/witness.py completes seeds with it)
+        self.concrete_points = {(256, i): 256 ** i for i in range(32)}
 
     def create_condition(self, base: BitVec, exponent: BitVec) -> Tuple[BitVec, Bool]:
         power = Function("Power", [256, 256], 256)

@@ -330,7 +330,7 @@ class ModelCache:
             if pre is None or not all(id(m) in pre[0] for m in models):
                 pre = self._eval_keys([key], self._full_pool(models), keep=False).get(key)
             if pre is not None:
-                pos, row = pre
+                pos, row = pre[0], pre[1]
                 for m in models:
                     p = pos[id(m)]
                     if (int(row[p >> 6]) >> (p & 63)) & 1:
@@ -396,6 +396,10 @@ class ModelCache:
         pos = {}
         for i, m in enumerate(pool):
             pos.setdefault(id(m), i)
+        # the bitmaps place models by id(): the entry keeps its pool's models
+        # alive, so no model created later (after an LRU eviction frees one)
+        # can take a dead model's id and read its bit
+        alive = tuple(pool)
         for k in keys:
             acc = ones.copy()
             ok = True
@@ -410,7 +414,7 @@ class ModelCache:
                     break
                 acc &= r
             if ok:
-                out[k] = (pos, acc)
+                out[k] = (pos, acc, alive)
                 self.device_evals += len(pool)
         if keep:
             self._bits.update(out)
@@ -461,7 +465,7 @@ class ModelCache:
             pre = self._eval_keys([key], seeds, keep=False).get(key)
         found = None
         if pre is not None:
-            pos, row = pre
+            pos, row = pre[0], pre[1]
             for m in seeds:
                 p = pos[id(m)]
                 if (int(row[p >> 6]) >> (p & 63)) & 1:

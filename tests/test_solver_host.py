@@ -157,3 +157,34 @@ def test_keccak_conjunct_compiles_and_matches_python():
         vals = [evaluate(And(*s_).raw, m) for m in models]
         assert (next((i for i, v in enumerate(vals) if v), 0xFFFFFFFF), sum(vals)) == (fs[d], sc[d])
     assert 0 < sc[0] < len(models)
+
+
+def test_prefetched_bitmaps_survive_an_lru_eviction(monkeypatch):
+    """a prefetch window's bitmaps place models by id().  When
+    a backend miss inside the window evicts the LRU's oldest model, a model
+    created afterwards must not inherit the dead model's bit: the entry keeps its
+    pool alive, so the evicted model's id stays taken and quick-sat answers
+    exactly as without the prefetch."""
+    import gc
+    import weakref
+    from oracle_device import OracleK2
+    mc = ModelCache(device=OracleK2())
+    monkeypatch.setattr(solver, "model_cache", mc)
+    x = BVS("x", 256)
+    olds = [Model({"x": v}) for v in range(100)]
+    for m in olds:
+        mc.put(m, 1)
+    key = ULT(x, BVV(1, 256)).raw                 # only x == 0 (the LRU's oldest) satisfies it
+    mc.prefetch([key])
+    oldest = weakref.ref(olds[0])
+    del olds, m
+    mc.put(Model({"x": 500}), 1)                  # a backend miss in the window evicts x == 0
+    gc.collect()
+    assert oldest() is not None                   # held by the prefetched entry, id not reusable
+    fresh_models = [Model({"x": 1000 + k}) for k in range(200)]
+    for fm in fresh_models[:99]:
+        mc.put(fm, 1)
+    assert mc.check_quick_sat(key) is False       # no model in the LRU satisfies x < 1
+    mc.clear_prefetch()
+    gc.collect()
+    assert oldest() is None                       # released with the window
