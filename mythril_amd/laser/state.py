@@ -537,7 +537,12 @@ class Storage:
 
 
 class Account:
-    """account.py:102-228 (concrete)."""
+    """account.py:102-228.  The balance is ``balances[address]`` over the world
+    state's symbolic ``Array("balance")`` (world_state.py:31-33), as in the
+    reference: concrete balances are stores into it, so a path's balance
+    arithmetic and the ``UGE(balances[sender], value)`` conjunct of every
+    transaction are the reference's terms.  An account not yet put into a world
+    state keeps a balance set on it and hands it over on put_account."""
 
     def __init__(self, address, code: Optional[Disassembly] = None, contract_name: str = None,
                  balances=None, concrete_storage: bool = True, dynamic_loader=None, nonce: int = 0):
@@ -545,32 +550,54 @@ class Account:
             address, BitVec) else address
         self.nonce = nonce
         self.code = code or Disassembly("")
+        if contract_name is None:
+            # account.py:139-146
+            contract_name = ("{0:#0{1}x}".format(self.address.value, 42) if self.address.value is not None
+                             else "unknown")
         self.contract_name = contract_name
+        self.concrete_storage = concrete_storage
         self.storage = Storage(concrete_storage, address=self.address)
-        self._balance = 0
-
-    def set_balance(self, balance) -> None:
-        self._balance = concrete(balance)
-
-    def add_balance(self, balance) -> None:
-        self._balance = (self._balance + concrete(balance)) & M256
+        self.deleted = False
+        self._balances = balances
+        self._pending_balance = None
 
     def balance(self) -> BitVec:
-        return symbol_factory.BitVecVal(self._balance, 256)
+        if self._balances is None:
+            return symbol_factory.BitVecVal(concrete(self._pending_balance or 0), 256)
+        return self._balances[self.address]
+
+    def set_balance(self, balance) -> None:
+        balance = balance if isinstance(balance, BitVec) else symbol_factory.BitVecVal(concrete(balance), 256)
+        if self._balances is None:
+            self._pending_balance = balance
+            return
+        self._balances[self.address] = balance
+
+    def add_balance(self, balance) -> None:
+        balance = balance if isinstance(balance, BitVec) else symbol_factory.BitVecVal(concrete(balance), 256)
+        if self._balances is None:
+            self._pending_balance = (self._pending_balance or symbol_factory.BitVecVal(0, 256)) + balance
+            return
+        self._balances[self.address] = self._balances[self.address] + balance
 
     def __copy__(self):
-        a = Account(self.address, self.code, self.contract_name, nonce=self.nonce)
+        a = Account(self.address, self.code, self.contract_name, balances=copy(self._balances),
+                    concrete_storage=self.concrete_storage, nonce=self.nonce)
         a.storage = copy(self.storage)
-        a._balance = self._balance
+        a.deleted = self.deleted
+        a._pending_balance = self._pending_balance
         return a
 
 
 class WorldState:
-    """world_state.py:18-242 (concrete accounts; constraints stay empty for
-    concrete paths)."""
+    """world_state.py:18-242: accounts, the symbolic ``balances`` array and its
+    ``starting_balances`` copy, path constraints, transaction sequence,
+    annotations."""
 
     def __init__(self, transaction_sequence=None, annotations=None, constraints=None):
         self._accounts: Dict[int, Account] = {}
+        self.balances = Array("balance", 256, 256)
+        self.starting_balances = copy(self.balances)
         self.constraints = list(constraints or [])
         self.transaction_sequence = list(transaction_sequence or [])
         self._annotations = list(annotations or [])
@@ -581,15 +608,33 @@ class WorldState:
         return self._accounts
 
     def put_account(self, account: Account) -> None:
+        """world_state.py:249-255 (an account's balance lives in this world
+        state's array from now on)."""
         self._accounts[concrete(account.address)] = account
+        pending = account._pending_balance if account._balances is None else None
+        account._balances = self.balances
+        account._pending_balance = None
+        if pending is not None:
+            account.set_balance(pending)
 
     def __getitem__(self, item) -> Account:
-        return self._accounts[concrete(item)]
+        """world_state.py:43-57: an unknown address gets a fresh account."""
+        key = concrete(item)
+        try:
+            return self._accounts[key]
+        except KeyError:
+            acct = Account(item if isinstance(item, BitVec) else key, balances=self.balances)
+            self._accounts[key] = acct
+            return acct
 
     def __copy__(self):
-        w = WorldState(self.transaction_sequence, self._annotations, self.constraints)
+        w = WorldState(self.transaction_sequence, [copy(a) for a in self._annotations], self.constraints)
+        w.balances = copy(self.balances)
+        w.starting_balances = copy(self.starting_balances)
         for k, a in self._accounts.items():
-            w._accounts[k] = copy(a)
+            c = copy(a)
+            c._balances = w.balances
+            w._accounts[k] = c
         w.node = self.node
         return w
 

@@ -5,8 +5,9 @@ Mirrors transaction/concolic.py:23-151 (``execute_contract_creation``,
 of transaction/transaction_models.py:21-284 those use (tx ids,
 MessageCallTransaction, ContractCreationTransaction, initial_global_state with the
 value transfer, the creation ``end`` that installs the returned runtime code).
-Balances are concrete here: the reference's ``UGE(balances[sender], value)``
-conjunct is a constant for concrete balances and is not recorded.
+Balances live in the world state's symbolic ``Array("balance")`` as in the
+reference: every transaction's initial state appends ``UGE(balances[sender],
+value)`` and moves the value (transaction_models.py:127-148).
 
 A creation transaction's calldata is the reference's ``SymbolicCalldata``
 (concolic.py:57-70 passes ``call_data=None``): its lanes carry
@@ -78,15 +79,7 @@ class MessageCallTransaction:
                           code=self.code or self.callee_account.code, static=self.static)
         gs = GlobalState(self.world_state, env, None)
         gs.environment.active_function_name = "fallback"
-        value = getattr(self.call_value, "value", self.call_value)
-        if value:      # a symbolic value moves no concrete balance (balances stay concrete here)
-            sender, receiver = concrete(env.sender), concrete(env.active_account.address)
-            ws = gs.world_state
-            if receiver in ws.accounts:
-                ws.accounts[receiver].add_balance(value)
-            if sender in ws.accounts:
-                ws.accounts[sender].add_balance(-value)
-        return gs
+        return _transfer_call_value(gs)
 
     def end(self, global_state: GlobalState, return_data=None, revert=False) -> None:
         self.return_data = return_data
@@ -95,6 +88,19 @@ class MessageCallTransaction:
     def __str__(self):
         return "{} {} from {} to {:#42x}".format(type(self).__name__, self.id, self.caller,
                                                  concrete(self.callee_account.address))
+
+
+def _transfer_call_value(gs: GlobalState) -> GlobalState:
+    """transaction_models.py:127-148 (initial_global_state_from_environment):
+    ``UGE(balances[sender], value)`` joins the path constraints, then the value
+    moves from the sender's balance to the receiver's."""
+    from ..smt.expr import UGE
+    env, ws = gs.environment, gs.world_state
+    value = env.callvalue
+    ws.constraints.append(UGE(ws.balances[env.sender], value))
+    ws.balances[env.active_account.address] = ws.balances[env.active_account.address] + value
+    ws.balances[env.sender] = ws.balances[env.sender] - value
+    return gs
 
 
 # transaction/symbolic.py:28-40 Actors
@@ -158,7 +164,15 @@ def execute_symbolic_contract_creation(laser_evm, contract_initialization_code, 
         origin=origin, code=code if isinstance(code, Disassembly) else Disassembly(code), caller=caller,
         contract_name=contract_name, call_data=SymbolicCalldata(txid),
         call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
-    _setup_global_state_for_execution(laser_evm, tx)
+    # transaction/symbolic.py:202-219 (its _setup_global_state_for_execution
+    # also pins the caller to the actors)
+    from ..smt.expr import Or
+    gs = tx.initial_global_state()
+    gs.transaction_stack.append((tx, None))
+    gs.world_state.constraints.append(
+        Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
+    gs.world_state.transaction_sequence.append(tx)
+    laser_evm.work_list.append(gs)
     new_account = tx.callee_account
     laser_evm.exec(True)
     return new_account
@@ -204,7 +218,8 @@ def create_account(world_state: WorldState, balance=0, address=None, concrete_st
         address = generate_contract_address(creator, accounts[creator].nonce)
     if creator:
         accounts[creator].nonce += 1
-    acct = Account(address, code=code, concrete_storage=concrete_storage, nonce=nonce)
+    acct = Account(address, code=code, concrete_storage=concrete_storage, nonce=nonce,
+                   balances=world_state.balances)
     acct.set_balance(balance)
     world_state.put_account(acct)
     return acct

@@ -297,11 +297,19 @@ ULT, UGT = _ucmp("bvult"), _ucmp("bvugt")
 
 
 def ULE(a, b) -> Bool:  # bitvec_helper.py:85-95
-    return Or(ULT(a, b), _bv(a) == _bv(b))
+    a = _bv(a)
+    b = _bv(b, a.size())
+    if a.raw.op == "const" and a.raw.param == 0:
+        return Bool(TRUE, _ann(a, b))        # z3 simplify: 0 <=u x is true
+    return Or(ULT(a, b), a == b)
 
 
 def UGE(a, b) -> Bool:  # bitvec_helper.py:97-105
-    return Or(UGT(a, b), _bv(a) == _bv(b))
+    a = _bv(a)
+    b = _bv(b, a.size())
+    if b.raw.op == "const" and b.raw.param == 0:
+        return Bool(TRUE, _ann(a, b))        # z3 simplify: x >=u 0 is true (a zero-value transfer)
+    return Or(UGT(a, b), a == b)
 
 
 def Concat(*args) -> BitVec:

@@ -179,6 +179,9 @@ def run_creation_both(device, name, monkeypatch):
     tx = _creation_tx(ws_ref, code, txid)
     gs = tx.initial_global_state()
     gs.transaction_stack.append((tx, None))
+    # transaction/symbolic.py:202-219: the caller is one of the actors
+    gs.world_state.constraints.append(
+        Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
     ref_engine.run([gs])
 
     def ends(c):

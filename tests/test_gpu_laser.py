@@ -456,7 +456,7 @@ def test_transaction_rounds_device_equal_oracle_device(dev):
         execute_message_calls(vm, ts.CALLEE, ts.ATTACKER, ts.ATTACKER, ts.DATAS,
                               gas_limit=8_000_000, gas_price=0, value=0)
         ids.extend(s.transaction_sequence[-1].id for s in vm.open_states)
-    prints = sorted((tuple(sorted(s[ts.CALLEE].storage.items())), int(s[ts.CALLEE].balance().value))
+    prints = sorted((tuple(sorted(s[ts.CALLEE].storage.items())), str(s[ts.CALLEE].balance().raw))
                     for s in vm.open_states)
     table = {k: list(v[1]) for k, v in vm.coverage().items()}
     ref = ts._rounds()

@@ -50,14 +50,30 @@ def _rounds():
     from mythril_amd.laser import (Account, Disassembly, InstructionCoveragePlugin, LaserEVM,
                                    WorldState, tx_id_manager)
     from mythril_amd.laser.sharded import execute_message_calls
-    from oracle_device import OracleDevice
+    from mythril_amd.smt import solver
+    from oracle_device import OracleDevice, OracleK2
 
+    # the reachability filter's queries (each round's transaction appends its
+    # UGE(balances[sender], value) conjunct) run on the oracle's kernel 2
+    saved = solver.model_cache
+    solver.model_cache = solver.ModelCache(device=OracleK2())
+    solver.get_model.cache_clear()
+    try:
+        return _rounds_body(execute_message_calls, OracleDevice())
+    finally:
+        solver.model_cache = saved
+        solver.get_model.cache_clear()
+
+
+def _rounds_body(execute_message_calls, device):
+    from mythril_amd.laser import (Account, Disassembly, InstructionCoveragePlugin, LaserEVM,
+                                   WorldState, tx_id_manager)
     tx_id_manager.restart_counter()
     ws = WorldState()
     acct = Account(CALLEE, concrete_storage=True)
     acct.code = Disassembly(workloads.bytecode("overflow.sol.o").hex())
     ws.put_account(acct)
-    vm = LaserEVM(device=OracleDevice())
+    vm = LaserEVM(device=device)
     cov = InstructionCoveragePlugin()
     cov.initialize(vm)
     vm.open_states = [ws]
@@ -67,7 +83,7 @@ def _rounds():
                               gas_price=0, value=0)
         for s in vm.open_states:
             ids.append(s.transaction_sequence[-1].id)
-    prints = sorted((tuple(sorted(s[CALLEE].storage.items())), int(s[CALLEE].balance().value))
+    prints = sorted((tuple(sorted(s[CALLEE].storage.items())), str(s[CALLEE].balance().raw))
                     for s in vm.open_states)
     table = {k: list(v[1]) for k, v in vm.coverage().items()}
     return prints, table, tx_id_manager._next_transaction_id, ids, vm.lane_steps
