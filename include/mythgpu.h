@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 9u   /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 10u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -39,7 +39,9 @@ extern "C" {
                                   through one pinned DMA per phase; symbolic
                                   calldata copies (MG_SYM_CDBYTE) and a creation's
                                   calldata opcodes (MG_REC_CDSIZE) on symbolic lanes;
-                                  symbolic EXP (MG_SYM_BIN 0x0a, MG_REC_SYMEXP) */
+                                  symbolic EXP (MG_SYM_BIN 0x0a, MG_REC_SYMEXP)
+                              10: MG_LANE_RETDATA (a host CALL left return data:
+                                  RETURNDATASIZE / RETURNDATACOPY escape) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -149,6 +151,11 @@ extern "C" {
                                  Array("Storage{address}") (account.py:26-29), not K(0) */
 #define MG_LANE_MEMTAG 8192u  /* symbolic lane whose memory may hold symbolic bytes
                                  (mtag); set by the host or by the device on a write */
+#define MG_LANE_RETDATA 16384u /* the path's last_return_data is set (a CALL the host's
+                                 escape handler ran): RETURNDATASIZE and RETURNDATACOPY
+                                 escape; without it they push 0 / pop only, as the
+                                 reference does with last_return_data None
+                                 (instructions.py:1314-1370)                       */
 
 /* environment words, per lane */
 #define MG_ENV_ADDRESS   0

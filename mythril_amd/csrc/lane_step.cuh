@@ -55,6 +55,7 @@ struct OpInfo {
 #define LANE_CREATION 2u
 #define LANE_HOOK_ACK 4u
 #define LANE_STEP1 8u
+#define LANE_RETDATA 16384u
 
 #define MSTATE_GAS_LIMIT 1000000000ull
 #ifndef MG_K1_PF
@@ -502,7 +503,10 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
             tos_done = true;
             break;
         }
-        case K_LOG: case K_POP: case K_RDCOPY: case K_JUMPDEST:
+        case K_RDCOPY:                                      // last_return_data None: pops only
+            if (E.flags & LANE_RETDATA) ESCX(ESC_OPCODE)
+            break;
+        case K_LOG: case K_POP: case K_JUMPDEST:
             break;                                          // pops only / no-op
         case K_ENV:
             switch (op) {
@@ -516,7 +520,10 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
             case 0x45: res = u_small(MSTATE_GAS_LIMIT); break;
             case 0x58: res = u_small(a32[C.addr_off + pc]); break;
             case 0x59: res = u_small(msize0); break;
-            default: res = u_zero(); break;                 // RETURNDATASIZE
+            default:                                        // RETURNDATASIZE
+                if (E.flags & LANE_RETDATA) ESCX(ESC_OPCODE)
+                res = u_zero();
+                break;
             }
             break;
         case K_STOP: STOPX(ST_STOP, 0u)
@@ -1415,7 +1422,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             }
             break;
         case K_ENV:
-            ok = gas_ok && sp + 1u <= stack_lim;
+            ok = gas_ok && sp + 1u <= stack_lim && !(op == 0x3du && (flags & LANE_RETDATA));
             if (ok) {
                 U256 r;
                 switch (op) {

@@ -668,6 +668,9 @@ class Environment:
         self.origin = origin if isinstance(origin, BitVec) else symbol_factory.BitVecVal(concrete(origin), 256)
         self.basefee = basefee
         self.static = static
+        # environment.py:47-48: always symbolic
+        self.block_number = symbol_factory.BitVecSym("block_number", 256)
+        self.chainid = symbol_factory.BitVecSym("chain_id", 256)
 
     def __copy__(self):
         e = Environment(self.active_account, self.sender, self.calldata, self.gasprice, self.callvalue,
@@ -696,6 +699,12 @@ class GlobalState:
 
     def add_annotations(self, annotations: List) -> None:
         self._annotations += annotations
+
+    def new_bitvec(self, name: str, size: int = 256, annotations=None) -> BitVec:
+        """global_state.py:146-156: a fresh symbol named after the current
+        transaction."""
+        return symbol_factory.BitVecSym("{}_{}".format(self.current_transaction.id, name), size,
+                                        annotations=annotations)
 
     def __copy__(self) -> "GlobalState":
         world_state = copy(self.world_state)

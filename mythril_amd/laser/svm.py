@@ -54,7 +54,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
-                     MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
+                     MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_RETDATA, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
                      MG_STACK_LIMIT,
                      limbs_to_word, rows_to_words, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
@@ -345,13 +345,97 @@ class LaserEVM:
             if self.escape_handler is None:
                 log.debug("state not representable on a lane and no escape handler: dropped")
                 continue
-            new_states = self.escape_handler(st)
+            new_states = self._escape_step(st, hooks_done=False, track_gas=track_gas,
+                                           final_states=final_states)
+            if new_states is None:
+                continue
             self._filter_fork(new_states)
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
             if not new_states and track_gas:
                 final_states.append(st)
         return keep
+
+    def _escape_step(self, s: GlobalState, hooks_done: bool, track_gas: bool, final_states: list):
+        """svm.py:369-491 execute_state for a state the escape handler steps.
+
+        The handler is the instruction's mutator -- in an integration the
+        reference's ``Instruction(op, dynamic_loader).evaluate(state)``: it
+        returns the successor states or raises a transaction-end signal
+        (``TransactionEndSignal``: ``global_state``, ``revert``), a VmException,
+        a ``TransactionStartSignal`` or ``NotImplementedError``.  This method
+        runs what execute_state runs around it: the execute_state hooks, the
+        precheck, the svm and instruction pre hooks (unless the device already
+        stopped the lane for them: ``hooks_done``), the transaction-end hooks,
+        ``check_potential_issues`` and ``_add_world_state`` of a top-level end,
+        and the post hooks on the successors.  Returns the successors, or None
+        when the state was consumed without any (final states already noted)."""
+        instrs = s.environment.code.instruction_list
+        name = instrs[s.mstate.pc]["opcode"] if s.mstate.pc < len(instrs) else None
+        if not hooks_done:
+            try:
+                for hook in self._execute_state_hooks:
+                    hook(s)
+            except PluginSkipState:
+                if track_gas:
+                    final_states.append(s)
+                return None
+            if name is None:
+                self._add_world_state(s)                  # svm.py:384-389
+                return None
+            if len(s.mstate.stack) < get_required_stack_elements(name):
+                if track_gas:                             # svm.py:391-402 precheck underflow
+                    final_states.append(s)
+                return None
+            try:
+                self._execute_pre_hook(name, s)
+            except PluginSkipState:
+                if track_gas:
+                    final_states.append(s)
+                return None
+            for hook in self.instr_pre_hook.get(name, ()):
+                hook(s)
+        snapshot = copy(s) if self.instr_post_hook.get(name) else None
+        try:
+            new_states = list(self.escape_handler(s))
+        except Exception as exc:          # noqa: BLE001 -- classified below, else re-raised
+            kind = _signal_kind(exc)
+            tx = s.current_transaction
+            if kind == "end":
+                self._end_transaction(exc.global_state, s, bool(getattr(exc, "revert", False)))
+            elif kind == "vm":
+                for hook in self._transaction_end_hooks:     # svm.py:417-425
+                    hook(s, tx, None, False)
+            elif kind in ("start", "unimplemented"):
+                # svm.py:314-316: a NotImplementedError drops the path; a call
+                # into code (a nested transaction) is outside the batched core
+                log.debug("escape handler cannot step %s (%s): state dropped", name, type(exc).__name__)
+                self.escapes_dropped += 1
+            else:
+                raise
+            new_states = []
+        if snapshot is not None:
+            for hook in self.instr_post_hook.get(name, ()):
+                hook(snapshot)
+        if name is not None:
+            self._execute_post_hook(name, new_states)
+        return new_states
+
+    def _end_transaction(self, end_state: GlobalState, pre_state: GlobalState, revert: bool) -> None:
+        """svm.py:427-465 for a TransactionEndSignal: the transaction-end hooks;
+        at the top level a kept end (not a revert, and a creation only when it
+        returned code) runs check_potential_issues on the state before the
+        ending instruction and adds the world state."""
+        tx, return_state = end_state.transaction_stack[-1] if end_state.transaction_stack else (None, None)
+        for hook in self._transaction_end_hooks:
+            hook(end_state, tx, return_state, revert)
+        if return_state is not None:
+            log.debug("nested message call ends outside the batched core: state dropped")
+            self.escapes_dropped += 1
+            return
+        if (not isinstance(tx, ContractCreationTransaction) or tx.return_data) and not revert:
+            check_potential_issues(pre_state)
+            self._add_world_state(end_state)
 
     def _filter_fork(self, new_states: list) -> None:
         """svm.py:319-326: a fork keeps the successors whose path constraints are
@@ -592,7 +676,8 @@ class LaserEVM:
         b.status[i] = MG_RUNNING
         b.aux[i] = 0
         b.flags[i] = (MG_LANE_STATIC if env.static else 0) | (
-            MG_LANE_CREATION if isinstance(tx, ContractCreationTransaction) else 0) | sflags
+            MG_LANE_CREATION if isinstance(tx, ContractCreationTransaction) else 0) | sflags | (
+            MG_LANE_RETDATA if s.last_return_data is not None else 0)
         b.gas_min[i] = ms.min_gas_used
         b.gas_max[i] = ms.max_gas_used
         b.gas_limit[i] = _NO_GAS_LIMIT if gas_limit is None else min(concrete(gas_limit), _NO_GAS_LIMIT)
@@ -1088,6 +1173,7 @@ class LaserEVM:
             for hook in self._transaction_end_hooks:
                 hook(s, tx, None, False)
             if keep:
+                check_potential_issues(s)                 # svm.py:456-462
                 self._add_world_state(s)
         elif status == MG_HALT_REVERT:
             if tx is not None:
@@ -1144,7 +1230,11 @@ class LaserEVM:
                 log.debug("Encountered unimplemented instruction %s", name)
                 self.escapes_dropped += 1
                 return              # svm.py:314-316: NotImplementedError -> continue
-            new_states = self.escape_handler(s)
+            # the device stopped the lane for this instruction's pre hooks first
+            # (hook mask), so they have run
+            new_states = self._escape_step(s, hooks_done=True, track_gas=track_gas, final_states=final_states)
+            if new_states is None:
+                return
             self._filter_fork(new_states)
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
@@ -1323,6 +1413,33 @@ def _hook_sig(s: GlobalState):
             ms.depth, ms.min_gas_used, ms.max_gas_used, id(env), id(env.code), env.static, id(env.calldata),
             id(env.address), id(env.sender), id(env.origin), id(env.callvalue), id(env.gasprice),
             id(acct), id(acct.storage), acct.storage._ver, id(s.current_transaction))
+
+
+def _no_potential_issues(state: GlobalState) -> None:
+    """Default of the check_potential_issues seam: no analysis installed."""
+
+
+# svm.py:456-462 calls mythril.analysis.potential_issues.check_potential_issues
+# at every kept top-level transaction end; an integration installs it here
+# (``mythril_amd.laser.svm.check_potential_issues = check_potential_issues``)
+check_potential_issues: Callable[[GlobalState], None] = _no_potential_issues
+
+
+def _signal_kind(exc: BaseException) -> Optional[str]:
+    """What an escape handler's exception means to execute_state, by the
+    reference's class names (so its own Instruction.evaluate can be the
+    handler): a transaction end, a VmException, a nested transaction start, an
+    unimplemented opcode; None for anything else (a real error)."""
+    names = {k.__name__ for k in type(exc).__mro__}
+    if "TransactionEndSignal" in names:
+        return "end"
+    if "VmException" in names:
+        return "vm"
+    if "TransactionStartSignal" in names:
+        return "start"
+    if "NotImplementedError" in names:
+        return "unimplemented"
+    return None
 
 
 def _held(s: GlobalState) -> Tuple[int, ...]:

@@ -613,8 +613,12 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
             for (uint64_t k = 0; k < ncopy; ++k) mem[m0 + k] = c->bytes[b.w[0] + k];
             break;
         }
-        case 0x3d: PUSH1(u_zero()); break;                 /* RETURNDATASIZE: no last_return_data */
-        case 0x3e: NEED_POP(3); sp -= 3; break;            /* RETURNDATACOPY: last_return_data None */
+        case 0x3d:                                         /* RETURNDATASIZE: no last_return_data */
+            if (flags & MG_LANE_RETDATA) ESC(MG_ESC_OPCODE);
+            PUSH1(u_zero()); break;
+        case 0x3e:                                         /* RETURNDATACOPY: last_return_data None */
+            if (flags & MG_LANE_RETDATA) ESC(MG_ESC_OPCODE);
+            NEED_POP(3); sp -= 3; break;
         case 0x45: PUSH1(u_from64(MG_MSTATE_GAS_LIMIT)); break;   /* GASLIMIT (:1427-1435) */
         case 0x50: NEED_POP(1); sp -= 1; break;
         case 0x51: { /* MLOAD (:1438-1451) */

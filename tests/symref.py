@@ -16,12 +16,26 @@ arena nodes into expressions) so the two meet only in the expression layer:
   (oracle/evm_ref.c, pinned on the reference's VMTests) over a concrete
   projection of the state.
 
-An instruction with symbolic inputs outside that set raises ``Unsupported``.
+* the opcodes kernel 1 leaves to the host (instructions.py:907-1000,
+  1151-1440, 1700-1711, 1862-2470): BALANCE / SELFBALANCE over the world
+  state's balances array, EXTCODESIZE, RETURNDATASIZE / RETURNDATACOPY,
+  GAS and the block values as fresh symbols, SELFDESTRUCT, and the CALL family
+  where the reference answers without running callee code -- a code-less
+  callee (an ether transfer, ``transfer_ether``) or an address the disabled
+  dynamic loader cannot load (``myth analyze --no-onchain-data``): symbolic
+  return data and a fresh ``retval`` (call.py:36-257).  A call into code or a
+  precompile raises ``Unsupported``.
+
+An instruction with symbolic inputs outside that set raises ``Unsupported``
+(a NotImplementedError, which LaserEVM drops as svm.py:314-316 does).
 Halts are reported in ``Engine.ended`` as (kind, state); ``Engine.run`` is a
 BFS over paths with the svm.py:319-326 fork filter, the restatement the
-device-driven LaserEVM is compared against."""
+device-driven LaserEVM is compared against.  ``Engine(signals=True)`` is the
+escape-handler form (the reference's Instruction.evaluate): halts and
+exceptions are raised as TransactionEndSignal / VmException instead."""
 from __future__ import annotations
 
+from collections import Counter
 from copy import copy
 
 import numpy as np
@@ -30,10 +44,11 @@ from mythril_amd.lanes import (LaneBatch, LaneShape, MG_HALT_DROPPED, MG_HALT_EN
                                MG_HALT_REVERT, MG_HALT_STOP, MG_RUNNING, MG_VMEXC, limbs_to_word,
                                word_to_limbs)
 from mythril_amd.laser.opcodes import ADDRESS_OPCODE_MAPPING
-from mythril_amd.laser.state import Memory, MachineStack, OutOfGasException
+from mythril_amd.laser.state import (Account, Memory, MachineStack, OutOfGasException, VmException,
+                                    WriteProtection)
 from mythril_amd.laser.transaction import ContractCreationTransaction
-from mythril_amd.smt.expr import (BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT, URem,
-                                  simplify_concat, symbol_factory)
+from mythril_amd.smt.expr import (UGE, BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT,
+                                  URem, simplify_concat, symbol_factory)
 from mythril_amd.smt.exponent_manager import exponent_function_manager
 from mythril_amd.smt.keccak_manager import keccak_function_manager
 from oracle.evm_ref import OracleEVM
@@ -41,8 +56,30 @@ from oracle.evm_ref import OracleEVM
 BVV = symbol_factory.BitVecVal
 
 
-class Unsupported(Exception):
+class Unsupported(NotImplementedError):
     pass
+
+
+class ReturnData:
+    """state/return_data.py:9-31."""
+
+    def __init__(self, return_data, return_data_size):
+        self.return_data = return_data
+        self.return_data_size = return_data_size
+
+    @property
+    def size(self):
+        return self.return_data_size
+
+
+PRECOMPILE_COUNT = 9          # natives.py:253-265
+
+
+def _z3str(x) -> str:
+    """str() of a reference BitVec as the names built from it print it (z3's
+    decimal for a constant)."""
+    v = _val(x)
+    return str(v) if v is not None else repr(getattr(x, "raw", x))
 
 
 def _val(x):
@@ -73,11 +110,20 @@ _SYM_ENV = {0x30: "address", 0x33: "sender", 0x32: "origin", 0x34: "callvalue", 
 
 
 class Engine:
-    def __init__(self, pruning=None):
+    def __init__(self, pruning=None, signals: bool = False):
         self.o = OracleEVM()
         self.code_ids = {}
         self.ended = []            # (kind, state): stop / return / revert / exception / end / unsupported
         self.pruning = pruning     # callable(list of states) -> kept states (the fork filter)
+        self.signals = signals     # escape-handler form: raise the reference's signals
+        self.host_ops = Counter()  # opcodes stepped by the host-op restatement
+
+    def _vmexc(self, state):
+        """A VmException at `state` (the path ends without a world state)."""
+        if self.signals:
+            raise VmException()
+        self.ended.append(("exception", state))
+        return []
 
     # ---- concrete instructions on the oracle ---------------------------------
     def _cid(self, code):
@@ -125,10 +171,25 @@ class Engine:
 
     def _ended(self, s, b):
         st = int(b.status[0])
+        data = bytes(b.memory[0, int(b.ret_offset[0]):int(b.ret_offset[0]) + int(b.ret_len[0])])
         if st == MG_HALT_RETURN:
-            s.return_data = bytes(b.memory[0, int(b.ret_offset[0]):int(b.ret_offset[0]) + int(b.ret_len[0])])
+            s.return_data = data
         kind = {MG_HALT_STOP: "stop", MG_HALT_RETURN: "return", MG_HALT_REVERT: "revert", MG_VMEXC: "exception",
                 MG_HALT_END: "end", MG_HALT_DROPPED: "dropped"}.get(st, "unsupported")   # oracle escapes
+        if self.signals:
+            self._advance(s, b)
+            tx = s.current_transaction
+            if kind == "stop":
+                tx.end(s)
+            elif kind == "return":
+                tx.end(s, return_data=data)
+            elif kind == "revert":
+                tx.end(s, return_data=data, revert=True)
+            elif kind == "exception":
+                raise VmException()
+            elif kind == "unsupported":
+                raise Unsupported("the oracle escapes this instruction")
+            return []
         if kind != "dropped":
             self.ended.append((kind, s))
         return []
@@ -245,6 +306,9 @@ class Engine:
         name = instrs[ms.pc]["opcode"]
         op = next(k for k, v in ADDRESS_OPCODE_MAPPING.items() if v == name)
         st = ms.stack
+        if op in _HOST_OPS:
+            self.host_ops[name] += 1
+            return self._host_op(state, s, op, name)
         nin = {"DUP": int(name[3:]) if name.startswith("DUP") else 0,
                "SWAP": int(name[4:]) + 1 if name.startswith("SWAP") else 0}
         reads = nin["DUP"] or nin["SWAP"] or _POPS.get(op, 0)
@@ -303,8 +367,7 @@ class Engine:
         if len(st) + 1 > 1024:
             raise Unsupported("stack overflow")
         if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
-            self.ended.append(("exception", state))
-            return []
+            return self._vmexc(state)
         if cond_after is not None:
             s.world_state.constraints.append(cond_after)
         st.append(res)
@@ -312,6 +375,164 @@ class Engine:
         ms.min_gas_used += gmin
         ms.max_gas_used += gmax
         return [s]
+
+    # ---- opcodes kernel 1 leaves to the host --------------------------------------
+    def _host_op(self, state, s, op, name):
+        """StateTransition (instructions.py:98-202) around the reference's
+        mutators of the opcodes kernel 1 escapes: write protection, the
+        mutator, accumulate_gas with its OOG checks, pc + 1."""
+        ms, env, ws = s.mstate, s.environment, s.world_state
+        st = ms.stack
+        gmin, gmax = _GAS[op]
+        try:
+            if op == 0xFF:
+                if env.static:
+                    raise WriteProtection()
+                return self._selfdestruct(s)
+            if op == 0x31:                                      # balance_ :907-931
+                address = _pop_bitvec(st.pop())
+                acct = ws.accounts.get(_val(address)) if _val(address) is not None else None
+                if acct is not None:
+                    bal = acct.balance()
+                else:                     # symbolic, or the disabled loader cannot load it
+                    bal = BVV(0, 256)
+                    for a in ws.accounts.values():
+                        bal = If(address == a.address, a.balance(), bal)
+                st.append(bal)
+            elif op == 0x47:                                    # selfbalance_ :968-976
+                st.append(env.active_account.balance())
+            elif op == 0x3B:                                    # extcodesize_ :1151-1175
+                addr = st.pop()
+                v = _val(addr)
+                if v is None:
+                    st.append(s.new_bitvec("extcodesize_" + _z3str(addr), 256))
+                elif v in ws.accounts:
+                    code = ws.accounts[v].code.bytecode
+                    st.append(BVV(len(code) // 2 if isinstance(code, str) else len(code), 256))
+                else:
+                    st.append(s.new_bitvec("extcodesize_" + hex(v), 256))
+            elif op == 0x3D:                                    # returndatasize_ :1359-1370
+                rd = s.last_return_data
+                st.append(rd.size if rd is not None else BVV(0, 256))
+            elif op == 0x3E:                                    # returndatacopy_ :1314-1357
+                mo, ro, size = st.pop(), st.pop(), st.pop()
+                if None not in (_val(mo), _val(ro), _val(size)) and s.last_return_data is not None:
+                    mo, ro, size = _val(mo), _val(ro), _val(size)
+                    ms.mem_extend(BVV(mo, 256), BVV(size, 256))
+                    rd = s.last_return_data
+                    for i in range(size):
+                        # `ro + i < rd.size`: a signed compare whose Bool is False
+                        # unless it simplifies to True (bool.py:72-80)
+                        inside = _val(rd.size) is not None and ro + i < _val(rd.size)
+                        ms.memory[mo + i] = rd.return_data[ro + i] if inside else 0
+            elif op == 0x5A:                                    # gas_ :1700-1709
+                st.append(s.new_bitvec("gas", 256))
+            elif op == 0x40:                                    # blockhash_ :1372-1384
+                n = st.pop()
+                st.append(s.new_bitvec("blockhash_block_" + _z3str(n), 256))
+            elif op == 0x41:
+                st.append(s.new_bitvec("coinbase", 256))
+            elif op == 0x42:
+                st.append(s.new_bitvec("timestamp", 256))
+            elif op == 0x43:
+                st.append(env.block_number)
+            elif op == 0x44:
+                st.append(s.new_bitvec("block_difficulty", 256))
+            elif op == 0x46:
+                st.append(env.chainid)
+            elif op == 0x48:
+                bf = env.basefee
+                st.append(bf if isinstance(bf, BitVec) else BVV(int(bf or 0), 256))
+            else:
+                self._call(s, op)
+            if len(st) > 1024:
+                raise VmException()
+            ms.min_gas_used += gmin
+            ms.max_gas_used += gmax
+            if ms.min_gas_used > 10 ** 9 or ms.min_gas_used >= _gas_limit(s):
+                raise OutOfGasException()
+        except VmException:
+            return self._vmexc(state)
+        ms.pc += 1
+        return [s]
+
+    def _call(self, s, op):
+        """call_ / callcode_ / delegatecall_ / staticcall_ (instructions.py:
+        1999-2470) with get_call_parameters (call.py:36-79) where no callee code
+        runs: a symbolic callee or a known code-less account receives an ether
+        transfer; an address the disabled dynamic loader cannot load
+        (ValueError) gets nothing; both write symbolic return data and push a
+        fresh retval.  A callee with code or a precompile starts a nested
+        transaction / native call: Unsupported."""
+        ms, env, ws = s.mstate, s.environment, s.world_state
+        st = ms.stack
+        with_value = op in (0xF1, 0xF2)
+        instr_addr = env.code.instruction_list[ms.pc]["address"]
+        gas, to = st.pop(), st.pop()
+        value = st.pop() if with_value else BVV(0, 256)
+        in_off, in_size, out_off, out_size = st.pop(), st.pop(), st.pop(), st.pop()
+        to_v = _val(to)
+        callee = None
+        unloadable = False
+        if to_v is None:
+            callee = Account(_pop_bitvec(to), balances=ws.balances)    # get_callee_account, call.py:147-151
+        elif to_v > PRECOMPILE_COUNT or to_v == 0:
+            if to_v in ws.accounts:
+                callee = ws.accounts[to_v]
+            else:
+                unloadable = True         # accounts_exist_or_load: "Dynamic Loader is deactivated"
+        if not unloadable:
+            code = callee.code.bytecode if callee is not None else None
+            if callee is None or code not in ("", b""):
+                raise Unsupported("a call into code or a precompile (a nested transaction)")
+            self._transfer_ether(s, env.active_account.address, callee.address, _pop_bitvec(value))
+        self._write_symbolic_returndata(s, out_off, out_size)
+        st.append(s.new_bitvec("retval_" + str(instr_addr), 256))
+
+    @staticmethod
+    def _transfer_ether(s, sender, receiver, value):
+        """instructions.py:74-96."""
+        ws = s.world_state
+        ws.constraints.append(UGE(ws.balances[sender], value))
+        ws.balances[receiver] = ws.balances[receiver] + value
+        ws.balances[sender] = ws.balances[sender] - value
+
+    @staticmethod
+    def _write_symbolic_returndata(s, off, size):
+        """instructions.py:1961-1997."""
+        if _val(off) is None or _val(size) is None:
+            return
+        ms = s.mstate
+        off, size = _val(off), _val(size)
+        data = [s.new_bitvec("call_output_var({})_{}".format((off + i) % (1 << 256), ms.pc), 8)
+                for i in range(size)]
+        rds = s.new_bitvec("returndatasize", 256)
+        ms.mem_extend(BVV(off, 256), BVV(size, 256))
+        for i in range(size):
+            old = ms.memory[off + i]
+            old = old if isinstance(old, BitVec) else BVV(old, 8)
+            ms.memory[off + i] = If(rds >= BVV(i, 256), data[i], old)     # `i <= size`: signed
+        s.last_return_data = ReturnData(data, rds)
+
+    def _selfdestruct(self, s):
+        """selfdestruct_ (instructions.py:1876-1897): the balance goes to the
+        target and the transaction ends.  The reference zeroes the balance on a
+        deepcopy of the account whose balance array is detached from the world
+        state's (and whose balance() still reads the world state's), so the
+        world state's array keeps the old balance: restated as such."""
+        env, ws = s.environment, s.world_state
+        target = _pop_bitvec(s.mstate.stack.pop())
+        amount = env.active_account.balance()
+        ws.balances[target] = ws.balances[target] + amount
+        acct = copy(env.active_account)
+        acct._balances = ws.balances
+        acct.deleted = True
+        ws._accounts[_val(acct.address)] = acct
+        env.active_account = acct
+        if self.signals:
+            s.current_transaction.end(s)
+        self.ended.append(("stop", s))
+        return []
 
     # ---- symbolic calldata copies, a creation's calldata opcodes ---------------
     def _calldata_ops(self, state, s, op, creation):
@@ -347,13 +568,11 @@ class Engine:
                 try:
                     ms.mem_extend(BVV(dst, 256), BVV(size, 256))
                 except OutOfGasException:
-                    self.ended.append(("exception", state))
-                    return []
+                    return self._vmexc(state)
                 for k in range(size):
                     ms.memory[dst + k] = env.calldata[src + k]
         if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
-            self.ended.append(("exception", state))
-            return []
+            return self._vmexc(state)
         ms.pc += 1
         ms.min_gas_used += gmin
         ms.max_gas_used += gmax
@@ -411,16 +630,13 @@ class Engine:
         k = int(name[3:]) if name.startswith("DUP") else int(name[4:])
         need = k if name.startswith("DUP") else k + 1
         if len(st) < need:
-            self.ended.append(("exception", s))
-            return []
+            return self._vmexc(s)
         gmin, gmax = 3, 3
         if s.mstate.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
-            self.ended.append(("exception", s))
-            return []
+            return self._vmexc(s)
         if name.startswith("DUP"):
             if len(st) + 1 > 1024:
-                self.ended.append(("exception", s))
-                return []
+                return self._vmexc(s)
             st.append(st[-k])
         else:
             st[-1], st[-1 - k] = st[-1 - k], st[-1]
@@ -505,6 +721,9 @@ _POPS = {**{op: 2 for op in list(range(0x01, 0x08)) + [0x0A, 0x0B] + list(range(
             list(range(0x16, 0x19)) + list(range(0x1A, 0x1E)) + [0x20, 0x52, 0x53, 0x55, 0x57, 0xF3, 0xFD]},
          0x08: 3, 0x09: 3, 0x15: 1, 0x19: 1, 0x35: 1, 0x37: 3, 0x39: 3, 0x3E: 3, 0x50: 1, 0x51: 1,
          0x54: 1, 0x56: 1, 0xA0: 2, 0xA1: 3, 0xA2: 4, 0xA3: 5, 0xA4: 6}
+# opcodes kernel 1 escapes and the host restates (instructions.py)
+_HOST_OPS = {0x31, 0x3B, 0x3D, 0x3E, 0x40, 0x41, 0x42, 0x43, 0x44, 0x46, 0x47, 0x48, 0x5A,
+             0xF1, 0xF2, 0xF4, 0xFA, 0xFF}
 _SYM_OK = set(range(0x01, 0x08)) | set(range(0x10, 0x15)) | {0x15, 0x16, 0x17, 0x18, 0x19, 0x1A, 0x1B, 0x1C, 0x1D}
 
 
