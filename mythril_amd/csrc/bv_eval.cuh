@@ -69,7 +69,7 @@ enum BvOp : uint32_t {
 #define BV_REF_SLOT 1u
 #define BV_REF_VAR 2u
 #define BV_REF_CONST 3u
-#define BV_MAX_SLOTS 8u
+#define BV_MAX_SLOTS 16u    // 4-bit slot field; 16 slots = 128 KiB of LDS per block
 #define BV_BLOCK 256u
 #define BV_TILE_INSNS 2048u   // longest program (LDS tile upper bound: 32 KiB)
 #ifndef BV_TILE_MIN
@@ -97,8 +97,6 @@ struct BvState {
     bool want_bits = false;
     size_t cap_insns = 0, cap_dags = 0, cap_consts = 0, cap_values = 0, cap_tiles = 0;
     size_t cap_entries = 0;
-    bool lds_prog = false;           // MG_BV_PROG=lds stages the program tile in LDS
-    bool pair = false;               // MG_BV_PROG=pair: two models per thread (k_bv_eval_pair)
     std::vector<uint32_t> h_tiles;
     std::vector<uint32_t> h_insns, h_off;   // the fused programs (bv_fuse)
 };
@@ -305,7 +303,6 @@ __device__ __forceinline__ U256 bv_simple(uint32_t k, const U256 &a, const U256 
 }
 static const uint32_t kBvSimple[9] = {BV_ADD, BV_SUB, BV_MUL, BV_AND, BV_OR, BV_XOR, BV_UMAX, BV_UMIN, BV_RSUB};
 
-template <bool kLdsProg>
 __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                                                       const uint32_t *__restrict__ prog_off,
                                                       const uint32_t *__restrict__ tile_dag,
@@ -320,12 +317,10 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                                                       unsigned long long *__restrict__ sat_bits,
                                                       uint32_t bit_words) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    // kLdsProg: the program tile is staged in LDS and read with a broadcast
-    // ds_read + readfirstlane; otherwise instructions are read with scalar loads
-    // (uniform address -> s_load_dwordx4 through the scalar cache) and LDS only
-    // holds the register slots (higher occupancy)
-    uint4 *prog = smem;                          // [tile_cap] (kLdsProg)
-    uint4 *slots = kLdsProg ? smem + tile_cap : smem;   // [n_slots][2][BV_BLOCK]
+    // instructions are read with scalar loads (uniform address -> s_load_dwordx4
+    // through the scalar cache); LDS holds only the register slots.  Staging the
+    // program tile in LDS measured slower (occupancy, ab/k2_lds_fetch.diff)
+    uint4 *slots = smem;                         // [n_slots][2][BV_BLOCK]
     // group-major order with the tile count padded to a multiple of 8: the blocks
     // of one program tile share blockIdx % 8, i.e. one XCD's L2 (speed only)
     const uint32_t b = blockIdx.x;
@@ -340,8 +335,6 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     // its totals to HBM once per DAG (not one atomic pair per wave per DAG)
     __shared__ uint32_t blk_cnt[BV_TILE_DAGS], blk_first[BV_TILE_DAGS];
     if (threadIdx.x < BV_TILE_DAGS) { blk_cnt[threadIdx.x] = 0u; blk_first[threadIdx.x] = 0xffffffffu; }
-    if (kLdsProg)
-        for (uint32_t i = threadIdx.x; i < i1 - i0; i += BV_BLOCK) prog[i] = insns[i0 + i];
     __syncthreads();
 
     const uint32_t n_chunks = (n_models + BV_BLOCK - 1u) / BV_BLOCK;
@@ -364,10 +357,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             // keeping them in extra VGPRs across the loop (they spilled)
             asm volatile("" : "+v"(c.m));
             uint32_t w0, ra, rb, rc;
-            if (kLdsProg) {
-                const uint4 ins = prog[p];
-                w0 = uni(ins.x); ra = uni(ins.y); rb = uni(ins.z); rc = uni(ins.w);
-            } else {
+            {
                 const uint4 ins = insns[i0 + uni(p)];
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
             }
@@ -483,10 +473,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
                 case BV_BINX: {
                     uint32_t e0, e1, e2;
-                    if (kLdsProg) {
-                        const uint4 x = prog[p + 1];
-                        e0 = uni(x.x); e1 = uni(x.y); e2 = uni(x.z);
-                    } else {
+                    {
                         const uint4 x = insns[i0 + uni(p + 1u)];
                         e0 = x.x; e1 = x.y; e2 = x.z;
                     }
@@ -520,10 +507,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 // {kinds | count << 28, B1, B2, B3}
                 if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);
                 uint32_t e0, e1, e2, e3;
-                if (kLdsProg) {
-                    const uint4 x = prog[p + 1];
-                    e0 = uni(x.x); e1 = uni(x.y); e2 = uni(x.z); e3 = uni(x.w);
-                } else {
+                {
                     const uint4 x = insns[i0 + uni(p + 1u)];
                     e0 = x.x; e1 = x.y; e2 = x.z; e3 = x.w;
                 }
@@ -570,210 +554,6 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     }
 }
 
-// ---- pair mode (MG_BV_PROG=pair): two models per thread ------------------------
-// Thread t of a block evaluates models m = chunk * 2 BV_BLOCK + t and m + BV_BLOCK
-// with ONE decode of each instruction: the per-instruction scalar work (fetch,
-// dispatch, loop) is shared by the two models and the two 256-bit chains are
-// independent, so each wave carries twice the VALU work between its scalar
-// steps and its carry chains interleave (the single-model chain stalls on its
-// own VCC between limbs).  Slots: LDS [n_slots][2 halves][2 models][BV_BLOCK].
-struct BvCtx2 {
-    const uint4 *__restrict__ values;
-    const uint4 *__restrict__ consts;
-    uint4 *slots;
-    uint32_t n_models, m;
-    BvTables tab;
-    DEV uint32_t model(uint32_t k) const { return min(m + k * BV_BLOCK, n_models - 1u); }
-    DEV uint32_t tid() const { return m & (BV_BLOCK - 1u); }
-};
-
-DEV U256 bv_fetch2(const BvCtx2 &c, uint32_t ref, uint32_t k) {
-    const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
-    U256 r;
-    if (kind <= BV_REF_SLOT) {
-        const uint4 x = c.slots[((idx * 2u) * 2u + k) * BV_BLOCK + c.tid()];
-        const uint4 y = c.slots[((idx * 2u + 1u) * 2u + k) * BV_BLOCK + c.tid()];
-        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-        BV_PIN("; slot operand", r);
-        return r;
-    }
-    if (kind == BV_REF_VAR) {
-        const size_t row = (size_t)idx * c.n_models + c.model(k);
-        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
-        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-        BV_PIN("; variable operand", r);
-        return r;
-    }
-    const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
-    r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-    r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-    BV_PIN("; constant operand", r);
-    return r;
-}
-
-DEV U256 bv_table_m(const BvTables &tab, uint32_t n_models, uint32_t model, const U256 &k0, const U256 &k1,
-                    uint32_t imm) {
-    const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
-    const size_t tm = (size_t)t * n_models + model;
-    const uint32_t s0 = tab.start[tm], cnt = tab.count[tm];
-    U256 v = ld2(tab.dflt + tm * 4u + part * 2u);
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const uint4 *e = tab.entries + (size_t)(s0 + k) * 8u;
-        if (u_eq(ld2(e), k0) && u_eq(ld2(e + 2), k1)) {
-            v = ld2(e + 4 + part * 2u);
-            break;
-        }
-    }
-    return lo ? u_shr_n(v, lo, 0u) : v;
-}
-
-// both models' results of one binary op: E is an expression of A, B (and width, rc)
-#define BV2(E) { { const U256 &A = a0; const U256 &B = b0; r0 = (E); } \
-                 { const U256 &A = a1; const U256 &B = b1; r1 = (E); } }
-
-__global__ __launch_bounds__(BV_BLOCK, 4) void k_bv_eval_pair(
-        const uint4 *__restrict__ insns, const uint32_t *__restrict__ prog_off, const uint32_t *__restrict__ tile_dag,
-        const uint4 *__restrict__ consts, const uint4 *__restrict__ values, uint32_t n_models, BvTables tab,
-        uint32_t n_slots, uint32_t tile_first, uint32_t n_tiles, uint32_t tiles_pad, uint32_t dag_lo, uint32_t dag_hi,
-        uint32_t chunks_per_block, uint32_t *__restrict__ first_sat, uint32_t *__restrict__ sat_count,
-        unsigned long long *__restrict__ sat_bits, uint32_t bit_words) {
-    extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-    uint4 *slots = smem;
-    const uint32_t b = blockIdx.x;
-    const uint32_t tile = tile_first + (b % tiles_pad);
-    const uint32_t group = b / tiles_pad;
-    if (tile >= tile_first + n_tiles) return;
-    const uint32_t d0 = max(tile_dag[tile], dag_lo), d1 = min(tile_dag[tile + 1], dag_hi);
-    if (d0 >= d1) return;
-    const uint32_t i0 = prog_off[d0];
-    __shared__ uint32_t blk_cnt[BV_TILE_DAGS], blk_first[BV_TILE_DAGS];
-    if (threadIdx.x < BV_TILE_DAGS) { blk_cnt[threadIdx.x] = 0u; blk_first[threadIdx.x] = 0xffffffffu; }
-    __syncthreads();
-    const uint32_t n_chunks = (n_models + 2u * BV_BLOCK - 1u) / (2u * BV_BLOCK);
-    const uint32_t c_lo = group * chunks_per_block, c_hi = min(c_lo + chunks_per_block, n_chunks);
-    const uint32_t wave0 = uni(threadIdx.x) & ~63u;
-    for (uint32_t d = d0; d < d1; ++d) {
-    const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
-    for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-        BvCtx2 c{values, consts, slots, n_models, chunk * 2u * BV_BLOCK + wave0 + __lane_id(), tab};
-        U256 a0 = u_zero(), a1 = u_zero();
-        for (uint32_t p = p0; p < p1; ++p) {
-            asm volatile("" : "+v"(c.m));
-            const uint4 ins = insns[i0 + uni(p)];
-            const uint32_t w0 = ins.x, ra = ins.y, rb = ins.z, rc = ins.w;
-            const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
-            if ((ra >> 30) != BV_REF_ACC) { a0 = bv_fetch2(c, ra, 0u); a1 = bv_fetch2(c, ra, 1u); }
-            U256 r0, r1;
-            switch (op) {
-            case BV_COPY: case BV_ZEXT: r0 = a0; r1 = a1; break;
-            case BV_NOT: r0 = u_not(a0); r1 = u_not(a1); break;
-            case BV_NEG: r0 = u_neg(a0); r1 = u_neg(a1); break;
-            case BV_BNOT: r0 = u_small((a0.w[0] & 1u) ^ 1u); r1 = u_small((a1.w[0] & 1u) ^ 1u); break;
-            case BV_EXTRACT: r0 = u_shr_n(a0, rb & 0xffu, 0u); r1 = u_shr_n(a1, rb & 0xffu, 0u); break;
-            case BV_SEXT: r0 = bv_sext(a0, rb); r1 = bv_sext(a1, rb); break;
-            default: {
-                const U256 b0 = bv_fetch2(c, rb, 0u), b1 = bv_fetch2(c, rb, 1u);
-                if (op == BV_UDIV || op == BV_UREM) {
-                    r0 = bv_udivrem(op == BV_UDIV, a0, b0);
-                    r1 = bv_udivrem(op == BV_UDIV, a1, b1);
-                    break;
-                }
-                if ((BV_DIV_OPS >> op) & 1ull) {
-                    r0 = bv_divop(op, width, rc, a0, b0);
-                    r1 = bv_divop(op, width, rc, a1, b1);
-                    break;
-                }
-                switch (op) {
-                case BV_ADD: BV2(u_add(A, B)) break;
-                case BV_SUB: BV2(u_sub(A, B)) break;
-                case BV_MUL: BV2(u_mul(A, B)) break;
-                case BV_AND: BV2(u_and(A, B)) break;
-                case BV_OR: BV2(u_or(A, B)) break;
-                case BV_XOR: BV2(u_xor(A, B)) break;
-                case BV_SHL: BV2((u_fits32(B) && B.w[0] < width) ? u_shl_n(A, B.w[0]) : u_zero()) break;
-                case BV_LSHR: BV2((u_fits32(B) && B.w[0] < width) ? u_shr_n(A, B.w[0], 0u) : u_zero()) break;
-                case BV_ASHR:
-                    BV2(u_shr_n(bv_sext(A, width), (u_fits32(B) && B.w[0] < width) ? B.w[0] : 255u,
-                                u_isneg(bv_sext(A, width)) ? 0xffffffffu : 0u))
-                    break;
-                case BV_EQ: BV2(u_small(u_eq(A, B))) break;
-                case BV_NE: BV2(u_small(!u_eq(A, B))) break;
-                case BV_ULT: BV2(u_small(u_lt(A, B))) break;
-                case BV_ULE: BV2(u_small(!u_lt(B, A))) break;
-                case BV_UGT: BV2(u_small(u_lt(B, A))) break;
-                case BV_UGE: BV2(u_small(!u_lt(A, B))) break;
-                case BV_SLT: BV2(u_small(u_slt(bv_sext(A, rc), bv_sext(B, rc)))) break;
-                case BV_SLE: BV2(u_small(!u_slt(bv_sext(B, rc), bv_sext(A, rc)))) break;
-                case BV_SGT: BV2(u_small(u_slt(bv_sext(B, rc), bv_sext(A, rc)))) break;
-                case BV_SGE: BV2(u_small(!u_slt(bv_sext(A, rc), bv_sext(B, rc)))) break;
-                case BV_BAND: BV2(u_small(A.w[0] & B.w[0] & 1u)) break;
-                case BV_BOR: BV2(u_small((A.w[0] | B.w[0]) & 1u)) break;
-                case BV_BXOR: BV2(u_small((A.w[0] ^ B.w[0]) & 1u)) break;
-                case BV_BIMPLIES: BV2(u_small(((A.w[0] & 1u) ^ 1u) | (B.w[0] & 1u))) break;
-                case BV_ITE: {
-                    const U256 c0 = bv_fetch2(c, rc, 0u), c1 = bv_fetch2(c, rc, 1u);
-                    r0 = u_select((a0.w[0] & 1u) != 0u, b0, c0);
-                    r1 = u_select((a1.w[0] & 1u) != 0u, b1, c1);
-                    break;
-                }
-                case BV_CONCAT: BV2(u_or(u_shl_n(A, rc), B)) break;
-                case BV_ADD_NOOVF_U:
-                    BV2(u_small(!(rc >= 256u ? u_lt(u_add(A, B), A) : !u_iszero(u_shr_n(u_add(A, B), rc, 0u)))))
-                    break;
-                case BV_SUB_NOUDF_U: BV2(u_small(!u_lt(A, B))) break;
-                case BV_TAB:
-                    r0 = bv_table_m(c.tab, n_models, c.model(0u), a0, b0, rc);
-                    r1 = bv_table_m(c.tab, n_models, c.model(1u), a1, b1, rc);
-                    break;
-                case BV_UMIN: BV2(u_select(u_lt(B, A), B, A)) break;
-                case BV_UMAX: BV2(u_select(u_lt(A, B), B, A)) break;
-                case BV_SMIN: BV2(u_select(u_slt(bv_sext(B, width), bv_sext(A, width)), B, A)) break;
-                case BV_SMAX: BV2(u_select(u_slt(bv_sext(A, width), bv_sext(B, width)), B, A)) break;
-                case BV_RSUB: BV2(u_sub(B, A)) break;
-                case BV_RCONCAT: BV2(u_or(u_shl_n(B, rc), A)) break;
-                default: r0 = u_zero(); r1 = u_zero(); break;
-                }
-            }
-            }
-            if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) { r0 = bv_mask(r0, width); r1 = bv_mask(r1, width); }
-            a0 = r0;
-            a1 = r1;
-            if ((w0 >> 17) & 1u) {
-                const uint32_t ds = (w0 >> 18) & 0xfu;
-                slots[((ds * 2u) * 2u) * BV_BLOCK + c.tid()] = make_uint4(r0.w[0], r0.w[1], r0.w[2], r0.w[3]);
-                slots[((ds * 2u + 1u) * 2u) * BV_BLOCK + c.tid()] = make_uint4(r0.w[4], r0.w[5], r0.w[6], r0.w[7]);
-                slots[((ds * 2u) * 2u + 1u) * BV_BLOCK + c.tid()] = make_uint4(r1.w[0], r1.w[1], r1.w[2], r1.w[3]);
-                slots[((ds * 2u + 1u) * 2u + 1u) * BV_BLOCK + c.tid()] =
-                    make_uint4(r1.w[4], r1.w[5], r1.w[6], r1.w[7]);
-            }
-        }
-        const uint32_t wm = uni(c.m) & ~63u;
-        const uint64_t bal0 = __ballot(c.m < n_models && (a0.w[0] & 1u));
-        const uint64_t bal1 = __ballot(c.m + BV_BLOCK < n_models && (a1.w[0] & 1u));
-        if ((bal0 | bal1) && __lane_id() == 0u) {
-            if (sat_bits) {
-                if (bal0) sat_bits[(size_t)d * bit_words + (wm >> 6)] = bal0;
-                if (bal1) sat_bits[(size_t)d * bit_words + ((wm + BV_BLOCK) >> 6)] = bal1;
-            }
-            atomicAdd(&blk_cnt[d - d0], (uint32_t)(__popcll(bal0) + __popcll(bal1)));
-            atomicMin(&blk_first[d - d0], bal0 ? wm + (uint32_t)(__ffsll((long long)bal0) - 1)
-                                               : wm + BV_BLOCK + (uint32_t)(__ffsll((long long)bal1) - 1));
-        }
-    }
-    }
-    __syncthreads();
-    const uint32_t tid = wave0 + __lane_id();
-    if (tid < d1 - d0) {
-        const uint32_t n = blk_cnt[tid], f = blk_first[tid];
-        if (n) {
-            atomicAdd(&sat_count[d0 + tid], n);
-            atomicMin(&first_sat[d0 + tid], f);
-        }
-    }
-}
-#undef BV2
 
 template <class T>
 static int bv_ensure(T *&p, size_t &cap, size_t need) {
@@ -939,19 +719,14 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
             }
         }
     }
-    const char *pv = getenv("MG_BV_PROG");
-    // scalar-load fetch by default: at 8 waves per SIMD the LDS tile would cost
-    // occupancy (C4: scalar 220 ms, LDS 232 ms); MG_BV_PROG=lds selects the other
-    s.lds_prog = pv && std::string(pv) == "lds";
-    s.pair = pv && std::string(pv) == "pair";
     const char *fv = getenv("MG_BV_FUSE");
     const uint32_t *insns = dags->insns, *prog_off = dags->prog_off;
     uint32_t total_up = total;
-    if (!s.pair && !(fv && fv[0] == '0')) {
-        // MG_BV_FUSE=1: only the compare->and and extract->rconcat shapes, 2: and
-        // binary-op pairs, 3: and their chains, unset (4): and fused tails
-        const char lvl = fv && fv[0] >= '1' && fv[0] <= '4' ? fv[0] : '5';
-        bv_fuse(dags, s.h_insns, s.h_off, lvl >= '2', lvl >= '3', lvl >= '4', lvl >= '5');
+    if (!(fv && fv[0] == '0')) {
+        // superinstructions, all shapes (MG_BV_FUSE=0 uploads the programs as
+        // given: the parity tests compare both; the per-shape A/B levels are in
+        // ab/k2_fuse_levels.diff)
+        bv_fuse(dags, s.h_insns, s.h_off, true, true, true, true);
         insns = s.h_insns.data();
         prog_off = s.h_off.data();
         total_up = s.h_off[n];
@@ -1049,27 +824,21 @@ static int bv_run(BvState &s, uint32_t dag_first, uint32_t dag_count, hipStream_
     const uint32_t tiles_pad = (nt + 7u) & ~7u;
     // model chunks per block: as many as keep >= BV_GROUP_TARGET blocks in flight,
     // so each program tile is staged once per block instead of once per chunk
-    const uint32_t chunk_models = s.pair ? 2u * BV_BLOCK : BV_BLOCK;
+    const uint32_t chunk_models = BV_BLOCK;
     const uint32_t chunks = (s.n_models + chunk_models - 1) / chunk_models;
     const uint32_t groups_wanted = std::max<uint32_t>(1u, (BV_GROUP_TARGET + tiles_pad - 1u) / tiles_pad);
     const uint32_t cpb = std::max<uint32_t>(1u, chunks / std::min(groups_wanted, chunks));
     const uint32_t groups = (chunks + cpb - 1u) / cpb;
     const size_t grid = (size_t)tiles_pad * groups;
     if (grid > 0x7fffffffull) { msg = "grid too large"; return MG_EINVAL; }
-    const bool lds_prog = s.lds_prog;
-    if (s.pair) {
-        const size_t lds2 = (size_t)s.n_slots * 4 * BV_BLOCK * sizeof(uint4);
-        hipLaunchKernelGGL(k_bv_eval_pair, dim3((unsigned)grid), dim3(BV_BLOCK), lds2, st,
-                           s.insns, s.prog_off, s.tile_dag, s.consts, s.values, s.n_models,
-                           BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
-                           s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi, cpb, s.first_sat, s.sat_count,
-                           s.want_bits ? s.sat_bits : nullptr, bit_words);
-        e = hipGetLastError();
-        if (e != hipSuccess) { msg = std::string("k_bv_eval_pair launch: ") + hipGetErrorString(e); return MG_EDEVICE; }
-        return 0;
+    const size_t lds = (size_t)s.n_slots * 2 * BV_BLOCK * sizeof(uint4);
+    static bool lds_attr = false;      // programs with more than 4 slots need > 64 KiB of LDS
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void *)k_bv_eval, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(BV_MAX_SLOTS * 2 * BV_BLOCK * sizeof(uint4)));
+        lds_attr = true;
     }
-    const size_t lds = ((lds_prog ? (size_t)s.tile_cap : 0u) + (size_t)s.n_slots * 2 * BV_BLOCK) * sizeof(uint4);
-    hipLaunchKernelGGL(lds_prog ? k_bv_eval<true> : k_bv_eval<false>, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
+    hipLaunchKernelGGL(k_bv_eval, dim3((unsigned)grid), dim3(BV_BLOCK), lds, st,
                        s.insns, s.prog_off, s.tile_dag,
                        s.consts, s.values, s.n_models, BvTables{s.tab_start, s.tab_count, s.tab_entries, s.tab_default},
                        s.n_slots, t0, nt, tiles_pad, dag_first, dag_hi,

@@ -245,16 +245,25 @@ class LazyStack(MachineStack):
 
 
 class Memory:
-    """memory.py:28-208 at concrete offsets: a byte is an int or, for a symbolic
-    byte, an 8-bit expression (``Extract(i + 7, i, value)`` of a symbolic word
-    written with write_word_at, memory.py:102-115); reads of unset bytes give 0,
-    writes at index >= msize are dropped (memory.py:202-203), and a word read
+    """memory.py:28-208: a byte is an int or, for a symbolic byte, an 8-bit
+    expression (``Extract(i + 7, i, value)`` of a symbolic word written with
+    write_word_at, memory.py:102-115); reads of unset bytes give 0, writes at a
+    concrete index >= msize are dropped (memory.py:202-203), and a word read
     with a symbolic byte in it is ``simplify(Concat(bytes))`` (memory.py:70-82,
-    expr.simplify_concat).  Symbolic offsets stay with the host's handler."""
+    expr.simplify_concat).
 
-    def __init__(self, data: bytes = b"", sym: Optional[Dict[int, BitVec]] = None):
+    A symbolic index is a key of its own (the reference's dict keyed by
+    ``simplify(index)``): ``memory_key`` gathers the constants of an add chain
+    as z3's simplify does, so ``(p + 1) + 31`` and ``p + 32`` are one byte.
+    Its ``bv_key >= len(self)`` guard is a symbolic (signed) compare that never
+    drops the write.  Lanes carry concrete offsets only: a state with bytes at
+    symbolic keys stays with the host's handler."""
+
+    def __init__(self, data: bytes = b"", sym: Optional[Dict[int, BitVec]] = None,
+                 keys: Optional[Dict[Node, object]] = None):
         self._m = bytearray(data)
         self._sym: Dict[int, BitVec] = dict(sym) if sym else {}
+        self._keys: Dict[Node, object] = dict(keys) if keys else {}     # symbolic index -> byte
         self._ver = 0            # bumped by every mutation (LaserEVM's unchanged-after-hooks test)
 
     def __len__(self):
@@ -270,59 +279,134 @@ class Memory:
         s = self._sym.get(k) if self._sym else None
         return self._m[k] if s is None else s
 
+    @staticmethod
+    def _index(item):
+        """(int index, None) or (None, normalised symbolic key)."""
+        if isinstance(item, Expression):
+            if item.value is not None:
+                return item.value, None
+            return None, memory_key(item.raw)
+        return int(item), None
+
     def __getitem__(self, item):
         if isinstance(item, slice):
             start, stop = item.start or 0, item.stop if item.stop is not None else len(self._m)
+            if isinstance(start, Expression) or isinstance(stop, Expression):
+                return [self[_add(start, k)] for k in range(_slice_len(start, stop))]
             return [self._byte(k) for k in range(start, stop)]
-        return self._byte(item)
+        k, key = self._index(item)
+        if key is not None:
+            return self._keys.get(key, 0)
+        return self._byte(k)
 
-    def __setitem__(self, key: int, value):
-        if key >= len(self._m):
+    def __setitem__(self, key, value):
+        k, skey = self._index(key)
+        if skey is not None:
+            self._ver += 1
+            if isinstance(value, Expression) and value.symbolic and value.size() != 8:
+                raise ValueError("a memory byte is an 8-bit expression")
+            self._keys[skey] = value if isinstance(value, Expression) and value.symbolic else concrete(value) & 0xFF
+            return
+        if k >= len(self._m):
             return
         self._ver += 1
         if isinstance(value, Expression) and value.symbolic:
             if value.size() != 8:
                 raise ValueError("a memory byte is an 8-bit expression")
-            self._sym[key] = value
-            self._m[key] = 0                 # the byte's concrete image (as a lane holds it)
+            self._sym[k] = value
+            self._m[k] = 0                 # the byte's concrete image (as a lane holds it)
             return
-        self._m[key] = concrete(value) & 0xFF
+        self._m[k] = concrete(value) & 0xFF
         if self._sym:
-            self._sym.pop(key, None)
+            self._sym.pop(k, None)
 
     @property
     def symbolic(self) -> bool:
-        return bool(self._sym)
+        return bool(self._sym) or bool(self._keys)
+
+    @property
+    def symbolic_keys(self) -> bool:
+        """Bytes stored at symbolic indices (no lane can carry them)."""
+        return bool(self._keys)
 
     def symbolic_bytes(self) -> Dict[int, BitVec]:
-        """{offset: 8-bit expression} of the symbolic bytes."""
+        """{offset: 8-bit expression} of the symbolic bytes at concrete offsets."""
         return self._sym
 
-    def get_word_at(self, index: int) -> BitVec:
-        if self._sym and any(k in self._sym for k in range(index, index + 32)):
-            return simplify_concat(self[index: index + 32])
-        b = bytes(self._m[index: index + 32]).ljust(32, b"\x00") if index < len(self._m) else bytes(32)
+    def get_word_at(self, index) -> BitVec:
+        k, key = self._index(index)
+        if key is not None:
+            parts = [self[_add(index, j)] for j in range(32)]
+            if all(not isinstance(b, Expression) for b in parts):
+                return symbol_factory.BitVecVal(int.from_bytes(bytes(parts), "big"), 256)
+            return simplify_concat(parts)
+        if self._sym and any(j in self._sym for j in range(k, k + 32)):
+            return simplify_concat(self[k: k + 32])
+        b = bytes(self._m[k: k + 32]).ljust(32, b"\x00") if k < len(self._m) else bytes(32)
         return symbol_factory.BitVecVal(int.from_bytes(b, "big"), 256)
 
-    def write_word_at(self, index: int, value) -> None:
+    def write_word_at(self, index, value) -> None:
+        k, key = self._index(index)
+        pos = (lambda j: _add(index, j)) if key is not None else (lambda j: k + j)
         if isinstance(value, Expression) and value.symbolic:
             if isinstance(value, Bool):
                 value = If(value, symbol_factory.BitVecVal(1, 256), symbol_factory.BitVecVal(0, 256))
             for i in range(0, 256, 8):
-                self[index + 31 - i // 8] = Extract(i + 7, i, value)
+                self[pos(31 - i // 8)] = Extract(i + 7, i, value)
             return
-        v = concrete(value).to_bytes(32, "big")
-        for k in range(32):
-            self[index + k] = v[k]
+        v = (int(bool(value)) if isinstance(value, bool) else concrete(value)).to_bytes(32, "big")
+        for j in range(32):
+            self[pos(j)] = v[j]
 
     def raw(self) -> bytes:
         """Concrete bytes (a symbolic byte reads as 0)."""
         return bytes(self._m)
 
     def copy(self) -> "Memory":
-        return Memory(self._m, self._sym)
+        return Memory(self._m, self._sym, self._keys)
 
     __copy__ = copy
+
+
+def memory_key(raw: Node) -> Node:
+    """The key ``simplify(index)`` gives a symbolic memory index (memory.py:
+    167,200): the constants of a chain of bit-vector additions summed into one
+    trailing constant (0 dropped), the other operands in their order."""
+    terms, c = [], 0
+    stack = [raw]
+    while stack:
+        n = stack.pop()
+        if n.op == "bvadd" and n.width == 256:
+            stack.extend(reversed(n.args))
+        elif n.op == "const":
+            c = (c + n.param) & M256
+        else:
+            terms.append(n)
+    acc = terms[0] if terms else None
+    for t in terms[1:]:
+        acc = Node("bvadd", 256, (acc, t))
+    if acc is None:
+        return _const_node(c)
+    return acc if c == 0 else Node("bvadd", 256, (acc, _const_node(c)))
+
+
+def _const_node(c: int) -> Node:
+    from ..smt.expr import const
+    return const(c, 256)
+
+
+def _add(index, j: int):
+    """index + j as the reference's slice loops build it (a BitVec add)."""
+    if isinstance(index, Expression):
+        return index + symbol_factory.BitVecVal(j, 256) if j else index
+    return index + j
+
+
+def _slice_len(start, stop) -> int:
+    """memory.py:137-155: the slice length when stop - start folds to a
+    constant, else APPROX_ITR + 1 = 101 entries."""
+    d = _add(stop, 0) - start if isinstance(stop, Expression) else symbol_factory.BitVecVal(stop, 256) - start
+    return d.value if d.value is not None else 101
 
 
 class MachineState:

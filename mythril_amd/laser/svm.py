@@ -287,6 +287,32 @@ class LaserEVM:
         return final_states if track_gas else None
 
     # ------------------------------------------------------------- transactions
+    def sym_exec(self, world_state=None, target_address=None, creation_code=None,
+                 contract_name=None) -> None:
+        """svm.py:142-212: analyse a preconfigured world state (message calls
+        to ``target_address``) or, in scratch mode, run the symbolic creation
+        of ``creation_code`` and then the message calls to the new account."""
+        from .transaction import execute_symbolic_contract_creation
+        pre_configuration_mode = target_address is not None
+        scratch_mode = creation_code is not None and contract_name is not None
+        if pre_configuration_mode == scratch_mode:
+            raise ValueError("Symbolic execution started with invalid parameters")
+        for hook in self._start_sym_exec_hooks:
+            hook()
+        solver_mod.time_handler.start_execution(self.execution_timeout)
+        self.time = datetime.now()
+        if pre_configuration_mode:
+            self.open_states = [world_state]
+            self.execute_transactions(symbol_factory.BitVecVal(concrete(target_address), 256))
+        else:
+            created = execute_symbolic_contract_creation(self, creation_code, contract_name,
+                                                         world_state=world_state)
+            if len(self.open_states) == 0:
+                log.warning("No contract was created during the execution of contract creation")
+            self.execute_transactions(created.address)
+        for hook in self._stop_sym_exec_hooks:
+            hook()
+
     def execute_transactions(self, address) -> None:
         """svm.py:214-228: plugins may order transactions themselves
         (executed_transactions); otherwise transaction_count symbolic message
@@ -1231,8 +1257,12 @@ class LaserEVM:
                 self.escapes_dropped += 1
                 return              # svm.py:314-316: NotImplementedError -> continue
             # the device stopped the lane for this instruction's pre hooks first
-            # (hook mask), so they have run
-            new_states = self._escape_step(s, hooks_done=True, track_gas=track_gas, final_states=final_states)
+            # (hook mask), so they have run -- unless they are batch-safe device
+            # actions (laser/taint.py), which an escaping instruction never applied
+            batch_safe = (self._plan is not None and name is not None
+                          and OPCODES.get(name) in self._plan.safe)
+            new_states = self._escape_step(s, hooks_done=not batch_safe, track_gas=track_gas,
+                                           final_states=final_states)
             if new_states is None:
                 return
             self._filter_fork(new_states)

@@ -541,6 +541,8 @@ def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> La
     represent.  The lane is symbolic when any of them is, or its calldata or
     environment words are, or its storage base is the symbolic Array."""
     enc = _Encoder(node_cap, const_cap)
+    if state.mstate.memory.symbolic_keys:
+        raise NotEncodable("memory bytes at symbolic offsets")
     flags = lane_flags(state)
     storage = state.environment.active_account.storage
     symstore = not storage.concrete or (storage.is_chain and any(

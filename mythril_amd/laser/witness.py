@@ -62,7 +62,8 @@ class WitnessSeeds:
     kept)."""
 
     def __init__(self, codes: Sequence[bytes], n: int = 1024, seed: int = 0x5EED5EED,
-                 storage_names: Iterable[str] = (), manager: KeccakFunctionManager = keccak_function_manager):
+                 storage_names: Iterable[str] = (), manager: KeccakFunctionManager = keccak_function_manager,
+                 balance_names: Iterable[str] = ()):
         self.n = n
         self.rng = np.random.default_rng(seed)
         sel = []
@@ -72,9 +73,15 @@ class WitnessSeeds:
         self.storage_names = list(storage_names)
         self.km = manager
         self.assign: List[Dict[str, object]] = [{} for _ in range(n)]
-        for a in self.assign:
+        # balances (world_state.py:31-33 Array("balance")): every account starts
+        # with the same balance, a few ether, mostly (reachable under
+        # analysis/solver.py's 100 / 1000 ether bounds; 0 for some seeds)
+        self.balance_names = list(balance_names)
+        for m, a in enumerate(self.assign):
             for name in self.storage_names:
                 a[name] = ArrayInterp(0, {})
+            for name in self.balance_names:
+                a[name] = ArrayInterp(0 if m % 8 == 7 else 10 ** (18 + m % 3), {})
         self.tx_ids: List[str] = []
         self._done: List[Dict[Node, int]] = [{} for _ in range(n)]   # keccak input -> value, per seed
         self._next: List[Dict[int, int]] = [{} for _ in range(n)]    # next free slot per input size

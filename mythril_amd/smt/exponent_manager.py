@@ -32,6 +32,9 @@ class ExponentFunctionManager:
         # concrete (base, exponent) -> power of every EXP registered so far (what
         # a model must interpret Power as; laser/witness.py completes seeds with it)
         self.concrete_points = {(256, i): 256 ** i for i in range(32)}
+        # (base, exponent) of every EXP with a symbolic operand (host bookkeeping:
+        # a candidate model interprets Power at their values, laser/witness.py)
+        self.symbolic_points = []
 
     def create_condition(self, base: BitVec, exponent: BitVec) -> Tuple[BitVec, Bool]:
         power = Function("Power", [256, 256], 256)
@@ -41,6 +44,7 @@ class ExponentFunctionManager:
                                              annotations=base.annotations.union(exponent.annotations))
             self.concrete_points[(base.value, exponent.value)] = const.value
             return const, const == exponentiation
+        self.symbolic_points.append((base, exponent))
         constraint = And(exponentiation > 0, self.concrete_constraints)
         if base.value == 256:
             constraint = And(constraint,

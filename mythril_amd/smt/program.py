@@ -29,7 +29,7 @@ OPCODE = {name: i for i, name in enumerate(OPS)}
 UNARY = {"copy", "bvnot", "bvneg", "not", "extract", "zero_extend", "sign_extend"}
 REF_ACC, REF_SLOT, REF_VAR, REF_CONST = 0, 1, 2, 3
 TAB_PART_SHIFT, TAB_LO_SHIFT, TAB_INDEX_MASK = 20, 21, (1 << 20) - 1
-MAX_SLOTS = 8
+MAX_SLOTS = 16       # kernel 2's 4-bit slot field (BV_MAX_SLOTS)
 TILE_INSNS = 2048
 
 

@@ -257,7 +257,7 @@ class ModelCache:
         self._compiler = None                 # persistent: conjunct programs are compiled once
         self._progs: Dict[Node, object] = {}
         self.part_evals = 0            # conjunct programs x models run on kernel 2
-        self.stats = {"queries": 0, "lru_hits": 0, "seed_hits": 0, "misses": 0}
+        self.stats = {"queries": 0, "lru_hits": 0, "seed_hits": 0, "misses": 0, "divergences": 0}
 
     @property
     def device(self):
@@ -364,32 +364,7 @@ class ModelCache:
                 distinct[c] = None
         plist = [c for c in distinct if c.op != "const"]
         words = (len(pool) + 63) // 64
-        rows: Dict[Node, np.ndarray] = {}
-        if plist:
-            # every conjunct is compiled once per cache, by one compiler whose
-            # index spaces only grow (flatten.batch_from)
-            if self._compiler is None:
-                self._compiler = Compiler()
-            progs, kept = [], []
-            for c in plist:
-                pr = self._progs.get(c, _MISSING)
-                if pr is _MISSING:
-                    try:
-                        pr = self._compiler.compile(c)
-                    except Unsupported:
-                        pr = None
-                    self._progs[c] = pr
-                if pr is not None:
-                    progs.append(pr)
-                    kept.append(c)
-            if kept:
-                prog = batch_from(self._compiler, progs)
-                _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
-                self.part_evals += len(kept) * len(pool)
-                self.device_ms += float(ms or 0.0)
-                self.launches += 1
-                for row, c in enumerate(kept):
-                    rows[c] = bits[row]
+        rows = self.conjunct_rows(plist, pool)
         ones = np.zeros(words, dtype=np.uint64)
         for i in range(len(pool)):
             ones[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
@@ -419,6 +394,38 @@ class ModelCache:
         if keep:
             self._bits.update(out)
         return out
+
+    def conjunct_rows(self, conjuncts: Sequence[Node], pool: List) -> Dict[Node, np.ndarray]:
+        """Per conjunct, the bitmap of the pool's models that satisfy it, from
+        ONE kernel-2 launch; conjuncts the device does not evaluate get no row.
+        Every conjunct is compiled once per cache, by one compiler whose index
+        spaces only grow (flatten.batch_from)."""
+        rows: Dict[Node, np.ndarray] = {}
+        if not conjuncts or not pool:
+            return rows
+        if self._compiler is None:
+            self._compiler = Compiler()
+        progs, kept = [], []
+        for c in conjuncts:
+            pr = self._progs.get(c, _MISSING)
+            if pr is _MISSING:
+                try:
+                    pr = self._compiler.compile(c)
+                except Unsupported:
+                    pr = None
+                self._progs[c] = pr
+            if pr is not None:
+                progs.append(pr)
+                kept.append(c)
+        if kept:
+            prog = batch_from(self._compiler, progs)
+            _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
+            self.part_evals += len(kept) * len(pool)
+            self.device_ms += float(ms or 0.0)
+            self.launches += 1
+            for row, c in enumerate(kept):
+                rows[c] = bits[row]
+        return rows
 
     # -- witness seeds and prefetched groups ------------------------------------
     def _seed_models(self) -> List:
@@ -644,20 +651,44 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         if ret_model:
             model_cache.stats["lru_hits"] += 1
             return ret_model
-        seed = model_cache.check_seeds(key)
-        if seed is not None:
-            # a model of the query, as the backend would have returned one
-            model_cache.stats["seed_hits"] += 1
-            model_cache.put(seed, 1)
-            return seed
+        if _seeds_first():
+            # no solver that can refute: a seed model of the query is what the
+            # backend would return (the SAT-only backend searches from them)
+            seed = model_cache.check_seeds(key)
+            if seed is not None:
+                model_cache.stats["seed_hits"] += 1
+                model_cache.put(seed, 1)
+                return seed
         model_cache.stats["misses"] += 1
     if args.solver_log:
         from .smtlib import log_query, to_smt2
         log_query(args.solver_log, to_smt2(constraints, minimize, maximize))
     fut = _speculative.pop(_spec_key(constraints, minimize, maximize), None)
-    model = fut.result() if fut is not None else solver_backend(constraints, minimize, maximize, timeout)
+    try:
+        model = fut.result() if fut is not None else solver_backend(constraints, minimize, maximize, timeout)
+    except SolverTimeOutException:
+        # a real solver timed out: the reference prunes here (constraints.py:
+        # 35-38).  A witness seed that satisfies the query keeps the path
+        # instead -- a divergence from the reference, counted
+        if not minimize and not maximize and not _seeds_first():
+            seed = model_cache.check_seeds(simplify(And(*constraints)).raw)
+            if seed is not None:
+                model_cache.stats["divergences"] += 1
+                model_cache.put(seed, 1)
+                return seed
+        raise
     model_cache.put(model, 1)
     return model
+
+
+def _seeds_first() -> bool:
+    """Witness seeds are consulted before the backend only when the backend
+    cannot refute anything (the built-in one, or the SAT-only search, which
+    starts from the seeds itself).  With a real SMT backend installed the
+    backend answers first, as the reference's z3 does, so the models that
+    reach the LRU -- and later quick-sat choices (arbitrary_jump.py:29-40) --
+    are the backend's."""
+    return solver_backend is _no_backend or bool(getattr(solver_backend, "uses_seeds", False))
 
 
 # ------------------------------------------------------------------ fallback pool

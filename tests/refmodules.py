@@ -320,7 +320,11 @@ def get_transaction_sequence(state, constraints):
     """analysis/solver.py get_transaction_sequence, stubbed: UnsatError when the
     (constant) constraint set is unsat, else the ids of the path's transactions
     (the concrete model the reference would minimise is not rebuilt here)."""
-    if not _sat(constraints):
+    try:
+        sat = _sat(constraints)
+    except NotImplementedError:          # symbolic: the SAT-only backend decides (or not)
+        return get_transaction_sequence_sat(state, constraints)
+    if not sat:
         raise UnsatError()
     return {"steps": [str(getattr(tx, "id", tx)) for tx in state.world_state.transaction_sequence]}
 
@@ -459,3 +463,193 @@ class StateChangeAfterCall(_Base):
         if len(annotations) == 0:
             return []
         return [(self.swc_id, state.get_current_instruction()["address"], state.environment.code.bytecode)]
+
+
+# ------------------------------------------------ issue confirmation (SAT only)
+class ConfirmationUnknown(UnsatError):
+    """A confirmation the SAT-only backend could not decide: neither a model
+    nor a proof of unsat.  Modules treat it as the reference treats UnsatError
+    (no issue); CONFIRMATIONS counts it apart."""
+
+
+CONFIRMATIONS = {"sat": 0, "unknown": 0}
+
+
+def _sat_or_unknown(call):
+    """Run a get_model-style call under the SAT-only backend: a model, or
+    ConfirmationUnknown (SolverBackendMissing: no candidate satisfied and no
+    solver can say more)."""
+    from mythril_amd.smt.solver import SolverBackendMissing
+    from mythril_amd.smt.solver import UnsatError as SmtUnsat
+    try:
+        model = call()
+    except SolverBackendMissing:
+        CONFIRMATIONS["unknown"] += 1
+        raise ConfirmationUnknown()
+    except SmtUnsat:
+        raise UnsatError()
+    CONFIRMATIONS["sat"] += 1
+    return model
+
+
+def get_model(constraints):
+    """analysis/solver.py's ``get_model`` (support/model.py:21-82) as the
+    modules call it, through the product's kernel-2 path."""
+    from mythril_amd.smt import solver
+    return _sat_or_unknown(lambda: solver.get_model(tuple(constraints)))
+
+
+def _minimisation_constraints(state, constraints):
+    """analysis/solver.py:219-259 _set_minimisation_constraints: calldata size
+    bound, caller / account starting-balance bounds; the minimised terms."""
+    from mythril_amd.smt.expr import UGE
+    ws = state.world_state
+    out, minimize = list(constraints), []
+    for tx in ws.transaction_sequence:
+        out.append(UGE(symbol_factory.BitVecVal(5000, 256), tx.call_data.calldatasize))
+        minimize.append(tx.call_data.calldatasize)
+        minimize.append(tx.call_value)
+        out.append(UGE(symbol_factory.BitVecVal(10 ** 21, 256), ws.starting_balances[
+            tx.caller if hasattr(tx.caller, "raw") else symbol_factory.BitVecVal(int(tx.caller), 256)]))
+    for account in ws.accounts.values():
+        out.append(UGE(symbol_factory.BitVecVal(10 ** 20, 256), ws.starting_balances[account.address]))
+    return out, tuple(minimize)
+
+
+def get_transaction_sequence_sat(state, constraints):
+    """analysis/solver.py:54-104 get_transaction_sequence over the SAT-only
+    backend: the same tx constraints and minimised terms, through get_model
+    (the backend minimises by descent, it does not prove optimality).  Returns
+    {"steps": [{"input", "value", "origin", "address"}]} as
+    _get_concrete_transaction builds it (solver.py:191-219)."""
+    from mythril_amd.laser.transaction import ContractCreationTransaction
+    from mythril_amd.smt import solver
+    from mythril_amd.smt.solver import Constraints
+    cons, minimize = _minimisation_constraints(state, constraints)
+    model = _sat_or_unknown(lambda: solver.get_model(Constraints(cons), minimize=minimize))
+    steps = []
+    def word(x):
+        return x if hasattr(x, "raw") else symbol_factory.BitVecVal(int(x), 256)
+    for tx in state.world_state.transaction_sequence:
+        cd = tx.call_data
+        size = model.eval(cd.calldatasize.raw, model_completion=True).param
+        data = bytes(model.eval(cd[k].raw, model_completion=True).param for k in range(min(size, 5000)))
+        inp = (tx.code.raw.hex() if isinstance(tx, ContractCreationTransaction) else "") + data.hex()
+        steps.append({"input": "0x" + inp,
+                      "value": hex(model.eval(word(tx.call_value).raw, model_completion=True).param),
+                      "origin": "0x%040x" % model.eval(word(tx.caller).raw, model_completion=True).param,
+                      "address": "" if isinstance(tx, ContractCreationTransaction)
+                      else hex(tx.callee_account.address.value)})
+    return {"steps": steps}
+
+
+# ---------------------------------------------------------------- suicide.py
+class AccidentallyKillable(_Base):
+    """analysis/module/modules/suicide.py:25-120: a SELFDESTRUCT any sender
+    reaches is an issue; the first confirmation asks the beneficiary to be the
+    attacker, the fallback drops that.  An issue is (swc, address, withdraws,
+    bytecode) with the transaction sequence kept on the annotation."""
+    swc_id = "106"
+    pre_hooks = ["SELFDESTRUCT"]
+    post_hooks: List[str] = []
+
+    def _execute(self, state):
+        from mythril_amd.laser.transaction import ACTORS, ContractCreationTransaction
+        instruction = state.get_current_instruction()
+        to = state.mstate.stack[-1]
+        attacker = symbol_factory.BitVecVal(ACTORS["ATTACKER"], 256)
+        attacker_constraints = []
+        for tx in state.world_state.transaction_sequence:
+            if not isinstance(tx, ContractCreationTransaction):
+                attacker_constraints.append(And(tx.caller == attacker, tx.caller == tx.origin))
+        try:
+            try:
+                constraints = list(state.world_state.constraints) + [to == attacker] + attacker_constraints
+                seq = get_transaction_sequence_sat(state, constraints)
+                withdraws = True
+            except UnsatError:
+                constraints = list(state.world_state.constraints) + attacker_constraints
+                seq = get_transaction_sequence_sat(state, constraints)
+                withdraws = False
+        except UnsatError:
+            return []
+        issue = (self.swc_id, instruction["address"], withdraws, state.environment.code.bytecode)
+        state.annotate(IssueAnnotation(conditions=[And(*constraints)], issue=(issue, seq), detector=self))
+        return [issue]
+
+
+# ------------------------------------------------ ether_thief.py + potential_issues.py
+class PotentialIssue:
+    """analysis/potential_issues.py:10-62 (the fields check_potential_issues uses)."""
+
+    def __init__(self, address, swc_id, bytecode, detector, constraints=None):
+        self.address = address
+        self.swc_id = swc_id
+        self.bytecode = bytecode
+        self.detector = detector
+        self.constraints = constraints or []
+
+
+def check_potential_issues(state) -> None:
+    """analysis/potential_issues.py:93-140: at a kept transaction end, each
+    potential issue whose constraints (with the path's) have a transaction
+    sequence becomes an issue of its detector; the others stay potential."""
+    annotation = get_potential_issues_annotation(state)
+    unsat = []
+    for p in annotation.potential_issues:
+        if not isinstance(p, PotentialIssue):
+            unsat.append(p)
+            continue
+        try:
+            seq = get_transaction_sequence_sat(state, list(state.world_state.constraints) + p.constraints)
+        except UnsatError:
+            unsat.append(p)
+            continue
+        issue = (p.swc_id, p.address, p.bytecode)
+        state.annotate(IssueAnnotation(detector=p.detector, issue=(issue, seq),
+                                       conditions=[And(*(list(state.world_state.constraints) + p.constraints))]))
+        p.detector.issues.append(issue)
+        p.detector.update_cache([issue])
+        p.detector.sequences.append(seq)
+    annotation.potential_issues = unsat
+
+
+class EtherThief(_Base):
+    """analysis/module/modules/ether_thief.py:23-99: after a CALL / STATICCALL,
+    a potential issue when the attacker's balance can end above its starting
+    balance (pre-solved with get_model); confirmed at the transaction end."""
+    swc_id = "105"
+    pre_hooks: List[str] = []
+    post_hooks = ["CALL", "STATICCALL"]
+
+    def __init__(self):
+        super().__init__()
+        self.sequences = []
+
+    def update_cache(self, issues=None):
+        for issue in issues or self.issues:
+            self.cache.add((issue[1], issue[-1]))
+
+    def _execute(self, state):
+        potential = self._analyze_state(state)
+        get_potential_issues_annotation(state).potential_issues.extend(potential)
+
+    def _analyze_state(self, state):
+        from mythril_amd.laser.transaction import ACTORS
+        from mythril_amd.smt.expr import UGT
+        state = copy(state)
+        instruction = state.get_current_instruction()
+        attacker = symbol_factory.BitVecVal(ACTORS["ATTACKER"], 256)
+        ws = state.world_state
+        constraints = list(ws.constraints) + [
+            UGT(ws.balances[attacker], ws.starting_balances[attacker]),
+            state.environment.sender == attacker,
+            state.current_transaction.caller == state.current_transaction.origin,
+        ]
+        try:
+            get_model(list(constraints))
+        except UnsatError:
+            return []
+        return [PotentialIssue(address=instruction["address"] - 1, swc_id=self.swc_id,
+                               bytecode=state.environment.code.bytecode, detector=self,
+                               constraints=constraints)]

@@ -250,15 +250,17 @@ class Engine:
         return [n]
 
     # ---- memory, storage and SHA3 of a symbolic state ----------------------------
-    def _memstore(self, s, op):
+    def _memstore(self, s, op, state=None):
         """instructions.py:1013-1051 (sha3_), 1437-1518 (mload_ .. sstore_) on the
         host's Memory / Storage restatements (memory.py, account.py): the
         oracle's projection decides status, gas and memory size, the values are
         the reference's expressions."""
         ms, env = s.mstate, s.environment
         st = ms.stack
-        if op in (0x20, 0x51, 0x52, 0x53) and _val(st[-1]) is None:
-            raise Unsupported("symbolic memory offset")
+        if op in (0x51, 0x52, 0x53) and _val(st[-1]) is None:
+            return self._symbolic_offset(state if state is not None else s, s, op)
+        if op == 0x20 and _val(st[-1]) is None:
+            raise Unsupported("symbolic SHA3 offset")
         if op == 0x20 and _val(st[-2]) is None:
             raise Unsupported("symbolic SHA3 length")
         b = self._oracle_run(s)
@@ -295,6 +297,45 @@ class Engine:
             st.append(keccak_function_manager.create_keccak(data))
         return [s]
 
+    def _symbolic_offset(self, state, s, op):
+        """mload_ / mstore_ / mstore8_ (instructions.py:1437-1485) at a symbolic
+        offset: mem_extend extends nothing, the bytes live at symbolic keys
+        (memory.py:117-203), table gas only."""
+        ms = s.mstate
+        st = ms.stack
+        off = st.pop()
+        if op == 0x51:
+            st.append(ms.memory.get_word_at(off))
+        elif op == 0x52:
+            ms.memory.write_word_at(off, st.pop())
+        else:
+            v = st.pop()
+            ms.memory[off] = (_val(v) % 256) if _val(v) is not None else Extract(7, 0, _pop_bitvec(v))
+        gmin, gmax = _GAS[op]
+        ms.min_gas_used += gmin
+        ms.max_gas_used += gmax
+        if ms.min_gas_used > 10 ** 9 or ms.min_gas_used >= _gas_limit(s):
+            return self._vmexc(state)
+        ms.pc += 1
+        return [s]
+
+    def _halt_symbolic(self, state, s, op):
+        """return_ / revert_ (instructions.py:1857-1934) with a symbolic offset
+        or length: the return data stays symbolic (the reference logs "not
+        supported") and the transaction ends; RETURN's mem_extend of a symbolic
+        range extends nothing."""
+        ms = s.mstate
+        off, length = ms.stack.pop(), ms.stack.pop()
+        tx = s.current_transaction
+        if op == 0xF3 and isinstance(tx, ContractCreationTransaction):
+            raise Unsupported("a creation returning code at a symbolic range")
+        if op == 0xF3 and ms.min_gas_used >= _gas_limit(s):
+            return self._vmexc(state)
+        if self.signals:
+            tx.end(s, return_data=None, revert=op == 0xFD)
+        self.ended.append(("revert" if op == 0xFD else "return", s))
+        return []
+
     # ---- one instruction ----------------------------------------------------------
     def step(self, state):
         s = copy(state)
@@ -309,6 +350,8 @@ class Engine:
         if op in _HOST_OPS:
             self.host_ops[name] += 1
             return self._host_op(state, s, op, name)
+        if op in (0xF3, 0xFD) and len(st) >= 2 and (_val(st[-1]) is None or _val(st[-2]) is None):
+            return self._halt_symbolic(state, s, op)
         nin = {"DUP": int(name[3:]) if name.startswith("DUP") else 0,
                "SWAP": int(name[4:]) + 1 if name.startswith("SWAP") else 0}
         reads = nin["DUP"] or nin["SWAP"] or _POPS.get(op, 0)
@@ -318,7 +361,7 @@ class Engine:
         sym_env = env_attr is not None and _val(getattr(env, env_attr)) is None
         if op in (0x20, 0x51, 0x52, 0x53, 0x54, 0x55) and _symbolic_state(s) and len(st) >= _POPS[op]:
             s.environment.active_account.storage.to_chain()
-            return self._memstore(s, op)
+            return self._memstore(s, op, state)
         creation = isinstance(s.current_transaction, ContractCreationTransaction)
         if symcd and (op == 0x37 or (creation and op in (0x38, 0x39))) and len(st) >= _POPS.get(op, 0):
             out = self._calldata_ops(state, s, op, creation)

@@ -94,14 +94,11 @@ def ULT_x():
     return ULT(symbol_factory.BitVecSym("x", 256), symbol_factory.BitVecVal(3, 256))
 
 
-@pytest.mark.parametrize("fetch", ["lds", "scalar", "pair"])
-def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
-    """The scalar-load fetch is the default; MG_BV_PROG=lds stages the program tile
-    in LDS, MG_BV_PROG=pair evaluates two models per thread (k_bv_eval_pair).
-    All read at upload, all equal the oracle (plain ops and tables; 333 and 300
-    models: a partial second model half in pair mode)."""
+def test_plain_ops_and_tables_equal_oracle(dev):
+    """The shipped kernel (scalar-load instruction fetch) on C4-mix programs and on
+    array / function-table sets equals the oracle (333 and 300 models: partial
+    model chunks)."""
     from test_smt_programs import _random_table_constraints, _random_table_models
-    monkeypatch.setenv("MG_BV_PROG", fetch)
     prog = synth.c4_programs(synth.Draws(900, seed=synth.C4_SEED + 9))
     models = synth.c4_models(333, seed=19)
     fs, sc, _ = dev.eval(prog, models)
@@ -116,16 +113,46 @@ def test_both_instruction_fetch_modes_equal_oracle(dev, monkeypatch, fetch):
     assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
 
 
-@pytest.mark.parametrize("mode", ["scalar", "pair"])
+def test_sixteen_slot_programs_equal_oracle(dev):
+    """Programs that keep up to 16 values live (128 KiB of LDS per block): a
+    balanced sum tree of distinct variable products needs a slot per pending
+    subtree, and a path's balance store chain read at several keys."""
+    from mythril_amd.smt.expr import Array, UGT, symbol_factory
+    BVS = symbol_factory.BitVecSym
+    xs = [BVS(f"x{k}", 256) for k in range(24)]
+
+    def tree(lo, hi):
+        if hi - lo == 1:
+            return xs[lo] * xs[(lo + 7) % 24]
+        mid = (lo + hi) // 2
+        return tree(lo, mid) + tree(mid, hi)
+    bal = Array("balance", 256, 256)
+    for k in range(6):
+        bal[xs[k]] = bal[xs[k]] + xs[k + 6]
+    sets = [[tree(0, 24) == xs[0]], [UGT(bal[xs[1]] + bal[xs[2]] * bal[xs[3]], bal[xs[4]] - bal[xs[5]])]]
+    prog, kept = compile_sets(sets)
+    assert kept == [0, 1] and prog.n_slots > 8
+    rng = random.Random(16)
+    from mythril_amd.smt.program import ArrayInterp
+    models = []
+    for m in range(700):
+        a = {f"x{k}": rng.choice([0, 1, 2, rng.getrandbits(256), rng.getrandbits(8)]) for k in range(24)}
+        a["balance"] = ArrayInterp(rng.getrandbits(64), {a["x1"]: rng.getrandbits(256)})
+        models.append(a)
+    pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables)
+    fs, sc, _ = dev.eval(prog, pool)
+    rfs, rsc = eval_batch(prog, pool)
+    assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
+
+
 @pytest.mark.parametrize("w", [8, 64, 255, 256])
-def test_division_class_ops_at_every_width(dev, w, mode, monkeypatch):
+def test_division_class_ops_at_every_width(dev, w):
     """UDIV UREM SDIV SREM SMOD and the unsigned multiply-overflow test share one
     division site in the kernel (bv_divop): each op at width w, against values
     at the sign / zero / all-ones edges (z3 zero-divisor semantics)."""
     from mythril_amd.smt.expr import (BVMulNoOverflow, SDiv, SMod, SRem, UDiv, URem,
                                       symbol_factory)
     BVS = symbol_factory.BitVecSym
-    monkeypatch.setenv("MG_BV_PROG", mode)
     x, y, z = BVS("x", w), BVS("y", w), BVS("z", w)
     sets = []
     for f in (UDiv, URem, SDiv, SRem, SMod):
@@ -152,21 +179,6 @@ def test_division_class_ops_at_every_width(dev, w, mode, monkeypatch):
     rfs, rsc = eval_batch(prog, pool)
     assert np.array_equal(fs, rfs) and np.array_equal(sc, rsc)
     assert (sc[:10] > 0).all()
-
-
-def test_pair_mode_bitmaps_equal_single_mode(dev, monkeypatch):
-    """mg_eval_bits in pair mode: per-model bitmaps (the LRU replay input) equal
-    the single-model kernel's, with a model count that leaves the second half
-    of the last pair partly empty."""
-    prog = synth.c4_programs(synth.Draws(700, seed=synth.C4_SEED + 13))
-    models = synth.c4_models(1100, seed=23)
-    out = {}
-    for mode in ("scalar", "pair"):
-        monkeypatch.setenv("MG_BV_PROG", mode)
-        out[mode] = dev.eval_bits(prog, models)
-    for k in range(3):
-        assert np.array_equal(out["scalar"][k], out["pair"][k])
-    assert int(out["pair"][1].sum()) > 0
 
 
 def _fusable_programs(n_dags, seed):
@@ -244,14 +256,12 @@ def test_fused_programs_equal_unfused_and_oracle(dev, monkeypatch):
                        (synth.c4_programs(synth.Draws(500, seed=synth.C4_SEED + 29)), synth.c4_models(300, seed=31))):
         pool = pool or ModelPool.from_dicts(models, prog.var_names, prog.var_widths)
         out = {}
-        # all shapes (the default), wide tails only, no tails, pairs only, no binary-op
-        # shape, none
-        for fuse in ("5", "4", "3", "2", "1", "0"):
+        # all shapes (the shipped default) and none (MG_BV_FUSE=0)
+        for fuse in ("5", "0"):
             monkeypatch.setenv("MG_BV_FUSE", fuse)
             out[fuse] = dev.eval_bits(prog, pool)
         for k in range(3):
-            for fuse in ("5", "4", "3", "2", "1"):
-                assert np.array_equal(out[fuse][k], out["0"][k]), fuse
+            assert np.array_equal(out["5"][k], out["0"][k])
         rfs, rsc = eval_batch(prog, pool)
         assert np.array_equal(out["5"][0], rfs) and np.array_equal(out["5"][1], rsc)
         assert 0 < int(out["5"][1].sum()) < prog.n_dags * pool.n_models

@@ -265,3 +265,39 @@ def test_accumulator_is_only_operand_a():
     for w, op in zip(c4.insns, ops4):
         nref = 3 if op == OPCODE["ite"] else (1 if op in unary else 2)
         assert all(int(w[1 + k]) >> 30 != REF_ACC for k in range(1, nref))
+
+
+def test_programs_with_more_than_eight_live_values():
+    """The flattener allows 16 slots (kernel 2's 4-bit slot field): a set that
+    keeps 10 values live compiles, and the oracle evaluator agrees with the
+    pure-Python DAG evaluation on it."""
+    import random as _r
+    from mythril_amd.smt.expr import Array, UGT, symbol_factory
+    from mythril_amd.smt.program import ArrayInterp, ModelPool
+    from oracle.bv_ref import eval_batch
+    from smt_eval import evaluate
+    BVS = symbol_factory.BitVecSym
+    xs = [BVS(f"x{k}", 256) for k in range(24)]
+
+    def tree(lo, hi):
+        if hi - lo == 1:
+            return xs[lo] * xs[(lo + 7) % 24]
+        mid = (lo + hi) // 2
+        return tree(lo, mid) + tree(mid, hi)
+    bal = Array("balance", 256, 256)
+    for k in range(6):
+        bal[xs[k]] = bal[xs[k]] + xs[k + 6]
+    sets = [[tree(0, 24) == xs[0]], [UGT(bal[xs[1]] + bal[xs[2]] * bal[xs[3]], bal[xs[4]] - bal[xs[5]])]]
+    prog, kept = compile_sets(sets)
+    assert kept == [0, 1] and 8 < prog.n_slots <= 16
+    rng = _r.Random(16)
+    models = []
+    for m in range(60):
+        a = {f"x{k}": rng.choice([0, 1, 2, rng.getrandbits(256), rng.getrandbits(8)]) for k in range(24)}
+        a["balance"] = ArrayInterp(rng.getrandbits(64), {a["x1"]: rng.getrandbits(256)})
+        models.append(a)
+    pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables)
+    fs, sc = eval_batch(prog, pool)
+    for d, s_ in enumerate(sets):
+        vals = [evaluate(s_[0].raw, m) for m in models]
+        assert (next((i for i, v in enumerate(vals) if v), 0xFFFFFFFF), sum(vals)) == (fs[d], sc[d])
