@@ -78,6 +78,35 @@ def allgather_models(values: np.ndarray) -> np.ndarray:
     return np.concatenate(out, axis=0)
 
 
+def alltoall_bytes(blobs: Sequence[bytes]) -> List[bytes]:
+    """Point-to-point exchange of byte payloads: ``blobs[q]`` goes to rank q, the
+    result's entry r is what rank r sent here.  Two all-to-alls (the sizes, then
+    the bytes with per-rank split sizes): every payload crosses the fabric once,
+    between the two ranks that need it -- on xGMI a direct link per pair --
+    instead of every rank receiving every rank's outgoing states."""
+    import torch
+    import torch.distributed as dist
+    rank, world = rank_world()
+    if world == 1:
+        return [bytes(blobs[0])] if blobs else [b""]
+    dev = _device()
+    sizes = torch.tensor([len(b) for b in blobs], dtype=torch.int64, device=dev)
+    got = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(got, sizes)
+    send_sz, recv_sz = [len(b) for b in blobs], [int(x) for x in got.cpu().tolist()]
+    buf = np.frombuffer(b"".join(bytes(b) for b in blobs), dtype=np.uint8) if sum(send_sz) else \
+        np.zeros(0, dtype=np.uint8)
+    send = torch.from_numpy(buf.copy()).to(dev)
+    recv = torch.empty(sum(recv_sz), dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv, send, output_split_sizes=recv_sz, input_split_sizes=send_sz)
+    data = recv.cpu().numpy().tobytes()
+    out, at = [], 0
+    for n in recv_sz:
+        out.append(data[at: at + n])
+        at += n
+    return out
+
+
 def reduce_timing(elapsed: float, work: float) -> Tuple[float, float]:
     """(max elapsed over ranks, total work over ranks): whole-job throughput =
     total / max (bench.py contract)."""

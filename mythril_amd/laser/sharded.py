@@ -381,8 +381,9 @@ def rebalance(laser_evm) -> List[int]:
     """SURVEY §8(e) rebalancing at a transaction boundary: the open world
     states of all ranks, in rank-major order, are re-dealt in equal contiguous
     runs (rank r gets positions [t_r, t_r + n_r), n_r = total // world, the
-    first total % world ranks one more).  Only states that change owner move
-    (one all-gather of pickled states; expression nodes as flat tables).
+    first total % world ranks one more).  Only states that change owner move,
+    each straight to its new owner (one all-to-all of pickled states, dist.
+    alltoall_bytes; expression nodes as flat tables).
     Returns the per-rank counts before the move."""
     from .. import dist as mdist
     rank, world = mdist.rank_world()
@@ -407,10 +408,10 @@ def rebalance(laser_evm) -> List[int]:
         (keep if q == rank else send.setdefault(q, [])).append((g, ws))
     objs = _shared_objects(laser_evm)
     shared = {id(o): k for k, o in enumerate(objs)}
-    blob = _dumps_states(send, shared) if send else b""
-    import torch.distributed as dist
-    parts: List[Optional[bytes]] = [None] * world
-    dist.all_gather_object(parts, blob)
+    # one payload per destination, exchanged point to point (an all-to-all):
+    # a state crosses the fabric once, to the rank that takes it over
+    blobs = [_dumps_states({q: send[q]}, shared) if send.get(q) else b"" for q in range(world)]
+    parts = mdist.alltoall_bytes(blobs)
     got = list(keep)
     for r, b in enumerate(parts):
         if r == rank or not b:

@@ -85,3 +85,28 @@ def test_model_allgather_feeds_every_candidate_pool():
         assert xs[1:] == [5 + r for r in range(world) if r != rank]   # peers in rank order
         assert sorted(defaults) == [0, 1, 2]
         assert all({(7 + r,): 9} in ents for r in range(world))
+
+
+def _a2a_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mythril_amd import dist as mdist
+        # rank r sends q bytes of value 10 r + q to rank q (nothing to itself when q = 0)
+        blobs = [bytes([10 * rank + q]) * q for q in range(world)]
+        out[rank] = [list(b) for b in mdist.alltoall_bytes(blobs)]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_alltoall_bytes_delivers_each_payload_to_its_rank():
+    """rebalance's exchange (laser/sharded.py): payload q of rank r arrives at
+    rank q as entry r, empty payloads included, at 2 and 3 ranks."""
+    for world in (2, 3):
+        port = _free_port()
+        with mp.Manager() as m:
+            out = m.dict()
+            mp.spawn(_a2a_worker, args=(world, port, out), nprocs=world)
+            got = dict(out)
+        for q in range(world):
+            assert got[q] == [[10 * r + q] * q for r in range(world)]

@@ -98,3 +98,38 @@ def test_witness_seeds_satisfy_the_keccak_axioms():
     cond = keccak_function_manager.create_conditions()
     for m in seeds.models():
         assert m.eval(cond.raw, model_completion=True).param == 1
+
+
+def test_refuting_backend_prunes_and_counts_divergences(monkeypatch):
+    """With a real (here: stub) backend installed the backend answers before the
+    witness seeds (mythril_amd/smt/solver.py _seeds_first); an UNSAT prunes, a
+    timeout prunes unless a seed satisfies the query -- then the path is kept
+    and counted as a divergence."""
+    import symcases
+    import symref
+    from test_gpu_fork_filter import StubBackend
+    from mythril_amd import workloads
+    from mythril_amd.laser import BreadthFirstSearchStrategy, LaserEVM
+    from mythril_amd.laser.transaction import tx_id_manager
+    from mythril_amd.smt.keccak_manager import keccak_function_manager
+    keccak_function_manager.reset()
+    tx_id_manager.restart_counter()
+    solver.get_model.cache_clear()
+    monkeypatch.setattr(solver.args, "pruning_factor", 1)
+    mc = solver.ModelCache(device=OracleK2())
+    monkeypatch.setattr(solver, "model_cache", mc)
+    be = StubBackend()
+    monkeypatch.setattr(solver, "solver_backend", be)
+    name = "overflow.sol.o"
+    ws, addr = symcases.deploy(OracleDevice(), name)
+    mc.seed_source = WitnessSeeds([workloads.bytecode(name)], n=48, storage_names=[f"Storage{addr}"])
+    eng = symref.Engine()
+    laser = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=2,
+                     execution_timeout=0, escape_handler=lambda st: eng.step(st))
+    laser.open_states = [ws]
+    laser.execute_transactions(addr)
+    assert be.calls > 0
+    assert laser.fork_stats["pruned"] > 0
+    assert mc.stats["divergences"] > 0, (laser.fork_stats, mc.stats)
+    assert mc.stats["seed_hits"] == 0            # seeds never pre-empt a real backend
+    solver.get_model.cache_clear()

@@ -60,13 +60,35 @@ class _CountingK2:
         return self.dev.eval_bits(prog, pool)
 
 
-def _run(name, k1, k2, monkeypatch, n_seeds=48):
+class StubBackend:
+    """A stand-in SMT backend that refutes a fixed subset of queries: UNSAT
+    when the query has an even number (at least 4) of leaf conjuncts, a solver
+    timeout otherwise (constraints.py:35-38: a timeout prunes with the default timeout;
+    get_model then tries the witness seeds, a counted divergence).  Decisions
+    depend only on the query, so two runs that pose the same queries prune the
+    same paths."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def __call__(self, constraints, minimize, maximize, timeout):
+        from mythril_amd.smt.solver import SolverTimeOutException, UnsatError, _conjuncts, query_raw
+        self.calls += 1
+        n = len(_conjuncts(query_raw(constraints)))
+        if n >= 4 and n % 2 == 0:
+            raise UnsatError()
+        raise SolverTimeOutException()
+
+
+def _run(name, k1, k2, monkeypatch, n_seeds=48, backend=None):
     keccak_function_manager.reset()
     tx_id_manager.restart_counter()
     solver.get_model.cache_clear()
     monkeypatch.setattr(solver.args, "pruning_factor", 1)
     mc = ModelCache(device=k2)
     monkeypatch.setattr(solver, "model_cache", mc)
+    if backend is not None:
+        monkeypatch.setattr(solver, "solver_backend", backend)
     code = workloads.bytecode(name)
     ws, addr = symcases.deploy(k1, name)
     seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"])
@@ -105,3 +127,18 @@ def test_fork_and_reachability_filters_on_kernel2_equal_the_oracles(dev, name, m
     assert k2.launches > 0 and got["device_evals"] > 0
     assert got["forks"]["queries"] > 10 and got["cache"]["queries"] > 10
     assert got["lane_steps"] > 100 and len(got["ends"]) > 10
+
+
+@pytest.mark.parametrize("name", ["overflow.sol.o", "exceptions.sol.o"])
+def test_prunes_with_a_refuting_backend_equal_the_oracles(dev, name, monkeypatch):
+    """with a backend that refutes (UNSAT) and times out on a
+    known subset, the fork and reachability filters really prune, kernel 2 still
+    answers what the LRU and the seeds can, and every decision, end and open
+    state equals the run with kernel 2's C oracle.  Seeds are consulted only
+    where the backend timed out (counted as divergences from the reference)."""
+    got = _run(name, dev, _CountingK2(dev), monkeypatch, backend=StubBackend())
+    want = _run(name, dev, OracleK2(), monkeypatch, backend=StubBackend())
+    for key in ("ends", "open", "forks", "cache", "lru", "lane_steps"):
+        assert got[key] == want[key], key
+    assert got["forks"]["pruned"] > 0
+    assert got["cache"]["divergences"] == want["cache"]["divergences"]
