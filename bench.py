@@ -585,7 +585,7 @@ def symbolic_lane_batch(dev, lanes: int):
     return laser, big
 
 
-def run_symbolic_lanes(dev, lanes: int, reps: int = 5):
+def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True):
     """k_sym_step at `lanes` lanes: every lane runs from the
     start of its symbolic message call to its first stop -- MG_FORK at a
     symbolic JUMPI (the dispatcher's selector compare), an escape or a halt --
@@ -614,6 +614,10 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5):
     created = int(out_b.n_nodes.sum()) - n0
     statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
                 for k, v in zip(*np.unique(out_b.status, return_counts=True))}
+    if not profile:            # the timed launches alone (PMC passes of k_sym_step)
+        kms = float(np.median(ms))
+        return {"lanes": lanes, "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
+                "lane_steps_per_s": steps / (kms / 1e3), "statuses": statuses}
     dev.upload(b)
     op_counts, extra = dev.step_profile()
     ops, byts, psteps = roofline.algorithmic_work(op_counts, extra)
@@ -765,7 +769,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
                 addr = workloads.CONTRACT
                 ws.put_account(Account(addr, code=Disassembly(code), concrete_storage=False))
             mc = solver.ModelCache(device=dev)
-            seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"])
+            seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"], balance_names=["balance"])
             mc.seed_source = seeds
             solver.model_cache = mc
             laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
