@@ -89,6 +89,7 @@ class WitnessSeeds:
         self._epoch = None
         self._rev: Dict[str, int] = {}           # interpretation changes per name (PoolColumns)
         self._tx_top = -1
+        self._sym_pts = 0                        # symbolic EXP points completed so far
 
     def revision(self, name: str) -> int:
         return self._rev.get(name, 0)
@@ -153,20 +154,25 @@ class WitnessSeeds:
             km.create_conditions()          # assigns the intervals in the reference's order
         from ..smt.exponent_manager import exponent_function_manager
         power = exponent_function_manager.concrete_points
-        self._touch("Power")
-        for (n, _), _h in concrete.items():
-            self._touch(f"keccak256_{n}")
-            self._touch(f"keccak256_{n}-1")
-        for x in inputs:
-            self._touch(f"keccak256_{x.size()}")
-            self._touch(f"keccak256_{x.size()}-1")
+        # an interpretation's revision changes only when entries are added to it
+        # (PoolColumns re-serialises a table per revision)
+        changed = set()
         for m, a in enumerate(self.assign):
             pw = a.setdefault("Power", FuncInterp(0, {}))
-            for (b, e), v in power.items():
-                pw.entries.setdefault((b, e), v)
+            if len(pw.entries) != len(power):
+                for (b, e), v in power.items():
+                    if (b, e) not in pw.entries:
+                        pw.entries[(b, e)] = v
+                        changed.add("Power")
             for (n, cv), h in concrete.items():
-                a.setdefault(f"keccak256_{n}", FuncInterp(0, {})).entries.setdefault((cv,), h)
-                a.setdefault(f"keccak256_{n}-1", FuncInterp(0, {})).entries.setdefault((h,), cv)
+                f = a.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
+                if (cv,) not in f.entries:
+                    f.entries[(cv,)] = h
+                    changed.add(f"keccak256_{n}")
+                inv = a.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
+                if (h,) not in inv.entries:
+                    inv.entries[(h,)] = cv
+                    changed.add(f"keccak256_{n}-1")
         # inputs in registration order (an input may hash an earlier one's hash):
         # each evaluated under every seed at once, then entered into the seeds'
         # keccak tables
@@ -191,6 +197,27 @@ class WitnessSeeds:
                     h = (lo + 63) // 64 * 64 + 64 * (k - 1)     # in [lo, lo + PART), % 64 == 0
                 f.entries[(v,)] = h
                 inv.entries[(h,)] = v
+                changed.add(f"keccak256_{n}")
+                changed.add(f"keccak256_{n}-1")
+        # Power at every symbolic EXP's (base, exponent) under each seed: the
+        # exponent manager's axioms for base 256 (Power(256, e) == Power(256,
+        # e % 32) and the 256**i table) fix it to 256**(e % 32); any other base
+        # takes its true power when positive (the `Power > 0` conjunct), else 1
+        sym_pts = exponent_function_manager.symbolic_points
+        for j in range(self._sym_pts, len(sym_pts)):
+            base, expo = sym_pts[j]
+            bs, es = eval_all(base.raw, self.assign), eval_all(expo.raw, self.assign)
+            for a, b, e in zip(self.assign, bs, es):
+                b, e = int(b), int(e)
+                v = 256 ** (e % 32) if b == 256 else pow(b, e, 1 << 256)
+                v = v if 0 < v < 1 << 255 else 1
+                pw = a["Power"]
+                if (b, e) not in pw.entries:
+                    pw.entries[(b, e)] = v
+                    changed.add("Power")
+        self._sym_pts = len(sym_pts)
+        for name in changed:
+            self._touch(name)
 
     @property
     def epoch(self):
@@ -209,7 +236,8 @@ class WitnessSeeds:
             self._tx_top = top
         from ..smt.exponent_manager import exponent_function_manager
         epoch = (len(self.tx_ids), sum(len(v) for v in self.km.symbolic_inputs.values()),
-                 len(self.km.concrete_hashes), len(exponent_function_manager.concrete_points))
+                 len(self.km.concrete_hashes), len(exponent_function_manager.concrete_points),
+                 len(exponent_function_manager.symbolic_points))
         if self._models is None or epoch != self._epoch:
             self._complete()
             if self._models is None:
@@ -225,10 +253,18 @@ class WitnessSeeds:
 def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
     """Value of a bit-vector / Bool term under every assignment (model
     completion: absent variables 0, arrays and functions their default /
-    else value), one pass over the DAG with a value list per node."""
+    else value), one pass over the DAG with a column of values per node.
+    Columns are numpy object arrays of Python ints, so each operator runs as
+    one vectorised loop over the models instead of an interpreted call per
+    model (the witness completion's hot path)."""
     from ..smt.semantics import apply_op
     n = len(assigns)
     memo: Dict[int, object] = {}
+
+    def col(x):
+        out = np.empty(n, dtype=object)
+        out[:] = x
+        return out
 
     def arr(node):
         """Per model: (default, {index: value}) of an array term."""
@@ -252,31 +288,81 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
         memo[id(node)] = out
         return out
 
+    def signed(x, w):
+        return np.where((x >> (w - 1)) & 1, x - (1 << w), x)
+
     def val(node):
         got = memo.get(id(node))
         if got is not None:
             return got
-        op = node.op
+        op, w = node.op, node.width
+        M = (1 << w) - 1 if w else 0
         if op == "const":
-            out = [node.param] * n
+            out = col(node.param)
         elif op == "var":
-            out = [(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns]
+            out = col([(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns])
         elif op == "select":
             ar, idx = arr(node.args[0]), val(node.args[1])
-            out = [ar[m][1].get(idx[m], ar[m][0]) for m in range(n)]
+            out = col([ar[m][1].get(idx[m], ar[m][0]) for m in range(n)])
         elif op == "uf":
             args = [val(x) for x in node.args]
             name = node.param[0]
-            out = []
+            vals = []
             for m, a in enumerate(assigns):
                 it = a.get(name)
-                key = tuple(col[m] for col in args)
-                out.append(it.entries.get(key, it.else_value) if isinstance(it, FuncInterp) else 0)
+                key = tuple(c[m] for c in args)
+                vals.append(it.entries.get(key, it.else_value) if isinstance(it, FuncInterp) else 0)
+            out = col(vals)
         else:
             args = [val(x) for x in node.args]
             ws = [x.width for x in node.args]
-            out = [apply_op(op, node.width, [col[m] for col in args], ws, node.param) for m in range(n)]
+            a = args[0] if args else None
+            b = args[1] if len(args) > 1 else None
+            if op == "bvadd":
+                out = (a + b) & M
+            elif op == "bvsub":
+                out = (a - b) & M
+            elif op == "bvmul":
+                out = (a * b) & M
+            elif op == "bvand":
+                out = a & b
+            elif op == "bvor":
+                out = a | b
+            elif op == "bvxor":
+                out = a ^ b
+            elif op == "bvnot":
+                out = ~a & M
+            elif op == "bvneg":
+                out = -a & M
+            elif op in ("eq", "distinct", "bvult", "bvule", "bvugt", "bvuge"):
+                cmp = {"eq": np.equal, "distinct": np.not_equal, "bvult": np.less, "bvule": np.less_equal,
+                       "bvugt": np.greater, "bvuge": np.greater_equal}[op]
+                out = cmp(a, b).astype(np.int64).astype(object)
+            elif op in ("bvslt", "bvsle", "bvsgt", "bvsge"):
+                cmp = {"bvslt": np.less, "bvsle": np.less_equal, "bvsgt": np.greater,
+                       "bvsge": np.greater_equal}[op]
+                out = cmp(signed(a, ws[0]), signed(b, ws[0])).astype(np.int64).astype(object)
+            elif op == "not":
+                out = (a & 1) ^ 1
+            elif op == "and":
+                out = col(1)
+                for c in args:
+                    out = out & (c & 1)
+            elif op == "or":
+                out = col(0)
+                for c in args:
+                    out = out | (c & 1)
+            elif op == "ite":
+                out = np.where((a & 1).astype(bool), args[1], args[2])
+            elif op == "concat":
+                out = (a << ws[1]) | b
+            elif op == "extract":
+                out = (a >> node.param[1]) & M
+            elif op == "zero_extend":
+                out = a
+            else:                               # the rest one model at a time
+                out = col([apply_op(op, w, [c[m] for c in args], ws, node.param) for m in range(n)])
         memo[id(node)] = out
         return out
 
-    return val(raw)
+    return list(val(raw))
