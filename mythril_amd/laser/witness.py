@@ -105,37 +105,54 @@ class WitnessSeeds:
         self._touch(f"{txid}_calldata")
         actors = list(ACTORS.values())
         r = self.rng
+        n = self.n
+        # every seed's draws at once (numpy), then one pass to build the arrays
+        nargs = r.integers(0, 4, n)
+        use_sel = r.random(n) < 0.9
+        sel = r.integers(0, len(self.selectors), n)
+        junk = r.integers(0, 256, (n, 4), dtype=np.uint8)
+        args = self._args(actors, n * 3)
+        cut = r.random(n) < 0.05
+        cut_at = r.random(n)
+        value_nz = r.random(n) >= 0.85
+        values = r.integers(1, 1 << 20, n)
+        gas = r.integers(0, 1 << 40, n)
         for m, a in enumerate(self.assign):
-            nargs = int(r.integers(0, 4))
-            data = bytearray()
-            if r.random() < 0.9:
-                data += self.selectors[int(r.integers(0, len(self.selectors)))].to_bytes(4, "big")
-            else:
-                data += bytes(r.integers(0, 256, 4, dtype=np.uint8))
-            for _ in range(nargs):
-                data += self._arg(actors).to_bytes(32, "big")
-            if r.random() < 0.05 and data:
-                data = data[:int(r.integers(0, len(data)))]
-            a[f"{txid}_calldata"] = ArrayInterp(0, {k: b for k, b in enumerate(data)})
+            data = bytearray(self.selectors[int(sel[m])].to_bytes(4, "big") if use_sel[m] else bytes(junk[m]))
+            for j in range(int(nargs[m])):
+                data += args[m * 3 + j].to_bytes(32, "big")
+            if cut[m] and data:
+                data = data[:int(cut_at[m] * len(data))]
+            a[f"{txid}_calldata"] = ArrayInterp(0, dict(enumerate(data)))
             a[f"{txid}_calldatasize"] = len(data)
             a[f"sender_{txid}"] = actors[m % len(actors)]
-            a[f"call_value{txid}"] = 0 if r.random() < 0.85 else int(r.integers(1, 1 << 20))
-            a[f"gas_price{txid}"] = int(r.integers(0, 1 << 40))
+            a[f"call_value{txid}"] = int(values[m]) if value_nz[m] else 0
+            a[f"gas_price{txid}"] = int(gas[m])
 
-    def _arg(self, actors) -> int:
+    def _args(self, actors, k: int) -> List[int]:
+        """k argument words: zero, small, an actor, a random address, a random
+        word or all ones."""
         r = self.rng
-        u = r.random()
-        if u < 0.15:
-            return 0
-        if u < 0.40:
-            return int(r.integers(0, 1 << 16))
-        if u < 0.60:
-            return actors[int(r.integers(0, len(actors)))]
-        if u < 0.75:
-            return int.from_bytes(bytes(r.integers(0, 256, 20, dtype=np.uint8)), "big")
-        if u < 0.90:
-            return int.from_bytes(bytes(r.integers(0, 256, 32, dtype=np.uint8)), "big")
-        return M256
+        u = r.random(k)
+        small = r.integers(0, 1 << 16, k)
+        who = r.integers(0, len(actors), k)
+        raw = r.integers(0, 256, (k, 32), dtype=np.uint8)
+        out = []
+        for i in range(k):
+            x = u[i]
+            if x < 0.15:
+                out.append(0)
+            elif x < 0.40:
+                out.append(int(small[i]))
+            elif x < 0.60:
+                out.append(actors[int(who[i])])
+            elif x < 0.75:
+                out.append(int.from_bytes(raw[i, :20].tobytes(), "big"))
+            elif x < 0.90:
+                out.append(int.from_bytes(raw[i].tobytes(), "big"))
+            else:
+                out.append(M256)
+        return out
 
     def note_query_vars(self, names: Iterable[str]) -> None:
         for name in names:

@@ -249,11 +249,18 @@ class PoolColumns:
                 ser[m], done[m] = bytearray(), 0
             dflt[m] = d
             if len(ent) > done[m]:
-                buf = ser[m]
-                for k, v in itertools.islice(ent.items(), done[m], None):
-                    k0, k1 = sig.key_chunks((k,) if arr else tuple(k))
-                    buf += (k0 & M256_).to_bytes(32, "little") + (k1 & M256_).to_bytes(32, "little") + \
-                        (v & M512_).to_bytes(64, "little")
+                # a row is (k0, k1, value): for a one-argument key of up to 512 bits
+                # k0 | k1 << 256 is the key itself (TableSig.key_chunks), so the
+                # first 64 bytes are the key's little-endian bytes
+                new = itertools.islice(ent.items(), done[m], None)
+                if arr:
+                    ser[m] += b"".join((k & M512_).to_bytes(64, "little") + (v & M512_).to_bytes(64, "little")
+                                       for k, v in new)
+                else:
+                    ser[m] += b"".join(
+                        ((k[0] & M512_).to_bytes(64, "little") if len(k) == 1 else
+                         (k[0] & M256_).to_bytes(32, "little") + (k[1] & M256_).to_bytes(32, "little")) +
+                        (v & M512_).to_bytes(64, "little") for k, v in new)
                 done[m] = len(ent)
         count = np.array(done, dtype=np.uint32)
         start = np.zeros(nm, dtype=np.uint32)
