@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 10u  /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 11u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -41,7 +41,8 @@ extern "C" {
                                   calldata opcodes (MG_REC_CDSIZE) on symbolic lanes;
                                   symbolic EXP (MG_SYM_BIN 0x0a, MG_REC_SYMEXP)
                               10: MG_LANE_RETDATA (a host CALL left return data:
-                                  RETURNDATASIZE / RETURNDATACOPY escape) */
+                                  RETURNDATASIZE / RETURNDATACOPY escape)
+                              11: mg_cc_* (native conjunct compiler for kernel 2) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -50,6 +51,7 @@ extern "C" {
 #define MG_ENOMEM     -3   /* device or host allocation failed                  */
 #define MG_ESTATE     -4   /* call out of order (e.g. step before upload)       */
 #define MG_ENOCODE    -5   /* unknown code_id                                   */
+#define MG_EUNSUPPORTED -6 /* a constraint the device does not evaluate (mg_cc_compile) */
 
 /* ------------------------------------------------------------ lane status */
 /* What ended (or paused) a lane.  Fields pc/sp/msize/gas of a lane that is no
@@ -514,6 +516,32 @@ int         mg_eval_upload(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model
 int         mg_eval_run(mg_ctx *ctx, uint32_t dag_first, uint32_t dag_count, float *kernel_ms);
 int         mg_eval_download(mg_ctx *ctx, uint32_t *first_sat_model, uint32_t *sat_count,
                              uint32_t dag_first, uint32_t dag_count);
+
+/* ------------------------------------------------------ conjunct compiler */
+/* Kernel 2's register programs compiled on the host from lowered constraint
+ * DAGs (mythril_amd/smt/flatten.py's passes in native code; replaces the
+ * Python compile of every quick-sat query's conjuncts, support/model.py:48-56
+ * -> get_model's And(constraints)).  Nodes are registered once each into a
+ * growing table (ids only grow), programs are compiled per conjunct root.
+ * Host only: no device, no context needed.                                  */
+typedef struct mg_cc mg_cc;
+int         mg_cc_open(mg_cc **out);
+void        mg_cc_close(mg_cc *cc);
+const char *mg_cc_error(mg_cc *cc);
+/* rows: n x {op, width, first_arg, n_args, imm}; op = a kernel-2 opcode
+ * (bv_eval.cuh BV_*), or 0x1000 (variable: imm = its model-pool index) /
+ * 0x1001 (constant: imm = its constant-pool index).  args[first_arg ..]: node
+ * ids, or 0x80000000 | k for row k of this call.  ids[i] <- row i's id (an
+ * equal existing node's id when there is one).  imm: the low bit of an
+ * extract; table index | part << 20 | low bit << 21 of a table lookup.      */
+int         mg_cc_add(mg_cc *cc, const uint32_t *rows, uint32_t n, const uint32_t *args, uint32_t n_args,
+                      uint32_t *ids);
+/* The program of the conjunct rooted at node `root`: n_insns x 4 u32 into
+ * insns (cap instructions); *max_slots is raised to the slots it uses.
+ * MG_EUNSUPPORTED: more than 16 live values, more than 2048 instructions or
+ * a value wider than 256 bits (the set stays with the SMT backend).        */
+int         mg_cc_compile(mg_cc *cc, uint32_t root, uint32_t *insns, uint32_t cap, uint32_t *n_insns,
+                          uint32_t *max_slots);
 
 #ifdef __cplusplus
 }

@@ -15,9 +15,11 @@
 
 #include "../../include/mythgpu.h"
 #include <cstdlib>
+#include <new>
 #include "bv_eval.cuh"
 #include "lane_step.cuh"
 #include "sym_step.cuh"
+#include "cc.h"
 
 // ------------------------------------------------------------------ context
 struct mg_ctx {
@@ -1693,4 +1695,41 @@ extern "C" int mg_eval(mg_ctx *ctx, const mg_dag_batch *dags, const mg_model_bat
     if ((rc = mg_eval_upload(ctx, dags, models))) return rc;
     if ((rc = mg_eval_run(ctx, 0, dags->n_dags, kernel_ms))) return rc;
     return mg_eval_download(ctx, first_sat, sat_count, 0, dags->n_dags);
+}
+
+// ------------------------------------------------------------ conjunct compiler
+// mg_cc_*: kernel 2's program compiler on the host, over a growing native node
+// table (csrc/cc.h; the passes of mythril_amd/smt/flatten.py).
+struct mg_cc {
+    mgcc::Compiler c;
+    std::vector<uint32_t> buf;
+};
+
+extern "C" int mg_cc_open(mg_cc **out) {
+    if (!out) return MG_EINVAL;
+    *out = new (std::nothrow) mg_cc();
+    return *out ? MG_OK : MG_ENOMEM;
+}
+
+extern "C" void mg_cc_close(mg_cc *cc) { delete cc; }
+
+extern "C" const char *mg_cc_error(mg_cc *cc) { return cc ? cc->c.err.c_str() : "null compiler"; }
+
+extern "C" int mg_cc_add(mg_cc *cc, const uint32_t *rows, uint32_t n, const uint32_t *args, uint32_t n_args,
+                         uint32_t *ids) {
+    if (!cc || (n && (!rows || !ids))) return MG_EINVAL;
+    return cc->c.add(rows, n, args, n_args, ids) ? MG_EINVAL : MG_OK;
+}
+
+extern "C" int mg_cc_compile(mg_cc *cc, uint32_t root, uint32_t *insns, uint32_t cap, uint32_t *n_insns,
+                             uint32_t *max_slots) {
+    if (!cc || !n_insns || !max_slots) return MG_EINVAL;
+    uint32_t ms = *max_slots;
+    const int n = cc->c.compile(root, cc->buf, ms);
+    if (n < 0) return MG_EUNSUPPORTED;
+    *n_insns = (uint32_t)n;
+    if ((uint32_t)n > cap || !insns) { cc->c.err = "instruction buffer too small"; return MG_EINVAL; }
+    std::memcpy(insns, cc->buf.data(), (size_t)n * 4 * sizeof(uint32_t));
+    *max_slots = ms;
+    return MG_OK;
 }

@@ -19,7 +19,7 @@ INCLUDE = PKG_DIR.parent / "include"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
-MG_OK, MG_EINVAL, MG_EDEVICE, MG_ENOMEM, MG_ESTATE, MG_ENOCODE = 0, -1, -2, -3, -4, -5
+MG_OK, MG_EINVAL, MG_EDEVICE, MG_ENOMEM, MG_ESTATE, MG_ENOCODE, MG_EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 
 
 class MythGpuError(RuntimeError):
@@ -107,6 +107,11 @@ _P, _U32, _U64, _I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c
 _PU32 = ctypes.POINTER(ctypes.c_uint32)
 SIGNATURES = {
     "mg_abi_version": (_I, []),
+    "mg_cc_open": (_I, [ctypes.POINTER(_P)]),
+    "mg_cc_close": (None, [_P]),
+    "mg_cc_error": (ctypes.c_char_p, [_P]),
+    "mg_cc_add": (_I, [_P, _P, _U32, _P, _U32, _P]),
+    "mg_cc_compile": (_I, [_P, _U32, _P, _U32, _PU32, _PU32]),
     "mg_open": (_I, [_I, ctypes.POINTER(_P)]),
     "mg_close": (None, [_P]),
     "mg_last_error": (ctypes.c_char_p, [_P]),

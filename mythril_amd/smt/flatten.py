@@ -96,7 +96,10 @@ class _Virt:
         self.op, self.width, self.args, self.imm, self.node = op, width, args, imm, node
 
 
-class Compiler:
+class PyCompiler:
+    """The passes in Python: the reference implementation the native compiler
+    (NativeCompiler, libmythgpu mg_cc_*) is tested against."""
+
     def __init__(self):
         self.var_index: Dict[str, int] = {}
         self.var_widths: List[int] = []
@@ -278,7 +281,124 @@ class Compiler:
         return out
 
 
-def compile_sets(sets: Sequence[Sequence], compiler: Compiler = None) -> Tuple[ProgramBatch, List[int]]:
+class NativeCompiler(PyCompiler):
+    """The same compiler with every pass after lowering in libmythgpu
+    (csrc/cc.h through mg_cc_*): the lowered DAG's nodes are registered once
+    each into the library's node table (a calldata word or a store chain
+    shared by many conjuncts crosses once), leaves get their model-pool /
+    constant-pool indices here, and each conjunct's program comes back from
+    one call.  Lowering (arrays, uninterpreted functions, wide values ->
+    256-bit ops and table lookups) stays in lower.py."""
+
+    _VAR, _CONST, _BAD = 0x1000, 0x1001, 0xFFFF
+
+    def __init__(self):
+        super().__init__()
+        import ctypes
+        from .. import native
+        self._ct = ctypes
+        self._lib = native.load()
+        self._cc = ctypes.c_void_p()
+        if self._lib.mg_cc_open(ctypes.byref(self._cc)) != 0:
+            raise native.MythGpuError("mg_cc_open failed")
+        self._ids: Dict[Node, int] = {}
+        self._buf = np.zeros((TILE_INSNS, 4), dtype=np.uint32)
+        self._n = ctypes.c_uint32(0)
+        self._ms = ctypes.c_uint32(0)
+
+    def __del__(self):
+        cc = getattr(self, "_cc", None)
+        if cc:
+            self._lib.mg_cc_close(cc)
+            self._cc = None
+
+    def _row(self, x: Node) -> Tuple[int, int]:
+        """(op, imm) of a node for the library; _BAD for a node no program may
+        contain (a variable used at two widths, an operation the device lacks)."""
+        op = x.op
+        if op == "const":
+            i = self.const_index.get(x.param)
+            if i is None:
+                i = self.const_index[x.param] = len(self.consts)
+                self.consts.append(x.param)
+            return self._CONST, i
+        if op == "var":
+            i = self.var_index.get(x.param)
+            if i is None:
+                i = self.var_index[x.param] = len(self.var_widths)
+                self.var_widths.append(x.width)
+            elif self.var_widths[i] != x.width:
+                return self._BAD, 0
+            return self._VAR, i
+        code = OPCODE.get(op)
+        if code is None or op in ("bvumin", "bvumax", "bvsmin", "bvsmax", "bvrsub", "rconcat"):
+            return self._BAD, 0
+        if op == "extract":
+            return code, x.param[1]
+        if op == "tab":
+            name, part, lo = x.param
+            t = self.table_index.get(name)
+            if t is None:
+                t = self.table_index[name] = len(self.table_index)
+            return code, t | (part << TAB_PART_SHIFT) | (lo << TAB_LO_SHIFT)
+        return code, 0
+
+    def _register(self, root: Node) -> int:
+        ids = self._ids
+        if root in ids:
+            return ids[root]
+        new: List[Node] = []
+        local: Dict[Node, int] = {}
+        stack = [(root, False)]
+        while stack:
+            x, ready = stack.pop()
+            if x in ids or x in local:
+                continue
+            if not ready:
+                stack.append((x, True))
+                stack.extend((c, False) for c in x.args if c not in ids and c not in local)
+                continue
+            local[x] = len(new)
+            new.append(x)
+        flat: List[int] = []
+        args: List[int] = []
+        row = self._row
+        for x in new:
+            op, imm = row(x)
+            flat += (op, x.width, len(args), len(x.args), imm)
+            for c in x.args:
+                j = local.get(c)
+                args.append(ids[c] if j is None else (0x80000000 | j))
+        rows = np.array(flat, dtype=np.uint32)
+        a = np.array(args, dtype=np.uint32) if args else np.zeros(1, dtype=np.uint32)
+        out = np.zeros(len(new), dtype=np.uint32)
+        rc = self._lib.mg_cc_add(self._cc, rows.ctypes.data, len(new), a.ctypes.data, len(args), out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError(f"mg_cc_add: {self._lib.mg_cc_error(self._cc).decode()}")
+        for x, i in zip(new, out.tolist()):
+            ids[x] = i
+        return ids[root]
+
+    def compile(self, root: Node) -> np.ndarray:
+        low = self.lowering.lower(root)
+        rid = self._register(low)
+        ct = self._ct
+        self._ms.value = self.max_slots
+        rc = self._lib.mg_cc_compile(self._cc, rid, self._buf.ctypes.data, TILE_INSNS, ct.byref(self._n),
+                                     ct.byref(self._ms))
+        if rc == -6:
+            raise Unsupported(self._lib.mg_cc_error(self._cc).decode())
+        if rc != 0:
+            raise RuntimeError(f"mg_cc_compile: {self._lib.mg_cc_error(self._cc).decode()}")
+        self.max_slots = int(self._ms.value)
+        return self._buf[: self._n.value].copy()
+
+
+# the product compiler: native passes (libmythgpu); PyCompiler is their reference
+Compiler = NativeCompiler
+
+
+def compile_sets(sets: Sequence[Sequence], compiler: PyCompiler = None) -> Tuple[ProgramBatch, List[int]]:
     """Compile constraint sets (each a list of Bool / Node) into one ProgramBatch.
     Returns the batch and the indices of the sets it contains (unsupported sets
     are left out and must go to z3)."""
@@ -310,7 +430,7 @@ def compile_sets(sets: Sequence[Sequence], compiler: Compiler = None) -> Tuple[P
                         tables), kept
 
 
-def batch_from(c: "Compiler", progs: List[np.ndarray]) -> ProgramBatch:
+def batch_from(c: "PyCompiler", progs: List[np.ndarray]) -> ProgramBatch:
     """A ProgramBatch of programs compiled by one (persistent) Compiler: its
     variable, constant and table index spaces only grow, so programs compiled
     for earlier batches stay valid in later ones."""

@@ -301,3 +301,29 @@ def test_programs_with_more_than_eight_live_values():
     for d, s_ in enumerate(sets):
         vals = [evaluate(s_[0].raw, m) for m in models]
         assert (next((i for i, v in enumerate(vals) if v), 0xFFFFFFFF), sum(vals)) == (fs[d], sc[d])
+
+
+def test_native_compiler_programs_equal_the_python_passes():
+    """mg_cc_* (csrc/cc.h) against flatten.PyCompiler: on C4 DAGs, random
+    operator sets, array / function-table sets and >8-slot sets, both compilers
+    accept the same sets, use as many instructions, and their programs give the
+    same first-satisfying model and count on the oracle evaluator (instruction
+    order may differ only where equal-size operand subtrees tie)."""
+    from mythril_amd.smt.flatten import NativeCompiler, PyCompiler
+    rng = random.Random(77)
+    dr = synth.Draws(200, seed=synth.C4_SEED + 17)
+    sets = [[synth.dag_expr(dr, i)] for i in range(200)]
+    sets += [_random_constraints(rng) for _ in range(150)]
+    sets += [_random_table_constraints(rng) for _ in range(150)]
+    pn, kn = compile_sets(sets, NativeCompiler())
+    pp, kp = compile_sets(sets, PyCompiler())
+    assert kn == kp and len(kn) > 400
+    assert np.array_equal(np.diff(pn.prog_off.astype(np.int64)), np.diff(pp.prog_off.astype(np.int64)))
+    assert set(pn.var_names) == set(pp.var_names)
+    models = _random_table_models(random.Random(5), 160, pp)
+    out = []
+    for prog in (pn, pp):
+        pool = ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables)
+        out.append(eval_batch(prog, pool))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert 0 < int(out[1][1].sum()) < len(kn) * 160
