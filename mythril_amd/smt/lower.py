@@ -23,7 +23,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Tuple
 
-from .expr import Node, const
+from .expr import Node, const, var
 
 WMAX = 256
 KEY_MAX = 512
@@ -31,6 +31,18 @@ KEY_MAX = 512
 
 class Unsupported(Exception):
     pass
+
+
+SELECT_SEP = "\x1f"       # never part of a variable name the expression layer makes
+
+
+def select_var(array_name: str, index: int) -> str:
+    """The model-pool variable standing for ``select(Array(array_name), index)``."""
+    return f"{array_name}{SELECT_SEP}{index}"
+
+
+def rng_ok(a: Node) -> bool:
+    return a.param[2] <= WMAX
 
 
 class TableSig:
@@ -132,6 +144,12 @@ class Lowering:
             a = a.args[0]
         if a.op == "K":
             r = self.lower(a.args[0])
+        elif a.op == "array" and j.op == "const" and rng_ok(a):
+            # a constant index into a symbolic array (calldata bytes, a fixed
+            # storage slot, an actor's balance) is one value per model: a model-pool
+            # variable instead of a table lookup (no entry scan on the device, no
+            # table rows on the host); program.select_var_value reads it back
+            r = var(select_var(a.param[0], j.param), a.param[2])
         elif a.op == "array":
             name, dom, rng = a.param
             self._table(name, "array", (dom,), rng)

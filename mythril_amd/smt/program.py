@@ -94,6 +94,20 @@ class FuncInterp:
         self.entries = dict(entries or {})
 
 
+def model_value(model: Dict[str, object], name: str) -> int:
+    """A variable's value in a model dict; a constant-index select variable
+    (lower.select_var: ``array<SEP>index``) reads the array interpretation's
+    entry or default.  Anything absent is 0 (z3 model_completion)."""
+    x = model.get(name)
+    if x is None and "\x1f" in name:
+        arr, _, k = name.partition("\x1f")
+        interp = model.get(arr)
+        if isinstance(interp, ArrayInterp):
+            return interp.entries.get(int(k), interp.default)
+        return 0
+    return x if isinstance(x, int) else 0
+
+
 def _wide_limbs(x: int) -> np.ndarray:
     """512-bit value -> 16 little-endian u32 limbs."""
     return np.frombuffer((x & ((1 << 512) - 1)).to_bytes(64, "little"), dtype="<u4")
@@ -147,8 +161,7 @@ class ModelPool:
         vals = np.zeros((max(len(var_names), 1), max(len(models), 1), 8), dtype=np.uint32)
         for m, model in enumerate(models):
             for v, (name, w) in enumerate(zip(var_names, var_widths)):
-                x = model.get(name, 0)
-                x = (x if isinstance(x, int) else 0) & ((1 << w) - 1)
+                x = model_value(model, name) & ((1 << w) - 1)
                 vals[v, m] = np.frombuffer(x.to_bytes(32, "little"), dtype="<u4")
         pool = ModelPool(vals)
         tables = tables or []
@@ -210,15 +223,18 @@ class PoolColumns:
         self.revision = revision or (lambda name: 0)
 
     def _var(self, name: str, w: int) -> np.ndarray:
-        col = self._vars.get((name, w))
-        if col is None:
-            raw = bytearray()
-            for a in self.assigns:
-                x = a.get(name, 0)
-                x = (x if isinstance(x, int) else 0) & ((1 << w) - 1)
-                raw += x.to_bytes(32, "little")
-            col = self._vars[(name, w)] = np.frombuffer(bytes(raw), dtype="<u4").reshape(-1, 8).astype(np.uint32)
-        return col
+        sel = "\x1f" in name
+        rev = self.revision(name.partition("\x1f")[0]) if sel else 0
+        got = self._vars.get((name, w))
+        if got is None or got[0] != rev:
+            mask = (1 << w) - 1
+            if sel:
+                raw = b"".join((model_value(a, name) & mask).to_bytes(32, "little") for a in self.assigns)
+            else:
+                raw = b"".join(((x if isinstance(x := a.get(name, 0), int) else 0) & mask).to_bytes(32, "little")
+                               for a in self.assigns)
+            got = self._vars[(name, w)] = (rev, np.frombuffer(raw, dtype="<u4").reshape(-1, 8).astype(np.uint32))
+        return got[1]
 
     def _tab(self, sig) -> tuple:
         """(start, count, entries, default) of one table over every model.

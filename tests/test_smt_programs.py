@@ -327,3 +327,29 @@ def test_native_compiler_programs_equal_the_python_passes():
         out.append(eval_batch(prog, pool))
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
     assert 0 < int(out[1][1].sum()) < len(kn) * 160
+
+
+def test_constant_index_selects_are_pool_variables():
+    """select(Array, const) lowers to a model-pool variable (no table): its
+    column reads the array interpretation's entry or default, and a
+    PoolColumns column is rebuilt when the array's revision moves."""
+    from mythril_amd.smt.lower import select_var
+    from mythril_amd.smt.program import PoolColumns
+    cd = Array("7_calldata", 256, 8)
+    sets = [[cd[BVV(4, 256)] == BVV(0x2A, 8)], [ULT(ZeroExt(248, cd[BVV(0, 256)]), BVV(3, 256))]]
+    prog, kept = compile_sets(sets)
+    assert len(kept) == 2 and not prog.tables
+    assert set(prog.var_names) == {select_var("7_calldata", 4), select_var("7_calldata", 0)}
+    models = [{"7_calldata": ArrayInterp(0x2A, {0: 9})}, {"7_calldata": ArrayInterp(0, {4: 0x2A, 0: 2})},
+              {"7_calldata": ArrayInterp(1, {})}, {}]
+    want = [[evaluate(And(*s).raw, m) for m in models] for s in sets]
+    fs, sc = eval_batch(prog, ModelPool.from_dicts(models, prog.var_names, prog.var_widths, prog.tables))
+    assert [sum(w) for w in want] == list(sc) == [2, 3]
+    rev = [0]
+    cols = PoolColumns(models, revision=lambda name: rev[0] if name == "7_calldata" else 0)
+    assert (cols.pool(prog.var_names, prog.var_widths).values
+            == ModelPool.from_dicts(models, prog.var_names, prog.var_widths).values).all()
+    models[3]["7_calldata"] = ArrayInterp(0x2A, {})
+    rev[0] += 1
+    _, sc2 = eval_batch(prog, cols.pool(prog.var_names, prog.var_widths, prog.tables))
+    assert list(sc2) == [3, 2]
