@@ -218,6 +218,7 @@ class PoolColumns:
         self.assigns = assigns
         self._vars: Dict[tuple, np.ndarray] = {}
         self._tabs: Dict[tuple, tuple] = {}
+        self._dense_cache: Dict[str, tuple] = {}
         # revision(name) -> a value that changes whenever any assignment's
         # interpretation of `name` changes (None: interpretations never change)
         self.revision = revision or (lambda name: 0)
@@ -228,6 +229,16 @@ class PoolColumns:
         got = self._vars.get((name, w))
         if got is None or got[0] != rev:
             mask = (1 << w) - 1
+            k = int(name.partition("\x1f")[2]) if sel else -1
+            dense = self._dense(name.partition("\x1f")[0], rev) if sel and w <= 64 and k < self.DENSE_KEYS else None
+            if dense is not None:
+                mat, dflt = dense
+                v = (mat[:, k] if k < mat.shape[1] else dflt) & np.uint64(mask)
+                col = np.zeros((len(self.assigns), 8), dtype=np.uint32)
+                col[:, 0] = (v & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+                col[:, 1] = (v >> np.uint64(32)).astype(np.uint32)
+                got = self._vars[(name, w)] = (rev, col)
+                return col
             if sel:
                 raw = b"".join((model_value(a, name) & mask).to_bytes(32, "little") for a in self.assigns)
             else:
@@ -235,6 +246,45 @@ class PoolColumns:
                                for a in self.assigns)
             got = self._vars[(name, w)] = (rev, np.frombuffer(raw, dtype="<u4").reshape(-1, 8).astype(np.uint32))
         return got[1]
+
+    DENSE_KEYS = 4096
+
+    def _dense(self, arr: str, rev):
+        """Every model's interpretation of array ``arr`` at small indices as one
+        (n_models, K) uint64 matrix plus the defaults (the witness seeds'
+        calldata bytes): a constant-index select column is then one numpy
+        slice instead of a dictionary lookup per model.  None when a value
+        does not fit 64 bits."""
+        got = self._dense_cache.get(arr)
+        if got is not None and got[0] == rev:
+            return got[1]
+        nm = len(self.assigns)
+        keys, vals, dflt = [], [], np.zeros(nm, dtype=np.uint64)
+        top = 0
+        for m, a in enumerate(self.assigns):
+            interp = a.get(arr)
+            if not isinstance(interp, ArrayInterp):
+                keys.append(()), vals.append(())
+                continue
+            if interp.default >> 64:
+                self._dense_cache[arr] = (rev, None)
+                return None
+            dflt[m] = interp.default
+            ks = [k for k in interp.entries if k < self.DENSE_KEYS]
+            vs = [interp.entries[k] for k in ks]
+            if vs and max(vs) >> 64:
+                self._dense_cache[arr] = (rev, None)
+                return None
+            keys.append(ks), vals.append(vs)
+            if ks:
+                top = max(top, max(ks) + 1)
+        mat = np.repeat(dflt[:, None], top, axis=1)
+        for m in range(nm):
+            if keys[m]:
+                mat[m, keys[m]] = vals[m]
+        out = (mat, dflt)
+        self._dense_cache[arr] = (rev, out)
+        return out
 
     def _tab(self, sig) -> tuple:
         """(start, count, entries, default) of one table over every model.
