@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--symbolic-replicas", type=int, default=8,
                     help="replicas of each contract in the symbolic_tx field (0: off)")
     ap.add_argument("--symbolic-tx", type=int, default=2, help="transactions of the symbolic_tx field (-t)")
+    ap.add_argument("--analyses", type=int, default=2,
+                    help="transactions (-t) of the 18-contract analyses field (0: skip)")
     ap.add_argument("--seed-models", type=int, default=1024,
                     help="witness seed models beside the LRU cache in the symbolic_tx field")
     ap.add_argument("--taint-modes", default="device,host",
@@ -266,6 +268,12 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         symb = host_profiled("symbolic_tx", lambda: run_symbolic_tx(
             dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models, log=lambda m: _log(rank, m)))
 
+    analyses = None
+    if args.analyses and gpu and not args.profile_only:
+        _log(rank, f"18-contract analyses (-t {args.analyses})")
+        analyses = host_profiled("analyses", lambda: run_analyses(
+            dev, args.analyses, args.seed_models, log=lambda m: _log(rank, m)))
+
     c4 = None
     if not args.no_c4:
         _log(rank, "C4")
@@ -323,6 +331,8 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["taint_lanes"] = taintlanes
         if symb is not None:
             out["symbolic_tx"] = symb
+        if analyses is not None:
+            out["analyses"] = analyses
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
@@ -815,6 +825,88 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
         tx_id_manager.restart_counter()
         solver.get_model.cache_clear()
     return out
+
+
+def run_analyses(dev, tx_count: int, n_seeds: int, log=None, escape_handler=None, names=None):
+    """The 18 reference contracts (tests/testdata/inputs/*.sol.o, the inputs of
+    analysis_tests.py and the graph/statespace tests) analysed as ``myth
+    analyze -f <code> -t tx_count`` explores them (analysis/symbolic.py:82-200:
+    creator and attacker accounts, BFS + BoundedLoopsStrategy(3), max depth
+    128, a symbolic creation then tx_count symbolic message calls), with the
+    fork filter and the reachability filter on kernel 2 over the model cache
+    plus ``n_seeds`` witness seeds.  No detection modules and no SMT backend:
+    a query no candidate satisfies is UNKNOWN and its path kept; escaped paths
+    (no host handler for CALL*, SELFDESTRUCT, ...) are dropped and counted.
+    With N ranks the contracts are dealt round-robin (total work fixed); the
+    whole-job rates sum the ranks' work over the slowest rank's wall time."""
+    from mythril_amd import dist as mdist
+    from mythril_amd import workloads
+    from mythril_amd.laser import (Account, BoundedLoopsStrategy, BreadthFirstSearchStrategy, LaserEVM,
+                                   WorldState)
+    from mythril_amd.laser.transaction import ACTORS, tx_id_manager
+    from mythril_amd.laser.witness import WitnessSeeds
+    from mythril_amd.smt import solver
+    from mythril_amd.smt.exponent_manager import exponent_function_manager
+    from mythril_amd.smt.keccak_manager import keccak_function_manager
+    rank, world = mdist.rank_world()
+    names = sorted(names or workloads.bytecode_names())
+    per, tot = {}, {"wall_s": 0.0, "kernel1_s": 0.0, "kernel2_s": 0.0, "lane_steps": 0, "queries": 0,
+                    "answered": 0, "unknown": 0, "constraint_evals": 0, "escapes_dropped": 0,
+                    "forks": 0, "pruned": 0}
+    saved_cache = solver.model_cache
+    try:
+        for name in names[rank::world]:
+            keccak_function_manager.reset()
+            exponent_function_manager.reset()
+            tx_id_manager.restart_counter()
+            solver.get_model.cache_clear()
+            code = workloads.bytecode(name)
+            mc = solver.ModelCache(device=dev)
+            mc.seed_source = WitnessSeeds([code], n=n_seeds, balance_names=["balance"])
+            solver.model_cache = mc
+            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, max_depth=128,
+                             execution_timeout=86400, create_timeout=10, transaction_count=tx_count,
+                             requires_statespace=False, escape_handler=escape_handler)
+            laser.unknown_forks = "keep"
+            laser.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
+            ws = WorldState()
+            for actor in ("CREATOR", "ATTACKER"):
+                ws.put_account(Account(ACTORS[actor], contract_name=None))
+            if log:
+                log(f"analyses: {name}")
+            t0 = time.perf_counter()
+            laser.sym_exec(world_state=ws, creation_code=code, contract_name="MAIN")
+            wall = time.perf_counter() - t0
+            st = mc.stats
+            row = {"wall_s": wall, "kernel1_s": laser.device_ms / 1e3, "kernel2_s": mc.device_ms / 1e3,
+                   "lane_steps": int(laser.lane_steps), "queries": st["queries"],
+                   "answered": st["lru_hits"] + st["seed_hits"], "unknown": st["misses"],
+                   "constraint_evals": int(mc.device_evals), "escapes_dropped": laser.escapes_dropped,
+                   "forks": laser.forks, "pruned": laser.fork_stats.get("pruned", 0),
+                   "open_states": len(laser.open_states)}
+            per[name] = row
+            for k in tot:
+                tot[k] += row[k]
+    finally:
+        solver.model_cache = saved_cache
+        keccak_function_manager.reset()
+        exponent_function_manager.reset()
+        tx_id_manager.restart_counter()
+        solver.get_model.cache_clear()
+    job_wall, job_evals = mdist.reduce_timing(tot["wall_s"], float(tot["constraint_evals"]))
+    _, job_steps = mdist.reduce_timing(tot["wall_s"], float(tot["lane_steps"]))
+    _, job_q = mdist.reduce_timing(tot["wall_s"], float(tot["queries"]))
+    _, job_a = mdist.reduce_timing(tot["wall_s"], float(tot["answered"]))
+    return {"metric": "in-situ constraint-evals/s of the fork and reachability filters over the 18 "
+                      "reference contracts, -t %d" % tx_count,
+            "mode": "prefilter-only (no SMT backend, no detection modules); escaped paths dropped (counted)",
+            "transactions": tx_count, "seed_models": n_seeds, "contracts_analysed": len(per),
+            "ranks": world, "totals": tot,
+            "job_wall_s": job_wall, "job_constraint_evals_per_s_wall": job_evals / job_wall if job_wall else None,
+            "job_lane_steps_per_s": job_steps / job_wall if job_wall else None,
+            "prefilter_hit_rate": job_a / job_q if job_q else None,
+            "host_fraction": 1.0 - (tot["kernel1_s"] + tot["kernel2_s"]) / tot["wall_s"] if tot["wall_s"] else None,
+            "contracts": per}
 
 
 def run_c4(args, dev, rank, world, barrier, dist_on):

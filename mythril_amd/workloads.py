@@ -26,6 +26,11 @@ C2_SEED = 0x4D595448
 C2_SELECTORS = (0x18160DDD, 0x70A08231, 0xA3210E87)     # totalSupply, balanceOf, sendeth
 
 
+def bytecode_names():
+    """The reference's precompiled test contracts (tests/testdata/inputs/*.sol.o)."""
+    return list(json.loads((GOLDEN / "bytecodes.json").read_text()))
+
+
 def bytecode(name: str) -> bytes:
     codes = json.loads((GOLDEN / "bytecodes.json").read_text())
     return bytes.fromhex(codes[name])
