@@ -61,7 +61,6 @@ struct mg_ctx {
     // pinned host side of the batched transfers (XferPlan): one DMA per phase
     uint8_t *h_xfer = nullptr;
     size_t h_xfer_bytes = 0;
-    bool xfer_legacy = false;            // MG_XFER=legacy: one pageable copy + sync per field (A/B)
     DevCounters *d_ctr = nullptr;        // [blocks] per-block statistics of the last launch
     uint32_t ctr_cap = 0;
     std::vector<DevCounters> h_ctr;
@@ -217,8 +216,6 @@ extern "C" int mg_open(int device, mg_ctx **out) {
             if (v != 64 && v != 32 && v != 16) { rc = MG_EINVAL; break; }
             ctx->lpw = (uint32_t)v;
         }
-        const char *xf = getenv("MG_XFER");
-        ctx->xfer_legacy = xf && std::string(xf) == "legacy";
     } while (0);
     if (rc != MG_OK) { mg_close(ctx); return rc; }
     *out = ctx;
@@ -562,96 +559,14 @@ static int ensure_stage(mg_ctx *ctx, size_t bytes) {
 
 static unsigned blocks_for(size_t work, unsigned bs = 256) { return (unsigned)((work + bs - 1) / bs); }
 
-// upload one lane-major field of Uh units x W dwords per lane
-static int up_units(mg_ctx *ctx, const void *host, uint32_t n, uint32_t Uh, uint32_t W, void *dst, uint32_t first) {
-    if (!host || Uh == 0) return MG_OK;
-    const size_t bytes = (size_t)n * Uh * W * 4;
-    int rc;
-    if ((rc = ensure_stage(ctx, bytes))) return rc;
-    HIPX(ctx, hipMemcpyAsync(ctx->d_stage, host, bytes, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_scatter_units, dim3(blocks_for((size_t)n * Uh * W)), dim3(256), 0, ctx->stream,
-                       (const uint32_t *)ctx->d_stage, n, Uh, W, (uint32_t *)dst, ctx->L.N, first);
-    HIPX(ctx, hipGetLastError());
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    return MG_OK;
-}
-// Uc (<= Uh): units copied per lane (the rest of each host row is left as is)
-static int down_units(mg_ctx *ctx, void *host, uint32_t n, uint32_t Uh, uint32_t W, const void *src, uint32_t first,
-                      uint32_t Uc = 0xffffffffu) {
-    if (!host || Uh == 0) return MG_OK;
-    Uc = std::min(Uc, Uh);
-    if (Uc == 0 || n == 0) return MG_OK;
-    const size_t bytes = (size_t)n * Uc * W * 4;
-    int rc;
-    if ((rc = ensure_stage(ctx, bytes))) return rc;
-    hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)n * Uc * W)), dim3(256), 0, ctx->stream,
-                       (const uint32_t *)src, n, Uc, W, (uint32_t *)ctx->d_stage, ctx->L.N, first);
-    HIPX(ctx, hipGetLastError());
-    if (Uc == Uh) {
-        HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    } else {
-        HIPX(ctx, hipMemcpy2DAsync(host, (size_t)Uh * W * 4, ctx->d_stage, (size_t)Uc * W * 4, (size_t)Uc * W * 4,
-                                   n, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    return MG_OK;
-}
-static int up_bytes(mg_ctx *ctx, const uint8_t *host, uint32_t n, uint32_t bytes_h, uint32_t *dst, uint32_t first) {
-    if (!host || bytes_h == 0) return MG_OK;
-    const uint32_t Dh = bytes_h / 4;
-    const size_t bytes = (size_t)n * bytes_h;
-    int rc;
-    if ((rc = ensure_stage(ctx, bytes))) return rc;
-    HIPX(ctx, hipMemcpyAsync(ctx->d_stage, host, bytes, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_scatter_bytes, dim3(blocks_for((size_t)n * Dh)), dim3(256), 0, ctx->stream,
-                       (const uint8_t *)ctx->d_stage, n, Dh, dst, ctx->L.N, first);
-    HIPX(ctx, hipGetLastError());
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    return MG_OK;
-}
-// Dc (<= bytes_h / 4): dwords copied per lane (the rest of each host row is left as is)
-static int down_bytes(mg_ctx *ctx, uint8_t *host, uint32_t n, uint32_t bytes_h, const uint32_t *src, uint32_t first,
-                      uint32_t Dc = 0xffffffffu) {
-    if (!host || bytes_h == 0) return MG_OK;
-    const uint32_t Dh = bytes_h / 4;
-    Dc = std::min(Dc, Dh);
-    if (Dc == 0 || n == 0) return MG_OK;
-    const size_t bytes = (size_t)n * Dc * 4;
-    int rc;
-    if ((rc = ensure_stage(ctx, bytes))) return rc;
-    hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)n * Dc)), dim3(256), 0, ctx->stream,
-                       src, n, Dc, (uint8_t *)ctx->d_stage, ctx->L.N, first);
-    HIPX(ctx, hipGetLastError());
-    if (Dc == Dh) {
-        HIPX(ctx, hipMemcpyAsync(host, ctx->d_stage, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    } else {
-        HIPX(ctx, hipMemcpy2DAsync(host, (size_t)bytes_h, ctx->d_stage, (size_t)Dc * 4, (size_t)Dc * 4, n,
-                                   hipMemcpyDeviceToHost, ctx->stream));
-    }
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    return MG_OK;
-}
-static int up_scalar(mg_ctx *ctx, const void *host, size_t elem, uint32_t n, void *dst, uint32_t first) {
-    if (!host) return MG_OK;
-    HIPX(ctx, hipMemcpyAsync((char *)dst + (size_t)first * elem, host, (size_t)n * elem,
-                             hipMemcpyHostToDevice, ctx->stream));
-    return MG_OK;
-}
-static int down_scalar(mg_ctx *ctx, void *host, size_t elem, uint32_t n, const void *src, uint32_t first) {
-    if (!host) return MG_OK;
-    HIPX(ctx, hipMemcpyAsync(host, (const char *)src + (size_t)first * elem, (size_t)n * elem,
-                             hipMemcpyDeviceToHost, ctx->stream));
-    return MG_OK;
-}
-
 // ---- batched transfers ---------------------------------------------------------
 // One host<->device transfer of many lane fields.  Download: every field is
 // gathered (lane-major) into the device stage, ONE DMA copies the stage into a
 // pinned host buffer, ONE stream synchronisation, then the host copies the
 // rows into the caller's arrays.  Upload: the rows are packed into the pinned
 // buffer, ONE DMA, then scatter kernels / device copies (the caller syncs once).
-// The per-field form (pageable copy + synchronisation per field, kept as
-// MG_XFER=legacy) cost ~2.5 ms per LaserEVM launch (profiles/r03/hostprof).
+// The per-field form it replaced (pageable copy + synchronisation per field,
+// now ab/xfer_legacy.diff) cost ~2.5 ms per LaserEVM launch (profiles/r03/hostprof).
 struct XferPlan {
     enum Kind { SCALAR, UNITS, BYTES };
     struct Item {
@@ -797,60 +712,6 @@ static int check_host_shape(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, u
     return MG_OK;
 }
 
-// MG_XFER=legacy: the per-field upload (one pageable copy + synchronisation per field)
-static int lanes_upload_legacy(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
-    DevLanes &L = ctx->L;
-    int rc;
-    const size_t S4 = 4, S8 = 8;
-    if ((rc = up_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
-    if ((rc = up_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
-    if ((rc = up_scalar(ctx, h->sp, S4, n, L.sp, first))) return rc;
-    if ((rc = up_scalar(ctx, h->msize, S4, n, L.msize, first))) return rc;
-    if ((rc = up_scalar(ctx, h->depth, S4, n, L.depth, first))) return rc;
-    if ((rc = up_scalar(ctx, h->status, S4, n, L.status, first))) return rc;
-    if ((rc = up_scalar(ctx, h->aux, S4, n, L.aux, first))) return rc;
-    if ((rc = up_scalar(ctx, h->steps, S4, n, L.steps, first))) return rc;
-    if ((rc = up_scalar(ctx, h->flags, S4, n, L.flags, first))) return rc;
-    if ((rc = up_scalar(ctx, h->calldata_len, S4, n, L.calldata_len, first))) return rc;
-    if ((rc = up_scalar(ctx, h->storage_count, S4, n, L.storage_count, first))) return rc;
-    if ((rc = up_scalar(ctx, h->ret_offset, S4, n, L.ret_offset, first))) return rc;
-    if ((rc = up_scalar(ctx, h->ret_len, S4, n, L.ret_len, first))) return rc;
-    if ((rc = up_scalar(ctx, h->gas_min, S8, n, L.gas_min, first))) return rc;
-    if ((rc = up_scalar(ctx, h->gas_max, S8, n, L.gas_max, first))) return rc;
-    if ((rc = up_scalar(ctx, h->gas_limit, S8, n, L.gas_limit, first))) return rc;
-    // resident initial image
-    if ((rc = up_scalar(ctx, h->pc, S4, n, ctx->i_pc, first))) return rc;
-    if ((rc = up_scalar(ctx, h->depth, S4, n, ctx->i_depth, first))) return rc;
-    if ((rc = up_scalar(ctx, h->status, S4, n, ctx->i_status, first))) return rc;
-    if ((rc = up_scalar(ctx, h->aux, S4, n, ctx->i_aux, first))) return rc;
-    if ((rc = up_scalar(ctx, h->steps, S4, n, ctx->i_steps, first))) return rc;
-    if ((rc = up_scalar(ctx, h->storage_count, S4, n, ctx->i_storage_count, first))) return rc;
-    if ((rc = up_scalar(ctx, h->gas_min, S8, n, ctx->i_gas_min, first))) return rc;
-    if ((rc = up_scalar(ctx, h->gas_max, S8, n, ctx->i_gas_max, first))) return rc;
-    HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
-    HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = up_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first))) return rc;
-    if ((rc = up_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
-    if ((rc = up_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first))) return rc;
-    if ((rc = up_units(ctx, h->storage, n, h->storage_cap, 16, ctx->i_storage, first))) return rc;
-    if ((rc = up_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first))) return rc;
-    if ((rc = up_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
-    if (h->trace_cap) {
-        if ((rc = up_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
-        if ((rc = up_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first))) return rc;
-    } else {
-        HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
-    }
-    if (h->rec_cap) {
-        if ((rc = up_scalar(ctx, h->rec_len, S4, n, L.rec_len, first))) return rc;
-        if ((rc = up_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first))) return rc;
-    } else {
-        HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
-    }
-    return MG_OK;
-}
-
 static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n, bool live);
 
 extern "C" int mg_lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint32_t n) {
@@ -882,48 +743,44 @@ static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint3
     for (uint32_t i = 0; i < n && fresh; ++i)
         fresh = h->sp[i] == 0 && h->msize[i] == 0 && (!h->trace_cap || h->trace_len[i] == 0) &&
                 (!h->rec_cap || h->rec_len[i] == 0);
-    if (ctx->xfer_legacy) {
-        if ((rc = lanes_upload_legacy(ctx, h, first, n))) return rc;
-    } else {
-        const uint32_t ALL = 0xffffffffu;
-        XferPlan x(n, first);
-        x.scalar(h->code_id, L.code_id, 4);
-        x.scalar(h->pc, L.pc, 4, ctx->i_pc);
-        x.scalar(h->sp, L.sp, 4);
-        x.scalar(h->msize, L.msize, 4);
-        x.scalar(h->depth, L.depth, 4, ctx->i_depth);
-        x.scalar(h->status, L.status, 4, ctx->i_status);
-        x.scalar(h->aux, L.aux, 4, ctx->i_aux);
-        x.scalar(h->steps, L.steps, 4, ctx->i_steps);
-        x.scalar(h->flags, L.flags, 4);
-        x.scalar(h->calldata_len, L.calldata_len, 4);
-        x.scalar(h->storage_count, L.storage_count, 4, ctx->i_storage_count);
-        x.scalar(h->ret_offset, L.ret_offset, 4);
-        x.scalar(h->ret_len, L.ret_len, 4);
-        x.scalar(h->gas_min, L.gas_min, 8, ctx->i_gas_min);
-        x.scalar(h->gas_max, L.gas_max, 8, ctx->i_gas_max);
-        x.scalar(h->gas_limit, L.gas_limit, 8);
-        x.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
-        x.units(h->env, MG_ENV_WORDS, 8, L.env);
-        x.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL,
-                ctx->i_storage);
-        x.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
-        x.bytes(h->calldata, h->calldata_cap, L.calldata);
-        if (h->trace_cap) {
-            x.scalar(h->trace_len, L.trace_len, 4);
-            x.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
-        }
-        if (h->rec_cap) {
-            x.scalar(h->rec_len, L.rec_len, 4);
-            x.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
-        }
-        HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
-        HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
-        if (!h->trace_cap) HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
-        if (!h->rec_cap) HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
-        if ((rc = xfer_up(ctx, x))) return rc;
-        HIPX(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t ALL = 0xffffffffu;
+    XferPlan x(n, first);
+    x.scalar(h->code_id, L.code_id, 4);
+    x.scalar(h->pc, L.pc, 4, ctx->i_pc);
+    x.scalar(h->sp, L.sp, 4);
+    x.scalar(h->msize, L.msize, 4);
+    x.scalar(h->depth, L.depth, 4, ctx->i_depth);
+    x.scalar(h->status, L.status, 4, ctx->i_status);
+    x.scalar(h->aux, L.aux, 4, ctx->i_aux);
+    x.scalar(h->steps, L.steps, 4, ctx->i_steps);
+    x.scalar(h->flags, L.flags, 4);
+    x.scalar(h->calldata_len, L.calldata_len, 4);
+    x.scalar(h->storage_count, L.storage_count, 4, ctx->i_storage_count);
+    x.scalar(h->ret_offset, L.ret_offset, 4);
+    x.scalar(h->ret_len, L.ret_len, 4);
+    x.scalar(h->gas_min, L.gas_min, 8, ctx->i_gas_min);
+    x.scalar(h->gas_max, L.gas_max, 8, ctx->i_gas_max);
+    x.scalar(h->gas_limit, L.gas_limit, 8);
+    x.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
+    x.units(h->env, MG_ENV_WORDS, 8, L.env);
+    x.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL,
+            ctx->i_storage);
+    x.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
+    x.bytes(h->calldata, h->calldata_cap, L.calldata);
+    if (h->trace_cap) {
+        x.scalar(h->trace_len, L.trace_len, 4);
+        x.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
     }
+    if (h->rec_cap) {
+        x.scalar(h->rec_len, L.rec_len, 4);
+        x.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
+    }
+    HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
+    HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
+    if (!h->trace_cap) HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
+    if (!h->rec_cap) HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
+    if ((rc = xfer_up(ctx, x))) return rc;
+    HIPX(ctx, hipStreamSynchronize(ctx->stream));
     ctx->uploaded = true;
     ctx->init_fresh = (first == 0 && n == L.n) ? fresh : (ctx->init_fresh && fresh);
     return MG_OK;
@@ -977,27 +834,16 @@ extern "C" int mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, u
     for (uint32_t i = 0; i < n; ++i)
         if (h->n_nodes[i] > h->node_cap || h->n_consts[i] > h->const_cap)
             return set_err(ctx, MG_EINVAL, "lane %u: arena exceeds its host capacities", first + i);
-    if (!ctx->xfer_legacy) {
-        XferPlan x(n, first);
-        x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
-        x.scalar(h->n_consts, ctx->S.n_consts, 4);
-        x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
-        x.units(h->node, h->node_cap, 4, ctx->S.node);
-        x.units(h->cval, h->const_cap, 8, ctx->S.cval);
-        x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
-        x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
-        if ((rc = xfer_up(ctx, x))) return rc;
-        HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        return MG_OK;
-    }
-    if ((rc = up_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
-    if ((rc = up_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
+    XferPlan x(n, first);
+    x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
+    x.scalar(h->n_consts, ctx->S.n_consts, 4);
+    x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
+    x.units(h->node, h->node_cap, 4, ctx->S.node);
+    x.units(h->cval, h->const_cap, 8, ctx->S.cval);
+    x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
+    x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
+    if ((rc = xfer_up(ctx, x))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = up_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
-    if ((rc = up_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
-    if ((rc = up_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
-    if ((rc = up_units(ctx, h->mtag, n, h->mem_cap, 1, ctx->S.mtag, first))) return rc;
-    if ((rc = up_units(ctx, h->sttag, n, h->storage_cap, 2, ctx->S.sttag, first))) return rc;
     return MG_OK;
 }
 
@@ -1006,26 +852,15 @@ extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint3
     int rc;
     if ((rc = check_sym_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
-    if (!ctx->xfer_legacy) {
-        XferPlan x(n, first);
-        x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
-        x.scalar(h->n_consts, ctx->S.n_consts, 4);
-        x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
-        x.units(h->node, h->node_cap, 4, ctx->S.node);
-        x.units(h->cval, h->const_cap, 8, ctx->S.cval);
-        x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
-        x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
-        return xfer_down(ctx, x);
-    }
-    if ((rc = down_scalar(ctx, h->n_nodes, 4, n, ctx->S.n_nodes, first))) return rc;
-    if ((rc = down_scalar(ctx, h->n_consts, 4, n, ctx->S.n_consts, first))) return rc;
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = down_units(ctx, h->stag, n, h->stack_cap, 1, ctx->S.stag, first))) return rc;
-    if ((rc = down_units(ctx, h->node, n, h->node_cap, 4, ctx->S.node, first))) return rc;
-    if ((rc = down_units(ctx, h->cval, n, h->const_cap, 8, ctx->S.cval, first))) return rc;
-    if ((rc = down_units(ctx, h->mtag, n, h->mem_cap, 1, ctx->S.mtag, first))) return rc;
-    if ((rc = down_units(ctx, h->sttag, n, h->storage_cap, 2, ctx->S.sttag, first))) return rc;
-    return MG_OK;
+    XferPlan x(n, first);
+    x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
+    x.scalar(h->n_consts, ctx->S.n_consts, 4);
+    x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
+    x.units(h->node, h->node_cap, 4, ctx->S.node);
+    x.units(h->cval, h->const_cap, 8, ctx->S.cval);
+    x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
+    x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
+    return xfer_down(ctx, x);
 }
 
 // ---- taint planes ------------------------------------------------------------
@@ -1136,29 +971,17 @@ extern "C" int mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *h, uint32_t firs
                 return set_err(ctx, MG_EINVAL, "lane %u slot %u: handle %u past obj_cap", first + i, k, so[k]);
     }
     DevTaint &T = ctx->T;
-    if (!ctx->xfer_legacy) {
-        XferPlan x(n, first);
-        x.scalar(h->n_obj, T.n_obj, 4);
-        x.scalar(h->n_fixed, T.n_fixed, 4);
-        x.scalar(h->n_atoms, T.n_atoms, 4);
-        x.scalar(h->tflags, T.tflags, 4);
-        x.scalar(h->sink, T.sink, 8);
-        x.scalar(h->ymask, T.ymask, 8);
-        x.units(h->sobj, h->stack_cap, 1, T.sobj);
-        x.units(h->omask, h->obj_cap, 2, T.omask);
-        if ((rc = xfer_up(ctx, x))) return rc;
-        HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        return MG_OK;
-    }
-    if ((rc = up_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
-    if ((rc = up_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
-    if ((rc = up_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
-    if ((rc = up_scalar(ctx, h->tflags, 4, n, T.tflags, first))) return rc;
-    if ((rc = up_scalar(ctx, h->sink, 8, n, T.sink, first))) return rc;
-    if ((rc = up_scalar(ctx, h->ymask, 8, n, T.ymask, first))) return rc;
+    XferPlan x(n, first);
+    x.scalar(h->n_obj, T.n_obj, 4);
+    x.scalar(h->n_fixed, T.n_fixed, 4);
+    x.scalar(h->n_atoms, T.n_atoms, 4);
+    x.scalar(h->tflags, T.tflags, 4);
+    x.scalar(h->sink, T.sink, 8);
+    x.scalar(h->ymask, T.ymask, 8);
+    x.units(h->sobj, h->stack_cap, 1, T.sobj);
+    x.units(h->omask, h->obj_cap, 2, T.omask);
+    if ((rc = xfer_up(ctx, x))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = up_units(ctx, h->sobj, n, h->stack_cap, 1, T.sobj, first))) return rc;
-    if ((rc = up_units(ctx, h->omask, n, h->obj_cap, 2, T.omask, first))) return rc;
     return MG_OK;
 }
 
@@ -1168,28 +991,16 @@ extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, u
     if ((rc = check_taint_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
     DevTaint &T = ctx->T;
-    if (!ctx->xfer_legacy) {
-        XferPlan x(n, first);
-        x.scalar(h->n_obj, T.n_obj, 4);
-        x.scalar(h->n_fixed, T.n_fixed, 4);
-        x.scalar(h->n_atoms, T.n_atoms, 4);
-        x.scalar(h->tflags, T.tflags, 4);
-        x.scalar(h->sink, T.sink, 8);
-        x.scalar(h->ymask, T.ymask, 8);
-        x.units(h->sobj, h->stack_cap, 1, T.sobj);
-        x.units(h->omask, h->obj_cap, 2, T.omask);
-        return xfer_down(ctx, x);
-    }
-    if ((rc = down_scalar(ctx, h->n_obj, 4, n, T.n_obj, first))) return rc;
-    if ((rc = down_scalar(ctx, h->n_fixed, 4, n, T.n_fixed, first))) return rc;
-    if ((rc = down_scalar(ctx, h->n_atoms, 4, n, T.n_atoms, first))) return rc;
-    if ((rc = down_scalar(ctx, h->tflags, 4, n, T.tflags, first))) return rc;
-    if ((rc = down_scalar(ctx, h->sink, 8, n, T.sink, first))) return rc;
-    if ((rc = down_scalar(ctx, h->ymask, 8, n, T.ymask, first))) return rc;
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = down_units(ctx, h->sobj, n, h->stack_cap, 1, T.sobj, first))) return rc;
-    if ((rc = down_units(ctx, h->omask, n, h->obj_cap, 2, T.omask, first))) return rc;
-    return MG_OK;
+    XferPlan x(n, first);
+    x.scalar(h->n_obj, T.n_obj, 4);
+    x.scalar(h->n_fixed, T.n_fixed, 4);
+    x.scalar(h->n_atoms, T.n_atoms, 4);
+    x.scalar(h->tflags, T.tflags, 4);
+    x.scalar(h->sink, T.sink, 8);
+    x.scalar(h->ymask, T.ymask, 8);
+    x.units(h->sobj, h->stack_cap, 1, T.sobj);
+    x.units(h->omask, h->obj_cap, 2, T.omask);
+    return xfer_down(ctx, x);
 }
 
 
@@ -1209,82 +1020,39 @@ static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t 
     if ((rc = check_host_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
     DevLanes &L = ctx->L;
-    if (!ctx->xfer_legacy) {
-        // phase 1: the per-lane scalars (they bound phase 2's rows)
-        XferPlan x(n, first);
-        x.scalar(h->code_id, L.code_id, 4);
-        x.scalar(h->pc, L.pc, 4);
-        x.scalar(h->sp, L.sp, 4);
-        x.scalar(h->msize, L.msize, 4);
-        x.scalar(h->depth, L.depth, 4);
-        x.scalar(h->status, L.status, 4);
-        x.scalar(h->aux, L.aux, 4);
-        x.scalar(h->steps, L.steps, 4);
-        x.scalar(h->flags, L.flags, 4);
-        x.scalar(h->calldata_len, L.calldata_len, 4);
-        x.scalar(h->storage_count, L.storage_count, 4);
-        x.scalar(h->ret_offset, L.ret_offset, 4);
-        x.scalar(h->ret_len, L.ret_len, 4);
-        x.scalar(h->gas_min, L.gas_min, 8);
-        x.scalar(h->gas_max, L.gas_max, 8);
-        x.scalar(h->gas_limit, L.gas_limit, 8);
-        if (h->trace_cap) x.scalar(h->trace_len, L.trace_len, 4);
-        if (h->rec_cap) x.scalar(h->rec_len, L.rec_len, 4);
-        if ((rc = xfer_down(ctx, x))) return rc;
-        // phase 2: rows; live: only what a step can have written, below the
-        // range's largest sp / storage count / msize / trace and record length
-        const uint32_t ALL = 0xffffffffu;
-        XferPlan y(n, first);
-        y.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
-        if (!live) y.units(h->env, MG_ENV_WORDS, 8, L.env);
-        y.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL);
-        y.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
-        if (!live) y.bytes(h->calldata, h->calldata_cap, L.calldata);
-        if (h->trace_cap) y.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
-        if (h->rec_cap) y.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
-        return xfer_down(ctx, y);
-    }
-    const size_t S4 = 4, S8 = 8;
-    if ((rc = down_scalar(ctx, h->code_id, S4, n, L.code_id, first))) return rc;
-    if ((rc = down_scalar(ctx, h->pc, S4, n, L.pc, first))) return rc;
-    if ((rc = down_scalar(ctx, h->sp, S4, n, L.sp, first))) return rc;
-    if ((rc = down_scalar(ctx, h->msize, S4, n, L.msize, first))) return rc;
-    if ((rc = down_scalar(ctx, h->depth, S4, n, L.depth, first))) return rc;
-    if ((rc = down_scalar(ctx, h->status, S4, n, L.status, first))) return rc;
-    if ((rc = down_scalar(ctx, h->aux, S4, n, L.aux, first))) return rc;
-    if ((rc = down_scalar(ctx, h->steps, S4, n, L.steps, first))) return rc;
-    if ((rc = down_scalar(ctx, h->flags, S4, n, L.flags, first))) return rc;
-    if ((rc = down_scalar(ctx, h->calldata_len, S4, n, L.calldata_len, first))) return rc;
-    if ((rc = down_scalar(ctx, h->storage_count, S4, n, L.storage_count, first))) return rc;
-    if ((rc = down_scalar(ctx, h->ret_offset, S4, n, L.ret_offset, first))) return rc;
-    if ((rc = down_scalar(ctx, h->ret_len, S4, n, L.ret_len, first))) return rc;
-    if ((rc = down_scalar(ctx, h->gas_min, S8, n, L.gas_min, first))) return rc;
-    if ((rc = down_scalar(ctx, h->gas_max, S8, n, L.gas_max, first))) return rc;
-    if ((rc = down_scalar(ctx, h->gas_limit, S8, n, L.gas_limit, first))) return rc;
-    HIPX(ctx, hipStreamSynchronize(ctx->stream));
-    // live: only what a step can have written, below the range's largest bound
+    // phase 1: the per-lane scalars (they bound phase 2's rows)
+    XferPlan x(n, first);
+    x.scalar(h->code_id, L.code_id, 4);
+    x.scalar(h->pc, L.pc, 4);
+    x.scalar(h->sp, L.sp, 4);
+    x.scalar(h->msize, L.msize, 4);
+    x.scalar(h->depth, L.depth, 4);
+    x.scalar(h->status, L.status, 4);
+    x.scalar(h->aux, L.aux, 4);
+    x.scalar(h->steps, L.steps, 4);
+    x.scalar(h->flags, L.flags, 4);
+    x.scalar(h->calldata_len, L.calldata_len, 4);
+    x.scalar(h->storage_count, L.storage_count, 4);
+    x.scalar(h->ret_offset, L.ret_offset, 4);
+    x.scalar(h->ret_len, L.ret_len, 4);
+    x.scalar(h->gas_min, L.gas_min, 8);
+    x.scalar(h->gas_max, L.gas_max, 8);
+    x.scalar(h->gas_limit, L.gas_limit, 8);
+    if (h->trace_cap) x.scalar(h->trace_len, L.trace_len, 4);
+    if (h->rec_cap) x.scalar(h->rec_len, L.rec_len, 4);
+    if ((rc = xfer_down(ctx, x))) return rc;
+    // phase 2: rows; live: only what a step can have written, below the
+    // range's largest sp / storage count / msize / trace and record length
     const uint32_t ALL = 0xffffffffu;
-    const uint32_t u_st = live ? max_of(h->sp, n) : ALL;
-    const uint32_t u_sto = live ? max_of(h->storage_count, n) : ALL;
-    const uint32_t d_mem = live ? (max_of(h->msize, n) + 3u) / 4u : ALL;
-    if ((rc = down_units(ctx, h->stack, n, h->stack_cap, 8, L.stack, first, u_st))) return rc;
-    if (!live && (rc = down_units(ctx, h->env, n, MG_ENV_WORDS, 8, L.env, first))) return rc;
-    if ((rc = down_units(ctx, h->storage, n, h->storage_cap, 16, L.storage, first, u_sto))) return rc;
-    if ((rc = down_bytes(ctx, h->memory, n, h->mem_cap, L.mem, first, d_mem))) return rc;
-    if (!live && (rc = down_bytes(ctx, h->calldata, n, h->calldata_cap, L.calldata, first))) return rc;
-    if (h->trace_cap) {
-        if ((rc = down_scalar(ctx, h->trace_len, S4, n, L.trace_len, first))) return rc;
-        HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        if ((rc = down_units(ctx, h->trace, n, h->trace_cap, 1, L.trace, first,
-                             live ? max_of(h->trace_len, n) : ALL))) return rc;
-    }
-    if (h->rec_cap) {
-        if ((rc = down_scalar(ctx, h->rec_len, S4, n, L.rec_len, first))) return rc;
-        HIPX(ctx, hipStreamSynchronize(ctx->stream));
-        if ((rc = down_units(ctx, h->rec, n, h->rec_cap, 1, L.rec, first, live ? max_of(h->rec_len, n) : ALL)))
-            return rc;
-    }
-    return MG_OK;
+    XferPlan y(n, first);
+    y.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
+    if (!live) y.units(h->env, MG_ENV_WORDS, 8, L.env);
+    y.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL);
+    y.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
+    if (!live) y.bytes(h->calldata, h->calldata_cap, L.calldata);
+    if (h->trace_cap) y.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
+    if (h->rec_cap) y.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
+    return xfer_down(ctx, y);
 }
 
 extern "C" int mg_set_loop_bound(mg_ctx *ctx, uint32_t bound) {
@@ -1387,7 +1155,8 @@ static LdsPlan lds_plan(const mg_ctx *ctx) {
     return p;
 }
 
-// MG_K1_RUNS=reg: straight-line runs in the register form only (A/B switch,
+// MG_K1_RUNS=reg: straight-line runs in the register form only (the fallback
+// form; forced for the parity tests and A/B runs,
 // read per launch so one process can alternate the two forms)
 static uint32_t k1_flags() {
     const char *r = getenv("MG_K1_RUNS");

@@ -10,7 +10,9 @@ switches the library reads per launch force every layout onto small codes:
 * MG_K1_PUSH=global: push immediates read from the code arena;
 * MG_K1_MEMWIN: LDS memory window bytes per lane (0 = off; 32 puts the
   window's edge inside the free-memory pointer's word; 1024 covers all of C2's
-  memory), with the VMTests' unaligned and straddling memory accesses.
+  memory), with the VMTests' unaligned and straddling memory accesses;
+* MG_K1_RUNS=reg: every straight-line run in the register form (the fallback
+  for a run whose stack window does not fit the LDS-resident form).
 """
 import os
 
@@ -25,7 +27,7 @@ from vmtests_util import fill_lane, load_vmtests, vm_shape
 
 pytestmark = pytest.mark.gpu
 
-SWITCHES = ("MG_K1_PD_CAP", "MG_K1_JR_CAP", "MG_K1_PUSH", "MG_K1_MEMWIN")
+SWITCHES = ("MG_K1_PD_CAP", "MG_K1_JR_CAP", "MG_K1_PUSH", "MG_K1_MEMWIN", "MG_K1_RUNS")
 
 
 @pytest.fixture(scope="module")
@@ -54,6 +56,7 @@ def env():
     {"MG_K1_MEMWIN": "0"},
     {"MG_K1_MEMWIN": "32"},
     {"MG_K1_MEMWIN": "1024", "MG_K1_PD_CAP": "150"},
+    {"MG_K1_RUNS": "reg"},
 ])
 def test_c2_under_lds_plan_variants(dev, env, switches):
     env.update(switches)
