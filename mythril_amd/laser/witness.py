@@ -90,6 +90,8 @@ class WitnessSeeds:
         self._rev: Dict[str, int] = {}           # interpretation changes per name (PoolColumns)
         self._tx_top = -1
         self._sym_pts = 0                        # symbolic EXP points completed so far
+        self._pw_seen: set = set()               # concrete EXP points entered into every seed
+        self._cc_seen: set = set()               # concrete hashes entered into every seed
 
     def revision(self, name: str) -> int:
         return self._rev.get(name, 0)
@@ -174,14 +176,17 @@ class WitnessSeeds:
         # an interpretation's revision changes only when entries are added to it
         # (PoolColumns re-serialises a table per revision)
         changed = set()
-        for m, a in enumerate(self.assign):
+        # concrete points and hashes only accumulate: each is entered into the
+        # seeds once (an entry a seed already holds is left as it is)
+        new_pw = [(k, v) for k, v in power.items() if k not in self._pw_seen]
+        new_cc = [(k, h) for k, h in concrete.items() if k not in self._cc_seen]
+        for a in self.assign:
             pw = a.setdefault("Power", FuncInterp(0, {}))
-            if len(pw.entries) != len(power):
-                for (b, e), v in power.items():
-                    if (b, e) not in pw.entries:
-                        pw.entries[(b, e)] = v
-                        changed.add("Power")
-            for (n, cv), h in concrete.items():
+            for be, v in new_pw:
+                if be not in pw.entries:
+                    pw.entries[be] = v
+                    changed.add("Power")
+            for (n, cv), h in new_cc:
                 f = a.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
                 if (cv,) not in f.entries:
                     f.entries[(cv,)] = h
@@ -190,6 +195,8 @@ class WitnessSeeds:
                 if (h,) not in inv.entries:
                     inv.entries[(h,)] = cv
                     changed.add(f"keccak256_{n}-1")
+        self._pw_seen.update(k for k, _ in new_pw)
+        self._cc_seen.update(k for k, _ in new_cc)
         # inputs in registration order (an input may hash an earlier one's hash):
         # each evaluated under every seed at once, then entered into the seeds'
         # keccak tables

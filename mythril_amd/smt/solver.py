@@ -248,6 +248,7 @@ class ModelCache:
         # evaluates thousands where the reference keeps 100): consulted only
         # where the reference would call its SMT backend, see get_model
         self.seeds: List = []
+        self._seed_list = None
         # an object with models() and epoch (laser/witness.WitnessSeeds), or None
         self.seed_source = None
         self._seed_cols = None               # (epoch, PoolColumns) of the seeds
@@ -375,6 +376,11 @@ class ModelCache:
         # alive, so no model created later (after an LRU eviction frees one)
         # can take a dead model's id and read its bit
         alive = tuple(pool)
+        # the seeds as a contiguous tail of the pool (its usual shape, _full_pool):
+        # check_seeds then reads the first satisfying seed off the bitmap
+        ns = len(self.seeds)
+        tail = (self.seeds, len(pool) - ns) if ns and len(pool) >= ns and \
+            all(a is b for a, b in zip(pool[len(pool) - ns:], self.seeds)) else None
         for k in keys:
             acc = ones.copy()
             ok = True
@@ -389,7 +395,7 @@ class ModelCache:
                     break
                 acc &= r
             if ok:
-                out[k] = (pos, acc, alive)
+                out[k] = (pos, acc, alive, tail)
                 self.device_evals += len(pool)
         if keep:
             self._bits.update(out)
@@ -430,7 +436,12 @@ class ModelCache:
     # -- witness seeds and prefetched groups ------------------------------------
     def _seed_models(self) -> List:
         if self.seed_source is not None:
-            self.seeds = list(self.seed_source.models())
+            ms = self.seed_source.models()
+            # a seed source keeps its Model objects (completion updates them in
+            # place): the list is re-taken only when the source hands out another
+            if ms is not self._seed_list or len(ms) != len(self.seeds):
+                self._seed_list = ms
+                self.seeds = list(ms)
         return self.seeds
 
     def prefetch(self, raws: Sequence[Node]) -> None:
@@ -468,16 +479,14 @@ class ModelCache:
         if not seeds:
             return None
         pre = self._bits.get(key)
-        if pre is None or not all(id(m) in pre[0] for m in seeds):
+        if pre is None or pre[3] is None or pre[3][0] is not seeds:
             pre = self._eval_keys([key], seeds, keep=False).get(key)
         found = None
-        if pre is not None:
-            pos, row = pre[0], pre[1]
-            for m in seeds:
-                p = pos[id(m)]
-                if (int(row[p >> 6]) >> (p & 63)) & 1:
-                    found = m
-                    break
+        if pre is not None and pre[3] is not None:
+            off = pre[3][1]
+            hit = np.unpackbits(pre[1].view(np.uint8), bitorder="little")[off:off + len(seeds)]
+            if hit.any():
+                found = seeds[int(np.argmax(hit))]
         self._seed_memo[key] = found
         return found
 
