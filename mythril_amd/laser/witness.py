@@ -125,7 +125,7 @@ class WitnessSeeds:
                 data += args[m * 3 + j].to_bytes(32, "big")
             if cut[m] and data:
                 data = data[:int(cut_at[m] * len(data))]
-            a[f"{txid}_calldata"] = ArrayInterp(0, dict(enumerate(data)))
+            a[f"{txid}_calldata"] = ArrayInterp(0, dense=bytes(data))
             a[f"{txid}_calldatasize"] = len(data)
             a[f"sender_{txid}"] = actors[m % len(actors)]
             a[f"call_value{txid}"] = int(values[m]) if value_nz[m] else 0
@@ -325,6 +325,19 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
             out = col(node.param)
         elif op == "var":
             out = col([(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns])
+        elif op == "select" and node.args[0].op == "array":
+            # a read of a symbolic array: dense (calldata) interpretations are
+            # read from their bytes, without building the entry dict
+            name, idx, vals = node.args[0].param[0], val(node.args[1]), []
+            for m, a in enumerate(assigns):
+                it = a.get(name)
+                if not isinstance(it, ArrayInterp):
+                    vals.append(0)
+                    continue
+                raw, k = it.untouched_dense(), idx[m]
+                vals.append((raw[k] if k < len(raw) else it.default) if raw is not None
+                            else it.entries.get(k, it.default))
+            out = col(vals)
         elif op == "select":
             ar, idx = arr(node.args[0]), val(node.args[1])
             out = col([ar[m][1].get(idx[m], ar[m][0]) for m in range(n)])

@@ -77,11 +77,26 @@ class ProgramBatch:
 class ArrayInterp:
     """A model's interpretation of a symbolic array: default + entries
     (z3's K(default) + stores / as-array)."""
-    __slots__ = ("default", "entries")
+    __slots__ = ("default", "_entries", "dense")
 
-    def __init__(self, default: int = 0, entries: Optional[Dict[int, int]] = None):
+    def __init__(self, default: int = 0, entries: Optional[Dict[int, int]] = None,
+                 dense: Optional[bytes] = None):
         self.default = default
-        self.entries = dict(entries or {})
+        # dense: entries 0..len-1 as bytes (a witness seed's calldata), turned
+        # into the entry dict only when something reads `entries`
+        self.dense = dense if entries is None else None
+        self._entries = dict(entries) if entries is not None else (None if dense is not None else {})
+
+    @property
+    def entries(self) -> Dict[int, int]:
+        if self._entries is None:
+            self._entries = dict(enumerate(self.dense))
+        return self._entries
+
+    def untouched_dense(self) -> Optional[bytes]:
+        """The dense bytes while no one has taken the entry dict (which may then
+        have been changed), else None."""
+        return self.dense if self._entries is None else None
 
 
 class FuncInterp:
@@ -270,6 +285,12 @@ class PoolColumns:
                 self._dense_cache[arr] = (rev, None)
                 return None
             dflt[m] = interp.default
+            raw = interp.untouched_dense()
+            if raw is not None:
+                ks = slice(0, min(len(raw), self.DENSE_KEYS))
+                keys.append(ks), vals.append(np.frombuffer(raw, dtype=np.uint8)[ks])
+                top = max(top, ks.stop)
+                continue
             ks = [k for k in interp.entries if k < self.DENSE_KEYS]
             vs = [interp.entries[k] for k in ks]
             if vs and max(vs) >> 64:
@@ -280,7 +301,7 @@ class PoolColumns:
                 top = max(top, max(ks) + 1)
         mat = np.repeat(dflt[:, None], top, axis=1)
         for m in range(nm):
-            if keys[m]:
+            if isinstance(keys[m], slice) or keys[m]:
                 mat[m, keys[m]] = vals[m]
         out = (mat, dflt)
         self._dense_cache[arr] = (rev, out)
@@ -305,6 +326,15 @@ class PoolColumns:
         M256_, M512_ = (1 << 256) - 1, (1 << 512) - 1
         for m, a in enumerate(self.assigns):
             interp = a.get(sig.name)
+            raw = interp.untouched_dense() if isinstance(interp, ArrayInterp) else None
+            if raw is not None:
+                # rows (key, 0, byte) of a dense interpretation, in key order (the
+                # entry dict's insertion order when it is taken later)
+                rows = np.zeros((len(raw), 32), dtype="<u4")
+                rows[:, 0] = np.arange(len(raw), dtype=np.uint32)
+                rows[:, 16] = np.frombuffer(raw, dtype=np.uint8)
+                ser[m], done[m], dflt[m] = bytearray(rows.tobytes()), len(raw), interp.default
+                continue
             if isinstance(interp, ArrayInterp):
                 d, ent, arr = interp.default, interp.entries, True
             elif isinstance(interp, FuncInterp):

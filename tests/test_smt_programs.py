@@ -353,3 +353,28 @@ def test_constant_index_selects_are_pool_variables():
     rev[0] += 1
     _, sc2 = eval_batch(prog, cols.pool(prog.var_names, prog.var_widths, prog.tables))
     assert list(sc2) == [3, 2]
+
+
+def test_dense_array_interpretations_read_like_entry_dicts():
+    """A witness seed's calldata is held as bytes (ArrayInterp dense=) until
+    something takes its entry dict: pools built from either form agree."""
+    from mythril_amd.smt.program import PoolColumns
+    cd = Array("3_calldata", 256, 8)
+    sets = [[cd[BVV(k, 256)] == BVV(k + 1, 8)] for k in (0, 2, 5, 70)] + \
+           [[cd[BVS("i", 256)] == BVV(3, 8)]]
+    prog, kept = compile_sets(sets)
+    assert len(kept) == len(sets)
+    data = [bytes([1, 9, 3, 4, 5, 6]), bytes([1, 2, 3]), b"", bytes(range(1, 80))]
+    dense = [{"3_calldata": ArrayInterp(d, dense=x), "i": 2} for d, x in zip((0, 6, 0, 1), data)]
+    plain = [{"3_calldata": ArrayInterp(d, dict(enumerate(x))), "i": 2} for d, x in zip((0, 6, 0, 1), data)]
+    a = PoolColumns(dense).pool(prog.var_names, prog.var_widths, prog.tables)
+    b = PoolColumns(plain).pool(prog.var_names, prog.var_widths, prog.tables)
+    assert (a.values == b.values).all()
+    assert [list(x) for x in eval_batch(prog, a)] == [list(x) for x in eval_batch(prog, b)]
+    want = [sum(evaluate(And(*s).raw, m) for m in plain) for s in sets]
+    assert list(eval_batch(prog, a)[1]) == want
+    assert dense[0]["3_calldata"].untouched_dense() is not None
+    dense[0]["3_calldata"].entries[0] = 7          # taken and changed: the dict is what counts
+    assert dense[0]["3_calldata"].untouched_dense() is None
+    assert PoolColumns(dense).pool(prog.var_names, prog.var_widths).values[prog.var_names.index(
+        "3_calldata\x1f0"), 0, 0] == 7
