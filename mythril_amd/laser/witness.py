@@ -113,47 +113,47 @@ class WitnessSeeds:
         use_sel = r.random(n) < 0.9
         sel = r.integers(0, len(self.selectors), n)
         junk = r.integers(0, 256, (n, 4), dtype=np.uint8)
-        args = self._args(actors, n * 3)
+        argb = self._args(actors, n * 3)
         cut = r.random(n) < 0.05
         cut_at = r.random(n)
         value_nz = r.random(n) >= 0.85
         values = r.integers(1, 1 << 20, n)
         gas = r.integers(0, 1 << 40, n)
+        sel_bytes = [x.to_bytes(4, "big") for x in self.selectors]
+        na = len(actors)
         for m, a in enumerate(self.assign):
-            data = bytearray(self.selectors[int(sel[m])].to_bytes(4, "big") if use_sel[m] else bytes(junk[m]))
-            for j in range(int(nargs[m])):
-                data += args[m * 3 + j].to_bytes(32, "big")
+            data = sel_bytes[int(sel[m])] if use_sel[m] else junk[m].tobytes()
+            k = int(nargs[m])
+            if k:
+                data += argb[m * 3:m * 3 + k].tobytes()
             if cut[m] and data:
                 data = data[:int(cut_at[m] * len(data))]
-            a[f"{txid}_calldata"] = ArrayInterp(0, dense=bytes(data))
+            a[f"{txid}_calldata"] = ArrayInterp(0, dense=data)
             a[f"{txid}_calldatasize"] = len(data)
-            a[f"sender_{txid}"] = actors[m % len(actors)]
+            a[f"sender_{txid}"] = actors[m % na]
             a[f"call_value{txid}"] = int(values[m]) if value_nz[m] else 0
             a[f"gas_price{txid}"] = int(gas[m])
 
-    def _args(self, actors, k: int) -> List[int]:
-        """k argument words: zero, small, an actor, a random address, a random
-        word or all ones."""
+    def _args(self, actors, k: int) -> np.ndarray:
+        """k argument words as (k, 32) big-endian bytes: zero, small, an actor, a
+        random address, a random word or all ones."""
         r = self.rng
         u = r.random(k)
         small = r.integers(0, 1 << 16, k)
         who = r.integers(0, len(actors), k)
         raw = r.integers(0, 256, (k, 32), dtype=np.uint8)
-        out = []
-        for i in range(k):
-            x = u[i]
-            if x < 0.15:
-                out.append(0)
-            elif x < 0.40:
-                out.append(int(small[i]))
-            elif x < 0.60:
-                out.append(actors[int(who[i])])
-            elif x < 0.75:
-                out.append(int.from_bytes(raw[i, :20].tobytes(), "big"))
-            elif x < 0.90:
-                out.append(int.from_bytes(raw[i].tobytes(), "big"))
-            else:
-                out.append(M256)
+        out = np.zeros((k, 32), dtype=np.uint8)
+        sm = (u >= 0.15) & (u < 0.40)
+        out[sm, 30] = (small[sm] >> 8).astype(np.uint8)
+        out[sm, 31] = (small[sm] & 0xFF).astype(np.uint8)
+        ac = (u >= 0.40) & (u < 0.60)
+        table = np.frombuffer(b"".join(x.to_bytes(32, "big") for x in actors), dtype=np.uint8).reshape(-1, 32)
+        out[ac] = table[who[ac]]
+        ad = (u >= 0.60) & (u < 0.75)
+        out[ad, 12:] = raw[ad, :20]
+        wd = (u >= 0.75) & (u < 0.90)
+        out[wd] = raw[wd]
+        out[u >= 0.90] = 0xFF
         return out
 
     def note_query_vars(self, names: Iterable[str]) -> None:
