@@ -497,48 +497,66 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     return MG_OK;
 }
 
-// lane-major host units -> interleaved device units:
-// dst[(u * N + lane) * W + k] = src[(lane * Uh + u) * W + k]  for u < Uh
-__global__ void k_scatter_units(const uint32_t *__restrict__ src, uint32_t n, uint32_t Uh,
-                                uint32_t W, uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t total = (size_t)n * Uh * W;
-    if (i >= total) return;
-    const uint32_t k = i % W;
-    const size_t rest = i / W;
-    const uint32_t u = rest % Uh;
-    const uint32_t lane = (uint32_t)(rest / Uh);
-    dst[((size_t)u * N + first + lane) * W + k] = src[i];
+// ---- lane transfers: stage (lane-major rows) <-> device (unit-major, lanes interleaved)
+// A field of U units x W dwords per lane lives on the device as
+// dst[(u * N + lane) * W + k]; the host stage holds each lane's row contiguously,
+// src[(lane * U + u) * W + k].  One block moves a tile of 64 lanes x 64 dwords
+// (64 / W units) through LDS, so both the row reads and the unit-major writes
+// are contiguous runs (a per-element kernel writes one side at stride N * W).
+// Byte fields (memory, calldata) are W = 1 with each dword byte-swapped: the
+// stage holds bytes, the device big-endian dwords.  W is a power of two <= 64.
+#define XT_LANES 64u
+#define XT_COLS 64u
+template <bool BSWAP>
+__global__ __launch_bounds__(256) void k_xfer_scatter(const uint32_t *__restrict__ src, uint32_t n, uint32_t U,
+                                                     uint32_t lgW, uint32_t *__restrict__ dst, uint32_t N,
+                                                     uint32_t first) {
+    __shared__ uint32_t tile[XT_LANES][XT_COLS + 1];
+    const uint32_t W = 1u << lgW, TU = XT_COLS >> lgW;
+    const uint32_t l0 = blockIdx.x * XT_LANES, u0 = blockIdx.y * TU;
+    const uint32_t nl = min(XT_LANES, n - l0), nu = min(TU, U - u0), cols = nu << lgW;
+    const size_t row = (size_t)U << lgW;
+    for (uint32_t i = threadIdx.x; i < XT_LANES * XT_COLS; i += blockDim.x) {
+        const uint32_t l = i / XT_COLS, c = i % XT_COLS;
+        if (l < nl && c < cols) {
+            uint32_t v = src[(size_t)(l0 + l) * row + ((size_t)u0 << lgW) + c];
+            tile[l][c] = BSWAP ? __builtin_bswap32(v) : v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < XT_LANES * XT_COLS; i += blockDim.x) {
+        const uint32_t uo = i / (XT_LANES * W), rem = i % (XT_LANES * W);
+        const uint32_t l = rem >> lgW, k = rem & (W - 1u);
+        if (uo < nu && l < nl)
+            dst[(((size_t)(u0 + uo) * N + first + l0 + l) << lgW) + k] = tile[l][(uo << lgW) + k];
+    }
 }
-__global__ void k_gather_units(const uint32_t *__restrict__ src, uint32_t n, uint32_t Uh,
-                               uint32_t W, uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t total = (size_t)n * Uh * W;
-    if (i >= total) return;
-    const uint32_t k = i % W;
-    const size_t rest = i / W;
-    const uint32_t u = rest % Uh;
-    const uint32_t lane = (uint32_t)(rest / Uh);
-    dst[i] = src[((size_t)u * N + first + lane) * W + k];
+template <bool BSWAP>
+__global__ __launch_bounds__(256) void k_xfer_gather(const uint32_t *__restrict__ src, uint32_t n, uint32_t U,
+                                                    uint32_t lgW, uint32_t *__restrict__ dst, uint32_t N,
+                                                    uint32_t first) {
+    __shared__ uint32_t tile[XT_LANES][XT_COLS + 1];
+    const uint32_t W = 1u << lgW, TU = XT_COLS >> lgW;
+    const uint32_t l0 = blockIdx.x * XT_LANES, u0 = blockIdx.y * TU;
+    const uint32_t nl = min(XT_LANES, n - l0), nu = min(TU, U - u0), cols = nu << lgW;
+    const size_t row = (size_t)U << lgW;
+    for (uint32_t i = threadIdx.x; i < XT_LANES * XT_COLS; i += blockDim.x) {
+        const uint32_t uo = i / (XT_LANES * W), rem = i % (XT_LANES * W);
+        const uint32_t l = rem >> lgW, k = rem & (W - 1u);
+        if (uo < nu && l < nl) {
+            const uint32_t v = src[(((size_t)(u0 + uo) * N + first + l0 + l) << lgW) + k];
+            tile[l][(uo << lgW) + k] = BSWAP ? __builtin_bswap32(v) : v;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < XT_LANES * XT_COLS; i += blockDim.x) {
+        const uint32_t l = i / XT_COLS, c = i % XT_COLS;
+        if (l < nl && c < cols) dst[(size_t)(l0 + l) * row + ((size_t)u0 << lgW) + c] = tile[l][c];
+    }
 }
-// lane-major bytes -> interleaved big-endian dwords (memory / calldata); Dh dwords per lane
-__global__ void k_scatter_bytes(const uint8_t *__restrict__ src, uint32_t n, uint32_t Dh,
-                                uint32_t *__restrict__ dst, uint32_t N, uint32_t first) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)n * Dh) return;
-    const uint32_t d = i % Dh, lane = (uint32_t)(i / Dh);
-    const uint8_t *p = src + (size_t)lane * Dh * 4 + (size_t)d * 4;
-    dst[(size_t)d * N + first + lane] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
-                                         ((uint32_t)p[2] << 8) | (uint32_t)p[3];
-}
-__global__ void k_gather_bytes(const uint32_t *__restrict__ src, uint32_t n, uint32_t Dh,
-                               uint8_t *__restrict__ dst, uint32_t N, uint32_t first) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)n * Dh) return;
-    const uint32_t d = i % Dh, lane = (uint32_t)(i / Dh);
-    const uint32_t v = src[(size_t)d * N + first + lane];
-    uint8_t *p = dst + (size_t)lane * Dh * 4 + (size_t)d * 4;
-    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+static uint32_t lg2(uint32_t w) { uint32_t r = 0; while ((1u << r) < w) ++r; return r; }
+static dim3 xfer_grid(uint32_t n, uint32_t U, uint32_t W) {
+    return dim3((n + XT_LANES - 1) / XT_LANES, (U + (XT_COLS / W) - 1) / (XT_COLS / W));
 }
 // restore the working state from the resident initial image
 __global__ void k_reset(DevLanes L, DevResetImage R) {
@@ -578,6 +596,7 @@ struct XferPlan {
         size_t off, len;        // in the stage
     };
     std::vector<Item> items;
+    bool bad = false;           // a field the transfer kernels cannot move
     size_t total = 0;
     uint32_t n = 0, first = 0;
     XferPlan(uint32_t n_, uint32_t first_) : n(n_), first(first_) {}
@@ -597,6 +616,8 @@ struct XferPlan {
         add(Item{SCALAR, host, dev, dev2, elem, 0, 0, 0, 0, 0});
     }
     void units(void *host, uint32_t Uh, uint32_t W, void *dev, uint32_t Uc = 0xffffffffu, void *dev2 = nullptr) {
+        // the transpose kernels take W as a power of two up to a tile row
+        if (W == 0 || (W & (W - 1u)) || W > XT_COLS) { bad = true; return; }
         if (Uh) add(Item{UNITS, host, dev, dev2, 0, Uh, W, Uc, 0, 0});
     }
     void bytes(void *host, uint32_t bytes_h, void *dev, uint32_t Dc = 0xffffffffu) {
@@ -631,6 +652,7 @@ static void rows_copy(uint8_t *dst, size_t dst_row, const uint8_t *src, size_t s
 }
 
 static int xfer_down(mg_ctx *ctx, const XferPlan &x) {
+    if (x.bad) return set_err(ctx, MG_EINVAL, "lane transfer: unit width not a power of two <= 64");
     if (x.items.empty()) return MG_OK;
     int rc;
     if ((rc = ensure_stage(ctx, x.total)) || (rc = ensure_hxfer(ctx, x.total))) return rc;
@@ -641,11 +663,12 @@ static int xfer_down(mg_ctx *ctx, const XferPlan &x) {
             HIPX(ctx, hipMemcpyAsync(ds + it.off, (const uint8_t *)it.dev + (size_t)x.first * it.elem, it.len,
                                      hipMemcpyDeviceToDevice, ctx->stream));
         } else if (it.kind == XferPlan::UNITS) {
-            hipLaunchKernelGGL(k_gather_units, dim3(blocks_for((size_t)x.n * it.Uc * it.W)), dim3(256), 0, ctx->stream,
-                               (const uint32_t *)it.dev, x.n, it.Uc, it.W, (uint32_t *)(ds + it.off), N, x.first);
+            hipLaunchKernelGGL(k_xfer_gather<false>, xfer_grid(x.n, it.Uc, it.W), dim3(256), 0, ctx->stream,
+                               (const uint32_t *)it.dev, x.n, it.Uc, lg2(it.W), (uint32_t *)(ds + it.off), N,
+                               x.first);
         } else {
-            hipLaunchKernelGGL(k_gather_bytes, dim3(blocks_for((size_t)x.n * it.Uc)), dim3(256), 0, ctx->stream,
-                               (const uint32_t *)it.dev, x.n, it.Uc, ds + it.off, N, x.first);
+            hipLaunchKernelGGL(k_xfer_gather<true>, xfer_grid(x.n, it.Uc, 1), dim3(256), 0, ctx->stream,
+                               (const uint32_t *)it.dev, x.n, it.Uc, 0u, (uint32_t *)(ds + it.off), N, x.first);
         }
     }
     HIPX(ctx, hipGetLastError());
@@ -665,6 +688,7 @@ static int xfer_down(mg_ctx *ctx, const XferPlan &x) {
 
 // enqueues the upload; the caller synchronises the stream (h_xfer is reused)
 static int xfer_up(mg_ctx *ctx, const XferPlan &x) {
+    if (x.bad) return set_err(ctx, MG_EINVAL, "lane transfer: unit width not a power of two <= 64");
     if (x.items.empty()) return MG_OK;
     int rc;
     if ((rc = ensure_stage(ctx, x.total)) || (rc = ensure_hxfer(ctx, x.total))) return rc;
@@ -687,12 +711,12 @@ static int xfer_up(mg_ctx *ctx, const XferPlan &x) {
                 HIPX(ctx, hipMemcpyAsync((uint8_t *)dev + (size_t)x.first * it.elem, ds + it.off, it.len,
                                          hipMemcpyDeviceToDevice, ctx->stream));
             } else if (it.kind == XferPlan::UNITS) {
-                hipLaunchKernelGGL(k_scatter_units, dim3(blocks_for((size_t)x.n * it.Uc * it.W)), dim3(256), 0,
-                                   ctx->stream, (const uint32_t *)(ds + it.off), x.n, it.Uc, it.W, (uint32_t *)dev,
-                                   N, x.first);
+                hipLaunchKernelGGL(k_xfer_scatter<false>, xfer_grid(x.n, it.Uc, it.W), dim3(256), 0, ctx->stream,
+                                   (const uint32_t *)(ds + it.off), x.n, it.Uc, lg2(it.W), (uint32_t *)dev, N,
+                                   x.first);
             } else {
-                hipLaunchKernelGGL(k_scatter_bytes, dim3(blocks_for((size_t)x.n * it.Uc)), dim3(256), 0, ctx->stream,
-                                   ds + it.off, x.n, it.Uc, (uint32_t *)dev, N, x.first);
+                hipLaunchKernelGGL(k_xfer_scatter<true>, xfer_grid(x.n, it.Uc, 1), dim3(256), 0, ctx->stream,
+                                   (const uint32_t *)(ds + it.off), x.n, it.Uc, 0u, (uint32_t *)dev, N, x.first);
             }
         }
     }

@@ -312,6 +312,25 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
         memo[id(node)] = out
         return out
 
+    def dense_rows(node):
+        """Per model (bytes, default) of an `array` term when every model holds
+        it as untouched dense bytes, else None."""
+        key = ("dense", id(node))
+        if key in memo:
+            return memo[key]
+        rows = None
+        if node.op == "array":
+            rows = []
+            for a in assigns:
+                it = a.get(node.param[0])
+                raw = it.untouched_dense() if isinstance(it, ArrayInterp) else None
+                if raw is None:
+                    rows = None
+                    break
+                rows.append((raw, it.default))
+        memo[key] = rows
+        return rows
+
     def signed(x, w):
         return np.where((x >> (w - 1)) & 1, x - (1 << w), x)
 
@@ -325,19 +344,11 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
             out = col(node.param)
         elif op == "var":
             out = col([(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns])
-        elif op == "select" and node.args[0].op == "array":
-            # a read of a symbolic array: dense (calldata) interpretations are
-            # read from their bytes, without building the entry dict
-            name, idx, vals = node.args[0].param[0], val(node.args[1]), []
-            for m, a in enumerate(assigns):
-                it = a.get(name)
-                if not isinstance(it, ArrayInterp):
-                    vals.append(0)
-                    continue
-                raw, k = it.untouched_dense(), idx[m]
-                vals.append((raw[k] if k < len(raw) else it.default) if raw is not None
-                            else it.entries.get(k, it.default))
-            out = col(vals)
+        elif op == "select" and dense_rows(node.args[0]) is not None:
+            # a read of an array every model holds as dense bytes (the seeds'
+            # calldata): read from the bytes, no entry dicts built
+            rows, idx = dense_rows(node.args[0]), val(node.args[1])
+            out = col([raw[k] if k < len(raw) else d for (raw, d), k in zip(rows, idx)])
         elif op == "select":
             ar, idx = arr(node.args[0]), val(node.args[1])
             out = col([ar[m][1].get(idx[m], ar[m][0]) for m in range(n)])
