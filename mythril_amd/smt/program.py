@@ -234,6 +234,9 @@ class PoolColumns:
         self._vars: Dict[tuple, np.ndarray] = {}
         self._tabs: Dict[tuple, tuple] = {}
         self._dense_cache: Dict[str, tuple] = {}
+        self._mat: Optional[np.ndarray] = None   # rows of the last pool's variables
+        self._mat_keys: List[tuple] = []
+        self._mat_revs: List[object] = []
         # revision(name) -> a value that changes whenever any assignment's
         # interpretation of `name` changes (None: interpretations never change)
         self.revision = revision or (lambda name: 0)
@@ -371,10 +374,29 @@ class PoolColumns:
 
     def pool(self, var_names: List[str], var_widths: List[int], tables: Optional[List] = None) -> ModelPool:
         nm = len(self.assigns)
-        vals = np.zeros((max(len(var_names), 1), max(nm, 1), 8), dtype=np.uint32)
+        nv = len(var_names)
+        # one persistent (variables x models) matrix: a persistent compiler's
+        # variable list only grows, so a launch fills the rows of new variables
+        # and of select variables whose array changed, not every row again
+        if self._mat is None or self._mat.shape[0] < max(nv, 1):
+            grown = np.zeros((max(nv, 1, 2 * (0 if self._mat is None else self._mat.shape[0])), max(nm, 1), 8),
+                             dtype=np.uint32)
+            if self._mat is not None:
+                grown[:self._mat.shape[0]] = self._mat
+            self._mat = grown
+        keys, revs = self._mat_keys, self._mat_revs
         for v, (name, w) in enumerate(zip(var_names, var_widths)):
-            vals[v, :nm] = self._var(name, w)
-        out = ModelPool(vals)
+            arr = name.partition("\x1f")[0] if "\x1f" in name else None
+            rev = self.revision(arr) if arr is not None else 0
+            if v < len(keys) and keys[v] == (name, w) and revs[v] == rev:
+                continue
+            self._mat[v, :nm] = self._var(name, w)
+            if v < len(keys):
+                keys[v], revs[v] = (name, w), rev
+            else:
+                keys.append((name, w))
+                revs.append(rev)
+        out = ModelPool(self._mat[:max(nv, 1)])
         if tables:
             parts = [self._tab(sig) for sig in tables]
             starts, counts, defaults, ents, off = [], [], [], [], 0
