@@ -93,8 +93,15 @@ def run_both(device, name, monkeypatch):
         except symref.Unsupported:
             handler_engine.ended.append(("unsupported", state))
             return []
+    escaped = Counter()
+
+    def counting_handler(state):
+        ins = state.environment.code.instruction_list
+        escaped.update([ins[state.mstate.pc]["opcode"] if state.mstate.pc < len(ins) else "END"])
+        return handler(state)
     laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
-                     escape_handler=handler)
+                     escape_handler=counting_handler)
+    laser.escaped_ops = escaped
     got = Counter()
     laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
         [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
