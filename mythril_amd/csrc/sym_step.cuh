@@ -539,7 +539,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         // the code's size + 0x200 with `calldata.size == it` appended to the path
         // (MG_REC_CDSIZE, replayed by the host in execution order), and CODECOPY from
         // at or past the end of the code is that calldata copy at code_offset minus
-        // the code's size.  Symbolic offsets or sizes stay with the host.
+        // the code's size.  A message call's CALLDATACOPY with a symbolic memory offset
+        // copies nothing and one with a symbolic size copies 320 bytes, as the
+        // reference does; a symbolic calldata offset stays with the host.
         if (symlane && (flags & LANE_SYMCD) && !tl && sp >= max(req, npop) &&
             (op == 0x37u || (creation && op == 0x38u) ||
              (creation && op == 0x39u && !sym_tag(S, N, lane, sp - 2u) &&
@@ -568,9 +570,18 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
                     break;
                 }
-                const uint32_t ta = sym_tag(S, N, lane, sp - 1u), tb = sym_tag(S, N, lane, sp - 2u),
-                               tc = sym_tag(S, N, lane, sp - 3u);
-                const U256 a = V.stack(sp - 1u), b = V.stack(sp - 2u), c = V.stack(sp - 3u);
+                const uint32_t ta = sym_tag(S, N, lane, sp - 1u), tb = sym_tag(S, N, lane, sp - 2u);
+                uint32_t tc = sym_tag(S, N, lane, sp - 3u);
+                U256 a = V.stack(sp - 1u), b = V.stack(sp - 2u), c = V.stack(sp - 3u);
+                if (op == 0x37u && ta) {
+                    // a symbolic memory offset: the copy is dropped (instructions.py:810-814)
+                    ngmin += gtmin; ngmax += gtmax;
+                    if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
+                    break;
+                }
+                // a symbolic size copies SYMBOLIC_CALLDATA_SIZE bytes (instructions.py:822-826,
+                // call.py:33); a symbolic calldata offset stays with the host
+                if (op == 0x37u && tc && !tb) { c = u_small(320u); tc = 0u; }
                 if (ta || tb || tc) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                 if (u_iszero(c)) {                                   // size 0: nothing but the gas
                     ngmin += gtmin; ngmax += gtmax;

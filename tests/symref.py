@@ -599,11 +599,16 @@ class Engine:
             dst, src, size = st[-1], st[-2], st[-3]
             if op == 0x39 and _val(src) is not None and _val(src) < code_len:
                 return None
-            if any(_val(x) is None for x in (dst, src, size)):
+            skip = False
+            if op == 0x37 and not creation and _val(dst) is None:
+                skip = True                          # instructions.py:810-814: nothing copied
+            elif op == 0x37 and not creation and _val(src) is not None and _val(size) is None:
+                size = BVV(320, 256)                 # SYMBOLIC_CALLDATA_SIZE (instructions.py:822-826)
+            if not skip and not (creation and op == 0x37) and any(_val(x) is None for x in (dst, src, size)):
                 raise Unsupported("symbolic calldata copy operand")
             del st[-3:]
             dst, src, size = _val(dst), _val(src), _val(size)
-            if not (creation and op == 0x37) and size > 0:
+            if not skip and not (creation and op == 0x37) and size > 0:
                 if op == 0x39:
                     src -= code_len
                 if src + size >= 1 << 32:

@@ -131,11 +131,23 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
         assert sym_sha3 > 0 and halts_past_sha3 > 0, (sym_sha3, halts_past_sha3)
 
 
+# what a symbolic lane still hands to the host: the call family and SELFDESTRUCT
+# (the reference's world-state transitions), a symbolic jump target, the
+# symbolic balance array's reads, and what follows a call that returned symbolic
+# data (RETURNDATASIZE / RETURNDATACOPY of it, RETURN / REVERT of a symbolic
+# length, which names fresh return-data variables, instructions.py:1858-1930)
+HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT",
+            "JUMP", "JUMPI", "BALANCE", "SELFBALANCE", "RETURNDATASIZE", "RETURNDATACOPY", "RETURN", "REVERT"}
+
+
 @pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
 def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
     assert laser.forks >= 3 and laser.lane_steps > 100
+    # symbolic memory offsets and copy sizes run on the device (CALLDATACOPY of a
+    # symbolic size or memory offset included): nothing else escapes
+    assert set(laser.escaped_ops) <= HOST_OPS, dict(laser.escaped_ops)
 
 
 @pytest.mark.parametrize("name", symcases.SYM_CREATIONS)
