@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 11u  /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 12u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -42,7 +42,9 @@ extern "C" {
                                   symbolic EXP (MG_SYM_BIN 0x0a, MG_REC_SYMEXP)
                               10: MG_LANE_RETDATA (a host CALL left return data:
                                   RETURNDATASIZE / RETURNDATACOPY escape)
-                              11: mg_cc_* (native conjunct compiler for kernel 2) */
+                              11: mg_cc_* (native conjunct compiler for kernel 2)
+                              12: CALLDATACOPY of a symbolic size / memory offset /
+                                  calldata offset on symbolic lanes (MG_SYM_CDBYTEX) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -265,6 +267,9 @@ typedef struct mg_ctx mg_ctx;
 #define MG_SYM_CDBYTE 12u /* calldata[w]: one 8-bit byte of the calldata, If(w < size,
                              calldata_array[w], 0) (state/calldata.py:253-262), as
                              _calldata_copy_helper writes it (instructions.py:807-875) */
+#define MG_SYM_CDBYTEX 13u /* calldata[simplify(y + w)]: byte w of a CALLDATACOPY from a
+                              symbolic calldata offset y (instructions.py:816-860; a
+                              symbolic size copies 320 bytes, call.py:33)           */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */

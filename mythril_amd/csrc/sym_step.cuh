@@ -81,6 +81,7 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define SYM_TERM 10u
 #define SYM_NONE 0xffffffffu
 #define SYM_CDBYTE 12u
+#define SYM_CDBYTEX 13u
 
 DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
 DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
@@ -580,9 +581,10 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     break;
                 }
                 // a symbolic size copies SYMBOLIC_CALLDATA_SIZE bytes (instructions.py:822-826,
-                // call.py:33); a symbolic calldata offset stays with the host
-                if (op == 0x37u && tc && !tb) { c = u_small(320u); tc = 0u; }
-                if (ta || tb || tc) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                // call.py:33); a symbolic calldata offset y makes byte k calldata[y + k]
+                const bool symsrc = op == 0x37u && tb != 0u;
+                if (op == 0x37u && tc) { c = u_small(320u); tc = 0u; }
+                if (ta || (tb && !symsrc) || tc) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                 if (u_iszero(c)) {                                   // size 0: nothing but the gas
                     ngmin += gtmin; ngmax += gtmax;
                     if (ngmin >= glim) CSTOPX(ST_VMEXC, EXC_OOG)
@@ -596,12 +598,14 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                 // the source index of every byte must stay below 2^32 on the device
                 const uint32_t src = op == 0x39u ? b.w[0] - C.n_bytes : b.w[0];
                 const uint32_t size = c.w[0], mst = a.w[0];
-                if (!u_fits32(b) || (uint64_t)src + size > 0xffffffffull) CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                if (!symsrc && (!u_fits32(b) || (uint64_t)src + size > 0xffffffffull))
+                    CSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                 if ((uint64_t)lnn + size > S.node_cap) CSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
                 if (nmsize > msize) V.mzero(msize, nmsize);
                 for (uint32_t k = 0; k < size; ++k) {
                     uint32_t tg;
-                    sym_node_push(S, N, lane, SYM_CDBYTE | (8u << 8), 0u, 0u, src + k, lnn, tg);
+                    if (symsrc) sym_node_push(S, N, lane, SYM_CDBYTEX | (8u << 8), tb - 1u, 0u, k, lnn, tg);
+                    else sym_node_push(S, N, lane, SYM_CDBYTE | (8u << 8), 0u, 0u, src + k, lnn, tg);
                     V.set_mbyte(mst + k, 0u);
                     set_mtag(S, N, lane, mst + k, 1u + (((tg - 1u) << 5) | 31u));
                 }

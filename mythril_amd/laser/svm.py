@@ -689,6 +689,8 @@ class LaserEVM:
                 sflags = le.flags
             else:
                 le = None
+        # the terms behind the lane's first arena nodes, for _materialise's decode
+        s._arena_prefix = le.enc.node_raw if le is not None else None
         if le is None:
             stack = [concrete(x) for x in ms.stack]
             if stack:
@@ -750,7 +752,7 @@ class LaserEVM:
         sp = int(b.sp[i])
         symlane = b.symbolic and int(b.flags[i]) & MG_LANE_SYMBOLIC
         if symlane:
-            stack, memory, storage = sym.decode_lane(b, i, s)
+            stack, memory, storage = sym.decode_lane(b, i, s, getattr(s, "_arena_prefix", None))
             ms.stack = MachineStack(stack)
         elif b.taint and int(b.flags[i]) & MG_LANE_TAINT:
             ms.stack = MachineStack([symbol_factory.BitVecVal(w, 256) for w in rows_to_words(b.stack[i, :sp])])

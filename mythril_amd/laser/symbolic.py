@@ -36,7 +36,7 @@ import numpy as np
 from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_CALLVALUE as MG_ENV_CALLVALUE, ENV_GASPRICE as MG_ENV_GASPRICE,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
-                     MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDLOAD,
+                     MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
                      MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
@@ -188,10 +188,14 @@ class _Decoder:
     """The expressions of one lane's planes: its stack words, memory bytes and
     storage chain (the arena is shared by all three, nodes memoised)."""
 
-    def __init__(self, b, i: int, state):
+    def __init__(self, b, i: int, state, prefix: Optional[list] = None):
         self.b, self.i, self.state = b, i, state
         self.n_nodes = int(b.n_nodes[i])
         self.memo: List[Optional[object]] = [None] * self.n_nodes
+        # the terms of the nodes the host encoded into this lane (the arena only
+        # grows on the device): node k < len(prefix) decodes to prefix[k] with no
+        # rebuild of its expression
+        self.prefix = prefix if prefix is not None and len(prefix) <= self.n_nodes else None
         self._entries = None
         self._raws = None
 
@@ -220,7 +224,14 @@ class _Decoder:
             raise ValueError(f"lane {self.i}: arena reference {k} past its {self.n_nodes} nodes")
         e = self.memo[k]
         if e is None:
-            e = self.memo[k] = self._build(k)
+            pre = self.prefix
+            if pre is not None and k < len(pre):
+                raw = pre[k]
+                kind = int(self.b.node[self.i, k, 0]) & 0xFF
+                e = Bool(raw) if kind == MG_SYM_TERM and raw.width == 1 and _is_bool_op(raw) else BitVec(raw)
+                self.memo[k] = e
+            else:
+                e = self.memo[k] = self._build(k)
         return e
 
     def _build(self, k: int):
@@ -240,6 +251,11 @@ class _Decoder:
         if kind == MG_SYM_CDBYTE:
             # the byte _calldata_copy_helper writes: calldata[index] (instructions.py:850-860)
             return _mark(self.state.environment.calldata[w], kind, w, (), 8)
+        if kind == MG_SYM_CDBYTEX:
+            # a copy from a symbolic calldata offset: calldata[simplify(offset + w)]
+            # (instructions.py:816-820, 847-858)
+            base = self.ref(y)
+            return _mark(self.state.environment.calldata[cd_index(base, w)], kind, w, (base,), 8)
         if kind == MG_SYM_SLOAD:
             # Storage.__getitem__: simplify(Select(chain after z stores, index))
             return BitVec(_select(self.chain_raw(z), self.ref(y).raw))
@@ -309,6 +325,16 @@ class _Decoder:
         return Storage.from_chain(not symstore, acct.address, self.entries())
 
 
+def cd_index(base, k: int) -> BitVec:
+    """The calldata index _calldata_copy_helper reads byte k of a copy from a
+    symbolic offset at: simplify(offset) then simplify(i + 1) per byte
+    (instructions.py:816-820, 854-858) -- z3 folds the additions' constants
+    into one (state.memory_key)."""
+    from .state import memory_key
+    raw = base.raw if k == 0 else (base + symbol_factory.BitVecVal(k, 256)).raw
+    return BitVec(memory_key(raw))
+
+
 def keccak_of(data):
     """KeccakFunctionManager.create_keccak's value for `data` without its
     registration: the concrete hash, or keccak256_<bits>(data)."""
@@ -332,9 +358,10 @@ def decode_stack(b, i: int, state, dec: Optional[_Decoder] = None) -> list:
     return out
 
 
-def decode_lane(b, i: int, state):
-    """(stack, memory, storage) of a symbolic lane."""
-    dec = _Decoder(b, i, state)
+def decode_lane(b, i: int, state, prefix: Optional[list] = None):
+    """(stack, memory, storage) of a symbolic lane; `prefix`: the terms of the
+    nodes its state was encoded with (LaneEncoding.enc.node_raw)."""
+    dec = _Decoder(b, i, state, prefix)
     return decode_stack(b, i, state, dec), dec.memory(), dec.storage()
 
 
@@ -380,6 +407,7 @@ class _Encoder:
         self._cref: dict = {}
         self._nref: dict = {}             # raw -> node index
         self.raws: list = []              # this lane's chain prefixes (encode_storage)
+        self.node_raw: list = []          # node index -> the term it encodes
 
     def cref(self, v: int) -> int:
         r = self._cref.get(v)
@@ -394,6 +422,7 @@ class _Encoder:
         if len(self.nodes) >= self.node_cap:
             raise NotEncodable("arena full")
         self.nodes.append((x, y, z, w))
+        self.node_raw.append(raw)
         self._nref[raw] = len(self.nodes) - 1
         return len(self.nodes) - 1
 

@@ -45,7 +45,7 @@ from mythril_amd.lanes import (LaneBatch, LaneShape, MG_HALT_DROPPED, MG_HALT_EN
                                word_to_limbs)
 from mythril_amd.laser.opcodes import ADDRESS_OPCODE_MAPPING
 from mythril_amd.laser.state import (Account, Memory, MachineStack, OutOfGasException, VmException,
-                                    WriteProtection)
+                                    WriteProtection, memory_key)
 from mythril_amd.laser.transaction import ContractCreationTransaction
 from mythril_amd.smt.expr import (UGE, BitVec, Bool, Concat, Extract, If, LShR, Not, SRem, UDiv, UGT, ULT,
                                   URem, simplify_concat, symbol_factory)
@@ -599,26 +599,41 @@ class Engine:
             dst, src, size = st[-1], st[-2], st[-3]
             if op == 0x39 and _val(src) is not None and _val(src) < code_len:
                 return None
-            skip = False
-            if op == 0x37 and not creation and _val(dst) is None:
-                skip = True                          # instructions.py:810-814: nothing copied
-            elif op == 0x37 and not creation and _val(src) is not None and _val(size) is None:
-                size = BVV(320, 256)                 # SYMBOLIC_CALLDATA_SIZE (instructions.py:822-826)
-            if not skip and not (creation and op == 0x37) and any(_val(x) is None for x in (dst, src, size)):
+            skip = symsrc = False
+            if op == 0x37 and not creation:
+                # _calldata_copy_helper (instructions.py:807-860): a symbolic memory
+                # offset copies nothing; a symbolic calldata offset reads
+                # calldata[simplify(offset + k)]; a symbolic size copies
+                # SYMBOLIC_CALLDATA_SIZE = 320 bytes
+                if _val(dst) is None:
+                    skip = True
+                else:
+                    symsrc = _val(src) is None
+                    if _val(size) is None:
+                        size = BVV(320, 256)
+            if not skip and not symsrc and not (creation and op == 0x37) and \
+                    any(_val(x) is None for x in (dst, src, size)):
                 raise Unsupported("symbolic calldata copy operand")
             del st[-3:]
+            base = src
             dst, src, size = _val(dst), _val(src), _val(size)
             if not skip and not (creation and op == 0x37) and size > 0:
                 if op == 0x39:
                     src -= code_len
-                if src + size >= 1 << 32:
+                if not symsrc and src + size >= 1 << 32:
                     raise Unsupported("calldata index past 2^32")
                 try:
                     ms.mem_extend(BVV(dst, 256), BVV(size, 256))
                 except OutOfGasException:
                     return self._vmexc(state)
-                for k in range(size):
-                    ms.memory[dst + k] = env.calldata[src + k]
+                if symsrc:
+                    idx = BitVec(memory_key(base.raw))            # simplify(dstart)
+                    for k in range(size):
+                        ms.memory[dst + k] = env.calldata[idx]
+                        idx = BitVec(memory_key((idx + BVV(1, 256)).raw))     # simplify(i_data + 1)
+                else:
+                    for k in range(size):
+                        ms.memory[dst + k] = env.calldata[src + k]
         if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
             return self._vmexc(state)
         ms.pc += 1

@@ -264,6 +264,15 @@ def test_lane_encoding_of_memory_and_storage_round_trips():
     assert [(a.raw, c.raw) for a, c in storage.chain()] == \
         [(a.raw, c.raw) for a, c in s.environment.active_account.storage.chain()]
     assert storage.chain_raw() is s.environment.active_account.storage.chain_raw()
+    # decoding with the encoder's terms as the arena prefix (what _materialise does
+    # for a lane it packed) gives every node the same term and type as rebuilding it
+    full, pre = sym._Decoder(b, 0, s), sym._Decoder(b, 0, s, le.enc.node_raw)
+    for k in range(int(b.n_nodes[0])):
+        x, y = full.node(k), pre.node(k)
+        assert x.raw is y.raw and type(x) is type(y), k
+    st2, mem2, sto2 = sym.decode_lane(b, 0, s, le.enc.node_raw)
+    assert [(type(w), w.raw) for w in st2] == [(type(w), w.raw) for w in stack]
+    assert [(a.raw, c.raw) for a, c in sto2.chain()] == [(a.raw, c.raw) for a, c in storage.chain()]
 
 
 def test_device_memory_parts_decode_to_the_reference_word():
@@ -291,3 +300,39 @@ def test_device_memory_parts_decode_to_the_reference_word():
     assert word.raw is mem.get_word_at(16).raw
     from mythril_amd.smt.keccak_manager import KeccakFunctionManager
     assert h.raw is KeccakFunctionManager().create_keccak(mem.get_word_at(16)).raw
+
+
+def test_restated_symbolic_calldata_copy_follows_the_reference():
+    """_calldata_copy_helper (instructions.py:807-860) with a symbolic size and a
+    symbolic calldata offset: 320 bytes (SYMBOLIC_CALLDATA_SIZE), byte k =
+    calldata[simplify(offset + k)]; the arena's MG_SYM_CDBYTEX nodes decode to
+    the same bytes.  A symbolic memory offset copies nothing."""
+    from mythril_amd.lanes import MG_SYM_CDBYTEX, MG_SYM_CDLOAD
+    # CALLDATASIZE | PUSH1 4 CALLDATALOAD | PUSH1 0x80 CALLDATACOPY | STOP
+    s = _run_restatement("36" "600435" "608037" "00", 5)
+    cd = s.environment.calldata
+    x = cd.get_word_at(BVV(4, 256))
+    mem = s.mstate.memory
+    assert len(mem) == (0x80 + 320 + 31) // 32 * 32 and len(s.mstate.stack) == 0
+    got = mem.symbolic_bytes()
+    assert sorted(got) == list(range(0x80, 0x80 + 320))
+    for k in (0, 1, 2, 31, 319):
+        assert got[0x80 + k].raw is cd[sym.cd_index(x, k)].raw
+    assert sym.cd_index(x, 2).raw is sym.cd_index(sym.cd_index(x, 1), 1).raw
+    # the device's form: CDLOAD(4) then 320 CDBYTEX nodes on it
+    b = _batch()
+    b.node[0, 0] = (MG_SYM_CDLOAD | 256 << 8, MG_SYM_CONST | 0, 0, 0)
+    b.cval[0, 0] = word_to_limbs(4)
+    for k in range(3):
+        b.node[0, 1 + k] = (MG_SYM_CDBYTEX | 8 << 8, 0, 0, k)
+    b.n_nodes[0], b.n_consts[0] = 4, 1
+    dec = sym._Decoder(b, 0, s)
+    for k in range(3):
+        assert dec.node(1 + k).raw is got[0x80 + k].raw
+    # re-encoding a byte replays its provenance: node (CDBYTEX, offset node, k)
+    enc = sym._Encoder()
+    t = enc.byte(dec.node(3))
+    assert enc.nodes[(t - 1) >> 5][0] & 0xFF == MG_SYM_CDBYTEX and enc.nodes[(t - 1) >> 5][3] == 2
+    # a symbolic memory offset: the copy is dropped, the operands popped
+    s2 = _run_restatement("6020" "6000" "600035" "37" "00", 5)     # PUSH1 32 PUSH1 0 (PUSH1 0 CALLDATALOAD) CALLDATACOPY
+    assert len(s2.mstate.stack) == 0 and len(s2.mstate.memory) == 0
