@@ -27,6 +27,7 @@ stopped with MG_FORK exactly as instructions.py:1558-1636 does.
 """
 from __future__ import annotations
 
+import bisect
 import weakref
 from copy import copy, deepcopy
 from typing import List, Optional, Tuple
@@ -704,9 +705,14 @@ def _pop2(s):
     st.pop()
 
 
+_ADDRS: dict = {}        # id(instruction list) -> (the list, its addresses)
+
+
 def _instruction_index(instrs, address: int) -> Optional[int]:
-    """util.get_instruction_index (util.py:45-59): first index at or past address."""
-    for k, ins in enumerate(instrs):
-        if ins["address"] >= address:
-            return k
-    return None
+    """util.get_instruction_index (util.py:45-59): first index at or past address
+    (a bisection over the list's addresses, which increase)."""
+    got = _ADDRS.get(id(instrs))
+    if got is None or got[0] is not instrs or len(got[1]) != len(instrs):
+        got = _ADDRS[id(instrs)] = (instrs, [ins["address"] for ins in instrs])
+    k = bisect.bisect_left(got[1], address)
+    return k if k < len(instrs) else None
