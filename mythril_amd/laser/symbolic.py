@@ -197,8 +197,15 @@ class _Decoder:
         # grows on the device): node k < len(prefix) decodes to prefix[k] with no
         # rebuild of its expression
         self.prefix = prefix if prefix is not None and len(prefix) <= self.n_nodes else None
+        self._rows = None
         self._entries = None
         self._raws = None
+
+    def row(self, k: int):
+        """Node k's (x, y, z, w) as ints (the lane's node rows read once)."""
+        if self._rows is None:
+            self._rows = self.b.node[self.i, :self.n_nodes].tolist()
+        return self._rows[k]
 
     # -- operands
     def const(self, r: int, width: int = 256):
@@ -212,10 +219,9 @@ class _Decoder:
         """The memory parts an operand of a CONCAT / KECCAK stands for."""
         if r & MG_SYM_CONST:
             return [self.const(r, width)]
-        x = int(self.b.node[self.i, r, 0])
+        x, y, z, w = self.row(r)
         kind = x & 0xFF
         if kind == MG_SYM_CONCAT:
-            _, y, z, w = (int(v) for v in self.b.node[self.i, r])
             return self.parts(y, w & 0xFFFF) + self.parts(z, w >> 16)
         return [self.node(r)]
 
@@ -228,7 +234,7 @@ class _Decoder:
             pre = self.prefix
             if pre is not None and k < len(pre):
                 raw = pre[k]
-                kind = int(self.b.node[self.i, k, 0]) & 0xFF
+                kind = self.row(k)[0] & 0xFF
                 e = Bool(raw) if kind == MG_SYM_TERM and raw.width == 1 and _is_bool_op(raw) else BitVec(raw)
                 self.memo[k] = e
             else:
@@ -236,7 +242,7 @@ class _Decoder:
         return e
 
     def _build(self, k: int):
-        x, y, z, w = (int(v) for v in self.b.node[self.i, k])
+        x, y, z, w = self.row(k)
         kind = x & 0xFF
         if kind == MG_SYM_BIN:
             a, c = self.ref(y), self.ref(z)
@@ -352,11 +358,10 @@ def decode_stack(b, i: int, state, dec: Optional[_Decoder] = None) -> list:
     words, the node's expression for symbolic ones."""
     dec = dec or _Decoder(b, i, state)
     sp = int(b.sp[i])
-    out = []
-    for s in range(sp):
-        t = int(b.stag[i, s])
-        out.append(dec.node(t - 1) if t else symbol_factory.BitVecVal(limbs_to_word(b.stack[i, s]), 256))
-    return out
+    tags = b.stag[i, :sp].tolist()
+    raw = b.stack[i, :sp].astype("<u4", copy=False).tobytes()
+    return [dec.node(t - 1) if t else symbol_factory.BitVecVal(int.from_bytes(raw[32 * s:32 * s + 32], "little"), 256)
+            for s, t in enumerate(tags)]
 
 
 def decode_lane(b, i: int, state, prefix: Optional[list] = None):
