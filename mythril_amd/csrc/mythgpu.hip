@@ -858,12 +858,14 @@ extern "C" int mg_sym_upload(mg_ctx *ctx, const mg_sym_soa *h, uint32_t first, u
     for (uint32_t i = 0; i < n; ++i)
         if (h->n_nodes[i] > h->node_cap || h->n_consts[i] > h->const_cap)
             return set_err(ctx, MG_EINVAL, "lane %u: arena exceeds its host capacities", first + i);
+    // the arena only grows from each lane's node / constant count and no step reads a
+    // row past it: rows up to the range's largest count cross PCIe, not the capacity
     XferPlan x(n, first);
     x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
     x.scalar(h->n_consts, ctx->S.n_consts, 4);
     x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
-    x.units(h->node, h->node_cap, 4, ctx->S.node);
-    x.units(h->cval, h->const_cap, 8, ctx->S.cval);
+    x.units(h->node, h->node_cap, 4, ctx->S.node, max_of(h->n_nodes, n));
+    x.units(h->cval, h->const_cap, 8, ctx->S.cval, max_of(h->n_consts, n));
     x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
     x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
     if ((rc = xfer_up(ctx, x))) return rc;
@@ -876,15 +878,18 @@ extern "C" int mg_sym_download(mg_ctx *ctx, mg_sym_soa *h, uint32_t first, uint3
     int rc;
     if ((rc = check_sym_shape(ctx, h, first, n))) return rc;
     HIPX(ctx, hipSetDevice(ctx->device));
+    // phase 1: the counts (they bound phase 2's arena rows)
     XferPlan x(n, first);
     x.scalar(h->n_nodes, ctx->S.n_nodes, 4);
     x.scalar(h->n_consts, ctx->S.n_consts, 4);
-    x.units(h->stag, h->stack_cap, 1, ctx->S.stag);
-    x.units(h->node, h->node_cap, 4, ctx->S.node);
-    x.units(h->cval, h->const_cap, 8, ctx->S.cval);
-    x.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
-    x.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
-    return xfer_down(ctx, x);
+    if ((rc = xfer_down(ctx, x))) return rc;
+    XferPlan y(n, first);
+    y.units(h->stag, h->stack_cap, 1, ctx->S.stag);
+    y.units(h->node, h->node_cap, 4, ctx->S.node, max_of(h->n_nodes, n));
+    y.units(h->cval, h->const_cap, 8, ctx->S.cval, max_of(h->n_consts, n));
+    y.units(h->mtag, h->mem_cap, 1, ctx->S.mtag);
+    y.units(h->sttag, h->storage_cap, 2, ctx->S.sttag);
+    return xfer_down(ctx, y);
 }
 
 // ---- taint planes ------------------------------------------------------------
