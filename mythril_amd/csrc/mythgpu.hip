@@ -785,19 +785,23 @@ static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint3
     x.scalar(h->gas_min, L.gas_min, 8, ctx->i_gas_min);
     x.scalar(h->gas_max, L.gas_max, 8, ctx->i_gas_max);
     x.scalar(h->gas_limit, L.gas_limit, 8);
-    x.units(h->stack, h->stack_cap, 8, L.stack, live ? max_of(h->sp, n) : ALL);
+    // rows below the range's largest sp / storage count / msize / trace and record
+    // length: no step reads above them before writing (pushes write their slot,
+    // stores and logs append, memory is zero-filled when it extends), so the rest
+    // of each capacity never crosses PCIe (`live` only leaves out env and calldata)
+    (void)ALL;
+    x.units(h->stack, h->stack_cap, 8, L.stack, max_of(h->sp, n));
     x.units(h->env, MG_ENV_WORDS, 8, L.env);
-    x.units(h->storage, h->storage_cap, 16, L.storage, live ? max_of(h->storage_count, n) : ALL,
-            ctx->i_storage);
-    x.bytes(h->memory, h->mem_cap, L.mem, live ? (max_of(h->msize, n) + 3u) / 4u : ALL);
+    x.units(h->storage, h->storage_cap, 16, L.storage, max_of(h->storage_count, n), ctx->i_storage);
+    x.bytes(h->memory, h->mem_cap, L.mem, (max_of(h->msize, n) + 3u) / 4u);
     x.bytes(h->calldata, h->calldata_cap, L.calldata);
     if (h->trace_cap) {
         x.scalar(h->trace_len, L.trace_len, 4);
-        x.units(h->trace, h->trace_cap, 1, L.trace, live ? max_of(h->trace_len, n) : ALL);
+        x.units(h->trace, h->trace_cap, 1, L.trace, max_of(h->trace_len, n));
     }
     if (h->rec_cap) {
         x.scalar(h->rec_len, L.rec_len, 4);
-        x.units(h->rec, h->rec_cap, 1, L.rec, live ? max_of(h->rec_len, n) : ALL);
+        x.units(h->rec, h->rec_cap, 1, L.rec, max_of(h->rec_len, n));
     }
     HIPX(ctx, hipMemsetAsync(L.sha3_count + first, 0, (size_t)n * 4, ctx->stream));
     HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
@@ -1008,7 +1012,7 @@ extern "C" int mg_taint_upload(mg_ctx *ctx, const mg_taint_soa *h, uint32_t firs
     x.scalar(h->sink, T.sink, 8);
     x.scalar(h->ymask, T.ymask, 8);
     x.units(h->sobj, h->stack_cap, 1, T.sobj);
-    x.units(h->omask, h->obj_cap, 2, T.omask);
+    x.units(h->omask, h->obj_cap, 2, T.omask, max_of(h->n_obj, n));    // objects past n_obj are unread
     if ((rc = xfer_up(ctx, x))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     return MG_OK;
@@ -1027,9 +1031,11 @@ extern "C" int mg_taint_download(mg_ctx *ctx, mg_taint_soa *h, uint32_t first, u
     x.scalar(h->tflags, T.tflags, 4);
     x.scalar(h->sink, T.sink, 8);
     x.scalar(h->ymask, T.ymask, 8);
-    x.units(h->sobj, h->stack_cap, 1, T.sobj);
-    x.units(h->omask, h->obj_cap, 2, T.omask);
-    return xfer_down(ctx, x);
+    if ((rc = xfer_down(ctx, x))) return rc;
+    XferPlan y(n, first);
+    y.units(h->sobj, h->stack_cap, 1, T.sobj);
+    y.units(h->omask, h->obj_cap, 2, T.omask, max_of(h->n_obj, n));
+    return xfer_down(ctx, y);
 }
 
 
