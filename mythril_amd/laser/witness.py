@@ -331,6 +331,46 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
         memo[key] = rows
         return rows
 
+    def cd_word(node):
+        """A calldata word (SymbolicCalldata.get_word_at, marked MG_SYM_CDLOAD):
+        byte k = If(off + k < size, calldata[off + k], 0) (calldata.py:253-262),
+        read straight from each model's calldata bytes -- the 32 ite / select /
+        compare columns it would otherwise take.  None when the term is not of
+        that shape or a model does not hold the array as bytes."""
+        from .symbolic import _PROV, MG_SYM_CDLOAD
+        prov = _PROV.get(node)
+        if prov is None or prov[0] != MG_SYM_CDLOAD or node.width != 256:
+            return None
+        first = node
+        while first.op == "concat":
+            first = first.args[0]
+        if first.op != "ite" or first.args[1].op != "select" or first.args[0].op != "bvslt":
+            return None
+        sel, cond = first.args[1], first.args[0]
+        off = prov[2][0].raw
+        if sel.args[1] is not off or cond.args[0] is not off or sel.args[0].op != "array":
+            return None
+        rows = dense_rows(sel.args[0])
+        if rows is None:
+            return None
+        offs, sizes = val(off), val(cond.args[1])
+        H, M256 = 1 << 255, (1 << 256) - 1
+        out = []
+        for (raw, d), o, sz in zip(rows, offs, sizes):
+            n_raw = len(raw)
+            if o + 32 <= n_raw and o + 31 < sz < H:
+                out.append(int.from_bytes(raw[o:o + 32], "big"))
+                continue
+            ssz = sz - (1 << 256) if sz >= H else sz
+            word = 0
+            for k in range(32):
+                idx = (o + k) & M256
+                sidx = idx - (1 << 256) if idx >= H else idx
+                byte = (raw[idx] if idx < n_raw else d) if sidx < ssz else 0
+                word = (word << 8) | byte
+            out.append(word)
+        return col(out)
+
     def signed(x, w):
         return np.where((x >> (w - 1)) & 1, x - (1 << w), x)
 
@@ -340,7 +380,9 @@ def eval_all(raw: Node, assigns: List[Dict[str, object]]) -> List[int]:
             return got
         op, w = node.op, node.width
         M = (1 << w) - 1 if w else 0
-        if op == "const":
+        if op == "concat" and (out := cd_word(node)) is not None:
+            pass
+        elif op == "const":
             out = col(node.param)
         elif op == "var":
             out = col([(a.get(node.param, 0) if isinstance(a.get(node.param, 0), int) else 0) for a in assigns])

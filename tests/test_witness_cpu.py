@@ -39,3 +39,27 @@ def test_eval_all_reads_dense_calldata_like_entries():
         want = [evaluate(t.raw, m) for m in plain]
         assert list(eval_all(t.raw, dense)) == want == list(eval_all(t.raw, plain))
     assert all(m["1_calldata"].untouched_dense() is not None for m in dense)
+
+
+def test_eval_all_calldata_words_read_the_bytes():
+    """SymbolicCalldata words (the MG_SYM_CDLOAD concat of 32 guarded selects)
+    evaluated from the seeds' bytes equal the per-byte semantics, at offsets
+    inside, across and past the data, with sizes that disagree with the data's
+    length, and at offsets past 2^255 (signed guard)."""
+    from mythril_amd.laser.symbolic import SymbolicCalldata
+    cd = SymbolicCalldata("9")
+    o = BVS("o", 256)
+    words = [cd.get_word_at(BVV(4, 256)), cd.get_word_at(BVV(60, 256)), cd.get_word_at(o),
+             cd.get_word_at(o + BVV(4, 256))]
+    rng = random.Random(11)
+    dense, plain = [], []
+    for m in range(120):
+        data = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 4, 36, 68, 100])))
+        size = len(data) if m % 3 else rng.choice([0, len(data) + 5, max(len(data) - 7, 0), (1 << 256) - 1])
+        off = rng.choice([0, 3, 30, 64, 99, (1 << 255) + 2, (1 << 256) - 2])
+        d = rng.choice([0, 0, 7])
+        dense.append({"9_calldata": ArrayInterp(d, dense=data), "9_calldatasize": size, "o": off})
+        plain.append({"9_calldata": ArrayInterp(d, dict(enumerate(data))), "9_calldatasize": size, "o": off})
+    for w in words:
+        want = [evaluate(w.raw, m) for m in plain]
+        assert list(eval_all(w.raw, dense)) == want == list(eval_all(w.raw, plain))
