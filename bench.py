@@ -20,6 +20,7 @@ status; under torch.distributed.run (WORLD_SIZE set) it is one of the ranks.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -760,6 +761,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     saved_cache = solver.model_cache
     try:
         for name in SYMBOLIC_TX_CODES:
+            gc.collect()                     # the earlier fields' garbage is not this field's work
             keccak_function_manager.reset()
             tx_id_manager.restart_counter()
             solver.get_model.cache_clear()
@@ -856,6 +858,7 @@ def run_analyses(dev, tx_count: int, n_seeds: int, log=None, escape_handler=None
     saved_cache = solver.model_cache
     try:
         for name in names[rank::world]:
+            gc.collect()
             keccak_function_manager.reset()
             exponent_function_manager.reset()
             tx_id_manager.restart_counter()

@@ -214,17 +214,6 @@ DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
     return r;
 }
 
-#ifdef MG_K2_NARROW
-// A Boolean operand's low dword (0 or 1): one 4-byte read from the slot, the
-// variable's row or the constant instead of the operand's 32 bytes
-DEV uint32_t bv_fetch_lo(const BvCtx &c, uint32_t ref) {
-    const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
-    if (kind <= BV_REF_SLOT) return c.slots[(idx * 2u) * BV_BLOCK + c.tid()].x;
-    if (kind == BV_REF_VAR) return c.values[2 * ((size_t)idx * c.n_models + c.model())].x;
-    return c.consts[2 * (size_t)idx].x;
-}
-#endif
-
 // The division-class ops go through TWO inlined u_divmod_nz sites instead of
 // six: UDIV/UREM (bv_udivrem), and SDIV SREM SMOD MUL_NOOVF_U (bv_divop:
 // operands prepared per op -- sign-extend + magnitude for the signed ops,
@@ -384,12 +373,6 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             case BV_EXTRACT: r = u_shr_u(A, rb & 0xffu, 0u); break;          // rb: uniform immediate
             case BV_ZEXT: r = A; break;
             case BV_SEXT: r = bv_sext(A, rb); break;
-#ifdef MG_K2_NARROW
-            case BV_BAND: r = u_small(A.w[0] & bv_fetch_lo(c, rb) & 1u); break;
-            case BV_BOR: r = u_small((A.w[0] | bv_fetch_lo(c, rb)) & 1u); break;
-            case BV_BXOR: r = u_small((A.w[0] ^ bv_fetch_lo(c, rb)) & 1u); break;
-            case BV_BIMPLIES: r = u_small(((A.w[0] & 1u) ^ 1u) | (bv_fetch_lo(c, rb) & 1u)); break;
-#endif
             default: {
                 U256 B = bv_fetch(c, rb);
                 if (op == BV_UDIV || op == BV_UREM) {        // the unsigned division site
@@ -478,12 +461,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     case BV_SGT: t = u_slt(bv_sext(B, width), bv_sext(A, width)); break;
                     default: t = !u_slt(bv_sext(A, width), bv_sext(B, width)); break;   // BV_SGE
                     }
-#ifdef MG_K2_NARROW
-                    r = u_small((t ? 1u : 0u) & bv_fetch_lo(c, rc));
-#else
                     const U256 C = bv_fetch(c, rc);
                     r = u_small((t ? 1u : 0u) & C.w[0]);
-#endif
                     break;
                 }
                 case BV_BIN2: {
