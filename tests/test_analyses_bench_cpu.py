@@ -38,3 +38,41 @@ def test_analyses_field_on_the_oracle_device():
     assert tot["pruned"] == 0 and tot["escapes_dropped"] == 0
     assert out["prefilter_hit_rate"] is not None and 0 <= out["prefilter_hit_rate"] <= 1
     assert out["contracts"]["calls.sol.o"]["open_states"] >= 1
+
+
+def _rank_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["suicide.sol.o", "origin.sol.o", "calls.sol.o"]
+        res = bench.run_analyses(_Both(), 2, 128, escape_handler=symref.Engine(signals=True).step, names=names)
+        out[rank] = {"mine": sorted(res["contracts"]), "totals": res["totals"], "ranks": res["ranks"],
+                     "job_wall": res["job_wall_s"], "rate": res["job_constraint_evals_per_s_wall"],
+                     "hit": res["prefilter_hit_rate"]}
+    finally:
+        dist.destroy_process_group()
+
+
+def test_analyses_field_deals_contracts_over_ranks():
+    """With N ranks each analyses contracts rank::N (total work fixed); the job
+    figures sum the ranks' work over the slowest rank's wall time."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_rank_worker, args=(2, port, out), nprocs=2, join=True)
+        r0, r1 = dict(out[0]), dict(out[1])
+    assert r0["mine"] == ["calls.sol.o", "suicide.sol.o"] and r1["mine"] == ["origin.sol.o"]
+    assert r0["ranks"] == r1["ranks"] == 2
+    assert r0["job_wall"] == r1["job_wall"] == max(r0["totals"]["wall_s"], r1["totals"]["wall_s"])
+    evals = r0["totals"]["constraint_evals"] + r1["totals"]["constraint_evals"]
+    assert abs(r0["rate"] - evals / r0["job_wall"]) < 1e-6 * max(evals, 1)
+    q = r0["totals"]["queries"] + r1["totals"]["queries"]
+    a = r0["totals"]["answered"] + r1["totals"]["answered"]
+    assert r0["hit"] == r1["hit"] == a / q
