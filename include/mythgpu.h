@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 12u  /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 13u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -44,7 +44,9 @@ extern "C" {
                                   RETURNDATASIZE / RETURNDATACOPY escape)
                               11: mg_cc_* (native conjunct compiler for kernel 2)
                               12: CALLDATACOPY of a symbolic size / memory offset /
-                                  calldata offset on symbolic lanes (MG_SYM_CDBYTEX) */
+                                  calldata offset on symbolic lanes (MG_SYM_CDBYTEX)
+                              13: MLOAD / MSTORE / MSTORE8 at symbolic memory offsets
+                                  (MG_SYM_MSTOREK events, MG_SYM_MLOADK reads) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -270,6 +272,13 @@ typedef struct mg_ctx mg_ctx;
 #define MG_SYM_CDBYTEX 13u /* calldata[simplify(y + w)]: byte w of a CALLDATACOPY from a
                               symbolic calldata offset y (instructions.py:816-860; a
                               symbolic size copies 320 bytes, call.py:33)           */
+#define MG_SYM_MSTOREK 14u /* an event, not a term: a write at the symbolic memory offset y
+                              of value ref z -- w = 1: MSTORE (write_word_at), 2: MSTORE8
+                              (the value's low byte), 3: one byte (a host-encoded key).  The
+                              lane's events in arena order are its byte map at symbolic keys
+                              (memory.py:117-203, keys simplify(index))                    */
+#define MG_SYM_MLOADK 15u  /* memory.get_word_at(y) over the byte map the events before this
+                              node build (a read at a symbolic offset; instructions.py:1439-1451) */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */

@@ -82,6 +82,8 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define SYM_NONE 0xffffffffu
 #define SYM_CDBYTE 12u
 #define SYM_CDBYTEX 13u
+#define SYM_MSTOREK 14u
+#define SYM_MLOADK 15u
 
 DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
 DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
@@ -675,7 +677,30 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                                                              (later_), txlim); \
                                   if (mx_ == MX_OOG) MSTOPX(ST_VMEXC, EXC_OOG) \
                                   if (mx_ == MX_ESCAPE) MSTOPX(ST_ESCAPE, op | (ESC_MEMORY << 8)) }
-                if (memsym && ta) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))      // symbolic offset
+                if (memsym && ta) {
+                    // a symbolic offset: the reference keys its byte map by simplify(index)
+                    // (memory.py:117-203).  MSTORE / MSTORE8 append an event node (offset,
+                    // value, kind) to the arena and MLOAD makes an MLOADK node; the host
+                    // decodes both by replaying the events into that byte map, so no key
+                    // equality is decided here.  No extension and no memory gas
+                    // (mem_extend returns on a symbolic start, machine_state.py:171-180).
+                    // SHA3 and taint lanes stay with the host.
+                    if (tl || kind == K_SHA3) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    if (kind == K_MLOAD) {
+                        MPUSHCHK()
+                        MGAS()
+                        if (!sym_node_push(S, N, lane, SYM_MLOADK | (256u << 8), ta - 1u, 0u, 0u, lnn, rtag))
+                            MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                    } else {
+                        MGAS()
+                        uint32_t vref, et;
+                        if (!sym_ref(S, N, lane, tb, b, lnc, vref) ||
+                            !sym_node_push(S, N, lane, SYM_MSTOREK, ta - 1u, vref, kind == K_MSTORE8 ? 2u : 1u,
+                                           lnn, et))
+                            MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                    }
+                    break;
+                }
                 if (kind == K_SLOAD) {
                     // simplify(Select(chain, index)): from the newest store, the same
                     // index term answers, a distinct constant index (both constant) is

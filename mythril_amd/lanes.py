@@ -49,6 +49,8 @@ MG_SYM_CDLOAD, MG_SYM_CDSIZE, MG_SYM_ENV, MG_SYM_BIN, MG_SYM_UN = 1, 2, 3, 4, 5
 MG_SYM_SLOAD, MG_SYM_KECCAK, MG_SYM_EXTRACT, MG_SYM_CONCAT, MG_SYM_TERM = 6, 7, 8, 9, 10
 MG_SYM_CDBYTE = 12      # calldata[w]: one byte of a symbolic calldata copy
 MG_SYM_CDBYTEX = 13     # calldata[simplify(y + w)]: a copy from a symbolic calldata offset
+MG_SYM_MSTOREK = 14     # event: write of value ref z at symbolic offset y (w: 1 word, 2 low byte, 3 byte)
+MG_SYM_MLOADK = 15      # get_word_at(y) over the byte map of the events before it
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
 MG_LANE_RETDATA = 16384
 MG_SYM_CONST = 0x80000000

@@ -256,8 +256,8 @@ class Memory:
     ``simplify(index)``): ``memory_key`` gathers the constants of an add chain
     as z3's simplify does, so ``(p + 1) + 31`` and ``p + 32`` are one byte.
     Its ``bv_key >= len(self)`` guard is a symbolic (signed) compare that never
-    drops the write.  Lanes carry concrete offsets only: a state with bytes at
-    symbolic keys stays with the host's handler."""
+    drops the write.  A lane carries the bytes at symbolic keys as write events
+    in its arena (MG_SYM_MSTOREK, laser/symbolic.py), replayed into this map."""
 
     def __init__(self, data: bytes = b"", sym: Optional[Dict[int, BitVec]] = None,
                  keys: Optional[Dict[Node, object]] = None):
@@ -332,6 +332,10 @@ class Memory:
     def symbolic_bytes(self) -> Dict[int, BitVec]:
         """{offset: 8-bit expression} of the symbolic bytes at concrete offsets."""
         return self._sym
+
+    def symbolic_key_bytes(self) -> Dict[Node, object]:
+        """{normalised symbolic key: byte (int or 8-bit expression)}, in write order."""
+        return self._keys
 
     def get_word_at(self, index) -> BitVec:
         k, key = self._index(index)

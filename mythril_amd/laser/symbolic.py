@@ -38,6 +38,7 @@ from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_CALLVALUE as MG_ENV_CALLVALUE, ENV_GASPRICE as MG_ENV_GASPRICE,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
                      MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
+                     MG_SYM_MLOADK, MG_SYM_MSTOREK,
                      MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
@@ -274,7 +275,29 @@ class _Decoder:
             return keccak_of(simplify_concat(self.parts(y, w)))
         if kind == MG_SYM_TERM:
             return term(w)
+        if kind == MG_SYM_MLOADK:
+            # get_word_at(offset) over the byte map the writes before this node made
+            mem = Memory()
+            self.replay_keys(mem, k)
+            return mem.get_word_at(self.ref(y))
         raise NotEncodable(f"unknown arena node kind {kind}")
+
+    def replay_keys(self, mem, upto: int) -> None:
+        """Apply the lane's writes at symbolic offsets (MG_SYM_MSTOREK events of
+        nodes [0, upto), in arena order = execution order) to `mem`: MSTORE's
+        write_word_at, MSTORE8's low byte, a host-encoded byte (memory.py:84-115,
+        instructions.py:1454-1493)."""
+        for j in range(upto):
+            x, y, z, w = self.row(j)
+            if x & 0xFF != MG_SYM_MSTOREK:
+                continue
+            off, val = self.ref(y), self.ref(z)
+            if w == 1:
+                mem.write_word_at(off, val)
+            elif w == 2:
+                mem[off] = val.value % 256 if val.value is not None else Extract(7, 0, val)
+            else:
+                mem[off] = val.value if val.value is not None else val
 
     # -- memory and storage
     def memory(self):
@@ -290,7 +313,10 @@ class _Decoder:
                 node, j = t >> 5, t & 31
                 word = self.node(node)
                 symb[int(p)] = word if word.size() == 8 else Extract(255 - 8 * j, 248 - 8 * j, word)
-        return Memory(bytes(b.memory[i, :msize]), symb)
+        mem = Memory(bytes(b.memory[i, :msize]), symb)
+        if any(r[0] & 0xFF == MG_SYM_MSTOREK for r in (self.row(k) for k in range(self.n_nodes))):
+            self.replay_keys(mem, self.n_nodes)
+        return mem
 
     def entry(self, e: int):
         """Storage chain entry e as (key, value).  Entries decode one at a time:
@@ -431,6 +457,13 @@ class _Encoder:
         self.node_raw.append(raw)
         self._nref[raw] = len(self.nodes) - 1
         return len(self.nodes) - 1
+
+    def event(self, x, y=0, z=0, w=0) -> None:
+        """An arena entry that is not a term (MG_SYM_MSTOREK)."""
+        if len(self.nodes) >= self.node_cap:
+            raise NotEncodable("arena full")
+        self.nodes.append((x, y, z, w))
+        self.node_raw.append(None)
 
     def enc(self, raw) -> int:
         """Operand ref of a raw term (a node index or a constant ref)."""
@@ -576,8 +609,6 @@ def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> La
     represent.  The lane is symbolic when any of them is, or its calldata or
     environment words are, or its storage base is the symbolic Array."""
     enc = _Encoder(node_cap, const_cap)
-    if state.mstate.memory.symbolic_keys:
-        raise NotEncodable("memory bytes at symbolic offsets")
     flags = lane_flags(state)
     storage = state.environment.active_account.storage
     symstore = not storage.concrete or (storage.is_chain and any(
@@ -603,6 +634,13 @@ def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> La
         for p, e in state.mstate.memory.symbolic_bytes().items():
             mem[p] = enc.byte(e)
         flags |= MG_LANE_MEMTAG
+    # bytes at symbolic keys: one write event per key, in the map's order
+    for key, byte in state.mstate.memory.symbolic_key_bytes().items():
+        off = enc.enc(key)
+        if off & MG_SYM_CONST:
+            raise NotEncodable("a symbolic memory key that folds to a constant")
+        val = enc.cref(byte) if isinstance(byte, int) else enc.enc(byte.raw)
+        enc.event(MG_SYM_MSTOREK, off, val, 3)
     return LaneEncoding(enc, stack, mem, store, flags)
 
 

@@ -234,7 +234,8 @@ class Engine:
                     n_w = min(code_len - src, size) if src < code_len else 0
             for p in range(lo, lo + n_w):
                 sym.pop(p, None)
-        n.mstate.memory = Memory(bytes(b.memory[0, :int(b.msize[0])]), sym)
+        # bytes at symbolic keys are untouched by an instruction the oracle runs
+        n.mstate.memory = Memory(bytes(b.memory[0, :int(b.msize[0])]), sym, ms.memory.symbolic_key_bytes())
         n.mstate.pc = int(b.pc[0])
         n.mstate.depth = int(b.depth[0])
         n.mstate.min_gas_used, n.mstate.max_gas_used = int(b.gas_min[0]), int(b.gas_max[0])

@@ -100,6 +100,10 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
             assert got.mstate.memory.raw() == ref.mstate.memory.raw()
             assert {p: e.raw for p, e in got.mstate.memory.symbolic_bytes().items()} == \
                 {p: e.raw for p, e in ref.mstate.memory.symbolic_bytes().items()}
+            # bytes at symbolic keys (MG_SYM_MSTOREK events), values and write order
+            assert [(k, v if isinstance(v, int) else v.raw)
+                    for k, v in got.mstate.memory.symbolic_key_bytes().items()] == \
+                [(k, v if isinstance(v, int) else v.raw) for k, v in ref.mstate.memory.symbolic_key_bytes().items()]
             gst, rst = got.environment.active_account.storage, ref.environment.active_account.storage
             if rst.is_chain:
                 assert [(k.raw, v.raw) for k, v in gst.chain()] == [(k.raw, v.raw) for k, v in rst.chain()]
@@ -145,17 +149,11 @@ def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch)
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
     assert laser.forks >= 3 and laser.lane_steps > 100
-    # CALLDATACOPY of a symbolic size, memory offset or calldata offset runs on the
-    # device; what else escapes is the host's part.  environments.sol's
-    # batchTransfer(address[]) then stores at a symbolic memory offset (its free
-    # pointer moves by a symbolic length): memory with symbolic keys is host-only
-    # (laser/state.py Memory), so those paths finish on the host
-    assert laser.escaped_ops["CALLDATACOPY"] == 0, dict(laser.escaped_ops)
-    if name not in SYMBOLIC_KEY_MEMORY:
-        assert set(laser.escaped_ops) <= HOST_OPS, dict(laser.escaped_ops)
-
-
-SYMBOLIC_KEY_MEMORY = {"environments.sol.o"}
+    # CALLDATACOPY of a symbolic size, memory offset or calldata offset, and MLOAD /
+    # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
+    # its free-memory pointer by a symbolic length) run on the device; what
+    # escapes is the host's part
+    assert set(laser.escaped_ops) <= HOST_OPS, dict(laser.escaped_ops)
 
 
 @pytest.mark.parametrize("name", symcases.SYM_CREATIONS)

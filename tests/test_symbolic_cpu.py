@@ -336,3 +336,53 @@ def test_restated_symbolic_calldata_copy_follows_the_reference():
     # a symbolic memory offset: the copy is dropped, the operands popped
     s2 = _run_restatement("6020" "6000" "600035" "37" "00", 5)     # PUSH1 32 PUSH1 0 (PUSH1 0 CALLDATALOAD) CALLDATACOPY
     assert len(s2.mstate.stack) == 0 and len(s2.mstate.memory) == 0
+
+
+def test_memory_at_symbolic_keys_round_trips_and_decodes_like_the_byte_map():
+    """MSTORE / MSTORE8 / MLOAD at symbolic offsets (memory.py:117-203): the
+    restatement's byte map keyed by simplify(index) survives encode -> lane ->
+    decode as MG_SYM_MSTOREK events, and the device's event + MLOADK nodes decode
+    to what the byte map gives."""
+    from mythril_amd.lanes import MG_SYM_BIN, MG_SYM_CDLOAD, MG_SYM_MLOADK, MG_SYM_MSTOREK
+    from mythril_amd.laser.state import Memory
+    from mythril_amd.smt.expr import Extract
+    # PUSH1 4 CALLDATALOAD (x) | PUSH2 0x1234 DUP2 MSTORE | PUSH1 0x20 CALLDATALOAD DUP2 PUSH1 0x28 ADD
+    # MSTORE8 | DUP1 PUSH1 0x10 ADD MLOAD | STOP
+    code = "600435" "611234" "81" "52" "602035" "81" "6028" "01" "53" "80" "6010" "01" "51" "00"
+    s = _run_restatement(code, 14)
+    mem = s.mstate.memory
+    assert mem.symbolic_keys and len(mem.symbolic_key_bytes()) == 33
+    le = sym.encode_state(s)
+    b = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=256, const_cap=64, mem_cap=64))
+    le.write(b, 0)
+    b.sp[0] = len(s.mstate.stack)
+    b.msize[0] = len(mem)
+    b.flags[0] = le.flags
+    stack, mem2, _ = sym.decode_lane(b, 0, s)
+    assert [w.raw for w in stack] == [w.raw for w in s.mstate.stack]
+    want = {k: (v if isinstance(v, int) else v.raw) for k, v in mem.symbolic_key_bytes().items()}
+    got = {k: (v if isinstance(v, int) else v.raw) for k, v in mem2.symbolic_key_bytes().items()}
+    assert got == want and list(got) == list(want)
+    # the device's form: x = CDLOAD(4); write 0x1234 at x; read at x; read at x + 16
+    c = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=16, const_cap=8))
+    c.node[0, 0] = (MG_SYM_CDLOAD | 256 << 8, MG_SYM_CONST | 0, 0, 0)
+    c.node[0, 1] = (MG_SYM_MSTOREK, 0, MG_SYM_CONST | 1, 1)
+    c.node[0, 2] = (MG_SYM_MLOADK | 256 << 8, 0, 0, 0)
+    c.node[0, 3] = (MG_SYM_BIN | 256 << 8, 0, MG_SYM_CONST | 2, 0x01)
+    c.node[0, 4] = (MG_SYM_MLOADK | 256 << 8, 3, 0, 0)
+    c.node[0, 5] = (MG_SYM_MSTOREK, 3, 0, 2)                   # MSTORE8 of x's low byte at x + 16
+    c.node[0, 6] = (MG_SYM_MLOADK | 256 << 8, 0, 0, 0)
+    for k, v in enumerate((4, 0x1234, 16)):
+        c.cval[0, k] = word_to_limbs(v)
+    c.n_nodes[0], c.n_consts[0] = 7, 3
+    dec = sym._Decoder(c, 0, s)
+    x = s.environment.calldata.get_word_at(BVV(4, 256))
+    ref = Memory()
+    ref.write_word_at(x, BVV(0x1234, 256))
+    assert dec.node(2).raw is ref.get_word_at(x).raw and dec.node(2).value == 0x1234
+    assert dec.node(4).raw is ref.get_word_at(x + BVV(16, 256)).raw
+    ref[x + BVV(16, 256)] = Extract(7, 0, x)
+    assert dec.node(6).raw is ref.get_word_at(x).raw and dec.node(6).symbolic
+    full = sym._Decoder(c, 0, s).memory()
+    assert {k: (v if isinstance(v, int) else v.raw) for k, v in full.symbolic_key_bytes().items()} == \
+        {k: (v if isinstance(v, int) else v.raw) for k, v in ref.symbolic_key_bytes().items()}
