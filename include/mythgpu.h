@@ -277,8 +277,10 @@ typedef struct mg_ctx mg_ctx;
                               (the value's low byte), 3: one byte (a host-encoded key).  The
                               lane's events in arena order are its byte map at symbolic keys
                               (memory.py:117-203, keys simplify(index))                    */
-#define MG_SYM_MLOADK 15u  /* memory.get_word_at(y) over the byte map the events before this
-                              node build (a read at a symbolic offset; instructions.py:1439-1451) */
+#define MG_SYM_MLOADK 15u  /* a read at the symbolic offset y over the byte map the events
+                              before this node build: w = 0, memory.get_word_at(y) (MLOAD,
+                              instructions.py:1439-1451); w = n > 0, simplify(Concat(memory[y :
+                              y + n])) (the data of a SHA3, instructions.py:1014-1051)     */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */

@@ -684,9 +684,31 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     // decodes both by replaying the events into that byte map, so no key
                     // equality is decided here.  No extension and no memory gas
                     // (mem_extend returns on a symbolic start, machine_state.py:171-180).
-                    // SHA3 and taint lanes stay with the host.
-                    if (tl || kind == K_SHA3) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
-                    if (kind == K_MLOAD) {
+                    // SHA3 of a concrete length reads the same way: an MLOADK node over
+                    // [offset, offset + length) feeds a KECCAK node (sha3_, instructions.py:
+                    // 1014-1051).  A symbolic or zero length and taint lanes stay with the host.
+                    if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    if (kind == K_SHA3) {
+                        if (tb || !u_fits32(b) || b.w[0] == 0u || b.w[0] > 4096u)
+                            MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                        const uint32_t len = b.w[0];
+                        if (!L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                        const uint64_t g = 30ull + 6ull * (((uint64_t)len + 31ull) >> 5);
+                        ngmin += g; ngmax += g;
+                        if (ngmin >= glim) MSTOPX(ST_VMEXC, EXC_OOG)
+                        const uint32_t rec_at = L.rec_len[lane];
+                        if ((uint64_t)rec_at + MG_REC_HEADER + 1u > L.rec_cap)
+                            MSTOPX(ST_ESCAPE, op | (ESC_RECORD << 8))
+                        MPUSHCHK()
+                        uint32_t mt;
+                        if (!sym_node_push(S, N, lane, SYM_MLOADK | ((8u * len) << 8), ta - 1u, 0u, len, lnn, mt) ||
+                            !sym_node_push(S, N, lane, SYM_KECCAK | (256u << 8), mt - 1u, 0u, 8u * len, lnn, rtag))
+                            MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
+                        rec_new = rec_head(L, lane, rec_at, MG_REC_SYMKECCAK, len, L.steps[lane] + executed, u_zero());
+                        L.rec[(size_t)rec_new * N + lane] = rtag - 1u;
+                        ++rec_new;
+                        ++n_sha3;
+                    } else if (kind == K_MLOAD) {
                         MPUSHCHK()
                         MGAS()
                         if (!sym_node_push(S, N, lane, SYM_MLOADK | (256u << 8), ta - 1u, 0u, 0u, lnn, rtag))

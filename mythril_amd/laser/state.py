@@ -407,10 +407,33 @@ def _add(index, j: int):
 
 
 def _slice_len(start, stop) -> int:
-    """memory.py:137-155: the slice length when stop - start folds to a
-    constant, else APPROX_ITR + 1 = 101 entries."""
+    """memory.py:137-155: the slice length when simplify(stop - start) folds to
+    a constant, else APPROX_ITR + 1 = 101 entries.  Two add chains over the
+    same operands differ by their constants (z3 cancels the common terms:
+    (x + 40) - x is 40)."""
     d = _add(stop, 0) - start if isinstance(stop, Expression) else symbol_factory.BitVecVal(stop, 256) - start
-    return d.value if d.value is not None else 101
+    if d.value is not None:
+        return d.value
+    a, ca = _chain(stop.raw if isinstance(stop, Expression) else _const_node(stop))
+    b, cb = _chain(start.raw if isinstance(start, Expression) else _const_node(start))
+    if sorted(map(id, a)) == sorted(map(id, b)):
+        return (ca - cb) & M256
+    return 101
+
+
+def _chain(raw: Node):
+    """The non-constant operands and the summed constant of a bvadd chain."""
+    terms, c = [], 0
+    stack = [raw]
+    while stack:
+        n = stack.pop()
+        if n.op == "bvadd" and n.width == 256:
+            stack.extend(n.args)
+        elif n.op == "const":
+            c = (c + n.param) & M256
+        else:
+            terms.append(n)
+    return terms, c
 
 
 class MachineState:

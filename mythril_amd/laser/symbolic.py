@@ -276,10 +276,16 @@ class _Decoder:
         if kind == MG_SYM_TERM:
             return term(w)
         if kind == MG_SYM_MLOADK:
-            # get_word_at(offset) over the byte map the writes before this node made
+            # over the byte map the writes before this node made: get_word_at(offset)
+            # (MLOAD), or the data SHA3 hashes, simplify(Concat(memory[offset:+w]))
             mem = Memory()
             self.replay_keys(mem, k)
-            return mem.get_word_at(self.ref(y))
+            off = self.ref(y)
+            if w == 0:
+                return mem.get_word_at(off)
+            data = [b if isinstance(b, BitVec) else symbol_factory.BitVecVal(b, 8)
+                    for b in mem[off: off + symbol_factory.BitVecVal(w, 256)]]
+            return simplify_concat(data) if len(data) > 1 else data[0]
         raise NotEncodable(f"unknown arena node kind {kind}")
 
     def replay_keys(self, mem, upto: int) -> None:

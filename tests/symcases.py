@@ -31,7 +31,14 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3")
+
+# synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
+# SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
+# storage:  MSTORE(x, CALLER); h = SHA3(x, 64); if !storage[h]: storage[h] = 1;
+# y = calldata[36:68]; if y: MSTORE8(x, y); if MLOAD(x): storage[0] = SHA3(x, 33)
+SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f578083535b"
+                        "825180602757005b6021842060005500"}
 
 
 def deploy(device, name):
@@ -41,7 +48,8 @@ def deploy(device, name):
     if name in RUNTIME:
         ws = WorldState()
         ws.put_account(Account(CREATOR, balances=None))
-        acct = Account(workloads.CONTRACT, code=Disassembly(workloads.bytecode(name)), concrete_storage=False)
+        code = bytes.fromhex(SYNTH[name]) if name in SYNTH else workloads.bytecode(name)
+        acct = Account(workloads.CONTRACT, code=Disassembly(code), concrete_storage=False)
         ws.put_account(acct)
         return ws, workloads.CONTRACT
     args, value = CONTRACTS[name]

@@ -261,7 +261,9 @@ class Engine:
         if op in (0x51, 0x52, 0x53) and _val(st[-1]) is None:
             return self._symbolic_offset(state if state is not None else s, s, op)
         if op == 0x20 and _val(st[-1]) is None:
-            raise Unsupported("symbolic SHA3 offset")
+            if _val(st[-2]) is None:
+                raise Unsupported("symbolic SHA3 offset and length")
+            return self._symbolic_sha3(state if state is not None else s, s)
         if op == 0x20 and _val(st[-2]) is None:
             raise Unsupported("symbolic SHA3 length")
         b = self._oracle_run(s)
@@ -296,6 +298,33 @@ class Engine:
                 st.append(keccak_function_manager.get_empty_keccak_hash())
                 return [s]
             st.append(keccak_function_manager.create_keccak(data))
+        return [s]
+
+    def _symbolic_sha3(self, state, s):
+        """sha3_ (instructions.py:1014-1051) at a symbolic offset, concrete length:
+        mem_extend extends nothing; the data are the bytes at the symbolic keys
+        offset + k (memory.py:117-203), joined by simplify(Concat); the sha3 gas."""
+        ms = s.mstate
+        st = ms.stack
+        index, length = st.pop(), _val(st.pop())
+        if length == 0 or length > 4096:
+            raise Unsupported("SHA3 length the device leaves to the host")
+        g = 30 + 6 * ((length + 31) // 32)
+        if ms.min_gas_used + g >= min(_gas_limit(s), 10 ** 9 + 1):
+            return self._vmexc(state)
+        ms.min_gas_used += g
+        ms.max_gas_used += g
+        data_list = [x if isinstance(x, BitVec) else BVV(x, 8) for x in ms.memory[index: index + BVV(length, 256)]]
+        if len(data_list) > 1:
+            data = simplify_concat(data_list)
+        elif len(data_list) == 1:
+            data = data_list[0]
+        else:
+            st.append(keccak_function_manager.get_empty_keccak_hash())
+            ms.pc += 1
+            return [s]
+        st.append(keccak_function_manager.create_keccak(data))
+        ms.pc += 1
         return [s]
 
     def _symbolic_offset(self, state, s, op):

@@ -24,7 +24,7 @@ from mythril_amd.lanes import (LaneBatch, LaneShape, MG_SYM_BIN, MG_SYM_CDLOAD, 
 from mythril_amd.laser import (Account, Disassembly, MessageCallTransaction, SymbolicCalldata,
                                WorldState)
 from mythril_amd.laser import symbolic as sym
-from mythril_amd.smt.expr import Bool, symbol_factory
+from mythril_amd.smt.expr import BitVec, Bool, symbol_factory
 from oracle_device import OracleDevice
 
 BVV, BVS = symbol_factory.BitVecVal, symbol_factory.BitVecSym
@@ -386,3 +386,46 @@ def test_memory_at_symbolic_keys_round_trips_and_decodes_like_the_byte_map():
     full = sym._Decoder(c, 0, s).memory()
     assert {k: (v if isinstance(v, int) else v.raw) for k, v in full.symbolic_key_bytes().items()} == \
         {k: (v if isinstance(v, int) else v.raw) for k, v in ref.symbolic_key_bytes().items()}
+
+
+def test_sha3_at_a_symbolic_offset_decodes_to_the_hash_of_the_byte_map():
+    """sha3_ (instructions.py:1014-1051) at a symbolic offset and concrete length:
+    the device's MLOADK range node (w = length) under a KECCAK node decodes to
+    keccak over simplify(Concat(memory[offset:offset + length])) of the byte map
+    the MSTOREK events before it built; the restatement hashes the same data."""
+    from mythril_amd.lanes import MG_SYM_CDLOAD, MG_SYM_KECCAK, MG_SYM_MLOADK, MG_SYM_MSTOREK
+    from mythril_amd.laser.state import Memory
+    c = LaneBatch(LaneShape(n=1, stack_cap=16, node_cap=16, const_cap=8))
+    c.node[0, 0] = (MG_SYM_CDLOAD | 256 << 8, MG_SYM_CONST | 0, 0, 0)
+    c.node[0, 1] = (MG_SYM_MSTOREK, 0, MG_SYM_CONST | 1, 1)              # MSTORE(x, 0x1234)
+    c.node[0, 2] = (MG_SYM_MLOADK | (8 * 40) << 8, 0, 0, 40)             # memory[x:x+40]
+    c.node[0, 3] = (MG_SYM_KECCAK | 256 << 8, 2, 0, 8 * 40)
+    c.node[0, 4] = (MG_SYM_MSTOREK, 0, 0, 1)                             # MSTORE(x, x)
+    c.node[0, 5] = (MG_SYM_MLOADK | (8 * 32) << 8, 0, 0, 32)
+    c.node[0, 6] = (MG_SYM_KECCAK | 256 << 8, 5, 0, 8 * 32)
+    for k, v in enumerate((4, 0x1234)):
+        c.cval[0, k] = word_to_limbs(v)
+    c.n_nodes[0], c.n_consts[0] = 7, 2
+    s = _run_restatement("5b00", 1)
+    dec = sym._Decoder(c, 0, s)
+    x = s.environment.calldata.get_word_at(BVV(4, 256))
+    ref = Memory()
+    ref.write_word_at(x, BVV(0x1234, 256))
+
+    def data(n):
+        return data_at(ref, x, n)
+    assert dec.node(2).raw is data(40).raw and dec.node(2).size() == 320
+    assert dec.node(3).raw is sym.keccak_of(data(40)).raw and not dec.node(3).symbolic
+    ref.write_word_at(x, x)
+    assert dec.node(5).raw is data(32).raw and dec.node(6).raw is sym.keccak_of(data(32)).raw
+    assert dec.node(6).symbolic
+    # the restatement at the same point: x = CALLDATALOAD(4); MSTORE(x, 0x1234); SHA3(x, 40)
+    s2 = _run_restatement("600435" "611234" "81" "52" "6028" "81" "20" "00", 8)
+    top = s2.mstate.stack[-1]
+    assert top.raw is sym.keccak_of(data_at(s2.mstate.memory, x, 40)).raw
+
+
+def data_at(mem, x, n):
+    """simplify(Concat(memory[x:x+n])) as sha3_ builds it (instructions.py:1036-1045)."""
+    from mythril_amd.smt.expr import simplify_concat
+    return simplify_concat([b if isinstance(b, BitVec) else BVV(b, 8) for b in mem[x: x + BVV(n, 256)]])
