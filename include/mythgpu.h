@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 13u  /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 14u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -46,7 +46,12 @@ extern "C" {
                               12: CALLDATACOPY of a symbolic size / memory offset /
                                   calldata offset on symbolic lanes (MG_SYM_CDBYTEX)
                               13: MLOAD / MSTORE / MSTORE8 at symbolic memory offsets
-                                  (MG_SYM_MSTOREK events, MG_SYM_MLOADK reads) */
+                                  (MG_SYM_MSTOREK events, MG_SYM_MLOADK reads)
+                              14: SHA3 at a symbolic offset (MLOADK ranges), RETURN /
+                                  REVERT of a symbolic range (MG_RET_SYMBOLIC),
+                                  SELFBALANCE on MG_LANE_SYMBAL lanes, RETURNDATASIZE
+                                  on MG_LANE_SYMRDS lanes, RETURNDATACOPY of a
+                                  symbolic operand (pops only) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -75,6 +80,13 @@ extern "C" {
 #define MG_DEPTH          9u  /* strategy depth cutoff (strategy/__init__.py:29) */
 #define MG_LOOP_BOUND    10u  /* BoundedLoopsStrategy dropped the state at a JUMPDEST
                                  (bounded_loops.py:119-145); aux = loop count      */
+
+/* ret_len of a symbolic lane's RETURN / REVERT whose offset or length is symbolic
+ * (instructions.py:1858-1934): the return data are the reference's fresh
+ * "return_data" bytes or a slice at symbolic keys, which the host does not
+ * read; LaneBatch.return_data gives None.  (A creation's RETURN of that kind
+ * escapes: its return data would be the runtime code.)                     */
+#define MG_RET_SYMBOLIC 0xFFFFFFFFu
 
 #define MG_EXC_STACK_UNDERFLOW     1u
 #define MG_EXC_STACK_OVERFLOW      2u
@@ -164,12 +176,21 @@ extern "C" {
                                  (instructions.py:1314-1370)                       */
 
 /* environment words, per lane */
+#define MG_LANE_SYMBAL 32768u /* symbolic lane whose active account's balance is
+                                 symbolic: SELFBALANCE pushes an MG_SYM_ENV node
+                                 (w = MG_ENV_SELFBALANCE, instructions.py:968-976) */
+#define MG_LANE_SYMRDS 65536u /* symbolic lane whose last_return_data has a symbolic
+                                 size (a host CALL's returndatasize variable):
+                                 RETURNDATASIZE pushes an MG_SYM_ENV node
+                                 (w = MG_ENV_RETURNDATASIZE, instructions.py:1359-1370) */
 #define MG_ENV_ADDRESS   0
 #define MG_ENV_CALLER    1
 #define MG_ENV_ORIGIN    2
 #define MG_ENV_CALLVALUE 3
 #define MG_ENV_GASPRICE  4
 #define MG_ENV_WORDS     5
+#define MG_ENV_SELFBALANCE 5  /* MG_SYM_ENV immediate only: environment.active_account.balance() */
+#define MG_ENV_RETURNDATASIZE 6 /* MG_SYM_ENV immediate only: last_return_data.size */
 
 #define MG_STACK_LIMIT 1024u              /* MachineStack.STACK_LIMIT           */
 #define MG_MSTATE_GAS_LIMIT 1000000000ull /* GlobalState default gas_limit      */

@@ -74,6 +74,8 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 // ---- symbolic memory, storage and SHA3 (ABI v7) ----------------------------------
 #define LANE_SYMSTORE 4096u
 #define LANE_MEMTAG 8192u
+#define LANE_SYMBAL 32768u
+#define LANE_SYMRDS 65536u
 #define SYM_SLOAD 6u
 #define SYM_KECCAK 7u
 #define SYM_EXTRACT 8u
@@ -441,7 +443,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         if (executed >= lane_max) break;
         const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
-        if ((uy & PD_SPECIAL) || (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
+        if (((uy & PD_SPECIAL) && !(op == 0x47u && (flags & LANE_SYMBAL) && !tl)) ||
+            (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
         const uint32_t req = d.y & 15u, npop = (d.y >> 4) & 15u;
@@ -847,6 +850,57 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }
             ++executed;
             continue;
+        }
+
+        if (op == 0x47u || (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
+            // SELFBALANCE on a lane whose balance is symbolic (selfbalance_,
+            // instructions.py:968-976; taint lanes escaped above):
+            // environment.active_account.balance(), the balances array at the active
+            // address; RETURNDATASIZE after a host CALL that left a symbolic size
+            // (returndatasize_, :1359-1370): last_return_data.size.  ENV nodes the
+            // host decodes.  No host CALL runs inside a device run, so neither value
+            // can move under it.
+            const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : MG_ENV_RETURNDATASIZE;
+            const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
+            uint32_t lnn = nn, rtag = 0u;
+            if (sp + 1u > STACK_LIMIT) { ++executed; status = ST_VMEXC; aux = EXC_OVERFLOW; break; }
+            if (sp + 1u > L.stack_cap) { status = ST_ESCAPE; aux = op | (ESC_STACK << 8); break; }
+            if (!sym_node_push(S, N, lane, SYM_ENV | (256u << 8), 0u, 0u, which, lnn, rtag)) {
+                status = ST_ESCAPE; aux = op | (ESC_ARENA << 8); break;
+            }
+            if (ngmin >= glim) { ++executed; status = ST_VMEXC; aux = EXC_OOG; break; }
+            V.set_stack(sp, u_zero());
+            sym_set_tag(S, N, lane, sp, rtag);
+            ++sp; ++pc; gmin = ngmin; gmax = ngmax; nn = lnn;
+            ++executed;
+            continue;
+        }
+
+        if (op == 0x3eu && any_sym && !tl && sp >= 3u) {
+            // RETURNDATACOPY with a symbolic memory offset, return offset or size
+            // (returndatacopy_, instructions.py:1314-1343): the three words are popped
+            // and nothing is copied; the table gas, then the OOG check
+            const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
+            ++executed;
+            if (ngmin >= glim) { status = ST_VMEXC; aux = EXC_OOG; break; }
+            sp -= 3u; ++pc; gmin = ngmin; gmax = ngmax;
+            continue;
+        }
+
+        if (any_sym && !tl && (kind == K_RETURN || (kind == K_REVERT)) && sp >= 2u &&
+            !(creation && kind == K_RETURN)) {
+            // ---- RETURN / REVERT with a symbolic offset or length (instructions.py:
+            // 1858-1934): the transaction ends; the return data are fresh
+            // "return_data" bytes or a slice at symbolic keys, left to the host
+            // (MG_RET_SYMBOLIC).  RETURN of a concrete length runs mem_extend, which
+            // returns on a symbolic start, then check_gas_usage_limit; a symbolic
+            // length skips both.  The lane stays at the instruction's start.
+            const uint32_t tlen = sym_tag(S, N, lane, sp - 2u);
+            ++executed;
+            if (kind == K_RETURN && !tlen && gmin >= glim) { status = ST_VMEXC; aux = EXC_OOG; break; }
+            L.ret_offset[lane] = 0u; L.ret_len[lane] = MG_RET_SYMBOLIC;
+            status = kind == K_RETURN ? ST_RETURN : ST_REVERT; aux = 0u;
+            break;
         }
 
         if ((any_sym || env_sym || cd_sym) && !stack_op && sp >= max(req, npop)) {

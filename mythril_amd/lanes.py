@@ -36,6 +36,7 @@ MG_EXC_INVALID_INSTRUCTION, MG_EXC_OUT_OF_GAS, MG_EXC_WRITE_PROTECTION = 4, 5, 6
 MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2, 3, 4, 5
 MG_ESC_RECORD = 6
 MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
+MG_RET_SYMBOLIC = 0xFFFFFFFF
 # function-manager records (include/mythgpu.h MG_REC_*)
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
 MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
@@ -52,6 +53,8 @@ MG_SYM_CDBYTEX = 13     # calldata[simplify(y + w)]: a copy from a symbolic call
 MG_SYM_MSTOREK = 14     # event: write of value ref z at symbolic offset y (w: 1 word, 2 low byte, 3 byte)
 MG_SYM_MLOADK = 15      # get_word_at(y) over the byte map of the events before it
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
+MG_LANE_SYMBAL, MG_LANE_SYMRDS = 32768, 65536
+MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE = 5, 6
 MG_LANE_RETDATA = 16384
 MG_SYM_CONST = 0x80000000
 MG_LANE_TAINT = 2048
@@ -397,10 +400,13 @@ class LaneBatch:
     def memory_bytes(self, i: int) -> bytes:
         return bytes(self.memory[i, : int(self.msize[i])])
 
-    def return_data(self, i: int) -> bytes:
+    def return_data(self, i: int) -> Optional[bytes]:
         """RETURN/REVERT data: memory[off:off+len], bytes past msize read as 0
-        (state/memory.py:152-157 reads missing keys as 0)."""
+        (state/memory.py:152-157 reads missing keys as 0); None for a symbolic
+        offset or length (MG_RET_SYMBOLIC)."""
         off, ln = int(self.ret_offset[i]), int(self.ret_len[i])
+        if ln == MG_RET_SYMBOLIC:
+            return None
         m = self.memory_bytes(i)
         return bytes(m[k] if k < len(m) else 0 for k in range(off, off + ln))
 

@@ -39,7 +39,7 @@ from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
                      MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
                      MG_SYM_MLOADK, MG_SYM_MSTOREK,
-                     MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_ENV_RETURNDATASIZE, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
                         URem, SRem, _select, simplify_concat, symbol_factory)
@@ -181,6 +181,10 @@ def source(kind: int, imm: int, arg, state):
     if kind == MG_SYM_CDSIZE:
         return env.calldata.calldatasize
     if kind == MG_SYM_ENV:
+        if imm == MG_ENV_SELFBALANCE:           # selfbalance_ (instructions.py:968-976)
+            return env.active_account.balance()
+        if imm == MG_ENV_RETURNDATASIZE:        # returndatasize_ (instructions.py:1359-1370)
+            return state.last_return_data.size
         return getattr(env, _ENV_ATTR[imm])
     raise NotEncodable(f"unknown source kind {kind}")
 
@@ -254,6 +258,10 @@ class _Decoder:
         if kind == MG_SYM_CDLOAD:
             a = self.ref(y)
             return _mark(source(kind, w, a, self.state), kind, w, (a,))
+        if kind == MG_SYM_ENV and w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE):
+            # no provenance: the balance and the return data change across host
+            # CALLs, so a re-encoded term rides as itself, not as "the value now"
+            return source(kind, w, None, self.state)
         if kind in (MG_SYM_CDSIZE, MG_SYM_ENV):
             return _mark(source(kind, w, None, self.state), kind, w, ())
         if kind == MG_SYM_CDBYTE:
@@ -634,6 +642,11 @@ def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> La
             enc.raws.append(Node("store", 0, (enc.raws[-1], k.raw, v.raw), (256, 256)))
         if not storage.concrete:
             flags |= MG_LANE_SYMSTORE
+        if state.environment.active_account.balance().symbolic:
+            flags |= MG_LANE_SYMBAL
+        rds = getattr(getattr(state, "last_return_data", None), "size", None)
+        if isinstance(rds, BitVec) and rds.symbolic:
+            flags |= MG_LANE_SYMRDS
     stack = [enc.word(x) for x in state.mstate.stack]
     mem = {}
     if state.mstate.memory.symbolic:

@@ -31,14 +31,18 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret")
 
 # synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
 # SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
 # storage:  MSTORE(x, CALLER); h = SHA3(x, 64); if !storage[h]: storage[h] = 1;
 # y = calldata[36:68]; if y: MSTORE8(x, y); if MLOAD(x): storage[0] = SHA3(x, 33)
 SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f578083535b"
-                        "825180602757005b6021842060005500"}
+                        "825180602757005b6021842060005500",
+         # b = SELFBALANCE; if b == 0: RETURN(0, b); x = calldata[0:32];
+         # if b < x: REVERT(0, x); if x & 1: RETURN(x, 32); REVERT(x, 4) -- halts of a
+         # symbolic length or offset (instructions.py:1858-1934)
+         "selfbalance_ret": "478015602457600035808210601f5780600116601a57600481fd5b602081f35b806000fd5b806000f3"}
 
 
 def deploy(device, name):

@@ -359,8 +359,8 @@ class Engine:
         tx = s.current_transaction
         if op == 0xF3 and isinstance(tx, ContractCreationTransaction):
             raise Unsupported("a creation returning code at a symbolic range")
-        if op == 0xF3 and ms.min_gas_used >= _gas_limit(s):
-            return self._vmexc(state)
+        if op == 0xF3 and _val(length) is not None and ms.min_gas_used >= min(_gas_limit(s), 10 ** 9 + 1):
+            return self._vmexc(state)      # mem_extend + check_gas_usage_limit (:1869-1870)
         if self.signals:
             tx.end(s, return_data=None, revert=op == 0xFD)
         self.ended.append(("revert" if op == 0xFD else "return", s))

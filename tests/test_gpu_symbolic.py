@@ -124,7 +124,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                 queue.extend(t for t in mine if sym.lane_eligible(t))
             elif st == MG_ESCAPE:
                 assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
-    assert forks >= 3 and device_steps > (50 if name in symcases.SYNTH else 100) and checked > forks
+    assert forks >= 3 and device_steps > (20 if name in symcases.SYNTH else 100) and checked > forks
     if name == "flag_array.sol.o":
         # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
         assert sym_exp > 0
@@ -139,19 +139,20 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
 
 
 # what a symbolic lane still hands to the host: the call family and SELFDESTRUCT
-# (the reference's world-state transitions), a symbolic jump target, the
-# symbolic balance array's reads, and what follows a call that returned symbolic
-# data (RETURNDATASIZE / RETURNDATACOPY of it, RETURN / REVERT of a symbolic
-# length, which names fresh return-data variables, instructions.py:1858-1930)
+# (the reference's world-state transitions), a symbolic jump target, and BALANCE
+# of another account (an If chain over the world state's accounts, instructions.py:
+# 907-931).  RETURN / REVERT of a symbolic range, SELFBALANCE, RETURNDATASIZE of a
+# host CALL's symbolic size and RETURNDATACOPY of a symbolic operand run on the
+# device (ABI v14).
 HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT",
-            "JUMP", "JUMPI", "BALANCE", "SELFBALANCE", "RETURNDATASIZE", "RETURNDATACOPY", "RETURN", "REVERT"}
+            "JUMP", "JUMPI", "BALANCE"}
 
 
 @pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
 def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
-    assert laser.forks >= 3 and laser.lane_steps > (50 if name in symcases.SYNTH else 100)
+    assert laser.forks >= 3 and laser.lane_steps > (20 if name in symcases.SYNTH else 100)
     # CALLDATACOPY of a symbolic size, memory offset or calldata offset, and MLOAD /
     # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
     # its free-memory pointer by a symbolic length) run on the device; what

@@ -152,7 +152,7 @@ def test_jumpi_successors_follow_the_reference():
 @pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
 def test_symbolic_call_outcomes_equal_the_restatement(name, monkeypatch):
     got, want, laser = symcases.run_both(OracleDevice(), name, monkeypatch)
-    assert sum(want.values()) >= 7
+    assert sum(want.values()) >= (5 if name in symcases.SYNTH else 7)
     assert got == want
 
 
@@ -429,3 +429,44 @@ def data_at(mem, x, n):
     """simplify(Concat(memory[x:x+n])) as sha3_ builds it (instructions.py:1036-1045)."""
     from mythril_amd.smt.expr import simplify_concat
     return simplify_concat([b if isinstance(b, BitVec) else BVV(b, 8) for b in mem[x: x + BVV(n, 256)]])
+
+
+def test_selfbalance_node_and_symbolic_return_range():
+    """selfbalance_ (instructions.py:968-976): a lane whose active account's
+    balance is symbolic carries MG_LANE_SYMBAL, and the device's MG_SYM_ENV node
+    with w = MG_ENV_SELFBALANCE decodes to environment.active_account.balance()
+    with no provenance (a later re-encode keeps the term itself).  A RETURN /
+    REVERT of a symbolic range halts with ret_len = MG_RET_SYMBOLIC: no return
+    data bytes (tests/symref.py ends such a transaction with return_data=None)."""
+    from mythril_amd.lanes import MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_RET_SYMBOLIC, MG_SYM_ENV
+    s = _run_restatement("47" "00", 1)                                 # SELFBALANCE STOP
+    bal = s.environment.active_account.balance()
+    assert bal.symbolic and s.mstate.stack[-1].raw is bal.raw
+    le = sym.encode_state(s)
+    assert le.flags & MG_LANE_SYMBAL
+    c = _batch()
+    c.node[0, 0] = (MG_SYM_ENV | 256 << 8, 0, 0, MG_ENV_SELFBALANCE)
+    c.n_nodes[0] = 1
+    assert sym._Decoder(c, 0, s).node(0).raw is bal.raw
+    assert sym._PROV.get(bal.raw) is None or sym._PROV[bal.raw][0] != MG_SYM_ENV
+    c.ret_offset[0], c.ret_len[0] = 0, MG_RET_SYMBOLIC
+    assert c.return_data(0) is None
+    c.ret_len[0] = 2
+    assert c.return_data(0) == b"\x00\x00"
+
+
+def test_returndatasize_node_decodes_to_the_last_return_data_size():
+    """returndatasize_ (instructions.py:1359-1370) after a host CALL that left a
+    symbolic size: the lane carries MG_LANE_SYMRDS and the device's MG_SYM_ENV node
+    (w = MG_ENV_RETURNDATASIZE) decodes to last_return_data.size."""
+    from mythril_amd.lanes import MG_ENV_RETURNDATASIZE, MG_LANE_SYMRDS, MG_SYM_ENV
+    s = _run_restatement("6000" "35" "00", 2)                           # a symbolic lane
+    rds = s.new_bitvec("returndatasize", 256)
+    s.last_return_data = symref.ReturnData([], rds)
+    assert sym.encode_state(s).flags & MG_LANE_SYMRDS
+    c = _batch()
+    c.node[0, 0] = (MG_SYM_ENV | 256 << 8, 0, 0, MG_ENV_RETURNDATASIZE)
+    c.n_nodes[0] = 1
+    assert sym._Decoder(c, 0, s).node(0).raw is rds.raw
+    s.last_return_data = None
+    assert not sym.encode_state(s).flags & MG_LANE_SYMRDS
