@@ -226,7 +226,7 @@ DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
 // signed ops and the overflow test share the second site
 DEV U256 bv_udivrem(bool quotient, const U256 &A, const U256 &B) {
     U256 q = u_ones(), r = A;                   // b == 0: bvudiv -> ones, bvurem -> a
-    if (!u_iszero(B)) u_divmod_nz(A, B, q, r);
+    if (!u_iszero(B)) u_divmod_nz_t<true>(A, B, q, r);
     return quotient ? q : r;
 }
 #define BV_DIV_OPS ((1ull << BV_SDIV) | (1ull << BV_SREM) | (1ull << BV_SMOD) | (1ull << BV_MUL_NOOVF_U))
@@ -246,7 +246,7 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
     if (op == BV_MUL_NOOVF_U) { keep = B; b = A; a = bv_mask(u_ones(), rc); }
     const bool bz = u_iszero(b);
     U256 q = u_ones(), r = a;                   // b == 0: q = ones, r = a
-    if (!bz) u_divmod_nz(a, b, q, r);
+    if (!bz) u_divmod_nz_t<true>(a, b, q, r);
     switch (op) {
     case BV_UDIV: return q;
     case BV_UREM: return r;

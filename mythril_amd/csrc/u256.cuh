@@ -304,7 +304,11 @@ DEV uint32_t mg_div21(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v, uint32_t
     return q1;
 }
 
-DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256 &r) {
+// SKIP (kernel 2): a quotient digit j is nonzero only when bitlen(a) - bitlen(b) >= 32 j (= dl),
+// so a digit no lane of the wave needs is skipped with a wave-uniform branch (a zero digit
+// leaves the remainder unchanged)
+template <bool SKIP>
+DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256 &r, int dl) {
     const uint32_t s = 256u - lb;                       // normalisation shift, < 256
     const U256 vn = u_shl_n(b, s);
     const U256 lo = u_shl_n(a, s);
@@ -319,6 +323,7 @@ DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256
     // a < 2^256 so the digit at 2^256 is 0: u[15..8] < vn and the loop starts at 7
 #pragma unroll
     for (int j = 7; j >= 0; --j) {
+        if (SKIP && __ballot(dl >= 32 * j) == 0ull) continue;   // q.w[j] stays 0
         const uint32_t u2 = u[j + 8], u1 = u[j + 7], u0 = u[j + 6];
         uint32_t qh, rh;
         bool rh_ovf;
@@ -371,7 +376,12 @@ DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256
     r = u_shr_n(rn, s, 0u);
 }
 
-DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) {
+// KNUTH_ALL (kernel 2's division sites): Knuth D with zero digits skipped for every
+// quotient length, instead of the shift-subtract loop below 32 quotient bits -- one
+// estimated digit costs less than a few shift-subtract rounds (C4 190.96 -> 189.69 ms,
+// profiles/r04/divab/).  Kernel 1 keeps the round-3 form.
+template <bool KNUTH_ALL>
+DEV void u_divmod_nz_t(const U256 &a, const U256 &b, U256 &q, U256 &r) {
     const uint32_t lb = u_bitlen(b), la = u_bitlen(a);
     if (u_popcount(b) == 1u) {
         const uint32_t k = lb - 1u;
@@ -379,8 +389,8 @@ DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) {
         r = u_and(a, u_sub(b, u_small(1)));
         return;
     }
-    if (__ballot(la >= lb + 32u) != 0ull) {            // some lane needs > 32 quotient bits
-        u_divmod_knuth(a, b, lb, q, r);
+    if (KNUTH_ALL ? __ballot(la >= lb) != 0ull : __ballot(la >= lb + 32u) != 0ull) {
+        u_divmod_knuth<KNUTH_ALL>(a, b, lb, q, r, (int)la - (int)lb);   // some lane needs the long form
         return;
     }
     q = u_zero();
@@ -401,6 +411,7 @@ DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) {
         bs.w[7] >>= 1;
     }
 }
+DEV void u_divmod_nz(const U256 &a, const U256 &b, U256 &q, U256 &r) { u_divmod_nz_t<false>(a, b, q, r); }
 DEV U256 z_udiv(const U256 &a, const U256 &b) {
     if (u_iszero(b)) return u_ones();
     U256 q, r;
