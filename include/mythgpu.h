@@ -51,7 +51,8 @@ extern "C" {
                                   REVERT of a symbolic range (MG_RET_SYMBOLIC),
                                   SELFBALANCE on MG_LANE_SYMBAL lanes, RETURNDATASIZE
                                   on MG_LANE_SYMRDS lanes, RETURNDATACOPY of a
-                                  symbolic operand (pops only) */
+                                  symbolic operand (pops only), BALANCE on
+                                  MG_LANE_BALANCE lanes (MG_SYM_BALANCE) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -183,6 +184,9 @@ extern "C" {
                                  size (a host CALL's returndatasize variable):
                                  RETURNDATASIZE pushes an MG_SYM_ENV node
                                  (w = MG_ENV_RETURNDATASIZE, instructions.py:1359-1370) */
+#define MG_LANE_BALANCE 131072u /* symbolic lane of a LaserEVM with no dynamic loader: BALANCE
+                                   pushes an MG_SYM_BALANCE node (the world state's accounts
+                                   cannot change inside a device run)                    */
 #define MG_ENV_ADDRESS   0
 #define MG_ENV_CALLER    1
 #define MG_ENV_ORIGIN    2
@@ -302,6 +306,10 @@ typedef struct mg_ctx mg_ctx;
                               before this node build: w = 0, memory.get_word_at(y) (MLOAD,
                               instructions.py:1439-1451); w = n > 0, simplify(Concat(memory[y :
                               y + n])) (the data of a SHA3, instructions.py:1014-1051)     */
+#define MG_SYM_BALANCE 16u /* BALANCE of the address ref y (balance_, instructions.py:907-931,
+                              no dynamic loader): the account's balance() when y is a known
+                              concrete address, else the If chain over the world state's
+                              accounts; on MG_LANE_BALANCE lanes                           */
 #define MG_SYM_CONST  0x80000000u
 #define MG_FORK      11u  /* status: JUMPI on a symbolic condition; the lane holds
                              the state at the start of the JUMPI (host forks)    */

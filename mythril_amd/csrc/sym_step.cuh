@@ -76,6 +76,7 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define LANE_MEMTAG 8192u
 #define LANE_SYMBAL 32768u
 #define LANE_SYMRDS 65536u
+#define LANE_BALANCE 131072u
 #define SYM_SLOAD 6u
 #define SYM_KECCAK 7u
 #define SYM_EXTRACT 8u
@@ -86,6 +87,7 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define SYM_CDBYTEX 13u
 #define SYM_MSTOREK 14u
 #define SYM_MLOADK 15u
+#define SYM_BALANCE 16u
 
 DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
 DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
@@ -443,7 +445,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         if (executed >= lane_max) break;
         const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
-        if (((uy & PD_SPECIAL) && !(op == 0x47u && (flags & LANE_SYMBAL) && !tl)) ||
+        if (((uy & PD_SPECIAL) &&
+             !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE))) && !tl)) ||
             (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
@@ -872,6 +875,30 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             V.set_stack(sp, u_zero());
             sym_set_tag(S, N, lane, sp, rtag);
             ++sp; ++pc; gmin = ngmin; gmax = ngmax; nn = lnn;
+            ++executed;
+            continue;
+        }
+
+        if (op == 0x31u) {   // (only on MG_LANE_BALANCE lanes; taint lanes escaped above)
+            // BALANCE (balance_, instructions.py:907-931) with no dynamic loader: the
+            // account's balance() for a known concrete address, else If(address ==
+            // account.address, account.balance(), ...) over the world state's accounts.
+            // A BALANCE node over the address; the host builds the term from the lane's
+            // world state, which no device instruction changes.
+            if (sp < 1u) { status = ST_ESCAPE; aux = op | (ESC_SYMBOLIC << 8); break; }   // the host's underflow
+            const U256 a = V.stack(sp - 1u);
+            const uint32_t ta = sym_tag(S, N, lane, sp - 1u);
+            if (ta && sym_width(S, N, lane, ta) == 1u) { status = ST_ESCAPE; aux = op | (ESC_SYMBOLIC << 8); break; }
+            const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
+            uint32_t lnn = nn, lnc = nc, ya = 0u, rtag = 0u;
+            if (!sym_ref(S, N, lane, ta, a, lnc, ya) ||
+                !sym_node_push(S, N, lane, SYM_BALANCE | (256u << 8), ya, 0u, 0u, lnn, rtag)) {
+                status = ST_ESCAPE; aux = op | (ESC_ARENA << 8); break;
+            }
+            if (ngmin >= glim) { ++executed; status = ST_VMEXC; aux = EXC_OOG; break; }
+            V.set_stack(sp - 1u, u_zero());
+            sym_set_tag(S, N, lane, sp - 1u, rtag);
+            ++pc; gmin = ngmin; gmax = ngmax; nn = lnn; nc = lnc;
             ++executed;
             continue;
         }

@@ -52,8 +52,9 @@ MG_SYM_CDBYTE = 12      # calldata[w]: one byte of a symbolic calldata copy
 MG_SYM_CDBYTEX = 13     # calldata[simplify(y + w)]: a copy from a symbolic calldata offset
 MG_SYM_MSTOREK = 14     # event: write of value ref z at symbolic offset y (w: 1 word, 2 low byte, 3 byte)
 MG_SYM_MLOADK = 15      # get_word_at(y) over the byte map of the events before it
+MG_SYM_BALANCE = 16     # balance_ of the address ref y over the world state's accounts
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
-MG_LANE_SYMBAL, MG_LANE_SYMRDS = 32768, 65536
+MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_LANE_BALANCE = 32768, 65536, 131072
 MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE = 5, 6
 MG_LANE_RETDATA = 16384
 MG_SYM_CONST = 0x80000000

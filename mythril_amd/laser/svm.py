@@ -50,7 +50,7 @@ import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
                      MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_ESC_ARENA,
-                     MG_ESC_TAINT, MG_FORK, MG_LANE_SYMBOLIC, MG_LANE_TAINT,
+                     MG_ESC_TAINT, MG_FORK, MG_LANE_BALANCE, MG_LANE_SYMBOLIC, MG_LANE_TAINT,
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
@@ -687,6 +687,8 @@ class LaserEVM:
                 le = sym.encode_state(s, b.shape.node_cap, b.shape.const_cap)
             if le.symbolic:
                 sflags = le.flags
+                if self.dynamic_loader is None:
+                    sflags |= MG_LANE_BALANCE        # BALANCE as an arena node (balance_ needs no loader)
             else:
                 le = None
         # the terms behind the lane's first arena nodes, for _materialise's decode

@@ -39,7 +39,7 @@ from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
                      MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
                      MG_SYM_MLOADK, MG_SYM_MSTOREK,
-                     MG_ENV_RETURNDATASIZE, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_ENV_RETURNDATASIZE, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_BALANCE, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
                         URem, SRem, _select, simplify_concat, symbol_factory)
@@ -189,6 +189,21 @@ def source(kind: int, imm: int, arg, state):
     raise NotEncodable(f"unknown source kind {kind}")
 
 
+def balance_of(state, address):
+    """balance_ (instructions.py:907-931) with no dynamic loader: a known concrete
+    address gives its account's balance(); otherwise (symbolic, or a concrete
+    address accounts_exist_or_load cannot load) the If chain over the world
+    state's accounts, in their order."""
+    ws = state.world_state
+    v = address.value
+    if v is not None and v in ws.accounts:
+        return ws.accounts[v].balance()
+    bal = symbol_factory.BitVecVal(0, 256)
+    for a in ws.accounts.values():
+        bal = If(address == a.address, a.balance(), bal)
+    return bal
+
+
 # ----------------------------------------------------------- decode / encode
 class _Decoder:
     """The expressions of one lane's planes: its stack words, memory bytes and
@@ -258,6 +273,8 @@ class _Decoder:
         if kind == MG_SYM_CDLOAD:
             a = self.ref(y)
             return _mark(source(kind, w, a, self.state), kind, w, (a,))
+        if kind == MG_SYM_BALANCE:
+            return balance_of(self.state, as_bitvec(self.ref(y)))    # no provenance, as below
         if kind == MG_SYM_ENV and w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE):
             # no provenance: the balance and the return data change across host
             # CALLs, so a re-encoded term rides as itself, not as "the value now"

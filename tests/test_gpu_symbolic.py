@@ -139,13 +139,12 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
 
 
 # what a symbolic lane still hands to the host: the call family and SELFDESTRUCT
-# (the reference's world-state transitions), a symbolic jump target, and BALANCE
-# of another account (an If chain over the world state's accounts, instructions.py:
-# 907-931).  RETURN / REVERT of a symbolic range, SELFBALANCE, RETURNDATASIZE of a
-# host CALL's symbolic size and RETURNDATACOPY of a symbolic operand run on the
-# device (ABI v14).
+# (the reference's world-state transitions) and a symbolic jump target.  RETURN /
+# REVERT of a symbolic range, SELFBALANCE, BALANCE (no dynamic loader),
+# RETURNDATASIZE of a host CALL's symbolic size and RETURNDATACOPY of a symbolic
+# operand run on the device (ABI v14).
 HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT",
-            "JUMP", "JUMPI", "BALANCE"}
+            "JUMP", "JUMPI"}
 
 
 @pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))

@@ -470,3 +470,23 @@ def test_returndatasize_node_decodes_to_the_last_return_data_size():
     assert sym._Decoder(c, 0, s).node(0).raw is rds.raw
     s.last_return_data = None
     assert not sym.encode_state(s).flags & MG_LANE_SYMRDS
+
+
+def test_balance_node_decodes_like_balance_():
+    """balance_ (instructions.py:907-931) with no dynamic loader: the device's
+    MG_SYM_BALANCE node over a known concrete address decodes to that account's
+    balance(), over a symbolic or unknown address to the If chain over the world
+    state's accounts -- the restatement's value for the same instruction."""
+    from mythril_amd.lanes import MG_SYM_BALANCE
+    s = _run_restatement("30" "31" "6000" "35" "31" "611234" "31" "00", 7)
+    want = [x.raw for x in s.mstate.stack]
+    c = _batch()
+    c.node[0, 0] = (MG_SYM_CDLOAD | 256 << 8, MG_SYM_CONST | 1, 0, 0)
+    c.node[0, 1] = (MG_SYM_BALANCE | 256 << 8, MG_SYM_CONST | 0, 0, 0)
+    c.node[0, 2] = (MG_SYM_BALANCE | 256 << 8, 0, 0, 0)
+    c.node[0, 3] = (MG_SYM_BALANCE | 256 << 8, MG_SYM_CONST | 2, 0, 0)
+    for k, v in enumerate((workloads.CONTRACT, 0, 0x1234)):
+        c.cval[0, k] = word_to_limbs(v)
+    c.n_nodes[0], c.n_consts[0] = 4, 3
+    dec = sym._Decoder(c, 0, s)
+    assert [dec.node(k).raw for k in (1, 2, 3)] == want
