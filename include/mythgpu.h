@@ -52,7 +52,9 @@ extern "C" {
                                   SELFBALANCE on MG_LANE_SYMBAL lanes, RETURNDATASIZE
                                   on MG_LANE_SYMRDS lanes, RETURNDATACOPY of a
                                   symbolic operand (pops only), BALANCE on
-                                  MG_LANE_BALANCE lanes (MG_SYM_BALANCE) */
+                                  MG_LANE_BALANCE lanes (MG_SYM_BALANCE), symbolic
+                                  jump targets (JUMP: VmException, JUMPI: falls
+                                  through) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0

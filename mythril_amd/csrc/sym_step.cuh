@@ -903,6 +903,18 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
+        if (any_sym && !tl && (kind == K_JUMP || (kind == K_JUMPI && sp >= 2u)) && sp >= 1u &&
+            sym_tag(S, N, lane, sp - 1u)) {
+            // a symbolic jump target: JUMP raises InvalidJumpDestination (jump_,
+            // instructions.py:1529-1532), a VmException at the instruction's start;
+            // JUMPI pops both words and falls through with its gas by hand and no
+            // depth step ("Skipping JUMPI to invalid destination", :1572-1579)
+            ++executed;
+            if (kind == K_JUMP) { status = ST_VMEXC; aux = EXC_BADJUMP; break; }
+            sp -= 2u; ++pc; gmin += 10u; gmax += 10u;
+            continue;
+        }
+
         if (op == 0x3eu && any_sym && !tl && sp >= 3u) {
             // RETURNDATACOPY with a symbolic memory offset, return offset or size
             // (returndatacopy_, instructions.py:1314-1343): the three words are popped

@@ -31,7 +31,7 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump")
 
 # synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
 # SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
@@ -45,7 +45,10 @@ SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f5
          "selfbalance_ret": "478015602457600035808210601f5780600116601a57600481fd5b602081f35b806000fd5b806000f3",
          # BALANCE (instructions.py:907-931) of the contract's own address, of calldata[0:32],
          # of CALLER and of an unknown concrete address, each feeding a JUMPI
-         "balance_of": "303160003531818111600d57005b333115601557005b61123431601e57005b00"}
+         "balance_of": "303160003531818111600d57005b333115601557005b61123431601e57005b00",
+         # symbolic jump targets: JUMPI(x, x) falls through (instructions.py:1572-1579),
+         # JUMP(x) raises InvalidJumpDestination (:1529-1532)
+         "symjump": "600035806001166019578080576001600055602035602357005b801560215780565b005b00"}
 
 
 def deploy(device, name):

@@ -409,8 +409,16 @@ class Engine:
         if op == 0x57:                                          # JUMPI
             target, cond = st[-1], st[-2]
             if _val(target) is None:
-                raise Unsupported("symbolic jump target")
+                # jumpi_ (instructions.py:1572-1579): "Skipping JUMPI to invalid
+                # destination" -- both words popped, pc + 1, the JUMPI gas by hand
+                st.pop(), st.pop()
+                ms.pc += 1
+                ms.min_gas_used += gmin
+                ms.max_gas_used += gmax
+                return [s]
             return self._jumpi(s, _val(target), cond)
+        if op == 0x56 and _val(st[-1]) is None:
+            return self._vmexc(state)     # jump_ (:1529-1532): InvalidJumpDestination
         if op == 0x37 or op not in _SYM_OK and not sym_env and op not in (0x35, 0x36, 0x0A):
             raise Unsupported(f"{name} with symbolic inputs")
         cond_after = None

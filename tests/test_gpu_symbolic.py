@@ -139,12 +139,11 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
 
 
 # what a symbolic lane still hands to the host: the call family and SELFDESTRUCT
-# (the reference's world-state transitions) and a symbolic jump target.  RETURN /
-# REVERT of a symbolic range, SELFBALANCE, BALANCE (no dynamic loader),
-# RETURNDATASIZE of a host CALL's symbolic size and RETURNDATACOPY of a symbolic
-# operand run on the device (ABI v14).
-HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT",
-            "JUMP", "JUMPI"}
+# (the reference's world-state transitions).  RETURN / REVERT of a symbolic range,
+# SELFBALANCE, BALANCE (no dynamic loader), RETURNDATASIZE of a host CALL's
+# symbolic size, RETURNDATACOPY of a symbolic operand and symbolic jump targets run
+# on the device (ABI v14).
+HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT"}
 
 
 @pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
