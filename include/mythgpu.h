@@ -54,7 +54,7 @@ extern "C" {
                                   symbolic operand (pops only), BALANCE on
                                   MG_LANE_BALANCE lanes (MG_SYM_BALANCE), symbolic
                                   jump targets (JUMP: VmException, JUMPI: falls
-                                  through) */
+                                  through), SHA3 of a symbolic length (MG_REC_SYMLEN) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -150,6 +150,11 @@ extern "C" {
  *                  Power(base, exponent); the host appends exponent_function_manager's
  *                  condition for (base, exponent) to the path.  len = 0.            */
 #define MG_REC_SYMEXP   7u
+/*   MG_REC_SYMLEN  SHA3 with a symbolic length (symbolic lanes, sha3_, instructions.py:
+ *                  1023-1028): the length is taken as 64 and the host appends
+ *                  `length == 64` to the path's constraints; len = 64, payload = the
+ *                  length's arena node.  Precedes the SHA3's MG_REC_SYMKECCAK.      */
+#define MG_REC_SYMLEN   8u
 #define MG_REC_HEADER   11u  /* kind, len, step, 8 result limbs                */
 
 /* lane flags */

@@ -809,16 +809,31 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                             for (uint32_t j = 0; j < (m8 ? 1u : 32u); ++j) set_mtag(S, N, lane, off + j, 0u);
                     }
                 } else {  // K_SHA3 over symbolic bytes: keccak256_<8 len>(data), create_keccak
-                    if (tb) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))   // symbolic length
                     if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
-                    const uint32_t len = b.w[0];
+                    // a symbolic length is taken as 64 with `length == 64` appended to the
+                    // path (instructions.py:1023-1028, an MG_REC_SYMLEN record before the
+                    // SHA3's own); only over a range holding a symbolic byte, so the data
+                    // (and the hash) stay symbolic as in the reference
+                    if (tb && (sym_width(S, N, lane, tb) == 1u || !u_fits32(a) ||
+                               !((lflags & LANE_MEMTAG) && mtag_any(S, N, lane, a.w[0], 64u, msize))))
+                        MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
+                    const uint32_t len = tb ? 64u : b.w[0];
                     if (!L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                     const uint64_t g = 30ull + 6ull * (((uint64_t)len + 31ull) >> 5);
                     ngmin += g; ngmax += g;
-                    if (ngmin >= glim) MSTOPX(ST_VMEXC, EXC_OOG)
-                    MMEMX(a, b, -1)
-                    const uint32_t rec_at = L.rec_len[lane];
-                    if ((uint64_t)rec_at + MG_REC_HEADER + 1u > L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_RECORD << 8))
+                    // the reference has appended the length constraint before this check:
+                    // an out-of-gas SHA3 of a symbolic length is the host's
+                    if (ngmin >= glim) MSTOPX(tb ? ST_ESCAPE : ST_VMEXC, tb ? op | (ESC_SYMBOLIC << 8) : EXC_OOG)
+                    MMEMX(a, u_small(len), -1)
+                    uint32_t rec_at = L.rec_len[lane];
+                    const uint32_t rec_need = (tb ? MG_REC_HEADER + 1u : 0u) + MG_REC_HEADER + 1u;
+                    if ((uint64_t)rec_at + rec_need > L.rec_cap) MSTOPX(ST_ESCAPE, op | (ESC_RECORD << 8))
+                    if (tb) {
+                        const uint32_t at = rec_head(L, lane, rec_at, MG_REC_SYMLEN, 64u, L.steps[lane] + executed,
+                                                     u_zero());
+                        L.rec[(size_t)at * N + lane] = tb - 1u;
+                        rec_at = at + 1u;
+                    }
                     if (nmsize > msize) V.mzero(msize, nmsize);
                     MPUSHCHK()
                     uint32_t r;

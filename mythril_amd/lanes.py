@@ -42,6 +42,7 @@ MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4
 MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
 MG_REC_CDSIZE = 6       # a creation's CODESIZE: the host appends calldata.size == result
 MG_REC_SYMEXP = 7       # EXP with a symbolic operand: payload = the Power node's index
+MG_REC_SYMLEN = 8       # SHA3 of a symbolic length: payload = the length's node; host appends len == 64
 MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
@@ -380,6 +381,10 @@ class LaneBatch:
             elif kind == MG_REC_SYMEXP:
                 # (step, "symexp", Power node index)
                 out.append((step, "symexp", int(q[k])))
+                k += 1
+            elif kind == MG_REC_SYMLEN:
+                # (step, "symlen", the length's node index, 64)
+                out.append((step, "symlen", int(q[k]), ln))
                 k += 1
             elif kind == MG_REC_CDSIZE:
                 # (step, "cdsize", the CODESIZE value pushed)

@@ -796,6 +796,8 @@ class LaserEVM:
                     r = (r[0], "symkeccak", sym.keccak_input(b, i, self._rec_lanes[i].state, r[2]))
                 elif r[1] == "symexp":
                     r = (r[0], "symexp", sym.exp_operands(b, i, self._rec_lanes[i].state, r[2]))
+                elif r[1] == "symlen":
+                    r = (r[0], "symlen", sym.decode_node(b, i, self._rec_lanes[i].state, r[2]), r[3])
                 key = (r[0], i) if self._rec_bfs else (-i, r[0])
                 heapq.heappush(self._recq, (key, next(self._rec_seq), i, r))
             b.rec_seen[i] = end
@@ -822,6 +824,9 @@ class LaserEVM:
                 # condition on Power(base, exponent)
                 _, cond = exponent_function_manager.create_condition(*r[2])
                 lanes[i].state.world_state.constraints.append(cond)
+            elif r[1] == "symlen":
+                # sha3_ of a symbolic length (instructions.py:1023-1028): length 64
+                lanes[i].state.world_state.constraints.append(r[2] == r[3])
             elif r[1] == "cdsize":
                 # codesize_ of a creation (instructions.py:989-997): the symbolic
                 # calldata's size is pinned to the pushed value

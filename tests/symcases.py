@@ -31,7 +31,7 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump", "symlen_sha3")
 
 # synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
 # SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
@@ -48,7 +48,10 @@ SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f5
          "balance_of": "303160003531818111600d57005b333115601557005b61123431601e57005b00",
          # symbolic jump targets: JUMPI(x, x) falls through (instructions.py:1572-1579),
          # JUMP(x) raises InvalidJumpDestination (:1529-1532)
-         "symjump": "600035806001166019578080576001600055602035602357005b801560215780565b005b00"}
+         "symjump": "600035806001166019578080576001600055602035602357005b801560215780565b005b00",
+         # SHA3 of a symbolic length over symbolic memory: length 64 and `n == 64` on the path
+         # (instructions.py:1023-1028)
+         "symlen_sha3": "600035806000526020356000205460165780602857005b6040356010206000558015602657005b005b00"}
 
 
 def deploy(device, name):

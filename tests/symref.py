@@ -265,7 +265,7 @@ class Engine:
                 raise Unsupported("symbolic SHA3 offset and length")
             return self._symbolic_sha3(state if state is not None else s, s)
         if op == 0x20 and _val(st[-2]) is None:
-            raise Unsupported("symbolic SHA3 length")
+            return self._symbolic_length_sha3(state if state is not None else s, s)
         b = self._oracle_run(s)
         if int(b.status[0]) != MG_RUNNING:
             return self._ended(s, b)
@@ -323,6 +323,31 @@ class Engine:
             st.append(keccak_function_manager.get_empty_keccak_hash())
             ms.pc += 1
             return [s]
+        st.append(keccak_function_manager.create_keccak(data))
+        ms.pc += 1
+        return [s]
+
+    def _symbolic_length_sha3(self, state, s):
+        """sha3_ (instructions.py:1014-1051) of a symbolic length at a concrete
+        offset: the length is taken as 64 and `length == 64` appended to the path
+        before the SHA3 gas; then mem_extend and the hash of memory[index:+64]."""
+        ms = s.mstate
+        st = ms.stack
+        index, op1 = st.pop(), st.pop()
+        if _val(index) is None or isinstance(op1, Bool):
+            raise Unsupported("SHA3 of a symbolic offset and length, or of a Bool length")
+        s.world_state.constraints.append(op1 == 64)
+        g = 30 + 6 * 2
+        if ms.min_gas_used + g >= min(_gas_limit(s), 10 ** 9 + 1):
+            raise Unsupported("an out-of-gas SHA3 of a symbolic length")
+        ms.min_gas_used += g
+        ms.max_gas_used += g
+        try:
+            ms.mem_extend(index, BVV(64, 256))
+        except VmException:
+            return self._vmexc(state)
+        data = simplify_concat([x if isinstance(x, BitVec) else BVV(x, 8)
+                                for x in ms.memory[_val(index): _val(index) + 64]])
         st.append(keccak_function_manager.create_keccak(data))
         ms.pc += 1
         return [s]

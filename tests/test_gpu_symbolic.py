@@ -85,6 +85,8 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                     _, cond = exponent_function_manager.create_condition(
                         symbol_factory.BitVecVal(r[2], 256), symbol_factory.BitVecVal(r[3], 256))
                     got.world_state.constraints.append(cond)
+                elif r[1] == "symlen":          # sha3_ of a symbolic length (:1023-1028)
+                    got.world_state.constraints.append(sym.decode_node(b, i, got, r[2]) == r[3])
             # the restatement: the same state, the same number of instructions (a
             # halt or VmException counts as a step but leaves the state at its start)
             ref = s0
@@ -133,6 +135,9 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
         # SHA3 of symbolic memory), read and write the symbolic storage and halt
         # on the device
         assert sym_sha3 > 0 and halts_past_sha3 > 0, (sym_sha3, halts_past_sha3)
+    if name == "symlen_sha3":
+        # SHA3 of a symbolic length: the record that pins it to 64 precedes its keccak
+        assert sym_sha3 > 0, sym_sha3
     if name == "symkey_sha3":
         # SHA3 over memory at a symbolic offset: an MLOADK range node under KECCAK
         assert sym_sha3 > 0 and halts_past_sha3 > 0, (sym_sha3, halts_past_sha3)

@@ -490,3 +490,19 @@ def test_balance_node_decodes_like_balance_():
     c.n_nodes[0], c.n_consts[0] = 4, 3
     dec = sym._Decoder(c, 0, s)
     assert [dec.node(k).raw for k in (1, 2, 3)] == want
+
+
+def test_symlen_record_parses_and_restates_sha3_of_a_symbolic_length():
+    """MG_REC_SYMLEN (sha3_ of a symbolic length, instructions.py:1023-1028): the
+    record parses to (step, "symlen", node, 64), and the restatement takes the
+    length as 64 with `n == 64` appended before the hash of memory[index:+64]."""
+    from mythril_amd.lanes import MG_REC_HEADER, MG_REC_SYMLEN
+    b = LaneBatch(LaneShape(n=1, stack_cap=16, rec_cap=64))
+    b.rec[0, :MG_REC_HEADER + 1] = [MG_REC_SYMLEN, 64, 3] + [0] * 8 + [5]
+    b.rec_len[0] = MG_REC_HEADER + 1
+    assert b.records(0) == [(3, "symlen", 5, 64)]
+    # x = CALLDATALOAD(0); MSTORE(0, x); SHA3(0, CALLDATALOAD(32)); STOP
+    s = _run_restatement("6000" "35" "80" "6000" "52" "6020" "35" "6000" "20" "00", 9)
+    n = s.environment.calldata.get_word_at(BVV(32, 256))
+    assert s.world_state.constraints[-1].raw is (n == 64).raw
+    assert s.mstate.stack[-1].symbolic and len(s.mstate.memory) == 64
