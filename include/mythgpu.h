@@ -54,7 +54,8 @@ extern "C" {
                                   symbolic operand (pops only), BALANCE on
                                   MG_LANE_BALANCE lanes (MG_SYM_BALANCE), symbolic
                                   jump targets (JUMP: VmException, JUMPI: falls
-                                  through), SHA3 of a symbolic length (MG_REC_SYMLEN) */
+                                  through), SHA3 of a symbolic length (MG_REC_SYMLEN),
+                                  GAS on symbolic lanes (MG_ENV_GAS) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -202,6 +203,7 @@ extern "C" {
 #define MG_ENV_WORDS     5
 #define MG_ENV_SELFBALANCE 5  /* MG_SYM_ENV immediate only: environment.active_account.balance() */
 #define MG_ENV_RETURNDATASIZE 6 /* MG_SYM_ENV immediate only: last_return_data.size */
+#define MG_ENV_GAS 7           /* MG_SYM_ENV immediate only: new_bitvec("gas", 256) (gas_, instructions.py:1700-1709) */
 
 #define MG_STACK_LIMIT 1024u              /* MachineStack.STACK_LIMIT           */
 #define MG_MSTATE_GAS_LIMIT 1000000000ull /* GlobalState default gas_limit      */

@@ -446,7 +446,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
         if (((uy & PD_SPECIAL) &&
-             !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE))) && !tl)) ||
+             !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE)) ||
+                (op == 0x5au && symlane)) && !tl)) ||
             (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
@@ -870,7 +871,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (op == 0x47u || (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
+        if (op == 0x47u || op == 0x5au || (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
             // SELFBALANCE on a lane whose balance is symbolic (selfbalance_,
             // instructions.py:968-976; taint lanes escaped above):
             // environment.active_account.balance(), the balances array at the active
@@ -878,7 +879,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             // (returndatasize_, :1359-1370): last_return_data.size.  ENV nodes the
             // host decodes.  No host CALL runs inside a device run, so neither value
             // can move under it.
-            const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : MG_ENV_RETURNDATASIZE;
+            // GAS on a symbolic lane (gas_, :1700-1709): the transaction's fresh "gas"
+            // variable, new_bitvec("gas", 256)
+            const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : op == 0x5au ? MG_ENV_GAS : MG_ENV_RETURNDATASIZE;
             const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
             uint32_t lnn = nn, rtag = 0u;
             if (sp + 1u > STACK_LIMIT) { ++executed; status = ST_VMEXC; aux = EXC_OVERFLOW; break; }
@@ -941,14 +944,15 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (any_sym && !tl && (kind == K_RETURN || (kind == K_REVERT)) && sp >= 2u &&
+        if (any_sym && (!tl || !tact) && (kind == K_RETURN || (kind == K_REVERT)) && sp >= 2u &&
             !(creation && kind == K_RETURN)) {
             // ---- RETURN / REVERT with a symbolic offset or length (instructions.py:
             // 1858-1934): the transaction ends; the return data are fresh
             // "return_data" bytes or a slice at symbolic keys, left to the host
             // (MG_RET_SYMBOLIC).  RETURN of a concrete length runs mem_extend, which
             // returns on a symbolic start, then check_gas_usage_limit; a symbolic
-            // length skips both.  The lane stays at the instruction's start.
+            // length skips both.  The lane stays at the instruction's start.  A taint
+            // lane ends here too when its modules have no device action on the opcode.
             const uint32_t tlen = sym_tag(S, N, lane, sp - 2u);
             ++executed;
             if (kind == K_RETURN && !tlen && gmin >= glim) { status = ST_VMEXC; aux = EXC_OOG; break; }

@@ -56,7 +56,7 @@ MG_SYM_MLOADK = 15      # get_word_at(y) over the byte map of the events before 
 MG_SYM_BALANCE = 16     # balance_ of the address ref y over the world state's accounts
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
 MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_LANE_BALANCE = 32768, 65536, 131072
-MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE = 5, 6
+MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE, MG_ENV_GAS = 5, 6, 7
 MG_LANE_RETDATA = 16384
 MG_SYM_CONST = 0x80000000
 MG_LANE_TAINT = 2048

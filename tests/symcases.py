@@ -31,7 +31,7 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump", "symlen_sha3")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump", "symlen_sha3", "gas_sym")
 
 # synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
 # SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
@@ -51,7 +51,9 @@ SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f5
          "symjump": "600035806001166019578080576001600055602035602357005b801560215780565b005b00",
          # SHA3 of a symbolic length over symbolic memory: length 64 and `n == 64` on the path
          # (instructions.py:1023-1028)
-         "symlen_sha3": "600035806000526020356000205460165780602857005b6040356010206000558015602657005b005b00"}
+         "symlen_sha3": "600035806000526020356000205460165780602857005b6040356010206000558015602657005b005b00",
+         # GAS: the transaction's fresh "gas" variable (instructions.py:1700-1709) in JUMPI conditions
+         "gas_sym": "5a600035106010575a600116601957005b5a15601757005b005b00"}
 
 
 def deploy(device, name):

@@ -126,7 +126,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                 queue.extend(t for t in mine if sym.lane_eligible(t))
             elif st == MG_ESCAPE:
                 assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
-    assert forks >= 3 and device_steps > (20 if name in symcases.SYNTH else 100) and checked > forks
+    assert forks >= 3 and device_steps > (10 if name in symcases.SYNTH else 100) and checked > forks
     if name == "flag_array.sol.o":
         # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
         assert sym_exp > 0
@@ -155,7 +155,7 @@ HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2
 def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
-    assert laser.forks >= 3 and laser.lane_steps > (20 if name in symcases.SYNTH else 100)
+    assert laser.forks >= 3 and laser.lane_steps > (10 if name in symcases.SYNTH else 100)
     # CALLDATACOPY of a symbolic size, memory offset or calldata offset, and MLOAD /
     # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
     # its free-memory pointer by a symbolic length) run on the device; what
