@@ -55,7 +55,8 @@ extern "C" {
                                   MG_LANE_BALANCE lanes (MG_SYM_BALANCE), symbolic
                                   jump targets (JUMP: VmException, JUMPI: falls
                                   through), SHA3 of a symbolic length (MG_REC_SYMLEN),
-                                  GAS on symbolic lanes (MG_ENV_GAS) */
+                                  GAS / COINBASE / TIMESTAMP / DIFFICULTY on symbolic
+                                  lanes (MG_ENV_GAS..MG_ENV_DIFFICULTY) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -204,6 +205,9 @@ extern "C" {
 #define MG_ENV_SELFBALANCE 5  /* MG_SYM_ENV immediate only: environment.active_account.balance() */
 #define MG_ENV_RETURNDATASIZE 6 /* MG_SYM_ENV immediate only: last_return_data.size */
 #define MG_ENV_GAS 7           /* MG_SYM_ENV immediate only: new_bitvec("gas", 256) (gas_, instructions.py:1700-1709) */
+#define MG_ENV_COINBASE 8      /* ... new_bitvec("coinbase", 256) (coinbase_, :1386-1393)                      */
+#define MG_ENV_TIMESTAMP 9     /* ... new_bitvec("timestamp", 256) (timestamp_, :1396-1403)                    */
+#define MG_ENV_DIFFICULTY 10   /* ... new_bitvec("block_difficulty", 256) (difficulty_, :1416-1425)            */
 
 #define MG_STACK_LIMIT 1024u              /* MachineStack.STACK_LIMIT           */
 #define MG_MSTATE_GAS_LIMIT 1000000000ull /* GlobalState default gas_limit      */

@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
         if (((uy & PD_SPECIAL) &&
              !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE)) ||
-                (op == 0x5au && symlane)) && !tl)) ||
+                ((op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u) && symlane)) && !tl)) ||
             (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
@@ -871,7 +871,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (op == 0x47u || op == 0x5au || (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
+        if (op == 0x47u || op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u ||
+            (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
             // SELFBALANCE on a lane whose balance is symbolic (selfbalance_,
             // instructions.py:968-976; taint lanes escaped above):
             // environment.active_account.balance(), the balances array at the active
@@ -879,9 +880,11 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             // (returndatasize_, :1359-1370): last_return_data.size.  ENV nodes the
             // host decodes.  No host CALL runs inside a device run, so neither value
             // can move under it.
-            // GAS on a symbolic lane (gas_, :1700-1709): the transaction's fresh "gas"
-            // variable, new_bitvec("gas", 256)
-            const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : op == 0x5au ? MG_ENV_GAS : MG_ENV_RETURNDATASIZE;
+            // GAS, COINBASE, TIMESTAMP, DIFFICULTY on a symbolic lane (:1386-1425,
+            // 1700-1709): the transaction's fresh variable of that name, new_bitvec
+            const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : op == 0x5au ? MG_ENV_GAS :
+                                   op == 0x41u ? MG_ENV_COINBASE : op == 0x42u ? MG_ENV_TIMESTAMP :
+                                   op == 0x44u ? MG_ENV_DIFFICULTY : MG_ENV_RETURNDATASIZE;
             const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
             uint32_t lnn = nn, rtag = 0u;
             if (sp + 1u > STACK_LIMIT) { ++executed; status = ST_VMEXC; aux = EXC_OVERFLOW; break; }

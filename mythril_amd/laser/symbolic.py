@@ -39,7 +39,7 @@ from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
                      MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
                      MG_SYM_MLOADK, MG_SYM_MSTOREK,
-                     MG_ENV_GAS, MG_ENV_RETURNDATASIZE, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_BALANCE, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_ENV_COINBASE, MG_ENV_DIFFICULTY, MG_ENV_GAS, MG_ENV_RETURNDATASIZE, MG_ENV_TIMESTAMP, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_BALANCE, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
                         URem, SRem, _select, simplify_concat, symbol_factory)
@@ -174,6 +174,12 @@ def unary(op: int, a):
     raise NotEncodable(f"no symbolic semantics for opcode {op:#x}")
 
 
+# the opcodes that push the transaction's fresh variable of a name (instructions.py:
+# 1386-1425, 1700-1709): MG_SYM_ENV immediates
+_FRESH = {MG_ENV_GAS: "gas", MG_ENV_COINBASE: "coinbase", MG_ENV_TIMESTAMP: "timestamp",
+          MG_ENV_DIFFICULTY: "block_difficulty"}
+
+
 def source(kind: int, imm: int, arg, state):
     env = state.environment
     if kind == MG_SYM_CDLOAD:
@@ -185,8 +191,8 @@ def source(kind: int, imm: int, arg, state):
             return env.active_account.balance()
         if imm == MG_ENV_RETURNDATASIZE:        # returndatasize_ (instructions.py:1359-1370)
             return state.last_return_data.size
-        if imm == MG_ENV_GAS:                   # gas_ (instructions.py:1700-1709)
-            return state.new_bitvec("gas", 256)
+        if imm in _FRESH:                       # gas_, coinbase_, timestamp_, difficulty_
+            return state.new_bitvec(_FRESH[imm], 256)
         return getattr(env, _ENV_ATTR[imm])
     raise NotEncodable(f"unknown source kind {kind}")
 
@@ -277,7 +283,7 @@ class _Decoder:
             return _mark(source(kind, w, a, self.state), kind, w, (a,))
         if kind == MG_SYM_BALANCE:
             return balance_of(self.state, as_bitvec(self.ref(y)))    # no provenance, as below
-        if kind == MG_SYM_ENV and w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE, MG_ENV_GAS):
+        if kind == MG_SYM_ENV and (w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE) or w in _FRESH):
             # no provenance: the balance and the return data change across host
             # CALLs, so a re-encoded term rides as itself, not as "the value now"
             return source(kind, w, None, self.state)

@@ -14,7 +14,7 @@ from mythril_amd.device import GpuDevice  # noqa: E402
 
 dev = GpuDevice(0)
 out = {}
-for name in sorted(symcases.CONTRACTS) + list(symcases.RUNTIME):
+for name in symcases.ALL_CASES:
     mp = pytest.MonkeyPatch()
     try:
         got, want, laser = symcases.run_both(dev, name, mp)

@@ -56,11 +56,16 @@ SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f5
          "gas_sym": "5a600035106010575a600116601957005b5a15601757005b005b00"}
 
 
+# the other reference codes (tests/testdata/inputs/*.sol.o), deployed as RUNTIME codes
+FIELD = [n for n in sorted(workloads.bytecode_names()) if n not in CONTRACTS and n not in RUNTIME]
+ALL_CASES = sorted(CONTRACTS) + list(RUNTIME) + FIELD
+
+
 def deploy(device, name):
     """Concolic creation (concolic.py:23-72) of a reference test contract (a
     RUNTIME code: the account holding it, with symbolic storage); returns (the
     open world state, the account's address)."""
-    if name in RUNTIME:
+    if name in RUNTIME or name not in CONTRACTS:
         ws = WorldState()
         ws.put_account(Account(CREATOR, balances=None))
         code = bytes.fromhex(SYNTH[name]) if name in SYNTH else workloads.bytecode(name)

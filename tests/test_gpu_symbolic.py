@@ -51,7 +51,7 @@ def _initial(ws, addr, txid="50"):
     return gs
 
 
-@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
+@pytest.mark.parametrize("name", symcases.ALL_CASES)
 def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
     ws, addr = symcases.deploy(dev, name)
     vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
@@ -126,7 +126,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                 queue.extend(t for t in mine if sym.lane_eligible(t))
             elif st == MG_ESCAPE:
                 assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
-    assert forks >= 3 and device_steps > (10 if name in symcases.SYNTH else 100) and checked > forks
+    assert forks >= (1 if name in symcases.FIELD else 3) and device_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100) and checked > forks
     if name == "flag_array.sol.o":
         # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
         assert sym_exp > 0
@@ -149,18 +149,24 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
 # symbolic size, RETURNDATACOPY of a symbolic operand and symbolic jump targets run
 # on the device (ABI v14).
 HOST_OPS = {"CALL", "CALLCODE", "DELEGATECALL", "STATICCALL", "CREATE", "CREATE2", "SELFDESTRUCT"}
+# and, in the other reference codes, reads of other accounts' code and of environment
+# words that are not fresh variables (extcodesize_ .. basefee_, instructions.py:935-1071,
+# 1372-1413); GAS, COINBASE, TIMESTAMP and DIFFICULTY push fresh variables on the device
+WORLD_READS = {"EXTCODESIZE", "EXTCODECOPY", "EXTCODEHASH", "BLOCKHASH", "NUMBER", "CHAINID", "BASEFEE"}
 
 
-@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
+@pytest.mark.parametrize("name", symcases.ALL_CASES)
 def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
-    assert laser.forks >= 3 and laser.lane_steps > (10 if name in symcases.SYNTH else 100)
+    assert laser.forks >= (1 if name in symcases.FIELD else 3) and \
+        laser.lane_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100)
     # CALLDATACOPY of a symbolic size, memory offset or calldata offset, and MLOAD /
     # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
     # its free-memory pointer by a symbolic length) run on the device; what
     # escapes is the host's part
-    assert set(laser.escaped_ops) <= HOST_OPS, dict(laser.escaped_ops)
+    assert set(laser.escaped_ops) <= (HOST_OPS if name not in symcases.FIELD else HOST_OPS | WORLD_READS), \
+        dict(laser.escaped_ops)
 
 
 @pytest.mark.parametrize("name", symcases.SYM_CREATIONS)

@@ -149,10 +149,10 @@ def test_jumpi_successors_follow_the_reference():
     assert jump.world_state.constraints[-1].raw is (cond < BVV(3, 256)).raw
 
 
-@pytest.mark.parametrize("name", sorted(symcases.CONTRACTS) + list(symcases.RUNTIME))
+@pytest.mark.parametrize("name", symcases.ALL_CASES)
 def test_symbolic_call_outcomes_equal_the_restatement(name, monkeypatch):
     got, want, laser = symcases.run_both(OracleDevice(), name, monkeypatch)
-    assert sum(want.values()) >= (5 if name in symcases.SYNTH else 7)
+    assert sum(want.values()) >= (2 if name in symcases.FIELD else 5 if name in symcases.SYNTH else 7)
     assert got == want
 
 
