@@ -22,4 +22,13 @@ for name in symcases.ALL_CASES:
     finally:
         mp.undo()
     print(name, json.dumps(out[name]), flush=True)
+for name in symcases.SYM_CREATIONS_ALL:
+    mp = pytest.MonkeyPatch()
+    try:
+        got, want, laser = symcases.run_creation_both(dev, name, mp)
+        out["creation:" + name] = {"equal": got == want, "escaped": dict(laser.escaped_ops),
+                                   "lane_steps": int(laser.lane_steps)}
+    finally:
+        mp.undo()
+    print("creation:" + name, json.dumps(out["creation:" + name]), flush=True)
 dev.close()

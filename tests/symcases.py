@@ -163,6 +163,8 @@ def run_both(device, name, monkeypatch):
 # constructor arguments are read past the end of the code from the symbolic
 # calldata (CODESIZE + 0x200 pins its size, instructions.py:979-1104)
 SYM_CREATIONS = ("symbolic_exec_bytecode.sol.o", "flag_array.sol.o")
+# every reference code as a symbolic creation (round 4)
+SYM_CREATIONS_ALL = list(SYM_CREATIONS) + [n for n in sorted(workloads.bytecode_names()) if n not in SYM_CREATIONS]
 
 
 def _creation_tx(ws, code, txid):

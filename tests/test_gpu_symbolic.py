@@ -169,7 +169,7 @@ def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch)
         dict(laser.escaped_ops)
 
 
-@pytest.mark.parametrize("name", symcases.SYM_CREATIONS)
+@pytest.mark.parametrize("name", symcases.SYM_CREATIONS_ALL)
 def test_symbolic_creation_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     """transaction/symbolic.py's creation on kernel 1: the creation's calldata
     opcodes (CALLDATACOPY pops, CODESIZE + 0x200 with calldata.size pinned
@@ -180,6 +180,6 @@ def test_symbolic_creation_on_kernel1_equals_the_restatement(dev, name, monkeypa
     assert sum(want.values()) >= 2
     assert got == want, ([(k[:2], [str(c) for c in k[2]], v) for k, v in (got - want).items()],
                          [(k[:2], [str(c) for c in k[2]], v) for k, v in (want - got).items()])
-    assert laser.lane_steps > 50
+    assert laser.lane_steps > (50 if name in symcases.SYM_CREATIONS else 10)
     for op in ("CODESIZE", "CODECOPY", "CALLDATACOPY", "CALLDATALOAD", "CALLDATASIZE"):
         assert laser.escaped_ops[op] == 0, (op, dict(laser.escaped_ops))

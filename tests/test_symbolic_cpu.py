@@ -156,7 +156,7 @@ def test_symbolic_call_outcomes_equal_the_restatement(name, monkeypatch):
     assert got == want
 
 
-@pytest.mark.parametrize("name", symcases.SYM_CREATIONS)
+@pytest.mark.parametrize("name", symcases.SYM_CREATIONS_ALL)
 def test_symbolic_creation_outcomes_equal_the_restatement(name, monkeypatch):
     """transaction/symbolic.py's creation (symbolic calldata: CODESIZE + 0x200
     pins its size, constructor arguments come from CODECOPY past the end of
