@@ -56,7 +56,8 @@ extern "C" {
                                   jump targets (JUMP: VmException, JUMPI: falls
                                   through), SHA3 of a symbolic length (MG_REC_SYMLEN),
                                   GAS / COINBASE / TIMESTAMP / DIFFICULTY on symbolic
-                                  lanes (MG_ENV_GAS..MG_ENV_DIFFICULTY) */
+                                  lanes (MG_ENV_GAS..MG_ENV_DIFFICULTY), NUMBER /
+                                  CHAINID on MG_LANE_SYMBLOCK lanes */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -193,6 +194,8 @@ extern "C" {
                                  size (a host CALL's returndatasize variable):
                                  RETURNDATASIZE pushes an MG_SYM_ENV node
                                  (w = MG_ENV_RETURNDATASIZE, instructions.py:1359-1370) */
+#define MG_LANE_SYMBLOCK 262144u /* symbolic lane whose environment's block_number and chainid are
+                                    symbolic: NUMBER / CHAINID push MG_SYM_ENV nodes          */
 #define MG_LANE_BALANCE 131072u /* symbolic lane of a LaserEVM with no dynamic loader: BALANCE
                                    pushes an MG_SYM_BALANCE node (the world state's accounts
                                    cannot change inside a device run)                    */
@@ -208,6 +211,8 @@ extern "C" {
 #define MG_ENV_COINBASE 8      /* ... new_bitvec("coinbase", 256) (coinbase_, :1386-1393)                      */
 #define MG_ENV_TIMESTAMP 9     /* ... new_bitvec("timestamp", 256) (timestamp_, :1396-1403)                    */
 #define MG_ENV_DIFFICULTY 10   /* ... new_bitvec("block_difficulty", 256) (difficulty_, :1416-1425)            */
+#define MG_ENV_NUMBER 11       /* ... environment.block_number (number_, :1406-1413), on MG_LANE_SYMBLOCK lanes  */
+#define MG_ENV_CHAINID 12      /* ... environment.chainid (chainid_, :958-965), on MG_LANE_SYMBLOCK lanes        */
 
 #define MG_STACK_LIMIT 1024u              /* MachineStack.STACK_LIMIT           */
 #define MG_MSTATE_GAS_LIMIT 1000000000ull /* GlobalState default gas_limit      */

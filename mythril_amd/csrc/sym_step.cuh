@@ -77,6 +77,7 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define LANE_SYMBAL 32768u
 #define LANE_SYMRDS 65536u
 #define LANE_BALANCE 131072u
+#define LANE_SYMBLOCK 262144u
 #define SYM_SLOAD 6u
 #define SYM_KECCAK 7u
 #define SYM_EXTRACT 8u
@@ -447,7 +448,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
         if (((uy & PD_SPECIAL) &&
              !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE)) ||
-                ((op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u) && symlane)) && !tl)) ||
+                ((op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u) && symlane) ||
+                ((op == 0x43u || op == 0x46u) && (flags & LANE_SYMBLOCK))) && !tl)) ||
             (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
@@ -871,7 +873,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (op == 0x47u || op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u ||
+        if (op == 0x47u || op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u || op == 0x43u || op == 0x46u ||
             (op == 0x3du && (flags & LANE_SYMRDS) && !tl)) {
             // SELFBALANCE on a lane whose balance is symbolic (selfbalance_,
             // instructions.py:968-976; taint lanes escaped above):
@@ -881,10 +883,13 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             // host decodes.  No host CALL runs inside a device run, so neither value
             // can move under it.
             // GAS, COINBASE, TIMESTAMP, DIFFICULTY on a symbolic lane (:1386-1425,
-            // 1700-1709): the transaction's fresh variable of that name, new_bitvec
+            // 1700-1709): the transaction's fresh variable of that name, new_bitvec;
+            // NUMBER, CHAINID (:958-965, 1406-1413) when the environment holds them
+            // symbolic (MG_LANE_SYMBLOCK): environment.block_number / chainid
             const uint32_t which = op == 0x47u ? MG_ENV_SELFBALANCE : op == 0x5au ? MG_ENV_GAS :
                                    op == 0x41u ? MG_ENV_COINBASE : op == 0x42u ? MG_ENV_TIMESTAMP :
-                                   op == 0x44u ? MG_ENV_DIFFICULTY : MG_ENV_RETURNDATASIZE;
+                                   op == 0x44u ? MG_ENV_DIFFICULTY : op == 0x43u ? MG_ENV_NUMBER :
+                                   op == 0x46u ? MG_ENV_CHAINID : MG_ENV_RETURNDATASIZE;
             const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
             uint32_t lnn = nn, rtag = 0u;
             if (sp + 1u > STACK_LIMIT) { ++executed; status = ST_VMEXC; aux = EXC_OVERFLOW; break; }

@@ -57,7 +57,8 @@ MG_SYM_BALANCE = 16     # balance_ of the address ref y over the world state's a
 MG_LANE_SYMSTORE, MG_LANE_MEMTAG = 4096, 8192
 MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_LANE_BALANCE = 32768, 65536, 131072
 MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE, MG_ENV_GAS = 5, 6, 7
-MG_ENV_COINBASE, MG_ENV_TIMESTAMP, MG_ENV_DIFFICULTY = 8, 9, 10
+MG_ENV_COINBASE, MG_ENV_TIMESTAMP, MG_ENV_DIFFICULTY, MG_ENV_NUMBER, MG_ENV_CHAINID = 8, 9, 10, 11, 12
+MG_LANE_SYMBLOCK = 262144
 MG_LANE_RETDATA = 16384
 MG_SYM_CONST = 0x80000000
 MG_LANE_TAINT = 2048

@@ -39,7 +39,7 @@ from ..lanes import (ENV_ADDRESS as MG_ENV_ADDRESS, ENV_CALLER as MG_ENV_CALLER,
                      ENV_ORIGIN as MG_ENV_ORIGIN, MG_LANE_MEMTAG, MG_LANE_SYMBOLIC, MG_LANE_SYMCD,
                      MG_LANE_SYMENV_SHIFT, MG_LANE_SYMSTORE, MG_SYM_BIN, MG_SYM_CDBYTE, MG_SYM_CDBYTEX, MG_SYM_CDLOAD,
                      MG_SYM_MLOADK, MG_SYM_MSTOREK,
-                     MG_ENV_COINBASE, MG_ENV_DIFFICULTY, MG_ENV_GAS, MG_ENV_RETURNDATASIZE, MG_ENV_TIMESTAMP, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_BALANCE, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
+                     MG_ENV_CHAINID, MG_ENV_COINBASE, MG_ENV_DIFFICULTY, MG_ENV_GAS, MG_ENV_NUMBER, MG_LANE_SYMBLOCK, MG_ENV_RETURNDATASIZE, MG_ENV_TIMESTAMP, MG_ENV_SELFBALANCE, MG_LANE_SYMBAL, MG_LANE_SYMRDS, MG_SYM_BALANCE, MG_SYM_CDSIZE, MG_SYM_CONCAT, MG_SYM_CONST, MG_SYM_ENV, MG_SYM_EXTRACT, MG_SYM_KECCAK, MG_SYM_SLOAD,
                      MG_SYM_TERM, MG_SYM_UN, limbs_to_word, word_to_limbs)
 from ..smt.expr import (Array, BitVec, Bool, Concat, Extract, Function, If, LShR, Node, Not, UDiv, UGT, ULT,
                         URem, SRem, _select, simplify_concat, symbol_factory)
@@ -193,6 +193,10 @@ def source(kind: int, imm: int, arg, state):
             return state.last_return_data.size
         if imm in _FRESH:                       # gas_, coinbase_, timestamp_, difficulty_
             return state.new_bitvec(_FRESH[imm], 256)
+        if imm == MG_ENV_NUMBER:                # number_ (instructions.py:1406-1413)
+            return env.block_number
+        if imm == MG_ENV_CHAINID:               # chainid_ (instructions.py:958-965)
+            return env.chainid
         return getattr(env, _ENV_ATTR[imm])
     raise NotEncodable(f"unknown source kind {kind}")
 
@@ -283,7 +287,8 @@ class _Decoder:
             return _mark(source(kind, w, a, self.state), kind, w, (a,))
         if kind == MG_SYM_BALANCE:
             return balance_of(self.state, as_bitvec(self.ref(y)))    # no provenance, as below
-        if kind == MG_SYM_ENV and (w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE) or w in _FRESH):
+        if kind == MG_SYM_ENV and (w in (MG_ENV_SELFBALANCE, MG_ENV_RETURNDATASIZE, MG_ENV_NUMBER, MG_ENV_CHAINID)
+                                   or w in _FRESH):
             # no provenance: the balance and the return data change across host
             # CALLs, so a re-encoded term rides as itself, not as "the value now"
             return source(kind, w, None, self.state)
@@ -669,6 +674,9 @@ def encode_state(state, node_cap: int = 1 << 30, const_cap: int = 1 << 30) -> La
             flags |= MG_LANE_SYMSTORE
         if state.environment.active_account.balance().symbolic:
             flags |= MG_LANE_SYMBAL
+        env = state.environment
+        if all(isinstance(w, BitVec) and w.symbolic for w in (env.block_number, env.chainid)):
+            flags |= MG_LANE_SYMBLOCK
         rds = getattr(getattr(state, "last_return_data", None), "size", None)
         if isinstance(rds, BitVec) and rds.symbolic:
             flags |= MG_LANE_SYMRDS
