@@ -57,7 +57,8 @@ extern "C" {
                                   through), SHA3 of a symbolic length (MG_REC_SYMLEN),
                                   GAS / COINBASE / TIMESTAMP / DIFFICULTY on symbolic
                                   lanes (MG_ENV_GAS..MG_ENV_DIFFICULTY), NUMBER /
-                                  CHAINID on MG_LANE_SYMBLOCK lanes */
+                                  CHAINID on MG_LANE_SYMBLOCK lanes, LOG0..4 of
+                                  symbolic operands (pops only) */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0

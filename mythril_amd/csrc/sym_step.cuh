@@ -941,6 +941,18 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
+        if (kind == K_LOG && any_sym && (!tl || !tact) && sp >= max(req, npop)) {
+            // LOG0..4 with a symbolic operand (log_, instructions.py:1710-1723): a state
+            // mutation (WriteProtection in a static call), then the words are popped and
+            // nothing else happens; the table gas, then the OOG check
+            const uint64_t ngmin = gmin + (d.x & 0xffffu), ngmax = gmax + (d.x >> 16);
+            ++executed;
+            if (flags & LANE_STATIC) { status = ST_VMEXC; aux = EXC_WRITEPROT; break; }
+            if (ngmin >= glim) { status = ST_VMEXC; aux = EXC_OOG; break; }
+            sp -= npop; ++pc; gmin = ngmin; gmax = ngmax;
+            continue;
+        }
+
         if (op == 0x3eu && any_sym && !tl && sp >= 3u) {
             // RETURNDATACOPY with a symbolic memory offset, return offset or size
             // (returndatacopy_, instructions.py:1314-1343): the three words are popped

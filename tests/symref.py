@@ -444,6 +444,18 @@ class Engine:
             return self._jumpi(s, _val(target), cond)
         if op == 0x56 and _val(st[-1]) is None:
             return self._vmexc(state)     # jump_ (:1529-1532): InvalidJumpDestination
+        if 0xA0 <= op <= 0xA4:
+            # log_ (:1710-1723): a state mutation, then the words are popped, nothing logged
+            if env.static:
+                return self._vmexc(state)
+            for _ in range(2 + op - 0xA0):
+                st.pop()
+            if ms.min_gas_used + gmin >= min(_gas_limit(s), 10 ** 9 + 1):
+                return self._vmexc(state)
+            ms.min_gas_used += gmin
+            ms.max_gas_used += gmax
+            ms.pc += 1
+            return [s]
         if op == 0x37 or op not in _SYM_OK and not sym_env and op not in (0x35, 0x36, 0x0A):
             raise Unsupported(f"{name} with symbolic inputs")
         cond_after = None
