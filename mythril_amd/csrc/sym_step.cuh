@@ -941,7 +941,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (kind == K_LOG && any_sym && (!tl || !tact) && sp >= max(req, npop)) {
+        if (kind == K_LOG && any_sym && !tl && sp >= max(req, npop)) {
             // LOG0..4 with a symbolic operand (log_, instructions.py:1710-1723): a state
             // mutation (WriteProtection in a static call), then the words are popped and
             // nothing else happens; the table gas, then the OOG check
