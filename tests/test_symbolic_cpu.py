@@ -506,3 +506,24 @@ def test_symlen_record_parses_and_restates_sha3_of_a_symbolic_length():
     n = s.environment.calldata.get_word_at(BVV(32, 256))
     assert s.world_state.constraints[-1].raw is (n == 64).raw
     assert s.mstate.stack[-1].symbolic and len(s.mstate.memory) == 64
+
+
+def test_fresh_variable_and_block_nodes_decode_like_the_restatement():
+    """gas_ / coinbase_ / timestamp_ / difficulty_ (instructions.py:1386-1425,
+    1700-1709) push the transaction's fresh variable of that name; number_ /
+    chainid_ (:958-965, 1406-1413) the environment's words.  The device's
+    MG_SYM_ENV nodes (MG_ENV_GAS .. MG_ENV_CHAINID) decode to the same terms the
+    restatement pushes, and a default Environment marks the lane MG_LANE_SYMBLOCK."""
+    from mythril_amd.lanes import (MG_ENV_CHAINID, MG_ENV_COINBASE, MG_ENV_DIFFICULTY, MG_ENV_GAS,
+                                   MG_ENV_NUMBER, MG_ENV_TIMESTAMP, MG_LANE_SYMBLOCK, MG_SYM_ENV)
+    # GAS COINBASE TIMESTAMP DIFFICULTY NUMBER CHAINID (PUSH1 0 CALLDATALOAD: a symbolic lane) STOP
+    s = _run_restatement("5a" "41" "42" "44" "43" "46" "6000" "35" "00", 8)
+    want = [x.raw for x in s.mstate.stack[:6]]
+    assert sym.encode_state(s).flags & MG_LANE_SYMBLOCK
+    c = _batch()
+    for k, w in enumerate((MG_ENV_GAS, MG_ENV_COINBASE, MG_ENV_TIMESTAMP, MG_ENV_DIFFICULTY, MG_ENV_NUMBER,
+                           MG_ENV_CHAINID)):
+        c.node[0, k] = (MG_SYM_ENV | 256 << 8, 0, 0, w)
+    c.n_nodes[0] = 6
+    dec = sym._Decoder(c, 0, s)
+    assert [dec.node(k).raw for k in range(6)] == want
