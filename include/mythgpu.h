@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 14u  /* 2: model tables (arrays, uninterpreted functions)
+#define MG_ABI_VERSION 15u  /* 2: model tables (arrays, uninterpreted functions)
                                3: per-lane instruction traces + loop bound
                                4: per-lane function-manager records (Keccak, EXP)
                                5: symbolic lanes: expression arena, MG_FORK
@@ -58,7 +58,10 @@ extern "C" {
                                   GAS / COINBASE / TIMESTAMP / DIFFICULTY on symbolic
                                   lanes (MG_ENV_GAS..MG_ENV_DIFFICULTY), NUMBER /
                                   CHAINID on MG_LANE_SYMBLOCK lanes, LOG0..4 of
-                                  symbolic operands (pops only) */
+                                  symbolic operands (pops only)
+                              15: function-entry tracking (mg_lane_soa.fent,
+                                  mg_code_fentries): the last JUMP / JUMPI landing
+                                  on a dispatcher entry, for active_function_name */
 
 /* ------------------------------------------------------------------ errors */
 #define MG_OK          0
@@ -260,7 +263,16 @@ typedef struct mg_lane_soa {
     uint32_t _pad3;
     uint32_t *rec_len;      /* [n] words used                                  */
     uint32_t *rec;          /* [n][rec_cap]                                    */
+    /* LaserEVM._new_node_state (svm.py:575-637): after every JUMP / JUMPI the
+     * successor's instruction address switches environment.active_function_name
+     * when it is a dispatcher entry (Disassembly.address_to_function_name,
+     * disassembly.py:36-56) or address 0 ("fallback").  The device keeps the
+     * instruction INDEX of the last such landing since the upload, or
+     * MG_FENT_NONE; the host maps it to the name.  NULL: uploads MG_FENT_NONE,
+     * downloads nothing (ABI <= 14 callers).                                  */
+    uint32_t *fent;         /* [n]                                             */
 } mg_lane_soa;
+#define MG_FENT_NONE 0xffffffffu
 
 /* Per-call statistics of mg_step. */
 typedef struct mg_step_stats {
@@ -438,6 +450,17 @@ int         mg_opcode_info(uint32_t byte, uint32_t *gas_min, uint32_t *gas_max,
 int         mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t *code_id);
 /* Number of instructions of a loaded code (len(instruction_list)).          */
 int         mg_code_info(mg_ctx *ctx, uint32_t code_id, uint32_t *n_instr);
+/* The device's function-entry flags of a loaded code, one byte per instruction
+ * (n = its instruction count): bit 0 = a JUMP / JUMPI landing on this index
+ * switches active_function_name (an entry of the PUSH1..4 EQ PUSHn dispatcher
+ * pattern, asm.py:66-94 + disassembly.py:36-56 / 64-114, or index 0 =
+ * address 0), bit 1 = the same for the next index (JUMPI fall-through).      */
+int         mg_code_fentries(mg_ctx *ctx, uint32_t code_id, uint8_t *out, uint32_t n);
+/* The device's instruction table of a loaded code (n = its instruction count):
+ * opcode byte per index (0xfe for bytes asm.py:126-131 disassembles to INVALID)
+ * and the byte address of each instruction -- Disassembly.instruction_list
+ * without the arguments (they are the code's bytes after each PUSH).          */
+int         mg_code_table(mg_ctx *ctx, uint32_t code_id, uint8_t *ops, uint32_t *addrs, uint32_t n);
 
 /* ----------------------------------------------------------------- lanes */
 int         mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg);

@@ -34,6 +34,9 @@ struct DevLanes {
     uint32_t rec_cap;
     uint32_t *rec_len;   // [N]
     uint32_t *rec;       // [rec_cap][N]
+    // active_function_name (svm.py:575-637): index of the last JUMP / JUMPI landing
+    // on a function entry since the upload, MG_FENT_NONE if none
+    uint32_t *fent;      // [N]
 };
 
 // Symbolic planes (mg_sym_alloc): stack tags, expression arena, constants.
@@ -82,7 +85,8 @@ struct DevCode {
     uint32_t bytes_off;  // u8  [n_bytes]            full bytecode
     uint32_t cov_off;    // u8  [n_instr]            coverage bytes
     uint32_t run_off;    // u32 [n_instr][2]         straight-line run from each instruction
-    uint32_t _pad[2];
+    uint32_t fent_off;   // u8  [n_instr]            bit 0: index is a function entry, bit 1: index + 1 is
+    uint32_t _pad;
 };
 
 // Per-launch statistics accumulated by the stepping kernel.
@@ -92,3 +96,4 @@ struct DevCounters {
 };
 
 #define MG_JRES_NONE 0xffffffffu
+#define MG_FENT_NONE 0xffffffffu

@@ -389,6 +389,7 @@ struct LaneRegs {
     uint32_t n_sha3, n_exp;
     uint32_t stop, sx;           // out: ST_RUNNING or the stop status and its aux word
     uint32_t step;               // instructions this launch executed before this one
+    uint32_t fent;               // last JUMP / JUMPI landing on a function entry (L.fent)
 };
 // What the handlers read besides the registers (per lane / per block).
 // Per-wave Keccak result cache in LDS (SHA3 of 64 aligned bytes: a mapping
@@ -435,7 +436,7 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
     const bool push = ((uk >> 16) & 1u) != 0u;
     const uint32_t gtab_min = ux & 0xffffu, gtab_max = ux >> 16;
     const uint32_t sp = R.sp, pc = R.pc, msize0 = R.msize;
-    uint32_t nmsize = R.msize, ndepth = R.depth, npc = pc + 1u;
+    uint32_t nmsize = R.msize, ndepth = R.depth, npc = pc + 1u, nfent = R.fent;
     uint64_t ngmin = R.gmin, ngmax = R.gmax;
     uint32_t stop = ST_RUNNING, sx = 0;
     bool by_table = true;
@@ -457,6 +458,8 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
 #define ZEROFILL() if (nmsize > msize0) V.mzero(msize0, nmsize);
 #define JUMP_OK(idx_) ((idx_) != MG_JRES_NONE && \
                        ((E.sflag && (idx_) < E.sn) ? (E.s_pd[(idx_)].y & 0xffu) : (uint32_t)gops[(idx_)]) == 0x5bu)
+    // _new_node_state (svm.py:575-637): a JUMP / JUMPI successor at a function entry
+#define FENT_AT(idx_) ((E.sflag && (idx_) < E.sn) ? (E.s_pd[(idx_)].y >> 22) & 1u : a8[C.fent_off + (idx_)] & 1u)
 
     do {
         // svm.py:391-402 precheck; instructions.py:188-193 write protection;
@@ -708,17 +711,20 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
             if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
             if (!JUMP_OK(idx)) EXCX(EXC_BADJUMP)
             ngmin += 8u; ngmax += 8u; npc = idx;
+            if (FENT_AT(idx)) nfent = idx;
             break;
         }
         case K_JUMPI: {  // gas 10 by hand, depth + 1 on the side taken (:1558-1636)
             by_table = false;
             if (u_iszero(b)) {
                 ngmin += 10u; ngmax += 10u; ++ndepth;
+                if ((uk >> 23) & 1u) nfent = pc + 1u;      // PD_NFENT: the fall-through
             } else {
                 uint32_t idx = MG_JRES_NONE;
                 if (u_fits32(a) && a.w[0] < C.n_jres) idx = a32[C.jres_off + a.w[0]];
                 if (!JUMP_OK(idx)) STOPX(ST_DROPPED, 0u)
                 ngmin += 10u; ngmax += 10u; ++ndepth; npc = idx;
+                if (FENT_AT(idx)) nfent = idx;
             }
             break;
         }
@@ -766,12 +772,13 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
 #undef MEMX
 #undef ZEROFILL
 #undef JUMP_OK
+#undef FENT_AT
     R.stop = stop;
     R.sx = sx;
     if (stop == ST_RUNNING) {
         if (rec_new) L.rec_len[lane] = rec_new;
         R.pc = npc; R.sp = nsp + (push ? 1u : 0u);
-        R.msize = nmsize; R.depth = ndepth; R.gmin = ngmin; R.gmax = ngmax;
+        R.msize = nmsize; R.depth = ndepth; R.gmin = ngmin; R.gmax = ngmax; R.fent = nfent;
     }
 }
 
@@ -780,6 +787,8 @@ DEV bool alu_is_fast(uint32_t op) { return op <= 0x03u || op == 0x0bu || (op >= 
 
 // Pre-decoded word (s_pd[i].y): op | req << 8 | npop << 12 | push << 16 |
 // kind << 17 | PD_CREATION | PD_SPECIAL | hook << 31.
+#define PD_FENT (1u << 22)       // a JUMP / JUMPI landing here switches active_function_name
+#define PD_NFENT (1u << 23)      // ... landing on the next instruction (JUMPI fall-through)
 #define PD_CREATION (1u << 29)   // escapes when the lane is a creation transaction
 #define PD_SPECIAL (1u << 30)    // kind >= K_ESCAPE (host opcode or past-the-end)
 DEV uint32_t pd_flags(uint32_t op, uint32_t dy, uint32_t hook) {
@@ -860,6 +869,7 @@ __device__ __forceinline__ void reset_lane(const DevLanes &L, const DevResetImag
     L.sha3_count[lane] = 0; L.exp_count[lane] = 0;
     L.trace_len[lane] = 0;                 // reset images start with empty traces
     L.rec_len[lane] = 0;                   // ... and empty record logs
+    L.fent[lane] = MG_FENT_NONE;           // ... and no function switch yet
     const uint32_t cnt = R.storage_count[lane];
     L.storage_count[lane] = cnt;
     for (uint32_t s = 0; s < cnt; ++s)
@@ -987,7 +997,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 const uint2 d = kDec[op];
                 const uint64_t hm = op < 64u ? m0 : op < 128u ? m1 : op < 192u ? m2 : m3;
                 const uint32_t hook = (uint32_t)((hm >> (op & 63u)) & 1ull);
-                s_pd[i] = make_uint4(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook),
+                s_pd[i] = make_uint4(d.x, op | (d.y << 8) | pd_flags(op, d.y, hook) |
+                                              ((uint32_t)a8[BC.fent_off + i] << 22),
                                      a32[BC.run_off + 2u * i], a32[BC.run_off + 2u * i + 1u]);
                 s_cov[i] = 0;
             }
@@ -1034,6 +1045,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     DevCode C{};
     uint32_t flags = 0, pc = 0, sp = 0, msize = 0, depth = 0, aux = 0, n_sha3 = 0, n_exp = 0;
     uint32_t tlen = 0;                                    // trace length (BoundedLoops)
+    uint32_t fent = MG_FENT_NONE;                         // last function-entry landing
     const uint32_t loop_on = kLoop ? loop_bound : 0u;     // kernel argument: uniform
     uint64_t txlim = 0, glim = 0, gmin = 0, gmax = 0;
     U256 T0 = u_zero(), T1 = u_zero();
@@ -1047,6 +1059,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         // accumulate_gas OOG test (instructions.py:162-176): min > 1e9 or min >= tx gas limit
         glim = txlim < MSTATE_GAS_LIMIT + 1ull ? txlim : MSTATE_GAS_LIMIT + 1ull;
         pc = L.pc[lane]; sp = L.sp[lane]; msize = L.msize[lane]; depth = L.depth[lane];
+        fent = L.fent[lane];
         if (loop_on) tlen = L.trace_len[lane];
         gmin = L.gas_min[lane]; gmax = L.gas_max[lane];
         for (uint32_t k = 0; k < min(sp, win); ++k) V.set_wstack(k, V.gstack(k));   // window fill
@@ -1066,6 +1079,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         lane_max = min(lane_max, horizon > s0 ? horizon - s0 : 0u);
     }
     const uint8_t *__restrict__ gops = a8 + C.op_off;
+    const uint8_t *__restrict__ gfent = a8 + C.fent_off;
     const StepEnv E{&L, C, a8, a32, s_win, s_mw, s_pd, s_push, s_prof, s_kc + (threadIdx.x >> 6) * KC_WAVE,
                     txlim, glim, lane, tid, lanes_pb, win, flags, sflag, psflag, prof ? 1u : 0u, mw, sn};
 
@@ -1093,7 +1107,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             const uint32_t o_ = gops[pc];                                                 \
             const uint2 d_ = s_dec[o_];                                                   \
             const uint64_t hm_ = o_ < 64u ? m0 : o_ < 128u ? m1 : o_ < 192u ? m2 : m3;    \
-            pd = make_uint2(d_.x, o_ | (d_.y << 8) |                                      \
+            pd = make_uint2(d_.x, o_ | (d_.y << 8) | ((uint32_t)gfent[pc] << 22) |         \
                             pd_flags(o_, d_.y, (uint32_t)((hm_ >> (o_ & 63u)) & 1ull)));  \
         }                                                                                 \
     } while (0)
@@ -1230,13 +1244,20 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                                 if (jflag && tgt.w[0] < jn) { idx = s_jr[tgt.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
                                 else idx = a32[C.jres_off + tgt.w[0]];
                             }
-                            if (!take || (idx != MG_JRES_NONE &&
-                                          (idx < sn ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu)) {
+                            const uint32_t ty = take && idx != MG_JRES_NONE
+                                                    ? (idx < sn ? s_pd[idx].y : (uint32_t)gops[idx] |
+                                                                                ((uint32_t)gfent[idx] << 22))
+                                                    : 0u;
+                            if (!take || (idx != MG_JRES_NONE && (ty & 0xffu) == 0x5bu)) {
                                 nsp = s - rjk;
                                 npc = take ? idx : upc + rlen;
                                 nexec = executed + rlen;
                                 jg = rjk == 1u ? 8u : 10u;      // added by hand, no OOG check
                                 if (rjk == 2u) ++depth;
+                                // _new_node_state: the successor at a function entry (the
+                                // fall-through's bit rides on the JUMPI's own decode word)
+                                const uint32_t jy = __builtin_amdgcn_readlane(ybulk, rsimple);
+                                if (take ? (ty & PD_FENT) : (jy & PD_NFENT)) fent = npc;
                             }
                         }
                         T0 = nsp >= 1u ? V.wstack(nsp - 1u) : u_zero();
@@ -1376,6 +1397,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
             const bool jumpi = kind == K_JUMPI;
             const bool take = !jumpi || !u_iszero(T1);
             uint32_t npc = pc + 1u;
+            uint32_t fbit = uk & PD_NFENT;              // the fall-through's entry bit
             ok = sp >= (jumpi ? 2u : 1u);
             if (take) {
                 uint32_t idx = MG_JRES_NONE;
@@ -1383,12 +1405,17 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                     if (jflag && T0.w[0] < jn) { idx = s_jr[T0.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
                     else idx = a32[C.jres_off + T0.w[0]];
                 }
-                ok = ok && idx != MG_JRES_NONE &&
-                     ((sflag && idx < sn) ? (s_pd[idx].y & 0xffu) : (uint32_t)gops[idx]) == 0x5bu;
+                const uint32_t ty = idx != MG_JRES_NONE
+                                        ? ((sflag && idx < sn) ? s_pd[idx].y
+                                                               : (uint32_t)gops[idx] | ((uint32_t)gfent[idx] << 22))
+                                        : 0u;
+                ok = ok && idx != MG_JRES_NONE && (ty & 0xffu) == 0x5bu;
                 npc = idx;
+                fbit = ty & PD_FENT;
             }
             if (ok) {
                 const uint32_t add = jumpi ? 10u : 8u;
+                if (fbit) fent = npc;                   // _new_node_state (svm.py:617-637)
                 gmin += add; gmax += add;
                 if (jumpi) {
                     ++depth;
@@ -1472,7 +1499,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         }
 #undef PUSHV
         if (!ok) {
-            LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed - 1u};
+            LaneRegs R{T0, T1, gmin, gmax, pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed - 1u, fent};
             slow_step(R, E, uk, ux);
             n_sha3 = R.n_sha3; n_exp = R.n_exp;
             if (R.stop != ST_RUNNING) {
@@ -1482,7 +1509,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                 live = false;
             } else {
                 T0 = R.T0; T1 = R.T1; gmin = R.gmin; gmax = R.gmax;
-                pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth;
+                pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth; fent = R.fent;
             }
         }
         CLK_MARK(261u);
@@ -1508,6 +1535,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
         L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
         L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
         L.status[lane] = status; L.aux[lane] = aux;
+        L.fent[lane] = fent;
         if (loop_on) L.trace_len[lane] = tlen;
         // HOOK_ACK covers one instruction: consumed once the lane has executed
         if (hook_ack && executed > 0u) L.flags[lane] = flags & ~LANE_HOOK_ACK;

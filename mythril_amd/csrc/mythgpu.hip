@@ -302,10 +302,16 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
         length = n >= 43 ? n - 43 : 0;
     std::vector<uint8_t> ops;
     std::vector<uint32_t> addrs, push;
+    // the argument as Disassembly's instruction_list holds it ("0x" + the bytes
+    // present in the code, asm.py:136-142: a PUSH at the end is truncated, not
+    // padded) as an integer, for the dispatcher table below; UINT64_MAX when it
+    // has no byte (int("0x", 16) fails) or cannot be an address
+    std::vector<uint64_t> argv;
     size_t a = 0;
     while (a < length) {
         const uint8_t b = code[a];
         uint32_t pv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t av = UINT64_MAX;
         addrs.push_back((uint32_t)a);
         if (!t[b].valid) {
             ops.push_back(0xfe);
@@ -319,12 +325,35 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
                     const size_t bit = 8 * (np - 1 - i);
                     pv[bit / 32] |= (uint32_t)v << (bit % 32);
                 }
+                const size_t present = std::min(np, n - (a + 1));
+                if (present > 0) {
+                    av = 0;
+                    for (size_t i = 0; i < present && av != UINT64_MAX; ++i)
+                        av = av >> 40 ? UINT64_MAX : (av << 8) | code[a + 1 + i];
+                }
                 a += np;
             }
         }
+        argv.push_back(av);
         push.insert(push.end(), pv, pv + 8);
         a += 1;
     }
+    // Dispatcher entries (Disassembly.assign_bytecode, disassembly.py:36-56):
+    // every PUSH1..PUSH4 followed by EQ (asm.find_op_code_sequence, asm.py:66-94)
+    // whose next instruction is a PUSH names an entry point = that PUSH's argument
+    // (get_function_info, disassembly.py:106-114); address_to_function_name is keyed
+    // by it, and _new_node_state (svm.py:617-637) switches the function name when a
+    // JUMP / JUMPI lands on the instruction at exactly that address; address 0
+    // switches it to "fallback".  fent[i]: bit 0 for index i, bit 1 for i + 1.
+    std::vector<uint8_t> fent(ops.size() + 1, 0);
+    if (!ops.empty()) fent[0] = 1;
+    for (size_t i = 0; i + 2 < ops.size(); ++i) {
+        if (ops[i] < 0x60 || ops[i] > 0x63 || ops[i + 1] != 0x14) continue;
+        if (ops[i + 2] < 0x60 || ops[i + 2] > 0x7f || argv[i + 2] > 0xffffffffull) continue;
+        const auto it = std::lower_bound(addrs.begin(), addrs.end(), (uint32_t)argv[i + 2]);
+        if (it != addrs.end() && *it == (uint32_t)argv[i + 2]) fent[it - addrs.begin()] = 1;
+    }
+    for (size_t i = 0; i < ops.size(); ++i) fent[i] = (uint8_t)((fent[i] & 1u) | ((fent[i + 1] & 1u) << 1));
     DevCode dc{};
     dc.n_instr = (uint32_t)ops.size();
     dc.n_bytes = (uint32_t)n;
@@ -334,6 +363,8 @@ extern "C" int mg_load_code(mg_ctx *ctx, const uint8_t *code, size_t n, uint32_t
     ctx->a8.insert(ctx->a8.end(), ops.begin(), ops.end());
     dc.bytes_off = (uint32_t)ctx->a8.size();
     ctx->a8.insert(ctx->a8.end(), code, code + n);
+    dc.fent_off = (uint32_t)ctx->a8.size();
+    ctx->a8.insert(ctx->a8.end(), fent.begin(), fent.begin() + ops.size());
     while (ctx->a8.size() % 16) ctx->a8.push_back(0);
     // arena32: push (32-byte aligned), addr, jres
     while (ctx->a32.size() % 8) ctx->a32.push_back(0);
@@ -433,6 +464,23 @@ extern "C" int mg_code_info(mg_ctx *ctx, uint32_t code_id, uint32_t *n_instr) {
     return MG_OK;
 }
 
+extern "C" int mg_code_fentries(mg_ctx *ctx, uint32_t code_id, uint8_t *out, uint32_t n) {
+    if (!ctx || code_id >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "unknown code_id %u", code_id);
+    const DevCode &c = ctx->codes[code_id];
+    if (!out || n != c.n_instr) return set_err(ctx, MG_EINVAL, "mg_code_fentries: need %u bytes", c.n_instr);
+    std::memcpy(out, ctx->a8.data() + c.fent_off, n);
+    return MG_OK;
+}
+
+extern "C" int mg_code_table(mg_ctx *ctx, uint32_t code_id, uint8_t *ops, uint32_t *addrs, uint32_t n) {
+    if (!ctx || code_id >= ctx->codes.size()) return set_err(ctx, MG_ENOCODE, "unknown code_id %u", code_id);
+    const DevCode &c = ctx->codes[code_id];
+    if (!ops || !addrs || n != c.n_instr) return set_err(ctx, MG_EINVAL, "mg_code_table: need %u entries", c.n_instr);
+    std::memcpy(ops, ctx->a8.data() + c.op_off, n);
+    std::memcpy(addrs, ctx->a32.data() + c.addr_off, (size_t)n * 4);
+    return MG_OK;
+}
+
 // ------------------------------------------------------------------- lanes
 template <class T>
 static int lane_alloc(mg_ctx *ctx, T *&p, size_t count) {
@@ -463,7 +511,7 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     int rc = 0;
     uint32_t **u32s[] = {&L.code_id, &L.pc, &L.sp, &L.msize, &L.depth, &L.status, &L.aux, &L.steps,
                          &L.flags, &L.calldata_len, &L.storage_count, &L.ret_offset, &L.ret_len,
-                         &L.sha3_count, &L.exp_count, &ctx->i_pc, &ctx->i_depth, &ctx->i_status,
+                         &L.sha3_count, &L.exp_count, &L.fent, &ctx->i_pc, &ctx->i_depth, &ctx->i_status,
                          &ctx->i_aux, &ctx->i_steps, &ctx->i_storage_count};
     for (auto pp : u32s)
         if ((rc = lane_alloc(ctx, *pp, N))) return rc;
@@ -491,6 +539,7 @@ extern "C" int mg_lanes_alloc(mg_ctx *ctx, const mg_batch_cfg *cfg) {
     HIPX(ctx, hipMemsetAsync(L.status, 0xff, N * 4, ctx->stream));
     HIPX(ctx, hipMemsetAsync(L.sha3_count, 0, N * 4, ctx->stream));
     HIPX(ctx, hipMemsetAsync(L.exp_count, 0, N * 4, ctx->stream));
+    HIPX(ctx, hipMemsetAsync(L.fent, 0xff, N * 4, ctx->stream));
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     ctx->have_lanes = true;
     ctx->cfg.calldata_cap = L.calldata_cap;
@@ -785,6 +834,7 @@ static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint3
     x.scalar(h->gas_min, L.gas_min, 8, ctx->i_gas_min);
     x.scalar(h->gas_max, L.gas_max, 8, ctx->i_gas_max);
     x.scalar(h->gas_limit, L.gas_limit, 8);
+    if (h->fent) x.scalar(h->fent, L.fent, 4);
     // rows below the range's largest sp / storage count / msize / trace and record
     // length: no step reads above them before writing (pushes write their slot,
     // stores and logs append, memory is zero-filled when it extends), so the rest
@@ -807,6 +857,7 @@ static int lanes_upload(mg_ctx *ctx, const mg_lane_soa *h, uint32_t first, uint3
     HIPX(ctx, hipMemsetAsync(L.exp_count + first, 0, (size_t)n * 4, ctx->stream));
     if (!h->trace_cap) HIPX(ctx, hipMemsetAsync(L.trace_len + first, 0, (size_t)n * 4, ctx->stream));
     if (!h->rec_cap) HIPX(ctx, hipMemsetAsync(L.rec_len + first, 0, (size_t)n * 4, ctx->stream));
+    if (!h->fent) HIPX(ctx, hipMemsetAsync(L.fent + first, 0xff, (size_t)n * 4, ctx->stream));
     if ((rc = xfer_up(ctx, x))) return rc;
     HIPX(ctx, hipStreamSynchronize(ctx->stream));
     ctx->uploaded = true;
@@ -1075,6 +1126,7 @@ static int lanes_download(mg_ctx *ctx, mg_lane_soa *h, uint32_t first, uint32_t 
     x.scalar(h->gas_limit, L.gas_limit, 8);
     if (h->trace_cap) x.scalar(h->trace_len, L.trace_len, 4);
     if (h->rec_cap) x.scalar(h->rec_len, L.rec_len, 4);
+    if (h->fent) x.scalar(h->fent, L.fent, 4);
     if ((rc = xfer_down(ctx, x))) return rc;
     // phase 2: rows; live: only what a step can have written, below the
     // range's largest sp / storage count / msize / trace and record length

@@ -89,6 +89,17 @@ DEV bool sym_node_push(const DevSym &S, size_t N, uint32_t lane, uint32_t kind_w
 #define SYM_MSTOREK 14u
 #define SYM_MLOADK 15u
 #define SYM_BALANCE 16u
+// A tagged word the host can only decode to a symbolic term: a fresh calldata word
+// or size, an environment word, a keccak of symbolic data.  Any other node (an
+// ALU result such as x - x, an MLOADK of a word stored concretely, a BALANCE of a
+// known account, a store-chain read) may decode to a constant after simplify, and
+// then the reference takes a concrete branch (util.get_concrete_int) -- the device
+// leaves those to the host.
+DEV bool sym_never_const(const DevSym &S, size_t N, uint32_t lane, uint32_t tag) {
+    if (!tag) return false;
+    const uint32_t kind = S.node[(size_t)(tag - 1u) * N + lane].x & 0xffu;
+    return kind == SYM_CDLOAD || kind == SYM_CDSIZE || kind == SYM_ENV || kind == SYM_KECCAK;
+}
 
 DEV uint32_t mtag_at(const DevSym &S, size_t N, uint32_t lane, uint32_t off) { return S.mtag[(size_t)off * N + lane]; }
 DEV void set_mtag(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32_t t) {
@@ -392,7 +403,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
     const bool tl = (flags & LANE_TAINT) && T.sobj != nullptr;
     const DevCode C = codes[L.code_id[lane]];
     const uint8_t *__restrict__ gops = a8 + C.op_off;
+    const uint8_t *__restrict__ gfent = a8 + C.fent_off;
     uint32_t pc = L.pc[lane], sp = L.sp[lane], msize = L.msize[lane], depth = L.depth[lane];
+    uint32_t fent = L.fent[lane];
     uint64_t gmin = L.gas_min[lane], gmax = L.gas_max[lane];
     const uint64_t txlim = L.gas_limit[lane];
     const uint64_t glim = txlim < MSTATE_GAS_LIMIT + 1ull ? txlim : MSTATE_GAS_LIMIT + 1ull;
@@ -444,12 +457,12 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         }
         if (hooked) { status = ST_HOOK; aux = op; break; }
         if (executed >= lane_max) break;
-        const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u);
+        const uint32_t uy = op | (d.y << 8) | pd_flags(op, d.y, 0u) | ((uint32_t)gfent[pc] << 22);
         // a creation's calldata opcodes run here on a lane with symbolic calldata (below)
         if (((uy & PD_SPECIAL) &&
-             !(((op == 0x47u && (flags & LANE_SYMBAL)) || (op == 0x31u && (flags & LANE_BALANCE)) ||
+             !(((op == 0x47u && (flags & LANE_SYMBAL) && symlane) || (op == 0x31u && (flags & LANE_BALANCE) && symlane) ||
                 ((op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u) && symlane) ||
-                ((op == 0x43u || op == 0x46u) && (flags & LANE_SYMBLOCK))) && !tl)) ||
+                ((op == 0x43u || op == 0x46u) && (flags & LANE_SYMBLOCK) && symlane)) && !tl)) ||
             (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
@@ -930,13 +943,14 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
         }
 
         if (any_sym && !tl && (kind == K_JUMP || (kind == K_JUMPI && sp >= 2u)) && sp >= 1u &&
-            sym_tag(S, N, lane, sp - 1u)) {
+            sym_never_const(S, N, lane, sym_tag(S, N, lane, sp - 1u))) {
             // a symbolic jump target: JUMP raises InvalidJumpDestination (jump_,
             // instructions.py:1529-1532), a VmException at the instruction's start;
             // JUMPI pops both words and falls through with its gas by hand and no
             // depth step ("Skipping JUMPI to invalid destination", :1572-1579)
             ++executed;
             if (kind == K_JUMP) { status = ST_VMEXC; aux = EXC_BADJUMP; break; }
+            if (gfent[pc] & 2u) fent = pc + 1u;     // _new_node_state on the fall-through
             sp -= 2u; ++pc; gmin += 10u; gmax += 10u;
             continue;
         }
@@ -953,7 +967,10 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             continue;
         }
 
-        if (op == 0x3eu && any_sym && !tl && sp >= 3u) {
+        if (op == 0x3eu && any_sym && !tl && sp >= 3u &&
+            (!sym_tag(S, N, lane, sp - 1u) || sym_never_const(S, N, lane, sym_tag(S, N, lane, sp - 1u))) &&
+            (!sym_tag(S, N, lane, sp - 2u) || sym_never_const(S, N, lane, sym_tag(S, N, lane, sp - 2u))) &&
+            (!sym_tag(S, N, lane, sp - 3u) || sym_never_const(S, N, lane, sym_tag(S, N, lane, sp - 3u)))) {
             // RETURNDATACOPY with a symbolic memory offset, return offset or size
             // (returndatacopy_, instructions.py:1314-1343): the three words are popped
             // and nothing is copied; the table gas, then the OOG check
@@ -1076,7 +1093,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (kind == K_SWAP && sp >= nin) { t_in0 = sym_tag(S, N, lane, sp - 1u); t_in1 = sym_tag(S, N, lane, sp - nin); }
         }
         LaneRegs R{sp >= 1u ? V.stack(sp - 1u) : u_zero(), sp >= 2u ? V.stack(sp - 2u) : u_zero(), gmin, gmax,
-                   pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed};
+                   pc, sp, msize, depth, n_sha3, n_exp, 0u, 0u, executed, fent};
         const U256 pa = R.T0, pb = R.T1;
         const uint32_t sp0 = sp;
         slow_step(R, E, uy, d.x);
@@ -1119,7 +1136,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }
             if (post_bit) { ++natoms; if (tact & T_YCLASS) tym |= post_bit; }
         }
-        pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth; gmin = R.gmin; gmax = R.gmax;
+        pc = R.pc; sp = R.sp; msize = R.msize; depth = R.depth; gmin = R.gmin; gmax = R.gmax; fent = R.fent;
         ++executed;
     }
     if (prof && executed != pexec) atomicAdd(&prof[pop], 1ull);
@@ -1127,6 +1144,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
     L.pc[lane] = pc; L.sp[lane] = sp; L.msize[lane] = msize; L.depth[lane] = depth;
     L.gas_min[lane] = gmin; L.gas_max[lane] = gmax;
     L.status[lane] = status; L.aux[lane] = aux;
+    L.fent[lane] = fent;
     if (hook_ack && executed > 0u) lflags &= ~LANE_HOOK_ACK;
     if (lflags != flags) L.flags[lane] = lflags;
     L.steps[lane] += executed;

@@ -80,6 +80,22 @@ class GpuDevice:
         self._check(self.lib.mg_code_info(self.ctx, code_id, ctypes.byref(n)), "mg_code_info")
         return n.value
 
+    def code_fentries(self, code_id: int) -> np.ndarray:
+        """mg_code_fentries: uint8[n_instr], bit 0 = a JUMP / JUMPI landing here
+        switches active_function_name, bit 1 = the same for the next index."""
+        out = np.zeros(self.n_instr(code_id), dtype=np.uint8)
+        self._check(self.lib.mg_code_fentries(self.ctx, code_id, out.ctypes.data, out.size), "mg_code_fentries")
+        return out
+
+    def code_table(self, code_id: int):
+        """mg_code_table: (opcode byte per instruction, byte address per instruction)."""
+        n = self.n_instr(code_id)
+        ops = np.zeros(n, dtype=np.uint8)
+        addrs = np.zeros(n, dtype=np.uint32)
+        self._check(self.lib.mg_code_table(self.ctx, code_id, ops.ctypes.data, addrs.ctypes.data, n),
+                    "mg_code_table")
+        return ops, addrs
+
     # -- lanes ---------------------------------------------------------------
     def alloc(self, shape: LaneShape, coverage: bool = False):
         cfg = native.MgBatchCfg(shape.n, shape.stack_cap, shape.mem_cap, shape.calldata_cap,

@@ -37,6 +37,7 @@ MG_ESC_OPCODE, MG_ESC_MEMORY, MG_ESC_STORAGE, MG_ESC_STACK, MG_ESC_TRACE = 1, 2,
 MG_ESC_RECORD = 6
 MG_ESC_SYMBOLIC, MG_ESC_ARENA, MG_ESC_TAINT = 7, 8, 9
 MG_RET_SYMBOLIC = 0xFFFFFFFF
+MG_FENT_NONE = 0xFFFFFFFF   # no JUMP / JUMPI landed on a function entry since the upload
 # function-manager records (include/mythgpu.h MG_REC_*)
 MG_REC_KECCAK, MG_REC_EXP, MG_REC_ANNOT, MG_REC_HOOK, MG_REC_HEADER = 1, 2, 3, 4, 11
 MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's index
@@ -120,6 +121,7 @@ class MgLaneSoa(ctypes.Structure):
         ("trace_len", ctypes.c_void_p), ("trace", ctypes.c_void_p),
         ("rec_cap", ctypes.c_uint32), ("_pad3", ctypes.c_uint32),
         ("rec_len", ctypes.c_void_p), ("rec", ctypes.c_void_p),
+        ("fent", ctypes.c_void_p),
     ]
 
 
@@ -144,7 +146,7 @@ class MgTaintSoa(ctypes.Structure):
 _TAINT_FIELDS = ("sobj", "omask", "n_obj", "n_fixed", "n_atoms", "sink", "ymask", "tflags")
 
 _U32_FIELDS = ("code_id", "pc", "sp", "msize", "depth", "status", "aux", "steps", "flags",
-               "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len", "rec_len")
+               "calldata_len", "storage_count", "ret_offset", "ret_len", "trace_len", "rec_len", "fent")
 _U64_FIELDS = ("gas_min", "gas_max", "gas_limit")
 
 
@@ -178,6 +180,7 @@ class LaneBatch:
             setattr(self, f, np.zeros(n, dtype=np.uint32))
         for f in _U64_FIELDS:
             setattr(self, f, np.zeros(n, dtype=np.uint64))
+        self.fent[:] = MG_FENT_NONE
         self.calldata = np.zeros((n, shape.calldata_cap), dtype=np.uint8)
         self.env = np.zeros((n, MG_ENV_WORDS, 8), dtype=np.uint32)
         self.stack = np.zeros((n, shape.stack_cap, 8), dtype=np.uint32)
@@ -323,6 +326,7 @@ class LaneBatch:
         self.pc[i] = self.sp[i] = self.msize[i] = self.depth[i] = 0
         self.status[i] = MG_RUNNING
         self.aux[i] = self.steps[i] = 0
+        self.fent[i] = MG_FENT_NONE
         self.flags[i] = flags
         self.gas_min[i] = self.gas_max[i] = 0
         self.gas_limit[i] = gas_limit
@@ -430,7 +434,7 @@ class LaneBatch:
 
 # Fields compared lane-by-lane in parity tests (device vs oracle).
 PARITY_SCALARS = ("pc", "sp", "msize", "depth", "status", "aux", "steps", "gas_min",
-                  "gas_max", "storage_count", "trace_len", "rec_len")
+                  "gas_max", "storage_count", "trace_len", "rec_len", "fent")
 
 
 def diff_batches(a: LaneBatch, b: LaneBatch, lanes: Optional[Iterable[int]] = None,

@@ -55,7 +55,7 @@ from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
                      MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_RETDATA, MG_LANE_STATIC, MG_LANE_STEP1, MG_RUNNING, MG_VMEXC,
-                     MG_STACK_LIMIT,
+                     MG_STACK_LIMIT, MG_FENT_NONE,
                      limbs_to_word, rows_to_words, word_to_limbs)
 from ..smt.exponent_manager import exponent_function_manager
 from ..smt.expr import ConstWord, Expression, symbol_factory
@@ -177,6 +177,7 @@ class LaserEVM:
             "transaction_end": self._transaction_end_hooks,
         }
         # batched-core specifics
+        self._single_step = False           # execute_state: no manage_cfg (exec() runs it)
         self._device = device
         self.escape_handler = escape_handler
         self.record_coverage = False        # set by the coverage plugin
@@ -371,11 +372,13 @@ class LaserEVM:
             if self.escape_handler is None:
                 log.debug("state not representable on a lane and no escape handler: dropped")
                 continue
+            op = _opcode_at(st)
             new_states = self._escape_step(st, hooks_done=False, track_gas=track_gas,
                                            final_states=final_states)
             if new_states is None:
                 continue
             self._filter_fork(new_states)
+            self.manage_cfg(op, new_states)
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
             if not new_states and track_gas:
@@ -516,6 +519,52 @@ class LaserEVM:
         finally:
             solver_mod.model_cache.clear_prefetch()
 
+    def manage_cfg(self, opcode: Optional[str], new_states: List[GlobalState]) -> None:
+        """svm.py:549-573 for the successors a host step produced: a JUMP /
+        JUMPI successor (and a RETURN's, i.e. the caller's state after a nested
+        call) enters a new node, whose function name _new_node_state sets.  The
+        statespace graph itself is not kept (requires_statespace); lanes apply
+        the same switch from the device's function-entry index (_materialise)."""
+        if opcode in ("JUMP", "JUMPI", "RETURN"):
+            for state in new_states:
+                self._new_node_state(state)
+
+    @staticmethod
+    def _new_node_state(state: GlobalState) -> None:
+        """svm.py:575-637, the environment part: a creation transaction's
+        states are "constructor"; a successor at a dispatcher entry takes its
+        name (Disassembly.address_to_function_name); at address 0, "fallback"."""
+        env = state.environment
+        code = env.code
+        try:
+            address = code.instruction_list[state.mstate.pc]["address"]
+        except IndexError:
+            return
+        seq = state.world_state.transaction_sequence
+        if seq and isinstance(seq[-1], ContractCreationTransaction):
+            env.active_function_name = "constructor"
+        elif address in code.address_to_function_name:
+            env.active_function_name = code.address_to_function_name[address]
+        elif address == 0:
+            env.active_function_name = "fallback"
+
+    def _apply_fent(self, b: LaneBatch, i: int, s: GlobalState) -> None:
+        """The device's record of the lane's last JUMP / JUMPI landing on a
+        function entry (mg_lane_soa.fent): _new_node_state at that successor --
+        the last switch is the only one that shows (every switch overwrites the
+        name; a landing elsewhere leaves it)."""
+        fe = int(b.fent[i])
+        if fe == MG_FENT_NONE:
+            return
+        env = s.environment
+        seq = s.world_state.transaction_sequence
+        if seq and isinstance(seq[-1], ContractCreationTransaction):
+            env.active_function_name = "constructor"
+            return
+        name = env.code.name_at(fe)
+        if name is not None:
+            env.active_function_name = name
+
     def _add_world_state(self, global_state: GlobalState) -> None:
         """svm.py:339-348."""
         for hook in self._add_world_state_hooks:
@@ -533,7 +582,11 @@ class LaserEVM:
         final: List[GlobalState] = []
         instrs = global_state.environment.code.instruction_list
         op = instrs[global_state.mstate.pc]["opcode"] if global_state.mstate.pc < len(instrs) else None
-        self._run_batch([global_state], final, False, True, single_step=True)
+        self._single_step = True
+        try:
+            self._run_batch([global_state], final, False, True, single_step=True)
+        finally:
+            self._single_step = False
         successors = self.work_list[:]
         self.work_list[:] = saved
         return successors, op
@@ -732,6 +785,7 @@ class LaserEVM:
                 b.storage[i, k, 8:] = word_to_limbs(val)
             b.storage_count[i] = len(slots)
         b.ret_offset[i] = b.ret_len[i] = 0
+        b.fent[i] = MG_FENT_NONE              # the host's environment holds the name so far
         if b.shape.trace_cap:
             tr = _trace_of(s)
             b.trace[i] = 0
@@ -747,8 +801,13 @@ class LaserEVM:
                 log.warning("state needs more than %d annotation atoms or objects: its lane drops "
                             "annotations", tnt.MAX_ATOMS)
 
-    def _materialise(self, b: LaneBatch, i: int, s: GlobalState) -> GlobalState:
-        """Write lane i of the host image back into its GlobalState (in place)."""
+    def _materialise(self, b: LaneBatch, i: int, s: GlobalState, fn: bool = True) -> GlobalState:
+        """Write lane i of the host image back into its GlobalState (in place);
+        with `fn`, the function-name switch of its last entry landing too
+        (manage_cfg runs after a step's post hooks: callers that run post hooks
+        on the successor apply it afterwards)."""
+        if fn and not self._single_step:
+            self._apply_fent(b, i, s)
         ms = s.mstate
         ms.pc = int(b.pc[i])
         sp = int(b.sp[i])
@@ -1173,9 +1232,11 @@ class LaserEVM:
                                  inclusive=True)
             for hook in self.instr_post_hook.get(name, ()):
                 hook(snapshot)
-            new = self._materialise(b, i, s)
+            new = self._materialise(b, i, s, fn=False)
             successors = [new]
             self._execute_post_hook(name, successors)
+            if not single_step:
+                self._apply_fent(b, i, new)     # manage_cfg after the post hooks (svm.py:327)
             if not successors:
                 self._sched.set(i, "done")
                 if track_gas:
@@ -1247,7 +1308,9 @@ class LaserEVM:
                     if track_gas:
                         final_states.append(s)
                     return
-            self._queue_fork(s, sym.jumpi_successors(s), track_gas, final_states)
+            successors = sym.jumpi_successors(s)
+            self.manage_cfg("JUMPI", successors)     # the filter only drops states: same names
+            self._queue_fork(s, successors, track_gas, final_states)
             return
         elif status == MG_ESCAPE:
             reason = int(b.aux[i]) >> 8
@@ -1275,6 +1338,7 @@ class LaserEVM:
             if new_states is None:
                 return
             self._filter_fork(new_states)
+            self.manage_cfg(name, new_states)
             self.work_list.extend(new_states)
             self.total_states += len(new_states)
             if new_states or not track_gas:
@@ -1452,6 +1516,12 @@ def _hook_sig(s: GlobalState):
             ms.depth, ms.min_gas_used, ms.max_gas_used, id(env), id(env.code), env.static, id(env.calldata),
             id(env.address), id(env.sender), id(env.origin), id(env.callvalue), id(env.gasprice),
             id(acct), id(acct.storage), acct.storage._ver, id(s.current_transaction))
+
+
+def _opcode_at(state: GlobalState) -> Optional[str]:
+    instrs = state.environment.code.instruction_list
+    pc = state.mstate.pc
+    return instrs[pc]["opcode"] if pc < len(instrs) else None
 
 
 def _no_potential_issues(state: GlobalState) -> None:

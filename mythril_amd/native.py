@@ -118,6 +118,8 @@ SIGNATURES = {
     "mg_opcode_info": (_I, [_U32, _PU32, _PU32, _PU32]),
     "mg_load_code": (_I, [_P, ctypes.c_char_p, ctypes.c_size_t, _PU32]),
     "mg_code_info": (_I, [_P, _U32, _PU32]),
+    "mg_code_fentries": (_I, [_P, _U32, _P, _U32]),
+    "mg_code_table": (_I, [_P, _U32, _P, _P, _U32]),
     "mg_lanes_alloc": (_I, [_P, ctypes.POINTER(MgBatchCfg)]),
     "mg_lanes_upload": (_I, [_P, _P, _U32, _U32]),
     "mg_lanes_download": (_I, [_P, _P, _U32, _U32]),

@@ -94,6 +94,8 @@ typedef struct {
     uint8_t *op;                          /* [n_instr] byte, 0xfe for INVALID  */
     uint32_t *addr;                       /* [n_instr] byte address            */
     u256 *push;                           /* [n_instr] push immediate          */
+    uint8_t *argn;                        /* [n_instr] argument bytes present  */
+    uint8_t *fent;                        /* [n_instr] function entry (0/1)    */
 } orc_code;
 
 #define ORC_MAX_CODES 4096
@@ -135,7 +137,8 @@ static int disassemble(const uint8_t *bc, size_t len, orc_code *c) {
     if (strstr(rep, "bzzr")) length = len >= 43 ? len - 43 : 0;   /* length -= 43 */
     c->op = malloc(length + 1); c->addr = malloc(sizeof(uint32_t) * (length + 1));
     c->push = malloc(sizeof(u256) * (length + 1));
-    if (!c->op || !c->addr || !c->push) return -1;
+    c->argn = calloc(length + 1, 1);
+    if (!c->op || !c->addr || !c->push || !c->argn) return -1;
     uint32_t k = 0;
     size_t a = 0;
     while (a < length) {
@@ -152,6 +155,9 @@ static int disassemble(const uint8_t *bc, size_t len, orc_code *c) {
             for (size_t i = 0; i < np; ++i)
                 if (a + 1 + i < len) buf[i] = bc[a + 1 + i];
             c->push[k] = u_from_be(buf, np);
+            /* asm.py:137-139: the instruction's "argument" is the hex of the bytes
+             * actually present (a PUSH at the end of the code is cut short) */
+            c->argn[k] = (uint8_t)(a + 1 + np <= len ? np : len - (a + 1));
             a += np;
         }
         ++k; a += 1;
@@ -164,19 +170,74 @@ static int disassemble(const uint8_t *bc, size_t len, orc_code *c) {
     return 0;
 }
 
+/* int(instruction_list[k]["argument"], 16) as the reference parses it: the
+ * hex text of the present argument bytes; -1 when it has none (the text "0x"
+ * does not parse) or the value cannot be an instruction address. */
+static int64_t argument_int(const orc_code *c, uint32_t k) {
+    static const char HX[] = "0123456789abcdef";
+    char txt[2 * 32 + 1];
+    uint32_t m = 0;
+    const uint32_t np = c->argn[k];
+    if (np == 0) return -1;
+    uint8_t be[32];
+    u_to_be(c->push[k], be);                  /* the present bytes are the high ones */
+    for (uint32_t j = 0; j < np; ++j) {
+        const uint8_t v = be[32 - (uint32_t)(c->op[k] - 0x5f) + j];
+        txt[m++] = HX[v >> 4]; txt[m++] = HX[v & 15];
+    }
+    txt[m] = 0;
+    const char *p = txt;
+    while (*p == '0' && p[1]) ++p;            /* int() ignores leading zeros */
+    if (strlen(p) > 8) return -1;
+    return (int64_t)strtoull(p, NULL, 16);
+}
+
+/* Disassembly.assign_bytecode (disassembly.py:36-56): the indices of
+ * asm.find_op_code_sequence([("PUSH1".."PUSH4"), ("EQ",)]) (asm.py:66-94) give,
+ * through get_function_info (disassembly.py:64-114), entry points = the argument
+ * of instruction index + 2; address_to_function_name is keyed by them.  An
+ * instruction is a function entry when its address is one (svm.py:617-631);
+ * address 0 switches the name too ("fallback", :632-633). */
+static int dispatcher_entries(orc_code *c) {
+    c->fent = calloc(c->n_instr + 1, 1);
+    if (!c->fent) return -1;
+    if (c->n_instr) c->fent[0] = 1;
+    for (uint32_t idx = 0; idx + 2 <= c->n_instr; ++idx) {
+        const uint8_t o0 = c->op[idx], o1 = c->op[idx + 1];
+        if (!(o0 >= 0x60 && o0 <= 0x63) || o1 != 0x14) continue;
+        if (idx + 2 >= c->n_instr) continue;           /* IndexError: no entry point */
+        const uint8_t o2 = c->op[idx + 2];
+        if (!(o2 >= 0x60 && o2 <= 0x7f)) continue;     /* KeyError: no "argument" */
+        const int64_t entry = argument_int(c, idx + 2);
+        if (entry < 0) continue;
+        for (uint32_t k = 0; k < c->n_instr; ++k)
+            if ((int64_t)c->addr[k] == entry) { c->fent[k] = 1; break; }
+    }
+    return 0;
+}
+
 int orc_load_code(const uint8_t *bc, size_t len, uint32_t *code_id) {
     init_optable();
     if (n_codes >= ORC_MAX_CODES) return -1;
     orc_code *c = &CODES[n_codes];
     memset(c, 0, sizeof *c);
     if (disassemble(bc, len, c)) return -1;
+    if (dispatcher_entries(c)) return -1;
     *code_id = (uint32_t)n_codes++;
+    return 0;
+}
+
+/* The function-entry flags of a loaded code (n_instr bytes, 0/1). */
+int orc_code_fentries(uint32_t id, uint8_t *out) {
+    if (id >= (uint32_t)n_codes) return -1;
+    memcpy(out, CODES[id].fent, CODES[id].n_instr);
     return 0;
 }
 
 void orc_reset_codes(void) {
     for (int i = 0; i < n_codes; ++i) {
         free(CODES[i].bytes); free(CODES[i].op); free(CODES[i].addr); free(CODES[i].push);
+        free(CODES[i].argn); free(CODES[i].fent);
     }
     n_codes = 0;
     memset(COV, 0, sizeof COV);
@@ -412,6 +473,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         uint64_t gmin = h->gas_min[i], gmax = h->gas_max[i];
         const uint64_t txlim = h->gas_limit[i];
         uint32_t new_pc = pc + 1;
+        int jumped = 0;           /* a JUMP / JUMPI successor (manage_cfg) */
         const orc_op *info = &OPT[op];
         int gas_by_table = 1, gas_done = 0;
         uint32_t status = MG_RUNNING, aux = 0;
@@ -673,6 +735,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
             long idx = resolve_jump(c, a);
             if (idx < 0 || c->op[idx] != 0x5b) EXC(MG_EXC_INVALID_JUMP);
             gmin += 8; gmax += 8; new_pc = (uint32_t)idx;
+            jumped = 1;
             break;
         }
         case 0x57: { /* JUMPI (:1558-1636): gas 10 by hand, depth+1 on a taken side */
@@ -685,6 +748,7 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
                 if (idx < 0 || c->op[idx] != 0x5b) STOP_WITH(MG_HALT_DROPPED, 0);
                 gmin += 10; gmax += 10; depth++; new_pc = (uint32_t)idx;
             }
+            jumped = 1;
             break;
         }
         case 0x58: PUSH1(u_from64(c->addr[pc])); break;   /* PC (:1674-1687) */
@@ -713,6 +777,8 @@ static uint32_t run_lane(const mg_lane_soa *h, uint32_t i, const orc_params *p) 
         h->pc[i] = new_pc; h->sp[i] = sp; h->msize[i] = msize; h->depth[i] = depth;
         h->gas_min[i] = gmin; h->gas_max[i] = gmax;
         if (rec_new) h->rec_len[i] = rec_new;
+        /* manage_cfg -> _new_node_state (svm.py:549-637) on a JUMP / JUMPI successor */
+        if (jumped && h->fent && new_pc < c->n_instr && c->fent[new_pc]) h->fent[i] = new_pc;
         continue;
     stop:
         h->status[i] = status; h->aux[i] = aux;

@@ -41,6 +41,14 @@ class OracleEVM:
         lib().orc_code_info(code_id, ctypes.byref(n), ops.ctypes.data, addrs.ctypes.data)
         return ops, addrs
 
+    def code_fentries(self, code_id: int) -> np.ndarray:
+        """uint8[n_instr]: 1 where a JUMP / JUMPI landing switches the function
+        name (the oracle's own restatement of the dispatcher table)."""
+        ops, _ = self.code_table(code_id)
+        out = np.zeros(ops.size, dtype=np.uint8)
+        lib().orc_code_fentries(code_id, out.ctypes.data)
+        return out
+
     def set_coverage(self, code_id: int, buf: Optional[np.ndarray]) -> None:
         """Record into `buf` (uint8[n_instr], kept alive by the caller) the
         instructions lanes of `code_id` start, as the device's mg_coverage."""

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 5: the -m gpu suite, the smoke and the default bench line, as the driver runs them.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/r05${1:-}
+mkdir -p $OUT
+timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
+timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1

@@ -22,6 +22,12 @@ and expected outputs taken from the reference's test suite — never source text
 * state_cases.json  <- tests/laser/state/{calldata,storage,mstate,mstack}_test.py: the
                        module-level parametrize tables (ast.literal_eval) and the
                        fixed cases' literal inputs / expected values
+* easm.json         <- tests/testdata/outputs_expected/*.easm (disassembler_test.py:13-27:
+                       Disassembly(code).get_easm() of tests/testdata/inputs/<name>)
+* signatures.json   <- tests/testdata/input_contracts/*.sol: the text signatures of the
+                       public / external functions and public state-variable getters
+                       (what solc's methodIdentifiers would give SignatureDB.add_sigs,
+                       support/signatures.py:239-250; no solc here), by contract file
 
 Usage:  python tests/golden/make_fixtures.py [--reference /root/reference]
 """
@@ -30,6 +36,7 @@ import ast
 import importlib.util
 import json
 import os
+import re
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
@@ -237,6 +244,75 @@ def make_disassembly(ref: Path):
     return {"code": code, "instructions": count}
 
 
+def make_easm(ref: Path):
+    """disassembler_test.py:13-27: the expected get_easm() text per input."""
+    out = {}
+    for f in sorted((ref / "tests/testdata/outputs_expected").glob("*.easm")):
+        out[f.name[: -len(".easm")]] = f.read_text()
+    return out
+
+
+_CANON = {"uint": "uint256", "int": "int256", "byte": "bytes1"}
+_LOCATIONS = {"memory", "calldata", "storage", "payable", "indexed"}
+
+
+def _canon_type(t: str) -> str:
+    t = t.strip()
+    m = re.match(r"^([A-Za-z_][A-Za-z0-9_]*)(.*)$", t)
+    base, rest = m.group(1), m.group(2)
+    return _CANON.get(base, base) + rest.replace(" ", "")
+
+
+def _param_types(params: str):
+    out = []
+    for p in [x.strip() for x in params.split(",") if x.strip()]:
+        words = [w for w in p.split() if w not in _LOCATIONS]
+        out.append(_canon_type(words[0]))
+    return out
+
+
+def _getter(decl: str):
+    """`T public name` -> name(<key types>): mappings take their keys, arrays
+    a uint256 index (solidity's public getters)."""
+    decl = " ".join(decl.split())
+    m = re.match(r"^(.*)\bpublic\b(?:\s+(?:constant|immutable))?\s+([A-Za-z_][A-Za-z0-9_]*)\s*(=.*)?$", decl)
+    if not m:
+        return None
+    typ, name = m.group(1).strip(), m.group(2)
+    args = []
+    while True:
+        mm = re.match(r"^mapping\s*\(\s*([A-Za-z0-9_]+)\s*=>\s*(.*)\)$", typ)
+        if mm:
+            args.append(_canon_type(mm.group(1)))
+            typ = mm.group(2).strip()
+            continue
+        if typ.endswith("]"):
+            args.append("uint256")
+            typ = typ[: typ.rindex("[")].strip()
+            continue
+        break
+    return f"{name}({','.join(args)})"
+
+
+def make_signatures(ref: Path):
+    """Text signatures of every input contract's external interface."""
+    out = {}
+    for f in sorted((ref / "tests/testdata/input_contracts").glob("*.sol")):
+        src = re.sub(r"//[^\n]*|/\*.*?\*/", "", f.read_text(errors="replace"), flags=re.S)
+        sigs = []
+        for m in re.finditer(r"\bfunction\s+([A-Za-z_][A-Za-z0-9_]*)\s*\(([^)]*)\)([^{;]*)", src):
+            attrs = m.group(3)
+            if re.search(r"\b(public|external)\b", attrs) or not re.search(r"\b(internal|private)\b", attrs):
+                sigs.append(f"{m.group(1)}({','.join(_param_types(m.group(2)))})")
+        for m in re.finditer(r"^\s*((?:mapping\s*\([^;{}]*\)|address|uint|int|bool|bytes|string)[^;(){}]*"
+                             r"\bpublic\b[^;(){}]*);", src, flags=re.M):
+            g = _getter(m.group(1))
+            if g:
+                sigs.append(g)
+        out[f.name] = sorted(set(sigs))
+    return out
+
+
 def make_model_cases(ref: Path):
     """tests/laser/smt/model_test.py:5-56: solver.add(x == BitVecVal(2, 256));
     the model declares x and evaluates it to 2 (decls / __getitem__ / eval)."""
@@ -357,6 +433,8 @@ def main():
         "loop_count.json": make_loop_counts(ref),
         "bytecodes.json": make_bytecodes(ref),
         "state_cases.json": make_state_cases(ref),
+        "easm.json": make_easm(ref),
+        "signatures.json": make_signatures(ref),
         "keccak_kat.json": {
             # keccak_function_manager.py:92 — keccak256(b"") as a decimal integer
             "empty": "89477152217924674838424037953991966239322087453347756267410168184682657981552",
@@ -368,6 +446,15 @@ def main():
                 ["exceptions_0.8.0.sol.o", "Exceptions", 1, 2],
                 ["symbolic_exec_bytecode.sol.o", "AccidentallyKillable", 1, 1],
                 ["extcall.sol.o", "Exceptions", 1, 1],
+            ],
+            # analysis_tests.py:71-82: the same rows under --strategy delayed
+            "delayed": True,
+            # integration_tests/test_safe_functions.py:26-51 (bytecode rows):
+            # `myth safe-functions --bin-runtime -f <file>` -> safe function names
+            "safe_functions": [
+                ["suicide.sol.o", []],
+                ["overflow.sol.o", ["balanceOf(address)", "totalSupply()"]],
+                ["ether_send.sol.o", ["crowdfunding()", "withdrawfunds()", "owner()", "balances(address)"]],
             ],
             "origin_swc": ["origin.sol.o", "115"],
         },

@@ -97,13 +97,14 @@ def _outcomes_of_restatement(engine):
     out = Counter()
     for kind, s in engine.ended:
         c = tuple(x.raw for x in s.world_state.constraints)
+        fn = s.environment.active_function_name
         if kind in ("stop", "return"):
-            out[("txend", False, c)] += 1
+            out[("txend", False, c, fn)] += 1
             out[("ws", c)] += 1
         elif kind == "exception":
-            out[("txend", False, c)] += 1
+            out[("txend", False, c, fn)] += 1
         elif kind == "revert":
-            out[("txend", True, c)] += 1
+            out[("txend", True, c, fn)] += 1
         elif kind == "end":
             out[("ws", c)] += 1
         else:
@@ -137,7 +138,8 @@ def run_both(device, name, monkeypatch):
     laser.escaped_ops = escaped
     got = Counter()
     laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
-        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
+        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints),
+          s.environment.active_function_name)]))
     laser.register_laser_hooks("add_world_state", lambda s: got.update(
         [("ws", tuple(x.raw for x in s.world_state.constraints))]))
     laser.open_states = [ws]
@@ -158,6 +160,7 @@ def run_both(device, name, monkeypatch):
                                 call_value=symbol_factory.BitVecSym(f"call_value{txid}", 256))
     gs = tx.initial_global_state()
     gs.transaction_stack.append((tx, None))
+    gs.world_state.transaction_sequence.append(tx)       # _setup_global_state_for_execution
     gs.world_state.constraints.append(
         Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
     ref_engine.run([gs])
@@ -211,7 +214,8 @@ def run_creation_both(device, name, monkeypatch):
     # a creation keeps its world state only when it returns code (svm.py:459-466):
     # path ends are compared by their transaction_end outcomes
     laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
-        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
+        [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints),
+          s.environment.active_function_name)]))
     tx0 = int(tx_id_manager.get_next_tx_id())
     tx_id_manager.set_counter(tx0 - 1)
     execute_symbolic_contract_creation(laser, code, world_state=ws0)
@@ -221,6 +225,7 @@ def run_creation_both(device, name, monkeypatch):
     tx = _creation_tx(ws_ref, code, txid)
     gs = tx.initial_global_state()
     gs.transaction_stack.append((tx, None))
+    gs.world_state.transaction_sequence.append(tx)       # _setup_global_state_for_execution
     # transaction/symbolic.py:202-219: the caller is one of the actors
     gs.world_state.constraints.append(
         Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))

@@ -823,6 +823,8 @@ class Engine:
                 return
             nxt = []
             for st in work:
+                instrs = st.environment.code.instruction_list
+                op = instrs[st.mstate.pc]["opcode"] if st.mstate.pc < len(instrs) else None
                 try:
                     succ = self.step(st)
                 except Unsupported as e:
@@ -830,9 +832,29 @@ class Engine:
                     continue
                 if len(succ) > 1 and self.pruning is not None:
                     succ = self.pruning(succ)
+                if op in ("JUMP", "JUMPI"):
+                    for t in succ:
+                        _switch_function(t)
                 nxt.extend(succ)
             work = nxt
         raise RuntimeError("restatement did not finish")
+
+
+def _switch_function(state) -> None:
+    """svm.py:549-637 (manage_cfg -> _new_node_state), the function name of a
+    JUMP / JUMPI successor: "constructor" in a creation, the dispatcher entry's
+    name at one of its addresses, "fallback" at address 0."""
+    env = state.environment
+    instrs = env.code.instruction_list
+    if state.mstate.pc >= len(instrs):
+        return
+    address = instrs[state.mstate.pc]["address"]
+    if isinstance(state.world_state.transaction_sequence[-1], ContractCreationTransaction):
+        env.active_function_name = "constructor"
+    elif address in env.code.address_to_function_name:
+        env.active_function_name = env.code.address_to_function_name[address]
+    elif address == 0:
+        env.active_function_name = "fallback"
 
 
 def _symbolic_state(s) -> bool:

@@ -21,7 +21,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(native.SIGNATURES), set(syms) ^ set(native.SIGNATURES)
-    assert lib.mg_abi_version() == 14
+    assert lib.mg_abi_version() == 15
 
 
 def test_device_opcode_table_matches_reference():
