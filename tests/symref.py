@@ -849,7 +849,8 @@ def _switch_function(state) -> None:
     if state.mstate.pc >= len(instrs):
         return
     address = instrs[state.mstate.pc]["address"]
-    if isinstance(state.world_state.transaction_sequence[-1], ContractCreationTransaction):
+    seq = state.world_state.transaction_sequence
+    if seq and isinstance(seq[-1], ContractCreationTransaction):
         env.active_function_name = "constructor"
     elif address in env.code.address_to_function_name:
         env.active_function_name = env.code.address_to_function_name[address]
