@@ -40,7 +40,8 @@ def test_packed_symbolic_state_runs_on_kernel1_and_writes_back(monkeypatch):
                          escape_handler=handler)
         got, ends = Counter(), []
         laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(
-            [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints))]))
+            [("txend", bool(revert), tuple(x.raw for x in s.world_state.constraints),
+              s.environment.active_function_name)]))
         laser.register_laser_hooks("add_world_state", lambda s: (got.update(
             [("ws", tuple(x.raw for x in s.world_state.constraints))]), ends.append(s)))
         laser.work_list.append(bridge.pack_global_state(_symbolic_ref_state(), z))
