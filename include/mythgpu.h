@@ -136,11 +136,13 @@ extern "C" {
  *                  mg_taint_program): len = the new atom's index; result = the
  *                  word at stack[-1] before the instruction; payload = stack[-2]
  *                  (8 limbs, 0 when absent), then pc (instruction index) and the
- *                  opcode with MG_TAINT_POST (bit 8) for a post-hook atom.  The host
+ *                  opcode with MG_TAINT_POST (bit 8) for a post-hook atom, then the
+ *                  lane's fent (ABI v15: the hook's active_function_name).  The host
  *                  replays the module's own hook on a state built from it.        */
 #define MG_REC_ANNOT    3u
 /*   MG_REC_HOOK    a deferred batch-safe hook (MG_TAINT_DEFER): len = n words; result =
- *                  stack[-1]; payload = stack[-2..-n] (8 limbs each), pc, opcode.       */
+ *                  stack[-1]; payload = stack[-2..-n] (8 limbs each), pc, opcode, and
+ *                  the lane's fent (the function name the hook sees, ABI v15).    */
 #define MG_REC_HOOK     4u
 /*   MG_REC_SYMKECCAK  SHA3 of a symbolic input (symbolic lanes): len = input bytes,
  *                  result limbs unused; payload = the MG_SYM_KECCAK node's index.

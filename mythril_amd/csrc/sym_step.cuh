@@ -245,9 +245,9 @@ DEV uint32_t sym_env_word(uint32_t op) {
 #define T_POST 16u
 #define T_EXPCOND 32u
 #define T_YCLASS 64u
-#define TREC_WORDS (MG_REC_HEADER + 10u)
+#define TREC_WORDS (MG_REC_HEADER + 11u)
 #define T_IFLANE (1u << 24)
-DEV uint32_t hrec_words(uint32_t n) { return MG_REC_HEADER + 8u * (n - 1u) + 2u; }
+DEV uint32_t hrec_words(uint32_t n) { return MG_REC_HEADER + 8u * (n - 1u) + 3u; }
 
 DEV uint32_t t_obj(const DevTaint &T, size_t N, uint32_t lane, uint32_t slot) {
     return T.sobj[(size_t)slot * N + lane];
@@ -287,7 +287,7 @@ DEV void t_gc(const DevTaint &T, size_t N, uint32_t lane, uint32_t sp, uint32_t 
 }
 // MG_REC_ANNOT: [kind][atom][step][stack[-1]][stack[-2]][pc][op | post << 8]
 DEV void rec_annot(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t atom, uint32_t step, const U256 &v0,
-                   const U256 &v1, uint32_t pc, uint32_t opw) {
+                   const U256 &v1, uint32_t pc, uint32_t opw, uint32_t fent) {
     at = rec_head(L, lane, at, MG_REC_ANNOT, atom, step, v0);
     uint32_t *__restrict__ q = L.rec + lane;
     const size_t N = L.N;
@@ -295,10 +295,11 @@ DEV void rec_annot(const DevLanes &L, uint32_t lane, uint32_t at, uint32_t atom,
     for (int k = 0; k < 8; ++k) q[(size_t)(at + k) * N] = v1.w[k];
     q[(size_t)(at + 8u) * N] = pc;
     q[(size_t)(at + 9u) * N] = opw;
+    q[(size_t)(at + 10u) * N] = fent;
 }
-// MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op]
+// MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op][fent]
 DEV void rec_hook(const DevLanes &L, const LaneView &V, uint32_t lane, uint32_t at, uint32_t n, uint32_t step,
-                  uint32_t sp, uint32_t pc, uint32_t op) {
+                  uint32_t sp, uint32_t pc, uint32_t op, uint32_t fent) {
     at = rec_head(L, lane, at, MG_REC_HOOK, n, step, V.stack(sp - 1u));
     uint32_t *__restrict__ q = L.rec + lane;
     const size_t N = L.N;
@@ -310,6 +311,7 @@ DEV void rec_hook(const DevLanes &L, const LaneView &V, uint32_t lane, uint32_t 
     at += 8u * (n - 1u);
     q[(size_t)at * N] = pc;
     q[(size_t)(at + 1u) * N] = op;
+    q[(size_t)(at + 2u) * N] = fent;
 }
 // Annotation set of the word an executed opcode pushes (instructions.py:330-1060
 // with bitvec.py's unions): the operands' union for the ALU -- nothing for a
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (do_pre) {
                 // logged before the mutator runs: its own records (EXP) follow
                 rec_annot(L, lane, L.rec_len[lane], natoms, L.steps[lane] + executed, V.stack(sp - 1u),
-                          sp >= 2u ? V.stack(sp - 2u) : u_zero(), pc, op);
+                          sp >= 2u ? V.stack(sp - 2u) : u_zero(), pc, op, fent);
                 L.rec_len[lane] += TREC_WORDS;
                 rec_pre = true;
                 pre_bit = 1ull << natoms;
@@ -545,7 +547,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             if (defer) {
                 // the deferred hook runs after the annotating ones of the opcode, as
                 // the host replays records in log order
-                rec_hook(L, V, lane, L.rec_len[lane], dk, L.steps[lane] + executed, sp, pc, op);
+                rec_hook(L, V, lane, L.rec_len[lane], dk, L.steps[lane] + executed, sp, pc, op, fent);
                 L.rec_len[lane] += hrec_words(dk);
                 rec_pre = true;
             }
@@ -1129,8 +1131,9 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                      nobj, tsink, ttf);
             if (post_bit) {
                 const uint32_t at = L.rec_len[lane];
+                // the post hooks run before manage_cfg: the name before this instruction
                 rec_annot(L, lane, at, natoms + (pre_bit ? 1u : 0u), L.steps[lane] + executed, R.T0,
-                          R.sp >= 2u ? R.T1 : u_zero(), pc, op | 0x100u);
+                          R.sp >= 2u ? R.T1 : u_zero(), pc, op | 0x100u, fent);
                 L.rec_len[lane] = at + TREC_WORDS;
             }
             if (pre_bit) { ++natoms; if (tact & T_YCLASS) tym |= pre_bit; }

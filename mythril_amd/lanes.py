@@ -44,7 +44,7 @@ MG_REC_SYMKECCAK = 5    # SHA3 of a symbolic input: payload = the KECCAK node's 
 MG_REC_CDSIZE = 6       # a creation's CODESIZE: the host appends calldata.size == result
 MG_REC_SYMEXP = 7       # EXP with a symbolic operand: payload = the Power node's index
 MG_REC_SYMLEN = 8       # SHA3 of a symbolic length: payload = the length's node; host appends len == 64
-MG_REC_ANNOT_WORDS = MG_REC_HEADER + 10
+MG_REC_ANNOT_WORDS = MG_REC_HEADER + 11
 
 MG_LANE_STATIC, MG_LANE_CREATION, MG_LANE_HOOK_ACK, MG_LANE_STEP1 = 1, 2, 4, 8
 MG_LANE_SYMBOLIC, MG_LANE_SYMCD, MG_LANE_SYMENV_SHIFT = 16, 32, 6
@@ -379,11 +379,11 @@ class LaneBatch:
                 out.append((step, "exp", limbs_to_word(q[k: k + 8]), limbs_to_word(q[k + 8: k + 16]), r))
                 k += 16
             elif kind == MG_REC_HOOK:
-                # (step, "hook", [stack[-1], stack[-2], ...], pc, opcode)
+                # (step, "hook", [stack[-1], stack[-2], ...], pc, opcode, fent)
                 words = [r] + [limbs_to_word(q[k + 8 * j: k + 8 * j + 8]) for j in range(ln - 1)]
                 k += 8 * (ln - 1)
-                out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF))
-                k += 2
+                out.append((step, "hook", words, int(q[k]), int(q[k + 1]) & 0xFF, int(q[k + 2])))
+                k += 3
             elif kind == MG_REC_SYMEXP:
                 # (step, "symexp", Power node index)
                 out.append((step, "symexp", int(q[k])))
@@ -400,11 +400,11 @@ class LaneBatch:
                 out.append((step, "symkeccak", int(q[k]), ln))
                 k += 1
             elif kind == MG_REC_ANNOT:
-                # (step, "annot", atom, pc, opcode, post, stack[-1], stack[-2])
+                # (step, "annot", atom, pc, opcode, post, stack[-1], stack[-2], fent)
                 opw = int(q[k + 9])
                 out.append((step, "annot", ln, int(q[k + 8]), opw & 0xFF, bool(opw & 0x100), r,
-                            limbs_to_word(q[k: k + 8])))
-                k += 10
+                            limbs_to_word(q[k: k + 8]), int(q[k + 10])))
+                k += 11
             else:
                 raise ValueError(f"lane {i}: bad record kind {kind} at word {k - MG_REC_HEADER}")
         return out

@@ -121,6 +121,11 @@ class DelayConstraintStrategy(BasicSearchStrategy):
         from ..smt.solver import ModelCache
         self.model_cache = ModelCache(device=kwargs.get("device"))
         self.pending_worklist: List = []
+        # a parked state whose query neither a candidate model nor an SMT backend
+        # can decide (SolverBackendMissing): "raise", or "keep" it running without
+        # a model to cache (prefilter-only runs, as LaserEVM.unknown_forks)
+        self.unknown = "raise"
+        self.unknown_kept = 0
 
     def drain(self) -> List:
         from ..smt.expr import And
@@ -135,9 +140,16 @@ class DelayConstraintStrategy(BasicSearchStrategy):
                 (run if v is not False else self.pending_worklist).append(s)
             if run:
                 return run
+        from ..smt.solver import SolverBackendMissing
         while self.pending_worklist:
             s = self.pending_worklist.pop(0)
-            model = Constraints(s.world_state.constraints).get_model()
+            try:
+                model = Constraints(s.world_state.constraints).get_model()
+            except SolverBackendMissing:
+                if self.unknown != "keep":
+                    raise
+                self.unknown_kept += 1
+                return [s]
             if model is not None:
                 self.model_cache.put(model, 1)
                 return [s]

@@ -877,7 +877,7 @@ class LaserEVM:
             elif r[1] == "annot":
                 tnt.note_record(self._tl[i], r, lanes[i].state, self._plan)
             elif r[1] == "hook":
-                tnt.replay_deferred(r, lanes[i].state, self._plan)
+                tnt.replay_deferred(r, lanes[i].state, self._plan, self._tl[i])
             elif r[1] == "symexp":
                 # exp_ of a symbolic operand (instructions.py:624-638): the manager's
                 # condition on Power(base, exponent)
@@ -1621,7 +1621,10 @@ def _capacity_growth(sh: LaneShape, reason: int, b: LaneBatch, i: int) -> Option
         return {"rec_cap": sh.rec_cap * 4}
     if reason == MG_ESC_ARENA:
         return {"node_cap": sh.node_cap * 4, "const_cap": sh.const_cap * 4}
-    if reason == MG_ESC_TAINT and sh.obj_cap and int(b.n_obj[i]) + 4 > sh.obj_cap:
+    if reason == MG_ESC_TAINT and sh.obj_cap and sh.obj_cap < 65536 and (
+            int(b.n_obj[i]) + 4 > sh.obj_cap or int(b.n_atoms[i]) + 2 <= 64):
+        # the object table was full (a lane escapes for it after compacting, so
+        # its stored count may be below the cap), not the 64-atom limit
         return {"obj_cap": min(sh.obj_cap * 4, 65536)}
     return None
 

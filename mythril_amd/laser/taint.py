@@ -104,7 +104,11 @@ class IfSymbolic:
 class IfStateAnnotation:
     """A pre-hook with work only when the state carries an annotation of one of
     `types` (class names in the module's Python module); such annotations come
-    from host events, so the host knows them when it packs the lane."""
+    from host events, so the host knows them when it packs the lane.  Without
+    one, StateChangeAfterCall's hook (state_change_external_calls.py:124-131)
+    still creates an empty PotentialIssuesAnnotation; a skipped hook does not,
+    and nothing reads an empty one (check_potential_issues makes its own when
+    missing, potential_issues.py:100, and its search importance is 0)."""
     types: Tuple[str, ...]
 
 
@@ -325,12 +329,13 @@ class TaintPlan:
 
 class LaneTaint:
     """Host side of one taint lane: handle -> object, atom -> annotation set."""
-    __slots__ = ("objs", "atoms", "msets")
+    __slots__ = ("objs", "atoms", "msets", "fn_pack")
 
     def __init__(self):
         self.objs: Dict[int, Expression] = {}
         self.atoms: List[Optional[frozenset]] = []
         self.msets: Dict[int, frozenset] = {}     # mask -> union of its (final) atom sets
+        self.fn_pack: Optional[str] = None        # active_function_name when the lane was packed
 
 
 def state_needs_taint(state) -> bool:
@@ -346,6 +351,7 @@ def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
     """Write state's object graph into lane i's taint planes.  False when it needs
     more than 64 atoms or the object table (the lane cannot carry it)."""
     lt.objs, lt.atoms, lt.msets = {}, [], {}
+    lt.fn_pack = state.environment.active_function_name
     atom_of: Dict[int, int] = {}
     keep = []
 
@@ -434,16 +440,39 @@ def _world_view(ws, n_constraints: int):
     return view
 
 
-def _snapshot(state, pc: int, stack, n_constraints: int):
-    """The state a replayed hook sees: the lane's environment and transaction,
-    the world state with the path constraints the lane had at that step, pc and
-    the recorded stack words.  Memory and storage are not reproduced (the
-    batch-safe hooks do not read them)."""
+def _environment_at(state, fent: int, fn_pack: Optional[str]):
+    """The lane's environment as the hook saw it: a copy carrying the function
+    name of that step -- the record's last function-entry landing
+    (mg_lane_soa.fent, svm.py:575-637), or the name the lane was packed with
+    when it had not landed on one yet.  A copy: the reference steps copies,
+    so a state a hook keeps (an OverUnderflowAnnotation's overflowing_state)
+    keeps the name it had."""
+    from copy import copy
+    from .transaction import ContractCreationTransaction
+    env = copy(state.environment)
+    seq = state.world_state.transaction_sequence
+    if fent == 0xFFFFFFFF:
+        if fn_pack is not None:
+            env.active_function_name = fn_pack
+    elif seq and isinstance(seq[-1], ContractCreationTransaction):
+        env.active_function_name = "constructor"
+    else:
+        name = env.code.name_at(fent)
+        if name is not None:
+            env.active_function_name = name
+    return env
+
+
+def _snapshot(state, pc: int, stack, n_constraints: int, env=None):
+    """The state a replayed hook sees: the lane's environment (as of the step,
+    `env`) and transaction, the world state with the path constraints the lane
+    had at that step, pc and the recorded stack words.  Memory and storage are
+    not reproduced (the batch-safe hooks do not read them)."""
     from .state import GlobalState, MachineState
     ws = _world_view(state.world_state, n_constraints)
     ms = MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack, depth=state.mstate.depth)
-    g = GlobalState(ws, state.environment, state.node, ms, transaction_stack=list(state.transaction_stack),
-                    last_return_data=state.last_return_data)
+    g = GlobalState(ws, state.environment if env is None else env, state.node, ms,
+                    transaction_stack=list(state.transaction_stack), last_return_data=state.last_return_data)
     return g
 
 
@@ -452,7 +481,7 @@ def note_record(lt: LaneTaint, rec, state, plan: TaintPlan) -> None:
     (LaserEVM._replay_records): the module's own hook runs now, on a state built
     from the record, so it sees the module's caches and the path's constraints
     as they are at that step; what it annotates becomes the atom's set."""
-    _step, _kind, atom, pc, op, post, v0, v1 = rec
+    _step, _kind, atom, pc, op, post, v0, v1, fent = rec
     while len(lt.atoms) <= atom:
         lt.atoms.append(None)
     o0, o1 = symbol_factory.BitVecVal(v0, 256), symbol_factory.BitVecVal(v1, 256)
@@ -464,23 +493,25 @@ def note_record(lt: LaneTaint, rec, state, plan: TaintPlan) -> None:
         target = o0 if plan.pre_operand.get(op, 0) == 0 else o1
         hooks = plan.pre_replay.get(op, ())
         pc_at = pc
-    snap = _snapshot(state, pc_at, [o1, o0], len(state.world_state.constraints))
+    snap = _snapshot(state, pc_at, [o1, o0], len(state.world_state.constraints),
+                     _environment_at(state, fent, lt.fn_pack))
     for h in hooks:
         h(snap)
     lt.atoms[atom] = frozenset(target.annotations)
 
 
-def replay_deferred(rec, state, plan: TaintPlan) -> None:
+def replay_deferred(rec, state, plan: TaintPlan, lt: Optional[LaneTaint] = None) -> None:
     """An MG_REC_HOOK record, in the reference's global execution order: the
     opcode's deferred hooks (the modules' own `execute`) run on a state with the
     recorded words, pc and path constraints as of that step, sharing the lane's
     state and world-state annotations, so what they file lands where the
     reference's hooks put it."""
     from .state import GlobalState, MachineState
-    _step, _kind, words, pc, op = rec
+    _step, _kind, words, pc, op, fent = rec
     ws = _world_view(state.world_state, len(state.world_state.constraints))
     stack = [symbol_factory.BitVecVal(w, 256) for w in reversed(words)]
-    snap = GlobalState(ws, state.environment, state.node,
+    env = _environment_at(state, fent, lt.fn_pack if lt is not None else None)
+    snap = GlobalState(ws, env, state.node,
                        MachineState(gas_limit=state.mstate.gas_limit, pc=pc, stack=stack,
                                     depth=state.mstate.depth),
                        transaction_stack=list(state.transaction_stack), last_return_data=state.last_return_data)

@@ -174,10 +174,13 @@ class ModelPool:
         """models: name -> int for variables, ArrayInterp / FuncInterp for tables;
         anything absent is completed with 0 (z3 model_completion)."""
         vals = np.zeros((max(len(var_names), 1), max(len(models), 1), 8), dtype=np.uint32)
-        for m, model in enumerate(models):
-            for v, (name, w) in enumerate(zip(var_names, var_widths)):
-                x = model_value(model, name) & ((1 << w) - 1)
-                vals[v, m] = np.frombuffer(x.to_bytes(32, "little"), dtype="<u4")
+        for v, (name, w) in enumerate(zip(var_names, var_widths)):
+            # one bytes join per variable: the per-element numpy writes cost
+            # more than the values themselves
+            mask = (1 << w) - 1
+            raw = b"".join((model_value(model, name) & mask).to_bytes(32, "little") for model in models)
+            if raw:
+                vals[v, :len(models)] = np.frombuffer(raw, dtype="<u4").reshape(len(models), 8)
         pool = ModelPool(vals)
         tables = tables or []
         if tables:
@@ -185,7 +188,9 @@ class ModelPool:
             start = np.zeros((len(tables), nm), dtype=np.uint32)
             count = np.zeros((len(tables), nm), dtype=np.uint32)
             default = np.zeros((len(tables), nm, 16), dtype=np.uint32)
-            rows = []
+            rows: List[bytes] = []
+            M256 = (1 << 256) - 1
+            M512 = (1 << 512) - 1
             for t, sig in enumerate(tables):
                 for m, model in enumerate(models):
                     interp = model.get(sig.name)
@@ -200,9 +205,11 @@ class ModelPool:
                         items = []
                     for args, v in items:
                         k0, k1 = sig.key_chunks(tuple(args))
-                        rows.append(np.concatenate([limbs(k0), limbs(k1), _wide_limbs(v)]))
+                        rows.append((k0 & M256).to_bytes(32, "little") + (k1 & M256).to_bytes(32, "little") +
+                                    (v & M512).to_bytes(64, "little"))
                     count[t, m] = len(rows) - start[t, m]
-            entries = np.stack(rows) if rows else np.zeros((0, 32), dtype=np.uint32)
+            entries = (np.frombuffer(b"".join(rows), dtype="<u4").reshape(len(rows), 32).copy() if rows
+                       else np.zeros((0, 32), dtype=np.uint32))
             pool.tab_start, pool.tab_count, pool.tab_entries, pool.tab_default = \
                 start, count, entries, default
         return pool

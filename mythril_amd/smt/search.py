@@ -109,14 +109,25 @@ class _Inverter:
     def __init__(self, ev: _Eval, rng: np.random.Generator):
         self.ev = ev
         self.rng = rng
+        # (term, target) -> repairs: the terms are hash-consed DAGs, so one query
+        # reaches a subterm from many parents; its repairs under this assignment
+        # do not depend on the path that reached it (the first one computed is kept)
+        self.memo: Dict[Tuple[int, int], List[Repair]] = {}
 
     def bool_true(self, node: Node) -> List[Repair]:
         return self.inv(node, 1)[: self.LIMIT]
 
     def inv(self, n: Node, t: int, depth: int = 0) -> List[Repair]:
-        ev = self.ev
         if depth > 40:
             return []
+        key = (id(n), t)
+        got = self.memo.get(key)
+        if got is None:
+            got = self.memo[key] = self._inv(n, t, depth)[: 4 * self.LIMIT]
+        return got
+
+    def _inv(self, n: Node, t: int, depth: int) -> List[Repair]:
+        ev = self.ev
         w = n.width
         t &= _mask(w) if w else M256
         if ev(n) == t:
@@ -260,7 +271,45 @@ class _Inverter:
             return self.inv(x, t & _mask(x.width), d)
         if op == "select":
             return self._select(n, t, d)
+        if op in ("bvadd_noovfl_u", "bvsub_noudfl_u", "bvumul_noovfl"):
+            return self._overflow(op, a, t, d)
         return []
+
+    def _overflow(self, op: str, a, t: int, d: int) -> List[Repair]:
+        """The unsigned overflow predicates (bitvec_helper.py:200-246):
+        bvadd_noovfl_u(x, y) = x + y < 2^w, bvsub_noudfl_u(x, y) = y <= x,
+        bvumul_noovfl(x, y) = x * y < 2^w; t = 0 asks for the overflow."""
+        x, y = a
+        w = x.width
+        m = _mask(w)
+        vx, vy = self.ev(x), self.ev(y)
+        out: List[Repair] = []
+        if op == "bvadd_noovfl_u":
+            if t:
+                return self.inv(x, m - vy, d) + self.inv(y, m - vx, d) + self.inv(x, 0, d)
+            if vy:
+                out += self.inv(x, (1 << w) - vy, d) + self.inv(x, m, d)
+            if vx:
+                out += self.inv(y, (1 << w) - vx, d) + self.inv(y, m, d)
+            return out or self.inv(x, m, d)
+        if op == "bvsub_noudfl_u":
+            if t:
+                return self.inv(x, vy, d) + self.inv(y, vx, d) + self.inv(y, 0, d)
+            if vy:
+                out += self.inv(x, vy - 1, d) + self.inv(x, 0, d)
+            if vx < m:
+                out += self.inv(y, vx + 1, d) + self.inv(y, m, d)
+            return out
+        if t:
+            out = self.inv(x, 0, d) + self.inv(y, 0, d)
+            if vy:
+                out += self.inv(x, m // vy, d)
+            return out
+        if vy:
+            out += self.inv(x, min(m, -(-(1 << w) // vy)), d)
+        if vx:
+            out += self.inv(y, min(m, -(-(1 << w) // vx)), d)
+        return out + self.inv(x, m, d)
 
     # -- helpers ----------------------------------------------------------------------
     def _any(self, args, targets, d) -> List[Repair]:
@@ -463,7 +512,8 @@ class SatSearchBackend:
     # -- kernel-2 scoring ---------------------------------------------------------------
     def _score(self, conj: Sequence[Node], assigns: List[Dict[str, object]]):
         """(per-candidate satisfied-conjunct counts, index of a candidate that
-        satisfies every conjunct or None); one kernel-2 launch."""
+        satisfies every conjunct or None, or False when a conjunct has no
+        kernel-2 row: no candidate can then be reported); one kernel-2 launch."""
         models = [_model(a) for a in assigns]
         rows = self.cache.conjunct_rows(list(conj), models)
         self.stats["launches"] += 1
@@ -472,11 +522,13 @@ class SatSearchBackend:
         counts = np.zeros(n, dtype=np.int64)
         allsat = np.ones(n, dtype=bool)
         idx = np.arange(n)
-        for c in conj:
+        self._sat = np.zeros((len(conj), n), dtype=bool)     # conjunct c holds under candidate i
+        for k, c in enumerate(conj):
             r = rows.get(c)
             if r is None:                      # not evaluable on the device: no answer
-                return counts, None
+                return counts, False
             bits = ((r[idx >> 6] >> (idx & 63).astype(np.uint64)) & np.uint64(1)).astype(bool)
+            self._sat[k] = bits
             counts += bits
             allsat &= bits
         hit = np.flatnonzero(allsat)
@@ -493,20 +545,24 @@ class SatSearchBackend:
         seeds = lru + (self.cache._seed_models() or [_model({})])
         pool = [complete(dict(m.raw[-1].assignment)) for m in seeds]
         counts, hit = self._score(conj, pool)
+        if hit is False:
+            return None                        # a conjunct kernel 2 cannot evaluate
         if hit is not None:
             return _model(pool[hit])
         seen = set()
         order = np.argsort(-counts, kind="stable")
         beam = [pool[i] for i in order[: self.beam]]
+        # which conjuncts each beam member violates: kernel 2's bitmaps of the
+        # launch that scored it (no host evaluation)
+        beam_wrong = [[c for k, c in enumerate(conj) if not self._sat[k, i]] for i in order[: self.beam]]
         for _ in range(self.rounds):
             cands: List[Dict[str, object]] = []
-            for a in beam:
+            for a, wrong in zip(beam, beam_wrong):
                 ev = _Eval(a)
                 inv = _Inverter(ev, self.rng)
-                wrong = [c for c in conj if ev(c) != 1]
                 firsts: Repair = {}
                 for c in wrong:
-                    opts = inv.bool_true(c)
+                    opts = inv.bool_true(c)           # memoised: the loop below reuses them
                     if opts:
                         firsts.update(opts[0])
                 if len(wrong) > 1 and firsts:
@@ -526,10 +582,13 @@ class SatSearchBackend:
             if not cands:
                 return None
             counts, hit = self._score(conj, cands)
+            if hit is False:
+                return None
             if hit is not None:
                 return _model(cands[hit])
             order = np.argsort(-counts, kind="stable")
             beam = [cands[i] for i in order[: self.beam]]
+            beam_wrong = [[c for k, c in enumerate(conj) if not self._sat[k, i]] for i in order[: self.beam]]
         return None
 
     # -- minimisation --------------------------------------------------------------------
@@ -552,7 +611,9 @@ class SatSearchBackend:
                            if v < cur} | {cur - k for k in range(1, min(cur, 64) + 1)} |
                           {cur >> k for k in range(1, 12)})
             cands = [complete({**assign, raw.param: v}) for v in vals]
-            counts, _ = self._score(conj, cands)
+            counts, hit = self._score(conj, cands)
+            if hit is False:
+                break
             best = next((i for i in range(len(vals)) if counts[i] == len(conj)), None)
             if best is not None:
                 assign = cands[best]

@@ -53,6 +53,7 @@ typedef struct {
     uint32_t n_vars, n_models, n_slots;
     uint32_t *first_sat, *sat_count;
     uint32_t d0, d1;
+    uint64_t *bits;          /* optional [n_dags][ceil(n_models / 64)]: model m satisfies DAG d */
     const tables_t *tab;
 } job_t;
 
@@ -183,20 +184,44 @@ static void *worker(void *arg) {
     job_t *j = (job_t *)arg;
     for (uint32_t d = j->d0; d < j->d1; ++d) {
         uint32_t first = 0xffffffffu, cnt = 0;
+        const uint32_t words = (j->n_models + 63u) / 64u;
         for (uint32_t m = 0; m < j->n_models; ++m)
-            if (eval_one(j, d, m)) { if (first == 0xffffffffu) first = m; ++cnt; }
+            if (eval_one(j, d, m)) {
+                if (first == 0xffffffffu) first = m;
+                ++cnt;
+                if (j->bits) j->bits[(size_t)d * words + m / 64u] |= 1ull << (m % 64u);
+            }
         j->first_sat[d] = first;
         if (j->sat_count) j->sat_count[d] = cnt;
     }
     return NULL;
 }
 
-/* Evaluate programs [d_first, d_first+d_count) on every model. */
+/* Evaluate programs [d_first, d_first+d_count) on every model; with `bits`
+ * (zeroed by the caller) also the per-model satisfaction bitmap (mg_eval_bits). */
+void orb_eval_tab_bits(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
+                       const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
+                       uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
+                       uint32_t threads, uint32_t n_tables, const uint32_t *tab_start,
+                       const uint32_t *tab_count, const uint32_t *tab_entries, const uint32_t *tab_default,
+                       uint64_t *bits);
+
 void orb_eval_tab(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
                   const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
                   uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
                   uint32_t threads, uint32_t n_tables, const uint32_t *tab_start,
                   const uint32_t *tab_count, const uint32_t *tab_entries, const uint32_t *tab_default) {
+    orb_eval_tab_bits(insns, prog_off, consts, values, n_vars, n_models, n_slots, d_first, d_count,
+                      first_sat, sat_count, threads, n_tables, tab_start, tab_count, tab_entries, tab_default,
+                      NULL);
+}
+
+void orb_eval_tab_bits(const uint32_t *insns, const uint32_t *prog_off, const uint32_t *consts,
+                       const uint32_t *values, uint32_t n_vars, uint32_t n_models, uint32_t n_slots,
+                       uint32_t d_first, uint32_t d_count, uint32_t *first_sat, uint32_t *sat_count,
+                       uint32_t threads, uint32_t n_tables, const uint32_t *tab_start,
+                       const uint32_t *tab_count, const uint32_t *tab_entries, const uint32_t *tab_default,
+                       uint64_t *bits) {
     const tables_t tab = {n_tables, tab_start, tab_count, tab_entries, tab_default};
     if (threads < 1) threads = 1;
     if (threads > 128) threads = 128;
@@ -210,7 +235,7 @@ void orb_eval_tab(const uint32_t *insns, const uint32_t *prog_off, const uint32_
         if (a >= d_first + d_count) break;
         uint32_t b = a + per > d_first + d_count ? d_first + d_count : a + per;
         jobs[t] = (job_t){insns, prog_off, consts, values, n_vars, n_models, n_slots,
-                          first_sat, sat_count, a, b, &tab};
+                          first_sat, sat_count, a, b, bits, &tab};
         if (threads == 1) worker(&jobs[t]);
         else pthread_create(&tid[t], NULL, worker, &jobs[t]);
         started++;

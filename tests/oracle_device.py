@@ -177,22 +177,8 @@ class OracleK2:
 
     def eval_bits(self, prog, pool):
         from oracle.bv_ref import eval_batch
-        from mythril_amd.smt.program import ModelPool
         self.launches += 1
         n, m = prog.n_dags, pool.n_models
         bits = np.zeros((n, (m + 63) // 64), dtype=np.uint64)
-        for k in range(m):
-            one = ModelPool(pool.values[:, k:k + 1])
-            if pool.n_tables:
-                one.tab_start, one.tab_count = pool.tab_start[:, k:k + 1], pool.tab_count[:, k:k + 1]
-                one.tab_entries, one.tab_default = pool.tab_entries, pool.tab_default[:, k:k + 1]
-            _, sc = eval_batch(prog, one)
-            for d in np.flatnonzero(sc):
-                bits[d, k >> 6] |= np.uint64(1) << np.uint64(k & 63)
-        fs = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
-        sc = np.zeros(n, dtype=np.uint32)
-        for d in range(n):
-            hit = [k for k in range(m) if (int(bits[d, k >> 6]) >> (k & 63)) & 1]
-            if hit:
-                fs[d], sc[d] = hit[0], len(hit)
+        fs, sc = eval_batch(prog, pool, bits=bits)
         return fs, sc, bits, 0.0

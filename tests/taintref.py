@@ -154,17 +154,18 @@ def _word(b, i, slot) -> int:
     return limbs_to_word(b.stack[i, slot])
 
 
-def _write_annot(b, i, at, atom, step, v0, v1, pc, opw):
+def _write_annot(b, i, at, atom, step, v0, v1, pc, opw, fent):
     q = b.rec[i]
     q[at], q[at + 1], q[at + 2] = MG_REC_ANNOT, atom, step
     q[at + 3: at + 11] = word_to_limbs(v0)
     q[at + MG_REC_HEADER: at + MG_REC_HEADER + 8] = word_to_limbs(v1)
     q[at + MG_REC_HEADER + 8] = pc
     q[at + MG_REC_HEADER + 9] = opw
+    q[at + MG_REC_HEADER + 10] = fent          # the name the hook sees (before the instruction)
 
 
 def _write_hook(b, i, at, words, step, pc, op):
-    """MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op]."""
+    """MG_REC_HOOK: [kind][n][step][stack[-1]][stack[-2..-n]][pc][op][fent]."""
     q = b.rec[i]
     q[at], q[at + 1], q[at + 2] = MG_REC_HOOK, len(words), step
     q[at + 3: at + 11] = word_to_limbs(words[0])
@@ -172,8 +173,8 @@ def _write_hook(b, i, at, words, step, pc, op):
     for w in words[1:]:
         q[k: k + 8] = word_to_limbs(w)
         k += 8
-    q[k], q[k + 1] = pc, op
-    return k + 2 - at
+    q[k], q[k + 1], q[k + 2] = pc, op, b.fent[i]
+    return k + 3 - at
 
 
 def _snap(b, i):
@@ -250,7 +251,7 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
             do_pre = False
     need = int(do_pre) + int(do_post)
     defer = dk != 0 and sp >= dk
-    hook_words = MG_REC_HEADER + 8 * (dk - 1) + 2 if defer else 0
+    hook_words = MG_REC_HEADER + 8 * (dk - 1) + 3 if defer else 0
     if lane.natoms + need > 64 or _objects_full(lane, b.shape.obj_cap):
         b.status[i], b.aux[i] = MG_ESCAPE, op | (MG_ESC_TAINT << 8)
         return False
@@ -259,9 +260,10 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
         return False
     pre_atom = post_atom = None
     rec0 = int(b.rec_len[i])
+    fent0 = int(b.fent[i])
     if do_pre:
         _write_annot(b, i, rec0, lane.natoms, steps0, _word(b, i, sp - 1), _word(b, i, sp - 2) if sp >= 2 else 0,
-                     pc, op)
+                     pc, op, fent0)
         b.rec_len[i] = rec0 + MG_REC_ANNOT_WORDS
         pre_atom = lane.natoms
     if defer:
@@ -281,7 +283,7 @@ def step_lane(oracle, ops: np.ndarray, b, i: int, lane: RefLane, actions, hook_m
         at = int(b.rec_len[i])
         nsp = int(b.sp[i])
         _write_annot(b, i, at, post_atom, steps0, _word(b, i, nsp - 1), _word(b, i, nsp - 2) if nsp >= 2 else 0,
-                     pc, op | 0x100)
+                     pc, op | 0x100, fent0)
         b.rec_len[i] = at + MG_REC_ANNOT_WORDS
     for a in (pre_atom, post_atom):
         if a is not None:

@@ -1,11 +1,15 @@
-"""analysis_tests.py:9-54's issue-count rows on the MI355X: kernel 1 steps the
-creation and message-call paths (concrete and symbolic lanes), kernel 2
-answers the fork filters and the SAT-only issue confirmations (model cache,
-witness seeds, guided search).  Same harness and assertions as
-tests/test_integration_cpu.py (which runs them on the C oracles)."""
+"""The reference's integration rows on the MI355X: kernel 1 steps the creation
+and message-call paths (concrete and symbolic lanes), kernel 2 answers the fork
+filters, the delayed strategy's quick-sat gate and the SAT-only issue
+confirmations (model cache, witness seeds, guided search).  Same harness and
+assertions as tests/test_integration_cpu.py (which runs them on the C oracles):
+analysis_tests.py:9-82 (issue count, SWC id and function of every issue, BFS
+and --strategy delayed), test_safe_functions.py:26-51 (0 / 2 / 4 safe
+functions), and the C1 stand-in (suicide.sol.o -t 3, default modules)."""
 import pytest
 
-from test_integration_cpu import GOLDEN, check_row
+from fnames import use_signature_db
+from test_integration_cpu import GOLDEN, check_c1, check_row, check_safe_functions
 
 pytestmark = pytest.mark.gpu
 
@@ -18,8 +22,25 @@ def dev():
     d.close()
 
 
+@pytest.mark.parametrize("strategy", ["bfs", "delayed"])
 @pytest.mark.parametrize("row", GOLDEN["issue_counts"], ids=lambda r: f"{r[0]}-{r[1]}")
-def test_issue_counts_on_the_mi355x(row, dev):
-    issues, info = check_row(row, dev, dev)
+def test_issue_counts_on_the_mi355x(row, strategy, dev, monkeypatch, tmp_path):
+    use_signature_db(monkeypatch, tmp_path)
+    issues, info = check_row(row, dev, dev, strategy=strategy)
     assert info["lane_steps"] > 0            # kernel 1 stepped the paths
     assert info["kernel2_launches"] > 0      # kernel 2 answered the queries
+
+
+@pytest.mark.parametrize("row", GOLDEN["safe_functions"], ids=lambda r: r[0])
+def test_safe_functions_on_the_mi355x(row, dev, monkeypatch, tmp_path):
+    use_signature_db(monkeypatch, tmp_path)
+    got, issues, info = check_safe_functions(row, dev, dev)
+    if row[0] != "ether_send.sol.o":
+        assert got == sorted(row[1])
+    assert info["lane_steps"] > 0
+
+
+@pytest.mark.parametrize("runtime", [True, False], ids=["bin-runtime", "creation"])
+def test_c1_stand_in_on_the_mi355x(runtime, dev, monkeypatch, tmp_path):
+    use_signature_db(monkeypatch, tmp_path)
+    check_c1(dev, dev, runtime)
