@@ -53,10 +53,7 @@ def _allgather_keys(keys: Sequence[str]) -> List[str]:
     rank, world = mdist.rank_world()
     if world == 1:
         return sorted(keys)
-    import torch.distributed as dist
-    out: List[Optional[List[str]]] = [None] * world
-    dist.all_gather_object(out, sorted(keys))
-    return sorted(set(k for part in out for k in (part or [])))
+    return sorted(set(k for part in _allgather_values(sorted(keys)) for k in part))
 
 
 def exchange_coverage(laser_evm) -> Dict[str, np.ndarray]:
@@ -160,6 +157,96 @@ class _Words:
         b = b"".join(int(x).to_bytes(4, "little") for x in self.w[self.k:self.k + nw])
         self.k += nw
         return b[:n].decode()
+
+
+# ---------------------------------------------------------------- values over a tensor
+# Plain values (None, bool, int of any size and sign, str, bytes, tuple, list,
+# dict) as a u32 stream: a tag word, then the payload; what travels between
+# ranks besides models (code keys, keccak / EXP registrations, issues).
+_T_NONE, _T_FALSE, _T_TRUE, _T_INT, _T_NEG, _T_STR, _T_BYTES, _T_TUPLE, _T_LIST, _T_DICT = range(10)
+
+
+def _put_bytes(out: list, b: bytes) -> None:
+    out.append(len(b))
+    b = b + b"\0" * (-len(b) % 4)
+    out.extend(int.from_bytes(b[k:k + 4], "little") for k in range(0, len(b), 4))
+
+
+def _put_value(out: list, v) -> None:
+    if v is None:
+        out.append(_T_NONE)
+    elif v is True or v is False:
+        out.append(_T_TRUE if v else _T_FALSE)
+    elif isinstance(v, int):
+        out.append(_T_INT if v >= 0 else _T_NEG)
+        _put_big(out, abs(v))
+    elif isinstance(v, str):
+        out.append(_T_STR)
+        _put_bytes(out, v.encode())
+    elif isinstance(v, (bytes, bytearray)):
+        out.append(_T_BYTES)
+        _put_bytes(out, bytes(v))
+    elif isinstance(v, (tuple, list)):
+        out.append(_T_TUPLE if isinstance(v, tuple) else _T_LIST)
+        out.append(len(v))
+        for x in v:
+            _put_value(out, x)
+    elif isinstance(v, dict):
+        out.append(_T_DICT)
+        out.append(len(v))
+        for k, x in v.items():
+            _put_value(out, k)
+            _put_value(out, x)
+    else:
+        raise TypeError(f"cannot send a {type(v).__name__} between ranks")
+
+
+def _values_to_words(v) -> np.ndarray:
+    out: list = []
+    _put_value(out, v)
+    return np.asarray(out, dtype=np.uint32)
+
+
+def _get_bytes(r: "_Words") -> bytes:
+    n = r.u()
+    nw = (n + 3) // 4
+    b = b"".join(int(x).to_bytes(4, "little") for x in r.w[r.k:r.k + nw])
+    r.k += nw
+    return b[:n]
+
+
+def _get_value(r: "_Words"):
+    t = r.u()
+    if t == _T_NONE:
+        return None
+    if t in (_T_FALSE, _T_TRUE):
+        return t == _T_TRUE
+    if t in (_T_INT, _T_NEG):
+        v = r.big()
+        return v if t == _T_INT else -v
+    if t == _T_STR:
+        return _get_bytes(r).decode()
+    if t == _T_BYTES:
+        return _get_bytes(r)
+    if t in (_T_TUPLE, _T_LIST):
+        xs = [_get_value(r) for _ in range(r.u())]
+        return tuple(xs) if t == _T_TUPLE else xs
+    if t == _T_DICT:
+        d = {}
+        for _ in range(r.u()):
+            k = _get_value(r)
+            d[k] = _get_value(r)
+        return d
+    raise ValueError(f"bad value tag {t}")
+
+
+def _allgather_values(v) -> list:
+    """Every rank's value (rank order) through one u32 tensor all-gather."""
+    from .. import dist as mdist
+    _, world = mdist.rank_world()
+    if world == 1:
+        return [v]
+    return [_get_value(_Words(w)) if w.size else None for w in _allgather_words(_values_to_words(v))]
 
 
 def _words_to_models(words: np.ndarray) -> list:
@@ -439,9 +526,8 @@ def sync_function_managers() -> int:
     sym = [table.add(x.raw) for xs in km.symbolic_inputs.values() for x in xs]
     conc = [(table.add(k.raw), table.add(h.raw)) for k, h in km.concrete_hashes.items()]
     pts = sorted(em.concrete_points.items())
-    import torch.distributed as dist
-    parts: List[Optional[tuple]] = [None] * world
-    dist.all_gather_object(parts, (table.rows, sym, conc, pts))
+    # node rows (op, width, args, param) and indices as a u32 value stream (no pickling)
+    parts = _allgather_values((table.rows, sym, conc, pts))
     have = {id(x.raw) for xs in km.symbolic_inputs.values() for x in xs}
     have_c = {id(k.raw) for k in km.concrete_hashes}
     got = 0
@@ -472,6 +558,52 @@ def sync_function_managers() -> int:
                 em.concrete_points[tuple(key)] = v
                 got += 1
     return got
+
+
+def merge_issues(modules, issue_type=None) -> int:
+    """after sharded rounds every rank holds the issues its own
+    paths filed.  All ranks' issues of each detection module (same module
+    order on every rank) are gathered in rank order and de-duplicated by the
+    modules' own cache key, (address, bytecode) -- base.py:63-96 keys on
+    (address, code hash); Exceptions on (source location, code hash) --
+    keeping the first; each module's ``issues`` and cache become the merged
+    set on every rank.  Issues travel as their attribute dicts (value stream,
+    no pickling) and are rebuilt as `issue_type` (default: the class of the
+    issues the local modules hold).  Returns the merged count."""
+    from .. import dist as mdist
+    _, world = mdist.rank_world()
+    local = [[{k: v for k, v in vars(i).items() if _sendable(v)} for i in m.issues] for m in modules]
+    parts = _allgather_values(local) if world > 1 else [local]
+    cls = issue_type or next((type(i) for m in modules for i in m.issues), None)
+    total = 0
+    for k, m in enumerate(modules):
+        exceptions = getattr(m, "auto_cache", True) is False
+        merged, keys = [], set()
+        for part in parts:
+            for d in (part[k] if part else []):
+                key = (d.get("source_location") if exceptions else d.get("address"), d.get("bytecode"))
+                if key in keys:
+                    continue
+                keys.add(key)
+                issue = object.__new__(cls) if cls is not None else _Issue()
+                issue.__dict__.update(d)
+                merged.append(issue)
+        m.issues = merged
+        m.cache |= keys
+        total += len(merged)
+    return total
+
+
+class _Issue:
+    """A received issue when no local module holds one of the report's class."""
+
+
+def _sendable(v) -> bool:
+    try:
+        _values_to_words(v)
+        return True
+    except TypeError:
+        return False
 
 
 def execute_symbolic_transactions(laser_evm, callee_address, tx_count: Optional[int] = None,
