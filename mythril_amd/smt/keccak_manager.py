@@ -81,6 +81,15 @@ class KeccakFunctionManager:
         self.concrete_hashes[bv] = h
         return h
 
+    def assign_intervals(self) -> None:
+        """The interval hooks create_conditions assigns (sizes in first-use
+        order), without building the conditions (search.complete needs only
+        the intervals)."""
+        for length in self.symbolic_inputs:
+            if length not in self.interval_hook_for_size:
+                self.interval_hook_for_size[length] = self._index_counter
+                self._index_counter -= INTERVAL_DIFFERENCE
+
     def create_conditions(self) -> Bool:
         condition = symbol_factory.Bool(True)
         for inputs_list in self.symbolic_inputs.values():

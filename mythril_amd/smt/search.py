@@ -40,7 +40,8 @@ import numpy as np
 from .expr import Node
 from .program import ArrayInterp, FuncInterp
 from .semantics import apply_op
-from .solver import Model, ModelRef, SolverBackendMissing, _conjuncts, query_raw
+from .refute import refutes
+from .solver import Model, ModelRef, SolverBackendMissing, UnsatError, _conjuncts, query_raw
 
 M256 = (1 << 256) - 1
 
@@ -273,7 +274,26 @@ class _Inverter:
             return self._select(n, t, d)
         if op in ("bvadd_noovfl_u", "bvsub_noudfl_u", "bvumul_noovfl"):
             return self._overflow(op, a, t, d)
+        if op == "uf":
+            return self._uf(n, t, d)
         return []
+
+    def _uf(self, n: Node, t: int, d: int) -> List[Repair]:
+        """f(args) := t for an uninterpreted function (keccak256_N, Power): the
+        interpretation holds no free choice (complete() rebuilds it from the
+        axioms), but another application with value t does -- move the
+        arguments to that application's key (a mapping slot keyed by a sender
+        made equal to one keyed by a calldata address, say)."""
+        it = self.ev.a.get(n.param[0])
+        if not isinstance(it, FuncInterp):
+            return []
+        out: List[Repair] = []
+        for key, v in it.entries.items():
+            if v == t and len(key) == len(n.args):
+                out += self._all(list(n.args), list(key), d)
+                if len(out) >= self.LIMIT:
+                    break
+        return out
 
     def _overflow(self, op: str, a, t: int, d: int) -> List[Repair]:
         """The unsigned overflow predicates (bitvec_helper.py:200-246):
@@ -396,6 +416,8 @@ class _Inverter:
             kv = self.ev(k)
             if kv != vi and (self.ev(v) == t or len(out) < 4):
                 out += self.inv(idx, kv, d)
+                if self.ev(v) == t:
+                    out += self.inv(k, vi, d)          # or the store's key to the index
         return out
 
 
@@ -436,14 +458,13 @@ def complete(assign: Dict[str, object]) -> Dict[str, object]:
     for (n, cv), h in concrete.items():
         tabs.setdefault(f"keccak256_{n}", FuncInterp(0, {})).entries[(cv,)] = h
         tabs.setdefault(f"keccak256_{n}-1", FuncInterp(0, {})).entries[(h,)] = cv
-    if km.symbolic_inputs:
-        km.create_conditions()          # intervals in the reference's order
+    km.assign_intervals()               # intervals in the reference's order
     fresh: Dict[int, int] = {}
     for n, xs in km.symbolic_inputs.items():
-        for x in xs:
-            f = tabs.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
-            inv = tabs.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
-            v = ev(x.raw)
+        f = tabs.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
+        inv = tabs.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
+        for x in dict.fromkeys(x.raw for x in xs):      # registered once per SHA3 executed
+            v = ev(x)
             if (v,) in f.entries:
                 continue
             h = concrete.get((n, v))
@@ -482,19 +503,23 @@ class SatSearchBackend:
     uses_seeds = True          # get_model consults the seeds before calling it
 
     def __init__(self, cache, search: bool = True, rounds: int = 12, beam: int = 6,
-                 max_candidates: int = 4096, seed: int = 0x5EA5C4):
+                 max_candidates: int = 4096, patience: int = 3, seed: int = 0x5EA5C4):
         self.cache = cache
         self.search = search
         self.rounds = rounds
         self.beam = beam
         self.max_candidates = max_candidates
+        self.patience = patience       # rounds without a better best count before giving up
         self.rng = np.random.default_rng(seed)
-        self.stats: Dict[str, int] = {"calls": 0, "seed": 0, "search": 0, "unknown": 0,
+        self.stats: Dict[str, int] = {"calls": 0, "refuted": 0, "seed": 0, "search": 0, "unknown": 0,
                                       "candidates": 0, "launches": 0, "minimised": 0}
 
     def __call__(self, constraints, minimize, maximize, timeout):
         self.stats["calls"] += 1
         key = query_raw(constraints)
+        if refutes(_conjuncts(key)):
+            self.stats["refuted"] += 1
+            raise UnsatError
         model = self.cache.check_seeds(key)
         if model is not None:
             self.stats["seed"] += 1
@@ -550,6 +575,7 @@ class SatSearchBackend:
         if hit is not None:
             return _model(pool[hit])
         seen = set()
+        best, stall = int(counts.max()), 0
         order = np.argsort(-counts, kind="stable")
         beam = [pool[i] for i in order[: self.beam]]
         # which conjuncts each beam member violates: kernel 2's bitmaps of the
@@ -586,6 +612,10 @@ class SatSearchBackend:
                 return None
             if hit is not None:
                 return _model(cands[hit])
+            top = int(counts.max())
+            best, stall = (top, 0) if top > best else (best, stall + 1)
+            if stall >= self.patience:
+                return None                    # no round has come closer: unknown
             order = np.argsort(-counts, kind="stable")
             beam = [cands[i] for i in order[: self.beam]]
             beam_wrong = [[c for k, c in enumerate(conj) if not self._sat[k, i]] for i in order[: self.beam]]

@@ -297,7 +297,9 @@ def _getter(decl: str):
 def make_signatures(ref: Path):
     """Text signatures of every input contract's external interface."""
     out = {}
-    for f in sorted((ref / "tests/testdata/input_contracts").glob("*.sol")):
+    files = sorted((ref / "tests/testdata/input_contracts").glob("*.sol"))
+    files += sorted((ref / "solidity_examples").glob("*.sol"))
+    for f in files:
         src = re.sub(r"//[^\n]*|/\*.*?\*/", "", f.read_text(errors="replace"), flags=re.S)
         sigs = []
         for m in re.finditer(r"\bfunction\s+([A-Za-z_][A-Za-z0-9_]*)\s*\(([^)]*)\)([^{;]*)", src):
@@ -309,7 +311,8 @@ def make_signatures(ref: Path):
             g = _getter(m.group(1))
             if g:
                 sigs.append(g)
-        out[f.name] = sorted(set(sigs))
+        key = f.name if f.parent.name == "input_contracts" else f"{f.parent.name}/{f.name}"
+        out[key] = sorted(set(sigs))
     return out
 
 

@@ -5,11 +5,12 @@ confirmations (model cache, witness seeds, guided search).  Same harness and
 assertions as tests/test_integration_cpu.py (which runs them on the C oracles):
 analysis_tests.py:9-82 (issue count, SWC id and function of every issue, BFS
 and --strategy delayed), test_safe_functions.py:26-51 (0 / 2 / 4 safe
-functions), and the C1 stand-in (suicide.sol.o -t 3, default modules)."""
+functions), the C1 stand-in (suicide.sol.o -t 3, default modules) and
+KillBilly -t 3 (tests/killbilly.py)."""
 import pytest
 
 from fnames import use_signature_db
-from test_integration_cpu import GOLDEN, check_c1, check_row, check_safe_functions
+from test_integration_cpu import GOLDEN, check_c1, check_killbilly, check_row, check_safe_functions
 
 pytestmark = pytest.mark.gpu
 
@@ -44,3 +45,9 @@ def test_safe_functions_on_the_mi355x(row, dev, monkeypatch, tmp_path):
 def test_c1_stand_in_on_the_mi355x(runtime, dev, monkeypatch, tmp_path):
     use_signature_db(monkeypatch, tmp_path)
     check_c1(dev, dev, runtime)
+
+
+def test_killbilly_on_the_mi355x(dev, monkeypatch, tmp_path):
+    use_signature_db(monkeypatch, tmp_path)
+    issues, info = check_killbilly(dev, dev)
+    assert info["lane_steps"] > 0 and info["kernel2_launches"] > 0

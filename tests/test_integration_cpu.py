@@ -20,6 +20,12 @@ runs the same rows on the MI355X).
   deployed (--bin-runtime, the deployed ``kill(address)``) and as ``-f``
   creation code (the reference runs the runtime code as its constructor: the
   issue's function is ``constructor``).
+* The README's C1 case itself, ``myth analyze killbilly.sol -t 3``: there is no
+  solc here, so tests/killbilly.py assembles the contract from its source; the
+  one issue is SWC-106 in commencekilling(), reached by killerize(attacker),
+  activatekillability(), commencekilling() from the attacker -- the mapping
+  slot keccak(addr . 1) written in transaction 1 must be the slot
+  keccak(msg.sender . 1) read in transaction 2.
 
 Function names come from a signature database holding the input contracts'
 text signatures (tests/golden/signatures.json), as the reference's
@@ -126,3 +132,27 @@ def test_c1_stand_in_on_the_oracle_device(runtime, monkeypatch, tmp_path):
     from oracle_device import OracleDevice, OracleK2
     use_signature_db(monkeypatch, tmp_path)
     check_c1(OracleDevice(), OracleK2(), runtime)
+
+
+def check_killbilly(device, k2):
+    import analyze
+    import killbilly
+    issues, info = analyze.analyze("killbilly", None, 3, device, k2, code=killbilly.creation())
+    assert info["escapes_dropped"] == 0, info
+    assert [(i.swc_id, i.function, i.title) for i in issues] == \
+        [("106", "commencekilling()", "Unprotected Selfdestruct")], (analyze.issue_table(issues), info)
+    assert issues[0].address == killbilly.selfdestruct_address()
+    steps = issues[0].transaction_sequence["steps"]
+    attacker = int(steps[-1]["origin"], 16)
+    assert [s["input"][:10] for s in steps[1:]] == \
+        ["0x%08x" % killbilly.selector(f) for f in ("killerize(address)", "activatekillability()",
+                                                     "commencekilling()")]
+    assert int(steps[1]["input"][10:74], 16) & ((1 << 160) - 1) == attacker
+    assert all(int(s["origin"], 16) == attacker for s in steps[1:])
+    return issues, info
+
+
+def test_killbilly_on_the_oracle_device(monkeypatch, tmp_path):
+    from oracle_device import OracleDevice, OracleK2
+    use_signature_db(monkeypatch, tmp_path)
+    check_killbilly(OracleDevice(), OracleK2())
