@@ -266,14 +266,17 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
     symb = None
     if args.symbolic_replicas and gpu and not args.profile_only:
         _log(rank, f"symbolic transactions (-t {args.symbolic_tx}, {args.symbolic_replicas} replicas)")
+        sys.path.insert(0, str(ROOT / "tests"))
+        import symref
         symb = host_profiled("symbolic_tx", lambda: run_symbolic_tx(
-            dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models, log=lambda m: _log(rank, m)))
+            dev, args.symbolic_replicas, args.symbolic_tx, args.seed_models, log=lambda m: _log(rank, m),
+            escape_handler=symref.Engine(signals=True).step))
 
     analyses = None
     if args.analyses and gpu and not args.profile_only:
-        _log(rank, f"18-contract analyses (-t {args.analyses})")
-        analyses = host_profiled("analyses", lambda: run_analyses(
-            dev, args.analyses, args.seed_models, log=lambda m: _log(rank, m)))
+        _log(rank, f"myth analyze over the 18 contracts (-t {args.analyses})")
+        analyses = host_profiled("myth_analyze", lambda: run_myth_analyze(
+            dev, args.analyses, log=lambda m: _log(rank, m), cpu=not args.no_cpu_baseline))
 
     c4 = None
     if not args.no_c4:
@@ -284,6 +287,10 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         value = total_steps / elapsed
         steps_per_batch = lane_steps / max(args.steps, 1)
         kms = float(np.mean(kernel_ms)) if kernel_ms else 0.0
+        if roof and roof.get("issue_floor") and kms > 0:
+            fl = roof["issue_floor"]
+            fl["ceiling_lane_steps_per_s"] = steps_per_batch / (kms / 1e3) / fl["busy_frac"]
+            fl["frac"] = (total_steps / elapsed / world) / fl["ceiling_lane_steps_per_s"]
         out = {
             "metric": "EVM lane-steps/s (kernel 1, C2: 65,536 concrete lanes/GPU, token.sol runtime)",
             "value": value,
@@ -333,7 +340,7 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         if symb is not None:
             out["symbolic_tx"] = symb
         if analyses is not None:
-            out["analyses"] = analyses
+            out["myth_analyze"] = analyses
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.destroy_process_group()
@@ -756,7 +763,8 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     out = {"metric": "in-situ constraint-evals/s of the fork and reachability filters (kernel 2) "
                      "+ symbolic lane-steps/s (kernel 1)",
            "mode": "prefilter-only: no SMT backend in the image; queries no candidate satisfies "
-                   "are UNKNOWN and their paths kept; escaped paths dropped (counted)",
+                   "are UNKNOWN and their paths kept; escapes stepped by the handler given "
+                   "(bench: tests/symref.py), else dropped (counted)",
            "transactions": tx_count, "replicas_per_gpu": replicas, "seed_models": n_seeds, "contracts": {}}
     saved_cache = solver.model_cache
     try:
@@ -829,87 +837,111 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     return out
 
 
-def run_analyses(dev, tx_count: int, n_seeds: int, log=None, escape_handler=None, names=None):
-    """The 18 reference contracts (tests/testdata/inputs/*.sol.o, the inputs of
-    analysis_tests.py and the graph/statespace tests) analysed as ``myth
-    analyze -f <code> -t tx_count`` explores them (analysis/symbolic.py:82-200:
-    creator and attacker accounts, BFS + BoundedLoopsStrategy(3), max depth
-    128, a symbolic creation then tx_count symbolic message calls), with the
-    fork filter and the reachability filter on kernel 2 over the model cache
-    plus ``n_seeds`` witness seeds.  No detection modules and no SMT backend:
-    a query no candidate satisfies is UNKNOWN and its path kept; escaped paths
-    (no host handler for CALL*, SELFDESTRUCT, ...) are dropped and counted.
-    With N ranks the contracts are dealt round-robin (total work fixed); the
-    whole-job rates sum the ranks' work over the slowest rank's wall time."""
+def _myth_analyze_rows(device, k2, tx_count: int, names, log=None):
+    """tests/analyze.py over `names`: per contract the issue table, the
+    confirmations (sat / unknown), escapes dropped, wall / kernel time and the
+    in-situ rates."""
+    import analyze
+    rows = {}
+    for name in names:
+        gc.collect()
+        if log:
+            log(f"myth_analyze: {name}")
+        issues, info = analyze.analyze(name, None, tx_count, device, k2)
+        k1_s = info["device_ms"] / 1e3
+        k2_s = info["k2_ms"] / 1e3
+        rows[name] = {"issues": [list(r) for r in analyze.issue_table(issues)],
+                      "confirmations": info["confirmations"], "escapes_dropped": info["escapes_dropped"],
+                      "wall_s": info["wall_s"], "kernel1_s": k1_s, "kernel2_s": k2_s,
+                      "lane_steps": int(info["lane_steps"]), "constraint_evals": int(info["device_evals"]),
+                      "launches_kernel2": int(info["kernel2_launches"]), "forks": info["forks"],
+                      "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown")},
+                      "constraint_evals_per_s_wall": info["device_evals"] / info["wall_s"] if info["wall_s"] else None}
+    return rows
+
+
+def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True):
+    """C3-shaped (BECToken needs solc, the reference's 18
+    precompiled test contracts stand in): ``myth analyze -f <code> -t tx_count``
+    with every detection module, as tests/analyze.py runs the reference's
+    integration rows -- symbolic creation then tx_count symbolic message calls,
+    BFS + BoundedLoopsStrategy(3), max depth 128, the mutation pruner, the
+    modules' hooks (tests/refmodules.py, restated: the reference's modules need
+    z3), the fork and reachability filters and every issue confirmation on
+    kernel 2 (SAT-only backend: model cache, witness seeds, guided search and
+    the keccak-axiom refutations; an unconfirmed issue stays "unknown",
+    counted), escapes stepped by the tests/symref.py handler so no path is
+    dropped.  Contracts are dealt round-robin over the ranks (total work
+    fixed).  The CPU comparator runs the same harness on rank 0 with the C
+    oracles as kernels 1 and 2 (oracle/evm_ref.c single-threaded,
+    oracle/bv_ref.c on up to 16 threads) and reports whether the issue sets
+    agree."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+    import tempfile
+    import fnames
     from mythril_amd import dist as mdist
     from mythril_amd import workloads
-    from mythril_amd.laser import (Account, BoundedLoopsStrategy, BreadthFirstSearchStrategy, LaserEVM,
-                                   WorldState)
-    from mythril_amd.laser.transaction import ACTORS, tx_id_manager
-    from mythril_amd.laser.witness import WitnessSeeds
-    from mythril_amd.smt import solver
-    from mythril_amd.smt.exponent_manager import exponent_function_manager
-    from mythril_amd.smt.keccak_manager import keccak_function_manager
+    from mythril_amd.laser.disassembly import SignatureDB
     rank, world = mdist.rank_world()
     names = sorted(names or workloads.bytecode_names())
-    per, tot = {}, {"wall_s": 0.0, "kernel1_s": 0.0, "kernel2_s": 0.0, "lane_steps": 0, "queries": 0,
-                    "answered": 0, "unknown": 0, "constraint_evals": 0, "escapes_dropped": 0,
-                    "forks": 0, "pruned": 0}
-    saved_cache = solver.model_cache
-    try:
-        for name in names[rank::world]:
-            gc.collect()
-            keccak_function_manager.reset()
-            exponent_function_manager.reset()
-            tx_id_manager.restart_counter()
-            solver.get_model.cache_clear()
-            code = workloads.bytecode(name)
-            mc = solver.ModelCache(device=dev)
-            mc.seed_source = WitnessSeeds([code], n=n_seeds, balance_names=["balance"])
-            solver.model_cache = mc
-            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, max_depth=128,
-                             execution_timeout=86400, create_timeout=10, transaction_count=tx_count,
-                             requires_statespace=False, escape_handler=escape_handler)
-            laser.unknown_forks = "keep"
-            laser.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
-            ws = WorldState()
-            for actor in ("CREATOR", "ATTACKER"):
-                ws.put_account(Account(ACTORS[actor], contract_name=None))
-            if log:
-                log(f"analyses: {name}")
-            t0 = time.perf_counter()
-            laser.sym_exec(world_state=ws, creation_code=code, contract_name="MAIN")
-            wall = time.perf_counter() - t0
-            st = mc.stats
-            row = {"wall_s": wall, "kernel1_s": laser.device_ms / 1e3, "kernel2_s": mc.device_ms / 1e3,
-                   "lane_steps": int(laser.lane_steps), "queries": st["queries"],
-                   "answered": st["lru_hits"] + st["seed_hits"], "unknown": st["misses"],
-                   "constraint_evals": int(mc.device_evals), "escapes_dropped": laser.escapes_dropped,
-                   "forks": laser.forks, "pruned": laser.fork_stats.get("pruned", 0),
-                   "open_states": len(laser.open_states)}
-            per[name] = row
-            for k in tot:
-                tot[k] += row[k]
-    finally:
-        solver.model_cache = saved_cache
-        keccak_function_manager.reset()
-        exponent_function_manager.reset()
-        tx_id_manager.restart_counter()
-        solver.get_model.cache_clear()
+    saved_dir = os.environ.get("MYTHRIL_DIR")
+    with tempfile.TemporaryDirectory() as sigdir:
+        # the signature database the reference builds by importing the inputs'
+        # sources (function names of the issues)
+        fnames.signature_db(Path(sigdir))
+        os.environ["MYTHRIL_DIR"] = sigdir
+        SignatureDB._reset()
+        try:
+            rows = _myth_analyze_rows(dev, dev, tx_count, names[rank::world], log)
+            cpu_rows = None
+            if cpu and rank == 0 and world == 1:
+                from oracle_device import OracleDevice, OracleK2
+                cpu_rows = _myth_analyze_rows(OracleDevice(), OracleK2(), tx_count, names, log)
+        finally:
+            if saved_dir is None:
+                os.environ.pop("MYTHRIL_DIR", None)
+            else:
+                os.environ["MYTHRIL_DIR"] = saved_dir
+            SignatureDB._reset()
+    tot = {k: sum(r[k] for r in rows.values()) for k in ("wall_s", "kernel1_s", "kernel2_s", "lane_steps",
+                                                         "constraint_evals", "escapes_dropped")}
+    tot["issues"] = sum(len(r["issues"]) for r in rows.values())
+    tot["unknown_confirmations"] = sum(r["confirmations"]["unknown"] for r in rows.values())
     job_wall, job_evals = mdist.reduce_timing(tot["wall_s"], float(tot["constraint_evals"]))
-    _, job_steps = mdist.reduce_timing(tot["wall_s"], float(tot["lane_steps"]))
-    _, job_q = mdist.reduce_timing(tot["wall_s"], float(tot["queries"]))
-    _, job_a = mdist.reduce_timing(tot["wall_s"], float(tot["answered"]))
-    return {"metric": "in-situ constraint-evals/s of the fork and reachability filters over the 18 "
-                      "reference contracts, -t %d" % tx_count,
-            "mode": "prefilter-only (no SMT backend, no detection modules); escaped paths dropped (counted)",
-            "transactions": tx_count, "seed_models": n_seeds, "contracts_analysed": len(per),
-            "ranks": world, "totals": tot,
-            "job_wall_s": job_wall, "job_constraint_evals_per_s_wall": job_evals / job_wall if job_wall else None,
-            "job_lane_steps_per_s": job_steps / job_wall if job_wall else None,
-            "prefilter_hit_rate": job_a / job_q if job_q else None,
-            "host_fraction": 1.0 - (tot["kernel1_s"] + tot["kernel2_s"]) / tot["wall_s"] if tot["wall_s"] else None,
-            "contracts": per}
+    out = {"metric": "myth analyze -f <code> -t %d, all detection modules, over the 18 reference "
+                     "contracts: contracts/s and in-situ constraint-evals/s" % tx_count,
+           "mode": "modules on; SAT-only confirmations on kernel 2 (unknowns counted); escapes stepped "
+                   "by the tests/symref.py handler",
+           "transactions": tx_count, "contracts_analysed": len(rows), "ranks": world, "totals": tot,
+           "job_wall_s": job_wall, "contracts_per_s": len(names) / job_wall if job_wall else None,
+           "job_constraint_evals_per_s_wall": job_evals / job_wall if job_wall else None,
+           "host_fraction": 1.0 - (tot["kernel1_s"] + tot["kernel2_s"]) / tot["wall_s"] if tot["wall_s"] else None,
+           "contracts": rows}
+    if cpu_rows is not None:
+        import platform
+        cw = sum(r["wall_s"] for r in cpu_rows.values())
+        mismatched = sorted(n for n in rows if rows[n]["issues"] != cpu_rows[n]["issues"])
+        out["cpu_baseline"] = {
+            "value": len(cpu_rows) / cw, "unit": "contracts/s", "wall_s": cw,
+            "cores": min(16, os.cpu_count() or 1), "kind": "port",
+            "sample": "the same 18 analyses, host layer + oracle/evm_ref.c (1 thread) as kernel 1 + "
+                      "oracle/bv_ref.c (%d threads) as kernel 2 (%s)" % (min(16, os.cpu_count() or 1),
+                                                                         _cpu_model() or platform.processor()),
+            "issue_sets_match": not mismatched, "mismatched": mismatched,
+            "wall_s_per_contract": {n: r["wall_s"] for n, r in cpu_rows.items()},
+            "unknown_confirmations": sum(r["confirmations"]["unknown"] for r in cpu_rows.values())}
+        out["speedup_vs_cpu"] = cw / tot["wall_s"] if tot["wall_s"] else None
+    return out
+
+
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
 
 
 def run_c4(args, dev, rank, world, barrier, dist_on):

@@ -48,7 +48,7 @@ def sustained_peaks():
 def with_sustained(roof: dict) -> dict:
     """Add peak_sustained / frac_sustained for the roofline's bound."""
     hbm, valu = sustained_peaks()
-    peak = hbm if roof["bound"] == "hbm" else valu
+    peak = hbm if roof.get("priced_as", roof["bound"]) == "hbm" else valu
     if peak:
         roof["peak_sustained"] = peak
         roof["frac_sustained"] = roof["achieved"] / peak
@@ -170,12 +170,18 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
     valu_frac = tops / VALU_PEAK_TOPS
     primary_hbm = hbm_frac >= valu_frac
     traffic, traffic_src = pmc_traffic("k_lane_step")
-    return with_sustained({
+    sq, sq_src = sq_per_wave("k_lane_step")
+    traffic_frac = (traffic / sec / 1e9 / HBM_PEAK_GBS) if traffic else None
+    roof = with_sustained({
         # SURVEY §8(d) prices a lane-step's stack words as bytes moved; kernel 1
-        # keeps them in registers and LDS, so the HBM fraction below is an
-        # algorithmic one.  `traffic_frac` is the measured HBM fraction, and the
-        # kernel's real bound at C2 is latency (one wave per SIMD): DESIGN.md §3.1.
-        "bound": "hbm" if primary_hbm else "valu-int32",
+        # keeps them in registers and LDS, so `frac` (algorithmic bytes over the
+        # HBM peak) is an accounting fraction.  The measured bound at C2 is
+        # latency: one wave per SIMD, half its cycles parked in s_waitcnt
+        # (counter_fracs).
+        "bound": "latency",
+        "frac_basis": ("§8(d) algorithmic bytes / HBM peak" if primary_hbm
+                       else "§8(d) algorithmic int32 ops / INT32 VALU peak"),
+        "priced_as": "hbm" if primary_hbm else "valu-int32",
         "achieved": gbs if primary_hbm else tops,
         "peak": HBM_PEAK_GBS if primary_hbm else VALU_PEAK_TOPS,
         "unit": "GB/s" if primary_hbm else "T int32-ops/s",
@@ -183,7 +189,7 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
         "traffic": traffic,
         "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
         "traffic_source": traffic_src,
-        "traffic_frac": (traffic / sec / 1e9 / HBM_PEAK_GBS) if traffic else None,
+        "traffic_frac": traffic_frac,
         "latency_bound": "65,536 lanes = 1,024 waves = one wave per SIMD: the slowest wave's "
                          "dependent dispatch chain sets the launch time (DESIGN.md §3.1)",
         "kernel": "k_lane_step",
@@ -197,3 +203,41 @@ def lane_step_roofline(dev, batch, code_id, kernel_ms: float) -> dict:
                 "peak": VALU_PEAK_TOPS if primary_hbm else HBM_PEAK_GBS,
                 "frac": valu_frac if primary_hbm else hbm_frac},
     })
+    # what the counters say the kernel uses: measured HBM bytes over the peak,
+    # int32 ops over the VALU peak, and the share of wave cycles parked in
+    # s_waitcnt (SQ_WAIT_ANY / SQ_WAVE_CYCLES) -- none near 1: latency
+    roof["counter_fracs"] = {"hbm_traffic": traffic_frac, "int32_valu": valu_frac,
+                             "sq_wait_any": sq.get("wait_any_frac") if sq else None,
+                             "sq_issue_stall": sq.get("wait_inst_frac") if sq else None,
+                             "sq_source": sq_src}
+    floor = issue_floor()
+    if floor:
+        roof["issue_floor"] = floor
+    return roof
+
+
+def sq_per_wave(kernel: str):
+    """The newest committed SQ per-wave summary of `kernel`
+    (profiles/rNN/prof/sq_per_wave.json).  (record, source) or (None, None)."""
+    for d in sorted(PROFILES.glob("r*"), reverse=True):
+        f = d / "prof" / "sq_per_wave.json"
+        if f.is_file():
+            try:
+                rec = json.loads(f.read_text()).get(kernel)
+            except (OSError, ValueError):
+                rec = None
+            if rec:
+                return rec, str(f.relative_to(PROFILES.parent))
+    return None, None
+
+
+def issue_floor():
+    """Kernel 1's single-batch issue-bound ceiling (a C2 wave
+    whose every s_waitcnt were hidden still takes its issue and issue-stall
+    cycles): lane-steps/s, from the SQ summary and the launch it was taken on."""
+    sq, src = sq_per_wave("k_lane_step")
+    if not sq:
+        return None
+    busy = 1.0 - float(sq["wait_any_frac"])
+    return {"busy_frac": busy, "note": "ceiling = measured lane-steps/s / busy_frac at the same launch "
+                                       "(waits hidden, issue unchanged)", "source": src}

@@ -95,7 +95,7 @@ def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, s
                 "escapes_dropped": laser.escapes_dropped, "confirmations": dict(refmodules.CONFIRMATIONS),
                 "cache": dict(mc.stats), "search": dict(backend.stats),
                 "kernel2_launches": mc.launches, "device_evals": mc.device_evals,
-                "device_ms": laser.device_ms, "modules": [type(m).__name__ for m in mods]}
+                "device_ms": laser.device_ms, "k2_ms": mc.device_ms, "modules": [type(m).__name__ for m in mods]}
         return issues, info
     finally:
         solver.model_cache, _, svm_mod.check_potential_issues = saved
