@@ -465,7 +465,10 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
              !(((op == 0x47u && (flags & LANE_SYMBAL) && symlane) || (op == 0x31u && (flags & LANE_BALANCE) && symlane) ||
                 ((op == 0x5au || op == 0x41u || op == 0x42u || op == 0x44u) && symlane) ||
                 ((op == 0x43u || op == 0x46u) && (flags & LANE_SYMBLOCK) && symlane)) && !tl)) ||
-            (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD)))) {
+            // a creation's CODESIZE / CODECOPY / CALLDATA* run below only on a
+            // symbolic-calldata lane without taint (the block that implements them
+            // skips taint lanes); anywhere else the host steps them
+            (creation && (uy & PD_CREATION) && !(symlane && (flags & LANE_SYMCD) && !tl))) {
             status = ST_ESCAPE; aux = op | (ESC_OPCODE << 8); break;
         }
         const uint32_t req = d.y & 15u, npop = (d.y >> 4) & 15u;

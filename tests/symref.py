@@ -106,6 +106,10 @@ def _word_at(calldata, off):
     return Concat(*parts)
 
 
+# pops k, pushes 1, but the pushed word is not an operation on the popped ones
+# (a load from memory, storage, calldata or the environment at that index)
+_NO_ANN_UNION = {"MLOAD", "SLOAD", "CALLDATALOAD", "BALANCE", "EXTCODESIZE", "EXTCODEHASH", "BLOCKHASH"}
+
 _SYM_ENV = {0x30: "address", 0x33: "sender", 0x32: "origin", 0x34: "callvalue", 0x3A: "gasprice"}
 
 
@@ -218,6 +222,13 @@ class Engine:
         # words below the instruction's reach keep their (maybe symbolic) objects
         for k in range(min(new_sp, len(old) - self._touched)):
             out[k] = old[k]
+        if self._touched and new_sp == len(old) - self._touched + 1 and op_name not in _NO_ANN_UNION:
+            # one word pushed for the words consumed: every BitVec operation
+            # unions its operands' annotations (bitvec.py:63-136), concrete
+            # operands included
+            ann = frozenset().union(*(getattr(x, "annotations", frozenset()) for x in old[-self._touched:]))
+            if ann:
+                out[-1].annotations = out[-1].annotations | ann
         n.mstate.stack = MachineStack(out)
         # memory: the oracle's bytes; symbolic bytes stay unless the instruction
         # wrote over them (CALLDATACOPY, CODECOPY: the bytes they copied)
@@ -382,10 +393,23 @@ class Engine:
         ms = s.mstate
         off, length = ms.stack.pop(), ms.stack.pop()
         tx = s.current_transaction
-        if op == 0xF3 and isinstance(tx, ContractCreationTransaction):
-            raise Unsupported("a creation returning code at a symbolic range")
         if op == 0xF3 and _val(length) is not None and ms.min_gas_used >= min(_gas_limit(s), 10 ** 9 + 1):
             return self._vmexc(state)      # mem_extend + check_gas_usage_limit (:1869-1870)
+        if op == 0xF3 and isinstance(tx, ContractCreationTransaction):
+            # return_ then ContractCreationTransaction.end (transaction_models.py:
+            # 265-284): a symbolic length returns one fresh symbolic byte, a
+            # symbolic offset the bytes at simplify(offset + k); unless every byte
+            # is an int the creation installs no code (return_data None)
+            n = _val(length)
+            data = None
+            if n is not None:
+                got = ms.memory[off: off + BVV(n, 256)] if n else []
+                if got and all(isinstance(x, int) for x in got):
+                    data = bytes(got)
+            if self.signals:
+                tx.end(s, return_data=data, revert=False)
+            self.ended.append(("return", s))
+            return []
         if self.signals:
             tx.end(s, return_data=None, revert=op == 0xFD)
         self.ended.append(("revert" if op == 0xFD else "return", s))

@@ -51,3 +51,19 @@ def test_killbilly_on_the_mi355x(dev, monkeypatch, tmp_path):
     use_signature_db(monkeypatch, tmp_path)
     issues, info = check_killbilly(dev, dev)
     assert info["lane_steps"] > 0 and info["kernel2_launches"] > 0
+
+
+@pytest.mark.parametrize("name", sorted(__import__("mythril_amd.workloads", fromlist=["x"]).bytecode_names()))
+def test_all_modules_issue_set_equals_the_oracle_devices(name, dev, monkeypatch, tmp_path):
+    """``myth analyze -f <code> -t 2`` with every module (bench.py's myth_analyze
+    field): kernels 1 and 2 on the MI355X file the issue set the same harness
+    files on the C oracles, where every symbolic instruction is the host
+    restatement's (tests/symref.py) -- taint lanes, symbolic lanes and their
+    escapes included."""
+    import analyze
+    from oracle_device import OracleDevice, OracleK2
+    use_signature_db(monkeypatch, tmp_path)
+    gi, ginfo = analyze.analyze(name, None, 2, dev, dev)
+    ci, cinfo = analyze.analyze(name, None, 2, OracleDevice(), OracleK2())
+    assert analyze.issue_table(gi) == analyze.issue_table(ci), (ginfo, cinfo)
+    assert ginfo["escapes_dropped"] == cinfo["escapes_dropped"]
