@@ -13,6 +13,8 @@ kernel 1 steps it.  ``to_lane``/``from_lane`` convert between the two.
 """
 from __future__ import annotations
 
+import weakref
+
 from copy import copy
 from typing import Dict, List, Optional, Union
 
@@ -375,7 +377,11 @@ class Memory:
 def memory_key(raw: Node) -> Node:
     """The key ``simplify(index)`` gives a symbolic memory index (memory.py:
     167,200): the constants of a chain of bit-vector additions summed into one
-    trailing constant (0 dropped), the other operands in their order."""
+    trailing constant (0 dropped), the other operands in a canonical order (z3
+    sorts the arguments of an associative-commutative operator, so ``a + b``
+    and ``b + a`` are one key there too).  The order is structural (the terms'
+    printed form), the same in every process, so a memory map that moved to
+    another rank keys its bytes as that rank's reads do."""
     terms, c = [], 0
     stack = [raw]
     while stack:
@@ -386,12 +392,24 @@ def memory_key(raw: Node) -> Node:
             c = (c + n.param) & M256
         else:
             terms.append(n)
+    if len(terms) > 1:
+        terms.sort(key=_term_order)
     acc = terms[0] if terms else None
     for t in terms[1:]:
         acc = Node("bvadd", 256, (acc, t))
     if acc is None:
         return _const_node(c)
     return acc if c == 0 else Node("bvadd", 256, (acc, _const_node(c)))
+
+
+_ORDER: "weakref.WeakKeyDictionary[Node, str]" = weakref.WeakKeyDictionary()
+
+
+def _term_order(n: Node) -> str:
+    k = _ORDER.get(n)
+    if k is None:
+        k = _ORDER[n] = repr(n)
+    return k
 
 
 def _const_node(c: int) -> Node:

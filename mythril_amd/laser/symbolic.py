@@ -316,8 +316,7 @@ class _Decoder:
         if kind == MG_SYM_MLOADK:
             # over the byte map the writes before this node made: get_word_at(offset)
             # (MLOAD), or the data SHA3 hashes, simplify(Concat(memory[offset:+w]))
-            mem = Memory()
-            self.replay_keys(mem, k)
+            mem = self._key_memory(k)
             off = self.ref(y)
             if w == 0:
                 return mem.get_word_at(off)
@@ -326,15 +325,42 @@ class _Decoder:
             return simplify_concat(data) if len(data) > 1 else data[0]
         raise NotEncodable(f"unknown arena node kind {kind}")
 
+    def _key_memory(self, upto: int):
+        """The byte map of the MSTOREK events below node `upto`, for an MLOADK
+        read: replayed incrementally (nodes decode in arena order, so each
+        event is applied once per lane decode), afresh only for a read below
+        the map's current point.  Reads never change the map."""
+        km = getattr(self, "_kmem", None)
+        if km is None or km[1] > upto:
+            km = (Memory(), 0)
+        mem, at = km
+        for j in range(at, upto):
+            # published before the event's operands decode: an MLOADK among them
+            # (below j) finds the map past its point and replays afresh
+            self._kmem = (mem, j)
+            self._apply_key_event(mem, self.row(j))
+        self._kmem = (mem, upto)
+        return mem
+
+    def _has_key_writes(self) -> bool:
+        """Whether the lane's arena holds an MSTOREK event (one vectorised test
+        of the node plane's kind bytes, without decoding any row)."""
+        if not self.n_nodes:
+            return False
+        kinds = np.asarray(self.b.node[self.i, :self.n_nodes, 0]) & 0xFF
+        return bool((kinds == MG_SYM_MSTOREK).any())
+
     def replay_keys(self, mem, upto: int) -> None:
         """Apply the lane's writes at symbolic offsets (MG_SYM_MSTOREK events of
         nodes [0, upto), in arena order = execution order) to `mem`: MSTORE's
         write_word_at, MSTORE8's low byte, a host-encoded byte (memory.py:84-115,
         instructions.py:1454-1493)."""
         for j in range(upto):
-            x, y, z, w = self.row(j)
-            if x & 0xFF != MG_SYM_MSTOREK:
-                continue
+            self._apply_key_event(mem, self.row(j))
+
+    def _apply_key_event(self, mem, row) -> None:
+        x, y, z, w = row
+        if x & 0xFF == MG_SYM_MSTOREK:
             off, val = self.ref(y), self.ref(z)
             if w == 1:
                 mem.write_word_at(off, val)
@@ -358,7 +384,7 @@ class _Decoder:
                 word = self.node(node)
                 symb[int(p)] = word if word.size() == 8 else Extract(255 - 8 * j, 248 - 8 * j, word)
         mem = Memory(bytes(b.memory[i, :msize]), symb)
-        if any(r[0] & 0xFF == MG_SYM_MSTOREK for r in (self.row(k) for k in range(self.n_nodes))):
+        if self._has_key_writes():
             self.replay_keys(mem, self.n_nodes)
         return mem
 
