@@ -412,6 +412,8 @@ struct StepEnv {
     uint32_t lane, tid, ws, win, flags, sflag, psflag, prof;
     uint32_t mw;
     uint32_t sn;         // s_pd holds instructions [0, sn) (the END sentinel included when staged whole)
+    uint32_t tosmem;     // the caller keeps the stack's top two words in memory too (k_sym_step):
+                         // no spill of T1 below a push
 };
 
 // Executes the instruction decoded as (uk, ux) for one lane, exactly as the
@@ -748,7 +750,7 @@ __device__ __forceinline__ void slow_step(LaneRegs &R, const StepEnv &E, uint32_
             if (nsp + 1u > L.stack_cap) ESCX(ESC_STACK)
             GASCOMMIT()
             if (npop == 0u) {            // T1 moves below the register window
-                if (sp >= 2u) V.set_stack(sp - 2u, b);
+                if (sp >= 2u && !E.tosmem) V.set_stack(sp - 2u, b);
                 R.T1 = a;
             } else if (npop >= 2u) {
                 R.T1 = sp >= npop + 1u ? V.stack(sp - npop - 1u) : u_zero();
@@ -1081,7 +1083,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
     const uint8_t *__restrict__ gops = a8 + C.op_off;
     const uint8_t *__restrict__ gfent = a8 + C.fent_off;
     const StepEnv E{&L, C, a8, a32, s_win, s_mw, s_pd, s_push, s_prof, s_kc + (threadIdx.x >> 6) * KC_WAVE,
-                    txlim, glim, lane, tid, lanes_pb, win, flags, sflag, psflag, prof ? 1u : 0u, mw, sn};
+                    txlim, glim, lane, tid, lanes_pb, win, flags, sflag, psflag, prof ? 1u : 0u, mw, sn, 0u};
 
     // Decode the instruction at pc and run the checks svm.execute_state makes
     // before evaluating it (svm.py:369-402): depth cut-off, past-the-end pc,

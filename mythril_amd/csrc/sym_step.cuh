@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
     const LaneView V{L, lane, nullptr, 0u, threadIdx.x, 256u, nullptr, 0u};
     const StepEnv E{&L, C, a8, a32, nullptr, nullptr, nullptr, nullptr, nullptr,
                     s_kc + (threadIdx.x >> 6) * KC_WAVE, txlim, glim, lane, threadIdx.x, 256u, 0u, flags,
-                    0u, 0u, 0u, 0u, 0u};
+                    0u, 0u, 0u, 0u, 0u, 1u};
 
     // optional opcode histogram (mg_step_profile; profiling passes only): the
     // previous instruction is counted once `executed` shows it completed
@@ -1122,8 +1122,11 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
             else if (u_fits32(pb) && pb.w[0] < C.n_bytes) n = min(C.n_bytes - pb.w[0], c.w[0]);
             for (uint32_t j = 0; j < n; ++j) set_mtag(S, N, lane, pa.w[0] + j, 0u);
         }
-        if (R.sp >= 1u) V.set_stack(R.sp - 1u, R.T0);
-        if (R.sp >= 2u) V.set_stack(R.sp - 2u, R.T1);
+        // the stack in memory is the truth here (no register window): write back
+        // only the words the instruction changed -- the new top of a push or a
+        // SWAP, and the second word of SWAP1 (SWAPn wrote its deep slot itself)
+        if (R.sp >= 1u && (pushes || kind == K_SWAP)) V.set_stack(R.sp - 1u, R.T0);
+        if (R.sp >= 2u && op == 0x90u) V.set_stack(R.sp - 2u, R.T1);
         if (symlane) {
             if (kind == K_DUP) sym_set_tag(S, N, lane, R.sp - 1u, t_in0);
             else if (kind == K_SWAP) { sym_set_tag(S, N, lane, sp - 1u, t_in1); sym_set_tag(S, N, lane, sp - nin, t_in0); }

@@ -16,10 +16,10 @@
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
-#define S2(a, b) asm volatile("s_add_u32 %0, %0, %2\n\ts_xor_b32 %1, %1, %2" : "+s"(a), "+s"(b) : "s"(k));
+#define S2(a, b) asm volatile("s_add_u32 %0, %0, %2\n\ts_xor_b32 %1, %1, %2" : "+s"(a), "+s"(b) : "s"(k) : "scc");
 #define V2(a, b) asm volatile("v_add_u32 %0, %0, %2\n\tv_xor_b32 %1, %1, %2" : "+v"(a), "+v"(b) : "v"(kv));
 
-__global__ __launch_bounds__(1024) void k_salu(uint32_t *out, uint32_t iters, uint32_t seed) {
+__global__ __launch_bounds__(256) void k_salu(uint32_t *out, uint32_t iters, uint32_t seed) {
     uint32_t k = __builtin_amdgcn_readfirstlane(seed | 1u);
     uint32_t a0 = k, a1 = k + 1, a2 = k + 2, a3 = k + 3, a4 = k + 4, a5 = k + 5, a6 = k + 6, a7 = k + 7;
     uint32_t b0 = k, b1 = k ^ 1, b2 = k ^ 2, b3 = k ^ 3, b4 = k ^ 4, b5 = k ^ 5, b6 = k ^ 6, b7 = k ^ 7;
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(1024) void k_salu(uint32_t *out, uint32_t iters, ui
     if (r == 0x9e3779b9u) out[blockIdx.x] = r;
 }
 
-__global__ __launch_bounds__(1024) void k_valu(uint32_t *out, uint32_t iters, uint32_t seed) {
+__global__ __launch_bounds__(256) void k_valu(uint32_t *out, uint32_t iters, uint32_t seed) {
     uint32_t kv = seed | 1u;
     uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
              a7 = a0 + 7;
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(1024) void k_valu(uint32_t *out, uint32_t iters, ui
     if (r == 0x9e3779b9u) out[blockIdx.x] = r;
 }
 
-__global__ __launch_bounds__(1024) void k_mix(uint32_t *out, uint32_t iters, uint32_t seed) {
+__global__ __launch_bounds__(256) void k_mix(uint32_t *out, uint32_t iters, uint32_t seed) {
     uint32_t k = __builtin_amdgcn_readfirstlane(seed | 1u);
     uint32_t kv = seed | 1u;
     uint32_t a0 = k, a1 = k + 1, a2 = k + 2, a3 = k + 3, b0 = k, b1 = k ^ 1, b2 = k ^ 2, b3 = k ^ 3;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(1024) void k_mix(uint32_t *out, uint32_t iters, uin
 
 #define BR() asm volatile("s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n1:" : : "s"(k) : "scc");
 
-__global__ __launch_bounds__(1024) void k_branch(uint32_t *out, uint32_t iters, uint32_t seed) {
+__global__ __launch_bounds__(256) void k_branch(uint32_t *out, uint32_t iters, uint32_t seed) {
     uint32_t k = __builtin_amdgcn_readfirstlane(seed | 1u);
     for (uint32_t i = 0; i < iters; ++i) {
         BR() BR() BR() BR() BR() BR() BR() BR()
@@ -101,13 +101,13 @@ int main() {
     for (int kk = 0; kk < 4; ++kk) {
         printf("%s\"%s\": {", kk ? ", " : "", names[kk]);
         for (int wps = 1; wps <= 8; wps *= 2) {
-            // one block of 4 x wps waves per CU: wps waves on each SIMD
-            const uint32_t threads = 256u * (uint32_t)wps;
+            // wps blocks of 4 waves per CU: wps waves on each SIMD
+            const uint32_t threads = 256u, nblk = (uint32_t)cus * (uint32_t)wps;
             auto launch = [&] {
-                if (kk == 0) hipLaunchKernelGGL(k_salu, dim3(cus), dim3(threads), 0, 0, out, iters, 7u);
-                if (kk == 1) hipLaunchKernelGGL(k_valu, dim3(cus), dim3(threads), 0, 0, out, iters, 7u);
-                if (kk == 2) hipLaunchKernelGGL(k_mix, dim3(cus), dim3(threads), 0, 0, out, iters, 7u);
-                if (kk == 3) hipLaunchKernelGGL(k_branch, dim3(cus), dim3(threads), 0, 0, out, iters, 7u);
+                if (kk == 0) hipLaunchKernelGGL(k_salu, dim3(nblk), dim3(threads), 0, 0, out, iters, 7u);
+                if (kk == 1) hipLaunchKernelGGL(k_valu, dim3(nblk), dim3(threads), 0, 0, out, iters, 7u);
+                if (kk == 2) hipLaunchKernelGGL(k_mix, dim3(nblk), dim3(threads), 0, 0, out, iters, 7u);
+                if (kk == 3) hipLaunchKernelGGL(k_branch, dim3(nblk), dim3(threads), 0, 0, out, iters, 7u);
             };
             const float ms = best_ms(launch, 8);
             CHK(hipGetLastError());

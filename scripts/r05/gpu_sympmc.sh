@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 5: k_sym_step FETCH_SIZE / WRITE_SIZE on the symbolic_lanes and taint_lanes fields'
+# timed launches (scripts/r04/sym_timed.py, no profiling pass), each pass its own run.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/r05${1:-s}
+mkdir -p $OUT
+for kind in symbolic taint; do
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $OUT/${kind}_fetch -o run --output-format csv -- python3 -u scripts/r04/sym_timed.py $kind > $OUT/${kind}_fetch.log 2>&1 && \
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $OUT/${kind}_write -o run --output-format csv -- python3 -u scripts/r04/sym_timed.py $kind > $OUT/${kind}_write.log 2>&1 || exit 1
+done
