@@ -554,12 +554,14 @@ def run_large(dev, args, rank, barrier):
 SYMBOLIC_TX_CODES = ("overflow.sol.o", "exceptions.sol.o", "flag_array.sol.o")
 
 
-def symbolic_lane_batch(dev, lanes: int):
+def symbolic_lane_batch(dev, lanes: int, order: str = "code"):
     """`lanes` symbolic lanes: the initial state of a symbolic message call
     (transaction/symbolic.py:105-150: symbolic calldata, sender, value, gas
     price; symbolic storage, as `myth analyze -f` analyses a runtime code) into
-    each of the reference's precompiled contracts, dealt round-robin.  Returns
-    (LaserEVM, batch)."""
+    each of the reference's precompiled contracts.  order "code": contiguous
+    runs of one contract (a wave's lanes share their code, so their stack
+    depths, arena sizes and memory offsets line up and the planes' writes
+    coalesce); "rr": dealt round-robin.  Returns (LaserEVM, batch)."""
     from dataclasses import replace
     from mythril_amd import workloads
     from mythril_amd.lanes import _ALL_FIELDS, _SYM_FIELDS, LaneBatch, LaneShape
@@ -595,7 +597,7 @@ def symbolic_lane_batch(dev, lanes: int):
     for i, gs in enumerate(states):
         laser._pack(small, i, gs)
     big = LaneBatch(replace(shape, n=lanes))
-    idx = np.arange(lanes) % len(states)
+    idx = (np.arange(lanes) * len(states) // lanes) if order == "code" else np.arange(lanes) % len(states)
     for f in _ALL_FIELDS + _SYM_FIELDS:
         src = getattr(small, f, None)
         if src is not None:
@@ -603,7 +605,7 @@ def symbolic_lane_batch(dev, lanes: int):
     return laser, big
 
 
-def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True):
+def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True, order: str = "code"):
     """k_sym_step at `lanes` lanes: every lane runs from the
     start of its symbolic message call to its first stop -- MG_FORK at a
     symbolic JUMPI (the dispatcher's selector compare), an escape or a halt --
@@ -616,7 +618,7 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True):
     created."""
     from mythril_amd import roofline
     from mythril_amd.lanes import MG_FORK, STATUS_NAMES, LaneBatch
-    laser, b = symbolic_lane_batch(dev, lanes)
+    laser, b = symbolic_lane_batch(dev, lanes, order)
     n0 = int(b.n_nodes.sum())
     dev.alloc(b.shape)
     dev.upload(b)
@@ -666,7 +668,7 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True):
                         "each lane runs to its first fork, escape or halt"}
 
 
-def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5):
+def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5, order: str = "code"):
     """k_sym_step at `lanes` taint lanes, the kernel alone: the
     first launch of `taint_c2`'s batch -- C2's lanes with the seven modules'
     batch-safe hooks as device actions -- packed by the batched LaserEVM for
@@ -703,6 +705,11 @@ def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5):
         small.steps[i] = 0
     big = LaneBatch(replace(shape, n=lanes))
     idx = np.arange(lanes) % distinct
+    if order == "code":
+        # C2's bucketing (code, selector, calldata length; lanes.bucket_order): a
+        # wave's lanes walk one function's path, so their writes coalesce
+        from mythril_amd.lanes import bucket_order
+        idx = idx[bucket_order(_rows(small, idx))]
     for f in _ALL_FIELDS + _TAINT_FIELDS:
         src = getattr(small, f, None)
         if src is not None:
@@ -858,6 +865,16 @@ def _myth_analyze_rows(device, k2, tx_count: int, names, log=None):
                       "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown")},
                       "constraint_evals_per_s_wall": info["device_evals"] / info["wall_s"] if info["wall_s"] else None}
     return rows
+
+
+def _rows(batch, idx):
+    """A view of `batch` with lanes idx (only the fields bucket_order reads)."""
+    class _V:
+        pass
+    v = _V()
+    v.code_id, v.calldata, v.calldata_len = batch.code_id[idx], batch.calldata[idx], batch.calldata_len[idx]
+    v.shape, v.n = batch.shape, len(idx)
+    return v
 
 
 def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True):

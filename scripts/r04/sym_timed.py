@@ -13,15 +13,15 @@ import bench  # noqa: E402
 from mythril_amd.device import GpuDevice  # noqa: E402
 
 
-def main(kind: str):
+def main(kind: str, order: str = "code"):
     dev = GpuDevice(0)
     if kind == "symbolic":
-        out = bench.run_symbolic_lanes(dev, 65536, reps=5, profile=False)
+        out = bench.run_symbolic_lanes(dev, 65536, reps=5, profile=False, order=order)
     else:
-        out = bench.run_taint_lanes(dev, 65536, reps=5)
+        out = bench.run_taint_lanes(dev, 65536, reps=5, order=order)
     print(json.dumps({kind: out}), flush=True)
     dev.close()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "symbolic")
+    main(sys.argv[1] if len(sys.argv) > 1 else "symbolic", sys.argv[2] if len(sys.argv) > 2 else "code")
