@@ -635,6 +635,20 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True, ord
     statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
                 for k, v in zip(*np.unique(out_b.status, return_counts=True))}
     if not profile:            # the timed launches alone (PMC passes of k_sym_step)
+        if os.environ.get("MG_SYM_FLUSH"):
+            # diagnostic: an L2/MALL-evicting read between the upload and each
+            # launch, so the upload's dirty lines are not written back during (and
+            # counted against) the kernel (scripts/r05/gpu_sympmc.sh)
+            import torch
+            junk = torch.empty(1 << 29, dtype=torch.float32, device="cuda")
+            ms = []
+            for _ in range(reps):
+                dev.upload(b)
+                float(junk.sum())
+                torch.cuda.synchronize()
+                st = dev.step()
+                ms.append(st.kernel_ms)
+            del junk
         kms = float(np.median(ms))
         return {"lanes": lanes, "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
                 "lane_steps_per_s": steps / (kms / 1e3), "statuses": statuses}

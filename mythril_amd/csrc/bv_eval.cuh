@@ -273,6 +273,29 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
                      (1ull << BV_UREM) | (1ull << BV_UMIN) | (1ull << BV_UMAX) | (1ull << BV_RSUB) | \
                      (1ull << BV_RCONCAT) | (1ull << BV_EXT_RCAT))
 
+// Predecode (bv_predecode, at upload, after bv_fuse): flags the kernel tests
+// with one scalar bit test instead of deriving them from op and width per
+// instruction -- op byte bit 7: the op has one operand (no B fetch, the small
+// switch); w0 bit 30: the result is masked to `width` (width < 256 and the op
+// in BV_MASK_OPS).  Internal to the library: the C-ABI's programs never carry
+// them (bv_upload rejects bits 22..31, and op < BV_NUM_OPS < 128).
+#define BV_W0_UNARY 0x80u
+#define BV_W0_MASK (1u << 30)
+static bool bv_is_unary(uint32_t op) {
+    return op == BV_COPY || op == BV_NOT || op == BV_NEG || op == BV_BNOT || op == BV_EXTRACT || op == BV_ZEXT ||
+           op == BV_SEXT;
+}
+static void bv_predecode(std::vector<uint32_t> &v, const std::vector<uint32_t> &off, uint32_t n) {
+    for (uint32_t d = 0; d < n; ++d) {
+        for (uint32_t i = off[d]; i < off[d + 1]; ++i) {
+            uint32_t &w0 = v[4 * (size_t)i];
+            const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
+                        if (width < 256u && op < 64u && ((BV_MASK_OPS >> op) & 1ull)) w0 |= BV_W0_MASK;
+            if (op == BV_BINX || (w0 >> 31)) ++i;      // skip the extension slot
+        }
+    }
+}
+
 // MG_BV_WAVES: minimum waves per SIMD the register allocation must allow (0
 // leaves the compiler's choice).  8 caps the kernel at 64 VGPRs (a few spill to
 // scratch); with the scalar-load instruction fetch the block's LDS is its 16 KiB of
@@ -361,28 +384,27 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 const uint4 ins = insns[i0 + uni(p)];
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
             }
-            const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
+            // op byte bit 7 = one operand (bv_predecode); w0 bit 30 = mask to width
+            const uint32_t op = w0 & 0x7fu, width = (w0 >> 8) & 0x1ffu;
             if ((ra >> 30) != BV_REF_ACC) acc = bv_fetch(c, ra);    // A in the accumulator's registers
             const U256 A = acc;
             U256 r;
-            switch (op) {
-            case BV_COPY: r = A; break;
-            case BV_NOT: r = u_not(A); break;
-            case BV_NEG: r = u_neg(A); break;
-            case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
-            case BV_EXTRACT: r = u_shr_u(A, rb & 0xffu, 0u); break;          // rb: uniform immediate
-            case BV_ZEXT: r = A; break;
-            case BV_SEXT: r = bv_sext(A, rb); break;
-            default: {
+            if (w0 & BV_W0_UNARY) {
+                switch (op) {
+                case BV_NOT: r = u_not(A); break;
+                case BV_NEG: r = u_neg(A); break;
+                case BV_BNOT: r = u_small((A.w[0] & 1u) ^ 1u); break;
+                case BV_EXTRACT: r = u_shr_u(A, rb & 0xffu, 0u); break;          // rb: uniform immediate
+                case BV_SEXT: r = bv_sext(A, rb); break;
+                default: r = A; break;                                          // BV_COPY, BV_ZEXT
+                }
+            } else {
                 U256 B = bv_fetch(c, rb);
                 if (op == BV_UDIV || op == BV_UREM) {        // the unsigned division site
                     r = bv_udivrem(op == BV_UDIV, A, B);
-                    break;
-                }
-                if ((BV_DIV_OPS >> op) & 1ull) {             // the signed / overflow site
+                } else if ((BV_DIV_OPS >> op) & 1ull) {      // the signed / overflow site
                     r = bv_divop(op, width, rc, A, B);
-                    break;
-                }
+                } else {
                 switch (op) {
                 case BV_ADD: r = u_add(A, B); break;
                 case BV_SUB: r = u_sub(A, B); break;
@@ -505,7 +527,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 // fused tail (bv_fuse): 1-3 bv_simple ops applied to this result
                 // (masked to its own width first), from an extension slot
                 // {kinds | count << 28, B1, B2, B3}
-                if (width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);
+                if (w0 & BV_W0_MASK) r = bv_mask(r, width);
                 uint32_t e0, e1, e2, e3;
                 {
                     const uint4 x = insns[i0 + uni(p + 1u)];
@@ -521,7 +543,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
             }
             // uniform; a tail's ops are 256-bit
-            if (!tail && width < 256u && ((BV_MASK_OPS >> op) & 1ull)) r = bv_mask(r, width);
+            if (!tail && (w0 & BV_W0_MASK)) r = bv_mask(r, width);
             acc = r;
             if ((w0 >> 17) & 1u) {
                 const uint32_t ds = (w0 >> 18) & 0xfu;
@@ -727,10 +749,14 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
         // given: the parity tests compare both; the per-shape A/B levels are in
         // ab/k2_fuse_levels.diff)
         bv_fuse(dags, s.h_insns, s.h_off, true, true, true, true);
-        insns = s.h_insns.data();
-        prog_off = s.h_off.data();
-        total_up = s.h_off[n];
+    } else {
+        s.h_insns.assign(dags->insns, dags->insns + 4 * (size_t)total);
+        s.h_off.assign(dags->prog_off, dags->prog_off + n + 1);
     }
+    bv_predecode(s.h_insns, s.h_off, n);
+    insns = s.h_insns.data();
+    prog_off = s.h_off.data();
+    total_up = s.h_off[n];
     // tiles: consecutive DAGs whose programs fit BV_TILE_INSNS together
     // LDS tile capacity: the longest program rounded up, at least BV_TILE_MIN, so
     // short-program batches keep a small LDS footprint (higher occupancy)
