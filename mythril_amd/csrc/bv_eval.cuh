@@ -290,7 +290,8 @@ static void bv_predecode(std::vector<uint32_t> &v, const std::vector<uint32_t> &
         for (uint32_t i = off[d]; i < off[d + 1]; ++i) {
             uint32_t &w0 = v[4 * (size_t)i];
             const uint32_t op = w0 & 0xffu, width = (w0 >> 8) & 0x1ffu;
-                        if (width < 256u && op < 64u && ((BV_MASK_OPS >> op) & 1ull)) w0 |= BV_W0_MASK;
+            if (bv_is_unary(op)) w0 |= BV_W0_UNARY;
+            if (width < 256u && op < 64u && ((BV_MASK_OPS >> op) & 1ull)) w0 |= BV_W0_MASK;
             if (op == BV_BINX || (w0 >> 31)) ++i;      // skip the extension slot
         }
     }
