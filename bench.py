@@ -636,19 +636,18 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True, ord
                 for k, v in zip(*np.unique(out_b.status, return_counts=True))}
     if not profile:            # the timed launches alone (PMC passes of k_sym_step)
         if os.environ.get("MG_SYM_FLUSH"):
-            # diagnostic: an L2/MALL-evicting read between the upload and each
-            # launch, so the upload's dirty lines are not written back during (and
-            # counted against) the kernel (scripts/r05/gpu_sympmc.sh)
-            import torch
-            junk = torch.empty(1 << 29, dtype=torch.float32, device="cuda")
+            # diagnostic: a kernel-2 launch that streams ~1 GB between the upload and
+            # each launch, so the upload's dirty lines leave L2 / MALL before the
+            # kernel runs instead of during it (scripts/r05/gpu_symflush.sh)
+            from mythril_amd.smt import synth
+            fprog, fmodels = synth.c4_batch(1_000_000, 4096)
+            dev.eval_upload(fprog, fmodels)
             ms = []
             for _ in range(reps):
                 dev.upload(b)
-                float(junk.sum())
-                torch.cuda.synchronize()
+                dev.eval_run()
                 st = dev.step()
                 ms.append(st.kernel_ms)
-            del junk
         kms = float(np.median(ms))
         return {"lanes": lanes, "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
                 "lane_steps_per_s": steps / (kms / 1e3), "statuses": statuses}
