@@ -412,7 +412,19 @@ class ModelCache:
         if self._compiler is None:
             self._compiler = Compiler()
         progs, kept = [], []
+        # a fork's two successors add X and its negation: the negation's bitmap is
+        # the complement of X's over the pool (both are evaluated exactly, per
+        # model), so only one of the pair is compiled and evaluated
+        derived: Dict[Node, Node] = {}
+        want = OrderedDict.fromkeys(conjuncts)
         for c in conjuncts:
+            if c in derived:
+                continue
+            q = _complement(c)
+            if q is not None and q in want and q not in derived and self._progs.get(c, _MISSING) is _MISSING \
+                    and self._progs.get(q, _MISSING) is not None:
+                derived[c] = q
+        for c in [c for c in conjuncts if c not in derived] + [q for q in derived.values() if q not in want]:
             pr = self._progs.get(c, _MISSING)
             if pr is _MISSING:
                 try:
@@ -431,6 +443,16 @@ class ModelCache:
             self.launches += 1
             for row, c in enumerate(kept):
                 rows[c] = bits[row]
+        if derived:
+            valid = np.zeros((len(pool) + 63) // 64, dtype=np.uint64)
+            full, rest = divmod(len(pool), 64)
+            valid[:full] = np.uint64(0xFFFFFFFFFFFFFFFF)
+            if rest:
+                valid[full] = np.uint64((1 << rest) - 1)
+            for c, q in derived.items():
+                r = rows.get(q)
+                if r is not None:
+                    rows[c] = ~r & valid
         return rows
 
     # -- witness seeds and prefetched groups ------------------------------------
@@ -527,6 +549,17 @@ class ModelCache:
             self._memo_put(k, result)
             out.append(result)
         return out
+
+
+def _complement(c: Node) -> Optional[Node]:
+    """The conjunct whose truth is the negation of c's under every model, when
+    the expression layer builds one: not(X) / X, and eq(a, b) / distinct(a, b)
+    (a JUMPI's two branch conditions on a bit-vector word)."""
+    if c.op == "not" and len(c.args) == 1:
+        return c.args[0]
+    if c.op in ("eq", "distinct") and len(c.args) == 2:
+        return Node("distinct" if c.op == "eq" else "eq", 1, c.args, c.param)
+    return None
 
 
 def _conjuncts(key: Node) -> List[Node]:
