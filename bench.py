@@ -681,7 +681,7 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True, ord
                         "each lane runs to its first fork, escape or halt"}
 
 
-def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5, order: str = "code"):
+def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5, order: str = "code", profile: bool = True):
     """k_sym_step at `lanes` taint lanes, the kernel alone: the
     first launch of `taint_c2`'s batch -- C2's lanes with the seven modules'
     batch-safe hooks as device actions -- packed by the batched LaserEVM for
@@ -743,11 +743,34 @@ def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5, order: str = 
     statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
                 for k, v in zip(*np.unique(out_b.status, return_counts=True))}
     kms = float(np.median(ms))
-    return {"metric": "taint lane-steps/s (k_sym_step, device actions; host replay excluded)",
-            "lanes": lanes, "distinct_calls": distinct, "modules": list(names),
-            "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
-            "lane_steps_per_s": steps / (kms / 1e3) if kms else None, "statuses": statuses,
-            "running_after": int((out_b.status == MG_RUNNING).sum())}
+    out = {"metric": "taint lane-steps/s (k_sym_step, device actions; host replay excluded)",
+           "lanes": lanes, "distinct_calls": distinct, "modules": list(names),
+           "lane_steps_per_launch": int(steps), "kernel_ms": kms, "kernel_ms_all": ms,
+           "lane_steps_per_s": steps / (kms / 1e3) if kms else None, "statuses": statuses,
+           "running_after": int((out_b.status == MG_RUNNING).sum()), "order": order}
+    if profile:
+        # §8(d)'s bytes per lane-step from the launch's own opcode histogram (an
+        # untimed profiling pass of the same image), plus what a taint lane moves
+        # besides: a 4-byte object handle per stack word moved and the hook
+        # records it writes (4 bytes a word; MG_REC_ANNOT / MG_REC_HOOK)
+        from mythril_amd import roofline
+        dev.upload(big)
+        op_counts, extra = dev.step_profile(mask)
+        ops, byts, psteps = roofline.algorithmic_work(op_counts, extra)
+        words = float((op_counts.astype(np.float64) * roofline.WORDS).sum())
+        rec_bytes = 4.0 * float(out_b.rec_len.astype(np.float64).sum())
+        byts += 4.0 * words + rec_bytes
+        traffic, src = roofline.pmc_traffic("k_sym_step_taint")
+        sec = kms / 1e3
+        gbs = byts / sec / 1e9
+        out["roofline"] = roofline.with_sustained({
+            "bound": "hbm", "achieved": gbs, "peak": roofline.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / roofline.HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+            "kernel": "k_sym_step (taint lanes)", "kernel_ms": kms,
+            "algorithmic_bytes_per_launch": byts, "algorithmic_int32_ops_per_launch": ops,
+            "record_bytes_per_launch": rec_bytes, "bytes_per_lane_step": byts / max(psteps, 1.0),
+            "traffic_over_algorithmic": (traffic / byts) if traffic else None})
+    return out
 
 
 def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_handler=None, log=None):

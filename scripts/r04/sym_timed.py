@@ -18,7 +18,7 @@ def main(kind: str, order: str = "code"):
     if kind == "symbolic":
         out = bench.run_symbolic_lanes(dev, 65536, reps=5, profile=False, order=order)
     else:
-        out = bench.run_taint_lanes(dev, 65536, reps=5, order=order)
+        out = bench.run_taint_lanes(dev, 65536, reps=5, order=order, profile=False)
     print(json.dumps({kind: out}), flush=True)
     dev.close()
 
