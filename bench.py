@@ -1037,8 +1037,7 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
         "ms_per_step": 1000.0 * el / args.c4_steps, "scaling": "strong",
         "config": {"workload": "C4", "dags": args.c4_dags, "models": args.c4_models,
                    "dags_with_a_satisfying_model": n_sat},
-        "roofline": with_sustained({"bound": "valu-int32", "achieved": tops, "peak": VALU_PEAK_TOPS,
-                     "unit": "T int32-ops/s", "frac": tops / VALU_PEAK_TOPS, "traffic": traffic,
+        "roofline": _k2_roofline(tops, k_ms, ops_nodiv, models.n_models, {"traffic": traffic,
                      "traffic_unit": "bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_source": traffic_src,
                      "kernel": "k_bv_eval", "kernel_ms": k_ms,
@@ -1054,6 +1053,29 @@ def run_c4(args, dev, rank, world, barrier, dist_on):
                      "divisions_per_eval": div_count / max(prog.n_dags, 1),
                      "model_bytes_per_eval": gather_bytes / max(prog.n_dags, 1)}),
     }
+
+
+def _k2_roofline(tops_charged, k_ms, ops_nodiv, n_models, extra):
+    """C4's roofline.  Headline: the §8(d) int32 ops WITHOUT the
+    2,048-op division charge over the INT32 VALU peak -- the charge is not work
+    the kernel does (with it the fraction passes the measured sustained peak);
+    the charged figure stays beside it.  The measured bound is the
+    interpreter's scalar issue (`issue_floor`)."""
+    from mythril_amd.roofline import VALU_PEAK_TOPS, k2_issue_floor, sustained_peaks, with_sustained
+    tops = ops_nodiv * n_models / (k_ms / 1e3) / 1e12
+    floor = k2_issue_floor(k_ms)
+    roof = with_sustained({"bound": (floor["bound"] + "-issue") if floor else "valu-int32",
+                           "priced_as": "valu-int32",
+                           "frac_basis": "§8(d) int32 ops without the division charge / INT32 VALU peak",
+                           "achieved": tops, "peak": VALU_PEAK_TOPS, "unit": "T int32-ops/s",
+                           "frac": tops / VALU_PEAK_TOPS})
+    _, valu_sust = sustained_peaks()
+    roof["with_division_charge"] = {"achieved": tops_charged, "frac": tops_charged / VALU_PEAK_TOPS,
+                                    "frac_sustained": tops_charged / valu_sust if valu_sust else None}
+    if floor:
+        roof["issue_floor"] = floor
+    roof.update(extra)
+    return roof
 
 
 def _k2_alt(ops_nodiv, div_count, n_models, k_ms, executed=False):

@@ -241,3 +241,41 @@ def issue_floor():
     busy = 1.0 - float(sq["wait_any_frac"])
     return {"busy_frac": busy, "note": "ceiling = measured lane-steps/s / busy_frac at the same launch "
                                        "(waits hidden, issue unchanged)", "source": src}
+
+
+def issue_rates():
+    """Wave-instructions one CU issues per clock at 8 waves per SIMD, per class,
+    from the newest profiles/rNN/issue_rates.json (scripts/probes/issue_rates.hip).
+    (dict, source) or (None, None)."""
+    for f in sorted(PROFILES.glob("r*/issue_rates.json"), reverse=True):
+        try:
+            r = json.loads(f.read_text())["rates"]
+            # the SALU loop carries 3 loop instructions per 16 measured ones
+            return ({"salu": r["salu"]["8"]["wave_instr_per_cu_clk"] * 19.0 / 16.0,
+                     "valu": r["valu"]["8"]["wave_instr_per_cu_clk"],
+                     "branch_pairs": r["branch"]["8"]["wave_instr_per_cu_clk"]},
+                    str(f.relative_to(PROFILES.parent)))
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
+def k2_issue_floor(kernel_ms: float, cus: int = 256, clock_hz: float = 2.4e9):
+    """Kernel 2's issue-bound floor on its C4 launch:
+    per class, the SQ pass's wave-instructions per launch over one CU's issue
+    rate; the floor is the largest, and the launch's measured time over it says
+    how close the interpreter runs to issue-bound."""
+    sq, sq_src = sq_per_wave("k_bv_eval")
+    rates, r_src = issue_rates()
+    if not sq or not rates or kernel_ms <= 0:
+        return None
+    waves = float(sq["SQ_WAVES"])
+    per_cu = lambda k: float(sq[k]) * waves / cus
+    ms = {"salu": per_cu("SQ_INSTS_SALU") / rates["salu"] / clock_hz * 1e3,
+          "valu": per_cu("SQ_INSTS_VALU") / rates["valu"] / clock_hz * 1e3,
+          "branch": 2.0 * per_cu("SQ_INSTS_BRANCH") / rates["branch_pairs"] / clock_hz * 1e3}
+    bound = max(ms, key=ms.get)
+    return {"floor_ms": ms[bound], "bound": bound, "class_ms": ms, "kernel_ms": kernel_ms,
+            "frac": ms[bound] / kernel_ms, "sq_source": sq_src, "rates_source": r_src,
+            "note": "per-class issue time of the SQ pass's instructions at the probe's rates "
+                    "(2.4 GHz assumed for both; the ratio does not depend on it)"}
