@@ -441,7 +441,46 @@ def apply_repair(assign: Dict[str, object], rep: Repair) -> Dict[str, object]:
     return out
 
 
-def complete(assign: Dict[str, object]) -> Dict[str, object]:
+class _Completed(dict):
+    """A completed assignment, with the value complete() gave each registered
+    keccak input (`kvals`): a candidate one repair away reuses the values of
+    the inputs the repair does not reach."""
+    __slots__ = ("kvals",)
+
+
+_DEPS: Dict[int, Tuple[Node, frozenset, bool]] = {}
+
+
+def _deps(raw: Node) -> Tuple[frozenset, bool]:
+    """(variable and array names a term reads, whether it reads an
+    uninterpreted function -- whose interpretation complete() rebuilds)."""
+    got = _DEPS.get(id(raw))
+    if got is not None and got[0] is raw:
+        return got[1], got[2]
+    names, uf, seen, stack = set(), False, set(), [raw]
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        if n.op == "var":
+            names.add(n.param)
+        elif n.op == "array":
+            names.add(n.param[0])
+        elif n.op == "uf":
+            uf = True
+        stack.extend(n.args)
+    fs = frozenset(names)
+    _DEPS[id(raw)] = (raw, fs, uf)
+    return fs, uf
+
+
+def _changed(rep: Repair) -> frozenset:
+    return frozenset(k if isinstance(k, str) else k[0] for k in rep)
+
+
+def complete(assign: Dict[str, object], base: Optional[_Completed] = None,
+             changed: frozenset = frozenset()) -> _Completed:
     """The function managers' interpretations under `assign`, rebuilt so their
     axioms hold (keccak_function_manager.py:116-179, exponent_function_manager
     .py:32-60): keccak256_N at every registered input's value (the concrete hash
@@ -451,8 +490,10 @@ def complete(assign: Dict[str, object]) -> Dict[str, object]:
     demands; other bases: the power when it is positive, else 1)."""
     from .exponent_manager import exponent_function_manager as em
     from .keccak_manager import PART, keccak_function_manager as km
-    out = {k: v for k, v in assign.items() if not k.startswith("keccak256_") and k != "Power"}
+    out = _Completed((k, v) for k, v in assign.items() if not k.startswith("keccak256_") and k != "Power")
     ev = _Eval(out)
+    prev = base.kvals if isinstance(base, _Completed) else None
+    kvals: Dict[Node, int] = {}
     concrete = {(c.size(), c.value): h.value for c, h in km.concrete_hashes.items()}
     tabs: Dict[str, FuncInterp] = {}
     for (n, cv), h in concrete.items():
@@ -464,7 +505,14 @@ def complete(assign: Dict[str, object]) -> Dict[str, object]:
         f = tabs.setdefault(f"keccak256_{n}", FuncInterp(0, {}))
         inv = tabs.setdefault(f"keccak256_{n}-1", FuncInterp(0, {}))
         for x in dict.fromkeys(x.raw for x in xs):      # registered once per SHA3 executed
-            v = ev(x)
+            v = prev.get(x) if prev is not None else None
+            if v is not None:
+                names, uf = _deps(x)
+                if uf or (names & changed):
+                    v = None
+            if v is None:
+                v = ev(x)
+            kvals[x] = v
             if (v,) in f.entries:
                 continue
             h = concrete.get((n, v))
@@ -486,6 +534,7 @@ def complete(assign: Dict[str, object]) -> Dict[str, object]:
         pw.entries.setdefault((b, e), v)
     out.update(tabs)
     out["Power"] = pw
+    out.kvals = kvals
     return out
 
 
@@ -511,6 +560,7 @@ class SatSearchBackend:
         self.max_candidates = max_candidates
         self.patience = patience       # rounds without a better best count before giving up
         self.rng = np.random.default_rng(seed)
+        self._memo_completed: Dict[int, tuple] = {}
         self.stats: Dict[str, int] = {"calls": 0, "refuted": 0, "seed": 0, "search": 0, "unknown": 0,
                                       "candidates": 0, "launches": 0, "minimised": 0}
 
@@ -533,6 +583,24 @@ class SatSearchBackend:
         if minimize:
             model = self._minimise(key, model, minimize)
         return model
+
+    def _completed(self, assign: Dict[str, object]) -> "_Completed":
+        """complete(assign), memoised per assignment object while neither it
+        (its size) nor the function managers' registrations change: the seeds
+        and LRU models start every search, and completing them anew each time
+        was most of a search's host time.  (Any candidate is still checked on
+        kernel 2 before it is reported, so the memo affects which model is
+        found, never whether one is.)"""
+        from .exponent_manager import exponent_function_manager as em
+        from .keccak_manager import keccak_function_manager as km
+        state = (sum(len(v) for v in km.symbolic_inputs.values()), len(km.concrete_hashes),
+                 len(em.symbolic_points), len(em.concrete_points), len(assign))
+        got = self._memo_completed.get(id(assign))
+        if got is not None and got[0] is assign and got[1] == state:
+            return got[2]
+        out = complete(dict(assign))
+        self._memo_completed[id(assign)] = (assign, state, out)
+        return out
 
     # -- kernel-2 scoring ---------------------------------------------------------------
     def _score(self, conj: Sequence[Node], assigns: List[Dict[str, object]]):
@@ -568,7 +636,7 @@ class SatSearchBackend:
         # then the seeds
         lru = [m for m in reversed(self.cache.model_cache.lru_cache.keys()) if isinstance(m, Model)]
         seeds = lru + (self.cache._seed_models() or [_model({})])
-        pool = [complete(dict(m.raw[-1].assignment)) for m in seeds]
+        pool = [self._completed(m.raw[-1].assignment) for m in seeds]
         counts, hit = self._score(conj, pool)
         if hit is False:
             return None                        # a conjunct kernel 2 cannot evaluate
@@ -595,14 +663,14 @@ class SatSearchBackend:
                     # every wrong conjunct's first repair at once (independent
                     # conjuncts -- a selector, a call value, a sender -- are
                     # usually fixed together)
-                    cands.append(complete(apply_repair(a, firsts)))
+                    cands.append(complete(apply_repair(a, firsts), a, _changed(firsts)))
                 for c in wrong[:4]:
                     for rep in inv.bool_true(c):
                         sig = (id(a), tuple(sorted(map(repr, rep.items()))))
                         if not rep or sig in seen:
                             continue
                         seen.add(sig)
-                        cands.append(complete(apply_repair(a, rep)))
+                        cands.append(complete(apply_repair(a, rep), a, _changed(rep)))
                         if len(cands) >= self.max_candidates:
                             break
             if not cands:
@@ -640,7 +708,7 @@ class SatSearchBackend:
             vals = sorted({v for v in (0, 1, 2, 3, 4, 32, 36, 64, 68, 100, 132, 164, 196, 228, 260)
                            if v < cur} | {cur - k for k in range(1, min(cur, 64) + 1)} |
                           {cur >> k for k in range(1, 12)})
-            cands = [complete({**assign, raw.param: v}) for v in vals]
+            cands = [complete({**assign, raw.param: v}, assign, frozenset((raw.param,))) for v in vals]
             counts, hit = self._score(conj, cands)
             if hit is False:
                 break
