@@ -635,6 +635,15 @@ def run_symbolic_lanes(dev, lanes: int, reps: int = 5, profile: bool = True, ord
     statuses = {STATUS_NAMES.get(int(k), str(int(k))): int(v)
                 for k, v in zip(*np.unique(out_b.status, return_counts=True))}
     if not profile:            # the timed launches alone (PMC passes of k_sym_step)
+        if os.environ.get("MG_SYM_MAXSTEPS"):
+            # diagnostic: every lane stops after K steps (the write traffic's slope per step)
+            k = int(os.environ["MG_SYM_MAXSTEPS"])
+            ms = []
+            for _ in range(reps):
+                dev.upload(b)
+                st = dev.step(max_steps=k)
+                ms.append(st.kernel_ms)
+                steps = st.lane_steps
         if os.environ.get("MG_SYM_FLUSH"):
             # diagnostic: a kernel-2 launch that streams ~1 GB between the upload and
             # each launch, so the upload's dirty lines leave L2 / MALL before the
