@@ -1,0 +1,11 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+T=${1:-s}
+OUT=gpurun_out/r05$T
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_eval.py tests/test_gpu_k2_pinning.py tests/test_gpu_fork_filter.py tests/test_gpu_solver.py -v --timeout 240 --timeout-method thread > $OUT/pytest_k2.log 2>&1 && \
+AB_K2_MODES=scalar timeout -k 10 700 python3 -u scripts/ab_k2.py 3 ab/k2_v10.so ab/k2_v12.so ab/k2_v13.so > $OUT/ab_k2.log 2>&1 && \
+bash scripts/r05/gpu_k2c4sq.sh $T && \
+bash scripts/r05/gpu_symsteps.sh $T

@@ -31,7 +31,7 @@ CONTRACTS = {
 # runtime bytecode analysed as `myth analyze -f <code>` does without on-chain data:
 # an account at a fixed address with the code and symbolic storage
 # (analysis/symbolic.py:183-193: concrete_storage=False, Array("Storage{address}"))
-RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump", "symlen_sha3", "gas_sym", "block_env", "log_sym")
+RUNTIME = ("overflow.sol.o", "exceptions.sol.o", "environments.sol.o", "symkey_sha3", "selfbalance_ret", "balance_of", "symjump", "symlen_sha3", "gas_sym", "block_env", "log_sym", "memjump")
 
 # synthetic runtime code: memory at a symbolic offset x = calldata[4:36] feeding
 # SHA3 (sha3_ at a symbolic offset, instructions.py:1014-1051) and symbolic
@@ -58,7 +58,14 @@ SYNTH = {"symkey_sha3": "600435338152604081208054601357600181555b6024358015601f5
          # 1386-1425)
          "block_env": "434210600e5746600114601657005b414411601857005b005b00",
          # LOG1 / LOG2 / LOG0 with symbolic topics, offset and length (log_, instructions.py:1710-1723)
-         "log_sym": "6000353360006000a1808060206000a280600116601f5780600216602b57005b8015602657005b8080a0005b00"}
+         "log_sym": "6000353360006000a1808060206000a280600116601f5780600216602b57005b8015602657005b8080a0005b00",
+         # a jump target read back from memory at a symbolic offset: MSTORE(x, 15),
+         # JUMP(MLOAD(x)) with x = calldata[0:32] -- the MLOADK node decodes to the concrete 15
+         # (get_word_at over the byte map), so the reference jumps; the device must hand the
+         # jump to the host instead of raising InvalidJumpDestination
+         # (then two calldata-bit branches, for paths past the jump)
+         "memjump": "600035600f81525156" + "00" * 6 + "5b602035806001166021576002166028570"
+                    "05b6001600055005b600260015500"}
 
 
 # the other reference codes (tests/testdata/inputs/*.sol.o), deployed as RUNTIME codes
