@@ -190,20 +190,20 @@ DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) 
 DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
     const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
     U256 r;
+    if (kind == BV_REF_VAR) {            // the commonest B operand (C4: 46 %) first
+        const size_t row = (size_t)idx * c.n_models + c.model();
+        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
+        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+        BV_PIN("; variable operand", r);
+        return r;
+    }
     if (kind <= BV_REF_SLOT) {
         const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid()];
         const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid()];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
         BV_PIN("; slot operand", r);
-        return r;
-    }
-    if (kind == BV_REF_VAR) {
-        const size_t row = (size_t)idx * c.n_models + c.model();
-        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
-        r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-        r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
-        BV_PIN("; variable operand", r);
         return r;
     }
     // constant: uniform address -> scalar loads
@@ -524,34 +524,35 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
             }
             }
-            const bool tail = (w0 >> 31) != 0u;
-            if (tail) {
-                // fused tail (bv_fuse): 1-3 bv_simple ops applied to this result
-                // (masked to its own width first), from an extension slot
-                // {kinds | count << 28, B1, B2, B3}
+            // mask, fused tail and store in one test for the common instruction
+            // that has none of them
+            if (w0 & (BV_W0_MASK | (1u << 31) | (1u << 17))) {
+                // the result masked to its width first (a tail's ops are 256-bit)
                 if (w0 & BV_W0_MASK) r = bv_mask(r, width);
-                uint32_t e0, e1, e2, e3;
-                {
-                    const uint4 x = insns[i0 + uni(p + 1u)];
-                    e0 = x.x; e1 = x.y; e2 = x.z; e3 = x.w;
-                }
-                ++p;
-                const uint32_t k = e0 >> 28;
+                if (w0 >> 31) {
+                    // fused tail (bv_fuse): 1-3 bv_simple ops applied to this result,
+                    // from an extension slot {kinds | count << 28, B1, B2, B3}
+                    uint32_t e0, e1, e2, e3;
+                    {
+                        const uint4 x = insns[i0 + uni(p + 1u)];
+                        e0 = x.x; e1 = x.y; e2 = x.z; e3 = x.w;
+                    }
+                    ++p;
+                    const uint32_t k = e0 >> 28;
 #pragma unroll 1
-                for (uint32_t j = 0; j < k; ++j) {
-                    const uint32_t ref = j == 0u ? e1 : j == 1u ? e2 : e3;
-                    const U256 C = bv_fetch(c, ref);
-                    r = bv_simple((e0 >> (4u * j)) & 0xfu, r, C);
+                    for (uint32_t j = 0; j < k; ++j) {
+                        const uint32_t ref = j == 0u ? e1 : j == 1u ? e2 : e3;
+                        const U256 C = bv_fetch(c, ref);
+                        r = bv_simple((e0 >> (4u * j)) & 0xfu, r, C);
+                    }
+                }
+                if ((w0 >> 17) & 1u) {
+                    const uint32_t ds = (w0 >> 18) & 0xfu;
+                    slots[(ds * 2u) * BV_BLOCK + c.tid()] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+                    slots[(ds * 2u + 1u) * BV_BLOCK + c.tid()] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
                 }
             }
-            // uniform; a tail's ops are 256-bit
-            if (!tail && (w0 & BV_W0_MASK)) r = bv_mask(r, width);
             acc = r;
-            if ((w0 >> 17) & 1u) {
-                const uint32_t ds = (w0 >> 18) & 0xfu;
-                slots[(ds * 2u) * BV_BLOCK + c.tid()] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
-                slots[(ds * 2u + 1u) * BV_BLOCK + c.tid()] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
-            }
         }
         const bool sat = c.m < n_models && (acc.w[0] & 1u);
         const uint64_t bal = __ballot(sat);

@@ -119,7 +119,11 @@ DEV bool mtag_any(const DevSym &S, size_t N, uint32_t lane, uint32_t off, uint32
 // equal headers whose operands are the same terms, walked with an explicit
 // stack.  A comparison deeper than the stack answers false, so the device keeps
 // a Select node the host's decode then folds (decoding decides the term).
-__device__ __noinline__ bool sym_same(const DevSym &S, size_t N, uint32_t lane, uint32_t x, uint32_t y) {
+// The planes come as pointers, not the kernel's DevSym: a reference argument
+// to a call forces the kernel's by-value argument structs into per-lane scratch
+// for the whole launch (every lane wrote them at entry: ~330 bytes a lane).
+__device__ __noinline__ bool sym_same(const uint4 *node, const uint4 *cval, size_t N, uint32_t lane, uint32_t x,
+                                      uint32_t y) {
     uint32_t st[32];
     int top = 0;
     st[top++] = x;
@@ -130,12 +134,12 @@ __device__ __noinline__ bool sym_same(const DevSym &S, size_t N, uint32_t lane, 
         const bool ca = (a & SYM_CONST) != 0u, cb = (b & SYM_CONST) != 0u;
         if (ca || cb) {
             if (!(ca && cb)) return false;
-            if (!u_eq(ld_word(gv(S.cval), (size_t)(a & ~SYM_CONST) * N + lane),
-                      ld_word(gv(S.cval), (size_t)(b & ~SYM_CONST) * N + lane)))
+            if (!u_eq(ld_word(gv(cval), (size_t)(a & ~SYM_CONST) * N + lane),
+                      ld_word(gv(cval), (size_t)(b & ~SYM_CONST) * N + lane)))
                 return false;
             continue;
         }
-        const uint4 na = S.node[(size_t)a * N + lane], nb = S.node[(size_t)b * N + lane];
+        const uint4 na = node[(size_t)a * N + lane], nb = node[(size_t)b * N + lane];
         if (na.x != nb.x || na.w != nb.w) return false;
         const uint32_t kind = na.x & 0xffu;
         const bool yref = kind != SYM_CDSIZE && kind != SYM_ENV && kind != SYM_TERM;
@@ -155,10 +159,10 @@ __device__ __noinline__ bool sym_same(const DevSym &S, size_t N, uint32_t lane, 
 // itself for its 32 bytes in order), joined left to right by CONCAT nodes.  The
 // host's decode joins the parts the same way expr.simplify_concat joins bytes.
 // False when the arena or the constant table is full.
-__device__ __noinline__ bool sym_mem_ref(const DevSym &S, const DevLanes &L, size_t N, uint32_t lane,
+// S by value (a few registers) and the memory plane as a pointer: see sym_same.
+__device__ __noinline__ bool sym_mem_ref(const DevSym S, const uint32_t *mem, size_t N, uint32_t lane,
                                          uint32_t off, uint32_t len, uint32_t msize, uint32_t &nn, uint32_t &nc,
                                          uint32_t &ref) {
-    const LaneView V{L, lane, nullptr, 0u, 0u, 256u, nullptr, 0u};
     uint32_t acc = SYM_NONE, accw = 0u, k = 0u;
     while (k < len) {
         const uint32_t p = off + k;
@@ -171,7 +175,8 @@ __device__ __noinline__ bool sym_mem_ref(const DevSym &S, const DevLanes &L, siz
                 const uint32_t q = off + k;
                 if (q < msize && mtag_at(S, N, lane, q) != 0u) break;
                 v = u_shl_n(v, 8u);
-                v.w[0] |= q < msize ? V.mbyte(q) : 0u;
+                v.w[0] |= q < msize ? (gp(mem)[(size_t)(q >> 2) * N + lane] >> (24u - 8u * (q & 3u))) & 0xffu
+                                    : 0u;
                 ++run;
                 ++k;
             }
@@ -763,7 +768,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                             if (u_eq(ld_word(gv(L.storage), V.row((uint32_t)e) * 2), a)) { hit = true; break; }
                             continue;
                         }
-                        if (ta && tg.x && sym_same(S, N, lane, ta - 1u, tg.x - 1u)) hit = true;
+                        if (ta && tg.x && sym_same(S.node, S.cval, N, lane, ta - 1u, tg.x - 1u)) hit = true;
                         break;
                     }
                     MPUSHCHK()
@@ -798,7 +803,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     if ((lflags & LANE_MEMTAG) && mtag_any(S, N, lane, a.w[0], 32u, nmsize)) {
                         if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                         uint32_t r;
-                        if (!sym_mem_ref(S, L, N, lane, a.w[0], 32u, nmsize, lnn, lnc, r))
+                        if (!sym_mem_ref(S, gp(L.mem), N, lane, a.w[0], 32u, nmsize, lnn, lnc, r))
                             MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
                         rtag = r + 1u;
                     } else {
@@ -858,7 +863,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     if (nmsize > msize) V.mzero(msize, nmsize);
                     MPUSHCHK()
                     uint32_t r;
-                    if (!sym_mem_ref(S, L, N, lane, a.w[0], len, nmsize, lnn, lnc, r) ||
+                    if (!sym_mem_ref(S, gp(L.mem), N, lane, a.w[0], len, nmsize, lnn, lnc, r) ||
                         !sym_node_push(S, N, lane, SYM_KECCAK | (256u << 8), r, 0u, 8u * len, lnn, rtag))
                         MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
                     rec_new = rec_head(L, lane, rec_at, MG_REC_SYMKECCAK, len, L.steps[lane] + executed, u_zero());
