@@ -803,7 +803,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     if ((lflags & LANE_MEMTAG) && mtag_any(S, N, lane, a.w[0], 32u, nmsize)) {
                         if (tl) MSTOPX(ST_ESCAPE, op | (ESC_SYMBOLIC << 8))
                         uint32_t r;
-                        if (!sym_mem_ref(S, gp(L.mem), N, lane, a.w[0], 32u, nmsize, lnn, lnc, r))
+                        if (!sym_mem_ref(S, L.mem, N, lane, a.w[0], 32u, nmsize, lnn, lnc, r))
                             MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
                         rtag = r + 1u;
                     } else {
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                     if (nmsize > msize) V.mzero(msize, nmsize);
                     MPUSHCHK()
                     uint32_t r;
-                    if (!sym_mem_ref(S, gp(L.mem), N, lane, a.w[0], len, nmsize, lnn, lnc, r) ||
+                    if (!sym_mem_ref(S, L.mem, N, lane, a.w[0], len, nmsize, lnn, lnc, r) ||
                         !sym_node_push(S, N, lane, SYM_KECCAK | (256u << 8), r, 0u, 8u * len, lnn, rtag))
                         MSTOPX(ST_ESCAPE, op | (ESC_ARENA << 8))
                     rec_new = rec_head(L, lane, rec_at, MG_REC_SYMKECCAK, len, L.steps[lane] + executed, u_zero());
