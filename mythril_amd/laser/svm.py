@@ -364,9 +364,14 @@ class LaserEVM:
         list; without a handler they are dropped as svm.py:314-316 drops a
         NotImplementedError.  Returns the lane-eligible states."""
         keep = []
+        # the encodings made here serve the batch's _shape and _pack (one encode per state)
+        self._pre_enc = pre = {}
         for st in states:
-            if sym.lane_eligible(st):
+            le = sym.lane_encoding(st)
+            if le is not None:
                 keep.append(st)
+                if le.symbolic:
+                    pre[id(st)] = (st, le)
                 continue
             self._flush_forks()
             if self.escape_handler is None:
@@ -703,12 +708,18 @@ class LaserEVM:
         mem_cap = (mem_cap + 31) // 32 * 32
         # symbolic lanes: their arena encodings (reused by _pack) size the planes
         self._encodings = {}
+        pre, self._pre_enc = getattr(self, "_pre_enc", None) or {}, None
         n_nodes = n_consts = 0
         for s in states:
-            if sym.state_is_symbolic(s):
+            got = pre.get(id(s))
+            if got is not None and got[0] is s:
+                le = self._encodings[id(s)] = got[1]
+            elif sym.state_is_symbolic(s):
                 le = self._encodings[id(s)] = sym.encode_state(s)
-                n_nodes = max(n_nodes, len(le.enc.nodes))
-                n_consts = max(n_consts, len(le.enc.consts))
+            else:
+                continue
+            n_nodes = max(n_nodes, len(le.enc.nodes))
+            n_consts = max(n_consts, len(le.enc.consts))
         symbolic = bool(self._encodings)
         return LaneShape(n=n, stack_cap=stack_cap, mem_cap=mem_cap,
                          calldata_cap=max((cdl + 31) // 32 * 32, 32),

@@ -813,11 +813,16 @@ def lane_eligible(state) -> bool:
     """Whether a lane can carry the state: every symbolic stack word, memory
     byte and storage key or value is an expression the arena represents
     (encode_state succeeds)."""
+    return lane_encoding(state) is not None
+
+
+def lane_encoding(state) -> Optional[LaneEncoding]:
+    """encode_state(state), or None when a lane cannot carry the state (the
+    batch keeps the encoding for its shape and its pack)."""
     try:
-        encode_state(state)
+        return encode_state(state)
     except NotEncodable:
-        return False
-    return True
+        return None
 
 
 def _pop2(s):
