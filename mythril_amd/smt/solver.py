@@ -229,6 +229,16 @@ class LRUCache:
 _MISSING = object()
 
 
+def _valid_bits(n: int) -> np.ndarray:
+    """The bitmap (uint64 words, bit i of word i >> 6) with the first n bits set."""
+    valid = np.zeros((n + 63) // 64, dtype=np.uint64)
+    full, rest = divmod(n, 64)
+    valid[:full] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    if rest:
+        valid[full] = np.uint64((1 << rest) - 1)
+    return valid
+
+
 def _raw(expr) -> Node:
     return expr.raw if isinstance(expr, Bool) else expr
 
@@ -364,14 +374,11 @@ class ModelCache:
             for c in cs:
                 distinct[c] = None
         plist = [c for c in distinct if c.op != "const"]
-        words = (len(pool) + 63) // 64
         rows = self.conjunct_rows(plist, pool)
-        ones = np.zeros(words, dtype=np.uint64)
-        for i in range(len(pool)):
-            ones[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
-        pos = {}
-        for i, m in enumerate(pool):
-            pos.setdefault(id(m), i)
+        ones = _valid_bits(len(pool))
+        # a model's first position (the dict keeps the last write: build back to front)
+        n = len(pool)
+        pos = dict(zip(map(id, reversed(pool)), range(n - 1, -1, -1)))
         # the bitmaps place models by id(): the entry keeps its pool's models
         # alive, so no model created later (after an LRU eviction frees one)
         # can take a dead model's id and read its bit
@@ -444,11 +451,7 @@ class ModelCache:
             for row, c in enumerate(kept):
                 rows[c] = bits[row]
         if derived:
-            valid = np.zeros((len(pool) + 63) // 64, dtype=np.uint64)
-            full, rest = divmod(len(pool), 64)
-            valid[:full] = np.uint64(0xFFFFFFFFFFFFFFFF)
-            if rest:
-                valid[full] = np.uint64((1 << rest) - 1)
+            valid = _valid_bits(len(pool))
             for c, q in derived.items():
                 r = rows.get(q)
                 if r is not None:
