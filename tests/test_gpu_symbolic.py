@@ -126,7 +126,12 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                 queue.extend(t for t in mine if sym.lane_eligible(t))
             elif st == MG_ESCAPE:
                 assert (int(b.aux[i]) >> 8) in (MG_ESC_SYMBOLIC, 1, 2, 3, 4, 8)
-    assert forks >= (1 if name in symcases.FIELD else 3) and device_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100) and checked > forks
+                if name == "memjump":
+                    # the host takes the jump (as LaserEVM's escape handler would):
+                    # the paths past it come back to the device
+                    queue.extend(t for t in eng.step(got) if sym.lane_eligible(t))
+    # memjump: two branches past its escaped jump
+    assert forks >= (1 if name in symcases.FIELD else 2 if name == "memjump" else 3) and device_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100) and checked > forks
     if name == "flag_array.sol.o":
         # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
         assert sym_exp > 0
