@@ -51,6 +51,11 @@ def _initial(ws, addr, txid="50"):
     return gs
 
 
+def _min_forks(name: str) -> int:
+    # memjump: two branches past its escaped jump
+    return 1 if name in symcases.FIELD else 2 if name == "memjump" else 3
+
+
 @pytest.mark.parametrize("name", symcases.ALL_CASES)
 def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
     ws, addr = symcases.deploy(dev, name)
@@ -130,8 +135,7 @@ def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
                     # the host takes the jump (as LaserEVM's escape handler would):
                     # the paths past it come back to the device
                     queue.extend(t for t in eng.step(got) if sym.lane_eligible(t))
-    # memjump: two branches past its escaped jump
-    assert forks >= (1 if name in symcases.FIELD else 2 if name == "memjump" else 3) and device_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100) and checked > forks
+    assert forks >= _min_forks(name) and device_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100) and checked > forks
     if name == "flag_array.sol.o":
         # _flags[idx]: EXP(256, idx % 32) of a symbolic index runs on the device
         assert sym_exp > 0
@@ -164,7 +168,7 @@ WORLD_READS = {"EXTCODESIZE", "EXTCODECOPY", "EXTCODEHASH", "BLOCKHASH", "NUMBER
 def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch):
     got, want, laser = symcases.run_both(dev, name, monkeypatch)
     assert got == want
-    assert laser.forks >= (1 if name in symcases.FIELD else 3) and \
+    assert laser.forks >= _min_forks(name) and \
         laser.lane_steps > (10 if name in symcases.SYNTH or name in symcases.FIELD else 100)
     # CALLDATACOPY of a symbolic size, memory offset or calldata offset, and MLOAD /
     # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
