@@ -9,6 +9,7 @@ T=${1:-u}
 OUT=gpurun_out/r05$T
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+AB_K2_MODES=scalar timeout -k 10 700 python3 -u scripts/ab_k2.py 3 ab/k2_v14.so > $OUT/ab_k2.log 2>&1 && \
 bash scripts/r05/gpu_sympmc.sh $T code && \
 bash scripts/r05/gpu_k2c4sq.sh $T && \
 timeout -k 10 300 python -u scripts/r05/prof_symtx.py $OUT/hostprof_exceptions.txt exceptions.sol.o 8 gpu > $OUT/hostprof.log 2>&1 && \
