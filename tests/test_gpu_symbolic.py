@@ -174,8 +174,9 @@ def test_symbolic_call_on_kernel1_equals_the_restatement(dev, name, monkeypatch)
     # MSTORE / MSTORE8 at symbolic offsets (environments.sol's batchTransfer moves
     # its free-memory pointer by a symbolic length) run on the device; what
     # escapes is the host's part
-    assert set(laser.escaped_ops) <= (HOST_OPS if name not in symcases.FIELD else HOST_OPS | WORLD_READS), \
-        dict(laser.escaped_ops)
+    # (memjump's jump to a target read back from symbolic memory is the host's by design)
+    allowed = HOST_OPS | (WORLD_READS if name in symcases.FIELD else set()) | ({"JUMP"} if name == "memjump" else set())
+    assert set(laser.escaped_ops) <= allowed, dict(laser.escaped_ops)
 
 
 @pytest.mark.parametrize("name", symcases.SYM_CREATIONS_ALL)
