@@ -38,7 +38,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .expr import Node
-from .program import ArrayInterp, FuncInterp
+from .program import ArrayInterp, FuncInterp, PoolColumns
 from .semantics import apply_op
 from .refute import refutes
 from .solver import Model, ModelRef, SolverBackendMissing, UnsatError, _conjuncts, query_raw
@@ -561,6 +561,7 @@ class SatSearchBackend:
         self.patience = patience       # rounds without a better best count before giving up
         self.rng = np.random.default_rng(seed)
         self._memo_completed: Dict[int, tuple] = {}
+        self._start_cols: Optional[tuple] = None      # (the starting pool's assignments, their PoolColumns)
         self.stats: Dict[str, int] = {"calls": 0, "refuted": 0, "seed": 0, "search": 0, "unknown": 0,
                                       "candidates": 0, "launches": 0, "minimised": 0}
 
@@ -602,13 +603,24 @@ class SatSearchBackend:
         self._memo_completed[id(assign)] = (assign, state, out)
         return out
 
+    def _columns(self, pool: List[Dict[str, object]]) -> PoolColumns:
+        """The starting pool's model columns, kept while the pool holds the same
+        completed assignments (the memo above returns the same objects until a
+        registration or the LRU changes): consecutive searches then serialise only
+        the variables they add, not every variable of 1,000+ models again.  A
+        completed assignment is never changed after it is made."""
+        got = self._start_cols
+        if got is None or len(got[0]) != len(pool) or not all(a is b for a, b in zip(got[0], pool)):
+            got = self._start_cols = (list(pool), PoolColumns(list(pool)))
+        return got[1]
+
     # -- kernel-2 scoring ---------------------------------------------------------------
-    def _score(self, conj: Sequence[Node], assigns: List[Dict[str, object]]):
+    def _score(self, conj: Sequence[Node], assigns: List[Dict[str, object]], columns=None):
         """(per-candidate satisfied-conjunct counts, index of a candidate that
         satisfies every conjunct or None, or False when a conjunct has no
         kernel-2 row: no candidate can then be reported); one kernel-2 launch."""
         models = [_model(a) for a in assigns]
-        rows = self.cache.conjunct_rows(list(conj), models)
+        rows = self.cache.conjunct_rows(list(conj), models, columns)
         self.stats["launches"] += 1
         self.stats["candidates"] += len(models)
         n = len(models)
@@ -637,7 +649,7 @@ class SatSearchBackend:
         lru = [m for m in reversed(self.cache.model_cache.lru_cache.keys()) if isinstance(m, Model)]
         seeds = lru + (self.cache._seed_models() or [_model({})])
         pool = [self._completed(m.raw[-1].assignment) for m in seeds]
-        counts, hit = self._score(conj, pool)
+        counts, hit = self._score(conj, pool, self._columns(pool))
         if hit is False:
             return None                        # a conjunct kernel 2 cannot evaluate
         if hit is not None:

@@ -439,7 +439,7 @@ class ModelCache:
             self._bits.update(out)
         return out
 
-    def conjunct_rows(self, conjuncts: Sequence[Node], pool: List) -> Dict[Node, np.ndarray]:
+    def conjunct_rows(self, conjuncts: Sequence[Node], pool: List, columns=None) -> Dict[Node, np.ndarray]:
         """Per conjunct, the bitmap of the pool's models that satisfy it, from
         ONE kernel-2 launch; conjuncts the device does not evaluate get no row.
         Every conjunct is compiled once per cache, by one compiler whose index
@@ -453,6 +453,10 @@ class ModelCache:
         (exceptions.sol.o -t 2: 89 % of them, over 3 generations in 150 groups)."""
         if not conjuncts or not pool:
             return {}
+        if columns is not None:
+            # a caller's own pool with its cached columns (program.PoolColumns over
+            # the pool's assignments, in order): the search's starting pool
+            return self._rows_uncached(conjuncts, pool, columns)
         gp = self._row_gen(pool)
         if gp is None:
             return self._rows_uncached(conjuncts, pool)
@@ -513,7 +517,7 @@ class ModelCache:
         perm[:h] = [gen.head_pos[i] for i in ids]
         return gen, perm
 
-    def _rows_uncached(self, conjuncts: Sequence[Node], pool: List) -> Dict[Node, np.ndarray]:
+    def _rows_uncached(self, conjuncts: Sequence[Node], pool: List, columns=None) -> Dict[Node, np.ndarray]:
         rows: Dict[Node, np.ndarray] = {}
         if self._compiler is None:
             self._compiler = Compiler()
@@ -543,7 +547,9 @@ class ModelCache:
                 kept.append(c)
         if kept:
             prog = batch_from(self._compiler, progs)
-            _, _, bits, ms = self.device.eval_bits(prog, self._pool(pool, prog))
+            mp = columns.pool(prog.var_names, prog.var_widths, prog.tables) if columns is not None \
+                else self._pool(pool, prog)
+            _, _, bits, ms = self.device.eval_bits(prog, mp)
             self.part_evals += len(kept) * len(pool)
             self.device_ms += float(ms or 0.0)
             self.launches += 1
