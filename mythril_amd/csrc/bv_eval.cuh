@@ -379,7 +379,10 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
         BvCtx c{values, consts, slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
         U256 acc = u_zero();
-        for (uint32_t p = p0; p < p1; ++p) {
+        // byte offsets into the tile (32-bit, wave-uniform): the scalar load takes the
+        // offset as its SGPR operand instead of a 64-bit address computed per instruction
+        const char *const tileb = reinterpret_cast<const char *>(insns + i0);
+        for (uint32_t off = p0 << 4, off_end = p1 << 4; off < off_end; off += 16u) {
             // c.m is the only per-lane context.  Round 3 hid its loop invariance
             // (an empty asm on it here) because min(m, n - 1) and m % 256 kept in
             // VGPRs across the loop spilled; with the predecoded dispatch the
@@ -387,7 +390,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
             // with them hoisted (profiles/r05/k2/ab_k2_q.log)
             uint32_t w0, ra, rb, rc;
             {
-                const uint4 ins = insns[i0 + uni(p)];
+                const uint4 ins = *reinterpret_cast<const uint4 *>(tileb + uni(off));
                 w0 = ins.x; ra = ins.y; rb = ins.z; rc = ins.w;
             }
             // op byte bit 7 = one operand (bv_predecode); w0 bit 30 = mask to width
@@ -503,10 +506,10 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_BINX: {
                     uint32_t e0, e1, e2;
                     {
-                        const uint4 x = insns[i0 + uni(p + 1u)];
+                        const uint4 x = *reinterpret_cast<const uint4 *>(tileb + uni(off + 16u));
                         e0 = x.x; e1 = x.y; e2 = x.z;
                     }
-                    ++p;                                     // the extension slot
+                    off += 16u;                              // the extension slot
                     const uint32_t k = (w0 >> 22) & 0x7u;
                     U256 t = bv_simple(e0 & 0xfu, A, B);
 #pragma unroll 1
@@ -539,10 +542,10 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     // from an extension slot {kinds | count << 28, B1, B2, B3}
                     uint32_t e0, e1, e2, e3;
                     {
-                        const uint4 x = insns[i0 + uni(p + 1u)];
+                        const uint4 x = *reinterpret_cast<const uint4 *>(tileb + uni(off + 16u));
                         e0 = x.x; e1 = x.y; e2 = x.z; e3 = x.w;
                     }
-                    ++p;
+                    off += 16u;
                     const uint32_t k = e0 >> 28;
 #pragma unroll 1
                     for (uint32_t j = 0; j < k; ++j) {

@@ -757,7 +757,12 @@ class WorldState:
             return acct
 
     def __copy__(self):
-        w = WorldState(self.transaction_sequence, [copy(a) for a in self._annotations], self.constraints)
+        # __init__'s fields without its fresh balance arrays (replaced right away)
+        w = WorldState.__new__(WorldState)
+        w._accounts = {}
+        w.constraints = list(self.constraints)
+        w.transaction_sequence = list(self.transaction_sequence)
+        w._annotations = [copy(a) for a in self._annotations]
         w.balances = copy(self.balances)
         w.starting_balances = copy(self.starting_balances)
         for k, a in self._accounts.items():
@@ -802,9 +807,10 @@ class Environment:
         self.chainid = symbol_factory.BitVecSym("chain_id", 256)
 
     def __copy__(self):
-        e = Environment(self.active_account, self.sender, self.calldata, self.gasprice, self.callvalue,
-                        self.origin, self.basefee, self.code, self.static)
-        e.active_function_name = self.active_function_name
+        # every field as it is (the words are immutable expressions; __init__
+        # would only rebuild the same block_number / chain_id symbols)
+        e = Environment.__new__(Environment)
+        e.__dict__.update(self.__dict__)
         return e
 
 
