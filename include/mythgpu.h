@@ -564,7 +564,9 @@ typedef struct mg_dag_batch {
 
 /* Candidate models, most-recently-used first (LRU order of
  * support_utils.py:62-63).  Variables absent from a model take 0
- * (z3 model_completion).
+ * (z3 model_completion).  The values table (n_vars x
+ * n_models x 32 bytes) must stay under 4 GiB: the kernel addresses it with
+ * 32-bit offsets, and a larger one is refused with MG_EINVAL.
  *
  * Tables are the models' interpretations of symbolic arrays (storage,
  * calldata, balances: array.py) and uninterpreted functions (keccak256_N and

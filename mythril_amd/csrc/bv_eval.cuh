@@ -191,8 +191,12 @@ DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
     const uint32_t kind = ref >> 30, idx = ref & 0x3fffffffu;
     U256 r;
     if (kind == BV_REF_VAR) {            // the commonest B operand (C4: 46 %) first
-        const size_t row = (size_t)idx * c.n_models + c.model();
-        const uint4 x = c.values[2 * row], y = c.values[2 * row + 1];
+        // a 32-bit byte offset from the table's base (bv_upload keeps the table
+        // under 4 GiB): the uniform part is one scalar multiply, the load takes the
+        // base as its SGPR address
+        const uint32_t off = (idx * c.n_models + c.model()) * 32u;
+        const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(c.values) + off);
+        const uint4 x = p[0], y = p[1];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
         BV_PIN("; variable operand", r);
@@ -715,6 +719,10 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
     if (dags->n_dags == 0 || !dags->prog_off || !dags->insns) { msg = "empty DAG batch"; return MG_EINVAL; }
     if (dags->n_slots > BV_MAX_SLOTS) { msg = "too many slots"; return MG_EINVAL; }
     if (models->n_models == 0 || (models->n_vars && !models->values)) { msg = "empty model batch"; return MG_EINVAL; }
+    if ((uint64_t)models->n_vars * models->n_models * 32u >= (1ull << 32)) {
+        msg = "model values over 4 GiB (variables x models x 32 bytes)";     // the kernel's 32-bit offsets
+        return MG_EINVAL;
+    }
     const uint32_t n = dags->n_dags;
     const uint32_t total = dags->prog_off[n];
     // validate programs on the host: refs in range, program fits a tile
