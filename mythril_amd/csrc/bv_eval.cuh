@@ -138,20 +138,21 @@ struct BvTables {
     const uint4 *__restrict__ dflt;
 };
 
-// Per lane, the whole context is ONE VGPR: m = chunk * BV_BLOCK + tid (the model
-// this thread evaluates, unclamped).  tid = m % BV_BLOCK addresses the LDS slots;
-// the value / table rows use min(m, n_models - 1) (a dead lane past the pool
-// reads the last model; its result is masked).  Keeping model, tid and the
-// live flag as separate VGPRs spilled them at 64 VGPRs inside the DAG loop
-// (12.6 GB of scratch traffic per C4 launch, profiles/r02/traffic.json).
+// Per lane, the context is two VGPRs: m = chunk * BV_BLOCK + tid (the model
+// this thread evaluates, unclamped) and the LDS address of the thread's slot
+// column (tid = m % BV_BLOCK, the same for every chunk: a slot access adds only
+// the slot's uniform offset, one VALU).  The value / table rows use
+// min(m, n_models - 1) (a dead lane past the pool reads the last model; its
+// result is masked).  Keeping model, tid and the live flag as separate VGPRs
+// spilled them at 64 VGPRs inside the DAG loop in round 2 (12.6 GB of scratch
+// traffic per C4 launch, profiles/r02/traffic.json); this build fits in 61.
 struct BvCtx {
     const uint4 *__restrict__ values;
     const uint4 *__restrict__ consts;
-    uint4 *slots;          // LDS [n_slots][2][BV_BLOCK]
+    uint4 *lane_slots;     // LDS [n_slots][2][BV_BLOCK], at this thread's column (+ tid)
     uint32_t n_models, m;
     BvTables tab;
     DEV uint32_t model() const { return min(m, n_models - 1u); }
-    DEV uint32_t tid() const { return m & (BV_BLOCK - 1u); }
 };
 
 DEV U256 ld2(const uint4 *p) {
@@ -162,6 +163,33 @@ DEV U256 ld2(const uint4 *p) {
     return r;
 }
 
+// Equality and zero tests as one VALU reduction and one compare.  Written plainly
+// (u256.cuh), instcombine turns (x0 | .. | x7) == 0 into eight per-limb compares
+// whose lane masks are joined by seven scalar s_or_b64 / s_and_b64 -- scalar issue,
+// which this kernel is bound by; the empty asm keeps the reduction in a VGPR.
+DEV bool bv_zero32(uint32_t o) {
+    asm volatile("" : "+v"(o));
+    return o == 0u;
+}
+DEV bool bv_eq(const U256 &a, const U256 &b) {
+    uint32_t o = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i] ^ b.w[i];
+    return bv_zero32(o);
+}
+DEV bool bv_iszero(const U256 &a) {
+    uint32_t o = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.w[i];
+    return bv_zero32(o);
+}
+DEV bool bv_fits32(const U256 &a) {
+    uint32_t o = 0u;
+#pragma unroll
+    for (int i = 1; i < 8; ++i) o |= a.w[i];
+    return bv_zero32(o);
+}
+
 // model interpretation lookup (entries are unique keys: first match wins)
 DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) {
     const uint32_t t = imm & 0xfffffu, part = (imm >> 20) & 1u, lo = (imm >> 21) & 0xffu;
@@ -170,7 +198,7 @@ DEV U256 bv_table(const BvCtx &c, const U256 &k0, const U256 &k1, uint32_t imm) 
     U256 v = ld2(c.tab.dflt + tm * 4u + part * 2u);
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint4 *e = c.tab.entries + (size_t)(s0 + k) * 8u;
-        if (u_eq(ld2(e), k0) && u_eq(ld2(e + 2), k1)) {
+        if (bv_eq(ld2(e), k0) && bv_eq(ld2(e + 2), k1)) {
             v = ld2(e + 4 + part * 2u);
             break;
         }
@@ -203,15 +231,17 @@ DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
         return r;
     }
     if (kind <= BV_REF_SLOT) {
-        const uint4 x = c.slots[(idx * 2u) * BV_BLOCK + c.tid()];
-        const uint4 y = c.slots[(idx * 2u + 1u) * BV_BLOCK + c.tid()];
+        const uint4 x = c.lane_slots[(idx * 2u) * BV_BLOCK];
+        const uint4 y = c.lane_slots[(idx * 2u + 1u) * BV_BLOCK];
         r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
         r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
         BV_PIN("; slot operand", r);
         return r;
     }
-    // constant: uniform address -> scalar loads
-    const uint4 x = c.consts[2 * (size_t)idx], y = c.consts[2 * (size_t)idx + 1];
+    // constant: uniform address -> scalar loads, at a 32-bit byte offset the load
+    // takes in an SGPR (bv_upload: the constant table is far below 4 GiB)
+    const uint4 *p = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(c.consts) + (idx << 5));
+    const uint4 x = p[0], y = p[1];
     r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
     r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
     BV_PIN("; constant operand", r);
@@ -230,7 +260,7 @@ DEV U256 bv_fetch(const BvCtx &c, uint32_t ref) {
 // signed ops and the overflow test share the second site
 DEV U256 bv_udivrem(bool quotient, const U256 &A, const U256 &B) {
     U256 q = u_ones(), r = A;                   // b == 0: bvudiv -> ones, bvurem -> a
-    if (!u_iszero(B)) u_divmod_nz_t<true>(A, B, q, r);
+    if (!bv_iszero(B)) u_divmod_nz_t<true>(A, B, q, r);
     return quotient ? q : r;
 }
 #define BV_DIV_OPS ((1ull << BV_SDIV) | (1ull << BV_SREM) | (1ull << BV_SMOD) | (1ull << BV_MUL_NOOVF_U))
@@ -248,7 +278,7 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
     }
     U256 keep = b;                              // divisor magnitude (SMOD) / B (MUL_NOOVF_U)
     if (op == BV_MUL_NOOVF_U) { keep = B; b = A; a = bv_mask(u_ones(), rc); }
-    const bool bz = u_iszero(b);
+    const bool bz = bv_iszero(b);
     U256 q = u_ones(), r = a;                   // b == 0: q = ones, r = a
     if (!bz) u_divmod_nz_t<true>(a, b, q, r);
     switch (op) {
@@ -258,7 +288,7 @@ DEV U256 bv_divop(uint32_t op, uint32_t width, uint32_t rc, const U256 &A, const
     case BV_SREM: return na ? u_neg(r) : r;     // b == 0: the signed dividend
     case BV_SMOD: {
         const U256 s = na ? u_neg(r) : r;       // srem: sign of the dividend
-        if (bz || u_iszero(s) || u_isneg(s) == nb) return s;
+        if (bz || bv_iszero(s) || u_isneg(s) == nb) return s;
         return u_add(s, nb ? u_neg(keep) : keep);   // smod: sign of the divisor
     }
     default:                                    // MUL_NOOVF_U: a*b <= 2^w-1 <=> b <= floor((2^w-1)/a)
@@ -374,6 +404,9 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     // thread index = the wave's first (an SGPR) + the lane id (v_mbcnt): nothing
     // keeps threadIdx.x alive across the loops
     const uint32_t wave0 = uni(threadIdx.x) & ~63u;
+    // this thread's column of the slot table (tid = m % BV_BLOCK = wave0 + lane for every
+    // chunk): a slot access adds only the slot's uniform offset
+    uint4 *const lane_slots = slots + wave0 + __lane_id();
     // DAG-major: one DAG's program (tens of instructions) is evaluated for all of
     // the block's model chunks while it is hot in the scalar cache; chunk-major
     // re-read the whole tile (up to 32 KiB) once per chunk, which the scalar
@@ -381,7 +414,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
     for (uint32_t d = d0; d < d1; ++d) {
     const uint32_t p0 = prog_off[d] - i0, p1 = prog_off[d + 1] - i0;
     for (uint32_t chunk = c_lo; chunk < c_hi; ++chunk) {
-        BvCtx c{values, consts, slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
+        BvCtx c{values, consts, lane_slots, n_models, chunk * BV_BLOCK + wave0 + __lane_id(), tab};
         U256 acc = u_zero();
         // byte offsets into the tile (32-bit, wave-uniform): the scalar load takes the
         // offset as its SGPR operand instead of a 64-bit address computed per instruction
@@ -420,8 +453,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     const uint32_t sub = (w0 >> 22) & 0x3fu;
                     bool t;
                     switch (sub) {
-                    case BV_EQ: t = u_eq(A, B); break;
-                    case BV_NE: t = !u_eq(A, B); break;
+                    case BV_EQ: t = bv_eq(A, B); break;
+                    case BV_NE: t = !bv_eq(A, B); break;
                     case BV_ULT: t = u_lt(A, B); break;
                     case BV_ULE: t = !u_lt(B, A); break;
                     case BV_UGT: t = u_lt(B, A); break;
@@ -448,7 +481,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_SHL: case BV_LSHR: case BV_ASHR: {
                     // a constant shift amount is wave-uniform: scalar-branch shifts
                     const bool ub = (rb >> 30) == BV_REF_CONST;
-                    const bool in = u_fits32(B) && B.w[0] < width;
+                    const bool in = bv_fits32(B) && B.w[0] < width;
                     if (op == BV_ASHR) {
                         const U256 sa = bv_sext(A, width);
                         const uint32_t fill = u_isneg(sa) ? 0xffffffffu : 0u;
@@ -467,8 +500,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                     }
                     break;
                 }
-                case BV_EQ: r = u_small(u_eq(A, B)); break;
-                case BV_NE: r = u_small(!u_eq(A, B)); break;
+                case BV_EQ: r = u_small(bv_eq(A, B)); break;
+                case BV_NE: r = u_small(!bv_eq(A, B)); break;
                 case BV_ULT: r = u_small(u_lt(A, B)); break;
                 case BV_ULE: r = u_small(!u_lt(B, A)); break;
                 case BV_UGT: r = u_small(u_lt(B, A)); break;
@@ -489,7 +522,7 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 case BV_CONCAT: r = u_or(u_shl_u(A, rc), B); break;                 // rc: uniform
                 case BV_ADD_NOOVF_U: {  // top bit of the (w+1)-bit sum is 0
                     const U256 s = u_add(A, B);
-                    const bool ovf = rc >= 256u ? u_lt(s, A) : !u_iszero(u_shr_u(s, rc, 0u));
+                    const bool ovf = rc >= 256u ? u_lt(s, A) : !bv_iszero(u_shr_u(s, rc, 0u));
                     r = u_small(!ovf);
                     break;
                 }
@@ -560,8 +593,8 @@ __global__ BV_BOUNDS void k_bv_eval(const uint4 *__restrict__ insns,
                 }
                 if ((w0 >> 17) & 1u) {
                     const uint32_t ds = (w0 >> 18) & 0xfu;
-                    slots[(ds * 2u) * BV_BLOCK + c.tid()] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
-                    slots[(ds * 2u + 1u) * BV_BLOCK + c.tid()] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
+                    lane_slots[(ds * 2u) * BV_BLOCK] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+                    lane_slots[(ds * 2u + 1u) * BV_BLOCK] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
                 }
             }
             acc = r;
@@ -718,6 +751,7 @@ static int bv_upload(BvState &s, const mg_dag_batch *dags, const mg_model_batch 
                      std::string &msg) {
     if (dags->n_dags == 0 || !dags->prog_off || !dags->insns) { msg = "empty DAG batch"; return MG_EINVAL; }
     if (dags->n_slots > BV_MAX_SLOTS) { msg = "too many slots"; return MG_EINVAL; }
+    if ((uint64_t)dags->n_consts * 32u >= (1ull << 32)) { msg = "constant table over 4 GiB"; return MG_EINVAL; }
     if (models->n_models == 0 || (models->n_vars && !models->values)) { msg = "empty model batch"; return MG_EINVAL; }
     if ((uint64_t)models->n_vars * models->n_models * 32u >= (1ull << 32)) {
         msg = "model values over 4 GiB (variables x models x 32 bytes)";     // the kernel's 32-bit offsets
