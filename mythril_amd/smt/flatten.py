@@ -440,11 +440,21 @@ def batch_from(c: "PyCompiler", progs: List[np.ndarray]) -> ProgramBatch:
         insns = np.concatenate(progs)
     else:
         insns = np.zeros((0, 4), dtype=np.uint32)
-    consts = np.stack([limbs(x) for x in c.consts]) if c.consts else np.zeros((0, 8), np.uint32)
-    names = [None] * len(c.var_widths)
-    for name, i in c.var_index.items():
-        names[i] = name
+    # the compiler's constant limbs and variable names, extended by what it added
+    # since the last batch (its index spaces only grow)
+    cache = getattr(c, "_batch_cache", None)
+    if cache is None:
+        cache = c._batch_cache = {"consts": np.zeros((0, 8), np.uint32), "names": []}
+    if cache["consts"].shape[0] < len(c.consts):
+        new = np.stack([limbs(x) for x in c.consts[cache["consts"].shape[0]:]])
+        cache["consts"] = np.concatenate([cache["consts"], new])
+    consts = cache["consts"]
+    names = cache["names"]
+    if len(names) < len(c.var_widths):
+        names.extend([None] * (len(c.var_widths) - len(names)))
+        for name, i in c.var_index.items():
+            names[i] = name
     tables = [None] * len(c.table_index)
     for name, t in c.table_index.items():
         tables[t] = c.lowering.tables[name]
-    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), names, list(c.var_widths), tables)
+    return ProgramBatch(insns, off, consts, max(c.max_slots, 1), list(names), list(c.var_widths), tables)

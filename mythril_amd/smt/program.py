@@ -33,6 +33,40 @@ MAX_SLOTS = 16       # kernel 2's 4-bit slot field (BV_MAX_SLOTS)
 TILE_INSNS = 2048
 
 
+# operand references per op (bv_upload: ite 3, one-operand ops 1, the rest 2)
+_NREF = np.array([3 if op == "ite" else 1 if op in UNARY else 2 for op in OPS], dtype=np.int64)
+def compact_vars(batch: "ProgramBatch") -> "ProgramBatch":
+    """The batch with its variables and tables renumbered to those its programs
+    read (a persistent compiler's batches carry every variable and table it has
+    seen; a pool built from model dicts then serialises all of them).  Same
+    programs, same values: only the index spaces shrink."""
+    ins = np.asarray(batch.insns, dtype=np.uint32)
+    if ins.shape[0] == 0:
+        return batch
+    op = (ins[:, 0] & 0xFF).astype(np.int64)
+    nref = _NREF[np.minimum(op, len(_NREF) - 1)]
+    isvar = [(nref > k) & ((ins[:, 1 + k] >> 30) == REF_VAR) for k in range(3)]
+    used = np.unique(np.concatenate([ins[m, 1 + k] & 0x3FFFFFFF for k, m in enumerate(isvar)]))
+    istab = op == OPCODE["tab"]
+    tabs = np.unique(ins[istab, 3] & TAB_INDEX_MASK) if istab.any() else np.zeros(0, dtype=np.uint32)
+    if used.size == len(batch.var_names) and tabs.size == len(batch.tables):
+        return batch
+    out = ins.copy()
+    vmap = np.zeros(max(len(batch.var_names), 1), dtype=np.uint32)
+    vmap[used] = np.arange(used.size, dtype=np.uint32)
+    for k, m in enumerate(isvar):
+        out[m, 1 + k] = (np.uint32(REF_VAR) << np.uint32(30)) | vmap[ins[m, 1 + k] & 0x3FFFFFFF]
+    if tabs.size:
+        tmap = np.zeros(max(len(batch.tables), 1), dtype=np.uint32)
+        tmap[tabs] = np.arange(tabs.size, dtype=np.uint32)
+        imm = ins[istab, 3]
+        out[istab, 3] = (imm & ~np.uint32(TAB_INDEX_MASK)) | tmap[imm & TAB_INDEX_MASK]
+    return ProgramBatch(out, batch.prog_off, batch.consts, batch.n_slots,
+                        [batch.var_names[i] for i in used.tolist()],
+                        [batch.var_widths[i] for i in used.tolist()],
+                        [batch.tables[i] for i in tabs.tolist()])
+
+
 def ref(kind: int, idx: int) -> int:
     return (kind << 30) | idx
 

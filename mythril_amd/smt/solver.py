@@ -39,7 +39,7 @@ import numpy as np
 from .expr import And, BitVec, Bool, Node, TRUE, _fold, _select, const, symbol_factory
 from .flatten import Compiler, batch_from, compile_sets
 from .lower import Unsupported
-from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, concat_pools
+from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, compact_vars, concat_pools
 
 NO_MODEL = 0xFFFFFFFF
 
@@ -335,6 +335,13 @@ class ModelCache:
         if len(self._memo) > self.QUICK_SAT_MEMO:
             self._memo.popitem(last=False)
 
+    def _seed_tailed(self, models: List) -> bool:
+        """Whether _pool takes the seed block from cached columns (the models end
+        with the seed list)."""
+        seeds = self.seeds
+        n = len(models) - len(seeds)
+        return bool(seeds) and n >= 0 and all(a is b for a, b in zip(models[n:], seeds))
+
     def _pool(self, models: List[Model], prog, key: Optional[Node] = None) -> ModelPool:
         seeds = self.seeds
         n = len(models) - len(seeds)
@@ -547,8 +554,15 @@ class ModelCache:
                 kept.append(c)
         if kept:
             prog = batch_from(self._compiler, progs)
-            mp = columns.pool(prog.var_names, prog.var_widths, prog.tables) if columns is not None \
-                else self._pool(pool, prog)
+            if columns is not None:
+                mp = columns.pool(prog.var_names, prog.var_widths, prog.tables)
+            else:
+                if not self._seed_tailed(pool):
+                    # a pool built from model dicts: only the variables and tables
+                    # these programs read (the seed block keeps the compiler's
+                    # numbering: its columns are cached by it)
+                    prog = compact_vars(prog)
+                mp = self._pool(pool, prog)
             _, _, bits, ms = self.device.eval_bits(prog, mp)
             self.part_evals += len(kept) * len(pool)
             self.device_ms += float(ms or 0.0)
