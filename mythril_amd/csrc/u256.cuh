@@ -166,6 +166,36 @@ DEV U256 u_shr_limbs(U256 a, uint32_t q, uint32_t fill) {
     }
     return a;
 }
+// The same limb moves with each stage skipped when no lane of the wave needs it
+// (one ballot each): in kernel 2's division the normalisation shift is below 32
+// bits for nearly every lane (random 256-bit divisors), so the three 8-wide
+// v_cndmask stages usually all drop out.
+DEV U256 u_shl_limbs_w(U256 a, uint32_t q) {
+#pragma unroll
+    for (int stage = 0; stage < 3; ++stage) {
+        const int s = 1 << stage;
+        const bool on = (q >> stage) & 1u;
+        if (__ballot(on) == 0ull) continue;
+        U256 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.w[i] = i >= s ? a.w[i - s] : 0u;
+        a = u_select(on, t, a);
+    }
+    return a;
+}
+DEV U256 u_shr_limbs_w(U256 a, uint32_t q, uint32_t fill) {
+#pragma unroll
+    for (int stage = 0; stage < 3; ++stage) {
+        const int s = 1 << stage;
+        const bool on = (q >> stage) & 1u;
+        if (__ballot(on) == 0ull) continue;
+        U256 t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.w[i] = i + s < 8 ? a.w[i + s] : fill;
+        a = u_select(on, t, a);
+    }
+    return a;
+}
 // (hi:lo) << r, high half, r in [0,32).  v_alignbit_b32 keeps each funnel
 // shift in one VALU op; written as a 64-bit shift of (hi << 32 | lo) the
 // compiler may merge adjacent limbs into 64-bit scratch loads instead.
@@ -189,6 +219,25 @@ DEV U256 u_shl_n(U256 a, uint32_t n) {
 // logical a >> n for n < 256; fill = 0 or 0xffffffff (arithmetic)
 DEV U256 u_shr_n(U256 a, uint32_t n, uint32_t fill) {
     a = u_shr_limbs(a, n >> 5, fill);
+    const uint32_t r = n & 31u;
+    U256 o;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) o.w[i] = fsr(a.w[i + 1], a.w[i], r);
+    o.w[7] = fsr(fill, a.w[7], r);
+    return o;
+}
+// u_shl_n / u_shr_n with the wave-skipped limb stages (kernel 2's division)
+DEV U256 u_shl_n_w(U256 a, uint32_t n) {
+    a = u_shl_limbs_w(a, n >> 5);
+    const uint32_t r = n & 31u;
+    U256 o;
+#pragma unroll
+    for (int i = 7; i >= 1; --i) o.w[i] = fsl(a.w[i], a.w[i - 1], r);
+    o.w[0] = a.w[0] << r;
+    return o;
+}
+DEV U256 u_shr_n_w(U256 a, uint32_t n, uint32_t fill) {
+    a = u_shr_limbs_w(a, n >> 5, fill);
     const uint32_t r = n & 31u;
     U256 o;
 #pragma unroll
@@ -292,6 +341,24 @@ DEV uint32_t mulhi32(uint32_t a, uint32_t b) { return __umulhi(a, b); }
 DEV uint32_t mg_reciprocal(uint32_t d) {
     return (uint32_t)((((uint64_t)(~d) << 32) | 0xffffffffull) / d);
 }
+// The same from the correctly rounded fp64 quotient 2^64 / d (absolute error < 2^-19),
+// made exact against the defining inequality (2^32 + v) d <= 2^64 - 1 < (2^32 + v + 1) d
+// (checked on the host for every d in [2^31, 2^32)): the 64-by-32 integer division
+// above is a long software sequence on the GPU.  Kernel 2's division sites use it
+// (C4 157.0 -> 154.6 ms); kernel 1 keeps the integer form (its C2 launch measured
+// 0.6 % slower with this one).
+DEV bool mg_recip_fits(uint32_t v, uint32_t d) {
+    const uint64_t vd = (uint64_t)v * d;
+    return (((uint64_t)d << 32) + vd) >= vd;          // no carry out of 2^64
+}
+DEV uint32_t mg_reciprocal_fp(uint32_t d) {
+    double e = 18446744073709551616.0 / (double)d - 4294967296.0;
+    e = e < 0.0 ? 0.0 : (e > 4294967295.0 ? 4294967295.0 : e);
+    uint32_t v = (uint32_t)e;
+    if (!mg_recip_fits(v, d)) v -= 1u;
+    else if (v != 0xffffffffu && mg_recip_fits(v + 1u, d)) v += 1u;
+    return v;
+}
 // (u1:u0) / d for u1 < d, d normalised, v = mg_reciprocal(d)  (MG 2011, Alg. 4)
 DEV uint32_t mg_div21(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v, uint32_t &rem) {
     const uint64_t p = (uint64_t)v * u1 + ((((uint64_t)u1 + 1u) << 32) | u0);
@@ -310,15 +377,22 @@ DEV uint32_t mg_div21(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v, uint32_t
 template <bool SKIP>
 DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256 &r, int dl) {
     const uint32_t s = 256u - lb;                       // normalisation shift, < 256
-    const U256 vn = u_shl_n(b, s);
-    const U256 lo = u_shl_n(a, s);
-    const U256 hi = s == 0u ? u_zero() : u_shr_n(a, 256u - s, 0u);
+    const U256 vn = SKIP ? u_shl_n_w(b, s) : u_shl_n(b, s);
+    const U256 lo = SKIP ? u_shl_n_w(a, s) : u_shl_n(a, s);
+    U256 hi;
+    if (SKIP && __ballot(s >= 32u) == 0ull) {
+        // every lane's shift is below one limb: a's top s bits are all that move up
+        hi = u_zero();
+        hi.w[0] = s == 0u ? 0u : a.w[7] >> (32u - s);
+    } else {
+        hi = s == 0u ? u_zero() : (SKIP ? u_shr_n_w(a, 256u - s, 0u) : u_shr_n(a, 256u - s, 0u));
+    }
     uint32_t u[17];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { u[i] = lo.w[i]; u[8 + i] = hi.w[i]; }
     u[16] = 0u;
     const uint32_t v7 = vn.w[7], v6 = vn.w[6];
-    const uint32_t rcp = mg_reciprocal(v7);
+    const uint32_t rcp = SKIP ? mg_reciprocal_fp(v7) : mg_reciprocal(v7);
     q = u_zero();
     // a < 2^256 so the digit at 2^256 is 0: u[15..8] < vn and the loop starts at 7
 #pragma unroll
@@ -373,7 +447,7 @@ DEV void u_divmod_knuth(const U256 &a, const U256 &b, uint32_t lb, U256 &q, U256
     U256 rn;
 #pragma unroll
     for (int i = 0; i < 8; ++i) rn.w[i] = u[i];
-    r = u_shr_n(rn, s, 0u);
+    r = SKIP ? u_shr_n_w(rn, s, 0u) : u_shr_n(rn, s, 0u);
 }
 
 // KNUTH_ALL (kernel 2's division sites): Knuth D with zero digits skipped for every
