@@ -7,5 +7,4 @@ export TMPDIR=/tmp
 T=${1:-ae}
 OUT=gpurun_out/r05$T
 mkdir -p $OUT
-timeout -k 10 400 python3 -u scripts/ab_libs.py mythril_amd/libmythgpu.so ab/f_ilp.so ab/f_bias0.so 3 > $OUT/ab_k1.log 2>&1 && \
-AB_K2_MODES=scalar timeout -k 10 500 python3 -u scripts/ab_k2.py 2 ab/f_ilp.so ab/f_bias0.so > $OUT/ab_k2.log 2>&1
+timeout -k 10 400 python3 -u scripts/ab_libs.py mythril_amd/libmythgpu.so ab/f_ilp.so ab/f_bias0.so 6 > $OUT/ab_k1.log 2>&1
