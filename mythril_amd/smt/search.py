@@ -451,13 +451,13 @@ class _Completed(dict):
 _DEPS: Dict[int, Tuple[Node, frozenset, bool]] = {}
 
 
-def _deps(raw: Node) -> Tuple[frozenset, bool]:
-    """(variable and array names a term reads, whether it reads an
-    uninterpreted function -- whose interpretation complete() rebuilds)."""
+def _deps(raw: Node) -> Tuple[frozenset, frozenset]:
+    """(variable and array names a term reads, the uninterpreted functions it
+    applies -- whose interpretations complete() rebuilds)."""
     got = _DEPS.get(id(raw))
     if got is not None and got[0] is raw:
         return got[1], got[2]
-    names, uf, seen, stack = set(), False, set(), [raw]
+    names, uf, seen, stack = set(), set(), set(), [raw]
     while stack:
         n = stack.pop()
         if id(n) in seen:
@@ -468,11 +468,11 @@ def _deps(raw: Node) -> Tuple[frozenset, bool]:
         elif n.op == "array":
             names.add(n.param[0])
         elif n.op == "uf":
-            uf = True
+            uf.add(n.param[0])
         stack.extend(n.args)
-    fs = frozenset(names)
-    _DEPS[id(raw)] = (raw, fs, uf)
-    return fs, uf
+    fs, fu = frozenset(names), frozenset(uf)
+    _DEPS[id(raw)] = (raw, fs, fu)
+    return fs, fu
 
 
 def _changed(rep: Repair) -> frozenset:
@@ -507,8 +507,12 @@ def complete(assign: Dict[str, object], base: Optional[_Completed] = None,
         for x in dict.fromkeys(x.raw for x in xs):      # registered once per SHA3 executed
             v = prev.get(x) if prev is not None else None
             if v is not None:
-                names, uf = _deps(x)
-                if uf or (names & changed):
+                # the base's value stands unless the input reads a changed name or
+                # an uninterpreted function the assignment interprets (during this
+                # loop `out` holds no keccak / Power tables: ev gives their
+                # applications the completion value, as it did for the base)
+                names, ufs = _deps(x)
+                if (names & changed) or (ufs & changed) or any(u in out for u in ufs):
                     v = None
             if v is None:
                 v = ev(x)
