@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--host-profile", default=None,
                     help="directory: cProfile the LaserEVM fields (hooked_c2, taint_c2, symbolic_tx) "
                          "and write each one's cumulative-time table there")
+    ap.add_argument("--full-record", default="gpurun_out/bench_full.json",
+                    help="where the whole record goes (stdout carries the compact line, <= 4 KB)")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the profiling pass behind `roofline` (CPU rehearsals of the rank launcher)")
     return ap.parse_args(argv)
@@ -341,9 +343,107 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["symbolic_tx"] = symb
         if analyses is not None:
             out["myth_analyze"] = analyses
-        print(json.dumps(out), flush=True)
+        full = Path(args.full_record)
+        try:
+            full.parent.mkdir(parents=True, exist_ok=True)
+            full.write_text(json.dumps(out, indent=1) + "\n")
+        except OSError as e:
+            _log(rank, f"full record not written ({e})")
+        print(json.dumps(compact_line(out, str(args.full_record))), flush=True)
     if dist_on:
         dist.destroy_process_group()
+
+
+LINE_LIMIT = 4096
+
+
+def _r(x, digits: int = 4):
+    """Floats to `digits` significant digits (the compact line's size)."""
+    if isinstance(x, float):
+        return float(f"{x:.{digits}g}")
+    if isinstance(x, dict):
+        return {k: _r(v, digits) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_r(v, digits) for v in x]
+    return x
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(out: dict, full_record: str) -> dict:
+    """The one JSON line the driver reads (at most LINE_LIMIT bytes): the
+    contract keys, the headline roofline and CPU baseline, and a summary of
+    every secondary field; the whole record goes to `full_record`."""
+    line = _pick(out, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                       "higher_is_better", "scaling", "vs_baseline", "dtype", "data"))
+    line["config"] = _pick(out.get("config", {}), ("workload", "lanes_per_gpu", "lane_steps_per_batch",
+                                                   "kernel_ms_per_batch", "parallelism"))
+    roof = out.get("roofline")
+    if roof:
+        line["roofline"] = _pick(roof, ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                        "kernel_ms", "priced_as", "traffic_frac", "frac_sustained"))
+        if "alt" in roof:
+            line["roofline"]["alt"] = _pick(roof["alt"], ("bound", "frac"))
+    else:
+        line["roofline"] = None
+    cb = out.get("cpu_baseline")
+    line["cpu_baseline"] = (_pick(cb, ("value", "unit", "cores", "kind", "sample", "single_core_value",
+                                       "usable_cores")) if cb else None)
+    f = {}
+    c4 = out.get("constraint_evals")
+    if c4:
+        f["c4"] = _pick(c4, ("value", "unit", "ms_per_step", "scaling"))
+        if c4.get("roofline"):
+            f["c4"]["roofline"] = _pick(c4["roofline"], ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                         "frac_sustained"))
+        if c4.get("cpu_baseline"):
+            f["c4"]["cpu_baseline"] = _pick(c4["cpu_baseline"], ("value", "cores", "kind"))
+    for k in ("c2_unbucketed", "c2_two_streams", "c2_large_contract"):
+        if out.get(k):
+            f[k] = out[k].get("value")
+    if out.get("hooked_c2"):
+        f["hooked_c2"] = out["hooked_c2"].get("lane_steps_per_s")
+    if out.get("taint_c2"):
+        t = out["taint_c2"]
+        f["taint_c2"] = {m: t[m].get("lane_steps_per_s") for m in ("device", "host") if isinstance(t.get(m), dict)}
+    for k in ("symbolic_lanes", "taint_lanes"):
+        v = out.get(k)
+        if v:
+            f[k] = {"value": v.get("lane_steps_per_s"), "steps_per_lane": (v.get("lane_steps_per_launch", 0) /
+                                                                           max(v.get("lanes", 1), 1)),
+                    "frac": (v.get("roofline") or {}).get("frac")}
+    st = out.get("symbolic_tx")
+    if st:
+        f["symbolic_tx_wall_s"] = {n.replace(".sol.o", ""): c.get("wall_s") for n, c in st.get("contracts", {}).items()}
+    ma = out.get("myth_analyze")
+    if ma:
+        m = {"contracts": ma.get("contracts_analysed"), "job_wall_s": ma.get("job_wall_s"),
+             "host_fraction": ma.get("host_fraction"), "totals": ma.get("totals")}
+        cpu = ma.get("cpu_baseline")
+        if cpu:
+            m["cpu"] = _pick(cpu, ("value", "wall_s", "cores", "issue_sets_match", "counters_match",
+                                   "unknown_confirmations"))
+            m["mismatched"] = (cpu.get("mismatched") or [])[:4]
+        for k in ("solver", "c3"):
+            if k in ma:
+                m[k] = ma[k]
+        f["myth_analyze"] = m
+    if out.get("c3_bectoken"):
+        f["c3_bectoken"] = out["c3_bectoken"].get("summary", out["c3_bectoken"])
+    line["fields"] = f
+    line["full_record"] = full_record
+    line = _r(line)
+    # the limit is the contract: shed the least important summaries first
+    for k in ("symbolic_tx_wall_s", "taint_lanes", "c2_large_contract", "c2_unbucketed", "taint_c2",
+              "hooked_c2", "c3_bectoken", "myth_analyze"):
+        if len(json.dumps(line)) <= LINE_LIMIT:
+            break
+        line["fields"].pop(k, None)
+    if len(json.dumps(line)) > LINE_LIMIT and line.get("cpu_baseline"):
+        line["cpu_baseline"]["sample"] = line["cpu_baseline"].get("sample", "")[:120]
+    return line
 
 
 # SURVEY §8(b): the opcodes the default detection modules hook (union of
@@ -907,7 +1007,10 @@ def _myth_analyze_rows(device, k2, tx_count: int, names, log=None):
                       "wall_s": info["wall_s"], "kernel1_s": k1_s, "kernel2_s": k2_s,
                       "lane_steps": int(info["lane_steps"]), "constraint_evals": int(info["device_evals"]),
                       "launches_kernel2": int(info["kernel2_launches"]), "forks": info["forks"],
-                      "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown")},
+                      "fork_filter": {k: info["fork_filter"].get(k) for k in ("groups", "queries", "kept", "pruned",
+                                                                               "unknown")},
+                      "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown")
+                                 if k in info["search"]},
                       "constraint_evals_per_s_wall": info["device_evals"] / info["wall_s"] if info["wall_s"] else None}
     return rows
 
@@ -981,15 +1084,19 @@ def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True)
            "contracts": rows}
     if cpu_rows is not None:
         import platform
+        from oracle.cpu_baseline import _cores_info, _cpu_share
         cw = sum(r["wall_s"] for r in cpu_rows.values())
         mismatched = sorted(n for n in rows if rows[n]["issues"] != cpu_rows[n]["issues"])
+        counters = ("confirmations", "forks", "fork_filter", "search", "escapes_dropped")
+        mismatched_counters = sorted(n for n in rows if any(rows[n][k] != cpu_rows[n][k] for k in counters))
         out["cpu_baseline"] = {
             "value": len(cpu_rows) / cw, "unit": "contracts/s", "wall_s": cw,
-            "cores": min(16, os.cpu_count() or 1), "kind": "port",
+            **_cores_info(_cpu_share()), "kind": "port",
             "sample": "the same 18 analyses, host layer + oracle/evm_ref.c (1 thread) as kernel 1 + "
-                      "oracle/bv_ref.c (%d threads) as kernel 2 (%s)" % (min(16, os.cpu_count() or 1),
+                      "oracle/bv_ref.c (%d threads) as kernel 2 (%s)" % (_cpu_share(),
                                                                          _cpu_model() or platform.processor()),
             "issue_sets_match": not mismatched, "mismatched": mismatched,
+            "counters_match": not mismatched_counters, "mismatched_counters": mismatched_counters,
             "wall_s_per_contract": {n: r["wall_s"] for n, r in cpu_rows.items()},
             "unknown_confirmations": sum(r["confirmations"]["unknown"] for r in cpu_rows.values())}
         out["speedup_vs_cpu"] = cw / tot["wall_s"] if tot["wall_s"] else None

@@ -1059,6 +1059,8 @@ __global__ __launch_bounds__(256) void k_sym_step(DevLanes L, DevSym S, DevTaint
                 else if (op == 0x18u && (sym_width(S, N, lane, ta) == 1u || sym_width(S, N, lane, tb) == 1u))
                     esc = true;                                          // Bool ^ ...
                 else if (zero_div || (op == 0x1au && !(u_fits32(a) && a.w[0] < 32u))) rval = u_zero();
+                else if (op == 0x14u && ta && tb && sym_same(S.node, S.cval, N, lane, ta - 1u, tb - 1u))
+                    rval = u_small(1u);     // x == x: the expression layer folds it (expr._fold), If(True, 1, 0)
                 else if (!sym_ref(S, N, lane, ta, a, lnc, ya) || !sym_ref(S, N, lane, tb, b, lnc, yb) ||
                          !sym_node_push(S, N, lane, SYM_BIN | ((sym_is_cmp(op) ? 1u : 256u) << 8), ya, yb, op,
                                         lnn, rtag))

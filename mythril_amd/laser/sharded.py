@@ -29,6 +29,8 @@ from __future__ import annotations
 from copy import copy
 from typing import Dict, List, Optional, Sequence
 
+import struct
+
 import numpy as np
 
 from .disassembly import Disassembly
@@ -163,7 +165,7 @@ class _Words:
 # Plain values (None, bool, int of any size and sign, str, bytes, tuple, list,
 # dict) as a u32 stream: a tag word, then the payload; what travels between
 # ranks besides models (code keys, keccak / EXP registrations, issues).
-_T_NONE, _T_FALSE, _T_TRUE, _T_INT, _T_NEG, _T_STR, _T_BYTES, _T_TUPLE, _T_LIST, _T_DICT = range(10)
+_T_NONE, _T_FALSE, _T_TRUE, _T_INT, _T_NEG, _T_STR, _T_BYTES, _T_TUPLE, _T_LIST, _T_DICT, _T_FLOAT = range(11)
 
 
 def _put_bytes(out: list, b: bytes) -> None:
@@ -180,6 +182,9 @@ def _put_value(out: list, v) -> None:
     elif isinstance(v, int):
         out.append(_T_INT if v >= 0 else _T_NEG)
         _put_big(out, abs(v))
+    elif isinstance(v, float):
+        out.append(_T_FLOAT)                    # IEEE-754 binary64, two words
+        _put_bytes(out, struct.pack("<d", v))
     elif isinstance(v, str):
         out.append(_T_STR)
         _put_bytes(out, v.encode())
@@ -224,6 +229,8 @@ def _get_value(r: "_Words"):
     if t in (_T_INT, _T_NEG):
         v = r.big()
         return v if t == _T_INT else -v
+    if t == _T_FLOAT:
+        return struct.unpack("<d", _get_bytes(r))[0]
     if t == _T_STR:
         return _get_bytes(r).decode()
     if t == _T_BYTES:
@@ -560,28 +567,52 @@ def sync_function_managers() -> int:
     return got
 
 
+def _issue_code_key(d: dict):
+    """The code half of a module's cache key for an issue's attribute dict:
+    the reference's Issue stores bytecode_hash (report.py:70) and the modules
+    cache (address, bytecode_hash) (base.py:63-70, exceptions.py:57); an issue
+    type that keeps the bytecode itself is keyed on that."""
+    if d.get("bytecode_hash") is not None:
+        return d["bytecode_hash"]
+    return d.get("bytecode")
+
+
 def merge_issues(modules, issue_type=None) -> int:
     """after sharded rounds every rank holds the issues its own
     paths filed.  All ranks' issues of each detection module (same module
     order on every rank) are gathered in rank order and de-duplicated by the
-    modules' own cache key, (address, bytecode) -- base.py:63-96 keys on
-    (address, code hash); Exceptions on (source location, code hash) --
-    keeping the first; each module's ``issues`` and cache become the merged
-    set on every rank.  Issues travel as their attribute dicts (value stream,
-    no pickling) and are rebuilt as `issue_type` (default: the class of the
-    issues the local modules hold).  Returns the merged count."""
+    modules' own cache key -- (address, code hash) for the modules that cache
+    automatically (base.py:63-96), (source location, code hash) for
+    Exceptions -- keeping the first; each module's ``issues`` become the
+    merged set on every rank and its cache gets their keys through the
+    module's own ``update_cache`` (or, for a module that caches by source
+    location, in that form), so re-detection is suppressed as the module
+    itself would suppress it.  Issues travel as their attribute dicts (value
+    stream, no pickling; floats such as discovery_time included) and are
+    rebuilt as `issue_type` (default: the class of the issues the local
+    modules hold).  An attribute the stream cannot carry raises TypeError
+    rather than being dropped.  Returns the merged count."""
     from .. import dist as mdist
     _, world = mdist.rank_world()
-    local = [[{k: v for k, v in vars(i).items() if _sendable(v)} for i in m.issues] for m in modules]
+    local = []
+    for m in modules:
+        rows = []
+        for i in m.issues:
+            d = dict(vars(i))
+            for k, v in d.items():
+                if not _sendable(v):
+                    raise TypeError(f"issue attribute {k!r} ({type(v).__name__}) cannot be sent between ranks")
+            rows.append(d)
+        local.append(rows)
     parts = _allgather_values(local) if world > 1 else [local]
     cls = issue_type or next((type(i) for m in modules for i in m.issues), None)
     total = 0
     for k, m in enumerate(modules):
-        exceptions = getattr(m, "auto_cache", True) is False
+        by_location = getattr(m, "auto_cache", True) is False
         merged, keys = [], set()
         for part in parts:
             for d in (part[k] if part else []):
-                key = (d.get("source_location") if exceptions else d.get("address"), d.get("bytecode"))
+                key = (d.get("source_location") if by_location else d.get("address"), _issue_code_key(d))
                 if key in keys:
                     continue
                 keys.add(key)
@@ -589,7 +620,10 @@ def merge_issues(modules, issue_type=None) -> int:
                 issue.__dict__.update(d)
                 merged.append(issue)
         m.issues = merged
-        m.cache |= keys
+        if by_location or not hasattr(m, "update_cache"):
+            m.cache |= keys
+        else:
+            m.update_cache(merged)
         total += len(merged)
     return total
 

@@ -50,7 +50,7 @@ import numpy as np
 
 from ..lanes import (LaneBatch, LaneShape, MG_DEPTH, MG_ENV_WORDS, MG_ESCAPE, MG_ESC_MEMORY,
                      MG_ESC_RECORD, MG_ESC_STACK, MG_ESC_STORAGE, MG_ESC_TRACE, MG_ESC_ARENA,
-                     MG_ESC_TAINT, MG_FORK, MG_LANE_BALANCE, MG_LANE_SYMBOLIC, MG_LANE_TAINT,
+                     MG_ESC_SYMBOLIC, MG_ESC_TAINT, MG_FORK, MG_LANE_BALANCE, MG_LANE_SYMBOLIC, MG_LANE_TAINT,
                      MG_EXC_STACK_UNDERFLOW,
                      MG_HALT_DROPPED, MG_LOOP_BOUND,
                      MG_HALT_END, MG_HALT_RETURN, MG_HALT_REVERT, MG_HALT_STOP, MG_HOOK,
@@ -1146,6 +1146,17 @@ class LaserEVM:
         if status != MG_FORK:
             self._flush_forks()        # queued fork filters come first (reference order)
         self._materialise(b, i, s)
+        if status == MG_FORK and len(s.mstate.stack) >= 2 and s.mstate.stack[-2].value is not None:
+            # the device tagged the condition symbolic, but its term folds to a
+            # constant on the host (an arena node over words the decode resolves:
+            # a store-chain read, a memory read, a balance): the reference's JUMPI
+            # is concrete there, so the lane takes the path of any instruction the
+            # device left to the host -- exactly where a lane whose word was
+            # concrete from the start goes (tests/oracle_device.py parks it so)
+            self._flush_forks()
+            status = MG_ESCAPE
+            b.status[i] = MG_ESCAPE
+            b.aux[i] = OPCODES["JUMPI"] | (MG_ESC_SYMBOLIC << 8)
         instrs = s.environment.code.instruction_list
         name = instrs[s.mstate.pc]["opcode"] if s.mstate.pc < len(instrs) else None
         self._sched.set(i, "done")

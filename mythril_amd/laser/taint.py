@@ -103,13 +103,18 @@ class IfSymbolic:
 @dataclass(frozen=True)
 class IfStateAnnotation:
     """A pre-hook with work only when the state carries an annotation of one of
-    `types` (class names in the module's Python module); such annotations come
-    from host events, so the host knows them when it packs the lane.  Without
-    one, StateChangeAfterCall's hook (state_change_external_calls.py:124-131)
-    still creates an empty PotentialIssuesAnnotation; a skipped hook does not,
-    and nothing reads an empty one (check_potential_issues makes its own when
-    missing, potential_issues.py:100, and its search importance is 0)."""
+    `types`, or lacks one of `missing` (class names in the module's Python
+    module); such annotations come from host events, so the host knows them
+    when it packs the lane.  `missing`: StateChangeAfterCall's hook
+    (state_change_external_calls.py:124-131) creates an empty
+    PotentialIssuesAnnotation on a state that has none, even when it files
+    nothing -- and that matters: the annotation has no __copy__, so every
+    state copied from this one later shares its issue list
+    (potential_issues.py:65-90), and a potential issue one branch files is
+    checked at the other branch's transaction end.  So the device stops there
+    (the host runs the hook) until the state has one."""
     types: Tuple[str, ...]
+    missing: Tuple[str, ...] = ()
 
 
 # The reference's modules (class name) -> {(hook type, opcode): action}
@@ -141,8 +146,10 @@ BATCH_SAFE: Dict[str, Dict[Tuple[str, str], object]] = {
     "Exceptions": {("pre", "JUMP"): Deferred(1)},
     # state_change_external_calls.py:112, 148-160: SLOAD/SSTORE return at once
     # while the state has no StateChangeCallsAnnotation (made by CALL hooks)
-    "StateChangeAfterCall": {("pre", "SLOAD"): IfStateAnnotation(("StateChangeCallsAnnotation",)),
-                             ("pre", "SSTORE"): IfStateAnnotation(("StateChangeCallsAnnotation",))},
+    "StateChangeAfterCall": {("pre", "SLOAD"): IfStateAnnotation(("StateChangeCallsAnnotation",),
+                                                                 ("PotentialIssuesAnnotation",)),
+                             ("pre", "SSTORE"): IfStateAnnotation(("StateChangeCallsAnnotation",),
+                                                                  ("PotentialIssuesAnnotation",))},
 }
 
 
@@ -169,11 +176,21 @@ def _spec(hook: Callable, hook_type: str, opcode: str):
 
 
 def _resolve_types(mod, names) -> Tuple[type, ...]:
+    """Classes named `names` in the module's Python module -- or, for a name it
+    does not import, in the modules its imported functions come from (the
+    reference's state_change_external_calls.py imports
+    get_potential_issues_annotation, not PotentialIssuesAnnotation)."""
     import sys
     pymod = sys.modules.get(type(mod).__module__)
     out = []
     for n in names:
         t = getattr(pymod, n, None)
+        if not isinstance(t, type):
+            for v in list(vars(pymod).values()) if pymod is not None else ():
+                home = sys.modules.get(getattr(v, "__module__", None) or "")
+                if callable(v) and home is not None and isinstance(getattr(home, n, None), type):
+                    t = getattr(home, n)
+                    break
         if isinstance(t, type):
             out.append(t)
     return tuple(out)
@@ -196,6 +213,7 @@ class TaintPlan:
         self.op_modules: Dict[int, List] = {}          # safe opcode -> modules hooked on it
         self.deferred: Dict[int, List[Callable]] = {}    # opcode -> Deferred hooks, in order
         self.iflane_types: Tuple[type, ...] = ()
+        self.iflane_missing: Tuple[type, ...] = ()     # yield while the state lacks one
         if laser._execute_state_hooks:
             return                                     # every opcode is a host event anyway
         sink_mod = None
@@ -221,6 +239,8 @@ class TaintPlan:
                 continue
             if any(not 1 <= s.words <= 3 for _, s in defers):
                 continue
+            if any(len(_resolve_types(_module_of(h), s.missing)) != len(s.missing) for h, s in iflanes):
+                continue                                # a side effect the host cannot see: host hooks
             if len({a.operand for a in ann}) > 1 or any(a.operand > 1 for a in ann):
                 continue
             if len({s.operand for _, s in sinks}) > 1 or len({s.operand for _, s in yields}) > 1:
@@ -262,6 +282,7 @@ class TaintPlan:
                 word |= MG_TAINT_IFLANE
                 for h, s in iflanes:
                     self.iflane_types += _resolve_types(_module_of(h), s.types)
+                    self.iflane_missing += _resolve_types(_module_of(h), s.missing)
             self.actions[op] = word
             self.safe.add(op)
             mods = []
@@ -415,8 +436,10 @@ def pack(b, i: int, state, lt: LaneTaint, plan: Optional[TaintPlan]) -> bool:
             if any(isinstance(a, plan.yield_types) for a in s):
                 ym |= 1 << k
     b.ymask[i] = ym
-    if plan is not None and plan.iflane_types and any(
-            isinstance(a, plan.iflane_types) for a in state.annotations):
+    if plan is not None and ((plan.iflane_types and any(isinstance(a, plan.iflane_types)
+                                                        for a in state.annotations))
+                             or any(not any(isinstance(a, t) for a in state.annotations)
+                                    for t in plan.iflane_missing)):
         b.tflags[i] = 2                    # MG_TAINT_IFLANE hooks have work on this path
     return True
 

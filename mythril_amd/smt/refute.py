@@ -63,7 +63,9 @@ def _unit(c: Node) -> Optional[tuple]:
         ite, k = c.args
         if ite.args[1].op != "const" or ite.args[2].op != "const" or ite.args[1].param == ite.args[2].param:
             return None
-        holds = (k.param == ite.args[1].param) == (c.op == "eq")
+        # P holds exactly when eq(ite, then-value) or distinct(ite, else-value);
+        # any other constant leaves P open (distinct(ite(P,1,0), 2) is a tautology)
+        holds = k.param == (ite.args[1].param if c.op == "eq" else ite.args[2].param)
         if not holds:
             return None
         c = ite.args[0]

@@ -13,7 +13,8 @@ def eval_batch(prog, models, first: int = 0, count: int = None, threads: int = 0
     program's per-model satisfaction bitmap."""
     n = prog.n_dags
     count = n - first if count is None else count
-    threads = threads or min(16, os.cpu_count() or 1)
+    from .cpu_baseline import _cpu_share
+    threads = threads or _cpu_share()
     fs = np.zeros(n, dtype=np.uint32)
     sc = np.zeros(n, dtype=np.uint32)
     insns = np.ascontiguousarray(prog.insns, dtype=np.uint32)

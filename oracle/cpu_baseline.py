@@ -25,10 +25,28 @@ def _cpu_model():
 
 
 def _usable_cores():
+    """CPUs this process may run on (its affinity mask)."""
     try:
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+def _cpu_share():
+    """The threads the comparator uses: every usable core, unless the host
+    states this job's CPU share (OMP_NUM_THREADS -- the GPU box sets it to the
+    share of one GPU, 16, and asks worker pools to stay within it)."""
+    n = _usable_cores()
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        share = 0
+    return min(n, share) if share > 0 else n
+
+
+def _cores_info(threads: int) -> dict:
+    return {"cores": threads, "usable_cores": _usable_cores(), "host_cpus": os.cpu_count(),
+            "cpu_share_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": _cpu_model()}
 
 
 def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, threads: int = 0) -> dict:
@@ -36,7 +54,7 @@ def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, thread
     o = OracleEVM()
     cid = o.load_code(code)
     base = workloads.c2_batch(lanes, code_id=cid, stack_cap=64, mem_cap=1024, rec_cap=128)
-    threads = threads or min(16, _usable_cores())
+    threads = threads or _cpu_share()
     mask = (ctypes.c_uint64 * 4)(0, 0, 0, 0)
     lib().orc_run_mt.restype = ctypes.c_uint64
     lib().orc_run_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
@@ -55,7 +73,7 @@ def c2_lane_steps(code: bytes, seconds: float = 10.0, lanes: int = 65536, thread
 
     single, reps1 = timed(1, min(seconds / 3, 5.0))
     multi, repsn = timed(threads, seconds)
-    return {"value": multi, "unit": "lane-steps/s", "cores": threads, "kind": "port",
+    return {"value": multi, "unit": "lane-steps/s", **_cores_info(threads), "kind": "port",
             "sample": f"C2 batch ({lanes} lanes, overflow.sol.o) x {repsn} runs on {threads} threads; "
                       f"C oracle oracle/evm_ref.c -O3 ({_cpu_model()})",
             "single_core_value": single}
@@ -66,7 +84,7 @@ def c4_evals(n_models: int = 4096, seconds: float = 10.0, threads: int = 0) -> d
     models), one pthread per core."""
     from mythril_amd.smt import synth
     from .bv_ref import eval_batch
-    threads = threads or min(16, _usable_cores())
+    threads = threads or _cpu_share()
     models = synth.c4_models(n_models, synth.C4_SEED + 0x1000)
     prog = synth.c4_programs(synth.Draws(4096, synth.C4_SEED))
     done, el, d = 0, 0.0, 0
@@ -77,6 +95,6 @@ def c4_evals(n_models: int = 4096, seconds: float = 10.0, threads: int = 0) -> d
         el += time.perf_counter() - t0
         done += cnt * n_models
         d += cnt
-    return {"value": done / el, "unit": "constraint-evals/s", "cores": threads, "kind": "port",
+    return {"value": done / el, "unit": "constraint-evals/s", **_cores_info(threads), "kind": "port",
             "sample": f"{d} C4 DAGs x {n_models} models on {threads} threads; oracle/bv_ref.c -O3 "
                       f"({_cpu_model()})"}

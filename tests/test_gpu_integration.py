@@ -67,3 +67,15 @@ def test_all_modules_issue_set_equals_the_oracle_devices(name, dev, monkeypatch,
     ci, cinfo = analyze.analyze(name, None, 2, OracleDevice(), OracleK2())
     assert analyze.issue_table(gi) == analyze.issue_table(ci), (ginfo, cinfo)
     assert ginfo["escapes_dropped"] == cinfo["escapes_dropped"]
+    # the run itself, not only its issues -- the fork events
+    # (a JUMPI the device tagged symbolic whose term folds to a constant is no
+    # fork), the fork filter's verdicts, every confirmation and what the
+    # solver backend answered
+    assert ginfo["forks"] == cinfo["forks"], (ginfo["forks"], cinfo["forks"])
+    ff = ("groups", "queries", "kept", "pruned", "unknown")      # not "flushes": how the device batches them
+    assert {k: ginfo["fork_filter"][k] for k in ff} == {k: cinfo["fork_filter"][k] for k in ff}, (
+        ginfo["fork_filter"], cinfo["fork_filter"])
+    assert ginfo["confirmations"] == cinfo["confirmations"], (ginfo["confirmations"], cinfo["confirmations"])
+    keys = ("calls", "refuted", "seed", "search", "unknown")
+    assert {k: ginfo["search"][k] for k in keys} == {k: cinfo["search"][k] for k in keys}, (
+        ginfo["search"], cinfo["search"])

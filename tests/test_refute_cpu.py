@@ -90,6 +90,18 @@ def test_unit_equalities():
     assert not refutes(query(Not(cv == bv(0)), E.UGT(cv, bv(0)), axioms=False))
 
 
+def test_ite_wrappers_only_pin_the_branch_they_force():
+    """distinct(ite(P, 1, 0), 2) holds whatever P is, so it must not
+    pin P's variable: next to cv == 5 the query is sat (cv = 5)."""
+    cv = word("call_value3")
+    wrapped = E.If(cv == bv(7), bv(1), bv(0))
+    assert not refutes(query(wrapped != bv(2), cv == bv(5), axioms=False))
+    assert not refutes(query(wrapped == bv(0), cv == bv(5), axioms=False))
+    # the forcing forms still pin it
+    assert refutes(query(wrapped != bv(0), cv == bv(5), axioms=False))
+    assert refutes(query(wrapped == bv(1), cv == bv(5), axioms=False))
+
+
 def test_array_reads_are_not_folded():
     cd = Array("calldata", 256, 8)
     q = query(cd[bv(0)] == bv(1, 8), word("x") == bv(3), axioms=False)

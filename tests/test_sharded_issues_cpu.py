@@ -73,9 +73,10 @@ def _run(name, module, tx_count, sigdir):
         ws.put_account(Account(ACTORS[actor], contract_name=None))
     created = execute_symbolic_contract_creation(vm, code, "MAIN", world_state=ws)
     execute_symbolic_transactions(vm, created.address)
-    before = len({i.key() for m in mods for i in m.issues})
+    unmerged = sorted({i.key() for m in mods for i in m.issues})
+    before = len(unmerged)
     merged = merge_issues(mods, refmodules.Issue)
-    return sorted(i.key() for m in mods for i in m.issues), merged, before
+    return sorted(i.key() for m in mods for i in m.issues), merged, before, unmerged
 
 
 def _worker(rank, world, port, out, case, sigdir):
@@ -91,26 +92,72 @@ def _worker(rank, world, port, out, case, sigdir):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
 def test_sharded_issue_sets_equal_single_process(case, tmp_path):
-    single, n, _ = _run(*case, str(tmp_path / "sig"))
-    assert n == len(single) and single
+    single, n, _, unmerged = _run(*case, str(tmp_path / "sig"))
+    # the one-process baseline is the run's own issue set, not a merge of it
+    assert single == unmerged and n == len(single) and single
     for world in (2, 3):
         port = _free_port()
         with mp.Manager() as m:
             out = m.dict()
             mp.spawn(_worker, args=(world, port, out, case, str(tmp_path / "sig")), nprocs=world, join=True)
             res = [out[r] for r in range(world)]
-        for issues, merged, _ in res:
+        for issues, merged, _, _ in res:
             assert issues == single and merged == len(single), (world, issues, single)
         if case[0] == "extcall.sol.o":
             # the constructor's issue: every rank filed it, the merge keeps one
-            assert all(before == len(single) for _, _, before in res)
+            assert all(before == len(single) for _, _, before, _ in res)
         else:
             # the message calls' issues: some rank filed fewer than the merged set
-            assert min(before for _, _, before in res) < len(single)
+            assert min(before for _, _, before, _ in res) < len(single)
 
 
 def test_value_stream_round_trips():
     from mythril_amd.laser.sharded import _Words, _get_value, _values_to_words
     v = (None, True, False, 0, -5, (1 << 300) + 7, "MAIN", b"\x00\x01", [1, (2, "x")],
-         {"steps": [{"input": "0xab", "value": "0x0"}], 3: None})
+         {"steps": [{"input": "0xab", "value": "0x0"}], 3: None}, 0.125, -1e300, 12.3456789)
     assert _get_value(_Words(_values_to_words(v))) == v
+
+
+class _RefIssue:
+    """The reference's Issue shape (report.py:26-72): bytecode_hash, no
+    bytecode, a float discovery_time."""
+
+    def __init__(self, address, code_hash, title, t):
+        self.address, self.bytecode_hash, self.title = address, code_hash, title
+        self.swc_id, self.function, self.contract = "106", "kill()", "MAIN"
+        self.discovery_time = t
+        self.transaction_sequence = {"steps": [{"input": "0x41c0e1b5", "value": "0x0"}]}
+        self.source_location = None
+
+
+class _RefModule:
+    """base.py:55-70: caches (address, bytecode_hash)."""
+    auto_cache = True
+
+    def __init__(self, issues):
+        self.issues, self.cache = list(issues), set()
+
+    def update_cache(self, issues=None):
+        for issue in issues or self.issues:
+            self.cache.add((issue.address, issue.bytecode_hash))
+
+
+def test_merge_keys_reference_issues_on_the_code_hash():
+    """two contracts at the same address are two issues; the cache
+    gets the module's own (address, bytecode_hash) keys; floats survive."""
+    from mythril_amd.laser.sharded import merge_issues
+    m = _RefModule([_RefIssue(146, "0xaa", "Unprotected Selfdestruct", 0.25),
+                    _RefIssue(146, "0xbb", "Unprotected Selfdestruct", 0.5),
+                    _RefIssue(146, "0xaa", "Unprotected Selfdestruct", 0.75)])
+    assert merge_issues([m], _RefIssue) == 2
+    assert m.cache == {(146, "0xaa"), (146, "0xbb")}
+    assert [i.discovery_time for i in m.issues] == [0.25, 0.5]
+    assert m.issues[0].transaction_sequence["steps"][0]["input"] == "0x41c0e1b5"
+
+
+def test_merge_refuses_an_attribute_it_cannot_send():
+    from mythril_amd.laser.sharded import merge_issues
+    i = _RefIssue(1, "0xaa", "t", 0.0)
+    i.detector = object()
+    with pytest.raises(TypeError, match="detector"):
+        merge_issues([_RefModule([i])], _RefIssue)
