@@ -914,11 +914,14 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     creator = ACTORS["CREATOR"]
     out = {"metric": "in-situ constraint-evals/s of the fork and reachability filters (kernel 2) "
                      "+ symbolic lane-steps/s (kernel 1)",
-           "mode": "prefilter-only: no SMT backend in the image; queries no candidate satisfies "
-                   "are UNKNOWN and their paths kept; escapes stepped by the handler given "
-                   "(bench: tests/symref.py), else dropped (counted)",
+           "mode": "kernel-2 prefilter (LRU + witness seeds), then the exact procedure "
+                   "(mythril_amd/smt/exact.py: bit-blasting + CDCL) on what it leaves open: forks "
+                   "pruned on unsat and on a budget timeout as is_possible does; escapes stepped by "
+                   "the handler given (bench: tests/symref.py), else dropped (counted)",
            "transactions": tx_count, "replicas_per_gpu": replicas, "seed_models": n_seeds, "contracts": {}}
-    saved_cache = solver.model_cache
+    from mythril_amd.smt.exact import ExactSolver
+    from mythril_amd.smt.search import SatSearchBackend
+    saved_cache, saved_backend = solver.model_cache, solver.solver_backend
     try:
         for name in SYMBOLIC_TX_CODES:
             gc.collect()                     # the earlier fields' garbage is not this field's work
@@ -944,9 +947,10 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
             seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"], balance_names=["balance"])
             mc.seed_source = seeds
             solver.model_cache = mc
+            backend = SatSearchBackend(mc, search=False, exact=ExactSolver(max_ms=10000))
+            solver.set_solver_backend(backend)
             laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                              transaction_count=tx_count, escape_handler=escape_handler)
-            laser.unknown_forks = "keep"
             if log:
                 log(f"symbolic_tx {name}")
                 laser.register_laser_hooks("start_sym_trans", lambda: log(
@@ -978,11 +982,14 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
                 "constraint_evals_per_s_kernel": mc.device_evals / k2_s if k2_s else None,
                 "constraint_evals_per_s_wall": mc.device_evals / wall,
                 "keccak_symbolic_inputs": sum(len(v) for v in keccak_function_manager.symbolic_inputs.values()),
+                "exact": {k: backend.stats[k] for k in ("exact_sat", "exact_unsat", "exact_timeout")},
+                "exact_ms": backend.exact.stats["ms"],
                 "ranks": world, "job_lane_steps_per_s": job_steps / job_wall,
                 "job_constraint_evals_per_s_wall": job_evals / job_wall,
             }
     finally:
         solver.model_cache = saved_cache
+        solver.set_solver_backend(saved_backend)
         keccak_function_manager.reset()
         tx_id_manager.restart_counter()
         solver.get_model.cache_clear()
@@ -1009,8 +1016,10 @@ def _myth_analyze_rows(device, k2, tx_count: int, names, log=None):
                       "launches_kernel2": int(info["kernel2_launches"]), "forks": info["forks"],
                       "fork_filter": {k: info["fork_filter"].get(k) for k in ("groups", "queries", "kept", "pruned",
                                                                                "unknown")},
-                      "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown")
+                      "search": {k: info["search"][k] for k in ("calls", "refuted", "seed", "search", "unknown",
+                                                                "exact_sat", "exact_unsat", "exact_timeout")
                                  if k in info["search"]},
+                      "exact_ms": (info.get("exact") or {}).get("ms", 0),
                       "constraint_evals_per_s_wall": info["device_evals"] / info["wall_s"] if info["wall_s"] else None}
     return rows
 
@@ -1072,11 +1081,19 @@ def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True)
                                                          "constraint_evals", "escapes_dropped")}
     tot["issues"] = sum(len(r["issues"]) for r in rows.values())
     tot["unknown_confirmations"] = sum(r["confirmations"]["unknown"] for r in rows.values())
+    tot["unsat_confirmations"] = sum(r["confirmations"].get("unsat", 0) for r in rows.values())
+    tot["timeout_confirmations"] = sum(r["confirmations"].get("timeout", 0) for r in rows.values())
+    for k in ("exact_sat", "exact_unsat", "exact_timeout"):
+        tot[k] = sum(r["search"].get(k, 0) for r in rows.values())
+    tot["exact_s"] = sum(r.get("exact_ms", 0) for r in rows.values()) / 1e3
+    tot["forks_pruned"] = sum(r["fork_filter"].get("pruned", 0) for r in rows.values())
+    tot["forks_unknown"] = sum(r["fork_filter"].get("unknown", 0) for r in rows.values())
     job_wall, job_evals = mdist.reduce_timing(tot["wall_s"], float(tot["constraint_evals"]))
     out = {"metric": "myth analyze -f <code> -t %d, all detection modules, over the 18 reference "
                      "contracts: contracts/s and in-situ constraint-evals/s" % tx_count,
-           "mode": "modules on; SAT-only confirmations on kernel 2 (unknowns counted); escapes stepped "
-                   "by the tests/symref.py handler",
+           "mode": "modules on; queries on kernel 2 (quick-sat, witness seeds, guided search), the rest "
+                   "decided by the exact procedure (mythril_amd/smt/exact.py): unsat and budget timeouts "
+                   "prune / refute as the reference's z3 does; escapes stepped by the tests/symref.py handler",
            "transactions": tx_count, "contracts_analysed": len(rows), "ranks": world, "totals": tot,
            "job_wall_s": job_wall, "contracts_per_s": len(names) / job_wall if job_wall else None,
            "job_constraint_evals_per_s_wall": job_evals / job_wall if job_wall else None,

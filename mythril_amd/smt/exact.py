@@ -1,0 +1,281 @@
+"""The exact decision procedure behind kernel 2 (include/mythsmt.h, libmythsmt.so).
+
+Kernel 2 (quick-sat over the model cache) and the SAT-only search
+(search.py) answer a query with a model or not at all.  The reference
+answers what they leave open with z3 (support/model.py:37-82): a model, or
+``UnsatError``, or ``SolverTimeOutException`` when the solver gives up --
+and ``Constraints.is_possible`` prunes on both of the latter
+(state/constraints.py:33-43).  ``ExactSolver`` is that last step here: the
+query's conjuncts go to ``ms_solve`` (bit-blasting + CDCL, host C++) as a
+post-order node table; the model it returns -- variable values, each array's
+point reads, each uninterpreted function's applications -- becomes a
+``ModelRef`` assignment the callers (and kernel 2, which re-checks it) read
+exactly as they read any other model.  ``minimize`` terms are met
+lexicographically, as z3's Optimize does with several objectives
+(analysis/solver.py:219-259).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .expr import Node
+
+PKG_DIR = Path(__file__).resolve().parents[1]
+SRC = PKG_DIR / "csrc" / "bvsat.cpp"
+HEADER = PKG_DIR.parent / "include" / "mythsmt.h"
+LIB_PATH = PKG_DIR / "libmythsmt.so"
+HASH_PATH = LIB_PATH.with_name(LIB_PATH.name + ".sha256")
+CXX = os.environ.get("CXX", "g++")
+
+# include/mythsmt.h opcodes, by expr.py op name
+OPS = {name: i for i, name in enumerate((
+    "const", "var", "bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod",
+    "bvand", "bvor", "bvxor", "bvnot", "bvneg", "bvshl", "bvlshr", "bvashr",
+    "eq", "distinct", "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge",
+    "and", "or", "not", "xor", "implies", "ite", "concat", "extract", "zero_extend", "sign_extend",
+    "bvadd_noovfl_u", "bvumul_noovfl", "bvsub_noudfl_u", "select", "uf", "array", "K", "store"))}
+MS_SAT, MS_UNSAT, MS_UNKNOWN, MS_EINVAL, MS_ESPACE = 1, 0, 2, -1, -2
+
+
+class MsQuery(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_uint32), ("nodes", ctypes.c_void_p), ("args", ctypes.c_void_p),
+                ("limbs", ctypes.c_void_p), ("n_roots", ctypes.c_uint32), ("roots", ctypes.c_void_p),
+                ("n_minimize", ctypes.c_uint32), ("minimize", ctypes.c_void_p),
+                ("n_vars", ctypes.c_uint32), ("n_arrays", ctypes.c_uint32), ("n_funcs", ctypes.c_uint32)]
+
+
+class MsLimits(ctypes.Structure):
+    _fields_ = [("max_conflicts", ctypes.c_uint64), ("max_ms", ctypes.c_uint32), ("minimize_ms", ctypes.c_uint32)]
+
+
+class MsStats(ctypes.Structure):
+    _fields_ = [("vars", ctypes.c_uint64), ("clauses", ctypes.c_uint64), ("conflicts", ctypes.c_uint64),
+                ("decisions", ctypes.c_uint64), ("propagations", ctypes.c_uint64), ("solves", ctypes.c_uint32),
+                ("ms", ctypes.c_uint32)]
+
+
+SIGNATURES = {
+    "ms_abi_version": (ctypes.c_int, []),
+    "ms_solve": (ctypes.c_int, [ctypes.POINTER(MsQuery), ctypes.POINTER(MsLimits), ctypes.c_void_p,
+                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(MsStats)]),
+}
+
+
+def _command(out: str) -> List[str]:
+    return [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", str(SRC), "-o", out]
+
+
+def source_hash() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for p in (SRC, HEADER):
+        h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
+    h.update(" ".join(a for a in _command("OUT")[1:] if not a.startswith("/")).encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile libmythsmt.so in-tree (host C++, g++ -O2); rebuilt when the
+    recorded source hash differs."""
+    want = source_hash()
+    if not force and LIB_PATH.exists() and HASH_PATH.exists() and HASH_PATH.read_text().strip() == want:
+        return LIB_PATH
+    cmd = _command(str(LIB_PATH) + ".tmp")
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(str(LIB_PATH) + ".tmp", LIB_PATH)
+    HASH_PATH.write_text(want + "\n")
+    return LIB_PATH
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> ctypes.CDLL:
+    """The in-tree libmythsmt.so; raises when it is missing or stale (no
+    fallback: a query the procedure cannot take is an error, not a guess)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                               "g.build()'`")
+        got = HASH_PATH.read_text().strip() if HASH_PATH.exists() else "missing"
+        if got != source_hash():
+            raise RuntimeError(f"{LIB_PATH} was not built from the current sources: rebuild it")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, argtypes) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, argtypes
+        _lib = lib
+        return lib
+
+
+class Unsupported(ValueError):
+    """A node the procedure has no encoding for."""
+
+
+def _limbs(v: int, w: int) -> List[int]:
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range((w + 31) // 32)]
+
+
+class _Table:
+    """The post-order node table of a set of roots (shared subterms once)."""
+
+    def __init__(self):
+        self.index: Dict[int, int] = {}
+        self.keep: List[Node] = []
+        self.nodes: List[int] = []
+        self.args: List[int] = []
+        self.limbs: List[int] = [0]
+        self.vars: Dict[str, Tuple[int, int]] = {}          # name -> (id, width)
+        self.arrays: Dict[str, Tuple[int, int, int]] = {}   # name -> (id, domain, range)
+        self.funcs: Dict[str, Tuple[int, tuple, int]] = {}  # name -> (id, domain widths, range)
+
+    def add(self, root: Node) -> int:
+        stack = [(root, False)]
+        while stack:
+            n, ready = stack.pop()
+            if id(n) in self.index:
+                continue
+            if not ready:
+                stack.append((n, True))
+                for a in reversed(n.args):
+                    if id(a) not in self.index:
+                        stack.append((a, False))
+                continue
+            self._emit(n)
+        return self.index[id(root)]
+
+    def _emit(self, n: Node) -> None:
+        op = OPS.get(n.op)
+        if op is None:
+            raise Unsupported(f"no exact encoding for {n.op}")
+        p0 = p1 = 0
+        width = n.width
+        if n.op == "const":
+            p0 = len(self.limbs)
+            self.limbs.extend(_limbs(n.param, n.width))
+        elif n.op == "var":
+            got = self.vars.setdefault(n.param, (len(self.vars), n.width))
+            if got[1] != n.width:
+                raise Unsupported(f"variable {n.param} at two widths")
+            p0 = got[0]
+        elif n.op == "array":
+            name, dom, rng = n.param
+            p0 = self.arrays.setdefault(name, (len(self.arrays), dom, rng))[0]
+            p1 = rng
+        elif n.op in ("K", "store"):
+            p1 = n.param[-1]
+        elif n.op == "uf":
+            name, dom, rng = n.param
+            p0 = self.funcs.setdefault(name, (len(self.funcs), tuple(dom), rng))[0]
+        elif n.op == "extract":
+            p0, p1 = n.param
+        elif n.op in ("zero_extend", "sign_extend"):
+            p0 = n.param
+        first = len(self.args)
+        self.args.extend(self.index[id(a)] for a in n.args)
+        self.index[id(n)] = len(self.keep)
+        self.keep.append(n)
+        self.nodes.extend((op, width, len(n.args), first, p0, p1))
+
+
+class ExactSolver:
+    """``check(conjuncts, minimize)`` -> ("sat", assignment) | ("unsat", None)
+    | ("unknown", None), the assignment in the ModelRef form (name -> int,
+    ArrayInterp, FuncInterp).  Budgets: conflicts and wall time per query."""
+
+    def __init__(self, max_ms: int = 10000, max_conflicts: int = 0, minimize_ms: int = 2000):
+        self.max_ms = max_ms
+        self.max_conflicts = max_conflicts
+        self.minimize_ms = minimize_ms
+        self.stats: Dict[str, int] = {"calls": 0, "sat": 0, "unsat": 0, "unknown": 0, "ms": 0,
+                                      "vars": 0, "clauses": 0, "conflicts": 0}
+
+    def check(self, conjuncts: Sequence[Node], minimize: Sequence[Node] = (), max_ms: Optional[int] = None):
+        import numpy as np
+        from .program import ArrayInterp, FuncInterp
+        lib = load()
+        t = _Table()
+        roots = [t.add(c) for c in conjuncts]
+        mins = [t.add(m) for m in minimize]
+        self.stats["calls"] += 1
+        nodes = np.asarray(t.nodes, dtype=np.uint32)
+        args = np.asarray(t.args or [0], dtype=np.uint32)
+        limbs = np.asarray(t.limbs, dtype=np.uint32)
+        roots_a = np.asarray(roots or [0], dtype=np.uint32)
+        mins_a = np.asarray(mins or [0], dtype=np.uint32)
+        q = MsQuery(len(t.keep), nodes.ctypes.data, args.ctypes.data, limbs.ctypes.data, len(roots),
+                    roots_a.ctypes.data, len(mins), mins_a.ctypes.data, len(t.vars), len(t.arrays), len(t.funcs))
+        lim = MsLimits(self.max_conflicts, self.max_ms if max_ms is None else max_ms, self.minimize_ms)
+        st = MsStats()
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, dtype=np.uint32)
+            n = ctypes.c_uint32(0)
+            rc = lib.ms_solve(ctypes.byref(q), ctypes.byref(lim), out.ctypes.data, cap, ctypes.byref(n),
+                              ctypes.byref(st))
+            if rc != MS_ESPACE:
+                break
+            cap = int(n.value) + 16
+        for k in ("vars", "clauses", "conflicts", "ms"):
+            self.stats[k] += int(getattr(st, k))
+        if rc == MS_EINVAL:
+            raise Unsupported("ms_solve rejected the query")
+        if rc == MS_UNSAT:
+            self.stats["unsat"] += 1
+            return "unsat", None
+        if rc == MS_UNKNOWN:
+            self.stats["unknown"] += 1
+            return "unknown", None
+        self.stats["sat"] += 1
+        words = out[: int(n.value)].tolist()
+        pos = 0
+
+        def take(w):
+            nonlocal pos
+            k = (w + 31) // 32
+            v = 0
+            for i in range(k):
+                v |= int(words[pos + i]) << (32 * i)
+            pos += k
+            return v
+
+        assign: Dict[str, object] = {}
+        for name, (vid, w) in sorted(t.vars.items(), key=lambda kv: kv[1][0]):
+            assign[name] = take(w)
+        arr_by_id = {v[0]: (k, v[1], v[2]) for k, v in t.arrays.items()}
+        fn_by_id = {v[0]: (k, v[1], v[2]) for k, v in t.funcs.items()}
+        while True:
+            tag = words[pos]
+            pos += 1
+            if tag == 0:
+                break
+            ident = words[pos]
+            pos += 1
+            if tag == 1:
+                name, dom, rng = arr_by_id[ident]
+                idx = take(dom)
+                val = take(rng)
+                interp = assign.setdefault(name, ArrayInterp(0, {}))
+                interp.entries[idx] = val
+            else:
+                name, dom, rng = fn_by_id[ident]
+                xs = tuple(take(w) for w in dom)
+                val = take(rng)
+                interp = assign.setdefault(name, FuncInterp(0, {}))
+                interp.entries[xs] = val
+        for name in t.arrays:
+            assign.setdefault(name, ArrayInterp(0, {}))
+        for name in t.funcs:
+            assign.setdefault(name, FuncInterp(0, {}))
+        return "sat", assign

@@ -37,7 +37,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .expr import Node
+from .expr import TRUE, Node
 from .program import ArrayInterp, FuncInterp, PoolColumns
 from .semantics import apply_op
 from .refute import refutes
@@ -551,14 +551,21 @@ def _model(assign: Dict[str, object]) -> Model:
 class SatSearchBackend:
     """``solver.set_solver_backend(SatSearchBackend(model_cache))``: answers
     get_model's misses with a model found on kernel 2, or raises
-    SolverBackendMissing (unknown)."""
+    SolverBackendMissing (unknown).  With ``exact`` (an exact.ExactSolver) the
+    queries the refutations, the seeds and the search leave open go to the
+    exact decision procedure: a model (re-checked on kernel 2), UnsatError, or
+    SolverTimeOutException when its budget runs out -- z3's three answers in
+    support/model.py:37-82, so nothing stays "unknown"."""
 
     uses_seeds = True          # get_model consults the seeds before calling it
 
     def __init__(self, cache, search: bool = True, rounds: int = 12, beam: int = 6,
-                 max_candidates: int = 4096, patience: int = 3, seed: int = 0x5EA5C4):
+                 max_candidates: int = 4096, patience: int = 3, seed: int = 0x5EA5C4,
+                 exact=None, exact_ms: int = 10000):
         self.cache = cache
         self.search = search
+        self.exact = exact
+        self.exact_ms = exact_ms
         self.rounds = rounds
         self.beam = beam
         self.max_candidates = max_candidates
@@ -567,7 +574,8 @@ class SatSearchBackend:
         self._memo_completed: Dict[int, tuple] = {}
         self._start_cols: Optional[tuple] = None      # (the starting pool's assignments, their PoolColumns)
         self.stats: Dict[str, int] = {"calls": 0, "refuted": 0, "seed": 0, "search": 0, "unknown": 0,
-                                      "candidates": 0, "launches": 0, "minimised": 0}
+                                      "candidates": 0, "launches": 0, "minimised": 0,
+                                      "exact_sat": 0, "exact_unsat": 0, "exact_timeout": 0}
 
     def __call__(self, constraints, minimize, maximize, timeout):
         self.stats["calls"] += 1
@@ -582,12 +590,42 @@ class SatSearchBackend:
             model = self._search(key)
             if model is not None:
                 self.stats["search"] += 1
+        if model is None and self.exact is not None:
+            return self._decide(key, minimize, timeout)
         if model is None:
             self.stats["unknown"] += 1
             raise SolverBackendMissing("SAT-only backend: no candidate model satisfies the query (unknown)")
         if minimize:
             model = self._minimise(key, model, minimize)
         return model
+
+    def _decide(self, key: Node, minimize, timeout) -> Model:
+        """The exact procedure on a query the cheaper answers left open."""
+        from .solver import SolverTimeOutException
+        conj = [c for c in _conjuncts(key) if c is not TRUE]
+        budget = int(min(timeout or self.exact_ms, self.exact_ms))
+        mins = [m.raw if hasattr(m, "raw") else m for m in minimize]
+        st, assign = self.exact.check(conj, mins, max_ms=max(budget, 1))
+        if st == "unsat":
+            self.stats["exact_unsat"] += 1
+            raise UnsatError
+        if st == "unknown":
+            self.stats["exact_timeout"] += 1
+            raise SolverTimeOutException
+        self.stats["exact_sat"] += 1
+        # every model is checked by kernel 2 before anyone sees it (a conjunct
+        # kernel 2 has no row for: by the host evaluator)
+        live = [c for c in conj if c.op != "const"]
+        if live:
+            counts, hit = self._score(live, [assign])
+            if hit is False:
+                ref = ModelRef(assign)
+                ok = all(ref.eval(c, model_completion=True).param == 1 for c in live)
+            else:
+                ok = hit == 0
+            if not ok:
+                raise RuntimeError("the exact procedure's model does not satisfy the query on kernel 2")
+        return _model(assign)
 
     def _completed(self, assign: Dict[str, object]) -> "_Completed":
         """complete(assign), memoised per assignment object while neither it

@@ -48,8 +48,9 @@ class UnsatError(Exception):
     """mythril/exceptions.py: the constraints are unsatisfiable."""
 
 
-class SolverTimeOutException(Exception):
-    """mythril/exceptions.py: the solver gave up."""
+class SolverTimeOutException(UnsatError):
+    """mythril/exceptions.py:23: the solver gave up -- an UnsatError, as there:
+    a module that catches UnsatError treats a timeout as "no issue"."""
 
 
 class SolverBackendMissing(RuntimeError):

@@ -43,14 +43,18 @@ from mythril_amd.smt.keccak_manager import keccak_function_manager
 
 def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, search=True,
             strategy: str = "bfs", runtime: bool = False, code: Optional[bytes] = None,
-            mutation_pruner: bool = True):
+            mutation_pruner: bool = True, exact: bool = True, exact_ms: int = 10000):
     """Run one analysis; returns (report issues, info).  `modules`: a module
-    name, a list of names, or None (all fourteen)."""
+    name, a list of names, or None (all fourteen).  `exact`: the queries the
+    SAT search leaves open go to the exact procedure (mythril_amd.smt.exact),
+    so fork filters and confirmations prune on unsat and on a budget timeout
+    exactly as the reference's is_possible / get_model do; without it they
+    stay "unknown" and the paths are kept (the prefilter-only mode)."""
     from mythril_amd.smt.search import SatSearchBackend
     keccak_function_manager.reset()
     exponent_function_manager.reset()
     tx_id_manager.restart_counter()
-    refmodules.CONFIRMATIONS.update(sat=0, unknown=0)
+    refmodules.CONFIRMATIONS.update(sat=0, unknown=0, timeout=0, unsat=0)
     code = workloads.bytecode(name) if code is None else code
     white = [modules] if isinstance(modules, str) else modules
     mods = refmodules.detection_modules(white)
@@ -58,7 +62,11 @@ def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, s
     mc = solver.ModelCache(device=k2)
     mc.seed_source = WitnessSeeds([code], n=n_seeds, balance_names=["balance"])
     solver.model_cache = mc
-    backend = SatSearchBackend(mc, search=search)
+    if exact:
+        from mythril_amd.smt.exact import ExactSolver
+        backend = SatSearchBackend(mc, search=search, exact=ExactSolver(max_ms=exact_ms), exact_ms=exact_ms)
+    else:
+        backend = SatSearchBackend(mc, search=search)
     solver.set_solver_backend(backend)
     svm_mod.check_potential_issues = refmodules.check_potential_issues
     strat = {"bfs": BreadthFirstSearchStrategy, "delayed": DelayConstraintStrategy}[strategy]
@@ -68,8 +76,10 @@ def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, s
                          requires_statespace=False, escape_handler=symref.Engine(signals=True).step)
         if strategy == "delayed":
             laser.strategy.model_cache._device = k2
-            laser.strategy.unknown = "keep"          # as the fork filters' unknown answers
-        laser.unknown_forks = "keep"
+            if not exact:
+                laser.strategy.unknown = "keep"      # as the fork filters' unknown answers
+        if not exact:
+            laser.unknown_forks = "keep"
         laser.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
         if mutation_pruner:
             refmodules.MutationPruner().initialize(laser)
@@ -94,6 +104,7 @@ def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, s
                 "forks": laser.forks, "fork_filter": dict(laser.fork_stats),
                 "escapes_dropped": laser.escapes_dropped, "confirmations": dict(refmodules.CONFIRMATIONS),
                 "cache": dict(mc.stats), "search": dict(backend.stats),
+                "exact": dict(backend.exact.stats) if backend.exact is not None else None,
                 "kernel2_launches": mc.launches, "device_evals": mc.device_evals,
                 "device_ms": laser.device_ms, "k2_ms": mc.device_ms, "modules": [type(m).__name__ for m in mods]}
         return issues, info

@@ -235,7 +235,7 @@ class ConfirmationUnknown(UnsatError):
     issue); CONFIRMATIONS counts it apart."""
 
 
-CONFIRMATIONS = {"sat": 0, "unknown": 0}
+CONFIRMATIONS = {"sat": 0, "unknown": 0, "timeout": 0, "unsat": 0}
 
 
 def _constant_verdict(constraints) -> Optional[bool]:
@@ -253,14 +253,19 @@ def _sat_or_unknown(call):
     """Run a get_model-style call under the SAT-only backend: a model, or
     ConfirmationUnknown (SolverBackendMissing: no candidate satisfied and no
     solver can say more)."""
-    from mythril_amd.smt.solver import SolverBackendMissing
+    from mythril_amd.smt.solver import SolverBackendMissing, SolverTimeOutException
     from mythril_amd.smt.solver import UnsatError as SmtUnsat
     try:
         model = call()
     except SolverBackendMissing:
         CONFIRMATIONS["unknown"] += 1
         raise ConfirmationUnknown()
+    except SolverTimeOutException:
+        # the reference's timeout is an UnsatError (exceptions.py:23): no issue
+        CONFIRMATIONS["timeout"] += 1
+        raise UnsatError()
     except SmtUnsat:
+        CONFIRMATIONS["unsat"] += 1
         raise UnsatError()
     CONFIRMATIONS["sat"] += 1
     return model
