@@ -947,7 +947,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
             seeds = WitnessSeeds([code], n=n_seeds, storage_names=[f"Storage{addr}"], balance_names=["balance"])
             mc.seed_source = seeds
             solver.model_cache = mc
-            backend = SatSearchBackend(mc, search=False, exact=ExactSolver(max_ms=10000))
+            backend = SatSearchBackend(mc, search=False, exact=ExactSolver(), exact_ms=60000)
             solver.set_solver_backend(backend)
             laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                              transaction_count=tx_count, escape_handler=escape_handler)

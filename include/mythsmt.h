@@ -79,14 +79,28 @@ typedef struct {
 int ms_abi_version(void);
 
 /* Decide q.  On MS_SAT the model is written to `model` (u32 words, capacity
- * `model_cap`, length in *model_len):
- *   every variable's value, in id order (ceil(w/32) limbs each, its width taken
- *   from the query), then records
- *     {1, array id, index limbs..., value limbs...}   one per array point read
+ * `model_cap`, length in *model_len) as records
+ *     {3, variable id, value limbs...}                  one per variable
+ *     {1, array id, index limbs..., value limbs...}     one per array point read
  *     {2, function id, argument limbs..., value limbs...}   one per application
- *   then {0}.  Widths of records follow the first node of that array / function. */
+ *   then {0}.  Widths follow the variable / the first node of that array or
+ *   function (the caller's table knows them). */
 int ms_solve(const ms_query *q, const ms_limits *lim, uint32_t *model, uint32_t model_cap,
              uint32_t *model_len, ms_stats *stats);
+
+/* Sessions: one node table and one clause database across the queries of an
+ * analysis.  Each ms_session_solve appends q's nodes (q.n_nodes new ones; their
+ * argument indices and roots / minimize index the whole table, node ids
+ * continuing from the previous call; n_vars / n_arrays / n_funcs are session
+ * totals), blasts only what is new, and decides the roots as assumptions -- the
+ * clause database holds definitions and congruence lemmas only, true of every
+ * query, so learnt clauses carry over.  The model stream lists every variable
+ * and read blasted so far.  A session is used by one thread at a time. */
+typedef struct ms_session ms_session;
+int ms_session_open(ms_session **out);
+void ms_session_close(ms_session *s);
+int ms_session_solve(ms_session *s, const ms_query *q, const ms_limits *lim, uint32_t *model,
+                     uint32_t model_cap, uint32_t *model_len, ms_stats *stats);
 
 #ifdef __cplusplus
 }

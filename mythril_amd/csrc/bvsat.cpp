@@ -24,8 +24,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace {
@@ -164,24 +168,29 @@ public:
         trail.push_back(p);
     }
 
-    // Level-0 clause: simplified against the current level-0 assignment.
-    bool add_clause(std::vector<Lit> ls) {
+    // Level-0 clause: simplified against the current level-0 assignment (scratch
+    // buffers: clause construction allocates nothing once they have grown).
+    std::vector<Lit> cl_in, cl_out;
+    bool add_clause(std::initializer_list<Lit> ls) { return add_clause(ls.begin(), ls.size()); }
+    bool add_clause(const std::vector<Lit> &ls) { return add_clause(ls.data(), ls.size()); }
+    bool add_clause(const Lit *ls, size_t n) {
         if (!ok) return false;
-        std::sort(ls.begin(), ls.end());
-        std::vector<Lit> out;
+        cl_in.assign(ls, ls + n);
+        std::sort(cl_in.begin(), cl_in.end());
+        cl_out.clear();
         Lit prev = -1;
-        for (Lit l : ls) {
+        for (Lit l : cl_in) {
             if (value(l) == LT || l == neg(prev)) return true;
-            if (value(l) != LF && l != prev) out.push_back(l);
+            if (value(l) != LF && l != prev) cl_out.push_back(l);
             prev = l;
         }
         ++n_clauses;
-        if (out.empty()) return ok = false;
-        if (out.size() == 1) {
-            enqueue(out[0], CR_NONE);
+        if (cl_out.empty()) return ok = false;
+        if (cl_out.size() == 1) {
+            enqueue(cl_out[0], CR_NONE);
             return ok = (propagate() == CR_NONE);
         }
-        attach(alloc(out, false));
+        attach(alloc(cl_out, false));
         return true;
     }
 
@@ -235,7 +244,7 @@ public:
             phase[v] = (int8_t)sgn(trail[c]);
             assigns[v] = LU;
             reason[v] = CR_NONE;
-            heap_insert(v);
+            if (rel.empty() || rel[v]) heap_insert(v);
         }
         trail.resize(trail_lim[lvl]);
         trail_lim.resize(lvl);
@@ -340,6 +349,26 @@ public:
     }
 
     // LT sat, LF unsat (under the assumptions), LU budget exhausted
+    // Decisions over `relevant` only (a session's query: the inputs of its
+    // cone -- every gate it depends on follows from them by propagation); the
+    // variables of other queries' terms stay unassigned, and a SAT answer is
+    // the cone's.  Empty: every variable.
+    std::vector<char> rel;
+    void set_relevant(const std::vector<int> *relevant) {
+        for (int v : heap) heap_pos[v] = -1;
+        heap.clear();
+        if (!relevant) {
+            rel.clear();
+            for (int v = 0; v < n_vars(); ++v)
+                if (assigns[v] == LU) heap_insert(v);
+            return;
+        }
+        rel.assign(n_vars(), 0);
+        for (int v : *relevant) rel[v] = 1;
+        for (int v : *relevant)
+            if (assigns[v] == LU) heap_insert(v);
+    }
+
     int8_t solve(const std::vector<Lit> &assumptions, uint64_t max_conflicts,
                  std::chrono::steady_clock::time_point deadline, bool timed) {
         model.clear();
@@ -447,7 +476,16 @@ public:
     }
     Lit fresh() { return mk(S.new_var()); }
     bool is_const(Lit l) const { return l == T || l == F; }
+    // a literal the level-0 assignment already decides is that constant: every
+    // gate is built at level 0 (no search runs while blasting), so the facts the
+    // asserted conjuncts propagate fold the gates built after them
+    Lit nrm(Lit l) const {
+        int8_t v = S.value(l);
+        return v == LT ? T : v == LF ? F : l;
+    }
     Lit and2(Lit a, Lit b) {
+        a = nrm(a);
+        b = nrm(b);
         if (a == F || b == F || a == neg(b)) return F;
         if (a == T) return b;
         if (b == T || a == b) return a;
@@ -464,6 +502,8 @@ public:
     }
     Lit or2(Lit a, Lit b) { return neg(and2(neg(a), neg(b))); }
     Lit xor2(Lit a, Lit b) {
+        a = nrm(a);
+        b = nrm(b);
         if (a == F) return b;
         if (b == F) return a;
         if (a == T) return neg(b);
@@ -490,6 +530,9 @@ public:
         return flip ? neg(o) : o;
     }
     Lit mux(Lit s, Lit a, Lit b) {      // s ? a : b
+        s = nrm(s);
+        a = nrm(a);
+        b = nrm(b);
         if (s == T || a == b) return a;
         if (s == F) return b;
         if (a == T && b == F) return s;
@@ -517,6 +560,9 @@ public:
         return o;
     }
     Lit maj(Lit a, Lit b, Lit c) {
+        a = nrm(a);
+        b = nrm(b);
+        c = nrm(c);
         if (is_const(a)) return a == T ? or2(b, c) : and2(b, c);
         if (is_const(b)) return b == T ? or2(a, c) : and2(a, c);
         if (is_const(c)) return c == T ? or2(a, b) : and2(a, b);
@@ -543,6 +589,7 @@ public:
     Lit and_n(const std::vector<Lit> &xs) {
         std::vector<Lit> v;
         for (Lit x : xs) {
+            x = nrm(x);
             if (x == F) return F;
             if (x != T) v.push_back(x);
         }
@@ -574,9 +621,13 @@ public:
         for (uint32_t i = 0; i < w; ++i) b[i] = ((limbs[i >> 5] >> (i & 31)) & 1u) ? T : F;
         return b;
     }
+    std::vector<int> inputs;            // variables of words (not gate outputs)
     Bits fresh_word(uint32_t w) {
         Bits b(w);
-        for (auto &x : b) x = fresh();
+        for (auto &x : b) {
+            x = fresh();
+            inputs.push_back(var(x));
+        }
         return b;
     }
     Bits bnot(const Bits &a) {
@@ -624,7 +675,7 @@ public:
     }
     bool all_const(const Bits &a) const {
         for (Lit l : a)
-            if (!is_const(l)) return false;
+            if (!is_const(nrm(l))) return false;
         return true;
     }
     // a * b truncated to `outw` bits (operands zero-extended)
@@ -633,14 +684,14 @@ public:
         // put the constant (or the one with fewer non-false bits) on b
         auto weight = [&](const Bits &x) {
             size_t n = 0;
-            for (Lit l : x) n += (l != F);
+            for (Lit l : x) n += (nrm(l) != F);
             return n;
         };
         if (all_const(*a) && !all_const(*b)) std::swap(a, b);
         else if (!all_const(*b) && weight(*a) < weight(*b)) std::swap(a, b);
         Bits acc(outw, F);
         for (size_t i = 0; i < b->size() && i < outw; ++i) {
-            Lit bi = (*b)[i];
+            Lit bi = nrm((*b)[i]);
             if (bi == F) continue;
             Bits row(outw, F);
             for (size_t j = 0; j + i < outw && j < a->size(); ++j) row[j + i] = and2((*a)[j], bi);
@@ -697,6 +748,15 @@ struct ReadRec {
     int kind;              // 1 array, 2 function
     std::vector<Bits> args;
     Bits val;
+    uint32_t idx_node;     // an array read's index node (UINT32_MAX: none / a function)
+};
+
+const uint32_t NO_BASE = 0xffffffffu;
+
+// A term as base + constant (mod 2^width): base NO_BASE for a constant.
+struct Affine {
+    uint32_t base;
+    std::vector<uint32_t> off;
 };
 
 struct VecHash {
@@ -709,7 +769,9 @@ struct VecHash {
 
 class Blaster {
 public:
-    const ms_query &q;
+    // the node table, owned: a session appends to it query after query
+    std::vector<uint32_t> nodes_, args_, limbs_;
+    uint32_t n_nodes = 0, n_vars = 0;
     Sat S;
     Gates G;
     std::vector<Bits> memo;           // per node (1-bit nodes: size 1)
@@ -722,25 +784,104 @@ public:
     // (node, index bits) -> select result
     std::unordered_map<std::vector<Lit>, Bits, VecHash> select_memo;
     std::unordered_map<uint64_t, std::pair<Bits, Bits>> divmod_memo;
+    std::vector<Affine> aff;
+    std::vector<char> aff_done;
     bool bad = false;
 
-    explicit Blaster(const ms_query &qq) : q(qq), G(S) {
-        memo.resize(q.n_nodes);
-        done.assign(q.n_nodes, 0);
-        var_bits.resize(q.n_vars);
-        var_width.assign(q.n_vars, 0);
+    Blaster() : G(S) { limbs_.push_back(0u); }
+
+    // Append a query's new nodes (their arguments are indices into the whole
+    // table, their first_arg / constant limbs local to the query's arrays).
+    bool append(const ms_query &q) {
+        const uint32_t base = n_nodes;
+        for (uint32_t k = 0; k < q.n_nodes; ++k) {
+            const uint32_t *n = q.nodes + 6 * (size_t)k;
+            if (n[0] >= MS_N_OPS) return false;
+            uint32_t row[6] = {n[0], n[1], n[2], (uint32_t)args_.size(), n[4], n[5]};
+            for (uint32_t i = 0; i < n[2]; ++i) {
+                uint32_t a = q.args[n[3] + i];
+                if (a >= base + k) return false;                     // post order
+                args_.push_back(a);
+            }
+            if (n[0] == MS_CONST) {
+                row[4] = (uint32_t)limbs_.size();
+                limbs_.insert(limbs_.end(), q.limbs + n[4], q.limbs + n[4] + (n[1] + 31) / 32);
+            }
+            if (n[0] == MS_VAR && n[4] >= q.n_vars) return false;
+            nodes_.insert(nodes_.end(), row, row + 6);
+        }
+        n_nodes = base + q.n_nodes;
+        if (q.n_vars > n_vars) {
+            n_vars = q.n_vars;
+            var_bits.resize(n_vars);
+            var_width.resize(n_vars, 0);
+        }
+        memo.resize(n_nodes);
+        done.resize(n_nodes, 0);
+        aff.resize(n_nodes);
+        aff_done.resize(n_nodes, 0);
+        return true;
     }
-    const uint32_t *node(uint32_t k) const { return q.nodes + 6 * (size_t)k; }
-    uint32_t arg(uint32_t k, uint32_t i) const { return q.args[node(k)[3] + i]; }
+
+    // Word-level index reasoning: calldata and memory reads at `p + k` for one
+    // symbolic p and many constants k (a CALLDATACOPY from a symbolic offset)
+    // are pairwise distinct whenever their constants differ, so their Ackermann
+    // pairs and store-chain hits are decided without an equality circuit.
+    static void add_limbs(std::vector<uint32_t> &a, const std::vector<uint32_t> &b, uint32_t w, bool sub) {
+        uint64_t carry = sub ? 1u : 0u;
+        for (size_t i = 0; i < a.size(); ++i) {
+            uint64_t x = (uint64_t)a[i] + (uint64_t)(sub ? ~b[i] : b[i]) + carry;
+            a[i] = (uint32_t)x;
+            carry = x >> 32;
+        }
+        if (w & 31u) a.back() &= (1u << (w & 31u)) - 1u;
+    }
+    const Affine &affine(uint32_t k) {
+        if (aff_done[k]) return aff[k];
+        const uint32_t *n = node(k);
+        uint32_t w = n[1];
+        size_t nl = (w + 31) / 32;
+        Affine r{k, std::vector<uint32_t>(nl, 0u)};
+        if (n[0] == MS_CONST) {
+            r.base = NO_BASE;
+            for (size_t i = 0; i < nl; ++i) r.off[i] = limbs_[n[4] + i];
+        } else if ((n[0] == MS_BVADD || n[0] == MS_BVSUB) && n[2] == 2) {
+            Affine a = affine(arg(k, 0));
+            const Affine &b = affine(arg(k, 1));
+            if (b.base == NO_BASE && a.off.size() == nl) {
+                add_limbs(a.off, b.off, w, n[0] == MS_BVSUB);
+                r = a;
+            } else if (n[0] == MS_BVADD && a.base == NO_BASE && b.off.size() == nl) {
+                Affine c = b;
+                add_limbs(c.off, a.off, w, false);
+                r = c;
+            }
+        }
+        aff[k] = r;
+        aff_done[k] = 1;
+        return aff[k];
+    }
+    // 1: the two terms are equal, -1: they differ, 0: not known
+    int relate(uint32_t a, uint32_t b) {
+        if (a == NO_BASE || b == NO_BASE) return 0;
+        if (a == b) return 1;
+        const Affine &x = affine(a), &y = affine(b);
+        if (x.base != y.base || x.off.size() != y.off.size()) return 0;
+        return x.off == y.off ? 1 : -1;
+    }
+    const uint32_t *node(uint32_t k) const { return nodes_.data() + 6 * (size_t)k; }
+    uint32_t arg(uint32_t k, uint32_t i) const { return args_[node(k)[3] + i]; }
 
     const Bits &get(uint32_t k) {
         if (!done[k]) { bad = true; static Bits empty; return empty; }
         return memo[k];
     }
 
-    // the read of a base array / function at `args`, Ackermannised against the
-    // earlier reads of the same one
-    Bits point(int kind, uint32_t id, const std::vector<Bits> &args, uint32_t width) {
+    // The read of a base array / function at `args`: a fresh word.  Ackermann's
+    // congruence between reads (equal arguments -> equal values) is added on
+    // demand (lemmas_for): all O(n^2) pairs up front dominated the CNF when a
+    // copy from a symbolic calldata offset reads hundreds of bytes.
+    Bits point(int kind, uint32_t id, const std::vector<Bits> &args, uint32_t width, uint32_t idx_node = NO_BASE) {
         std::vector<Lit> key{kind, (int)id};
         for (const Bits &a : args) {
             key.push_back((int)a.size());
@@ -748,31 +889,104 @@ public:
         }
         auto it = read_index.find(key);
         if (it != read_index.end()) return reads[it->second].val;
-        Bits v = G.fresh_word(width);
-        for (const ReadRec &r : reads) {
-            if (r.kind != kind || r.id != id || r.args.size() != args.size()) continue;
-            std::vector<Lit> same;
-            bool width_ok = true;
-            for (size_t i = 0; i < args.size(); ++i) {
-                if (r.args[i].size() != args[i].size()) { width_ok = false; break; }
-                same.push_back(G.eq(r.args[i], args[i]));
-            }
-            if (!width_ok || r.val.size() != width) continue;
-            Lit all = G.and_n(same);
-            if (all == G.F) continue;
-            // all -> v == r.val, bit by bit
-            for (size_t b = 0; b < width; ++b) {
-                S.add_clause({neg(all), neg(v[b]), r.val[b]});
-                S.add_clause({neg(all), v[b], neg(r.val[b])});
-            }
+        // a read at the same index term (word-level) is the same read
+        if (idx_node != NO_BASE) {
+            for (const ReadRec &r : reads)
+                if (r.kind == kind && r.id == id && relate(r.idx_node, idx_node) == 1 && r.val.size() == width)
+                    return r.val;
         }
+        Bits v = G.fresh_word(width);
         read_index.emplace(key, reads.size());
-        reads.push_back({id, kind, args, v});
+        reads.push_back({id, kind, args, v, idx_node});
         return v;
     }
 
+    // Congruence lemmas the model violates: reads of one array / function with
+    // equal argument values and different results get "args equal -> values
+    // equal".  Returns the number added (0: the model is consistent).
+    size_t lemmas_for(const std::vector<int8_t> &model) {
+        auto val = [&](const Bits &b) {
+            std::vector<uint32_t> out((b.size() + 31) / 32 + 1, 0u);
+            out[0] = (uint32_t)b.size();
+            for (size_t i = 0; i < b.size(); ++i) {
+                Lit l = G.nrm(b[i]);
+                bool v = l == G.T ? true : l == G.F ? false
+                                                   : ((model[var(l)] == LU ? false : (bool)model[var(l)]) != sgn(l));
+                if (v) out[1 + (i >> 5)] |= 1u << (i & 31);
+            }
+            return out;
+        };
+        auto assigned = [&](const Bits &b) {
+            for (Lit l : b) {
+                Lit n = G.nrm(l);
+                if (n != G.T && n != G.F && model[var(n)] == LU) return false;
+            }
+            return true;
+        };
+        std::unordered_map<std::vector<Lit>, std::vector<size_t>, VecHash> groups;
+        for (size_t i = 0; i < reads.size(); ++i) {
+            // a read of another query's terms the search left unassigned has no
+            // value to compare (its inputs are free: any extension can avoid or
+            // match the others)
+            bool full = assigned(reads[i].val);
+            for (const Bits &a : reads[i].args) full = full && assigned(a);
+            if (!full) continue;
+            std::vector<Lit> key{reads[i].kind, (int)reads[i].id};
+            for (const Bits &a : reads[i].args) {
+                auto v = val(a);
+                key.insert(key.end(), v.begin(), v.end());
+            }
+            groups[key].push_back(i);
+        }
+        size_t added = 0;
+        for (auto &g : groups) {
+            const std::vector<size_t> &ix = g.second;
+            if (ix.size() < 2) continue;
+            // chain every member to the first: a star of lemmas covers the group
+            for (size_t m = 1; m < ix.size(); ++m) {
+                size_t a = ix[0], b = ix[m];
+                if (val(reads[a].val) == val(reads[b].val)) continue;
+                if (a > b) std::swap(a, b);
+                uint64_t code = (uint64_t)a * 1000003ull + b;
+                if (!lemma_seen.insert(code).second) continue;
+                const ReadRec &r = reads[a], &t = reads[b];
+                if (r.args.size() != t.args.size() || r.val.size() != t.val.size()) continue;
+                std::vector<Lit> same;
+                bool ok = true;
+                for (size_t i = 0; i < r.args.size(); ++i) {
+                    if (r.args[i].size() != t.args[i].size()) { ok = false; break; }
+                    same.push_back(G.eq(r.args[i], t.args[i]));
+                }
+                if (!ok) continue;
+                Lit all = G.and_n(same);
+                for (size_t bit = 0; bit < r.val.size(); ++bit) {
+                    S.add_clause({neg(all), neg(r.val[bit]), t.val[bit]});
+                    S.add_clause({neg(all), r.val[bit], neg(t.val[bit])});
+                }
+                ++added;
+            }
+        }
+        return added;
+    }
+    std::unordered_set<uint64_t> lemma_seen;
+    size_t lemma_rounds = 0, lemmas = 0;
+
+    // solve with congruence lemmas on demand: LT only for a consistent model
+    int8_t solve_lazy(const std::vector<Lit> &assume, uint64_t max_conflicts,
+                      std::chrono::steady_clock::time_point deadline, bool timed) {
+        for (;;) {
+            int8_t r = S.solve(assume, max_conflicts, deadline, timed);
+            ++lemma_rounds;
+            if (r != LT) return r;
+            size_t got = lemmas_for(S.model);
+            lemmas += got;
+            if (got == 0) return LT;
+            if (timed && std::chrono::steady_clock::now() > deadline) return LU;
+        }
+    }
+
     // select(array node k, index bits)
-    Bits select(uint32_t k, const Bits &idx, uint32_t width) {
+    Bits select(uint32_t k, const Bits &idx, uint32_t width, uint32_t idx_node) {
         std::vector<Lit> key{(int)k};
         key.insert(key.end(), idx.begin(), idx.end());
         auto it = select_memo.find(key);
@@ -782,14 +996,16 @@ public:
         if (n[0] == MS_K) {
             r = get(arg(k, 0));
         } else if (n[0] == MS_ARRAY) {
-            r = point(1, n[4], {idx}, width);
+            r = point(1, n[4], {idx}, width, idx_node);
         } else if (n[0] == MS_STORE) {
             const Bits &i2 = get(arg(k, 1));
             const Bits &v = get(arg(k, 2));
-            Lit hit = G.eq(i2, idx);
+            int rel = relate(arg(k, 1), idx_node);
+            Lit hit = rel == 1 ? G.T : rel == -1 ? G.F : G.eq(i2, idx);
             if (hit == G.T) r = v;
+            else if (hit == G.F) r = select(arg(k, 0), idx, width, idx_node);
             else {
-                Bits rest = select(arg(k, 0), idx, width);
+                Bits rest = select(arg(k, 0), idx, width, idx_node);
                 r = G.ite(hit, v, rest);
             }
         } else {
@@ -810,7 +1026,7 @@ public:
             // constant divisor: zero, a power of two, or any other
             int ones = 0, pos = -1;
             for (size_t i = 0; i < w; ++i)
-                if (b[i] == G.T) { ++ones; pos = (int)i; }
+                if (G.nrm(b[i]) == G.T) { ++ones; pos = (int)i; }
             if (ones == 0) {
                 out = {Bits(w, G.T), a};
             } else if (ones == 1) {
@@ -853,10 +1069,10 @@ public:
         auto A = [&](uint32_t i) -> const Bits & { return get(arg(k, i)); };
         auto bit = [&](Lit l) { return Bits{l}; };
         switch (op) {
-        case MS_CONST: r = G.cnst(w, q.limbs + n[4]); break;
+        case MS_CONST: r = G.cnst(w, limbs_.data() + n[4]); break;
         case MS_VAR: {
             uint32_t id = n[4];
-            if (id >= q.n_vars) { bad = true; return; }
+            if (id >= n_vars) { bad = true; return; }
             if (var_bits[id].empty()) { var_bits[id] = G.fresh_word(w); var_width[id] = w; }
             if (var_bits[id].size() != w) { bad = true; return; }
             r = var_bits[id];
@@ -956,7 +1172,7 @@ public:
             break;
         }
         case MS_BVSUB_NOUDFL_U: r = bit(neg(G.ult(A(0), A(1)))); break;
-        case MS_SELECT: r = select(arg(k, 0), A(1), w); break;
+        case MS_SELECT: r = select(arg(k, 0), A(1), w, arg(k, 1)); break;
         case MS_UF: {
             std::vector<Bits> as;
             for (uint32_t i = 0; i < na; ++i) as.push_back(A(i));
@@ -993,95 +1209,250 @@ void put_bits(std::vector<uint32_t> &out, const Bits &b, const std::vector<int8_
 
 extern "C" int ms_abi_version(void) { return MS_ABI_VERSION; }
 
-extern "C" int ms_solve(const ms_query *q, const ms_limits *lim, uint32_t *model, uint32_t model_cap,
-                        uint32_t *model_len, ms_stats *stats) {
-    try {
-        if (!q || !q->nodes || (q->n_roots && !q->roots)) return MS_EINVAL;
-        auto t0 = std::chrono::steady_clock::now();
-        const uint32_t max_ms = lim ? lim->max_ms : 0u;
-        const uint64_t max_conf = lim ? lim->max_conflicts : 0u;
-        auto deadline = t0 + std::chrono::milliseconds(max_ms);
-        Blaster B(*q);
-        for (uint32_t k = 0; k < q->n_nodes; ++k) {
-            const uint32_t *n = B.node(k);
-            if (n[0] >= MS_N_OPS) return MS_EINVAL;
-            for (uint32_t i = 0; i < n[2]; ++i)
-                if (B.arg(k, i) >= k) return MS_EINVAL;           // post order
+namespace {
+
+// Blast the query's conjuncts (each asserted as it is built when `units`, the
+// stateless call; as assumptions in a session, whose clause database must stay
+// true of every later query), solve with congruence lemmas on demand,
+// minimise, write the model stream.
+int run(Blaster &B, const ms_query *q, const ms_limits *lim, bool units, uint32_t *model, uint32_t model_cap,
+        uint32_t *model_len, ms_stats *stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    const uint32_t max_ms = lim ? lim->max_ms : 0u;
+    const uint64_t max_conf = lim ? lim->max_conflicts : 0u;
+    auto deadline = t0 + std::chrono::milliseconds(max_ms);
+    const uint64_t conf0 = B.S.conflicts, dec0 = B.S.decisions, prop0 = B.S.propagations;
+    if (!B.append(*q)) return MS_EINVAL;
+    for (uint32_t i = 0; i < q->n_roots; ++i)
+        if (q->roots[i] >= B.n_nodes || B.node(q->roots[i])[1] != 1) return MS_EINVAL;
+    for (uint32_t i = 0; i < q->n_minimize; ++i)
+        if (q->minimize[i] >= B.n_nodes) return MS_EINVAL;
+    // Each conjunct is blasted (and, stateless, asserted) in turn, the smaller
+    // cones first: a bound (cnt <= 20), an equality with a constant, a selector
+    // check fixes bits at level 0 before the multipliers, store chains and
+    // congruence lemmas that read them are built, and those gates fold
+    // (Gates::nrm) instead of entering the CNF.
+    std::vector<uint32_t> order(q->roots, q->roots + q->n_roots);
+    std::stable_sort(order.begin(), order.end());
+    uint32_t blasted = 0;
+    bool timed_out = false;
+    auto cone = [&](uint32_t root) {
+        std::vector<std::pair<uint32_t, bool>> st{{root, false}};
+        while (!st.empty() && !B.bad) {
+            auto [k, ready] = st.back();
+            st.pop_back();
+            if (B.done[k]) continue;
+            if (!ready) {
+                st.push_back({k, true});
+                const uint32_t *n = B.node(k);
+                for (uint32_t i = n[2]; i-- > 0;)
+                    if (!B.done[B.arg(k, i)]) st.push_back({B.arg(k, i), false});
+                continue;
+            }
+            size_t first_input = B.G.inputs.size();
             B.blast(k);
-            if (B.bad) return MS_EINVAL;
-            if (max_ms && (k & 63u) == 0 && std::chrono::steady_clock::now() > deadline) {
-                if (stats) std::memset(stats, 0, sizeof(*stats));
-                return MS_UNKNOWN;
+            // decide the words' bits first: every gate output follows from them
+            // by propagation (the Tseitin encodings are complete), so the search
+            // does not wander through the gate variables
+            for (size_t j = first_input; j < B.G.inputs.size(); ++j) {
+                int v = B.G.inputs[j];
+                B.S.activity[v] = std::max(B.S.activity[v], B.S.var_inc);
+                if (B.S.heap_pos[v] >= 0) B.S.heap_up(B.S.heap_pos[v]);
+            }
+            if (max_ms && (++blasted & 63u) == 0 && std::chrono::steady_clock::now() > deadline) {
+                timed_out = true;
+                return;
             }
         }
-        for (uint32_t i = 0; i < q->n_roots; ++i) {
-            uint32_t r = q->roots[i];
-            if (r >= q->n_nodes || B.memo[r].size() != 1) return MS_EINVAL;
+    };
+    std::vector<Lit> assume;
+    for (uint32_t r : order) {
+        cone(r);
+        if (B.bad) return MS_EINVAL;
+        if (timed_out) break;
+        if (B.memo[r].size() != 1) return MS_EINVAL;
+        if (units) {
             B.S.add_clause({B.memo[r][0]});
+            if (!B.S.ok) break;                        // a conflict at level 0: unsat
+        } else {
+            assume.push_back(B.memo[r][0]);
         }
-        int8_t res = B.S.solve({}, max_conf, deadline, max_ms != 0);
-        uint32_t solves = 1;
-        std::vector<int8_t> best = B.S.model;
-        if (res == LT && q->n_minimize) {
-            // lexicographic minimisation (z3 Optimize's default priority), MSB
-            // first under assumptions; the best model so far stands on budget
-            auto mdeadline = std::chrono::steady_clock::now() +
-                             std::chrono::milliseconds(lim && lim->minimize_ms ? lim->minimize_ms : 2000u);
-            std::vector<Lit> assume;
-            bool stop = false;
-            for (uint32_t m = 0; m < q->n_minimize && !stop; ++m) {
-                uint32_t k = q->minimize[m];
-                if (k >= q->n_nodes) return MS_EINVAL;
-                const Bits bits = B.memo[k];
-                for (size_t i = bits.size(); i-- > 0 && !stop;) {
-                    Lit l = bits[i];
-                    if (l == B.G.T || l == B.G.F) continue;
-                    int8_t cur = best[var(l)];
-                    bool cur_v = (cur == LU ? false : (bool)cur) != sgn(l);
-                    if (!cur_v) { assume.push_back(neg(l)); continue; }
-                    assume.push_back(neg(l));
-                    int8_t r2 = B.S.solve(assume, 20000, mdeadline, true);
-                    ++solves;
-                    if (r2 == LT) best = B.S.model;
-                    else {
-                        assume.back() = l;
-                        if (r2 == LU) stop = true;
-                    }
+    }
+    for (uint32_t i = 0; i < q->n_minimize && B.S.ok && !timed_out; ++i) {
+        cone(q->minimize[i]);
+        if (B.bad) return MS_EINVAL;
+    }
+    auto fill_stats = [&](uint32_t solves) {
+        if (!stats) return;
+        stats->vars = (uint64_t)B.S.n_vars();
+        stats->clauses = B.S.n_clauses;
+        stats->conflicts = B.S.conflicts - conf0;
+        stats->decisions = B.S.decisions - dec0;
+        stats->propagations = B.S.propagations - prop0;
+        stats->solves = solves;
+        stats->ms = (uint32_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+            std::chrono::steady_clock::now() - t0).count();
+    };
+    if (timed_out) {
+        fill_stats(0);
+        return MS_UNKNOWN;
+    }
+    // the model of this query: the variables, arrays and functions its cone
+    // mentions (a session holds others, of earlier queries)
+    std::vector<char> in_cone(B.n_nodes, 0), var_in(B.n_vars, 0);
+    std::unordered_set<uint64_t> tables;          // (kind << 32) | id
+    {
+        std::vector<uint32_t> st(q->roots, q->roots + q->n_roots);
+        st.insert(st.end(), q->minimize, q->minimize + q->n_minimize);
+        while (!st.empty()) {
+            uint32_t k = st.back();
+            st.pop_back();
+            if (in_cone[k]) continue;
+            in_cone[k] = 1;
+            const uint32_t *n = B.node(k);
+            if (n[0] == MS_VAR) var_in[n[4]] = 1;
+            else if (n[0] == MS_ARRAY) tables.insert((1ull << 32) | n[4]);
+            else if (n[0] == MS_UF) tables.insert((2ull << 32) | n[4]);
+            for (uint32_t i = 0; i < n[2]; ++i) st.push_back(B.arg(k, i));
+        }
+    }
+    if (!units && std::getenv("MYTHSMT_RELEVANT")) {
+        // (A/B, off by default: measured slower on BECToken -- restricting the
+        // decisions to this query's inputs multiplied the lemma rounds)
+        // a session decides over this query's inputs only (Sat::set_relevant)
+        std::vector<int> relevant;
+        auto add_bits = [&](const Bits &b) {
+            for (Lit l : b)
+                if (l != B.G.T && l != B.G.F) relevant.push_back(var(l));
+        };
+        for (uint32_t v = 0; v < B.n_vars; ++v)
+            if (var_in[v]) add_bits(B.var_bits[v]);
+        for (const ReadRec &r : B.reads)
+            if (tables.count(((uint64_t)r.kind << 32) | r.id)) add_bits(r.val);
+        for (uint32_t k = 0; k < B.n_nodes; ++k) {
+            if (!in_cone[k]) continue;
+            const uint32_t *n = B.node(k);
+            uint64_t key;
+            if (n[0] == MS_BVUDIV || n[0] == MS_BVUREM) key = ((uint64_t)B.arg(k, 0) << 32) | B.arg(k, 1);
+            else if (n[0] == MS_BVSDIV || n[0] == MS_BVSREM || n[0] == MS_BVSMOD)
+                key = ((uint64_t)(0x80000000u | k) << 32) | (0x80000000u | n[0]);
+            else continue;
+            auto it = B.divmod_memo.find(key);
+            if (it != B.divmod_memo.end()) {
+                add_bits(it->second.first);
+                add_bits(it->second.second);
+            }
+        }
+        std::sort(relevant.begin(), relevant.end());
+        relevant.erase(std::unique(relevant.begin(), relevant.end()), relevant.end());
+        B.S.set_relevant(&relevant);
+    }
+    auto t_blast = std::chrono::steady_clock::now();
+    int8_t res = B.solve_lazy(assume, max_conf, deadline, max_ms != 0);
+    if (std::getenv("MYTHSMT_VERBOSE"))
+        std::fprintf(stderr, "ms_solve: blast %.1f ms (%d vars, %llu clauses, %zu reads), solve %.1f ms, %llu conflicts, "
+                             "%zu rounds, %zu lemmas, %llu decisions\n",
+                     std::chrono::duration<double, std::milli>(t_blast - t0).count(), B.S.n_vars(),
+                     (unsigned long long)B.S.n_clauses, B.reads.size(),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_blast).count(),
+                     (unsigned long long)(B.S.conflicts - conf0), B.lemma_rounds, B.lemmas,
+                     (unsigned long long)(B.S.decisions - dec0));
+    uint32_t solves = 1;
+    std::vector<int8_t> best = B.S.model;
+    if (res == LT && q->n_minimize) {
+        // lexicographic minimisation (z3 Optimize's default priority), MSB
+        // first under assumptions; the best model so far stands on budget
+        // per bit a conflict budget (deterministic); the wall clock only guards
+        auto mdeadline = std::chrono::steady_clock::now() +
+                         std::chrono::milliseconds(lim && lim->minimize_ms ? lim->minimize_ms : 10000u);
+        bool stop = false;
+        for (uint32_t m = 0; m < q->n_minimize && !stop; ++m) {
+            const Bits bits = B.memo[q->minimize[m]];
+            for (size_t i = bits.size(); i-- > 0 && !stop;) {
+                Lit l = B.G.nrm(bits[i]);
+                if (l == B.G.T || l == B.G.F) continue;
+                int8_t cur = best[var(l)];
+                bool cur_v = (cur == LU ? false : (bool)cur) != sgn(l);
+                assume.push_back(neg(l));
+                if (!cur_v) continue;
+                int8_t r2 = B.solve_lazy(assume, 20000, mdeadline, true);
+                ++solves;
+                if (r2 == LT) best = B.S.model;
+                else {
+                    assume.back() = l;
+                    if (r2 == LU) stop = true;
                 }
             }
         }
-        uint32_t ms = (uint32_t)std::chrono::duration_cast<std::chrono::milliseconds>(
-            std::chrono::steady_clock::now() - t0).count();
-        if (stats) {
-            stats->vars = (uint64_t)B.S.n_vars();
-            stats->clauses = B.S.n_clauses;
-            stats->conflicts = B.S.conflicts;
-            stats->decisions = B.S.decisions;
-            stats->propagations = B.S.propagations;
-            stats->solves = solves;
-            stats->ms = ms;
+    }
+    fill_stats(solves);
+    if (res == LF) return MS_UNSAT;
+    if (res == LU) return MS_UNKNOWN;
+    std::vector<uint32_t> out;
+    for (uint32_t v = 0; v < B.n_vars; ++v) {
+        if (B.var_bits[v].empty() || !var_in[v]) continue;
+        out.push_back(3u);
+        out.push_back(v);
+        put_bits(out, B.var_bits[v], best, B.G.T);
+    }
+    auto assigned = [&](const Bits &b) {
+        for (Lit l : b) {
+            Lit n = B.G.nrm(l);
+            if (n != B.G.T && n != B.G.F && best[var(n)] == LU) return false;
         }
-        if (res == LF) return MS_UNSAT;
-        if (res == LU) return MS_UNKNOWN;
-        std::vector<uint32_t> out;
-        for (uint32_t v = 0; v < q->n_vars; ++v) {
-            if (B.var_bits[v].empty()) {
-                // a variable no node uses: its width is unknown here; 0 limbs
-                continue;
-            }
-            put_bits(out, B.var_bits[v], best, B.G.T);
-        }
-        for (const ReadRec &r : B.reads) {
-            out.push_back((uint32_t)r.kind);
-            out.push_back(r.id);
-            for (const Bits &a : r.args) put_bits(out, a, best, B.G.T);
-            put_bits(out, r.val, best, B.G.T);
-        }
-        out.push_back(0u);
-        if (model_len) *model_len = (uint32_t)out.size();
-        if (out.size() > model_cap || !model) return MS_ESPACE;
-        std::memcpy(model, out.data(), out.size() * 4);
-        return MS_SAT;
+        return true;
+    };
+    for (const ReadRec &r : B.reads) {
+        if (!tables.count(((uint64_t)r.kind << 32) | r.id)) continue;
+        bool full = assigned(r.val);
+        for (const Bits &a : r.args) full = full && assigned(a);
+        if (!full) continue;                  // another query's read the search left open
+        out.push_back((uint32_t)r.kind);
+        out.push_back(r.id);
+        for (const Bits &a : r.args) put_bits(out, a, best, B.G.T);
+        put_bits(out, r.val, best, B.G.T);
+    }
+    out.push_back(0u);
+    if (model_len) *model_len = (uint32_t)out.size();
+    if (out.size() > model_cap || !model) return MS_ESPACE;
+    std::memcpy(model, out.data(), out.size() * 4);
+    return MS_SAT;
+}
+
+}  // namespace
+
+struct ms_session {
+    Blaster B;
+};
+
+extern "C" int ms_solve(const ms_query *q, const ms_limits *lim, uint32_t *model, uint32_t model_cap,
+                        uint32_t *model_len, ms_stats *stats) {
+    try {
+        if (!q || (q->n_nodes && (!q->nodes || !q->args)) || (q->n_roots && !q->roots)) return MS_EINVAL;
+        Blaster B;
+        return run(B, q, lim, true, model, model_cap, model_len, stats);
+    } catch (...) {
+        return MS_EINVAL;
+    }
+}
+
+extern "C" int ms_session_open(ms_session **out) {
+    try {
+        if (!out) return MS_EINVAL;
+        *out = new ms_session();
+        return 0;
+    } catch (...) {
+        return MS_EINVAL;
+    }
+}
+
+extern "C" void ms_session_close(ms_session *s) { delete s; }
+
+extern "C" int ms_session_solve(ms_session *s, const ms_query *q, const ms_limits *lim, uint32_t *model,
+                                uint32_t model_cap, uint32_t *model_len, ms_stats *stats) {
+    try {
+        if (!s || !q || (q->n_nodes && (!q->nodes || !q->args)) || (q->n_roots && !q->roots)) return MS_EINVAL;
+        return run(s->B, q, lim, false, model, model_cap, model_len, stats);
     } catch (...) {
         return MS_EINVAL;
     }

@@ -102,6 +102,10 @@ class _Lane:
         self.dirty = False        # host image changed, upload before the next launch
 
 
+class StatespaceNotBuilt(NotImplementedError):
+    """LaserEVM.nodes / .edges read with requires_statespace=True."""
+
+
 class LaserEVM:
     """The LASER engine with kernel 1 stepping every path of the work list."""
 
@@ -137,10 +141,11 @@ class LaserEVM:
         self.create_timeout = create_timeout or 0
 
         # the statespace graph (cfg.py nodes/edges) is not built by the batched
-        # core; a caller that needs it keeps the reference's host loop
+        # core: reading `nodes` / `edges` with requires_statespace raises
+        # (StatespaceNotBuilt) rather than returning an empty graph
         self.requires_statespace = requires_statespace
-        self.nodes: Dict = {}
-        self.edges: List = []
+        self._nodes: Dict = {}
+        self._edges: List = []
 
         self.time: Optional[datetime] = None
         self.executed_transactions = False
@@ -523,6 +528,27 @@ class LaserEVM:
                     final_states.append(s)
         finally:
             solver_mod.model_cache.clear_prefetch()
+
+    @property
+    def nodes(self) -> Dict:
+        """svm.py:549-637's statespace nodes: empty without requires_statespace
+        (as the reference leaves them); with it, refused -- the batched core runs
+        lanes many instructions per launch and never materialises the per-step
+        states a node lists (cfg.py Node.states), so an empty or partial graph
+        would be a silent wrong answer."""
+        if self.requires_statespace:
+            raise StatespaceNotBuilt("the statespace graph (requires_statespace=True) is not built by the "
+                                     "batched core; run the reference's LaserEVM for `myth graph` / "
+                                     "--statespace-json")
+        return self._nodes
+
+    @property
+    def edges(self) -> List:
+        if self.requires_statespace:
+            raise StatespaceNotBuilt("the statespace graph (requires_statespace=True) is not built by the "
+                                     "batched core; run the reference's LaserEVM for `myth graph` / "
+                                     "--statespace-json")
+        return self._edges
 
     def manage_cfg(self, opcode: Optional[str], new_states: List[GlobalState]) -> None:
         """svm.py:549-573 for the successors a host step produced: a JUMP /

@@ -20,6 +20,7 @@ import ctypes
 import os
 import subprocess
 import threading
+import time
 from pathlib import Path
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -59,15 +60,19 @@ class MsStats(ctypes.Structure):
                 ("ms", ctypes.c_uint32)]
 
 
+_SOLVE_ARGS = [ctypes.POINTER(MsQuery), ctypes.POINTER(MsLimits), ctypes.c_void_p, ctypes.c_uint32,
+               ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(MsStats)]
 SIGNATURES = {
     "ms_abi_version": (ctypes.c_int, []),
-    "ms_solve": (ctypes.c_int, [ctypes.POINTER(MsQuery), ctypes.POINTER(MsLimits), ctypes.c_void_p,
-                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(MsStats)]),
+    "ms_solve": (ctypes.c_int, _SOLVE_ARGS),
+    "ms_session_open": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+    "ms_session_close": (None, [ctypes.c_void_p]),
+    "ms_session_solve": (ctypes.c_int, [ctypes.c_void_p] + _SOLVE_ARGS),
 }
 
 
 def _command(out: str) -> List[str]:
-    return [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", str(SRC), "-o", out]
+    return [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", str(SRC), "-o", out]
 
 
 def source_hash() -> str:
@@ -133,9 +138,10 @@ class _Table:
     def __init__(self):
         self.index: Dict[int, int] = {}
         self.keep: List[Node] = []
-        self.nodes: List[int] = []
+        self.nodes: List[int] = []           # rows not yet sent (a session keeps the sent ones)
         self.args: List[int] = []
         self.limbs: List[int] = [0]
+        self.sent = 0                        # nodes the session already holds
         self.vars: Dict[str, Tuple[int, int]] = {}          # name -> (id, width)
         self.arrays: Dict[str, Tuple[int, int, int]] = {}   # name -> (id, domain, range)
         self.funcs: Dict[str, Tuple[int, tuple, int]] = {}  # name -> (id, domain widths, range)
@@ -165,19 +171,17 @@ class _Table:
             p0 = len(self.limbs)
             self.limbs.extend(_limbs(n.param, n.width))
         elif n.op == "var":
-            got = self.vars.setdefault(n.param, (len(self.vars), n.width))
-            if got[1] != n.width:
-                raise Unsupported(f"variable {n.param} at two widths")
-            p0 = got[0]
+            # z3 keys a constant by name and sort: x:4 and x:256 are two
+            p0 = self.vars.setdefault((n.param, n.width), (len(self.vars), n.width))[0]
         elif n.op == "array":
             name, dom, rng = n.param
-            p0 = self.arrays.setdefault(name, (len(self.arrays), dom, rng))[0]
+            p0 = self.arrays.setdefault((name, dom, rng), (len(self.arrays), dom, rng))[0]
             p1 = rng
         elif n.op in ("K", "store"):
             p1 = n.param[-1]
         elif n.op == "uf":
             name, dom, rng = n.param
-            p0 = self.funcs.setdefault(name, (len(self.funcs), tuple(dom), rng))[0]
+            p0 = self.funcs.setdefault((name, tuple(dom), rng), (len(self.funcs), tuple(dom), rng))[0]
         elif n.op == "extract":
             p0, p1 = n.param
         elif n.op in ("zero_extend", "sign_extend"):
@@ -188,49 +192,131 @@ class _Table:
         self.keep.append(n)
         self.nodes.extend((op, width, len(n.args), first, p0, p1))
 
+    def take_new(self):
+        """The rows added since the last call (arguments global, first_arg and
+        constant limbs local to the returned arrays), and mark them sent."""
+        out = (self.nodes, self.args, self.limbs)
+        self.sent = len(self.keep)
+        self.nodes, self.args, self.limbs = [], [], [0]
+        return out
+
 
 class ExactSolver:
     """``check(conjuncts, minimize)`` -> ("sat", assignment) | ("unsat", None)
     | ("unknown", None), the assignment in the ModelRef form (name -> int,
-    ArrayInterp, FuncInterp).  Budgets: conflicts and wall time per query."""
+    ArrayInterp, FuncInterp).  Budgets: conflicts and wall time per query.
 
-    def __init__(self, max_ms: int = 10000, max_conflicts: int = 0, minimize_ms: int = 2000):
+    The queries of one analysis share most of their terms (the path's prefix,
+    the keccak axioms, the calldata reads), so one session (ms_session_*) holds
+    them all: a query sends only the nodes the session lacks and is decided
+    under assumptions, over the clauses and lemmas its predecessors left.  The
+    session restarts when its CNF passes `session_vars`."""
+
+    def __init__(self, max_ms: int = 60000, max_conflicts: int = 200_000, minimize_ms: int = 60000,
+                 session: bool = True, session_vars: int = 4_000_000, session_conflicts: int = 5_000):
+        # the budget is a conflict count (deterministic: the same query order
+        # gives the same verdicts on any host), with a wall-clock cap as a guard
         self.max_ms = max_ms
         self.max_conflicts = max_conflicts
+        self.session_conflicts = session_conflicts
         self.minimize_ms = minimize_ms
+        self.use_session = session
+        self.session_vars = session_vars
+        self._session = None
+        self._table: Optional[_Table] = None
+        self._lock = threading.Lock()
         self.stats: Dict[str, int] = {"calls": 0, "sat": 0, "unsat": 0, "unknown": 0, "ms": 0,
-                                      "vars": 0, "clauses": 0, "conflicts": 0}
+                                      "vars": 0, "clauses": 0, "conflicts": 0, "sessions": 0}
 
-    def check(self, conjuncts: Sequence[Node], minimize: Sequence[Node] = (), max_ms: Optional[int] = None):
+    def close(self) -> None:
+        if self._session is not None:
+            load().ms_session_close(self._session)
+            self._session = None
+            self._table = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, conjuncts: Sequence[Node], minimize: Sequence[Node] = (), max_ms: Optional[int] = None,
+              fresh: bool = False):
+        """The session first, on `session_conflicts`; a query it cannot decide
+        within them is decided alone, on `max_conflicts`: its conjuncts asserted
+        as units, whose level-0 consequences fold the gates (a bounded factor
+        turns a 256 x 256 multiplier into a few rows) -- what the session's
+        assumptions cannot do for a shared clause database.  `max_ms` caps the
+        wall clock of each attempt."""
+        cap = self.max_ms if max_ms is None else max_ms
+        with self._lock:
+            if not self.use_session or fresh or minimize:
+                # the objectives are met bit by bit under assumptions: alone, the
+                # query's units fold what the bounds fix (and no other query's
+                # terms slow each of those solves)
+                return self._check(conjuncts, minimize, cap, False, self.max_conflicts)
+            st, a = self._check(conjuncts, minimize, cap, True, self.session_conflicts)
+            if st != "unknown":
+                return st, a
+            self.stats["fresh_retries"] = self.stats.get("fresh_retries", 0) + 1
+            self.stats["unknown"] -= 1
+            self.stats["calls"] -= 1
+            return self._check(conjuncts, minimize, cap, False, self.max_conflicts)
+
+    def _check(self, conjuncts, minimize, max_ms, session: bool, max_conflicts: int):
         import numpy as np
         from .program import ArrayInterp, FuncInterp
         lib = load()
-        t = _Table()
+        if session and self._session is None:
+            h = ctypes.c_void_p()
+            if lib.ms_session_open(ctypes.byref(h)) != 0:
+                raise RuntimeError("ms_session_open failed")
+            self._session, self._table = h, _Table()
+            self.stats["sessions"] += 1
+        t = self._table if session else _Table()
         roots = [t.add(c) for c in conjuncts]
         mins = [t.add(m) for m in minimize]
         self.stats["calls"] += 1
-        nodes = np.asarray(t.nodes, dtype=np.uint32)
-        args = np.asarray(t.args or [0], dtype=np.uint32)
-        limbs = np.asarray(t.limbs, dtype=np.uint32)
+        new_nodes, new_args, new_limbs = t.take_new()
+        nodes = np.asarray(new_nodes or [0], dtype=np.uint32)
+        args = np.asarray(new_args or [0], dtype=np.uint32)
+        limbs = np.asarray(new_limbs, dtype=np.uint32)
         roots_a = np.asarray(roots or [0], dtype=np.uint32)
         mins_a = np.asarray(mins or [0], dtype=np.uint32)
-        q = MsQuery(len(t.keep), nodes.ctypes.data, args.ctypes.data, limbs.ctypes.data, len(roots),
+        q = MsQuery(len(new_nodes) // 6, nodes.ctypes.data, args.ctypes.data, limbs.ctypes.data, len(roots),
                     roots_a.ctypes.data, len(mins), mins_a.ctypes.data, len(t.vars), len(t.arrays), len(t.funcs))
-        lim = MsLimits(self.max_conflicts, self.max_ms if max_ms is None else max_ms, self.minimize_ms)
+        lim = MsLimits(max_conflicts, max_ms, self.minimize_ms)
+        dump = os.environ.get("MYTHSMT_DUMP")
+        if dump and not session:        # diagnostics: the query as ms_solve sees it
+            os.makedirs(dump, exist_ok=True)
+            np.savez(os.path.join(dump, f"q{self.stats['calls']:05d}_{os.getpid()}.npz"), nodes=nodes, args=args,
+                     limbs=limbs, roots=roots_a[:len(roots)], mins=mins_a[:len(mins)],
+                     counts=np.asarray([len(t.vars), len(t.arrays), len(t.funcs)], dtype=np.uint32))
         st = MsStats()
         cap = 1 << 16
         while True:
             out = np.zeros(cap, dtype=np.uint32)
             n = ctypes.c_uint32(0)
-            rc = lib.ms_solve(ctypes.byref(q), ctypes.byref(lim), out.ctypes.data, cap, ctypes.byref(n),
-                              ctypes.byref(st))
+            if session:
+                rc = lib.ms_session_solve(self._session, ctypes.byref(q), ctypes.byref(lim), out.ctypes.data, cap,
+                                          ctypes.byref(n), ctypes.byref(st))
+                q.n_nodes = 0                    # appended: a retry sends nothing new
+            else:
+                rc = lib.ms_solve(ctypes.byref(q), ctypes.byref(lim), out.ctypes.data, cap, ctypes.byref(n),
+                                  ctypes.byref(st))
             if rc != MS_ESPACE:
                 break
             cap = int(n.value) + 16
-        for k in ("vars", "clauses", "conflicts", "ms"):
-            self.stats[k] += int(getattr(st, k))
+        self.stats["ms"] += int(st.ms)
+        self.stats["conflicts"] += int(st.conflicts)
+        self.stats["vars"] = max(self.stats["vars"], int(st.vars))
+        self.stats["clauses"] = max(self.stats["clauses"], int(st.clauses))
         if rc == MS_EINVAL:
+            if session:
+                self.close()
             raise Unsupported("ms_solve rejected the query")
+        if session and int(st.vars) > self.session_vars:
+            self.close()                          # the next query starts a fresh session
         if rc == MS_UNSAT:
             self.stats["unsat"] += 1
             return "unsat", None
@@ -250,11 +336,10 @@ class ExactSolver:
             pos += k
             return v
 
+        var_by_id = {v[0]: (k[0], v[1]) for k, v in t.vars.items()}
+        arr_by_id = {v[0]: (k[0], v[1], v[2]) for k, v in t.arrays.items()}
+        fn_by_id = {v[0]: (k[0], v[1], v[2]) for k, v in t.funcs.items()}
         assign: Dict[str, object] = {}
-        for name, (vid, w) in sorted(t.vars.items(), key=lambda kv: kv[1][0]):
-            assign[name] = take(w)
-        arr_by_id = {v[0]: (k, v[1], v[2]) for k, v in t.arrays.items()}
-        fn_by_id = {v[0]: (k, v[1], v[2]) for k, v in t.funcs.items()}
         while True:
             tag = words[pos]
             pos += 1
@@ -262,7 +347,10 @@ class ExactSolver:
                 break
             ident = words[pos]
             pos += 1
-            if tag == 1:
+            if tag == 3:
+                name, w = var_by_id[ident]
+                assign[name] = take(w)
+            elif tag == 1:
                 name, dom, rng = arr_by_id[ident]
                 idx = take(dom)
                 val = take(rng)
@@ -274,8 +362,4 @@ class ExactSolver:
                 val = take(rng)
                 interp = assign.setdefault(name, FuncInterp(0, {}))
                 interp.entries[xs] = val
-        for name in t.arrays:
-            assign.setdefault(name, ArrayInterp(0, {}))
-        for name in t.funcs:
-            assign.setdefault(name, FuncInterp(0, {}))
         return "sat", assign

@@ -561,7 +561,7 @@ class SatSearchBackend:
 
     def __init__(self, cache, search: bool = True, rounds: int = 12, beam: int = 6,
                  max_candidates: int = 4096, patience: int = 3, seed: int = 0x5EA5C4,
-                 exact=None, exact_ms: int = 10000):
+                 exact=None, exact_ms: int = 60000):
         self.cache = cache
         self.search = search
         self.exact = exact
@@ -603,7 +603,7 @@ class SatSearchBackend:
         """The exact procedure on a query the cheaper answers left open."""
         from .solver import SolverTimeOutException
         conj = [c for c in _conjuncts(key) if c is not TRUE]
-        budget = int(min(timeout or self.exact_ms, self.exact_ms))
+        budget = int(self.exact_ms)         # the wall-clock guard; the budget proper is conflicts
         mins = [m.raw if hasattr(m, "raw") else m for m in minimize]
         st, assign = self.exact.check(conj, mins, max_ms=max(budget, 1))
         if st == "unsat":
@@ -614,18 +614,29 @@ class SatSearchBackend:
             raise SolverTimeOutException
         self.stats["exact_sat"] += 1
         # every model is checked by kernel 2 before anyone sees it (a conjunct
-        # kernel 2 has no row for: by the host evaluator)
+        # kernel 2 has no row for: by the host evaluator); a session's model
+        # that fails is decided again alone, and a second failure is a bug
         live = [c for c in conj if c.op != "const"]
-        if live:
-            counts, hit = self._score(live, [assign])
-            if hit is False:
-                ref = ModelRef(assign)
-                ok = all(ref.eval(c, model_completion=True).param == 1 for c in live)
-            else:
-                ok = hit == 0
-            if not ok:
-                raise RuntimeError("the exact procedure's model does not satisfy the query on kernel 2")
-        return _model(assign)
+        for attempt in range(2):
+            if not live or self._holds(live, assign):
+                return _model(assign)
+            if attempt:
+                break
+            self.stats["exact_recheck"] = self.stats.get("exact_recheck", 0) + 1
+            st, assign = self.exact.check(conj, mins, max_ms=max(budget, 1), fresh=True)
+            if st == "unsat":
+                raise RuntimeError("the exact procedure answered sat and then unsat on one query")
+            if st == "unknown":
+                self.stats["exact_timeout"] += 1
+                raise SolverTimeOutException
+        raise RuntimeError("the exact procedure's model does not satisfy the query on kernel 2")
+
+    def _holds(self, live, assign) -> bool:
+        counts, hit = self._score(live, [assign])
+        if hit is False:
+            ref = ModelRef(assign)
+            return all(ref.eval(c, model_completion=True).param == 1 for c in live)
+        return hit == 0
 
     def _completed(self, assign: Dict[str, object]) -> "_Completed":
         """complete(assign), memoised per assignment object while neither it

@@ -43,7 +43,7 @@ from mythril_amd.smt.keccak_manager import keccak_function_manager
 
 def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, search=True,
             strategy: str = "bfs", runtime: bool = False, code: Optional[bytes] = None,
-            mutation_pruner: bool = True, exact: bool = True, exact_ms: int = 10000):
+            mutation_pruner: bool = True, exact: bool = True, exact_ms: int = 60000):
     """Run one analysis; returns (report issues, info).  `modules`: a module
     name, a list of names, or None (all fourteen).  `exact`: the queries the
     SAT search leaves open go to the exact procedure (mythril_amd.smt.exact),

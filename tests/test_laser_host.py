@@ -174,3 +174,18 @@ def test_event_order_bfs_and_dfs():
     assert order_bfs == [1, 2, 0]
     assert order_dfs == [2, 1, 0]
     assert _ranges([5, 1, 2, 3, 9]) == [[1, 3], [5, 1], [9, 1]]
+
+
+def test_statespace_graph_is_refused_not_faked():
+    """LaserEVM(requires_statespace=True) cannot hand out the
+    reference's nodes / edges (svm.py:549-637) -- reading them raises; without
+    the flag they are empty, as in the reference."""
+    import pytest
+    from mythril_amd.laser import LaserEVM, StatespaceNotBuilt
+    from oracle_device import OracleDevice
+    with pytest.raises(StatespaceNotBuilt):
+        LaserEVM(device=OracleDevice(), requires_statespace=True).nodes
+    with pytest.raises(StatespaceNotBuilt):
+        LaserEVM(device=OracleDevice(), requires_statespace=True).edges
+    vm = LaserEVM(device=OracleDevice(), requires_statespace=False)
+    assert vm.nodes == {} and vm.edges == []
