@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--host-profile", default=None,
                     help="directory: cProfile the LaserEVM fields (hooked_c2, taint_c2, symbolic_tx) "
                          "and write each one's cumulative-time table there")
+    ap.add_argument("--c3-tx", type=int, default=2,
+                    help="transactions of the C3 field (BECToken, all modules); 0 skips it")
     ap.add_argument("--full-record", default="gpurun_out/bench_full.json",
                     help="where the whole record goes (stdout carries the compact line, <= 4 KB)")
     ap.add_argument("--no-roofline", action="store_true",
@@ -280,6 +282,10 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
         analyses = host_profiled("myth_analyze", lambda: run_myth_analyze(
             dev, args.analyses, log=lambda m: _log(rank, m), cpu=not args.no_cpu_baseline))
 
+    c3 = None
+    if args.c3_tx and gpu and not args.profile_only and rank == 0:
+        c3 = host_profiled("c3_bectoken", lambda: run_c3_bectoken(dev, args.c3_tx, log=lambda m: _log(rank, m)))
+
     c4 = None
     if not args.no_c4:
         _log(rank, "C4")
@@ -343,6 +349,8 @@ def main(argv=None, device_factory=None, backend: str = "nccl"):
             out["symbolic_tx"] = symb
         if analyses is not None:
             out["myth_analyze"] = analyses
+        if c3 is not None:
+            out["c3_bectoken"] = c3
         full = Path(args.full_record)
         try:
             full.parent.mkdir(parents=True, exist_ok=True)
@@ -1118,6 +1126,60 @@ def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True)
             "unknown_confirmations": sum(r["confirmations"]["unknown"] for r in cpu_rows.values())}
         out["speedup_vs_cpu"] = cw / tot["wall_s"] if tot["wall_s"] else None
     return out
+
+
+def run_c3_bectoken(dev, tx_count: int, log=None):
+    """C3 (BASELINE configs[2]): ``myth analyze BECToken.sol -t
+    tx_count`` with every detection module on kernels 1 and 2 and the exact
+    procedure behind them.  BECToken needs solc 0.4 (absent): tests/bectoken.py
+    assembles the contract from its source.  Reports the issue table, whether
+    SWC-101 sits at batchTransfer's ``uint256(cnt) * _value`` (CVE-2018-10299),
+    the kernel-2 prefilter's hit rate over the queries get_model saw, and the
+    exact-procedure calls ("z3 calls") made and avoided."""
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
+    import tempfile
+    import analyze
+    import bectoken
+    import fnames
+    from mythril_amd.laser.disassembly import SignatureDB
+    saved_dir = os.environ.get("MYTHRIL_DIR")
+    with tempfile.TemporaryDirectory() as sigdir:
+        fnames.signature_db(Path(sigdir))
+        os.environ["MYTHRIL_DIR"] = sigdir
+        SignatureDB._reset()
+        try:
+            if log:
+                log(f"C3 BECToken -t {tx_count}")
+            gc.collect()
+            issues, info = analyze.analyze("BECToken", None, tx_count, dev, dev, code=bectoken.creation(),
+                                           search=False)
+        finally:
+            if saved_dir is None:
+                os.environ.pop("MYTHRIL_DIR", None)
+            else:
+                os.environ["MYTHRIL_DIR"] = saved_dir
+            SignatureDB._reset()
+    table = [list(r) for r in analyze.issue_table(issues)]
+    mul = bectoken.mul_address()
+    cache, srch, ex = info["cache"], info["search"], info["exact"] or {}
+    answered = cache["lru_hits"] + cache["seed_hits"]
+    queries = cache["queries"]
+    # every query the kernel-2 prefilter answered, the refutations and the fork
+    # filter's quick-sat answers are z3 calls the reference would have made
+    exact_calls = srch.get("exact_sat", 0) + srch.get("exact_unsat", 0) + srch.get("exact_timeout", 0)
+    summary = {"tx": tx_count, "wall_s": info["wall_s"], "issues": len(table),
+               "swc101_at_mul": any(r[0] == "101" and r[1] == mul and r[2] == "batchTransfer(address[],uint256)"
+                                    for r in table),
+               "prefilter_hit_rate": answered / queries if queries else None,
+               "exact_calls": exact_calls, "exact_calls_avoided": answered + srch.get("refuted", 0),
+               "exact_s": ex.get("ms", 0) / 1e3, "kernel1_s": info["device_ms"] / 1e3,
+               "kernel2_s": info["k2_ms"] / 1e3, "constraint_evals": int(info["device_evals"])}
+    return {"metric": "myth analyze BECToken.sol -t %d (C3): issues, prefilter hit rate, exact calls avoided"
+                      % tx_count,
+            "source": "tests/bectoken.py (assembled from solidity_examples/BECToken.sol; no solc here)",
+            "issues": table, "mul_address": mul, "confirmations": info["confirmations"],
+            "forks": info["forks"], "fork_filter": info["fork_filter"], "cache": cache,
+            "search": srch, "exact": ex, "lane_steps": int(info["lane_steps"]), "summary": summary}
 
 
 def _cpu_model() -> str:

@@ -558,6 +558,7 @@ class SatSearchBackend:
     support/model.py:37-82, so nothing stays "unknown"."""
 
     uses_seeds = True          # get_model consults the seeds before calling it
+    speculative = False        # it launches kernel 2: never from get_models' worker threads
 
     def __init__(self, cache, search: bool = True, rounds: int = 12, beam: int = 6,
                  max_candidates: int = 4096, patience: int = 3, seed: int = 0x5EA5C4,

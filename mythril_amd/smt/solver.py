@@ -879,6 +879,16 @@ def get_models(queries: Sequence, solver_timeout=None, workers: int = 8) -> List
         cs = q.get_all_constraints() if hasattr(q, "get_all_constraints") else list(q)
         prepared.append([c for c in cs if type(c) != bool])
     out: List[object] = []
+    if not getattr(solver_backend, "speculative", True):
+        # a backend that drives the device itself (kernel 2 in the SAT search and
+        # the exact procedure's re-check) runs in the sequential loop's thread:
+        # one library context is used from one host thread at a time (mythgpu.h)
+        for q in queries:
+            try:
+                out.append(get_model(q if isinstance(q, Constraints) else tuple(q), solver_timeout=solver_timeout))
+            except (UnsatError, SolverTimeOutException, SolverBackendMissing) as e:
+                out.append(e)
+        return out
     with ThreadPoolExecutor(max_workers=max(1, workers)) as pool:
         for cs in prepared:
             key = _spec_key(cs)

@@ -49,13 +49,20 @@ _orig_succ = sym.jumpi_successors
 _orig_call = search_mod.SatSearchBackend.__call__
 
 
+LIGHT = "--light" in sys.argv
+
+
 def traced_succ(state):
     st = state.mstate.stack
     cond = st[-2]
     raw = getattr(cond, "raw", None)
-    EVENTS.append(("fork", state.current_transaction.id if state.current_transaction else None,
-                   state.get_current_instruction()["address"], state.mstate.depth,
-                   digest(raw) if raw is not None else str(cond), repr(raw)[:300]))
+    if LIGHT:
+        EVENTS.append(("fork", state.current_transaction.id if state.current_transaction else None,
+                       state.get_current_instruction()["address"], state.mstate.depth))
+    else:
+        EVENTS.append(("fork", state.current_transaction.id if state.current_transaction else None,
+                       state.get_current_instruction()["address"], state.mstate.depth,
+                       digest(raw) if raw is not None else str(cond), repr(raw)[:300]))
     return _orig_succ(state)
 
 
@@ -112,6 +119,14 @@ refmodules.get_transaction_sequence = traced_gts
 
 
 def traced_call(self, constraints, minimize, maximize, timeout):
+    if LIGHT:
+        try:
+            m = _orig_call(self, constraints, minimize, maximize, timeout)
+            EVENTS.append(("search", len(constraints), "sat"))
+            return m
+        except Exception as e:
+            EVENTS.append(("search", len(constraints), type(e).__name__))
+            raise
     key = query_raw(constraints)
     d = hashlib.blake2b("".join(sorted(digest(c) for c in key)).encode(), digest_size=8).hexdigest() \
         if isinstance(key, (list, tuple)) else digest(key)
@@ -128,14 +143,29 @@ sym.jumpi_successors = traced_succ
 search_mod.SatSearchBackend.__call__ = traced_call
 
 
+TX = 2
+
+
 def main():
+    global TX
     names = sys.argv[1].split(",")
+    for a in sys.argv:
+        if a.startswith("--tx="):
+            TX = int(a[5:])
     d = tempfile.mkdtemp()
     fnames.signature_db(Path(d))
     os.environ["MYTHRIL_DIR"] = d
     SignatureDB._reset()
-    devs = [("cpu", OracleDevice(), OracleK2())]
-    if "--gpu" in sys.argv:
+    import threading
+
+    def beat():                      # a liveness line for the box's silence watchdog
+        import time as _t
+        while True:
+            _t.sleep(30)
+            print("...", flush=True, file=sys.stderr)
+    threading.Thread(target=beat, daemon=True).start()
+    devs = [] if "--only-gpu" in sys.argv else [("cpu", OracleDevice(), OracleK2())]
+    if "--gpu" in sys.argv or "--only-gpu" in sys.argv:
         from mythril_amd.device import GpuDevice
         g = GpuDevice(0)
         devs.append(("gpu", g, g))
@@ -146,7 +176,11 @@ def main():
             EVENTS.clear()
             _memo.clear()
             _lists.clear()
-            issues, info = analyze.analyze(name, None, 2, dev, k2)
+            if name == "BECToken":
+                import bectoken
+                issues, info = analyze.analyze(name, None, TX, dev, k2, code=bectoken.creation(), search=False)
+            else:
+                issues, info = analyze.analyze(name, None, TX, dev, k2)
             runs[tag] = {"events": list(EVENTS), "issues": analyze.issue_table(issues),
                          "info": {k: info[k] for k in ("forks", "confirmations", "search", "fork_filter")}}
             print(tag, name, json.dumps(runs[tag]["info"]), flush=True)
@@ -160,7 +194,7 @@ def main():
                     print("  ", i, a[i] if i < len(a) else None, "|", b[i] if i < len(b) else None)
         out[name] = runs
     os.makedirs(ROOT / "gpurun_out" / "r06", exist_ok=True)
-    with open(ROOT / "gpurun_out" / "r06" / "c3_trace.json", "w") as f:
+    with open(ROOT / "gpurun_out" / "r06" / ("c3_trace_%s.json" % names[0].replace(".sol.o", "")), "w") as f:
         json.dump(out, f, default=str)
 
 

