@@ -105,7 +105,7 @@ class OracleDevice:
         for cid, buf in self._cov.items():
             self.o.set_coverage(cid, buf if self._cov_on else None)
         bound = self._bound if self._img.shape.trace_cap else 0
-        self._park_symbolic(hook_mask, max_depth)
+        self._park_symbolic(hook_mask, max_depth, bound)
         img = self._img
         # taint lanes are k_sym_step's: the restatement steps them (tests/taintref.py)
         tl = np.nonzero((img.status == MG_RUNNING) & ((img.flags & MG_LANE_TAINT) != 0)
@@ -126,11 +126,12 @@ class OracleDevice:
                          int(((s != MG_RUNNING) & (s != MG_HOOK) & (s != MG_ESCAPE)).sum()),
                          int((s == MG_HOOK).sum()), int((s == MG_ESCAPE).sum()), 0.0)
 
-    def _park_symbolic(self, hook_mask, max_depth):
+    def _park_symbolic(self, hook_mask, max_depth, bound: int = 0):
         """The oracle has no symbolic lanes: a running MG_LANE_SYMBOLIC lane stops
         before its next instruction exactly as k_sym_step stops before one it
-        cannot run (depth cut, past the end, hook, else MG_ESC_SYMBOLIC), so the
-        host's escape handler executes it (test stand-in for k_sym_step)."""
+        cannot run (depth cut, past the end, the instruction traced and the loop
+        bound checked, hook, else MG_ESC_SYMBOLIC), so the host's escape handler
+        executes it (test stand-in for k_sym_step)."""
         img = self._img
         live = np.nonzero((img.status == MG_RUNNING) & ((img.flags & MG_LANE_SYMBOLIC) != 0))[0]
         mask = hook_mask or (0, 0, 0, 0)
@@ -143,7 +144,19 @@ class OracleDevice:
                 img.status[i] = MG_HALT_END
             else:
                 op = int(ops[pc])
-                hooked = (int(mask[op >> 6]) >> (op & 63)) & 1 and not int(img.flags[i]) & MG_LANE_HOOK_ACK
+                acked = int(img.flags[i]) & MG_LANE_HOOK_ACK
+                if bound and not acked:
+                    # BoundedLoopsStrategy sees every instruction the path is popped
+                    # at (sym_step.cuh: trace_step before the hook / escape checks):
+                    # the oracle traces it and stops there (a probe hook on it)
+                    probe = [int(x) for x in mask]
+                    probe[op >> 6] |= 1 << (op & 63)
+                    self.o.run(img, int(i), 1, hook_mask=probe, max_steps=1, max_depth=max_depth,
+                               loop_bound=bound)
+                    if int(img.status[i]) != MG_HOOK:
+                        continue                # the loop bound, or a full trace: as the device
+                    img.status[i], img.aux[i] = MG_RUNNING, 0
+                hooked = (int(mask[op >> 6]) >> (op & 63)) & 1 and not acked
                 sp = int(img.sp[i])
                 fork = (op == 0x57 and not hooked and sp >= 2 and img.symbolic and int(img.stag[i, sp - 2])
                         and not int(img.stag[i, sp - 1]))
