@@ -213,7 +213,7 @@ class ExactSolver:
     session restarts when its CNF passes `session_vars`."""
 
     def __init__(self, max_ms: int = 60000, max_conflicts: int = 200_000, minimize_ms: int = 60000,
-                 session: bool = True, session_vars: int = 4_000_000, session_conflicts: int = 5_000):
+                 session: bool = True, session_vars: int = 400_000, session_conflicts: int = 5_000):
         # the budget is a conflict count (deterministic: the same query order
         # gives the same verdicts on any host), with a wall-clock cap as a guard
         self.max_ms = max_ms

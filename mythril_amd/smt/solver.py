@@ -300,6 +300,12 @@ class ModelCache:
         self._progs: Dict[Node, object] = {}
         self.part_evals = 0            # conjunct programs x models run on kernel 2
         self._rowgens: "OrderedDict[tuple, _RowGen]" = OrderedDict()
+        # conjunct rows by model (_rows_by_model): the seed block per seed epoch,
+        # head models' bits by fingerprint (models kept alive in _head_keep)
+        self._seed_sig = None
+        self._seed_rows: Dict[Node, np.ndarray] = {}
+        self._head_bits: Dict[Node, Dict[tuple, bool]] = {}
+        self._head_keep: Dict[tuple, object] = {}
         self.stats = {"queries": 0, "lru_hits": 0, "seed_hits": 0, "misses": 0, "divergences": 0}
 
     @property
@@ -465,29 +471,87 @@ class ModelCache:
             # a caller's own pool with its cached columns (program.PoolColumns over
             # the pool's assignments, in order): the search's starting pool
             return self._rows_uncached(conjuncts, pool, columns)
-        gp = self._row_gen(pool)
-        if gp is None:
+        split = self._seed_split(pool)
+        if split is None:
             return self._rows_uncached(conjuncts, pool)
-        gen, perm = gp
+        return self._rows_by_model(conjuncts, pool, split)
+
+    HEAD_BITS_MODELS = 4096
+
+    def _seed_split(self, pool: List) -> Optional[int]:
+        """The head length of a model-cache pool -- LRU models that are not
+        seeds, then every seed (_full_pool) -- or None for any other pool (the
+        search's candidates)."""
+        seeds = self.seeds
+        ns, n = len(seeds), len(pool)
+        if not ns or n < ns or self.seed_source is None:
+            return None
+        h = n - ns
+        if pool[h] is not seeds[0] or not all(a is b for a, b in zip(pool[h:], seeds)):
+            return None
+        return h
+
+    def _rows_by_model(self, conjuncts: Sequence[Node], pool: List, h: int) -> Dict[Node, np.ndarray]:
+        """Rows kept per conjunct and per model: the seed block's bits per seed
+        epoch, each head model's bit by its fingerprint (identity and
+        interpretation sizes).  A model that enters the LRU (every answer of the
+        exact procedure puts one there) then costs one small launch over the new
+        models alone, not the whole pool again for every conjunct a generation
+        had already evaluated."""
+        seeds = self.seeds
         n = len(pool)
-        rows: Dict[Node, np.ndarray] = {}
-        todo = []
-        for c in conjuncts:
-            b = gen.rows.get(c)
-            if b is None:
-                todo.append(c)
-            else:
-                rows[c] = _pack_bits(b if perm is None else b[perm])
+        head = pool[:h]
+        sig = (id(seeds), len(seeds), getattr(self.seed_source, "epoch", None))
+        if self._seed_sig != sig:
+            self._seed_sig, self._seed_rows = sig, {}
+        if len(self._head_keep) > self.HEAD_BITS_MODELS:
+            self._head_keep, self._head_bits = {}, {}
+        fps = [_fingerprint(m) for m in head]
+        for fp, m in zip(fps, head):
+            self._head_keep.setdefault(fp, m)         # ids stay unique while a bit is kept
+        srows, hbits = self._seed_rows, self._head_bits
+        todo = [c for c in conjuncts if c not in srows and self._progs.get(c, _MISSING) is not None]
         if todo:
             fresh = self._rows_uncached(todo, pool)
             for c, r in fresh.items():
                 u = np.unpackbits(r.view(np.uint8), bitorder="little")[:n].astype(bool)
-                if perm is not None:
-                    base = np.empty(n, dtype=bool)
-                    base[perm] = u
-                    u = base
-                gen.rows[c] = u
-            rows.update(fresh)
+                srows[c] = u[h:]
+                hb = hbits.setdefault(c, {})
+                for fp, bit in zip(fps, u[:h]):
+                    hb[fp] = bool(bit)
+        # head models a kept conjunct has no bit for: one launch over them alone
+        missing: "OrderedDict[tuple, object]" = OrderedDict()
+        need = []
+        for c in conjuncts:
+            if c not in srows:
+                continue
+            hb = hbits.setdefault(c, {})
+            lack = [k for k, fp in enumerate(fps) if fp not in hb]
+            if lack:
+                need.append(c)
+                for k in lack:
+                    missing.setdefault(fps[k], head[k])
+        if need:
+            sub = list(missing.values())
+            sub_fps = list(missing.keys())
+            fresh = self._rows_uncached(need, sub)
+            for c, r in fresh.items():
+                u = np.unpackbits(r.view(np.uint8), bitorder="little")[:len(sub)].astype(bool)
+                hb = hbits[c]
+                for fp, bit in zip(sub_fps, u):
+                    hb.setdefault(fp, bool(bit))
+        rows: Dict[Node, np.ndarray] = {}
+        for c in conjuncts:
+            sr = srows.get(c)
+            if sr is None:
+                continue
+            hb = hbits[c]
+            if any(fp not in hb for fp in fps):
+                continue                              # not evaluable on these models
+            u = np.empty(n, dtype=bool)
+            u[:h] = [hb[fp] for fp in fps]
+            u[h:] = sr
+            rows[c] = _pack_bits(u)
         return rows
 
     ROW_GENERATIONS = 4

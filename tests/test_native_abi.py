@@ -48,3 +48,20 @@ def test_open_without_gpu_fails_cleanly():
     lib = native.load()
     ctx = ctypes.c_void_p()
     assert lib.mg_open(0, ctypes.byref(ctx)) != 0
+
+
+def test_exact_library_exports_every_declared_symbol():
+    """include/mythsmt.h (the exact procedure behind kernel 2): libmythsmt.so
+    loads, exports every declared function with the binding's signature, and
+    its opcode numbering is exact.py's."""
+    from mythril_amd.smt import exact
+    text = (HEADER.parent / "mythsmt.h").read_text()
+    syms = sorted(set(re.findall(r"\b(ms_[a-z_0-9]+)\s*\(", text)))
+    lib = exact.load()
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(exact.SIGNATURES), set(syms) ^ set(exact.SIGNATURES)
+    assert lib.ms_abi_version() == 1
+    enum = re.search(r"enum \{(.*?)\};", text, re.S).group(1)
+    names = [n.strip() for n in re.findall(r"MS_([A-Z_0-9]+)", enum) if n != "N_OPS"]
+    assert [n.lower() for n in names] == [k.lower() for k in sorted(exact.OPS, key=exact.OPS.get)]
