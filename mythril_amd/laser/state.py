@@ -406,10 +406,27 @@ _ORDER: "weakref.WeakKeyDictionary[Node, str]" = weakref.WeakKeyDictionary()
 
 
 def _term_order(n: Node) -> str:
+    """A structural sort key, the same on every rank: a digest computed bottom
+    up over (op, width, param, child keys), memoised per node -- not repr(),
+    which prints a DAG as a tree and grows ~32x per ABI nesting level of a
+    calldata-derived offset."""
     k = _ORDER.get(n)
-    if k is None:
-        k = _ORDER[n] = repr(n)
-    return k
+    if k is not None:
+        return k
+    import hashlib
+    stack = [(n, False)]
+    while stack:
+        x, ready = stack.pop()
+        if x in _ORDER:
+            continue
+        if not ready:
+            stack.append((x, True))
+            stack.extend((a, False) for a in x.args if a not in _ORDER)
+            continue
+        h = hashlib.blake2b(repr((x.op, x.width, x.param, tuple(_ORDER[a] for a in x.args))).encode(),
+                            digest_size=12).hexdigest()
+        _ORDER[x] = h
+    return _ORDER[n]
 
 
 def _const_node(c: int) -> Node:

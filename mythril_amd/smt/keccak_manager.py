@@ -33,6 +33,11 @@ class KeccakFunctionManager:
         self.reset()
 
     def reset(self):
+        try:                                  # the search's term-dependency memo holds terms
+            from .search import clear_deps
+            clear_deps()
+        except ImportError:
+            pass
         self.store_function: Dict[int, Tuple[Function, Function]] = {}
         self.interval_hook_for_size: Dict[int, int] = {}
         self.hash_result_store: Dict[int, List[BitVec]] = {}

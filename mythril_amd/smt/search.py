@@ -33,6 +33,7 @@ the query; the host does not decide satisfaction anywhere.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -121,7 +122,10 @@ class _Inverter:
     def inv(self, n: Node, t: int, depth: int = 0) -> List[Repair]:
         if depth > 40:
             return []
-        key = (id(n), t)
+        # a result computed near the depth cut may be truncated: the memo keeps
+        # it only for visits as deep (coarse buckets of 10), so a shallower visit
+        # of the same subterm computes its own
+        key = (id(n), t, depth // 10)
         got = self.memo.get(key)
         if got is None:
             got = self.memo[key] = self._inv(n, t, depth)[: 4 * self.LIMIT]
@@ -449,6 +453,11 @@ class _Completed(dict):
 
 
 _DEPS: Dict[int, Tuple[Node, frozenset, bool]] = {}
+_DEPS_MAX = 1 << 16          # entries keep their terms alive: bounded, cleared on keccak reset
+
+
+def clear_deps() -> None:
+    _DEPS.clear()
 
 
 def _deps(raw: Node) -> Tuple[frozenset, frozenset]:
@@ -471,6 +480,8 @@ def _deps(raw: Node) -> Tuple[frozenset, frozenset]:
             uf.add(n.param[0])
         stack.extend(n.args)
     fs, fu = frozenset(names), frozenset(uf)
+    if len(_DEPS) >= _DEPS_MAX:
+        _DEPS.clear()
     _DEPS[id(raw)] = (raw, fs, fu)
     return fs, fu
 
@@ -572,7 +583,11 @@ class SatSearchBackend:
         self.max_candidates = max_candidates
         self.patience = patience       # rounds without a better best count before giving up
         self.rng = np.random.default_rng(seed)
-        self._memo_completed: Dict[int, tuple] = {}
+        # completed assignments by the assignment's identity: an LRU bounded by
+        # the model cache plus the seeds (each entry holds the
+        # completed dict with its keccak and Power tables)
+        self._memo_completed: "OrderedDict[int, tuple]" = OrderedDict()
+        self._memo_cap = 2048
         self._start_cols: Optional[tuple] = None      # (the starting pool's assignments, their PoolColumns)
         self.stats: Dict[str, int] = {"calls": 0, "refuted": 0, "seed": 0, "search": 0, "unknown": 0,
                                       "candidates": 0, "launches": 0, "minimised": 0,
@@ -651,10 +666,15 @@ class SatSearchBackend:
         state = (sum(len(v) for v in km.symbolic_inputs.values()), len(km.concrete_hashes),
                  len(em.symbolic_points), len(em.concrete_points), len(assign))
         got = self._memo_completed.get(id(assign))
+        if got is not None:
+            self._memo_completed.move_to_end(id(assign))
         if got is not None and got[0] is assign and got[1] == state:
             return got[2]
         out = complete(dict(assign))
         self._memo_completed[id(assign)] = (assign, state, out)
+        self._memo_completed.move_to_end(id(assign))
+        while len(self._memo_completed) > self._memo_cap:
+            self._memo_completed.popitem(last=False)
         return out
 
     def _columns(self, pool: List[Dict[str, object]]) -> PoolColumns:
