@@ -910,10 +910,10 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
     reachability filter (svm.py:244-249).  Symbolic lanes run on kernel 1
     (store chains, symbolic memory, symbolic SHA3); every fork filter group and
     reachability round is one kernel-2 launch over the model cache plus
-    `n_seeds` witness seeds (laser/witness.py).  No SMT backend exists in the
-    image, so a query no candidate satisfies is an UNKNOWN and its path is kept
-    (mode "prefilter-only"); escaped paths (no host handler) are dropped and
-    counted.  Runtime codes are analysed as `myth analyze -f` does (symbolic
+    `n_seeds` witness seeds (laser/witness.py).  A query no candidate satisfies
+    goes to the exact procedure (smt/exact.py), and its fork is pruned on unsat
+    or on a budget timeout, as is_possible prunes (constraints.py:33-43);
+    escaped paths (no host handler) are dropped and counted.  Runtime codes are analysed as `myth analyze -f` does (symbolic
     storage); flag_array is deployed concretely first.  `replicas` copies of the
     deployed world state run together (one contract per replica, independent
     paths) for a batch that fills the GPU; replicas=1 is one analysis.  With
@@ -1018,7 +1018,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
 
 def _myth_analyze_rows(device, k2, tx_count: int, names, log=None):
     """tests/analyze.py over `names`: per contract the issue table, the
-    confirmations (sat / unknown), escapes dropped, wall / kernel time and the
+    confirmations (sat / unsat / timeout / unknown), escapes dropped, wall / kernel time and the
     in-situ rates."""
     import analyze
     rows = {}
@@ -1062,14 +1062,15 @@ def run_myth_analyze(dev, tx_count: int, log=None, names=None, cpu: bool = True)
     BFS + BoundedLoopsStrategy(3), max depth 128, the mutation pruner, the
     modules' hooks (tests/refmodules.py, restated: the reference's modules need
     z3), the fork and reachability filters and every issue confirmation on
-    kernel 2 (SAT-only backend: model cache, witness seeds, guided search and
-    the keccak-axiom refutations; an unconfirmed issue stays "unknown",
-    counted), escapes stepped by the tests/symref.py handler so no path is
-    dropped.  Contracts are dealt round-robin over the ranks (total work
+    kernel 2 (model cache, witness seeds, guided search and the keccak-axiom
+    refutations, then the exact procedure of smt/exact.py on what they leave
+    open: unsat and budget timeouts drop the issue and prune the fork, as the
+    reference does), escapes stepped by the tests/symref.py handler so no path
+    is dropped.  Contracts are dealt round-robin over the ranks (total work
     fixed).  The CPU comparator runs the same harness on rank 0 with the C
     oracles as kernels 1 and 2 (oracle/evm_ref.c single-threaded,
-    oracle/bv_ref.c on up to 16 threads) and reports whether the issue sets
-    agree."""
+    oracle/bv_ref.c on the host's CPU share) and reports whether the issue
+    sets agree."""
     sys.path.insert(0, str(Path(__file__).resolve().parent / "tests"))
     import tempfile
     import fnames

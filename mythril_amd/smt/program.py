@@ -35,6 +35,27 @@ TILE_INSNS = 2048
 
 # operand references per op (bv_upload: ite 3, one-operand ops 1, the rest 2)
 _NREF = np.array([3 if op == "ite" else 1 if op in UNARY else 2 for op in OPS], dtype=np.int64)
+def _reads(ins: np.ndarray):
+    """(opcodes, per-operand variable masks, variables read, table-read mask,
+    tables read) of an instruction array."""
+    op = (ins[:, 0] & 0xFF).astype(np.int64)
+    nref = _NREF[np.minimum(op, len(_NREF) - 1)]
+    isvar = [(nref > k) & ((ins[:, 1 + k] >> 30) == REF_VAR) for k in range(3)]
+    used = np.unique(np.concatenate([ins[m, 1 + k] & 0x3FFFFFFF for k, m in enumerate(isvar)]))
+    istab = op == OPCODE["tab"]
+    tabs = np.unique(ins[istab, 3] & TAB_INDEX_MASK) if istab.any() else np.zeros(0, dtype=np.uint32)
+    return op, isvar, used, istab, tabs
+
+
+def read_sets(batch: "ProgramBatch"):
+    """(variable indices, table indices) the batch's programs read."""
+    ins = np.asarray(batch.insns, dtype=np.uint32)
+    if ins.shape[0] == 0:
+        return frozenset(), frozenset()
+    _, _, used, _, tabs = _reads(ins)
+    return frozenset(used.tolist()), frozenset(tabs.tolist())
+
+
 def compact_vars(batch: "ProgramBatch") -> "ProgramBatch":
     """The batch with its variables and tables renumbered to those its programs
     read (a persistent compiler's batches carry every variable and table it has
@@ -43,12 +64,7 @@ def compact_vars(batch: "ProgramBatch") -> "ProgramBatch":
     ins = np.asarray(batch.insns, dtype=np.uint32)
     if ins.shape[0] == 0:
         return batch
-    op = (ins[:, 0] & 0xFF).astype(np.int64)
-    nref = _NREF[np.minimum(op, len(_NREF) - 1)]
-    isvar = [(nref > k) & ((ins[:, 1 + k] >> 30) == REF_VAR) for k in range(3)]
-    used = np.unique(np.concatenate([ins[m, 1 + k] & 0x3FFFFFFF for k, m in enumerate(isvar)]))
-    istab = op == OPCODE["tab"]
-    tabs = np.unique(ins[istab, 3] & TAB_INDEX_MASK) if istab.any() else np.zeros(0, dtype=np.uint32)
+    op, isvar, used, istab, tabs = _reads(ins)
     if used.size == len(batch.var_names) and tabs.size == len(batch.tables):
         return batch
     out = ins.copy()
@@ -204,11 +220,16 @@ class ModelPool:
 
     @staticmethod
     def from_dicts(models: List[Dict[str, object]], var_names: List[str], var_widths: List[int],
-                   tables: Optional[List] = None):
+                   tables: Optional[List] = None, reads=None):
         """models: name -> int for variables, ArrayInterp / FuncInterp for tables;
-        anything absent is completed with 0 (z3 model_completion)."""
+        anything absent is completed with 0 (z3 model_completion).  reads: the
+        (variable, table) index sets the programs evaluated on the pool read
+        (read_sets); the others are left zero / empty, as no program sees them."""
         vals = np.zeros((max(len(var_names), 1), max(len(models), 1), 8), dtype=np.uint32)
+        rv, rt = reads if reads is not None else (None, None)
         for v, (name, w) in enumerate(zip(var_names, var_widths)):
+            if rv is not None and v not in rv:
+                continue
             # one bytes join per variable: the per-element numpy writes cost
             # more than the values themselves
             mask = (1 << w) - 1
@@ -227,7 +248,7 @@ class ModelPool:
             M512 = (1 << 512) - 1
             for t, sig in enumerate(tables):
                 for m, model in enumerate(models):
-                    interp = model.get(sig.name)
+                    interp = model.get(sig.name) if rt is None or t in rt else None
                     start[t, m] = len(rows)
                     if isinstance(interp, ArrayInterp):
                         default[t, m] = _wide_limbs(interp.default)

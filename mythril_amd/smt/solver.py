@@ -39,7 +39,7 @@ import numpy as np
 from .expr import And, BitVec, Bool, Node, TRUE, _fold, _select, const, symbol_factory
 from .flatten import Compiler, batch_from, compile_sets
 from .lower import Unsupported
-from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, compact_vars, concat_pools
+from .program import ArrayInterp, FuncInterp, ModelPool, PoolColumns, compact_vars, concat_pools, read_sets
 
 NO_MODEL = 0xFFFFFFFF
 
@@ -362,8 +362,10 @@ class ModelCache:
             block = self._seed_cols[1].pool(prog.var_names, prog.var_widths, prog.tables)
             if n == 0:
                 return block
+            # the head's models over the variables these programs read only (the
+            # batch keeps the compiler's numbering for the seed block's columns)
             head = ModelPool.from_dicts([_view(m, key) for m in models[:n]], prog.var_names,
-                                        prog.var_widths, prog.tables)
+                                        prog.var_widths, prog.tables, reads=read_sets(prog))
             return concat_pools(head, block)
         return ModelPool.from_dicts([_view(m, key) for m in models], prog.var_names,
                                     prog.var_widths, prog.tables)

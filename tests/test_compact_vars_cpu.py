@@ -6,7 +6,7 @@ import numpy as np
 
 from mythril_amd.smt.expr import UGT, Function, If, symbol_factory
 from mythril_amd.smt.flatten import Compiler, batch_from
-from mythril_amd.smt.program import FuncInterp, ModelPool, compact_vars
+from mythril_amd.smt.program import FuncInterp, ModelPool, compact_vars, read_sets
 from oracle_device import OracleK2
 
 
@@ -44,6 +44,13 @@ def test_compacted_batches_evaluate_as_the_full_batch():
            for b in (full, small)]
     assert np.array_equal(got[0], got[1])
     assert got[0].any()
+    # the full batch over a pool that serialises only what it reads (the model
+    # cache's head block beside the cached seed columns)
+    reads = read_sets(full)
+    assert reads == ({full.var_names.index(n) for n in ("v3", "v7", "v9")}, {full.tables.index(small.tables[0])})
+    part = ModelPool.from_dicts(models, full.var_names, full.var_widths, full.tables, reads=reads)
+    assert not part.values[full.var_names.index("v0")].any()
+    assert np.array_equal(k2.eval_bits(full, part)[2], got[0])
 
 
 def test_a_batch_reading_everything_is_returned_as_is():
