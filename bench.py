@@ -78,8 +78,10 @@ def parse(argv=None):
     ap.add_argument("--host-profile", default=None,
                     help="directory: cProfile the LaserEVM fields (hooked_c2, taint_c2, symbolic_tx) "
                          "and write each one's cumulative-time table there")
-    ap.add_argument("--c3-tx", type=int, default=2,
-                    help="transactions of the C3 field (BECToken, all modules); 0 skips it")
+    ap.add_argument("--c3-tx", type=int, default=1,
+                    help="transactions of the C3 field (BECToken, all modules); 0 skips it.  -t 1 holds "
+                         "the CVE-2018-10299 finding (3 s on the MI355X); -t 2 takes about a minute, "
+                         "most of it in the exact procedure (profiles/r06/README.md)")
     ap.add_argument("--full-record", default="gpurun_out/bench_full.json",
                     help="where the whole record goes (stdout carries the compact line, <= 4 KB)")
     ap.add_argument("--no-roofline", action="store_true",

@@ -244,7 +244,7 @@ public:
             phase[v] = (int8_t)sgn(trail[c]);
             assigns[v] = LU;
             reason[v] = CR_NONE;
-            if (rel.empty() || rel[v]) heap_insert(v);
+            if (rel.empty() || (v < (int)rel.size() && rel[v])) heap_insert(v);
         }
         trail.resize(trail_lim[lvl]);
         trail_lim.resize(lvl);
@@ -971,11 +971,19 @@ public:
     std::unordered_set<uint64_t> lemma_seen;
     size_t lemma_rounds = 0, lemmas = 0;
 
-    // solve with congruence lemmas on demand: LT only for a consistent model
+    // solve with congruence lemmas on demand: LT only for a consistent model.
+    // One conflict budget across the lemma rounds (0: unbounded).
     int8_t solve_lazy(const std::vector<Lit> &assume, uint64_t max_conflicts,
                       std::chrono::steady_clock::time_point deadline, bool timed) {
+        const uint64_t c0 = S.conflicts;
         for (;;) {
-            int8_t r = S.solve(assume, max_conflicts, deadline, timed);
+            uint64_t left = 0;
+            if (max_conflicts) {
+                uint64_t used = S.conflicts - c0;
+                if (used >= max_conflicts) return LU;
+                left = max_conflicts - used;
+            }
+            int8_t r = S.solve(assume, left, deadline, timed);
             ++lemma_rounds;
             if (r != LT) return r;
             size_t got = lemmas_for(S.model);

@@ -212,10 +212,17 @@ class ExactSolver:
     under assumptions, over the clauses and lemmas its predecessors left.  The
     session restarts when its CNF passes `session_vars`."""
 
-    def __init__(self, max_ms: int = 60000, max_conflicts: int = 200_000, minimize_ms: int = 60000,
+    def __init__(self, max_ms: int = 60000, max_conflicts: int = 50_000, minimize_ms: int = 60000,
                  session: bool = True, session_vars: int = 400_000, session_conflicts: int = 5_000):
         # the budget is a conflict count (deterministic: the same query order
-        # gives the same verdicts on any host), with a wall-clock cap as a guard
+        # gives the same verdicts on any host), with a wall-clock cap as a guard.
+        # 50,000 conflicts take about 4 s on the GPU box's host cores, inside
+        # the reference's default z3 timeout (support_args.py:12, 10 s); every
+        # query the 18-contract field and BECToken -t 1 decide needs < 3,300
+        # (profiles/r06/exact_budget.txt); the budget is spent by divisions
+        # whose divisor is a Power() application (flag_array's packed bool
+        # array: `word / 256**(i % 32)`, a 256-bit divider over a symbolic
+        # divisor), a timeout that prunes, as the reference's does
         self.max_ms = max_ms
         self.max_conflicts = max_conflicts
         self.session_conflicts = session_conflicts

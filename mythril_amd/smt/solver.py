@@ -514,13 +514,13 @@ class ModelCache:
         srows, hbits = self._seed_rows, self._head_bits
         todo = [c for c in conjuncts if c not in srows and self._progs.get(c, _MISSING) is not None]
         if todo:
-            fresh = self._rows_uncached(todo, pool)
+            # the seed block alone (its cached columns as they are, no head block
+            # copied in front); the head models' bits follow below, over the
+            # variables the programs read
+            ns = n - h
+            fresh = self._rows_uncached(todo, pool[h:])
             for c, r in fresh.items():
-                u = np.unpackbits(r.view(np.uint8), bitorder="little")[:n].astype(bool)
-                srows[c] = u[h:]
-                hb = hbits.setdefault(c, {})
-                for fp, bit in zip(fps, u[:h]):
-                    hb[fp] = bool(bit)
+                srows[c] = np.unpackbits(r.view(np.uint8), bitorder="little")[:ns].astype(bool)
         # head models a kept conjunct has no bit for: one launch over them alone
         missing: "OrderedDict[tuple, object]" = OrderedDict()
         need = []
