@@ -1324,11 +1324,21 @@ int run(Blaster &B, const ms_query *q, const ms_limits *lim, bool units, uint32_
             for (uint32_t i = 0; i < n[2]; ++i) st.push_back(B.arg(k, i));
         }
     }
-    if (!units && std::getenv("MYTHSMT_RELEVANT")) {
-        // (A/B, off by default: measured slower on BECToken -- restricting the
-        // decisions to this query's inputs multiplied the lemma rounds)
-        // a session decides over this query's inputs only (Sat::set_relevant)
-        std::vector<int> relevant;
+    // A session query is first decided over its own cone's inputs only
+    // (Sat::set_relevant) on a small conflict budget: a satisfiable query then
+    // leaves the other queries' variables unassigned instead of deciding the
+    // whole session (2.5x faster on exceptions.sol.o).  A query that needs
+    // more than 20 conflicts goes on over every variable with the full budget:
+    // restricted decisions cost ~7x more per conflict on BECToken's
+    // multiplications (profiles/r06/exact_budget.txt).  MYTHSMT_REL_BUDGET sets the first
+    // budget (0: off); MYTHSMT_RELEVANT=1 keeps the restriction for the whole
+    // budget (the A/B).
+    std::vector<int> relevant;
+    const char *rel_env = std::getenv("MYTHSMT_REL_BUDGET");
+    const bool rel_only = std::getenv("MYTHSMT_RELEVANT") != nullptr;
+    const uint64_t rel_budget = rel_only ? max_conf : rel_env ? std::strtoull(rel_env, nullptr, 10) : 20u;
+    const bool use_rel = !units && (rel_only || rel_budget > 0);
+    if (use_rel) {
         auto add_bits = [&](const Bits &b) {
             for (Lit l : b)
                 if (l != B.G.T && l != B.G.F) relevant.push_back(var(l));
@@ -1353,10 +1363,19 @@ int run(Blaster &B, const ms_query *q, const ms_limits *lim, bool units, uint32_
         }
         std::sort(relevant.begin(), relevant.end());
         relevant.erase(std::unique(relevant.begin(), relevant.end()), relevant.end());
-        B.S.set_relevant(&relevant);
     }
     auto t_blast = std::chrono::steady_clock::now();
-    int8_t res = B.solve_lazy(assume, max_conf, deadline, max_ms != 0);
+    int8_t res;
+    if (use_rel) {
+        B.S.set_relevant(&relevant);
+        res = B.solve_lazy(assume, rel_budget, deadline, max_ms != 0);
+        B.S.set_relevant(nullptr);                    // every variable again
+        bool late = max_ms != 0 && std::chrono::steady_clock::now() > deadline;
+        if (res == LU && !rel_only && !late)
+            res = B.solve_lazy(assume, max_conf, deadline, max_ms != 0);
+    } else {
+        res = B.solve_lazy(assume, max_conf, deadline, max_ms != 0);
+    }
     if (std::getenv("MYTHSMT_VERBOSE"))
         std::fprintf(stderr, "ms_solve: blast %.1f ms (%d vars, %llu clauses, %zu reads), solve %.1f ms, %llu conflicts, "
                              "%zu rounds, %zu lemmas, %llu decisions\n",

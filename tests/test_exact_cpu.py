@@ -139,6 +139,33 @@ def test_random_narrow_queries_match_brute_force(solver, seed):
     assert checked >= 30 and sat_seen and unsat_seen
 
 
+@pytest.mark.parametrize("mode", [{"MYTHSMT_REL_BUDGET": "0"}, {"MYTHSMT_REL_BUDGET": "1"},
+                                  {"MYTHSMT_RELEVANT": "1"}])
+def test_session_decision_modes_match_brute_force(monkeypatch, mode):
+    """A session query is decided over its cone's inputs first (20 conflicts by
+    default), then over every variable: the verdicts and models must not depend
+    on that split -- whole-session decisions only, a 1-conflict first phase, and
+    cone-only decisions for the whole budget."""
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    s = exact.ExactSolver(max_ms=20000)
+    rng = random.Random(0x5E55)
+    x, y = E.var("x", W), E.var("y", W)
+    seen = set()
+    for _ in range(150):
+        conj = [c for c in (rand_bool(rng, [x, y], 3) for _ in range(rng.randint(1, 3))) if c.op != "const"]
+        if not conj or any("mem4" in repr(c) or "f4" in repr(c) for c in conj):
+            continue
+        st, assign = s.check(conj)
+        want = any(holds(a, conj) for a in enumerate_models(conj, ["x", "y"]))
+        assert st == ("sat" if want else "unsat"), (mode, conj, st)
+        if st == "sat":
+            assert holds(assign, conj), (mode, conj, assign)
+        seen.add(st)
+    assert seen == {"sat", "unsat"} and s.stats["sessions"] >= 1
+    s.close()
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_arrays_and_functions_match_brute_force(solver, seed):
     """One-bit reads of a 2-bit-domain array and function, over stores at
