@@ -946,30 +946,79 @@ public:
             for (size_t m = 1; m < ix.size(); ++m) {
                 size_t a = ix[0], b = ix[m];
                 if (val(reads[a].val) == val(reads[b].val)) continue;
-                if (a > b) std::swap(a, b);
-                uint64_t code = (uint64_t)a * 1000003ull + b;
-                if (!lemma_seen.insert(code).second) continue;
-                const ReadRec &r = reads[a], &t = reads[b];
-                if (r.args.size() != t.args.size() || r.val.size() != t.val.size()) continue;
-                std::vector<Lit> same;
-                bool ok = true;
-                for (size_t i = 0; i < r.args.size(); ++i) {
-                    if (r.args[i].size() != t.args[i].size()) { ok = false; break; }
-                    same.push_back(G.eq(r.args[i], t.args[i]));
-                }
-                if (!ok) continue;
-                Lit all = G.and_n(same);
-                for (size_t bit = 0; bit < r.val.size(); ++bit) {
-                    S.add_clause({neg(all), neg(r.val[bit]), t.val[bit]});
-                    S.add_clause({neg(all), r.val[bit], neg(t.val[bit])});
-                }
-                ++added;
+                if (congruence(a, b)) ++added;
             }
         }
         return added;
     }
     std::unordered_set<uint64_t> lemma_seen;
     size_t lemma_rounds = 0, lemmas = 0;
+
+    // "args(a) == args(b) -> val(a) == val(b)" for reads a and b, once per pair
+    bool congruence(size_t a, size_t b) {
+        if (a > b) std::swap(a, b);
+        uint64_t code = (uint64_t)a * 1000003ull + b;
+        if (!lemma_seen.insert(code).second) return false;
+        const ReadRec &r = reads[a], &t = reads[b];
+        if (r.args.size() != t.args.size() || r.val.size() != t.val.size()) return false;
+        std::vector<Lit> same;
+        for (size_t i = 0; i < r.args.size(); ++i) {
+            if (r.args[i].size() != t.args[i].size()) return false;
+            same.push_back(G.eq(r.args[i], t.args[i]));
+        }
+        Lit all = G.and_n(same);
+        for (size_t bit = 0; bit < r.val.size(); ++bit) {
+            S.add_clause({neg(all), neg(r.val[bit]), t.val[bit]});
+            S.add_clause({neg(all), r.val[bit], neg(t.val[bit])});
+        }
+        return true;
+    }
+
+    // Eager congruence for small-domain reads: a read whose arguments keep at
+    // most EAGER_FREE free bits after level-0 folding gets its lemma against
+    // every read of the same array / function at constant arguments its fixed
+    // bits allow, before the search -- a Power(256, i % 32) application against
+    // the 32 pinned points of the exponent table, say.  Lazily, the search first
+    // picks a divisor that is no power of 256 and meets the table lemma by
+    // lemma, each round a full re-solve (flag_array's division queries ran out
+    // of budget that way).  Reads at wide symbolic arguments stay lazy.
+    static constexpr size_t EAGER_FREE = 8;
+    size_t eager_done = 0, eager_lemmas_added = 0;
+    void eager_lemmas() {
+        const size_t n = reads.size();
+        if (eager_done == n) return;
+        std::vector<int> freeb(n);
+        for (size_t i = 0; i < n; ++i) {
+            size_t f = 0;
+            for (const Bits &a : reads[i].args)
+                for (Lit l : a) {
+                    Lit m = G.nrm(l);
+                    if (m != G.T && m != G.F) ++f;
+                }
+            freeb[i] = (int)f;
+        }
+        auto compatible = [&](const ReadRec &x, const ReadRec &c) {
+            if (x.args.size() != c.args.size()) return false;
+            for (size_t i = 0; i < x.args.size(); ++i) {
+                if (x.args[i].size() != c.args[i].size()) return false;
+                for (size_t j = 0; j < x.args[i].size(); ++j) {
+                    Lit s = G.nrm(x.args[i][j]), k = G.nrm(c.args[i][j]);
+                    if ((s == G.T && k == G.F) || (s == G.F && k == G.T)) return false;
+                }
+            }
+            return true;
+        };
+        for (size_t i = 0; i < n; ++i) {
+            if (freeb[i] == 0 || (size_t)freeb[i] > EAGER_FREE) continue;
+            for (size_t j = 0; j < n; ++j) {
+                if (freeb[j] != 0 || (i < eager_done && j < eager_done)) continue;
+                const ReadRec &x = reads[i], &c = reads[j];
+                if (x.kind != c.kind || x.id != c.id || x.val.size() != c.val.size() || !compatible(x, c)) continue;
+                if (congruence(i, j)) ++eager_lemmas_added;
+            }
+        }
+        eager_done = n;
+    }
 
     // solve with congruence lemmas on demand: LT only for a consistent model.
     // One conflict budget across the lemma rounds (0: unbounded).
@@ -1289,6 +1338,10 @@ int run(Blaster &B, const ms_query *q, const ms_limits *lim, bool units, uint32_
     for (uint32_t i = 0; i < q->n_minimize && B.S.ok && !timed_out; ++i) {
         cone(q->minimize[i]);
         if (B.bad) return MS_EINVAL;
+    }
+    {
+        const char *eager = std::getenv("MYTHSMT_EAGER");       // "0": lazy only (the A/B)
+        if (B.S.ok && !timed_out && !(eager && eager[0] == '0')) B.eager_lemmas();
     }
     auto fill_stats = [&](uint32_t solves) {
         if (!stats) return;

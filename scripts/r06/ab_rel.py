@@ -1,8 +1,12 @@
-"""Interleaved A/B of the exact procedure's first phase (MYTHSMT_REL_BUDGET: the
-conflicts a session query is decided on over its own cone before every
-variable; 0 = never) on the in-situ bench fields, in one process on one box:
+"""Interleaved A/B of an exact-procedure switch on the in-situ bench fields, in
+one process on one box (the switches are read at every solve):
 
-    python scripts/r06/ab_rel.py OUT.json [rounds]
+    python scripts/r06/ab_rel.py OUT.json [rounds] [VAR v1,v2] [codes]
+
+VAR defaults to MYTHSMT_REL_BUDGET 0,20 (the conflicts a session query is
+decided on over its own cone before every variable; 0 = never); MYTHSMT_EAGER
+0,1 is the eager small-domain congruence.  codes: the symbolic_tx contracts
+(default overflow.sol.o,exceptions.sol.o).
 
 Per round and mode: symbolic_tx (overflow, exceptions; 2 replicas), the
 18-contract myth_analyze field (no CPU comparator) and BECToken -t 1, with
@@ -22,10 +26,13 @@ import symref  # noqa: E402
 from mythril_amd.device import GpuDevice  # noqa: E402
 
 
+VAR, MODES, CODES = "MYTHSMT_REL_BUDGET", ("0", "20"), ("overflow.sol.o", "exceptions.sol.o")
+
+
 def one(dev, mode):
-    os.environ["MYTHSMT_REL_BUDGET"] = str(mode)
-    out = {"mode": mode}
-    bench.SYMBOLIC_TX_CODES = ("overflow.sol.o", "exceptions.sol.o")
+    os.environ[VAR] = str(mode)
+    out = {"var": VAR, "mode": mode}
+    bench.SYMBOLIC_TX_CODES = CODES
     st = bench.run_symbolic_tx(dev, 2, 2, 1024, symref.Engine(signals=True).step)
     for n, c in st["contracts"].items():
         out[n] = {"wall_s": c["wall_s"], "exact_ms": c["exact_ms"], "exact": c["exact"],
@@ -40,12 +47,17 @@ def one(dev, mode):
 
 
 def main():
+    global VAR, MODES, CODES
     dev = GpuDevice(0)
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    one(dev, 20)                                   # warm-up: compiles, caches, the signature DB
+    if len(sys.argv) > 4:
+        VAR, MODES = sys.argv[3], tuple(sys.argv[4].split(","))
+    if len(sys.argv) > 5:
+        CODES = tuple(sys.argv[5].split(","))
+    one(dev, MODES[-1])                            # warm-up: compiles, caches, the signature DB
     res = []
     for r in range(rounds):
-        for mode in (0, 20):
+        for mode in MODES:
             t0 = time.perf_counter()
             row = one(dev, mode)
             row["round"], row["total_s"] = r, time.perf_counter() - t0

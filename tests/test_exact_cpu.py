@@ -236,6 +236,37 @@ def test_storage_chain_and_congruence(solver):
     assert solver.check([(k(Concat(x, y)) != k(Concat(y, x))).raw, (x == y).raw])[0] == "unsat"
 
 
+def _power_division_query():
+    """flag_array's shape: a packed bool array read as ``(word / 256**(i % 32))
+    & 0xff != 0``, with Power(256, e) a function pinned at e = 0..31 (the
+    exponent manager's table, exponent_function_manager.py) and `word` a read
+    of symbolic storage at `i / 32` (one slot stored)."""
+    i = sf.BitVecSym("i", 256)
+    pw = Function("Power", [256], 256)
+    store = Array("Storage", 256, 256)
+    word = 0x1234 << (8 * 21)
+    store[sf.BitVecVal(0x26, 256)] = sf.BitVecVal(word, 256)
+    e = E.BitVec(E._fold("bvurem", 256, (i.raw, E.const(32, 256))))
+    j = E.BitVec(E._fold("bvudiv", 256, (i.raw, E.const(32, 256))))
+    div = E.BitVec(E._fold("bvudiv", 256, (store[j].raw, pw(e).raw)))
+    conj = [(pw(sf.BitVecVal(k, 256)) == 256 ** k).raw for k in range(32)]
+    conj += [((div & 0xFF) != 0).raw, ULT(i, 1 << 16).raw]
+    return conj
+
+
+def test_small_domain_reads_get_eager_congruence(monkeypatch):
+    """A read whose arguments keep few free bits (the exponent i % 32) is tied to
+    the pinned points before the search: the division by Power(256, i % 32) is
+    decided in a few conflicts, with a model that holds; without the eager
+    lemmas the same conflict budget is not enough."""
+    conj = _power_division_query()
+    st, a = exact.ExactSolver(max_ms=20000, max_conflicts=3000, session=False).check(conj)
+    assert st == "sat" and holds(a, conj)
+    monkeypatch.setenv("MYTHSMT_EAGER", "0")
+    st0, _ = exact.ExactSolver(max_ms=20000, max_conflicts=3000, session=False).check(conj)
+    assert st0 == "unknown"                    # (never unsat: the query is satisfiable)
+
+
 def test_reference_keccak_verdicts(solver):
     """tests/laser/keccak_tests.py:7-145 (tests/golden/keccak_cases.json): the
     reference's own sat / unsat verdicts -- z3's, in the reference's suite --
