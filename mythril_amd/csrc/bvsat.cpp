@@ -1094,6 +1094,18 @@ public:
             }
         }
         if (out.first.empty()) {
+            // a divisor that is a read with a small-domain argument, pinned at
+            // constant arguments to zero or powers of two (Power(256, i % 32)):
+            // per pinned case the quotient is a shift, and the general divider
+            // below only has to hold when no case applies
+            std::vector<std::pair<Lit, int>> cases;   // (args equal, bit of the power; -1: zero)
+            const char *dc = std::getenv("MYTHSMT_DIVCASES");   // "0": general divider only (the A/B)
+            Lit none = !(dc && dc[0] == '0') && divisor_cases(b, cases) ? G.F : G.T;
+            if (none == G.F) {
+                std::vector<Lit> conds;
+                for (auto &c : cases) conds.push_back(c.first);
+                none = neg(G.or_n(conds));
+            }
             Bits qv = G.fresh_word((uint32_t)w), r = G.fresh_word((uint32_t)w);
             std::vector<Lit> zs;
             for (Lit l : b) zs.push_back(neg(l));
@@ -1103,18 +1115,81 @@ public:
             Bits sum = G.add(prod, G.zext(r, 2 * w), G.F);
             Lit ok1 = G.eq(sum, G.zext(a, 2 * w));
             Lit ok2 = G.ult(r, b);
-            S.add_clause({bz, ok1});
-            S.add_clause({bz, ok2});
+            S.add_clause({neg(none), bz, ok1});
+            S.add_clause({neg(none), bz, ok2});
             // b == 0: q = all ones, r = a (SMT-LIB)
             for (size_t i = 0; i < w; ++i) {
-                S.add_clause({neg(bz), qv[i]});
-                S.add_clause({neg(bz), neg(r[i]), a[i]});
-                S.add_clause({neg(bz), r[i], neg(a[i])});
+                S.add_clause({neg(none), neg(bz), qv[i]});
+                S.add_clause({neg(none), neg(bz), neg(r[i]), a[i]});
+                S.add_clause({neg(none), neg(bz), r[i], neg(a[i])});
+            }
+            for (auto &c : cases) {
+                Bits cq(w, G.F), cr(w, G.F);
+                if (c.second < 0) {
+                    cq = Bits(w, G.T);
+                    cr = a;
+                } else {
+                    size_t pos = (size_t)c.second;
+                    for (size_t i = 0; i + pos < w; ++i) cq[i] = a[i + pos];
+                    for (size_t i = 0; i < pos; ++i) cr[i] = a[i];
+                }
+                qv = G.ite(c.first, cq, qv);
+                r = G.ite(c.first, cr, r);
             }
             out = {qv, r};
         }
         divmod_memo.emplace(mk_, out);
         return out;
+    }
+
+    // The pinned cases of a divisor (see udivrem): b is the value of a read
+    // whose arguments keep at most EAGER_FREE free bits, and reads of the same
+    // function / array at constant arguments its fixed bits allow have
+    // constant values, each zero or a power of two.  Fills (args equal, bit)
+    // per such read; false when b is no such read.  A case's value reaches b
+    // through the congruence lemma of the pair (eager_lemmas, or lazily).
+    bool divisor_cases(const Bits &b, std::vector<std::pair<Lit, int>> &cases) {
+        const ReadRec *R = nullptr;
+        for (const ReadRec &x : reads)
+            if (x.val == b) { R = &x; break; }
+        if (!R || R->args.empty()) {
+            if (std::getenv("MYTHSMT_VERBOSE")) std::fprintf(stderr, "divisor_cases: divisor is no read\n");
+            return false;
+        }
+        size_t fr = 0;
+        for (const Bits &a : R->args)
+            for (Lit l : a) {
+                Lit m = G.nrm(l);
+                if (m != G.T && m != G.F) ++fr;
+            }
+        if (fr == 0 || fr > EAGER_FREE) return false;
+        for (const ReadRec &c : reads) {
+            if (&c == R || c.kind != R->kind || c.id != R->id || c.val.size() != b.size() ||
+                c.args.size() != R->args.size())
+                continue;
+            bool cst = true, ok = true;
+            for (size_t i = 0; i < c.args.size() && cst && ok; ++i) {
+                if (c.args[i].size() != R->args[i].size()) { ok = false; break; }
+                for (size_t j = 0; j < c.args[i].size(); ++j) {
+                    Lit k = G.nrm(c.args[i][j]), s = G.nrm(R->args[i][j]);
+                    if (k != G.T && k != G.F) { cst = false; break; }
+                    if ((s == G.T && k == G.F) || (s == G.F && k == G.T)) { ok = false; break; }
+                }
+            }
+            if (!cst || !ok) continue;
+            int ones = 0, pos = -1;
+            for (size_t i = 0; i < c.val.size(); ++i) {
+                Lit v = G.nrm(c.val[i]);
+                if (v != G.T && v != G.F) { ones = -1; break; }
+                if (v == G.T) { ++ones; pos = (int)i; }
+            }
+            if (ones < 0 || ones > 1) continue;         // not pinned / no power of two: the general case
+            std::vector<Lit> same;
+            for (size_t i = 0; i < c.args.size(); ++i) same.push_back(G.eq(R->args[i], c.args[i]));
+            cases.push_back({G.and_n(same), ones == 0 ? -1 : pos});
+        }
+        if (std::getenv("MYTHSMT_VERBOSE")) std::fprintf(stderr, "divisor_cases: %zu cases, %zu free bits\n", cases.size(), fr);
+        return !cases.empty();
     }
 
     Bits absv(const Bits &a) { return G.ite(a.back(), G.bneg(a), a); }

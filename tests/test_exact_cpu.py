@@ -236,14 +236,14 @@ def test_storage_chain_and_congruence(solver):
     assert solver.check([(k(Concat(x, y)) != k(Concat(y, x))).raw, (x == y).raw])[0] == "unsat"
 
 
-def _power_division_query():
+def _power_division_query(base=None):
     """flag_array's shape: a packed bool array read as ``(word / 256**(i % 32))
     & 0xff != 0``, with Power(256, e) a function pinned at e = 0..31 (the
     exponent manager's table, exponent_function_manager.py) and `word` a read
     of symbolic storage at `i / 32` (one slot stored)."""
     i = sf.BitVecSym("i", 256)
     pw = Function("Power", [256], 256)
-    store = Array("Storage", 256, 256)
+    store = base if base is not None else Array("Storage", 256, 256)
     word = 0x1234 << (8 * 21)
     store[sf.BitVecVal(0x26, 256)] = sf.BitVecVal(word, 256)
     e = E.BitVec(E._fold("bvurem", 256, (i.raw, E.const(32, 256))))
@@ -254,17 +254,29 @@ def _power_division_query():
     return conj
 
 
-def test_small_domain_reads_get_eager_congruence(monkeypatch):
-    """A read whose arguments keep few free bits (the exponent i % 32) is tied to
-    the pinned points before the search: the division by Power(256, i % 32) is
-    decided in a few conflicts, with a model that holds; without the eager
-    lemmas the same conflict budget is not enough."""
+def _fresh(conflicts=3000):
+    return exact.ExactSolver(max_ms=20000, max_conflicts=conflicts, session=False)
+
+
+def test_division_by_a_pinned_power_is_decided(monkeypatch):
+    """A divisor read at a small-domain argument (the exponent i % 32) whose
+    constant-argument reads are pinned to powers of two is blasted as a case
+    split -- a shift per pinned point, the general divider only when none
+    applies -- and its congruence with the pinned reads is added before the
+    search.  Either one decides flag_array's division in a few conflicts; with
+    neither, the same budget runs out."""
     conj = _power_division_query()
-    st, a = exact.ExactSolver(max_ms=20000, max_conflicts=3000, session=False).check(conj)
+    st, a = _fresh().check(conj)
     assert st == "sat" and holds(a, conj)
+    for env in ({"MYTHSMT_EAGER": "0"}, {"MYTHSMT_DIVCASES": "0"}):
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            st, a = _fresh().check(conj)
+            assert st == "sat" and holds(a, conj), env
     monkeypatch.setenv("MYTHSMT_EAGER", "0")
-    st0, _ = exact.ExactSolver(max_ms=20000, max_conflicts=3000, session=False).check(conj)
-    assert st0 == "unknown"                    # (never unsat: the query is satisfiable)
+    monkeypatch.setenv("MYTHSMT_DIVCASES", "0")
+    assert _fresh().check(conj)[0] == "unknown"          # (never unsat: the query is satisfiable)
 
 
 def test_reference_keccak_verdicts(solver):
