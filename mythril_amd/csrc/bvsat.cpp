@@ -1099,29 +1099,35 @@ public:
             // per pinned case the quotient is a shift, and the general divider
             // below only has to hold when no case applies
             std::vector<std::pair<Lit, int>> cases;   // (args equal, bit of the power; -1: zero)
+            bool complete = false;
             const char *dc = std::getenv("MYTHSMT_DIVCASES");   // "0": general divider only (the A/B)
-            Lit none = !(dc && dc[0] == '0') && divisor_cases(b, cases) ? G.F : G.T;
-            if (none == G.F) {
+            Lit none = !(dc && dc[0] == '0') && divisor_cases(b, cases, complete) ? G.F : G.T;
+            if (none == G.F && !complete) {
                 std::vector<Lit> conds;
                 for (auto &c : cases) conds.push_back(c.first);
                 none = neg(G.or_n(conds));
             }
-            Bits qv = G.fresh_word((uint32_t)w), r = G.fresh_word((uint32_t)w);
-            std::vector<Lit> zs;
-            for (Lit l : b) zs.push_back(neg(l));
-            Lit bz = G.and_n(zs);                     // b == 0
-            // b != 0: a = q * b + r (in 2w bits, no wrap), r < b
-            Bits prod = G.mul(G.zext(qv, 2 * w), G.zext(b, 2 * w), 2 * w);
-            Bits sum = G.add(prod, G.zext(r, 2 * w), G.F);
-            Lit ok1 = G.eq(sum, G.zext(a, 2 * w));
-            Lit ok2 = G.ult(r, b);
-            S.add_clause({neg(none), bz, ok1});
-            S.add_clause({neg(none), bz, ok2});
-            // b == 0: q = all ones, r = a (SMT-LIB)
-            for (size_t i = 0; i < w; ++i) {
-                S.add_clause({neg(none), neg(bz), qv[i]});
-                S.add_clause({neg(none), neg(bz), neg(r[i]), a[i]});
-                S.add_clause({neg(none), neg(bz), r[i], neg(a[i])});
+            // cases covering every value of the argument's free bits: exactly one
+            // applies, and the general divider is never needed (none stays false)
+            Bits qv = complete ? Bits(w, G.F) : G.fresh_word((uint32_t)w);
+            Bits r = complete ? Bits(w, G.F) : G.fresh_word((uint32_t)w);
+            if (!complete) {
+                std::vector<Lit> zs;
+                for (Lit l : b) zs.push_back(neg(l));
+                Lit bz = G.and_n(zs);                     // b == 0
+                // b != 0: a = q * b + r (in 2w bits, no wrap), r < b
+                Bits prod = G.mul(G.zext(qv, 2 * w), G.zext(b, 2 * w), 2 * w);
+                Bits sum = G.add(prod, G.zext(r, 2 * w), G.F);
+                Lit ok1 = G.eq(sum, G.zext(a, 2 * w));
+                Lit ok2 = G.ult(r, b);
+                S.add_clause({neg(none), bz, ok1});
+                S.add_clause({neg(none), bz, ok2});
+                // b == 0: q = all ones, r = a (SMT-LIB)
+                for (size_t i = 0; i < w; ++i) {
+                    S.add_clause({neg(none), neg(bz), qv[i]});
+                    S.add_clause({neg(none), neg(bz), neg(r[i]), a[i]});
+                    S.add_clause({neg(none), neg(bz), r[i], neg(a[i])});
+                }
             }
             for (auto &c : cases) {
                 Bits cq(w, G.F), cr(w, G.F);
@@ -1148,7 +1154,7 @@ public:
     // constant values, each zero or a power of two.  Fills (args equal, bit)
     // per such read; false when b is no such read.  A case's value reaches b
     // through the congruence lemma of the pair (eager_lemmas, or lazily).
-    bool divisor_cases(const Bits &b, std::vector<std::pair<Lit, int>> &cases) {
+    bool divisor_cases(const Bits &b, std::vector<std::pair<Lit, int>> &cases, bool &complete) {
         const ReadRec *R = nullptr;
         for (const ReadRec &x : reads)
             if (x.val == b) { R = &x; break; }
@@ -1163,6 +1169,8 @@ public:
                 if (m != G.T && m != G.F) ++fr;
             }
         if (fr == 0 || fr > EAGER_FREE) return false;
+        complete = false;
+        std::unordered_set<uint32_t> seen;          // the free bits' values the cases cover
         for (const ReadRec &c : reads) {
             if (&c == R || c.kind != R->kind || c.id != R->id || c.val.size() != b.size() ||
                 c.args.size() != R->args.size())
@@ -1187,7 +1195,18 @@ public:
             std::vector<Lit> same;
             for (size_t i = 0; i < c.args.size(); ++i) same.push_back(G.eq(R->args[i], c.args[i]));
             cases.push_back({G.and_n(same), ones == 0 ? -1 : pos});
+            uint32_t key = 0, at = 0;
+            for (size_t i = 0; i < c.args.size(); ++i)
+                for (size_t j = 0; j < c.args[i].size(); ++j) {
+                    Lit sr = G.nrm(R->args[i][j]);
+                    if (sr == G.T || sr == G.F) continue;
+                    if (G.nrm(c.args[i][j]) == G.T) key |= 1u << at;
+                    ++at;
+                }
+            seen.insert(key);
         }
+        // every value of the free bits has its case: no general divider needed
+        complete = seen.size() == (size_t)1 << fr;
         if (std::getenv("MYTHSMT_VERBOSE")) std::fprintf(stderr, "divisor_cases: %zu cases, %zu free bits\n", cases.size(), fr);
         return !cases.empty();
     }

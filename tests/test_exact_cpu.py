@@ -262,12 +262,16 @@ def test_division_by_a_pinned_power_is_decided(monkeypatch):
     """A divisor read at a small-domain argument (the exponent i % 32) whose
     constant-argument reads are pinned to powers of two is blasted as a case
     split -- a shift per pinned point, the general divider only when none
-    applies -- and its congruence with the pinned reads is added before the
-    search.  Either one decides flag_array's division in a few conflicts; with
+    applies, and not at all when the points cover the argument's domain -- and
+    its congruence with the pinned reads is added before the search.  Either one decides flag_array's division in a few conflicts; with
     neither, the same budget runs out."""
     conj = _power_division_query()
-    st, a = _fresh().check(conj)
+    s = _fresh()
+    st, a = s.check(conj)
     assert st == "sat" and holds(a, conj)
+    # the 32 pinned points cover every value of i % 32: no general divider is
+    # built (a 512-bit product: ~270k variables without the split)
+    assert s.stats["vars"] < 60_000
     for env in ({"MYTHSMT_EAGER": "0"}, {"MYTHSMT_DIVCASES": "0"}):
         with monkeypatch.context() as m:
             for k, v in env.items():
