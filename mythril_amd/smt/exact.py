@@ -201,6 +201,21 @@ class _Table:
         return out
 
 
+def _divides_by_application(conjuncts: Sequence[Node]) -> bool:
+    """Whether a bvudiv / bvurem in the conjuncts divides by a function
+    application (its divisor node, directly)."""
+    seen, stack = set(), list(conjuncts)
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        if n.op in ("bvudiv", "bvurem") and len(n.args) == 2 and n.args[1].op == "uf":
+            return True
+        stack.extend(a for a in n.args if isinstance(a, Node))
+    return False
+
+
 class ExactSolver:
     """``check(conjuncts, minimize)`` -> ("sat", assignment) | ("unsat", None)
     | ("unknown", None), the assignment in the ModelRef form (name -> int,
@@ -257,6 +272,13 @@ class ExactSolver:
         wall clock of each attempt."""
         cap = self.max_ms if max_ms is None else max_ms
         with self._lock:
+            if not fresh and _divides_by_application(conjuncts):
+                # a division by a function application (Power(256, i % 32)): decided
+                # alone, its pinned points are units, and the blaster splits the
+                # division into shifts (bvsat.cpp divisor_cases) -- in a session they
+                # are assumptions, and every such query re-blasts a 512-bit divider
+                self.stats["fresh_direct"] = self.stats.get("fresh_direct", 0) + 1
+                fresh = True
             if not self.use_session or fresh or minimize:
                 # the objectives are met bit by bit under assumptions: alone, the
                 # query's units fold what the bounds fix (and no other query's

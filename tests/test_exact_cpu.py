@@ -272,6 +272,12 @@ def test_division_by_a_pinned_power_is_decided(monkeypatch):
     # the 32 pinned points cover every value of i % 32: no general divider is
     # built (a 512-bit product: ~270k variables without the split)
     assert s.stats["vars"] < 60_000
+    # a session sends such a query straight to a solve of its own (its pins
+    # are units there, assumptions in a session)
+    s2 = exact.ExactSolver(max_ms=20000)
+    st, a = s2.check(conj)
+    assert st == "sat" and holds(a, conj)
+    assert s2.stats.get("fresh_direct") == 1 and s2.stats["sessions"] == 0
     for env in ({"MYTHSMT_EAGER": "0"}, {"MYTHSMT_DIVCASES": "0"}):
         with monkeypatch.context() as m:
             for k, v in env.items():
