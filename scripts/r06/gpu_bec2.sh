@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 6: BECToken -t 2 (C3) on the MI355X with the final exact procedure.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/r06${1:-_b2}
+mkdir -p $OUT
+timeout -k 10 400 python -u scripts/r06/c3_bec.py 2 > $OUT/c3_bec2_gpu.log 2>&1

@@ -306,6 +306,20 @@ def test_reference_keccak_verdicts(solver):
     assert seen >= 10
 
 
+def test_products_of_words_are_decided_alone():
+    """A query multiplying two words goes straight to a solve of its own, where
+    a bound on one factor folds the multiplier at level 0; a product by a
+    constant stays in the session."""
+    x, y = sf.BitVecSym("x", 256), sf.BitVecSym("y", 256)
+    s = exact.ExactSolver(max_ms=20000)
+    st, a = s.check([Not(BVMulNoOverflow(x, y, False)).raw, ULT(x, 21).raw])
+    assert st == "sat" and a["x"] * a["y"] >= 1 << 256
+    assert s.stats.get("fresh_direct_mul") == 1 and s.stats["sessions"] == 0
+    st, a = s.check([(x * 3 == 7).raw])
+    assert st == "sat" and s.stats.get("fresh_direct_mul") == 1 and s.stats["sessions"] == 1
+    s.close()
+
+
 def test_minimize_is_lexicographic(solver):
     x, y = sf.BitVecSym("x", 256), sf.BitVecSym("y", 256)
     st, a = solver.check([UGT(x, 100).raw, UGT(y, x).raw], minimize=[x.raw, y.raw])
