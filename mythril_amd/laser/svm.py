@@ -211,7 +211,7 @@ class LaserEVM:
         self._pending_forks: List = []
         # a fork-filter query no quick-sat candidate answers and no SMT backend
         # can decide: "raise" (SolverBackendMissing) or "keep" the successor
-        # (prefilter-only runs: the image has no solver; counted in fork_stats)
+        # (prefilter-only runs, without smt.exact behind kernel 2; counted in fork_stats)
         self.unknown_forks = "raise"
         self.fork_stats = {"groups": 0, "queries": 0, "kept": 0, "pruned": 0, "unknown": 0, "flushes": 0}
         log.info("LASER EVM (MI355X batched core) initialized")
