@@ -492,7 +492,7 @@ def run_hooked_c2(dev, n_lanes, rank):
 
     code = workloads.bytecode("overflow.sol.o")
     b = workloads.c2_batch(n_lanes, seed=workloads.C2_SEED + 7 + rank)
-    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     events = [0]
 
     def hook(_state):
@@ -569,7 +569,7 @@ def run_taint_c2(dev, n_lanes, rank, modes=("device", "host")):
     try:
         for mode in modes:
             tnt.BATCH_SAFE = saved if mode == "device" else {}
-            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+            laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
             laser.track_objects = True
             mods = [getattr(refmodules, m)() for m in names]
             laser.register_hooks("pre", hooks_of(mods, "pre"))
@@ -692,7 +692,7 @@ def symbolic_lane_batch(dev, lanes: int, order: str = "code"):
     from mythril_amd.laser.transaction import ACTORS
     from mythril_amd.smt.expr import Or, symbol_factory
     codes = json.loads((ROOT / "tests" / "golden" / "bytecodes.json").read_text())
-    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     states = []
     for k, name in enumerate(sorted(codes)):
         ws = WorldState()
@@ -831,7 +831,7 @@ def run_taint_lanes(dev, lanes: int, rank: int = 0, reps: int = 5, order: str = 
     from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
     names = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJump", "UserAssertions",
              "Exceptions", "StateChangeAfterCall")
-    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     laser.track_objects = True
     mods = [getattr(refmodules, m)() for m in names]
     laser.register_hooks("pre", hooks_of(mods, "pre"))
@@ -954,7 +954,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
             ws = WorldState()
             ws.put_account(Account(creator))
             if name == "flag_array.sol.o":
-                laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+                laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
                 laser.open_states = [ws]
                 execute_contract_creation(laser, None, creator, creator, code, 8_000_000, 1, 10 ** 17)
                 if len(laser.open_states) != 1:
@@ -971,7 +971,7 @@ def run_symbolic_tx(dev, replicas: int, tx_count: int, n_seeds: int, escape_hand
             solver.model_cache = mc
             backend = SatSearchBackend(mc, search=False, exact=ExactSolver(), exact_ms=60000)
             solver.set_solver_backend(backend)
-            laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+            laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                              transaction_count=tx_count, escape_handler=escape_handler)
             if log:
                 log(f"symbolic_tx {name}")

@@ -7,7 +7,8 @@ from .state import (Account, Environment, GlobalState, MachineStack, MachineStat
                     Storage, WorldState)
 from .strategy import (BoundedLoopsStrategy, BreadthFirstSearchStrategy, DepthFirstSearchStrategy,
                        JumpdestCountAnnotation)
-from .svm import LaserEVM, StatespaceNotBuilt
+from .svm import LaserEVM
+from .cfg import Edge, JumpType, Node, NodeFlags
 from .transaction import (ContractCreationTransaction, MessageCallTransaction,
                           execute_contract_creation, execute_message_call, execute_symbolic_message_call,
                           execute_symbolic_contract_creation,

@@ -65,7 +65,8 @@ from ..smt.solver import Constraints, SnapshotConstraints, SolverBackendMissing,
 from .opcodes import ADDRESS_OPCODE_MAPPING, OPCODES, get_required_stack_elements
 from .signals import PluginSkipState, PluginSkipWorldState
 from .state import GlobalState, LazyStack, Memory, MachineStack, concrete
-from .strategy import DepthFirstSearchStrategy, JumpdestCountAnnotation
+from .cfg import Edge, JumpType, Node, NodeFlags
+from .strategy import DelayConstraintStrategy, DepthFirstSearchStrategy, JumpdestCountAnnotation
 from . import symbolic as sym
 from . import taint as tnt
 from .transaction import ContractCreationTransaction, install_runtime_code
@@ -102,10 +103,6 @@ class _Lane:
         self.dirty = False        # host image changed, upload before the next launch
 
 
-class StatespaceNotBuilt(NotImplementedError):
-    """LaserEVM.nodes / .edges read with requires_statespace=True."""
-
-
 class LaserEVM:
     """The LASER engine with kernel 1 stepping every path of the work list."""
 
@@ -140,12 +137,13 @@ class LaserEVM:
         self.execution_timeout = execution_timeout or 0
         self.create_timeout = create_timeout or 0
 
-        # the statespace graph (cfg.py nodes/edges) is not built by the batched
-        # core: reading `nodes` / `edges` with requires_statespace raises
-        # (StatespaceNotBuilt) rather than returning an empty graph
+        # the statespace graph (svm.py:94-97, cfg.py): with requires_statespace
+        # exec() steps every state one instruction at a time (_exec_stepwise) so
+        # that each node lists its states; without it the lanes run free and the
+        # graph stays empty
         self.requires_statespace = requires_statespace
-        self._nodes: Dict = {}
-        self._edges: List = []
+        self.nodes: Dict[int, Node] = {}
+        self.edges: List[Edge] = []
 
         self.time: Optional[datetime] = None
         self.executed_transactions = False
@@ -270,6 +268,8 @@ class LaserEVM:
                 gc.unfreeze()
 
     def _exec(self, create=False, track_gas=False) -> Optional[List[GlobalState]]:
+        if self.requires_statespace:
+            return self._exec_stepwise(create, track_gas)
         final_states: List[GlobalState] = []
         self._exec_stop = False
         for hook in self._start_exec_hooks:
@@ -285,6 +285,59 @@ class LaserEVM:
             if leftover is not None:       # timeout: the reference returns at once
                 return final_states + leftover if track_gas else None
             if self._exec_stop:            # BoundedLoops popped a past-the-end state
+                self._exec_stop = False
+                self.work_list.clear()
+                break
+        for hook in self._stop_exec_hooks:
+            hook()
+        return final_states if track_gas else None
+
+    def _exec_stepwise(self, create=False, track_gas=False) -> Optional[List[GlobalState]]:
+        """svm.py:293-337 as written, for the statespace graph: pop one state in
+        the strategy's order, step it one instruction on the device (a one-lane
+        batch, execute_state's path; a state no lane can carry takes the escape
+        handler), then manage_cfg on its successors.  Each node thereby holds the
+        state at every instruction it covers (cfg.py Node.states)."""
+        final_states: List[GlobalState] = []
+        self._exec_stop = False
+        for hook in self._start_exec_hooks:
+            hook()
+        queue: List[GlobalState] = []
+        while True:
+            if isinstance(self.strategy, DelayConstraintStrategy):
+                if not queue:
+                    queue = self.strategy.drain()
+                if not queue:
+                    break
+                state = queue.pop(0)
+            else:
+                state = None
+                while self.work_list:
+                    cand = self.work_list.pop() if self.strategy.order == "dfs" else self.work_list.pop(0)
+                    if cand.mstate.depth < self.max_depth:
+                        state = cand
+                        break
+                if state is None:
+                    break
+            if create and self._check_create_termination():
+                return final_states + [state] if track_gas else None
+            if not create and self._check_execution_termination():
+                return final_states + [state] if track_gas else None
+            op = _opcode_at(state)
+            saved = self.work_list[:]
+            del self.work_list[:]
+            self._single_step = True
+            try:
+                if self._host_only([state], final_states, track_gas):
+                    self._run_batch([state], final_states, create, track_gas, single_step=True)
+                self._flush_forks()
+            finally:
+                self._single_step = False
+            new_states = self.work_list[:]
+            self.work_list[:] = saved
+            self.manage_cfg(op, new_states, parent=state)
+            self.work_list.extend(new_states)
+            if self._exec_stop:
                 self._exec_stop = False
                 self.work_list.clear()
                 break
@@ -474,6 +527,7 @@ class LaserEVM:
             return
         if (not isinstance(tx, ContractCreationTransaction) or tx.return_data) and not revert:
             check_potential_issues(pre_state)
+            end_state.world_state.node = pre_state.node
             self._add_world_state(end_state)
 
     def _filter_fork(self, new_states: list) -> None:
@@ -529,36 +583,93 @@ class LaserEVM:
         finally:
             solver_mod.model_cache.clear_prefetch()
 
-    @property
-    def nodes(self) -> Dict:
-        """svm.py:549-637's statespace nodes: empty without requires_statespace
-        (as the reference leaves them); with it, refused -- the batched core runs
-        lanes many instructions per launch and never materialises the per-step
-        states a node lists (cfg.py Node.states), so an empty or partial graph
-        would be a silent wrong answer."""
-        if self.requires_statespace:
-            raise StatespaceNotBuilt("the statespace graph (requires_statespace=True) is not built by the "
-                                     "batched core; run the reference's LaserEVM for `myth graph` / "
-                                     "--statespace-json")
-        return self._nodes
-
-    @property
-    def edges(self) -> List:
-        if self.requires_statespace:
-            raise StatespaceNotBuilt("the statespace graph (requires_statespace=True) is not built by the "
-                                     "batched core; run the reference's LaserEVM for `myth graph` / "
-                                     "--statespace-json")
-        return self._edges
-
-    def manage_cfg(self, opcode: Optional[str], new_states: List[GlobalState]) -> None:
+    def manage_cfg(self, opcode: Optional[str], new_states: List[GlobalState],
+                   parent: Optional[GlobalState] = None) -> None:
         """svm.py:549-573 for the successors a host step produced: a JUMP /
         JUMPI successor (and a RETURN's, i.e. the caller's state after a nested
-        call) enters a new node, whose function name _new_node_state sets.  The
-        statespace graph itself is not kept (requires_statespace); lanes apply
-        the same switch from the device's function-entry index (_materialise)."""
-        if opcode in ("JUMP", "JUMPI", "RETURN"):
+        call) enters a new node, whose function name _new_node_state sets.
+        Without requires_statespace only the name switch is kept; lanes apply
+        it from the device's function-entry index (_materialise).  With it,
+        _exec_stepwise calls this once per step (the calls inside that step are
+        skipped) and the graph is built as the reference builds it."""
+        if not self.requires_statespace:
+            if opcode in ("JUMP", "JUMPI", "RETURN"):
+                for state in new_states:
+                    self._new_node_state(state)
+            return
+        if self._single_step:
+            return
+        if opcode == "JUMP":
             for state in new_states:
-                self._new_node_state(state)
+                self._new_graph_node(state)
+        elif opcode == "JUMPI" or (opcode in ("SLOAD", "SSTORE") and len(new_states) > 1):
+            for state in new_states:
+                self._new_graph_node(state, JumpType.CONDITIONAL, self._edge_condition(state, parent))
+        elif opcode == "RETURN":
+            for state in new_states:
+                self._new_graph_node(state, JumpType.RETURN)
+        for state in new_states:
+            if state.node is not None:
+                state.node.states.append(state)
+
+    @staticmethod
+    def _edge_condition(state: GlobalState, parent: Optional[GlobalState]):
+        """state.world_state.constraints[-1] (svm.py:563): jumpi_ appends the
+        simplified branch condition to every successor, True for a concrete one
+        (instructions.py:1581-1631); a successor whose list did not grow took a
+        concrete branch."""
+        cons = state.world_state.constraints
+        if parent is not None and len(cons) <= len(parent.world_state.constraints):
+            return symbol_factory.Bool(True)
+        return cons[-1] if len(cons) else None
+
+    def _new_graph_node(self, state: GlobalState, edge_type=JumpType.UNCONDITIONAL,
+                        condition=None) -> None:
+        """svm.py:575-637: the successor enters a fresh node of its active
+        account's contract, joined to its old node by an edge of `edge_type`;
+        the function-name switch of _new_node_state, with FUNC_ENTRY set on the
+        node where a dispatcher entry is entered."""
+        env = state.environment
+        code = env.code
+        try:
+            address = code.instruction_list[state.mstate.pc]["address"]
+        except IndexError:
+            return
+        new_node = Node(env.active_account.contract_name)
+        old_node = state.node
+        state.node = new_node
+        new_node.constraints = state.world_state.constraints
+        self.nodes[new_node.uid] = new_node
+        self.edges.append(Edge(old_node.uid if old_node is not None else None, new_node.uid,
+                               edge_type=edge_type, condition=condition))
+        if edge_type == JumpType.RETURN:
+            new_node.flags |= NodeFlags.CALL_RETURN
+        seq = state.world_state.transaction_sequence
+        if seq and isinstance(seq[-1], ContractCreationTransaction):
+            env.active_function_name = "constructor"
+        elif address in code.address_to_function_name:
+            env.active_function_name = code.address_to_function_name[address]
+            new_node.flags |= NodeFlags.FUNC_ENTRY
+        elif address == 0:
+            env.active_function_name = "fallback"
+        new_node.function_name = env.active_function_name
+
+    def transaction_node(self, global_state: GlobalState, transaction) -> None:
+        """transaction/symbolic.py:221-243 (concolic.py:134-156): a transaction's
+        first state starts a node of the callee's contract, joined by a
+        Transaction edge to the node its world state ended in."""
+        if not self.requires_statespace:
+            return
+        env = global_state.environment
+        new_node = Node(env.active_account.contract_name, function_name=env.active_function_name)
+        self.nodes[new_node.uid] = new_node
+        prev = transaction.world_state.node
+        if prev is not None:
+            self.edges.append(Edge(prev.uid, new_node.uid, edge_type=JumpType.Transaction,
+                                   condition=None))
+            new_node.constraints = global_state.world_state.constraints
+        global_state.node = new_node
+        new_node.states.append(global_state)
 
     @staticmethod
     def _new_node_state(state: GlobalState) -> None:
@@ -1318,6 +1429,7 @@ class LaserEVM:
                 hook(s, tx, None, False)
             if keep:
                 check_potential_issues(s)                 # svm.py:456-462
+                s.world_state.node = s.node
                 self._add_world_state(s)
         elif status == MG_HALT_REVERT:
             if tx is not None:

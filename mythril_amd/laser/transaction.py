@@ -139,6 +139,7 @@ def execute_symbolic_message_call(laser_evm, callee_address, gas_limit: int = 8_
         gs.world_state.constraints.append(
             Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
         gs.world_state.transaction_sequence.append(tx)
+        laser_evm.transaction_node(gs, tx)
         laser_evm.work_list.append(gs)
     laser_evm.exec()
 
@@ -172,6 +173,7 @@ def execute_symbolic_contract_creation(laser_evm, contract_initialization_code, 
     gs.world_state.constraints.append(
         Or(*[tx.caller == symbol_factory.BitVecVal(a, 256) for a in ACTORS.values()]))
     gs.world_state.transaction_sequence.append(tx)
+    laser_evm.transaction_node(gs, tx)
     laser_evm.work_list.append(gs)
     new_account = tx.callee_account
     laser_evm.exec(True)
@@ -275,6 +277,7 @@ def _setup_global_state_for_execution(laser_evm, transaction) -> None:
     global_state = transaction.initial_global_state()
     global_state.transaction_stack.append((transaction, None))
     global_state.world_state.transaction_sequence.append(transaction)
+    laser_evm.transaction_node(global_state, transaction)
     laser_evm.work_list.append(global_state)
 
 

@@ -43,7 +43,7 @@ def taint_device():
     from mythril_amd.laser.strategy import BreadthFirstSearchStrategy
     names = ("IntegerArithmetics", "TxOrigin", "ArbitraryStorage", "ArbitraryJump", "UserAssertions",
              "Exceptions", "StateChangeAfterCall")
-    laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     laser.track_objects = True
     mods = [getattr(refmodules, m)() for m in names]
     laser.register_hooks("pre", hooks_of(mods, "pre"))

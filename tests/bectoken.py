@@ -205,7 +205,7 @@ def concrete_exploit(dev):
     creator = Account(CREATOR, concrete_storage=True)
     creator.set_balance(10 ** 20)
     ws.put_account(creator)
-    vm = LaserEVM(device=dev)
+    vm = LaserEVM(requires_statespace=False, device=dev)
     vm.open_states = [ws]
     address = generate_contract_address(CREATOR, 0)
     execute_contract_creation(vm, None, CREATOR, CREATOR, creation(), gas_limit=8_000_000, gas_price=1, value=0,

@@ -27,7 +27,7 @@ def deploy(dev, name: str, value: int = 0):
     creator = Account(CREATOR, concrete_storage=True)
     creator.set_balance(10 ** 20)
     ws.put_account(creator)
-    laser_evm = LaserEVM(device=dev)
+    laser_evm = LaserEVM(requires_statespace=False, device=dev)
     laser_evm.open_states = [ws]
     address = generate_contract_address(CREATOR, 0)
     finals = execute_contract_creation(laser_evm, None, CREATOR, CREATOR, creation_code(name),

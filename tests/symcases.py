@@ -86,7 +86,7 @@ def deploy(device, name):
         return ws, workloads.CONTRACT
     args, value = CONTRACTS[name]
     eng = symref.Engine()       # CODESIZE of a creation with arguments escapes: concrete on the oracle
-    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+    laser = LaserEVM(requires_statespace=False, device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                      escape_handler=eng.step)
     ws = WorldState()
     creator = Account(CREATOR, balances=None)
@@ -140,7 +140,7 @@ def run_both(device, name, monkeypatch):
         ins = state.environment.code.instruction_list
         escaped.update([ins[state.mstate.pc]["opcode"] if state.mstate.pc < len(ins) else "END"])
         return handler(state)
-    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+    laser = LaserEVM(requires_statespace=False, device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                      escape_handler=counting_handler)
     laser.escaped_ops = escaped
     got = Counter()
@@ -214,7 +214,7 @@ def run_creation_both(device, name, monkeypatch):
         ins = state.environment.code.instruction_list
         escaped.update([ins[state.mstate.pc]["opcode"] if state.mstate.pc < len(ins) else "END"])
         return handler(state)
-    laser = LaserEVM(device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+    laser = LaserEVM(requires_statespace=False, device=device, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                      escape_handler=counting_handler)
     laser.escaped_ops = escaped
     got = Counter()

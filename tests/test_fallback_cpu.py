@@ -316,7 +316,7 @@ def test_fork_filter_at_escapes_prunes_impossible_successors(monkeypatch):
     acct = Account(workloads.CONTRACT, concrete_storage=True)
     acct.code = Disassembly("6000430000")      # PUSH1 0, NUMBER (escapes: symbolic), ...
     ws.put_account(acct)
-    vm = LaserEVM(device=OracleDevice(), escape_handler=handler)
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), escape_handler=handler)
     vm.open_states = [ws]
     execute_message_call(vm, workloads.CONTRACT, workloads.ATTACKER, workloads.ATTACKER, b"",
                          8_000_000, 0, 0)

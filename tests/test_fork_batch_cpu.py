@@ -45,7 +45,7 @@ def _run(name, batched, monkeypatch, n_seeds=48):
             return eng.step(st)
         except symref.Unsupported:
             return []
-    laser = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=2,
+    laser = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=2,
                      execution_timeout=0, escape_handler=handler)
     laser.unknown_forks = "keep"
     if not batched:
@@ -124,7 +124,7 @@ def test_refuting_backend_prunes_and_counts_divergences(monkeypatch):
     ws, addr = symcases.deploy(OracleDevice(), name)
     mc.seed_source = WitnessSeeds([workloads.bytecode(name)], n=48, storage_names=[f"Storage{addr}"])
     eng = symref.Engine()
-    laser = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=2,
+    laser = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=2,
                      execution_timeout=0, escape_handler=lambda st: eng.step(st))
     laser.open_states = [ws]
     laser.execute_transactions(addr)

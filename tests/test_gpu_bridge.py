@@ -36,7 +36,7 @@ def test_packed_symbolic_state_runs_on_kernel1_and_writes_back(monkeypatch):
             except symref.Unsupported:
                 eng.ended.append(("unsupported", st))
                 return []
-        laser = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
+        laser = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy, execution_timeout=0,
                          escape_handler=handler)
         got, ends = Counter(), []
         laser.register_laser_hooks("transaction_end", lambda s, tx, ret, revert: got.update(

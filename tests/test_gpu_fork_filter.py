@@ -100,7 +100,7 @@ def _run(name, k1, k2, monkeypatch, n_seeds=48, backend=None):
             return eng.step(st)
         except symref.Unsupported:
             return []
-    laser = LaserEVM(device=k1, strategy=BreadthFirstSearchStrategy, transaction_count=2,
+    laser = LaserEVM(requires_statespace=False, device=k1, strategy=BreadthFirstSearchStrategy, transaction_count=2,
                      execution_timeout=0, escape_handler=handler)
     laser.unknown_forks = "keep"
     ends = []

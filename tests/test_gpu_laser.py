@@ -61,7 +61,7 @@ def _run_vmtest(dev, v):
             acct.storage[int(key, 16)] = int(value, 16)
         world_state.put_account(acct)
         acct.set_balance(int(details["balance"], 16))
-    laser_evm = LaserEVM(device=dev)
+    laser_evm = LaserEVM(requires_statespace=False, device=dev)
     laser_evm.open_states = [world_state]
     final_states = execute_message_call(
         laser_evm,
@@ -216,7 +216,7 @@ def test_hooks_fire_in_reference_order(dev, strategy):
     b, txs = _c2_states(n)
     pre_ops, post_ops = {0x55, 0x57}, {0x54}        # SSTORE, JUMPI pre; SLOAD post
     expected = _oracle_events(b, pre_ops, post_ops)
-    vm = LaserEVM(device=dev, strategy=strategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=strategy)
     log = []
     pos = {}
 
@@ -254,7 +254,7 @@ def test_skip_state_and_skip_world_state(dev):
     reaching = {i for i in range(n) if int(ref.status[i]) == 7}
     assert 0 < len(reaching) < n
 
-    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
 
     def skip(state):
         raise PluginSkipState
@@ -271,7 +271,7 @@ def test_skip_state_and_skip_world_state(dev):
     assert len(vm.open_states) == len(kept)
     assert len(final) == n      # skipped states have no successor: final (svm.py:328-334)
 
-    vm2 = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm2 = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
 
     @vm2.laser_hook("add_world_state")
     def no_world(state):
@@ -291,7 +291,7 @@ def test_final_states_and_storage_match_oracle(dev):
     ref = b.copy()
     ref.code_id[:] = o.load_code(CODE)
     o.run(ref)
-    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
     for tx in txs:
         _setup_global_state_for_execution(vm, tx)
     states = list(vm.work_list)
@@ -329,7 +329,7 @@ def test_coverage_plugin_matches_oracle(dev):
             if int(ref.pc[i]) < ops.size:
                 covered[int(ref.pc[i])] = True
         o.run(ref, max_steps=1)
-    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
     plugin = InstructionCoveragePlugin()
     plugin.initialize(vm)
     dev.coverage_clear()
@@ -364,7 +364,7 @@ def test_bounded_loops_strategy_drops_like_the_oracle(dev, hooked):
     o = OracleEVM()
     b.code_id[:] = o.load_code(LOOP)
     o.run(b, loop_bound=3)
-    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
     vm.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
     seen = []
     if hooked:
@@ -417,7 +417,7 @@ def test_keccak_registrations_in_reference_order(dev, strategy):
     flat = sorted((key(rnd, i), i) for i, evs in events.items() for (_, rnd, _, _) in evs)
     want = [seen_before(k) for k, _ in flat]
     keccak_function_manager.reset()
-    vm = LaserEVM(device=dev, strategy=strategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=strategy)
     log = []
     vm.register_hooks("pre", {"SSTORE": [lambda s: log.append(len(keccak_function_manager.concrete_hashes))]})
     for tx in txs:
@@ -449,7 +449,7 @@ def test_transaction_rounds_device_equal_oracle_device(dev):
     acct = Account(ts.CALLEE, concrete_storage=True)
     acct.code = Disassembly(workloads.bytecode("overflow.sol.o").hex())
     ws.put_account(acct)
-    vm = LaserEVM(device=dev)
+    vm = LaserEVM(requires_statespace=False, device=dev)
     cov = InstructionCoveragePlugin()
     cov.initialize(vm)
     vm.open_states = [ws]

@@ -26,7 +26,7 @@ def test_symbolic_fixture_programs_on_the_device(name, code):
     from mythril_amd.laser import BreadthFirstSearchStrategy, LaserEVM
     dev = GpuDevice(0)
     try:
-        vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+        vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
         s0 = state_pins.symbolic_state(code)
         shape = vm._shape([s0])
         b = LaneBatch(shape)

@@ -62,7 +62,7 @@ def _min_forks(name: str) -> int:
 @pytest.mark.parametrize("name", symcases.ALL_CASES)
 def test_device_symbolic_lanes_cosimulate_with_the_restatement(dev, name):
     ws, addr = symcases.deploy(dev, name)
-    vm = LaserEVM(device=dev, strategy=BreadthFirstSearchStrategy)
+    vm = LaserEVM(requires_statespace=False, device=dev, strategy=BreadthFirstSearchStrategy)
     queue = [_initial(ws, addr)]
     eng = symref.Engine()
     forks = device_steps = checked = sym_sha3 = halts_past_sha3 = sym_exp = 0

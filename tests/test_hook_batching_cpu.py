@@ -62,7 +62,7 @@ def _run(strategy, batching, monkeypatch):
         monkeypatch.setattr(svm_mod.LaserEVM, "_ack_safe", lambda self, name, s, b: False)
     elif batching:
         monkeypatch.undo()
-    vm = LaserEVM(device=OracleDevice(), strategy=strategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=strategy, execution_timeout=0)
     log = []
     tag = {}
 
@@ -145,7 +145,7 @@ def test_a_kept_state_stays_the_one_the_hook_saw(keep, monkeypatch):
     (or its machine state, world state or storage) must find it exactly as it
     saw it after exec, as with the reference's copy per evaluate
     (instructions.py:121-130) -- and the event log must not depend on it."""
-    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     kept, seen, log = [], [], []
 
     def part(state):
@@ -184,7 +184,7 @@ def test_a_kept_state_stays_the_one_the_hook_saw(keep, monkeypatch):
 
 
 def _log_without_keeping():
-    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     log = []
 
     def hook(state):
@@ -206,7 +206,7 @@ def test_plain_hook_fast_path_equals_the_general_path(strategy, monkeypatch):
     log, open states and lane-steps."""
     def run(fast):
         monkeypatch.setattr(svm_mod.LaserEVM, "_fast_hooks", fast)
-        vm = LaserEVM(device=OracleDevice(), strategy=strategy, execution_timeout=0)
+        vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=strategy, execution_timeout=0)
         log, kept = [], []
 
         def view(state):
@@ -263,7 +263,7 @@ def test_hooks_that_keep_nothing_cost_no_state_copy(fast, monkeypatch):
     for keep, want_copies in ((False, False), (True, True)):
         copies[0] = 0
         kept, events = [], [0]
-        vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+        vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
 
         def hook(st):
             events[0] += 1

@@ -14,7 +14,7 @@ LONG = "600160016001600100"     # 4 x PUSH1, STOP at round 4
 
 
 def _run(codes, bounded):
-    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, execution_timeout=0)
     if bounded:
         vm.extend_strategy(BoundedLoopsStrategy, loop_bound=3)
     ends = []

@@ -60,7 +60,7 @@ def test_disassembly_push_argument_and_hex_input():
 
 
 def test_hook_registration_api():
-    vm = LaserEVM(device=object())
+    vm = LaserEVM(requires_statespace=False, device=object())
     seen = []
     vm.register_hooks("pre", {"SSTORE": [lambda s: seen.append("a")]})
     vm.register_hooks("post", {"SLOAD": [lambda s: seen.append("b")]})
@@ -92,7 +92,7 @@ def test_hook_registration_api():
 
 
 def test_hooked_ops_and_post_detection():
-    vm = LaserEVM(device=object())
+    vm = LaserEVM(requires_statespace=False, device=object())
     assert vm._hooked_ops() == set()
     vm.register_hooks("pre", {"SSTORE": [lambda s: None]})
     vm.register_instr_hooks("post", "JUMPI", lambda s: None)
@@ -103,7 +103,7 @@ def test_hooked_ops_and_post_detection():
 
 
 def test_lane_shape_is_a_valid_batch_configuration():
-    vm = LaserEVM(device=object())
+    vm = LaserEVM(requires_statespace=False, device=object())
     ws = WorldState()
     ws.put_account(Account(1, code=Disassembly("00")))
     vm.open_states = [ws]
@@ -126,7 +126,7 @@ def test_machine_stack_semantics():
 
 
 def test_execute_message_call_builds_states():
-    vm = LaserEVM(device=object())
+    vm = LaserEVM(requires_statespace=False, device=object())
     ws = WorldState()
     acct = Account(0x1234, code=Disassembly("6001600055"))
     acct.storage[7] = 9
@@ -176,16 +176,11 @@ def test_event_order_bfs_and_dfs():
     assert _ranges([5, 1, 2, 3, 9]) == [[1, 3], [5, 1], [9, 1]]
 
 
-def test_statespace_graph_is_refused_not_faked():
-    """LaserEVM(requires_statespace=True) cannot hand out the
-    reference's nodes / edges (svm.py:549-637) -- reading them raises; without
-    the flag they are empty, as in the reference."""
-    import pytest
-    from mythril_amd.laser import LaserEVM, StatespaceNotBuilt
+def test_statespace_graph_is_empty_without_the_flag():
+    """Without requires_statespace the lanes run free and no graph is kept
+    (the reference does not create the attributes at all, svm.py:94-97); the
+    graph itself is tested in test_statespace_cpu.py."""
+    from mythril_amd.laser import LaserEVM
     from oracle_device import OracleDevice
-    with pytest.raises(StatespaceNotBuilt):
-        LaserEVM(device=OracleDevice(), requires_statespace=True).nodes
-    with pytest.raises(StatespaceNotBuilt):
-        LaserEVM(device=OracleDevice(), requires_statespace=True).edges
     vm = LaserEVM(device=OracleDevice(), requires_statespace=False)
     assert vm.nodes == {} and vm.edges == []

@@ -49,7 +49,7 @@ def _txs(n_c2=24):
 
 
 def _run(strategy, grow, device=None):
-    vm = LaserEVM(device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
     vm._cap_grow = grow
     log, tag = [], {}
 

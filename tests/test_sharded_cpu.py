@@ -73,7 +73,7 @@ def _rounds_body(execute_message_calls, device):
     acct = Account(CALLEE, concrete_storage=True)
     acct.code = Disassembly(workloads.bytecode("overflow.sol.o").hex())
     ws.put_account(acct)
-    vm = LaserEVM(device=device)
+    vm = LaserEVM(requires_statespace=False, device=device)
     cov = InstructionCoveragePlugin()
     cov.initialize(vm)
     vm.open_states = [ws]

@@ -90,7 +90,7 @@ def _run():
                     hook(s, s.current_transaction, None, False)
                 vm._add_world_state(s)
         return out
-    vm = LaserEVM(device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=TX,
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice(), strategy=BreadthFirstSearchStrategy, transaction_count=TX,
                   execution_timeout=0, escape_handler=handler)
     vm.unknown_forks = "keep"
     cov = InstructionCoveragePlugin()

@@ -73,7 +73,7 @@ def _run(strategy, mode, monkeypatch, device=None, modules=("IntegerArithmetics"
     monkeypatch.setattr(solver, "model_cache", mc)
     monkeypatch.setattr(solver, "solver_backend", SatSearchBackend(mc))
     solver.get_model.cache_clear()
-    vm = LaserEVM(device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
+    vm = LaserEVM(requires_statespace=False, device=device or OracleDevice(), strategy=strategy, execution_timeout=0)
     vm.track_objects = True
     mods = [getattr(refmodules, m)() for m in modules]
     vm.register_hooks("pre", hooks_of(mods, "pre"))
@@ -143,7 +143,7 @@ def test_default_module_set_on_the_device_matches_host_hooks(strategy, monkeypat
 
 
 def test_plan_actions_for_the_reference_modules():
-    vm = LaserEVM(device=OracleDevice())
+    vm = LaserEVM(requires_statespace=False, device=OracleDevice())
     mods = [IntegerArithmetics(), TxOrigin()]
     vm.register_hooks("pre", hooks_of(mods, "pre"))
     vm.register_hooks("post", hooks_of(mods, "post"))
