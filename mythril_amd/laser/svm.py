@@ -608,9 +608,12 @@ class LaserEVM:
         elif opcode == "RETURN":
             for state in new_states:
                 self._new_graph_node(state, JumpType.RETURN)
+        # a node keeps each state as of its instruction: the device path steps
+        # the successor object itself onwards (materialised in place), where
+        # the reference's StateTransition steps a copy, so the node gets one
         for state in new_states:
             if state.node is not None:
-                state.node.states.append(state)
+                state.node.states.append(copy(state))
 
     @staticmethod
     def _edge_condition(state: GlobalState, parent: Optional[GlobalState]):
@@ -669,7 +672,7 @@ class LaserEVM:
                                    condition=None))
             new_node.constraints = global_state.world_state.constraints
         global_state.node = new_node
-        new_node.states.append(global_state)
+        new_node.states.append(copy(global_state))
 
     @staticmethod
     def _new_node_state(state: GlobalState) -> None:

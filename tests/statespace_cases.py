@@ -68,6 +68,10 @@ def check_graph(laser) -> dict:
     for e in edges:
         assert e.node_to in nodes and e.node_from in nodes
     targets = {e.node_to for e in edges}
+    # each node holds its own snapshot per instruction, never a live state
+    ids = [id(s) for n in nodes.values() for s in n.states]
+    assert len(ids) == len(set(ids))
+    assert not any(s in laser.work_list for n in nodes.values() for s in n.states)
     for uid, n in nodes.items():
         pcs = [s.mstate.pc for s in n.states]
         assert pcs == list(range(pcs[0], pcs[0] + len(pcs))), (n.function_name, pcs)
