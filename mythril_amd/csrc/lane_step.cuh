@@ -61,13 +61,6 @@ struct OpInfo {
 #ifndef MG_K1_PF
 #define MG_K1_PF 0
 #endif
-// MG_K1_TOPREG (A/B builds): LDS-resident straight-line runs keep the top
-// stack word in registers (T0) instead of spilling it to the window on entry
-// and moving every result through LDS.  Measured 2.2 % slower on C2 than the
-// all-LDS form (profiles/r06/ab_k1top/), so 0 is the shipped form.
-#ifndef MG_K1_TOPREG
-#define MG_K1_TOPREG 0
-#endif
 #define RUN_MAX 64u   // longest straight-line run executed as one block
 static_assert(RUN_MAX <= 64u, "a run is read as one pre-decoded word per wave lane");
 #define STACK_LIMIT 1024u
@@ -1201,105 +1194,6 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                     CLK_MARK(256u);
                     if (in_run && lds_run) {
                         uint32_t s = usp;
-#if MG_K1_TOPREG
-                        // T0 stays the top word while `tv` (wave-uniform: every lane
-                        // here has depth usp and runs the same opcodes); its window
-                        // slot s - 1 is then stale, every slot below is current.
-                        // PUSH / DUP1 only write the old top down, SWAP and a binary
-                        // ALU op read one word instead of two and write one or none.
-                        bool tv = s >= 1u;
-                        if (s >= 2u) V.set_wstack(s - 2u, T1);
-                        for (uint32_t k = 0; k < rsimple; ++k) {
-                            const uint32_t y = __builtin_amdgcn_readlane(ybulk, k);
-                            const uint32_t rop = y & 0xffu;
-                            switch ((y >> 17) & 31u) {
-                            case K_PUSH:
-                                if (tv) V.set_wstack(s - 1u, T0);
-                                T0 = PUSH_IMM(upc + k);
-                                tv = true;
-                                ++s;
-                                break;
-                            case K_DUP: {
-                                const uint32_t n = rop - 0x7fu;
-                                if (n == 1u) {
-                                    if (tv) V.set_wstack(s - 1u, T0);
-                                    else T0 = V.wstack(s - 1u);
-                                } else {
-                                    const U256 v = V.wstack(s - n);
-                                    if (tv) V.set_wstack(s - 1u, T0);
-                                    T0 = v;
-                                }
-                                tv = true;
-                                ++s;
-                                break;
-                            }
-                            case K_SWAP: {
-                                const uint32_t d = rop - 0x8fu;
-                                const U256 z = V.wstack(s - 1u - d);
-                                if (!tv) T0 = V.wstack(s - 1u);
-                                V.set_wstack(s - 1u - d, T0);
-                                T0 = z;
-                                tv = true;
-                                break;
-                            }
-                            case K_POP:
-                                --s;
-                                tv = false;
-                                break;
-                            case K_ALU: {
-                                if (!tv) T0 = V.wstack(s - 1u);
-                                if (rop == 0x15u || rop == 0x19u) {        // ISZERO, NOT
-                                    T0 = alu(rop, T0, T0, T0);
-                                } else {                                  // pop 2, push 1
-                                    const U256 b = V.wstack(s - 2u);
-                                    T0 = alu(rop, T0, b, b);
-                                    --s;
-                                }
-                                tv = true;
-                                break;
-                            }
-                            default:                                      // JUMPDEST
-                                break;
-                            }
-                        }
-                        // the closing jump (instructions.py:1520-1636), per lane: a lane
-                        // whose jump would raise or drop its path stops AT the jump and
-                        // the single-instruction path runs it (exceptions, drops)
-                        if (!tv && s >= 1u) { T0 = V.wstack(s - 1u); tv = true; }
-                        uint32_t nsp = s, npc = upc + rsimple, nexec = executed + rsimple;
-                        uint32_t jg = 0u;
-                        if (rjk) {
-                            const U256 tgt = T0;
-                            const bool take = rjk == 1u || !u_iszero(V.wstack(s - 2u));
-                            uint32_t idx = MG_JRES_NONE;
-                            if (take && u_fits32(tgt) && tgt.w[0] < C.n_jres) {
-                                if (jflag && tgt.w[0] < jn) { idx = s_jr[tgt.w[0]]; if (idx == 0xffffu) idx = MG_JRES_NONE; }
-                                else idx = a32[C.jres_off + tgt.w[0]];
-                            }
-                            const uint32_t ty = take && idx != MG_JRES_NONE
-                                                    ? (idx < sn ? s_pd[idx].y : (uint32_t)gops[idx] |
-                                                                                ((uint32_t)gfent[idx] << 22))
-                                                    : 0u;
-                            if (!take || (idx != MG_JRES_NONE && (ty & 0xffu) == 0x5bu)) {
-                                nsp = s - rjk;
-                                npc = take ? idx : upc + rlen;
-                                nexec = executed + rlen;
-                                jg = rjk == 1u ? 8u : 10u;      // added by hand, no OOG check
-                                if (rjk == 2u) ++depth;
-                                // _new_node_state: the successor at a function entry (the
-                                // fall-through's bit rides on the JUMPI's own decode word)
-                                const uint32_t jy = __builtin_amdgcn_readlane(ybulk, rsimple);
-                                if (take ? (ty & PD_FENT) : (jy & PD_NFENT)) fent = npc;
-                            }
-                        }
-                        // a lane that stopped at the jump (or ran no jump) keeps T0 as
-                        // its top; one past the jump reads its new top from the window
-                        if (nsp != s || !tv) T0 = nsp >= 1u ? V.wstack(nsp - 1u) : u_zero();
-                        T1 = nsp >= 2u ? V.wstack(nsp - 2u) : u_zero();
-                        sp = nsp;
-                        pc = npc; gmin += rg0 + jg; gmax += rg1 + jg; executed = nexec;
-                        FETCH();
-#else
                         if (s >= 1u) V.set_wstack(s - 1u, T0);
                         if (s >= 2u) V.set_wstack(s - 2u, T1);
                         for (uint32_t k = 0; k < rsimple; ++k) {
@@ -1373,7 +1267,6 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_lane_step(DevLanes L, const DevC
                         sp = nsp;
                         pc = npc; gmin += rg0 + jg; gmax += rg1 + jg; executed = nexec;
                         FETCH();
-#endif
                     } else if (in_run) {
                         // register form: the plain steps only; a closing jump runs as
                         // its own dispatch

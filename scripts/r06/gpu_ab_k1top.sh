@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6: kernel 1's LDS-resident runs with the top stack word kept in
-# registers (ab/k1_top1.so, -DMG_K1_TOPREG=1) against the shipped all-LDS form: kernel-1
+# registers (ab/k1_top1.so: ab/k1_topreg.diff applied, built with -DMG_K1_TOPREG=1) against the shipped all-LDS form: kernel-1
 # parity on the variant first, then interleaved processes on the bench's C2 batch.
 # (profiles/r06/ab_k1top/ was measured with the roles swapped: TOPREG=1 was then the default.)
 set -o pipefail
