@@ -43,13 +43,17 @@ from mythril_amd.smt.keccak_manager import keccak_function_manager
 
 def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, search=True,
             strategy: str = "bfs", runtime: bool = False, code: Optional[bytes] = None,
-            mutation_pruner: bool = True, exact: bool = True, exact_ms: int = 60000):
+            mutation_pruner: bool = True, exact: bool = True, exact_ms: int = 60000,
+            statespace: bool = False):
     """Run one analysis; returns (report issues, info).  `modules`: a module
     name, a list of names, or None (all fourteen).  `exact`: the queries the
     SAT search leaves open go to the exact procedure (mythril_amd.smt.exact),
     so fork filters and confirmations prune on unsat and on a budget timeout
     exactly as the reference's is_possible / get_model do; without it they
-    stay "unknown" and the paths are kept (the prefilter-only mode)."""
+    stay "unknown" and the paths are kept (the prefilter-only mode).
+    `statespace`: requires_statespace, as SymExecWrapper sets it for POST
+    modules and graphs (symbolic.py:110-113): every state stepped one
+    instruction at a time and the graph built."""
     from mythril_amd.smt.search import SatSearchBackend
     keccak_function_manager.reset()
     exponent_function_manager.reset()
@@ -73,7 +77,7 @@ def analyze(name: str, modules, tx_count: int, device, k2, n_seeds: int = 256, s
     try:
         laser = LaserEVM(device=device, strategy=strat, max_depth=128,
                          execution_timeout=86400, create_timeout=10, transaction_count=tx_count,
-                         requires_statespace=False, escape_handler=symref.Engine(signals=True).step)
+                         requires_statespace=statespace, escape_handler=symref.Engine(signals=True).step)
         if strategy == "delayed":
             laser.strategy.model_cache._device = k2
             if not exact:

@@ -35,3 +35,14 @@ def test_branch_program_graph_on_the_device(dev, monkeypatch):
     assert sorted(p for _, _, p, _ in sc.shape(laser)[0]) == sorted(tuple(v) for v in sc.BRANCH_PCS.values())
     _, ref = sc.run(OracleDevice(), "Branch", True, monkeypatch, code=sc.BRANCH, signals=True)
     assert sc.shape(laser) == sc.shape(ref)
+
+
+@pytest.mark.parametrize("row", __import__("test_integration_cpu").GOLDEN["issue_counts"],
+                         ids=lambda r: f"{r[0]}-{r[1]}")
+def test_analysis_rows_with_the_graph_on_the_device(dev, row, monkeypatch, tmp_path):
+    """analysis_tests.py's rows with requires_statespace on kernels 1 and 2:
+    the reference's counts, SWC ids and functions (flag_array's calldata too)."""
+    import test_integration_cpu as ti
+    from fnames import use_signature_db
+    use_signature_db(monkeypatch, tmp_path)
+    ti.check_row(row, dev, dev, statespace=True)

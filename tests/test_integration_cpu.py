@@ -61,11 +61,12 @@ def test_origin_contract_reports_swc_115(monkeypatch):
     assert swc in {i[0] for i in issues}
 
 
-def check_row(row, device, k2, strategy="bfs"):
+def check_row(row, device, k2, strategy="bfs", statespace=False):
     """Run one analysis_tests.py row and assert the reference's outcome."""
     import analyze
     name, module, tx_count, expected = row
-    issues, info = analyze.analyze(name, module, tx_count, device, k2, strategy=strategy)
+    issues, info = analyze.analyze(name, module, tx_count, device, k2, strategy=strategy,
+                                   statespace=statespace)
     report = analyze.issue_table(issues)
     assert info["escapes_dropped"] == 0, info
     assert len(issues) == expected, (name, module, report, info)

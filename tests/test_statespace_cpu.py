@@ -76,3 +76,47 @@ def test_graph_shape_is_deterministic(monkeypatch):
     a = sc.shape(sc.run(OracleDevice(), "exceptions.sol.o", True, monkeypatch)[1])
     b = sc.shape(sc.run(OracleDevice(), "exceptions.sol.o", True, monkeypatch)[1])
     assert a == b and len(a[0]) > 3
+
+
+@pytest.mark.parametrize("name", ["overflow.sol.o", "exceptions.sol.o"])
+def test_graph_run_filters_forks_as_the_batched_run(name, monkeypatch):
+    """Two transactions with the fork filter and the per-transaction
+    reachability filter on (pruning factor 1, kernel 2 on bv_ref, witness
+    seeds): the graph run -- svm.py's loop one state and one instruction at a
+    time -- and the batched run answer the same queries the same way, leave the
+    model cache's LRU in the same order and end the same paths in the same
+    order (the batched core's event order is the literal loop's, §3.3)."""
+    import test_fork_batch_cpu as fb
+    from mythril_amd.laser import LaserEVM
+
+    class GraphLaser(LaserEVM):
+        def __init__(self, *args, **kwargs):
+            kwargs["requires_statespace"] = True
+            super().__init__(*args, **kwargs)
+    try:
+        ends_a, lru_a, fs_a, st_a, _, open_a = fb._run(name, True, monkeypatch)
+        monkeypatch.setattr(fb, "LaserEVM", GraphLaser)
+        ends_b, lru_b, fs_b, st_b, _, open_b = fb._run(name, True, monkeypatch)
+    finally:
+        fb.keccak_function_manager.reset()
+        fb.tx_id_manager.restart_counter()
+        fb.solver.get_model.cache_clear()
+    assert ends_a == ends_b and open_a == open_b
+    assert lru_a == lru_b
+    for k in ("queries", "kept", "pruned", "unknown"):
+        assert fs_a[k] == fs_b[k]
+    assert st_a == st_b
+    assert fs_a["queries"] > 10
+
+
+@pytest.mark.parametrize("row", __import__("test_integration_cpu").GOLDEN["issue_counts"],
+                         ids=lambda r: f"{r[0]}-{r[1]}")
+def test_analysis_rows_with_the_graph(row, monkeypatch, tmp_path):
+    """analysis_tests.py's rows with requires_statespace set (as SymExecWrapper
+    sets it for POST modules): the reference's count and the same SWC ids and
+    functions as the batched run (test_integration_cpu.check_row)."""
+    import test_integration_cpu as ti
+    from fnames import use_signature_db
+    from oracle_device import OracleK2
+    use_signature_db(monkeypatch, tmp_path)
+    ti.check_row(row, OracleDevice(), OracleK2(), statespace=True)
