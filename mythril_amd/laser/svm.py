@@ -1083,6 +1083,7 @@ class LaserEVM:
         depth = 0 if self.max_depth == _INF else int(self.max_depth)
         bfs = getattr(self.strategy, "order", "bfs") == "bfs"
         regrow: List[GlobalState] = []
+        self._resumed = set()       # lanes a regrow resumed: not yet stepped (single_step)
         self._recq, self._rec_seq, self._rec_bfs, self._rec_lanes = [], itertools.count(), bfs, lanes
 
         sched = self._sched = _Schedule(lanes, b, bfs)
@@ -1108,6 +1109,7 @@ class LaserEVM:
             st = dev.step(mask, max_steps=1 if single_step else (1 << 30), max_depth=depth,
                           horizon=horizon)
             self.launches += 1
+            self._resumed.difference_update(run)
             self.device_ms += st.kernel_ms
             self.lane_steps += st.lane_steps
             self.total_states += st.lane_steps      # one successor per executed step
@@ -1135,6 +1137,8 @@ class LaserEVM:
             if single_step:
                 self._flush_forks()
                 for i in sorted(sched.paused):
+                    if i in self._resumed:
+                        continue            # regrown before its step: launched below
                     ln = lanes[i]
                     self._materialise(b, i, ln.state)
                     self.work_list.append(ln.state)
@@ -1275,6 +1279,7 @@ class LaserEVM:
         sched.b = b2
         for i, _ in resume:
             sched.set(i, "paused")
+            self._resumed.add(i)
         return b2
 
 

@@ -41,7 +41,10 @@ def test_branch_program_graph_on_the_device(dev, monkeypatch):
                          ids=lambda r: f"{r[0]}-{r[1]}")
 def test_analysis_rows_with_the_graph_on_the_device(dev, row, monkeypatch, tmp_path):
     """analysis_tests.py's rows with requires_statespace on kernels 1 and 2:
-    the reference's counts, SWC ids and functions (flag_array's calldata too)."""
+    the reference's counts, SWC ids and functions (flag_array's calldata too).
+    symbolic_exec_bytecode's constructor copies its arguments into a full
+    arena: the single step regrows the lane and runs it in the grown batch
+    (a regrown lane is not a stepped successor)."""
     import test_integration_cpu as ti
     from fnames import use_signature_db
     use_signature_db(monkeypatch, tmp_path)
