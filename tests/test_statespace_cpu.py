@@ -109,14 +109,16 @@ def test_graph_run_filters_forks_as_the_batched_run(name, monkeypatch):
     assert fs_a["queries"] > 10
 
 
+@pytest.mark.parametrize("strategy", ["bfs", "delayed"])
 @pytest.mark.parametrize("row", __import__("test_integration_cpu").GOLDEN["issue_counts"],
                          ids=lambda r: f"{r[0]}-{r[1]}")
-def test_analysis_rows_with_the_graph(row, monkeypatch, tmp_path):
+def test_analysis_rows_with_the_graph(row, strategy, monkeypatch, tmp_path):
     """analysis_tests.py's rows with requires_statespace set (as SymExecWrapper
-    sets it for POST modules): the reference's count and the same SWC ids and
-    functions as the batched run (test_integration_cpu.check_row)."""
+    sets it for POST modules), under BFS and --strategy delayed (whose drains
+    the graph run steps one state at a time): the reference's count and the
+    same SWC ids and functions as the batched run (test_integration_cpu.check_row)."""
     import test_integration_cpu as ti
     from fnames import use_signature_db
     from oracle_device import OracleK2
     use_signature_db(monkeypatch, tmp_path)
-    ti.check_row(row, OracleDevice(), OracleK2(), statespace=True)
+    ti.check_row(row, OracleDevice(), OracleK2(), strategy=strategy, statespace=True)
